@@ -1,0 +1,316 @@
+"""mpgmres_amd — MI355X-native mixed-precision restarted GMRES hot path.
+
+Python host mirror of the reference's solve interface (gmres_perf_test.cpp
+flags / run_tests) over the C-ABI libraries built by this package:
+
+  lib/libmpgmres_hip.so   gfx950 HIP kernels (include/mpgmres/capi.h)
+  lib/libmpgmres_host.so  operator surface + drivers + solve C-ABI
+                          (include/mpgmres/solve.h, problems.h)
+
+There is no CPU fallback: if the HIP libraries are missing, every entry
+point raises. The directory name is not a Python identifier, so load it with
+`load_package()` from bench.py / tests (it registers as `mpgmres_amd`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+from ._abi import ENGINES, MODES, ORTHS, PRECS, STATUS, HostCsr, SolveArgs, SolveResult
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+LIB_DIR = PKG_DIR / "lib"
+HIP_LIB = LIB_DIR / "libmpgmres_hip.so"
+HOST_LIB = LIB_DIR / "libmpgmres_host.so"
+CLI = PKG_DIR / "bin" / "gmres_perf_test"
+
+
+def build(jobs: int = 8) -> None:
+    """Compile the HIP + host libraries for gfx950 (hipcc cross-compiles; no GPU needed)."""
+    subprocess.run(["make", "-C", str(PKG_DIR), f"-j{jobs}"], check=True)
+
+
+_libs: dict = {}
+
+
+def _lib(name: str) -> C.CDLL:
+    if name in _libs:
+        return _libs[name]
+    path = HIP_LIB if name == "hip" else HOST_LIB
+    if not path.exists():
+        raise RuntimeError(f"{path} is missing: run build() (make -C {PKG_DIR}) — there is no CPU fallback")
+    if name == "host":
+        _lib("hip")
+    lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+    _libs[name] = lib
+    if name == "host":
+        _declare_host(lib)
+    else:
+        _declare_hip(lib)
+    return lib
+
+
+def hip_lib() -> C.CDLL:
+    return _lib("hip")
+
+
+def host_lib() -> C.CDLL:
+    return _lib("host")
+
+
+_P = C.c_void_p
+_I64 = C.c_int64
+_I32 = C.c_int32
+
+
+def _declare_host(lib: C.CDLL) -> None:
+    lib.mpg_solve.argtypes = [C.POINTER(SolveArgs), C.POINTER(SolveResult)]
+    lib.mpg_solve.restype = C.c_int
+    lib.mpg_gen_band.argtypes = [_I64, _I32, _I32, C.c_uint64, _I64, _I64, C.POINTER(HostCsr)]
+    lib.mpg_gen_laplace3d.argtypes = [_I32, _I32, _I32, C.POINTER(HostCsr)]
+    lib.mpg_load_mtx.argtypes = [C.c_char_p, C.POINTER(HostCsr), C.c_char_p, C.c_int]
+    lib.mpg_load_mtx_vector.argtypes = [C.c_char_p, _I32, C.POINTER(C.c_double), _I64, C.c_char_p, C.c_int]
+    lib.mpg_rand_vect.argtypes = [_I64, C.c_uint32, C.POINTER(C.c_double)]
+    lib.mpg_host_spmv.argtypes = [C.POINTER(HostCsr), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    lib.mpg_host_csr_free.argtypes = [C.POINTER(HostCsr)]
+    lib.mpg_host_csr_free.restype = None
+
+
+# (name, argtypes) for the kernel-level C-ABI, used by the per-kernel tests
+_HIP_DECLS = {
+    "mpg_error_string": ([C.c_int], C.c_char_p),
+    "mpg_ctx_last_error": ([_P], C.c_char_p),
+    "mpg_ctx_create": ([C.c_int, C.POINTER(_P)], C.c_int),
+    "mpg_ctx_destroy": ([_P], C.c_int),
+    "mpg_ctx_sync": ([_P], C.c_int),
+    "mpg_ctx_stream": ([_P], _P),
+    "mpg_malloc": ([_P, C.c_size_t, C.POINTER(_P)], C.c_int),
+    "mpg_free": ([_P, _P], C.c_int),
+    "mpg_memcpy_h2d": ([_P, _P, _P, C.c_size_t], C.c_int),
+    "mpg_memcpy_d2h": ([_P, _P, _P, C.c_size_t], C.c_int),
+    "mpg_csr_create": ([_P, _I32, _I32, _I64, _P, _P, _P, C.POINTER(_P)], C.c_int),
+    "mpg_csr_destroy": ([_P], C.c_int),
+    "mpg_csr_num_blocks": ([_P], C.c_int),
+}
+for _t, _ct in (("f64", C.c_double), ("f32", C.c_float)):
+    _HIP_DECLS.update({
+        f"mpg_dot_{_t}": ([_P, _I64, _P, _P, _P], C.c_int),
+        f"mpg_nrm2_{_t}": ([_P, _I64, _P, _P], C.c_int),
+        f"mpg_dot_{_t}_host": ([_P, _I64, _P, _P, _P], C.c_int),
+        f"mpg_nrm2_{_t}_host": ([_P, _I64, _P, _P], C.c_int),
+        f"mpg_axpy_{_t}": ([_P, _I64, _ct, _P, _P], C.c_int),
+        f"mpg_axpy_dev_{_t}": ([_P, _I64, _P, _P, _P], C.c_int),
+        f"mpg_naxpy_dev_{_t}": ([_P, _I64, _P, _P, _P], C.c_int),
+        f"mpg_scal_{_t}": ([_P, _I64, _ct, _P], C.c_int),
+        f"mpg_scal_copy_{_t}": ([_P, _I64, _ct, _P, _P], C.c_int),
+        f"mpg_scal_copy_dev_{_t}": ([_P, _I64, _P, _P, _P], C.c_int),
+        f"mpg_scal_recip_copy_dev_{_t}": ([_P, _I64, _P, _P, _P], C.c_int),
+        f"mpg_fill_{_t}": ([_P, _P, _I64, _I64, _I64, _ct], C.c_int),
+        f"mpg_gdmv_{_t}": ([_P, _I64, _ct, _P, _P, _ct, _P], C.c_int),
+        f"mpg_rotg_{_t}": ([_P, _P, _P, _P, _P], C.c_int),
+        f"mpg_rot_{_t}": ([_P, _P, _P, _P, _P], C.c_int),
+        f"mpg_rot_vec_{_t}": ([_P, C.c_int, _P, _P, _P], C.c_int),
+        f"mpg_scal_scalar_{_t}": ([_P, _ct, _P, _P], C.c_int),
+        f"mpg_scal_scalar_dev_{_t}": ([_P, _P, _P, _P], C.c_int),
+        f"mpg_gemv_{_t}": ([_P, C.c_int, _I64, _I64, _ct, _P, _I64, _P, _ct, _P], C.c_int),
+        f"mpg_trsv_{_t}": ([_P, C.c_int, C.c_int, _I64, _P, _I64, _P], C.c_int),
+        f"mpg_csr_spmv_{_t}": ([_P, _P, _ct, _P, _P, _ct, _P], C.c_int),
+        f"mpg_jacobi_setup_{_t}": ([_P, _P, _P, _P], C.c_int),
+    })
+_HIP_DECLS.update({
+    "mpg_csr_spmv_f16f32": ([_P, _P, C.c_float, _P, _P, C.c_float, _P], C.c_int),
+    "mpg_copy_f64f64": ([_P, _I64, _P, _P], C.c_int),
+    "mpg_copy_f32f32": ([_P, _I64, _P, _P], C.c_int),
+    "mpg_copy_f64f32": ([_P, _I64, _P, _P], C.c_int),
+    "mpg_copy_f32f64": ([_P, _I64, _P, _P], C.c_int),
+    "mpg_copy_f64f16": ([_P, _I64, _P, _P], C.c_int),
+    "mpg_copy_f32f16": ([_P, _I64, _P, _P], C.c_int),
+})
+
+
+def _declare_hip(lib: C.CDLL) -> None:
+    for name, (args, res) in _HIP_DECLS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+
+
+def exported_capi_symbols() -> list:
+    """Every function the C-ABI headers declare (parsed from include/mpgmres/*.h)."""
+    import re
+
+    names = []
+    for h in sorted((REPO_DIR / "include" / "mpgmres").glob("*.h")):
+        txt = h.read_text()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(mpg_\w+)\s*\(", txt, flags=re.M):
+            names.append((h.name, m.group(1)))
+    return names
+
+
+# ---------------------------------------------------------------- problems
+@dataclass
+class Csr:
+    """Host CSR (0-based int32 structure, fp64 values)."""
+    nrows: int
+    ncols: int
+    rowptr: np.ndarray
+    col: np.ndarray
+    val: np.ndarray
+
+    @property
+    def nnz(self) -> int:
+        return int(self.rowptr[-1])
+
+    @property
+    def n(self) -> int:
+        return self.nrows
+
+    def _c(self) -> HostCsr:
+        h = HostCsr()
+        h.nrows, h.ncols, h.nnz = self.nrows, self.ncols, self.nnz
+        h.rowptr = self.rowptr.ctypes.data_as(C.POINTER(C.c_int32))
+        h.col = self.col.ctypes.data_as(C.POINTER(C.c_int32))
+        h.val = self.val.ctypes.data_as(C.POINTER(C.c_double))
+        return h
+
+    def to_scipy(self):
+        import scipy.sparse as sp
+
+        return sp.csr_matrix((self.val, self.col, self.rowptr), shape=(self.nrows, self.ncols))
+
+
+def _take_csr(h: HostCsr) -> Csr:
+    lib = host_lib()
+    n, nnz = h.nrows, h.nnz
+    rp = np.ctypeslib.as_array(h.rowptr, shape=(n + 1,)).copy()
+    ci = np.ctypeslib.as_array(h.col, shape=(max(nnz, 1),))[:nnz].copy()
+    va = np.ctypeslib.as_array(h.val, shape=(max(nnz, 1),))[:nnz].copy()
+    out = Csr(n, h.ncols, rp, ci, va)
+    lib.mpg_host_csr_free(C.byref(h))
+    return out
+
+
+def gen_band(n: int, lo: int = 5, hi: int = 4, seed: int = 7, row_begin: int = 0,
+             row_end: Optional[int] = None) -> Csr:
+    """Banded test matrix (BAND-10M at n=1e6); any row slice matches the whole."""
+    h = HostCsr()
+    st = host_lib().mpg_gen_band(n, lo, hi, seed, row_begin, n if row_end is None else row_end, C.byref(h))
+    if st:
+        raise ValueError(f"mpg_gen_band failed ({st})")
+    return _take_csr(h)
+
+
+def gen_laplace3d(nx: int, ny: Optional[int] = None, nz: Optional[int] = None) -> Csr:
+    h = HostCsr()
+    st = host_lib().mpg_gen_laplace3d(nx, ny or nx, nz or nx, C.byref(h))
+    if st:
+        raise ValueError(f"mpg_gen_laplace3d failed ({st})")
+    return _take_csr(h)
+
+
+def load_mtx(path: str) -> Csr:
+    h = HostCsr()
+    err = C.create_string_buffer(256)
+    if host_lib().mpg_load_mtx(str(path).encode(), C.byref(h), err, 256):
+        raise ValueError(err.value.decode())
+    return _take_csr(h)
+
+
+def rand_vect(n: int, seed: int = 42) -> np.ndarray:
+    """x_true of gmres_perf_test.cpp:39-51 (mt19937 + uniform_real_distribution<float>)."""
+    out = np.empty(n, dtype=np.float64)
+    host_lib().mpg_rand_vect(n, seed, out.ctypes.data_as(C.POINTER(C.c_double)))
+    return out
+
+
+def host_spmv(A: Csr, x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty(A.nrows, dtype=np.float64)
+    h = A._c()
+    host_lib().mpg_host_spmv(C.byref(h), x.ctypes.data_as(C.POINTER(C.c_double)),
+                             y.ctypes.data_as(C.POINTER(C.c_double)))
+    return y
+
+
+# ---------------------------------------------------------------- solve
+@dataclass
+class Result:
+    status: str
+    restarts: int
+    inner_k: int
+    total_iters: int
+    res_norm: float
+    err_norm: float
+    gmres_seconds: float
+    setup_seconds: float
+    minvb_norm: float
+    x: np.ndarray
+    cyc_r_norm: np.ndarray
+    cyc_normalization: np.ndarray
+    cyc_beta: np.ndarray
+    step_res: np.ndarray
+    step_cycle: np.ndarray
+    message: str = ""
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def backward_error(self) -> np.ndarray:
+        return self.cyc_r_norm / self.cyc_normalization
+
+
+def make_args(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, mode="mixed", orth="mgs",
+              prec="identity", rlen=30, tol=1e-6, max_restarts=1_000_000, rtol=0.0, repeat_iter=False,
+              orthloss=False, jacobi_steps=1, engine="fused", verbose=False, device=0, threads=0):
+    """Build mpg_solve_args (shared by mpg_solve and the CPU oracle)."""
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    keep = [A.rowptr, A.col, A.val, b]
+    a = SolveArgs()
+    a.n, a.nnz = A.nrows, A.nnz
+    a.rowptr = A.rowptr.ctypes.data_as(C.POINTER(C.c_int32))
+    a.col = A.col.ctypes.data_as(C.POINTER(C.c_int32))
+    a.val = A.val.ctypes.data_as(C.POINTER(C.c_double))
+    a.b = b.ctypes.data_as(C.POINTER(C.c_double))
+    if x_true is not None:
+        x_true = np.ascontiguousarray(x_true, dtype=np.float64)
+        keep.append(x_true)
+        a.x_true = x_true.ctypes.data_as(C.POINTER(C.c_double))
+    a.mode, a.orth, a.prec, a.engine = MODES[mode], ORTHS[orth], PRECS[prec], ENGINES[engine]
+    a.rlen, a.tol, a.max_restarts, a.rtol = rlen, tol, max_restarts, rtol
+    a.repeat_iter, a.orthloss, a.jacobi_steps = int(repeat_iter), int(orthloss), jacobi_steps
+    a.verbose, a.device, a.threads = int(verbose), device, threads
+    return a, keep
+
+
+def run_solve(fn, args: SolveArgs, n: int, cycle_cap: int = 4096, step_cap: int = 1 << 17) -> Result:
+    """Call an mpg_solve-shaped entry point and collect the result + history."""
+    r = SolveResult()
+    x = np.zeros(n, dtype=np.float64)
+    cr, cn, cb = (np.zeros(cycle_cap) for _ in range(3))
+    sr = np.zeros(step_cap)
+    sc = np.zeros(step_cap, dtype=np.int32)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    r.x_out = dp(x)
+    r.cycle_cap, r.cyc_r_norm, r.cyc_normalization, r.cyc_beta = cycle_cap, dp(cr), dp(cn), dp(cb)
+    r.step_cap, r.step_res, r.step_cycle = step_cap, dp(sr), sc.ctypes.data_as(C.POINTER(C.c_int32))
+    st = fn(C.byref(args), C.byref(r))
+    msg = r.message.decode(errors="replace")
+    if st != 0:
+        raise RuntimeError(f"solve failed ({st}): {msg}")
+    nc, ns = min(r.n_cycles, cycle_cap), min(r.n_steps, step_cap)
+    return Result(STATUS.get(r.status, str(r.status)), r.restarts, r.inner_k, r.total_iters, r.res_norm,
+                  r.err_norm, r.gmres_seconds, r.setup_seconds, r.minvb_norm, x, cr[:nc].copy(), cn[:nc].copy(),
+                  cb[:nc].copy(), sr[:ns].copy(), sc[:ns].copy(), msg)
+
+
+def solve(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, **opts) -> Result:
+    """Restarted GMRES(m) on the MI355X (mpg_solve). Options as make_args."""
+    args, keep = make_args(A, b, x_true, **opts)
+    return run_solve(host_lib().mpg_solve, args, A.nrows)

@@ -1,0 +1,73 @@
+"""ctypes mirrors of the C-ABI structs in include/mpgmres/{solve,problems}.h.
+
+Field order and types must match the headers exactly.
+"""
+import ctypes as C
+
+MODES = {"mixed": 0, "baseline": 1, "single-prec": 2, "single": 3, "mixed-half": 4}
+ORTHS = {"cgs": 0, "mgs": 1, "cgsr": 2}
+PRECS = {"ilu": 0, "ilu_jacobi": 1, "jacobi": 2, "identity": 3}
+ENGINES = {"surface": 0, "fused": 1}
+STATUS = {1: "converged", 3: "aborted", -1: "error"}
+
+
+class SolveArgs(C.Structure):
+    _fields_ = [
+        ("n", C.c_int32),
+        ("nnz", C.c_int64),
+        ("rowptr", C.POINTER(C.c_int32)),
+        ("col", C.POINTER(C.c_int32)),
+        ("val", C.POINTER(C.c_double)),
+        ("b", C.POINTER(C.c_double)),
+        ("x_true", C.POINTER(C.c_double)),
+        ("mode", C.c_int32),
+        ("orth", C.c_int32),
+        ("prec", C.c_int32),
+        ("engine", C.c_int32),
+        ("rlen", C.c_int32),
+        ("tol", C.c_double),
+        ("max_restarts", C.c_int64),
+        ("rtol", C.c_double),
+        ("repeat_iter", C.c_int32),
+        ("orthloss", C.c_int32),
+        ("jacobi_steps", C.c_int32),
+        ("verbose", C.c_int32),
+        ("device", C.c_int32),
+        ("threads", C.c_int32),
+    ]
+
+
+class SolveResult(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32),
+        ("restarts", C.c_int64),
+        ("inner_k", C.c_int64),
+        ("total_iters", C.c_int64),
+        ("res_norm", C.c_double),
+        ("err_norm", C.c_double),
+        ("gmres_seconds", C.c_double),
+        ("setup_seconds", C.c_double),
+        ("minvb_norm", C.c_double),
+        ("x_out", C.POINTER(C.c_double)),
+        ("cycle_cap", C.c_int64),
+        ("n_cycles", C.c_int64),
+        ("cyc_r_norm", C.POINTER(C.c_double)),
+        ("cyc_normalization", C.POINTER(C.c_double)),
+        ("cyc_beta", C.POINTER(C.c_double)),
+        ("step_cap", C.c_int64),
+        ("n_steps", C.c_int64),
+        ("step_res", C.POINTER(C.c_double)),
+        ("step_cycle", C.POINTER(C.c_int32)),
+        ("message", C.c_char * 256),
+    ]
+
+
+class HostCsr(C.Structure):
+    _fields_ = [
+        ("nrows", C.c_int32),
+        ("ncols", C.c_int32),
+        ("nnz", C.c_int64),
+        ("rowptr", C.POINTER(C.c_int32)),
+        ("col", C.POINTER(C.c_int32)),
+        ("val", C.POINTER(C.c_double)),
+    ]

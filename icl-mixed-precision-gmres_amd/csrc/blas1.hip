@@ -1,0 +1,288 @@
+// BLAS-1 surface of the hot path on gfx950 (kernels.hpp:11-101,
+// kernels_mkl.cpp:73-260). Elementwise kernels are grid-stride with
+// contiguous lanes; reductions are a deterministic two-stage tree that
+// accumulates in fp64 for both fp32 and fp64 inputs (stage 1: one fp64
+// partial per workgroup into the context workspace, stage 2: one workgroup
+// sums the partials in a fixed order and writes the result on device).
+#include "internal.hpp"
+
+using namespace mpg;
+
+namespace {
+
+// ---------------- reductions ----------------
+template <class T, bool SQUARE>
+__global__ __launch_bounds__(kBlock) void k_reduce_stage1(int64_t n, const T* __restrict__ x,
+                                                          const T* __restrict__ y,
+                                                          double* __restrict__ partial) {
+    __shared__ double scratch[kBlock / kWave];
+    double acc = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        double a = (double)x[i];
+        acc += SQUARE ? a * a : a * (double)y[i];
+    }
+    double s = block_sum<kBlock>(acc, scratch);
+    if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+template <class T, bool SQRT>
+__global__ __launch_bounds__(1024) void k_reduce_stage2(int nparts, const double* __restrict__ partial,
+                                                        T* __restrict__ result) {
+    __shared__ double scratch[1024 / kWave];
+    double v = threadIdx.x < nparts ? partial[threadIdx.x] : 0.0;
+    double s = block_sum<1024>(v, scratch);
+    if (threadIdx.x == 0) *result = SQRT ? (T)sqrt(s) : (T)s;
+}
+
+template <class T, bool SQUARE>
+int reduce(mpg_ctx* ctx, int64_t n, const T* x, const T* y, T* result_dev) {
+    if (!ctx || n < 0) return MPG_ERR_ARG;
+    int g = grid_for(n, 4, kMaxRedBlocks);
+    k_reduce_stage1<T, SQUARE><<<g, kBlock, 0, ctx->stream>>>(n, x, y, ctx->red_ws);
+    MPG_LAUNCH_CHECK(ctx);
+    k_reduce_stage2<T, SQUARE><<<1, 1024, 0, ctx->stream>>>(g, ctx->red_ws, result_dev);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+template <class T, bool SQUARE>
+int reduce_host(mpg_ctx* ctx, int64_t n, const T* x, const T* y, T* result_host) {
+    if (!result_host) return MPG_ERR_ARG;
+    T* tmp = reinterpret_cast<T*>(ctx->red_ws + kMaxRedBlocks * kGemvMaxCols);
+    int st = reduce<T, SQUARE>(ctx, n, x, y, tmp);
+    if (st) return st;
+    MPG_HIP(ctx, hipMemcpyAsync(result_host, tmp, sizeof(T), hipMemcpyDeviceToHost, ctx->stream));
+    MPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MPG_OK;
+}
+
+// ---------------- elementwise ----------------
+// mode: 0 y += a x ; 1 y -= a x
+template <class T, bool ALPHA_DEV, bool NEG>
+__global__ __launch_bounds__(kBlock) void k_axpy(int64_t n, T alpha, const T* __restrict__ alpha_dev,
+                                                 const T* __restrict__ x, T* __restrict__ y) {
+    const T a = ALPHA_DEV ? *alpha_dev : alpha;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        if (NEG) y[i] -= a * x[i];   // naxpy: y(i) -= alpha()*x(i) (kernels_cuda.cpp:271-274)
+        else y[i] += a * x[i];
+    }
+}
+
+// y = a*x ; RECIP: a = 1/alpha formed on device in T
+template <class T, bool ALPHA_DEV, bool RECIP>
+__global__ __launch_bounds__(kBlock) void k_scal_copy(int64_t n, T alpha, const T* __restrict__ alpha_dev,
+                                                      const T* x, T* y) {
+    T a = ALPHA_DEV ? *alpha_dev : alpha;
+    if (RECIP) a = T(1) / a;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) y[i] = a * x[i];
+}
+
+template <class S, class D>
+__global__ __launch_bounds__(kBlock) void k_copy(int64_t n, const S* __restrict__ x, D* __restrict__ y) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) y[i] = (D)x[i];
+}
+
+template <class S>
+__global__ __launch_bounds__(kBlock) void k_copy_half(int64_t n, const S* __restrict__ x, uint16_t* __restrict__ y) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        y[i] = __half_as_ushort(__float2half_rn((float)x[i]));
+}
+
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_fill(T* x, int64_t rows, int64_t cols, int64_t ld, T v) {
+    const int64_t total = rows * cols;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += stride) {
+        int64_t c = t / rows, r = t - c * rows;
+        x[c * ld + r] = v;
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_gdmv(int64_t n, T alpha, const T* __restrict__ d,
+                                                 const T* x, T beta, T* y) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        y[i] = beta * y[i] + alpha * d[i] * x[i];   // kernels.hpp:141-144 (x may alias y)
+}
+
+// ---------------- Givens (single lane; O(1)/O(k) scalar work) ----------------
+// Exact IEEE order: products rounded separately, no FMA contraction, so the
+// results equal the reference BLAS formulas evaluated in T.
+#pragma clang fp contract(off)
+template <class T>
+__device__ void rotg_dev(T* a, T* b, T* c, T* s) {
+    // Reference BLAS xROTG (classic netlib form), then b := 0
+    // (kernels_mkl.cpp:214-226 zeroes b after cblas_?rotg).
+    T av = *a, bv = *b;
+    T roe = fabs(av) > fabs(bv) ? av : bv;
+    T scale = fabs(av) + fabs(bv);
+    T cc, ss, r;
+    if (scale == T(0)) {
+        cc = T(1); ss = T(0); r = T(0);
+    } else {
+        T as = av / scale, bs = bv / scale;
+        r = scale * sqrt(as * as + bs * bs);
+        r = roe >= T(0) ? r : -r;
+        cc = av / r;
+        ss = bv / r;
+    }
+    *a = r;
+    *b = T(0);
+    *c = cc;
+    *s = ss;
+}
+
+template <class T>
+__device__ void rot_pair(T* a, T* b, T c, T s) {
+    T a1 = *a, a2 = *b;
+    *a = c * a1 + s * a2;
+    *b = c * a2 - s * a1;
+}
+#pragma clang fp contract(on)
+
+template <class T>
+__global__ void k_rotg(T* a, T* b, T* c, T* s) { rotg_dev(a, b, c, s); }
+
+template <class T>
+__global__ void k_rot(T* a, T* b, const T* c, const T* s) { rot_pair(a, b, *c, *s); }
+
+template <class T>
+__global__ void k_rot_vec(int k, T* a, const T* c, const T* s) {
+    for (int j = 0; j < k; ++j) rot_pair(a + j, a + j + 1, c[j], s[j]);
+}
+
+template <class T, bool ALPHA_DEV>
+__global__ void k_scal_scalar(T alpha, const T* alpha_dev, const T* x, T* y) {
+    y[0] = (ALPHA_DEV ? *alpha_dev : alpha) * x[0];
+}
+
+template <class T, bool ALPHA_DEV, bool NEG>
+int axpy_impl(mpg_ctx* ctx, int64_t n, T alpha, const T* alpha_dev, const T* x, T* y) {
+    if (!ctx || n < 0) return MPG_ERR_ARG;
+    if (n == 0) return MPG_OK;
+    k_axpy<T, ALPHA_DEV, NEG><<<grid_for(n, 4), kBlock, 0, ctx->stream>>>(n, alpha, alpha_dev, x, y);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+template <class T, bool ALPHA_DEV, bool RECIP>
+int scal_copy_impl(mpg_ctx* ctx, int64_t n, T alpha, const T* alpha_dev, const T* x, T* y) {
+    if (!ctx || n < 0) return MPG_ERR_ARG;
+    if (n == 0) return MPG_OK;
+    k_scal_copy<T, ALPHA_DEV, RECIP><<<grid_for(n, 4), kBlock, 0, ctx->stream>>>(n, alpha, alpha_dev, x, y);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+template <class S, class D>
+int copy_impl(mpg_ctx* ctx, int64_t n, const S* x, D* y) {
+    if (!ctx || n < 0) return MPG_ERR_ARG;
+    if (n == 0) return MPG_OK;
+    k_copy<S, D><<<grid_for(n, 4), kBlock, 0, ctx->stream>>>(n, x, y);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+template <class T>
+int fill_impl(mpg_ctx* ctx, T* x, int64_t rows, int64_t cols, int64_t ld, T v) {
+    if (!ctx || rows < 0 || cols < 0 || (cols > 1 && ld < rows)) return MPG_ERR_ARG;
+    if (rows == 0 || cols == 0) return MPG_OK;
+    k_fill<T><<<grid_for(rows * cols, 4), kBlock, 0, ctx->stream>>>(x, rows, cols, ld, v);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+template <class T>
+int gdmv_impl(mpg_ctx* ctx, int64_t n, T alpha, const T* d, const T* x, T beta, T* y) {
+    if (!ctx || n < 0) return MPG_ERR_ARG;
+    if (n == 0) return MPG_OK;
+    k_gdmv<T><<<grid_for(n, 4), kBlock, 0, ctx->stream>>>(n, alpha, d, x, beta, y);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpg_dot_f64(mpg_ctx_t c, int64_t n, const double* x, const double* y, double* r) { return reduce<double, false>(c, n, x, y, r); }
+int mpg_dot_f32(mpg_ctx_t c, int64_t n, const float* x, const float* y, float* r) { return reduce<float, false>(c, n, x, y, r); }
+int mpg_dot_f64_host(mpg_ctx_t c, int64_t n, const double* x, const double* y, double* r) { return reduce_host<double, false>(c, n, x, y, r); }
+int mpg_dot_f32_host(mpg_ctx_t c, int64_t n, const float* x, const float* y, float* r) { return reduce_host<float, false>(c, n, x, y, r); }
+int mpg_nrm2_f64(mpg_ctx_t c, int64_t n, const double* x, double* r) { return reduce<double, true>(c, n, x, x, r); }
+int mpg_nrm2_f32(mpg_ctx_t c, int64_t n, const float* x, float* r) { return reduce<float, true>(c, n, x, x, r); }
+int mpg_nrm2_f64_host(mpg_ctx_t c, int64_t n, const double* x, double* r) { return reduce_host<double, true>(c, n, x, x, r); }
+int mpg_nrm2_f32_host(mpg_ctx_t c, int64_t n, const float* x, float* r) { return reduce_host<float, true>(c, n, x, x, r); }
+
+int mpg_axpy_f64(mpg_ctx_t c, int64_t n, double a, const double* x, double* y) { return axpy_impl<double, false, false>(c, n, a, nullptr, x, y); }
+int mpg_axpy_f32(mpg_ctx_t c, int64_t n, float a, const float* x, float* y) { return axpy_impl<float, false, false>(c, n, a, nullptr, x, y); }
+int mpg_axpy_dev_f64(mpg_ctx_t c, int64_t n, const double* a, const double* x, double* y) { return axpy_impl<double, true, false>(c, n, 0.0, a, x, y); }
+int mpg_axpy_dev_f32(mpg_ctx_t c, int64_t n, const float* a, const float* x, float* y) { return axpy_impl<float, true, false>(c, n, 0.f, a, x, y); }
+int mpg_naxpy_dev_f64(mpg_ctx_t c, int64_t n, const double* a, const double* x, double* y) { return axpy_impl<double, true, true>(c, n, 0.0, a, x, y); }
+int mpg_naxpy_dev_f32(mpg_ctx_t c, int64_t n, const float* a, const float* x, float* y) { return axpy_impl<float, true, true>(c, n, 0.f, a, x, y); }
+
+int mpg_scal_f64(mpg_ctx_t c, int64_t n, double a, double* x) { return scal_copy_impl<double, false, false>(c, n, a, nullptr, x, x); }
+int mpg_scal_f32(mpg_ctx_t c, int64_t n, float a, float* x) { return scal_copy_impl<float, false, false>(c, n, a, nullptr, x, x); }
+int mpg_scal_copy_f64(mpg_ctx_t c, int64_t n, double a, const double* x, double* y) { return scal_copy_impl<double, false, false>(c, n, a, nullptr, x, y); }
+int mpg_scal_copy_f32(mpg_ctx_t c, int64_t n, float a, const float* x, float* y) { return scal_copy_impl<float, false, false>(c, n, a, nullptr, x, y); }
+int mpg_scal_copy_dev_f64(mpg_ctx_t c, int64_t n, const double* a, const double* x, double* y) { return scal_copy_impl<double, true, false>(c, n, 0.0, a, x, y); }
+int mpg_scal_copy_dev_f32(mpg_ctx_t c, int64_t n, const float* a, const float* x, float* y) { return scal_copy_impl<float, true, false>(c, n, 0.f, a, x, y); }
+int mpg_scal_recip_copy_dev_f64(mpg_ctx_t c, int64_t n, const double* a, const double* x, double* y) { return scal_copy_impl<double, true, true>(c, n, 0.0, a, x, y); }
+int mpg_scal_recip_copy_dev_f32(mpg_ctx_t c, int64_t n, const float* a, const float* x, float* y) { return scal_copy_impl<float, true, true>(c, n, 0.f, a, x, y); }
+
+int mpg_copy_f64f64(mpg_ctx_t c, int64_t n, const double* x, double* y) { return copy_impl(c, n, x, y); }
+int mpg_copy_f32f32(mpg_ctx_t c, int64_t n, const float* x, float* y) { return copy_impl(c, n, x, y); }
+int mpg_copy_f64f32(mpg_ctx_t c, int64_t n, const double* x, float* y) { return copy_impl(c, n, x, y); }
+int mpg_copy_f32f64(mpg_ctx_t c, int64_t n, const float* x, double* y) { return copy_impl(c, n, x, y); }
+int mpg_copy_f64f16(mpg_ctx_t c, int64_t n, const double* x, uint16_t* y) {
+    if (!c || n < 0) return MPG_ERR_ARG;
+    if (n == 0) return MPG_OK;
+    k_copy_half<double><<<grid_for(n, 4), kBlock, 0, c->stream>>>(n, x, y);
+    MPG_LAUNCH_CHECK(c);
+    return MPG_OK;
+}
+int mpg_copy_f32f16(mpg_ctx_t c, int64_t n, const float* x, uint16_t* y) {
+    if (!c || n < 0) return MPG_ERR_ARG;
+    if (n == 0) return MPG_OK;
+    k_copy_half<float><<<grid_for(n, 4), kBlock, 0, c->stream>>>(n, x, y);
+    MPG_LAUNCH_CHECK(c);
+    return MPG_OK;
+}
+
+int mpg_fill_f64(mpg_ctx_t c, double* x, int64_t r, int64_t cl, int64_t ld, double v) { return fill_impl(c, x, r, cl, ld, v); }
+int mpg_fill_f32(mpg_ctx_t c, float* x, int64_t r, int64_t cl, int64_t ld, float v) { return fill_impl(c, x, r, cl, ld, v); }
+int mpg_gdmv_f64(mpg_ctx_t c, int64_t n, double a, const double* d, const double* x, double b, double* y) { return gdmv_impl(c, n, a, d, x, b, y); }
+int mpg_gdmv_f32(mpg_ctx_t c, int64_t n, float a, const float* d, const float* x, float b, float* y) { return gdmv_impl(c, n, a, d, x, b, y); }
+
+#define MPG_SINGLE(ctx, launch)             \
+    do {                                    \
+        if (!(ctx)) return MPG_ERR_ARG;     \
+        launch;                             \
+        MPG_LAUNCH_CHECK(ctx);              \
+        return MPG_OK;                      \
+    } while (0)
+
+int mpg_rotg_f64(mpg_ctx_t c, double* a, double* b, double* cs, double* s) { MPG_SINGLE(c, (k_rotg<double><<<1, 1, 0, c->stream>>>(a, b, cs, s))); }
+int mpg_rotg_f32(mpg_ctx_t c, float* a, float* b, float* cs, float* s) { MPG_SINGLE(c, (k_rotg<float><<<1, 1, 0, c->stream>>>(a, b, cs, s))); }
+int mpg_rot_f64(mpg_ctx_t c, double* a, double* b, const double* cs, const double* s) { MPG_SINGLE(c, (k_rot<double><<<1, 1, 0, c->stream>>>(a, b, cs, s))); }
+int mpg_rot_f32(mpg_ctx_t c, float* a, float* b, const float* cs, const float* s) { MPG_SINGLE(c, (k_rot<float><<<1, 1, 0, c->stream>>>(a, b, cs, s))); }
+int mpg_rot_vec_f64(mpg_ctx_t c, int k, double* a, const double* cs, const double* s) {
+    if (k <= 0) return c ? MPG_OK : MPG_ERR_ARG;
+    MPG_SINGLE(c, (k_rot_vec<double><<<1, 1, 0, c->stream>>>(k, a, cs, s)));
+}
+int mpg_rot_vec_f32(mpg_ctx_t c, int k, float* a, const float* cs, const float* s) {
+    if (k <= 0) return c ? MPG_OK : MPG_ERR_ARG;
+    MPG_SINGLE(c, (k_rot_vec<float><<<1, 1, 0, c->stream>>>(k, a, cs, s)));
+}
+int mpg_scal_scalar_f64(mpg_ctx_t c, double a, const double* x, double* y) { MPG_SINGLE(c, (k_scal_scalar<double, false><<<1, 1, 0, c->stream>>>(a, nullptr, x, y))); }
+int mpg_scal_scalar_f32(mpg_ctx_t c, float a, const float* x, float* y) { MPG_SINGLE(c, (k_scal_scalar<float, false><<<1, 1, 0, c->stream>>>(a, nullptr, x, y))); }
+int mpg_scal_scalar_dev_f64(mpg_ctx_t c, const double* a, const double* x, double* y) { MPG_SINGLE(c, (k_scal_scalar<double, true><<<1, 1, 0, c->stream>>>(0.0, a, x, y))); }
+int mpg_scal_scalar_dev_f32(mpg_ctx_t c, const float* a, const float* x, float* y) { MPG_SINGLE(c, (k_scal_scalar<float, true><<<1, 1, 0, c->stream>>>(0.f, a, x, y))); }
+
+}  // extern "C"

@@ -1,0 +1,178 @@
+// BLAS-2 surface (kernels_mkl.cpp:264-321): column-major gemv with explicit
+// lda, and small triangular solves.
+//
+// gemv^T on a tall-skinny panel (the CGS V^T w of Orthogonalization.hpp:
+// 83-87) is a two-stage panel reduction: every workgroup streams a slab of
+// rows once, keeps one fp64 accumulator per column (<= 32 per pass) in
+// registers, reduces each across its 4 waves with wave64 shuffles, and
+// writes per-workgroup partials; stage 2 sums the partials of each column in
+// a fixed order. gemv (no transpose) is row-per-lane with fp64 accumulation.
+#include "internal.hpp"
+
+using namespace mpg;
+
+namespace {
+
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_gemv_t_stage1(int64_t rows, int ncols, const T* __restrict__ A,
+                                                          int64_t lda, const T* __restrict__ x,
+                                                          double* __restrict__ partial) {
+    __shared__ double scratch[kBlock / kWave][kGemvMaxCols];
+    double acc[kGemvMaxCols];
+#pragma unroll
+    for (int c = 0; c < kGemvMaxCols; ++c) acc[c] = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < rows; i += stride) {
+        const double xi = (double)x[i];
+#pragma unroll
+        for (int c = 0; c < kGemvMaxCols; ++c)
+            if (c < ncols) acc[c] += (double)A[(int64_t)c * lda + i] * xi;
+    }
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+#pragma unroll
+    for (int c = 0; c < kGemvMaxCols; ++c) {
+        if (c < ncols) {
+            double v = wave_sum(acc[c]);
+            if (lane == 0) scratch[wid][c] = v;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < ncols) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kBlock / kWave; ++w) s += scratch[w][threadIdx.x];
+        partial[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(1024) void k_gemv_t_stage2(int nparts, const double* __restrict__ partial,
+                                                        T alpha, T beta, T* __restrict__ y) {
+    __shared__ double scratch[1024 / kWave];
+    const int c = blockIdx.x;
+    double v = threadIdx.x < nparts ? partial[(int64_t)c * nparts + threadIdx.x] : 0.0;
+    double s = block_sum<1024>(v, scratch);
+    if (threadIdx.x == 0) {
+        T t = (T)s;
+        y[c] = beta == T(0) ? alpha * t : alpha * t + beta * y[c];
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_gemv_n(int64_t rows, int64_t cols, T alpha, const T* __restrict__ A,
+                                                   int64_t lda, const T* __restrict__ x, T beta,
+                                                   T* __restrict__ y) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < rows; i += stride) {
+        double acc = 0.0;
+        for (int64_t c = 0; c < cols; ++c) acc += (double)A[c * lda + i] * (double)x[c];
+        T t = (T)acc;
+        y[i] = beta == T(0) ? alpha * t : alpha * t + beta * y[i];
+    }
+}
+
+template <class T>
+int gemv_impl(mpg_ctx* ctx, int trans, int64_t rows, int64_t cols, T alpha, const T* A, int64_t lda,
+              const T* x, T beta, T* y) {
+    if (!ctx || rows < 0 || cols < 0 || (cols > 0 && lda < (rows > 0 ? rows : 1))) return MPG_ERR_ARG;
+    if (!trans) {
+        if (rows == 0) return MPG_OK;
+        k_gemv_n<T><<<grid_for(rows, 1), kBlock, 0, ctx->stream>>>(rows, cols, alpha, A, lda, x, beta, y);
+        MPG_LAUNCH_CHECK(ctx);
+        return MPG_OK;
+    }
+    if (cols == 0) return MPG_OK;
+    int g = grid_for(rows, 4, kMaxRedBlocks);
+    for (int64_t c0 = 0; c0 < cols; c0 += kGemvMaxCols) {
+        int nc = (int)((cols - c0) < kGemvMaxCols ? (cols - c0) : kGemvMaxCols);
+        k_gemv_t_stage1<T><<<g, kBlock, 0, ctx->stream>>>(rows, nc, A + c0 * lda, lda, x, ctx->red_ws);
+        MPG_LAUNCH_CHECK(ctx);
+        k_gemv_t_stage2<T><<<nc, 1024, 0, ctx->stream>>>(g, ctx->red_ws, alpha, beta, y + c0);
+        MPG_LAUNCH_CHECK(ctx);
+    }
+    return MPG_OK;
+}
+
+// Triangular solve on one workgroup, x staged in LDS. Column-oriented
+// (axpy) forms for the non-transposed solves, row-oriented (dot) forms for
+// the transposed ones — the operation order of the reference BLAS xTRSV,
+// with rounded products (no FMA contraction).
+#pragma clang fp contract(off)
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_trsv(int upper, int trans, int n, const T* __restrict__ A,
+                                                 int64_t lda, T* __restrict__ x) {
+    extern __shared__ unsigned char smem_raw[];
+    T* xs = reinterpret_cast<T*>(smem_raw);
+    for (int i = threadIdx.x; i < n; i += kBlock) xs[i] = x[i];
+    __syncthreads();
+    if (!trans) {
+        for (int step = 0; step < n; ++step) {
+            const int j = upper ? n - 1 - step : step;
+            __shared__ T temp_s;
+            if (threadIdx.x == 0) {
+                T xj = xs[j];
+                if (xj != T(0)) xj = xj / A[(int64_t)j * lda + j];
+                xs[j] = xj;
+                temp_s = xj;
+            }
+            __syncthreads();
+            const T temp = temp_s;
+            if (temp != T(0)) {
+                if (upper) {
+                    for (int i = threadIdx.x; i < j; i += kBlock) xs[i] = xs[i] - temp * A[(int64_t)j * lda + i];
+                } else {
+                    for (int i = j + 1 + threadIdx.x; i < n; i += kBlock) xs[i] = xs[i] - temp * A[(int64_t)j * lda + i];
+                }
+            }
+            __syncthreads();
+        }
+    } else if (threadIdx.x == 0) {
+        if (upper) {  // solve U^T x = b : forward
+            for (int j = 0; j < n; ++j) {
+                T temp = xs[j];
+                for (int i = 0; i < j; ++i) temp = temp - A[(int64_t)j * lda + i] * xs[i];
+                xs[j] = temp / A[(int64_t)j * lda + j];
+            }
+        } else {      // solve L^T x = b : backward
+            for (int j = n - 1; j >= 0; --j) {
+                T temp = xs[j];
+                for (int i = n - 1; i > j; --i) temp = temp - A[(int64_t)j * lda + i] * xs[i];
+                xs[j] = temp / A[(int64_t)j * lda + j];
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += kBlock) x[i] = xs[i];
+}
+#pragma clang fp contract(on)
+
+template <class T>
+int trsv_impl(mpg_ctx* ctx, int upper, int trans, int64_t n, const T* A, int64_t lda, T* x) {
+    if (!ctx || n < 0 || n > 4096 || (n > 0 && lda < n)) return MPG_ERR_ARG;
+    if (n == 0) return MPG_OK;
+    k_trsv<T><<<1, kBlock, n * sizeof(T), ctx->stream>>>(upper, trans, (int)n, A, lda, x);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpg_gemv_f64(mpg_ctx_t c, int trans, int64_t rows, int64_t cols, double alpha, const double* A,
+                 int64_t lda, const double* x, double beta, double* y) {
+    return gemv_impl<double>(c, trans, rows, cols, alpha, A, lda, x, beta, y);
+}
+int mpg_gemv_f32(mpg_ctx_t c, int trans, int64_t rows, int64_t cols, float alpha, const float* A,
+                 int64_t lda, const float* x, float beta, float* y) {
+    return gemv_impl<float>(c, trans, rows, cols, alpha, A, lda, x, beta, y);
+}
+int mpg_trsv_f64(mpg_ctx_t c, int upper, int trans, int64_t n, const double* A, int64_t lda, double* x) {
+    return trsv_impl<double>(c, upper, trans, n, A, lda, x);
+}
+int mpg_trsv_f32(mpg_ctx_t c, int upper, int trans, int64_t n, const float* A, int64_t lda, float* x) {
+    return trsv_impl<float>(c, upper, trans, n, A, lda, x);
+}
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+// Context, memory and error plumbing of the C-ABI (include/mpgmres/capi.h).
+// Replaces the Kokkos::View allocation / deep_copy layer (types.hpp:15-228)
+// and the global cuBLAS/cuSPARSE singleton (types_cuda.hpp:9-36): one
+// explicit context per (GPU, host thread), no global mutable state.
+#include "internal.hpp"
+
+#include <new>
+
+extern "C" {
+
+const char* mpg_error_string(int status) {
+    switch (status) {
+        case MPG_OK: return "ok";
+        case MPG_ERR_HIP: return "HIP runtime error";
+        case MPG_ERR_ARG: return "invalid argument";
+        case MPG_ERR_ALLOC: return "device allocation failed";
+        case MPG_ERR_RCCL: return "RCCL error";
+        case MPG_ERR_UNSUPPORTED: return "unsupported operation";
+        case MPG_ERR_BREAKDOWN: return "Arnoldi breakdown / non-finite value";
+        default: return "unknown mpgmres status";
+    }
+}
+
+const char* mpg_ctx_last_error(mpg_ctx_t ctx) {
+    return ctx ? ctx->last_error.c_str() : "null context";
+}
+
+int mpg_ctx_create(int device, mpg_ctx_t* out) {
+    if (!out) return MPG_ERR_ARG;
+    *out = nullptr;
+    mpg_ctx* ctx = new (std::nothrow) mpg_ctx();
+    if (!ctx) return MPG_ERR_ALLOC;
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) {
+        ctx->red_ws_elems = (size_t)mpg::kMaxRedBlocks * mpg::kGemvMaxCols + 64;
+        e = hipMalloc(&ctx->red_ws, ctx->red_ws_elems * sizeof(double));
+    }
+    if (e != hipSuccess) {
+        if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        delete ctx;
+        return MPG_ERR_HIP;
+    }
+    *out = ctx;
+    return MPG_OK;
+}
+
+int mpg_ctx_destroy(mpg_ctx_t ctx) {
+    if (!ctx) return MPG_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->red_ws) (void)hipFree(ctx->red_ws);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return MPG_OK;
+}
+
+int mpg_ctx_sync(mpg_ctx_t ctx) {
+    if (!ctx) return MPG_ERR_ARG;
+    MPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MPG_OK;
+}
+
+void* mpg_ctx_stream(mpg_ctx_t ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int mpg_ctx_device(mpg_ctx_t ctx) { return ctx ? ctx->device : -1; }
+
+int mpg_malloc(mpg_ctx_t ctx, size_t bytes, void** out_dev) {
+    if (!ctx || !out_dev) return MPG_ERR_ARG;
+    *out_dev = nullptr;
+    if (bytes == 0) return MPG_OK;
+    // Round up to 256 B so vectorised kernels may touch whole 16-B granules.
+    size_t padded = (bytes + 255) & ~size_t(255);
+    hipError_t e = hipMalloc(out_dev, padded);
+    if (e != hipSuccess) {
+        mpg::set_hip_error(ctx, e, "hipMalloc");
+        return MPG_ERR_ALLOC;
+    }
+    MPG_HIP(ctx, hipMemsetAsync(*out_dev, 0, padded, ctx->stream));
+    return MPG_OK;
+}
+
+int mpg_free(mpg_ctx_t ctx, void* ptr_dev) {
+    if (!ptr_dev) return MPG_OK;
+    if (ctx) MPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    MPG_HIP(ctx, hipFree(ptr_dev));
+    return MPG_OK;
+}
+
+int mpg_memset(mpg_ctx_t ctx, void* ptr_dev, int value, size_t bytes) {
+    if (!ctx) return MPG_ERR_ARG;
+    if (bytes == 0) return MPG_OK;
+    MPG_HIP(ctx, hipMemsetAsync(ptr_dev, value, bytes, ctx->stream));
+    return MPG_OK;
+}
+
+int mpg_memcpy_h2d(mpg_ctx_t ctx, void* dst_dev, const void* src_host, size_t bytes) {
+    if (!ctx) return MPG_ERR_ARG;
+    if (bytes == 0) return MPG_OK;
+    MPG_HIP(ctx, hipMemcpyAsync(dst_dev, src_host, bytes, hipMemcpyHostToDevice, ctx->stream));
+    // The host buffer may be pageable and reused by the caller right away.
+    MPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MPG_OK;
+}
+
+int mpg_memcpy_d2h(mpg_ctx_t ctx, void* dst_host, const void* src_dev, size_t bytes) {
+    if (!ctx) return MPG_ERR_ARG;
+    if (bytes == 0) return MPG_OK;
+    MPG_HIP(ctx, hipMemcpyAsync(dst_host, src_dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    MPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return MPG_OK;
+}
+
+int mpg_memcpy_d2d(mpg_ctx_t ctx, void* dst_dev, const void* src_dev, size_t bytes) {
+    if (!ctx) return MPG_ERR_ARG;
+    if (bytes == 0) return MPG_OK;
+    MPG_HIP(ctx, hipMemcpyAsync(dst_dev, src_dev, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    return MPG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,114 @@
+// Internal helpers shared by the gfx950 kernels of libmpgmres_hip.so.
+// Not part of the C-ABI (see include/mpgmres/capi.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdint>
+#include <string>
+
+#include "mpgmres/capi.h"
+
+struct mpg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // Reduction workspace: per-workgroup fp64 partials of the two-stage
+    // deterministic reductions (dot, nrm2, gemv^T, Jacobi alpha).
+    double* red_ws = nullptr;
+    size_t red_ws_elems = 0;
+    std::string last_error;
+};
+
+namespace mpg {
+
+constexpr int kWave = 64;            // CDNA wavefront width (never 32)
+constexpr int kBlock = 256;          // default workgroup: 4 waves
+constexpr int kMaxRedBlocks = 1024;  // stage-1 grid cap for reductions
+constexpr int kGemvMaxCols = 32;     // columns per panel pass of gemv^T
+
+inline int set_hip_error(mpg_ctx* ctx, hipError_t e, const char* what) {
+    if (ctx) {
+        ctx->last_error = std::string(what) + ": " + hipGetErrorString(e);
+    }
+    return MPG_ERR_HIP;
+}
+
+#define MPG_HIP(ctx, call)                                              \
+    do {                                                                \
+        hipError_t mpg_e_ = (call);                                     \
+        if (mpg_e_ != hipSuccess) return mpg::set_hip_error(ctx, mpg_e_, #call); \
+    } while (0)
+
+#define MPG_LAUNCH_CHECK(ctx)                                           \
+    do {                                                                \
+        hipError_t mpg_e_ = hipGetLastError();                          \
+        if (mpg_e_ != hipSuccess) return mpg::set_hip_error(ctx, mpg_e_, "kernel launch"); \
+    } while (0)
+
+inline int grid_for(int64_t n, int per_thread, int cap = 2048) {
+    int64_t g = (n + (int64_t)kBlock * per_thread - 1) / ((int64_t)kBlock * per_thread);
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+// ---- wave / block reductions (wave64 shuffles, then LDS across waves) ----
+template <class T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_down(v, off, kWave);
+    return v;  // valid in lane 0
+}
+
+template <class T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        T o = __shfl_down(v, off, kWave);
+        v = v > o ? v : o;
+    }
+    return v;
+}
+
+// Block-wide sum for blockDim.x == BS (multiple of 64). Result valid in
+// thread 0. `scratch` must hold BS/64 elements.
+template <int BS, class T>
+__device__ __forceinline__ T block_sum(T v, T* scratch) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    v = wave_sum(v);
+    if (lane == 0) scratch[wid] = v;
+    __syncthreads();
+    T r = 0;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int w = 0; w < BS / kWave; ++w) r += scratch[w];
+    }
+    __syncthreads();
+    return r;
+}
+
+template <int BS, class T>
+__device__ __forceinline__ T block_max(T v, T* scratch) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    v = wave_max(v);
+    if (lane == 0) scratch[wid] = v;
+    __syncthreads();
+    T r = scratch[0];
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int w = 1; w < BS / kWave; ++w) r = r > scratch[w] ? r : scratch[w];
+    }
+    __syncthreads();
+    return r;
+}
+
+template <class T> struct acc_type { using type = double; };
+
+__device__ __forceinline__ float to_float(uint16_t h) {
+    return __half2float(__ushort_as_half(h));
+}
+
+}  // namespace mpg

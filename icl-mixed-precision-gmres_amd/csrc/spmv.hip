@@ -1,0 +1,222 @@
+// CSR SpMV on gfx950 (replaces mkl_sparse_?_mv, kernels_mkl.cpp:326-352, and
+// legacy cusparse?csrmv, kernels_cuda.cpp:576-614) + Jacobi setup
+// (types.hpp:393-431).
+//
+// CSR-adaptive schedule. mpg_csr_create splits the rows into "row blocks":
+// consecutive rows whose total nnz fits kNnzCap (streamed through LDS), or a
+// single row (long-row mode: the whole workgroup reduces it). One 256-lane
+// workgroup per row block:
+//   stream mode: lanes load (val, col) contiguously — every wave instruction
+//     touches 64 consecutive nonzeros — gather x[col], form the fp64 product
+//     and stage it in LDS; then one lane per row sums its LDS segment in
+//     column order (a segmented reduction with no cross-lane traffic);
+//   row mode: strided fp64 partial sums, wave64 shuffle + LDS tree.
+// Products and sums are fp64 for every precision (exact products for fp32
+// and fp16 values); the row sum is rounded once to the vector type, then
+// y = alpha*sum (+ beta*y when beta != 0).
+#include "internal.hpp"
+
+#include <cfloat>
+#include <new>
+#include <vector>
+
+using namespace mpg;
+
+struct mpg_csr {
+    mpg_ctx* ctx = nullptr;
+    int32_t rows = 0, cols = 0;
+    int64_t nnz = 0;
+    const int32_t* rowptr = nullptr;  // device, borrowed
+    const int32_t* col = nullptr;     // device, borrowed
+    int32_t* blocks = nullptr;        // device, owned: nblocks+1 row starts
+    int nblocks = 0;
+};
+
+namespace {
+
+constexpr int kNnzCap = 2048;   // nonzeros staged per stream-mode row block
+constexpr int kRowCap = 2048;   // rows per stream-mode row block
+
+template <class V>
+__device__ __forceinline__ double val_as_double(const V* v, int64_t i) { return (double)v[i]; }
+template <>
+__device__ __forceinline__ double val_as_double<uint16_t>(const uint16_t* v, int64_t i) {
+    return (double)to_float(v[i]);
+}
+
+template <class V, class X>
+__global__ __launch_bounds__(kBlock) void k_csr_adaptive(const int32_t* __restrict__ blocks,
+                                                         const int32_t* __restrict__ rowptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const V* __restrict__ val,
+                                                         const X* __restrict__ x, X alpha, X beta,
+                                                         X* __restrict__ y) {
+    __shared__ double prod[kNnzCap];
+    __shared__ double scratch[kBlock / kWave];
+    const int b = blockIdx.x;
+    const int r0 = blocks[b], r1 = blocks[b + 1];
+    const int nrows = r1 - r0;
+    const int s = rowptr[r0];
+    const int e = rowptr[r1];
+    if (nrows == 1) {
+        double acc = 0.0;
+        for (int i = s + threadIdx.x; i < e; i += kBlock) acc += val_as_double(val, i) * (double)x[col[i]];
+        double sum = block_sum<kBlock>(acc, scratch);
+        if (threadIdx.x == 0) {
+            X t = (X)sum;
+            y[r0] = beta == X(0) ? alpha * t : alpha * t + beta * y[r0];
+        }
+        return;
+    }
+    const int nnz = e - s;
+    for (int i = threadIdx.x; i < nnz; i += kBlock)
+        prod[i] = val_as_double(val, s + i) * (double)x[col[s + i]];
+    __syncthreads();
+    for (int r = threadIdx.x; r < nrows; r += kBlock) {
+        const int a = rowptr[r0 + r] - s;
+        const int z = rowptr[r0 + r + 1] - s;
+        double acc = 0.0;
+        for (int j = a; j < z; ++j) acc += prod[j];
+        X t = (X)acc;
+        y[r0 + r] = beta == X(0) ? alpha * t : alpha * t + beta * y[r0 + r];
+    }
+}
+
+template <class V, class X>
+int spmv_impl(mpg_ctx* ctx, mpg_csr* A, X alpha, const V* vals, const X* x, X beta, X* y) {
+    if (!ctx || !A) return MPG_ERR_ARG;
+    if (A->rows == 0) return MPG_OK;
+    k_csr_adaptive<V, X><<<A->nblocks, kBlock, 0, ctx->stream>>>(A->blocks, A->rowptr, A->col, vals, x,
+                                                                 alpha, beta, y);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+// ---------------- Jacobi setup (types.hpp:393-431) ----------------
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_rowabs_max(int32_t rows, const int32_t* __restrict__ rowptr,
+                                                       const T* __restrict__ val, double* __restrict__ partial) {
+    __shared__ double scratch[kBlock / kWave];
+    double m = 0.0;
+    const int stride = gridDim.x * kBlock;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < rows; i += stride) {
+        T sum = 0;  // summed in the values' precision, as the Kokkos lambda does
+        for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) sum += fabs(val[k]);
+        m = (double)sum > m ? (double)sum : m;
+    }
+    double bm = block_max<kBlock>(m, scratch);
+    if (threadIdx.x == 0) partial[blockIdx.x] = bm;
+}
+
+template <class T>
+__global__ __launch_bounds__(1024) void k_alpha(int nparts, const double* __restrict__ partial, T* __restrict__ alpha_out) {
+    __shared__ double scratch[1024 / kWave];
+    double v = threadIdx.x < nparts ? partial[threadIdx.x] : 0.0;
+    double m = block_max<1024>(v, scratch);
+    if (threadIdx.x == 0) {
+        T a = (T)m;                 // exact: m is one of the T row sums
+        a *= (T)FLT_EPSILON;        // alpha *= numeric_limits<float>::epsilon()
+        *alpha_out = a;
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_jacobi_diag(int32_t rows, int64_t nnz, const int32_t* __restrict__ rowptr,
+                                                        const int32_t* __restrict__ col, const T* __restrict__ val,
+                                                        const T* __restrict__ alpha_p, T* __restrict__ diag) {
+    const T alpha = *alpha_p;
+    const int stride = gridDim.x * kBlock;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < rows; i += stride) {
+        int64_t j = rowptr[i];
+        // `while (inds(j) < i) ++j;` — bounded here so a row without a
+        // diagonal cannot run off the end of the arrays.
+        while (j < nnz - 1 && col[j] < i) ++j;
+        const T v = val[j];
+        if (v >= T(0)) diag[i] = T(1) / ((v < alpha) ? alpha : v);
+        else diag[i] = T(1) / ((v > -alpha) ? -alpha : v);
+    }
+}
+
+template <class T>
+int jacobi_impl(mpg_ctx* ctx, mpg_csr* A, const T* vals, T* diag) {
+    if (!ctx || !A) return MPG_ERR_ARG;
+    if (A->rows == 0) return MPG_OK;
+    int g = grid_for(A->rows, 1, kMaxRedBlocks);
+    k_rowabs_max<T><<<g, kBlock, 0, ctx->stream>>>(A->rows, A->rowptr, vals, ctx->red_ws);
+    MPG_LAUNCH_CHECK(ctx);
+    T* alpha = reinterpret_cast<T*>(ctx->red_ws + (size_t)kMaxRedBlocks * kGemvMaxCols + 16);
+    k_alpha<T><<<1, 1024, 0, ctx->stream>>>(g, ctx->red_ws, alpha);
+    MPG_LAUNCH_CHECK(ctx);
+    k_jacobi_diag<T><<<grid_for(A->rows, 1), kBlock, 0, ctx->stream>>>(A->rows, A->nnz, A->rowptr, A->col, vals,
+                                                                      alpha, diag);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpg_csr_create(mpg_ctx_t ctx, int32_t rows, int32_t cols, int64_t nnz, const int32_t* rowptr_host,
+                   const int32_t* rowptr_dev, const int32_t* col_dev, mpg_csr_t* out) {
+    if (!ctx || !out || rows < 0 || cols < 0 || nnz < 0 || nnz > INT32_MAX || !rowptr_host) return MPG_ERR_ARG;
+    *out = nullptr;
+    if (rowptr_host[0] != 0 || rowptr_host[rows] != nnz) return MPG_ERR_ARG;
+    std::vector<int32_t> starts;
+    starts.reserve(rows / 64 + 2);
+    int32_t r = 0;
+    while (r < rows) {
+        starts.push_back(r);
+        const int64_t base = rowptr_host[r];
+        int32_t q = r + 1;
+        if (rowptr_host[q] - base <= kNnzCap) {
+            while (q < rows && q - r < kRowCap && rowptr_host[q + 1] - base <= kNnzCap) ++q;
+        }
+        r = q;
+    }
+    starts.push_back(rows);
+    mpg_csr* A = new (std::nothrow) mpg_csr();
+    if (!A) return MPG_ERR_ALLOC;
+    A->ctx = ctx;
+    A->rows = rows;
+    A->cols = cols;
+    A->nnz = nnz;
+    A->rowptr = rowptr_dev;
+    A->col = col_dev;
+    A->nblocks = (int)starts.size() - 1;
+    hipError_t e = hipMalloc(&A->blocks, starts.size() * sizeof(int32_t));
+    if (e == hipSuccess)
+        e = hipMemcpy(A->blocks, starts.data(), starts.size() * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (A->blocks) (void)hipFree(A->blocks);
+        delete A;
+        return set_hip_error(ctx, e, "mpg_csr_create");
+    }
+    *out = A;
+    return MPG_OK;
+}
+
+int mpg_csr_destroy(mpg_csr_t A) {
+    if (!A) return MPG_OK;
+    if (A->ctx) (void)hipStreamSynchronize(A->ctx->stream);
+    if (A->blocks) (void)hipFree(A->blocks);
+    delete A;
+    return MPG_OK;
+}
+
+int mpg_csr_num_blocks(mpg_csr_t A) { return A ? A->nblocks : -1; }
+
+int mpg_csr_spmv_f64(mpg_ctx_t c, mpg_csr_t A, double alpha, const double* vals, const double* x, double beta, double* y) {
+    return spmv_impl<double, double>(c, A, alpha, vals, x, beta, y);
+}
+int mpg_csr_spmv_f32(mpg_ctx_t c, mpg_csr_t A, float alpha, const float* vals, const float* x, float beta, float* y) {
+    return spmv_impl<float, float>(c, A, alpha, vals, x, beta, y);
+}
+int mpg_csr_spmv_f16f32(mpg_ctx_t c, mpg_csr_t A, float alpha, const uint16_t* vals, const float* x, float beta, float* y) {
+    return spmv_impl<uint16_t, float>(c, A, alpha, vals, x, beta, y);
+}
+
+int mpg_jacobi_setup_f64(mpg_ctx_t c, mpg_csr_t A, const double* vals, double* diag) { return jacobi_impl<double>(c, A, vals, diag); }
+int mpg_jacobi_setup_f32(mpg_ctx_t c, mpg_csr_t A, const float* vals, float* diag) { return jacobi_impl<float>(c, A, vals, diag); }
+
+}  // extern "C"

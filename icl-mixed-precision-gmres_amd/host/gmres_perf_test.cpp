@@ -1,0 +1,189 @@
+// Command-line driver with the reference's flags and stdout lines
+// (gmres_perf_test.cpp:309-455), running on MI355X through mpg_solve.
+//
+// Reference flags: --Apath --bpath --rlen --rtol --repeat-iter --orthloss
+// --tol --max-restarts --rand --mode {mixed,baseline,single-prec,single}
+// --orth {cgs,mgs,cgsr} --prec {ilu,identity,jacobi,ilu_jacobi}
+// --jacobi-steps --gpu (accepted; this build always runs on the GPU).
+// Additions: --matrix band:N[:LO:HI[:SEED]] | laplace:NX[:NY:NZ] (synthetic
+// input instead of --Apath), --mode mixed-half, --engine {fused,surface},
+// --device D.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "mpgmres/problems.h"
+#include "mpgmres/solve.h"
+
+namespace {
+
+double host_nrm2(const double* v, int64_t n) {
+    double s = 0;
+    for (int64_t i = 0; i < n; ++i) s += v[i] * v[i];
+    return std::sqrt(s);
+}
+
+bool parse_synthetic(const std::string& spec, mpg_host_csr* A, std::string& err) {
+    std::vector<std::string> f;
+    size_t p = 0;
+    while (true) {
+        size_t q = spec.find(':', p);
+        f.push_back(spec.substr(p, q == std::string::npos ? std::string::npos : q - p));
+        if (q == std::string::npos) break;
+        p = q + 1;
+    }
+    if (f[0] == "band" && f.size() >= 2) {
+        long long n = std::atoll(f[1].c_str());
+        int lo = f.size() > 2 ? std::atoi(f[2].c_str()) : 5;
+        int hi = f.size() > 3 ? std::atoi(f[3].c_str()) : 4;
+        unsigned long long seed = f.size() > 4 ? std::strtoull(f[4].c_str(), nullptr, 10) : 7;
+        if (mpg_gen_band(n, lo, hi, seed, 0, n, A) != 0) { err = "bad band spec"; return false; }
+        return true;
+    }
+    if (f[0] == "laplace" && f.size() >= 2) {
+        int nx = std::atoi(f[1].c_str());
+        int ny = f.size() > 2 ? std::atoi(f[2].c_str()) : nx;
+        int nz = f.size() > 3 ? std::atoi(f[3].c_str()) : nx;
+        if (mpg_gen_laplace3d(nx, ny, nz, A) != 0) { err = "bad laplace spec"; return false; }
+        return true;
+    }
+    err = "unknown --matrix spec (band:N[:LO:HI[:SEED]] or laplace:NX[:NY:NZ])";
+    return false;
+}
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+    const char* a_path = nullptr;
+    const char* b_path = nullptr;
+    std::string synthetic;
+    mpg_solve_args a{};
+    a.rlen = 0;
+    a.tol = 1e-6;
+    a.max_restarts = 1000000;
+    a.orth = MPG_ORTH_MGS;
+    a.mode = MPG_MODE_MIXED;
+    a.prec = MPG_PREC_ILU;
+    a.jacobi_steps = 1;
+    a.engine = MPG_ENGINE_FUSED;
+    a.verbose = 1;
+    unsigned rand_seed = 42;
+
+    for (int i = 1; i < argc; ++i) {
+        const std::string f = argv[i];
+        auto next = [&]() -> const char* {
+            if (i + 1 >= argc) {
+                std::cout << "Missing value for " << f << std::endl;
+                std::exit(1);
+            }
+            return argv[++i];
+        };
+        if (f == "--Apath") a_path = next();
+        else if (f == "--bpath") b_path = next();
+        else if (f == "--matrix") synthetic = next();
+        else if (f == "--rlen") a.rlen = std::stoi(next());
+        else if (f == "--rtol") a.rtol = std::stod(next());
+        else if (f == "--repeat-iter") a.repeat_iter = 1;
+        else if (f == "--orthloss") a.orthloss = 1;
+        else if (f == "--tol") a.tol = std::stod(next());
+        else if (f == "--max-restarts") a.max_restarts = std::stol(next());
+        else if (f == "--rand") rand_seed = (unsigned)std::stoi(next());
+        else if (f == "--jacobi-steps") a.jacobi_steps = std::stoi(next());
+        else if (f == "--gpu") { /* always on the GPU */ }
+        else if (f == "--device") a.device = std::stoi(next());
+        else if (f == "--mode") {
+            const std::string v = next();
+            if (v == "mixed") a.mode = MPG_MODE_MIXED;
+            else if (v == "baseline") a.mode = MPG_MODE_BASELINE;
+            else if (v == "single-prec") a.mode = MPG_MODE_SINGLE_PREC;
+            else if (v == "single") a.mode = MPG_MODE_SINGLE;
+            else if (v == "mixed-half") a.mode = MPG_MODE_MIXED_HALF;
+            else { std::cout << "Unknown test mode" << std::endl; return 1; }
+        } else if (f == "--orth") {
+            const std::string v = next();
+            if (v == "cgs") a.orth = MPG_ORTH_CGS;
+            else if (v == "mgs") a.orth = MPG_ORTH_MGS;
+            else if (v == "cgsr") a.orth = MPG_ORTH_CGSR;
+            else { std::cout << "Unknown Orthogonalization" << std::endl; return 1; }
+        } else if (f == "--prec") {
+            const std::string v = next();
+            if (v == "ilu") a.prec = MPG_PREC_ILU;
+            else if (v == "identity") a.prec = MPG_PREC_IDENTITY;
+            else if (v == "jacobi") a.prec = MPG_PREC_JACOBI;
+            else if (v == "ilu_jacobi") a.prec = MPG_PREC_ILU_JACOBI;
+            else { std::cout << "Unknown Preconditioner" << std::endl; return 1; }
+        } else if (f == "--engine") {
+            const std::string v = next();
+            if (v == "fused") a.engine = MPG_ENGINE_FUSED;
+            else if (v == "surface") a.engine = MPG_ENGINE_SURFACE;
+            else { std::cout << "Unknown engine" << std::endl; return 1; }
+        } else {
+            std::cout << "Unknown flag" << argv[i] << std::endl;
+            return 1;
+        }
+    }
+    if (a.repeat_iter && a.orthloss) {
+        std::cout << "Repeated Iteration Restart cannot be used with OrthLoss restart" << std::endl;
+        return 1;
+    }
+    if (a.rlen <= 0) {
+        // the reference indexes an empty H when --rlen is missing
+        std::cout << "A positive --rlen is required" << std::endl;
+        return 1;
+    }
+    if (!a_path && synthetic.empty()) {
+        std::cout << "No value suplied for A" << std::endl;
+        return 1;
+    }
+
+    mpg_host_csr A{};
+    char err[256] = {0};
+    if (a_path) {
+        if (mpg_load_mtx(a_path, &A, err, sizeof err) != 0) {
+            std::cerr << "LoadMatrix: " << err << std::endl;
+            return 1;
+        }
+    } else {
+        std::string e;
+        if (!parse_synthetic(synthetic, &A, e)) {
+            std::cerr << e << std::endl;
+            return 1;
+        }
+    }
+    const int64_t n = A.nrows;
+    std::vector<double> x_true((size_t)n), b((size_t)n);
+    if (!b_path) {
+        mpg_rand_vect(n, rand_seed, x_true.data());
+        mpg_host_spmv(&A, x_true.data(), b.data());
+    } else {
+        std::fill(x_true.begin(), x_true.end(), 0.0);
+        if (mpg_load_mtx_vector(b_path, 0, b.data(), n, err, sizeof err) != 0) {
+            std::cerr << "LoadVector: " << err << std::endl;
+            return 1;
+        }
+    }
+
+    std::cout << "||x|| = " << host_nrm2(x_true.data(), n) << std::endl;
+    std::cout << "||b|| = " << host_nrm2(b.data(), n) << std::endl;
+    std::cout << "||A|| = " << host_nrm2(A.val, A.nnz) << std::endl;
+
+    a.n = (int32_t)n;
+    a.nnz = A.nnz;
+    a.rowptr = A.rowptr;
+    a.col = A.col;
+    a.val = A.val;
+    a.b = b.data();
+    a.x_true = x_true.data();
+    mpg_solve_result r{};
+    int st = mpg_solve(&a, &r);
+    mpg_host_csr_free(&A);
+    if (st != 0) {
+        std::cerr << "mpg_solve failed: " << r.message << std::endl;
+        return 1;
+    }
+    return 0;
+}

@@ -1,0 +1,297 @@
+// `Hip` backend of the operator surface: explicit specialisations of every
+// kernels.hpp template for Device = Hip, each a thin call into the C-ABI of
+// libmpgmres_hip.so. Drop-in counterpart of kernels_mkl.cpp:73-352 and
+// kernels_cuda.cpp:111-614 (same operators, same argument meaning).
+//
+// Host-value variants (`Type dot(x, y)`, `Type nrm2(x)`) synchronise the
+// stream, like cuBLAS in host pointer mode; Scalar-result variants stay on
+// the device (device pointer mode, kernels_cuda.cpp:142-150).
+#include "types_hip.hpp"
+
+#include <cstdlib>
+#include <cstring>
+#include <sstream>
+
+#include "kernels.hpp"
+
+namespace mpg {
+
+namespace {
+thread_local mpg_ctx_t tl_ctx = nullptr;
+thread_local bool tl_owned = false;
+
+struct OwnedCtxReaper {
+    ~OwnedCtxReaper() {
+        // Process-exit path: the HIP runtime may already be torn down, so the
+        // lazily created default context is intentionally leaked.
+    }
+};
+}  // namespace
+
+void check(int status, const char* what, mpg_ctx_t ctx) {
+    if (status == MPG_OK) return;
+    std::ostringstream os;
+    os << "mpgmres: " << what << " failed: " << mpg_error_string(status);
+    mpg_ctx_t c = ctx ? ctx : tl_ctx;
+    if (c) {
+        const char* e = mpg_ctx_last_error(c);
+        if (e && *e) os << " (" << e << ")";
+    }
+    throw std::runtime_error(os.str());
+}
+
+mpg_ctx_t current_ctx() {
+    if (!tl_ctx) {
+        const char* env = std::getenv("MPG_DEVICE");
+        int dev = env ? std::atoi(env) : 0;
+        check(mpg_ctx_create(dev, &tl_ctx), "mpg_ctx_create");
+        tl_owned = true;
+    }
+    return tl_ctx;
+}
+
+ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) { tl_ctx = ctx; }
+ScopedContext::~ScopedContext() { tl_ctx = prev_; }
+
+}  // namespace mpg
+
+using mpg::check;
+using mpg::current_ctx;
+
+// ---------------- device tag ----------------
+void* Hip::allocate(size_t bytes) {
+    void* p = nullptr;
+    check(mpg_malloc(current_ctx(), bytes, &p), "mpg_malloc");
+    return p;
+}
+void Hip::deallocate(void* p) {
+    if (p) mpg_free(current_ctx(), p);
+}
+void Hip::to_host(void* dst, const void* src, size_t bytes) {
+    check(mpg_memcpy_d2h(current_ctx(), dst, src, bytes), "mpg_memcpy_d2h");
+}
+void Hip::to_device(void* dst, const void* src, size_t bytes) {
+    check(mpg_memcpy_h2d(current_ctx(), dst, src, bytes), "mpg_memcpy_h2d");
+}
+void Hip::fence() { check(mpg_ctx_sync(current_ctx()), "mpg_ctx_sync"); }
+
+#define C current_ctx()
+
+// ---------------- copy ----------------
+template <> void copy<double, double, Hip>(Vect<double, Hip> x, Vect<double, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_copy_f64f64(C, x.n(), x.data(), y.data()), "copy");
+}
+template <> void copy<float, float, Hip>(Vect<float, Hip> x, Vect<float, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_copy_f32f32(C, x.n(), x.data(), y.data()), "copy");
+}
+template <> void copy<double, float, Hip>(Vect<double, Hip> x, Vect<float, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_copy_f64f32(C, x.n(), x.data(), y.data()), "copy");
+}
+template <> void copy<float, double, Hip>(Vect<float, Hip> x, Vect<double, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_copy_f32f64(C, x.n(), x.data(), y.data()), "copy");
+}
+template <> void copy<double, double, Hip>(Scalar<double, Hip> x, Scalar<double, Hip> y) {
+    check(mpg_copy_f64f64(C, 1, x.data(), y.data()), "copy");
+}
+template <> void copy<float, float, Hip>(Scalar<float, Hip> x, Scalar<float, Hip> y) {
+    check(mpg_copy_f32f32(C, 1, x.data(), y.data()), "copy");
+}
+template <> void copy<double, float, Hip>(Scalar<double, Hip> x, Scalar<float, Hip> y) {
+    check(mpg_copy_f64f32(C, 1, x.data(), y.data()), "copy");
+}
+template <> void copy<float, double, Hip>(Scalar<float, Hip> x, Scalar<double, Hip> y) {
+    check(mpg_copy_f32f64(C, 1, x.data(), y.data()), "copy");
+}
+
+// ---------------- reductions ----------------
+template <> double dot<double, Hip>(Vect<double, Hip> x, Vect<double, Hip> y) {
+    assert(x.n() == y.n());
+    double r;
+    check(mpg_dot_f64_host(C, x.n(), x.data(), y.data(), &r), "dot");
+    return r;
+}
+template <> float dot<float, Hip>(Vect<float, Hip> x, Vect<float, Hip> y) {
+    assert(x.n() == y.n());
+    float r;
+    check(mpg_dot_f32_host(C, x.n(), x.data(), y.data(), &r), "dot");
+    return r;
+}
+template <> void dot<double, Hip>(Vect<double, Hip> x, Vect<double, Hip> y, Scalar<double, Hip> r) {
+    assert(x.n() == y.n());
+    check(mpg_dot_f64(C, x.n(), x.data(), y.data(), r.data()), "dot");
+}
+template <> void dot<float, Hip>(Vect<float, Hip> x, Vect<float, Hip> y, Scalar<float, Hip> r) {
+    assert(x.n() == y.n());
+    check(mpg_dot_f32(C, x.n(), x.data(), y.data(), r.data()), "dot");
+}
+template <> double nrm2<double, Hip>(Vect<double, Hip> x) {
+    double r;
+    check(mpg_nrm2_f64_host(C, x.n(), x.data(), &r), "nrm2");
+    return r;
+}
+template <> float nrm2<float, Hip>(Vect<float, Hip> x) {
+    float r;
+    check(mpg_nrm2_f32_host(C, x.n(), x.data(), &r), "nrm2");
+    return r;
+}
+template <> void nrm2<double, Hip>(Vect<double, Hip> x, Scalar<double, Hip> r) {
+    check(mpg_nrm2_f64(C, x.n(), x.data(), r.data()), "nrm2");
+}
+template <> void nrm2<float, Hip>(Vect<float, Hip> x, Scalar<float, Hip> r) {
+    check(mpg_nrm2_f32(C, x.n(), x.data(), r.data()), "nrm2");
+}
+
+// ---------------- axpy ----------------
+template <> void axpy<double, Hip>(double a, Vect<double, Hip> x, Vect<double, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_axpy_f64(C, x.n(), a, x.data(), y.data()), "axpy");
+}
+template <> void axpy<float, Hip>(float a, Vect<float, Hip> x, Vect<float, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_axpy_f32(C, x.n(), a, x.data(), y.data()), "axpy");
+}
+template <> void axpy<double, Hip>(Scalar<double, Hip> a, Vect<double, Hip> x, Vect<double, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_axpy_dev_f64(C, x.n(), a.data(), x.data(), y.data()), "axpy");
+}
+template <> void axpy<float, Hip>(Scalar<float, Hip> a, Vect<float, Hip> x, Vect<float, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_axpy_dev_f32(C, x.n(), a.data(), x.data(), y.data()), "axpy");
+}
+template <> void naxpy<double, Hip>(Scalar<double, Hip> a, Vect<double, Hip> x, Vect<double, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_naxpy_dev_f64(C, x.n(), a.data(), x.data(), y.data()), "naxpy");
+}
+template <> void naxpy<float, Hip>(Scalar<float, Hip> a, Vect<float, Hip> x, Vect<float, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_naxpy_dev_f32(C, x.n(), a.data(), x.data(), y.data()), "naxpy");
+}
+
+// ---------------- scal ----------------
+template <> void scal<double, Hip>(double a, Vect<double, Hip> x) {
+    check(mpg_scal_f64(C, x.n(), a, x.data()), "scal");
+}
+template <> void scal<float, Hip>(float a, Vect<float, Hip> x) {
+    check(mpg_scal_f32(C, x.n(), a, x.data()), "scal");
+}
+template <> void scal<double, Hip>(double a, Vect<double, Hip> x, Vect<double, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_scal_copy_f64(C, x.n(), a, x.data(), y.data()), "scal");
+}
+template <> void scal<float, Hip>(float a, Vect<float, Hip> x, Vect<float, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_scal_copy_f32(C, x.n(), a, x.data(), y.data()), "scal");
+}
+template <> void scal<double, Hip>(Scalar<double, Hip> a, Vect<double, Hip> x, Vect<double, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_scal_copy_dev_f64(C, x.n(), a.data(), x.data(), y.data()), "scal");
+}
+template <> void scal<float, Hip>(Scalar<float, Hip> a, Vect<float, Hip> x, Vect<float, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_scal_copy_dev_f32(C, x.n(), a.data(), x.data(), y.data()), "scal");
+}
+template <> void scal<double, Hip>(double a, Scalar<double, Hip> x, Scalar<double, Hip> y) {
+    check(mpg_scal_scalar_f64(C, a, x.data(), y.data()), "scal");
+}
+template <> void scal<float, Hip>(float a, Scalar<float, Hip> x, Scalar<float, Hip> y) {
+    check(mpg_scal_scalar_f32(C, a, x.data(), y.data()), "scal");
+}
+template <> void scal<double, Hip>(Scalar<double, Hip> a, Scalar<double, Hip> x, Scalar<double, Hip> y) {
+    check(mpg_scal_scalar_dev_f64(C, a.data(), x.data(), y.data()), "scal");
+}
+template <> void scal<float, Hip>(Scalar<float, Hip> a, Scalar<float, Hip> x, Scalar<float, Hip> y) {
+    check(mpg_scal_scalar_dev_f32(C, a.data(), x.data(), y.data()), "scal");
+}
+
+// ---------------- fill ----------------
+template <> void fill_strided<double, Hip>(double* x, size_t r, size_t c, size_t ld, double v) {
+    check(mpg_fill_f64(C, x, r, c, ld, v), "fill");
+}
+template <> void fill_strided<float, Hip>(float* x, size_t r, size_t c, size_t ld, float v) {
+    check(mpg_fill_f32(C, x, r, c, ld, v), "fill");
+}
+
+// ---------------- Givens ----------------
+template <> void rotg<double, Hip>(Scalar<double, Hip> a, Scalar<double, Hip> b, Scalar<double, Hip> c,
+                                   Scalar<double, Hip> s) {
+    check(mpg_rotg_f64(C, a.data(), b.data(), c.data(), s.data()), "rotg");
+}
+template <> void rotg<float, Hip>(Scalar<float, Hip> a, Scalar<float, Hip> b, Scalar<float, Hip> c,
+                                  Scalar<float, Hip> s) {
+    check(mpg_rotg_f32(C, a.data(), b.data(), c.data(), s.data()), "rotg");
+}
+template <> void rot<double, Hip>(Scalar<double, Hip> a, Scalar<double, Hip> b, Scalar<double, Hip> c,
+                                  Scalar<double, Hip> s) {
+    check(mpg_rot_f64(C, a.data(), b.data(), c.data(), s.data()), "rot");
+}
+template <> void rot<float, Hip>(Scalar<float, Hip> a, Scalar<float, Hip> b, Scalar<float, Hip> c,
+                                 Scalar<float, Hip> s) {
+    check(mpg_rot_f32(C, a.data(), b.data(), c.data(), s.data()), "rot");
+}
+template <> void rot<double, Hip>(Vect<double, Hip> a, Vect<double, Hip> c, Vect<double, Hip> s) {
+    check(mpg_rot_vec_f64(C, (int)c.n(), a.data(), c.data(), s.data()), "rot");
+}
+template <> void rot<float, Hip>(Vect<float, Hip> a, Vect<float, Hip> c, Vect<float, Hip> s) {
+    check(mpg_rot_vec_f32(C, (int)c.n(), a.data(), c.data(), s.data()), "rot");
+}
+
+// ---------------- BLAS-2 ----------------
+template <> void gemv<double, Hip>(double alpha, MultiVect<double, Hip> A, Vect<double, Hip> x, double beta,
+                                   Vect<double, Hip> y) {
+    assert(A.ncols() == x.n() && A.nrows() == y.n());
+    check(mpg_gemv_f64(C, A.transposed() ? 1 : 0, A.nrows_base(), A.ncols_base(), alpha, A.data(), A.stride(),
+                       x.data(), beta, y.data()),
+          "gemv");
+}
+template <> void gemv<float, Hip>(float alpha, MultiVect<float, Hip> A, Vect<float, Hip> x, float beta,
+                                  Vect<float, Hip> y) {
+    assert(A.ncols() == x.n() && A.nrows() == y.n());
+    check(mpg_gemv_f32(C, A.transposed() ? 1 : 0, A.nrows_base(), A.ncols_base(), alpha, A.data(), A.stride(),
+                       x.data(), beta, y.data()),
+          "gemv");
+}
+template <> void trsv<double, Hip>(const char* upper, MultiVect<double, Hip> A, Vect<double, Hip> x) {
+    assert(A.nrows() == A.ncols() && A.ncols() == x.n());
+    check(mpg_trsv_f64(C, *upper == 'U', A.transposed() ? 1 : 0, A.ncols(), A.data(), A.stride(), x.data()),
+          "trsv");
+}
+template <> void trsv<float, Hip>(const char* upper, MultiVect<float, Hip> A, Vect<float, Hip> x) {
+    assert(A.nrows() == A.ncols() && A.ncols() == x.n());
+    check(mpg_trsv_f32(C, *upper == 'U', A.transposed() ? 1 : 0, A.ncols(), A.data(), A.stride(), x.data()),
+          "trsv");
+}
+
+template <> void gdmv<double, Hip>(double alpha, Vect<double, Hip> d, Vect<double, Hip> x, double beta,
+                                   Vect<double, Hip> y) {
+    assert(d.n() == x.n() && d.n() == y.n());
+    check(mpg_gdmv_f64(C, d.n(), alpha, d.data(), x.data(), beta, y.data()), "gdmv");
+}
+template <> void gdmv<float, Hip>(float alpha, Vect<float, Hip> d, Vect<float, Hip> x, float beta,
+                                  Vect<float, Hip> y) {
+    assert(d.n() == x.n() && d.n() == y.n());
+    check(mpg_gdmv_f32(C, d.n(), alpha, d.data(), x.data(), beta, y.data()), "gdmv");
+}
+
+// ---------------- sparse ----------------
+template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Vect<double, Hip> x, double beta,
+                                   Vect<double, Hip> y) {
+    assert((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n());
+    check(mpg_csr_spmv_f64(C, A.csr(), alpha, A.vals_data(), x.data(), beta, y.data()), "spmv");
+}
+template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<float, Hip> x, float beta,
+                                  Vect<float, Hip> y) {
+    assert((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n());
+    check(mpg_csr_spmv_f32(C, A.csr(), alpha, A.vals_data(), x.data(), beta, y.data()), "spmv");
+}
+template <> void jacobi_diag<double, Hip>(SparseMatrix<double, Hip> A, Vect<double, Hip> d) {
+    check(mpg_jacobi_setup_f64(C, A.csr(), A.vals_data(), d.data()), "jacobi setup");
+}
+template <> void jacobi_diag<float, Hip>(SparseMatrix<float, Hip> A, Vect<float, Hip> d) {
+    check(mpg_jacobi_setup_f32(C, A.csr(), A.vals_data(), d.data()), "jacobi setup");
+}
+
+#undef C

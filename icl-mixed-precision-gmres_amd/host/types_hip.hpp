@@ -1,0 +1,113 @@
+// The `Hip` backend: device tag + CSR matrix type for MI355X (gfx950).
+//
+// Drop-in counterpart of types_mkl.hpp:11-107 / types_cuda.hpp:39-152. All
+// device work goes through the C-ABI of libmpgmres_hip.so
+// (include/mpgmres/capi.h); nothing here includes HIP kernels or Kokkos.
+#ifndef MPGMRES_TYPES_HIP_HPP
+#define MPGMRES_TYPES_HIP_HPP
+
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mpgmres/capi.h"
+#include "kernels.hpp"
+#include "types.hpp"
+
+namespace mpg {
+
+// Throws on a non-zero C-ABI status (the reference ignores cuBLAS statuses
+// and asserts MKL ones; we never drop an error).
+void check(int status, const char* what, mpg_ctx_t ctx = nullptr);
+
+// The calling thread's current HIP context (stream + workspace). Created
+// lazily on the device named by MPG_DEVICE (default 0) unless a
+// ScopedContext installed one.
+mpg_ctx_t current_ctx();
+
+class ScopedContext {
+    mpg_ctx_t prev_;
+public:
+    explicit ScopedContext(mpg_ctx_t ctx);
+    ~ScopedContext();
+    ScopedContext(const ScopedContext&) = delete;
+    ScopedContext& operator=(const ScopedContext&) = delete;
+};
+
+// Device CSR structure shared by every precision of one matrix.
+struct CsrStructure {
+    int m = 0, n = 0;
+    int64_t nnz = 0;
+    std::shared_ptr<void> row_map, inds;  // device int32
+    std::shared_ptr<mpg_csr> csr;        // analysed CSR-adaptive schedule
+};
+
+}  // namespace mpg
+
+// Device tag (types_mkl.hpp:11-15, types_cuda.hpp:39-44).
+struct Hip {
+    static constexpr bool host_accessible = false;
+    static void* allocate(size_t bytes);
+    static void deallocate(void* p);
+    static void to_host(void* dst, const void* src, size_t bytes);
+    static void to_device(void* dst, const void* src, size_t bytes);
+    static void fence();
+    using execution_space = Hip;
+    using memory_space = Hip;
+};
+
+// CSR on the device: shared int32 structure (row_map, inds, analysed row
+// blocks) plus values of precision Type.
+template <class Type>
+class SparseMatrix<Type, Hip> {
+    std::shared_ptr<mpg::CsrStructure> s_;
+    Vect<Type, Hip> vals_;
+
+    template <class, class> friend class SparseMatrix;
+
+public:
+    SparseMatrix() = default;
+
+    // From host CSR arrays (0-based, int32), the values given in Type.
+    SparseMatrix(int m, int n, const int* row_map, const int* inds, const Type* vals) {
+        s_ = std::make_shared<mpg::CsrStructure>();
+        s_->m = m;
+        s_->n = n;
+        s_->nnz = row_map[m];
+        const size_t ib = sizeof(int) * (size_t)(m + 1), jb = sizeof(int) * (size_t)s_->nnz;
+        s_->row_map = mpg::device_alloc<Hip>(ib);
+        s_->inds = mpg::device_alloc<Hip>(jb);
+        Hip::to_device(s_->row_map.get(), row_map, ib);
+        if (jb) Hip::to_device(s_->inds.get(), inds, jb);
+        mpg_csr_t csr = nullptr;
+        mpg::check(mpg_csr_create(mpg::current_ctx(), m, n, s_->nnz, row_map,
+                                  static_cast<const int32_t*>(s_->row_map.get()),
+                                  static_cast<const int32_t*>(s_->inds.get()), &csr),
+                   "mpg_csr_create");
+        s_->csr = std::shared_ptr<mpg_csr>(csr, [](mpg_csr* p) { mpg_csr_destroy(p); });
+        vals_ = Vect<Type, Hip>((size_t)s_->nnz);
+        if (s_->nnz) Hip::to_device(vals_.data(), vals, sizeof(Type) * (size_t)s_->nnz);
+    }
+
+    // Precision-converting copy: shares the structure, casts the values on
+    // the device (types_mkl.hpp:46-62, types_cuda.hpp:82-101). Implicit, as
+    // in the reference — DoBaselineProblem relies on it (§0.1-2 of SURVEY).
+    template <class OldType>
+    SparseMatrix(SparseMatrix<OldType, Hip> old) : s_(old.s_), vals_((size_t)old.s_->nnz) {
+        copy(old.vals_, vals_);
+    }
+
+    const std::shared_ptr<mpg::CsrStructure>& structure() const { return s_; }
+    int nrows() const { return s_->m; }
+    int ncols() const { return s_->n; }
+    int64_t nnz() const { return s_->nnz; }
+    const int* row_map_data() const { return static_cast<const int*>(s_->row_map.get()); }
+    const int* inds_data() const { return static_cast<const int*>(s_->inds.get()); }
+    Type* vals_data() const { return vals_.data(); }
+    mpg_csr_t csr() const { return s_->csr.get(); }
+    Vect<Type, Hip> vals_vect() const { return vals_; }
+    bool is_transposed() const { return false; }
+};
+
+#endif  // MPGMRES_TYPES_HIP_HPP

@@ -1,0 +1,176 @@
+/*
+ * mpgmres C-ABI — the drop-in boundary between host code and the hand-written
+ * gfx950 HIP kernels of the mixed-precision GMRES hot path.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, and
+ * returns an int status (0 = OK, < 0 = error; see mpg_status_t and
+ * mpg_error_string). No torch types, no C++ types. Pointers named *_dev are
+ * device (HBM) pointers; *_host are host pointers. All calls are ordered on
+ * the context's HIP stream and are asynchronous unless the name ends in
+ * `_host` (those synchronise the stream and return a value through host
+ * memory — the equivalent of the reference's host-pointer-mode BLAS calls).
+ *
+ * Each family cites the reference interface it replaces (paths are relative
+ * to the reference repository iamsonderr/icl-mixed-precision-gmres):
+ *   kernels.hpp:9-169        operator surface (templates on <Type, Device>)
+ *   kernels_mkl.cpp:73-352   MKL (host) specialisations — the semantics kept
+ *   kernels_cuda.cpp:111-614 cuBLAS/cuSPARSE specialisations — replaced
+ *   types.hpp:15-228         Scalar / Vect / MultiVect handles
+ *   types_cuda.hpp:47-152    SparseMatrix<T, Cuda> (CSR, int32 indices)
+ *   types.hpp:381-448        Jacobi preconditioner setup
+ * The host-side C++ that binds these (types_hip.hpp / kernels_hip.cpp) lives
+ * in icl-mixed-precision-gmres_amd/host/.
+ */
+#ifndef MPGMRES_CAPI_H
+#define MPGMRES_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    MPG_OK = 0,
+    MPG_ERR_HIP = -1,          /* a HIP runtime call failed */
+    MPG_ERR_ARG = -2,          /* invalid argument (size mismatch, null, range) */
+    MPG_ERR_ALLOC = -3,        /* device allocation failed */
+    MPG_ERR_RCCL = -4,         /* an RCCL call failed */
+    MPG_ERR_UNSUPPORTED = -5,  /* operation not supported for these arguments */
+    MPG_ERR_BREAKDOWN = -6     /* Arnoldi breakdown / non-finite value detected */
+} mpg_status_t;
+
+typedef struct mpg_ctx* mpg_ctx_t;   /* one per (GPU, host thread) */
+typedef struct mpg_csr* mpg_csr_t;   /* analysed CSR structure (row blocks) */
+
+const char* mpg_error_string(int status);
+/* Last HIP error text recorded in this context (for diagnostics). */
+const char* mpg_ctx_last_error(mpg_ctx_t ctx);
+
+/* ---- context / memory (replaces Kokkos::View allocation + deep_copy,
+ *      types.hpp:15-228, and CudaLibSingleton, types_cuda.hpp:9-36) ---- */
+int mpg_ctx_create(int device, mpg_ctx_t* out);
+int mpg_ctx_destroy(mpg_ctx_t ctx);
+/* Device::execution_space().fence() (gmres.cpp:113, 225) */
+int mpg_ctx_sync(mpg_ctx_t ctx);
+/* hipStream_t of the context, as an opaque pointer. */
+void* mpg_ctx_stream(mpg_ctx_t ctx);
+int mpg_ctx_device(mpg_ctx_t ctx);
+/* Zero-initialised device allocation (Kokkos views are zero-filled). */
+int mpg_malloc(mpg_ctx_t ctx, size_t bytes, void** out_dev);
+int mpg_free(mpg_ctx_t ctx, void* ptr_dev);
+int mpg_memset(mpg_ctx_t ctx, void* ptr_dev, int value, size_t bytes);
+int mpg_memcpy_h2d(mpg_ctx_t ctx, void* dst_dev, const void* src_host, size_t bytes);
+int mpg_memcpy_d2h(mpg_ctx_t ctx, void* dst_host, const void* src_dev, size_t bytes);
+int mpg_memcpy_d2d(mpg_ctx_t ctx, void* dst_dev, const void* src_dev, size_t bytes);
+
+/* ---- BLAS-1 (kernels.hpp:11-101; kernels_mkl.cpp:73-211) ----
+ * Reductions accumulate in fp64 for both precisions and are deterministic
+ * (fixed two-stage tree); *_dev variants leave the result in device memory
+ * (cuBLAS device pointer mode, kernels_cuda.cpp:142-150). */
+int mpg_dot_f64(mpg_ctx_t ctx, int64_t n, const double* x, const double* y, double* result_dev);
+int mpg_dot_f32(mpg_ctx_t ctx, int64_t n, const float* x, const float* y, float* result_dev);
+int mpg_dot_f64_host(mpg_ctx_t ctx, int64_t n, const double* x, const double* y, double* result_host);
+int mpg_dot_f32_host(mpg_ctx_t ctx, int64_t n, const float* x, const float* y, float* result_host);
+int mpg_nrm2_f64(mpg_ctx_t ctx, int64_t n, const double* x, double* result_dev);
+int mpg_nrm2_f32(mpg_ctx_t ctx, int64_t n, const float* x, float* result_dev);
+int mpg_nrm2_f64_host(mpg_ctx_t ctx, int64_t n, const double* x, double* result_host);
+int mpg_nrm2_f32_host(mpg_ctx_t ctx, int64_t n, const float* x, float* result_host);
+/* y += alpha*x, alpha on host (kernels_mkl.cpp:118-128) */
+int mpg_axpy_f64(mpg_ctx_t ctx, int64_t n, double alpha, const double* x, double* y);
+int mpg_axpy_f32(mpg_ctx_t ctx, int64_t n, float alpha, const float* x, float* y);
+/* y += alpha*x with alpha read from device memory (kernels_mkl.cpp:130-140) */
+int mpg_axpy_dev_f64(mpg_ctx_t ctx, int64_t n, const double* alpha_dev, const double* x, double* y);
+int mpg_axpy_dev_f32(mpg_ctx_t ctx, int64_t n, const float* alpha_dev, const float* x, float* y);
+/* y -= alpha*x, alpha on device (naxpy, kernels_mkl.cpp:143-153) */
+int mpg_naxpy_dev_f64(mpg_ctx_t ctx, int64_t n, const double* alpha_dev, const double* x, double* y);
+int mpg_naxpy_dev_f32(mpg_ctx_t ctx, int64_t n, const float* alpha_dev, const float* x, float* y);
+/* x *= alpha in place (kernels_mkl.cpp:155-163) */
+int mpg_scal_f64(mpg_ctx_t ctx, int64_t n, double alpha, double* x);
+int mpg_scal_f32(mpg_ctx_t ctx, int64_t n, float alpha, float* x);
+/* y = alpha*x (copy then scal, kernels_mkl.cpp:165-191); alpha host or device */
+int mpg_scal_copy_f64(mpg_ctx_t ctx, int64_t n, double alpha, const double* x, double* y);
+int mpg_scal_copy_f32(mpg_ctx_t ctx, int64_t n, float alpha, const float* x, float* y);
+int mpg_scal_copy_dev_f64(mpg_ctx_t ctx, int64_t n, const double* alpha_dev, const double* x, double* y);
+int mpg_scal_copy_dev_f32(mpg_ctx_t ctx, int64_t n, const float* alpha_dev, const float* x, float* y);
+/* y = (1/alpha)*x with the reciprocal formed on device in the vector's
+ * precision — the sync-free form of `scal(1/h_final, w, v)`
+ * (Orthogonalization.hpp:56-59). */
+int mpg_scal_recip_copy_dev_f64(mpg_ctx_t ctx, int64_t n, const double* alpha_dev, const double* x, double* y);
+int mpg_scal_recip_copy_dev_f32(mpg_ctx_t ctx, int64_t n, const float* alpha_dev, const float* x, float* y);
+/* copy with cast (kernels.hpp:11-30). Suffix = <src><dst>. */
+int mpg_copy_f64f64(mpg_ctx_t ctx, int64_t n, const double* x, double* y);
+int mpg_copy_f32f32(mpg_ctx_t ctx, int64_t n, const float* x, float* y);
+int mpg_copy_f64f32(mpg_ctx_t ctx, int64_t n, const double* x, float* y);
+int mpg_copy_f32f64(mpg_ctx_t ctx, int64_t n, const float* x, double* y);
+int mpg_copy_f64f16(mpg_ctx_t ctx, int64_t n, const double* x, uint16_t* y_half);
+int mpg_copy_f32f16(mpg_ctx_t ctx, int64_t n, const float* x, uint16_t* y_half);
+/* fill (kernels.hpp:88-101): strided 2-D form covers Scalar/Vect/MultiVect */
+int mpg_fill_f64(mpg_ctx_t ctx, double* x, int64_t rows, int64_t cols, int64_t ld, double value);
+int mpg_fill_f32(mpg_ctx_t ctx, float* x, int64_t rows, int64_t cols, int64_t ld, float value);
+/* y = beta*y + alpha*d∘x (gdmv, kernels.hpp:131-151; Jacobi::apply) */
+int mpg_gdmv_f64(mpg_ctx_t ctx, int64_t n, double alpha, const double* d, const double* x, double beta, double* y);
+int mpg_gdmv_f32(mpg_ctx_t ctx, int64_t n, float alpha, const float* d, const float* x, float beta, float* y);
+
+/* ---- Givens (kernels_mkl.cpp:214-260; device-resident form of
+ *      kernels_cuda.cpp:394-494) — all operands in device memory ---- */
+/* BLAS rotg on (a,b) -> (r, c, s); b is then set to 0 (kernels_mkl.cpp:218) */
+int mpg_rotg_f64(mpg_ctx_t ctx, double* a, double* b, double* c, double* s);
+int mpg_rotg_f32(mpg_ctx_t ctx, float* a, float* b, float* c, float* s);
+/* (a,b) <- (c a + s b, -s a + c b) on one pair (kernels_mkl.cpp:228-238) */
+int mpg_rot_f64(mpg_ctx_t ctx, double* a, double* b, const double* c, const double* s);
+int mpg_rot_f32(mpg_ctx_t ctx, float* a, float* b, const float* c, const float* s);
+/* apply rotations j=0..k-1 to the column a[0..k] (kernels_mkl.cpp:240-260) */
+int mpg_rot_vec_f64(mpg_ctx_t ctx, int k, double* a, const double* c, const double* s);
+int mpg_rot_vec_f32(mpg_ctx_t ctx, int k, float* a, const float* c, const float* s);
+/* y[0] = alpha*x[0] (scalar scal, kernels_mkl.cpp:193-211) */
+int mpg_scal_scalar_f64(mpg_ctx_t ctx, double alpha, const double* x, double* y);
+int mpg_scal_scalar_f32(mpg_ctx_t ctx, float alpha, const float* x, float* y);
+int mpg_scal_scalar_dev_f64(mpg_ctx_t ctx, const double* alpha_dev, const double* x, double* y);
+int mpg_scal_scalar_dev_f32(mpg_ctx_t ctx, const float* alpha_dev, const float* x, float* y);
+
+/* ---- BLAS-2 (kernels_mkl.cpp:264-321) — column-major, explicit lda ----
+ * trans = 0: y = alpha*A x + beta*y   (A is rows x cols, x: cols, y: rows)
+ * trans = 1: y = alpha*A^T x + beta*y (x: rows, y: cols)
+ * The tall-skinny cases of the Arnoldi step (rows = n, cols <= m+1) are the
+ * panel kernels of DESIGN.md §4. beta == 0 never reads y. */
+int mpg_gemv_f64(mpg_ctx_t ctx, int trans, int64_t rows, int64_t cols, double alpha,
+                 const double* A, int64_t lda, const double* x, double beta, double* y);
+int mpg_gemv_f32(mpg_ctx_t ctx, int trans, int64_t rows, int64_t cols, float alpha,
+                 const float* A, int64_t lda, const float* x, float beta, float* y);
+/* triangular solve, non-unit diagonal, single workgroup (n <= 4096).
+ * upper = 1 'U', 0 'L'; trans = 1 solves with A^T (kernels_mkl.cpp:291-321) */
+int mpg_trsv_f64(mpg_ctx_t ctx, int upper, int trans, int64_t n, const double* A, int64_t lda, double* x);
+int mpg_trsv_f32(mpg_ctx_t ctx, int upper, int trans, int64_t n, const float* A, int64_t lda, float* x);
+
+/* ---- CSR SpMV (kernels_mkl.cpp:326-352; kernels_cuda.cpp:576-614) ----
+ * rowptr/col are int32, 0-based, device pointers that must outlive the
+ * handle. mpg_csr_create analyses the row lengths (CSR-adaptive row blocks:
+ * short rows are streamed through LDS in nnz-chunks, long rows get a
+ * workgroup each) from a HOST copy of rowptr. */
+int mpg_csr_create(mpg_ctx_t ctx, int32_t rows, int32_t cols, int64_t nnz,
+                   const int32_t* rowptr_host, const int32_t* rowptr_dev,
+                   const int32_t* col_dev, mpg_csr_t* out);
+int mpg_csr_destroy(mpg_csr_t csr);
+int mpg_csr_num_blocks(mpg_csr_t csr);
+/* y = alpha*A x + beta*y; vals/x/y in the named precision.
+ * f16f32: half-precision values, fp32 x and y (low-precision cast path). */
+int mpg_csr_spmv_f64(mpg_ctx_t ctx, mpg_csr_t A, double alpha, const double* vals,
+                     const double* x, double beta, double* y);
+int mpg_csr_spmv_f32(mpg_ctx_t ctx, mpg_csr_t A, float alpha, const float* vals,
+                     const float* x, float beta, float* y);
+int mpg_csr_spmv_f16f32(mpg_ctx_t ctx, mpg_csr_t A, float alpha, const uint16_t* vals_half,
+                        const float* x, float beta, float* y);
+
+/* ---- Jacobi preconditioner setup (types.hpp:393-431) ----
+ * alpha = max_i sum_j |a_ij| (summed in the values' precision) *
+ * FLT_EPSILON; d_i = 1 / boost(a_ii) where the diagonal entry is the first
+ * entry of row i whose column >= i (types.hpp:422-425). */
+int mpg_jacobi_setup_f64(mpg_ctx_t ctx, mpg_csr_t A, const double* vals, double* diag_out);
+int mpg_jacobi_setup_f32(mpg_ctx_t ctx, mpg_csr_t A, const float* vals, float* diag_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPGMRES_CAPI_H */

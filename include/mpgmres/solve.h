@@ -1,0 +1,95 @@
+/*
+ * mpgmres solve C-ABI: one call = one restarted GMRES(m) solve of A x = b,
+ * set up and reported the way the reference's perf-test driver does
+ * (gmres_perf_test.cpp:53-182 DoBaselineProblem / DoMixedPrecisionProblem):
+ * x0 = 0, timer around the GMRES call only, then resNorm = ||b - A x|| with
+ * the original fp64 A and errNorm = ||x - x_true||.
+ *
+ * The same argument/result structs are used by the HIP path
+ * (libmpgmres_host.so: mpg_solve) and by the CPU oracle under oracle/
+ * (liboracle.so: oracle_solve), so parity tests can run both on one input.
+ */
+#ifndef MPGMRES_SOLVE_H
+#define MPGMRES_SOLVE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* gmres_perf_test.cpp:31-36 test_mode_t, plus a new fp16-value mode */
+typedef enum {
+    MPG_MODE_MIXED = 0,       /* fp64 residual/update, fp32 Arnoldi (gmres_singleUpdate) */
+    MPG_MODE_BASELINE = 1,    /* fp64 GMRES on double(float(A)) (gmres_baseline<d,d>) */
+    MPG_MODE_SINGLE_PREC = 2, /* fp64 GMRES, fp32 preconditioner (gmres_baseline<d,f>) */
+    MPG_MODE_SINGLE = 3,      /* fp32 GMRES (gmres_baseline<f,f>) */
+    MPG_MODE_MIXED_HALF = 4   /* like MIXED, but the inner SpMV reads fp16 values (new) */
+} mpg_mode_t;
+
+/* gmres_perf_test.cpp:17-22 orth_t */
+typedef enum { MPG_ORTH_CGS = 0, MPG_ORTH_MGS = 1, MPG_ORTH_CGSR = 2 } mpg_orth_t;
+
+/* gmres_perf_test.cpp:24-29 prec_t (same numbering) */
+typedef enum { MPG_PREC_ILU = 0, MPG_PREC_ILU_JACOBI = 1, MPG_PREC_JACOBI = 2, MPG_PREC_IDENTITY = 3 } mpg_prec_t;
+
+typedef enum {
+    MPG_ENGINE_SURFACE = 0,  /* generic driver over the kernels.hpp operator surface */
+    MPG_ENGINE_FUSED = 1     /* fused Arnoldi kernels, device-side Givens, graph-captured cycles */
+} mpg_engine_t;
+
+typedef enum { MPG_RESULT_CONVERGED = 1, MPG_RESULT_ABORTED = 3, MPG_RESULT_ERROR = -1 } mpg_result_status_t;
+
+typedef struct {
+    /* CSR matrix, 0-based int32 indices, fp64 values (host memory) */
+    int32_t n;
+    int64_t nnz;
+    const int32_t* rowptr;
+    const int32_t* col;
+    const double* val;
+    const double* b;       /* right-hand side (host, n) */
+    const double* x_true;  /* for errNorm (host, n); may be NULL */
+    int32_t mode, orth, prec, engine;
+    int32_t rlen;          /* restart length m (--rlen) */
+    double tol;            /* --tol */
+    int64_t max_restarts;  /* --max-restarts */
+    double rtol;           /* --rtol (0: base Convergence) */
+    int32_t repeat_iter;   /* --repeat-iter */
+    int32_t orthloss;      /* --orthloss */
+    int32_t jacobi_steps;  /* --jacobi-steps */
+    int32_t verbose;       /* print the reference's stdout lines */
+    int32_t device;        /* HIP device (mpg_solve only) */
+    int32_t threads;       /* host threads (oracle only; 0 = default) */
+} mpg_solve_args;
+
+typedef struct {
+    int32_t status;           /* mpg_result_status_t */
+    int64_t restarts;         /* value of i when the solver returned */
+    int64_t inner_k;          /* k when converged inside a cycle, else 0 */
+    int64_t total_iters;
+    double res_norm, err_norm;
+    double gmres_seconds, setup_seconds;
+    double minvb_norm;
+    /* caller-provided outputs (may be NULL / zero capacity) */
+    double* x_out;            /* n */
+    int64_t cycle_cap;        /* capacity of the per-cycle arrays */
+    int64_t n_cycles;         /* number of check_initial calls recorded */
+    double* cyc_r_norm;       /* true residual norm at each restart */
+    double* cyc_normalization;/* ||b|| + ||A||_F ||x|| */
+    double* cyc_beta;         /* preconditioned residual norm */
+    int64_t step_cap;
+    int64_t n_steps;          /* number of check calls recorded */
+    double* step_res;         /* |s(k+1)| per Arnoldi step */
+    int32_t* step_cycle;      /* cycle index of each step */
+    char message[256];        /* error text when status == MPG_RESULT_ERROR */
+} mpg_solve_result;
+
+/* HIP path (libmpgmres_host.so). Returns 0 on success (result->status tells
+ * converged/aborted), < 0 on error (result->message). */
+int mpg_solve(const mpg_solve_args* args, mpg_solve_result* result);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPGMRES_SOLVE_H */

@@ -1,0 +1,123 @@
+"""ORACLE — test infrastructure only. ctypes binding of oracle/_build/liboracle.so."""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB = ORACLE_DIR / "_build" / "liboracle.so"
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        _lib = C.CDLL(str(LIB))
+        _lib.oracle_backend.restype = C.c_char_p
+        _lib.oracle_max_threads.restype = C.c_int
+        _lib.oracle_solve.restype = C.c_int
+        d, f, i, p = C.c_double, C.c_float, C.c_int, C.c_void_p
+        _lib.oracle_spmv_f64.argtypes = [i, p, p, p, d, p, d, p]
+        _lib.oracle_spmv_f32.argtypes = [i, p, p, p, f, p, f, p]
+        _lib.oracle_dot_f64.argtypes = [i, p, p]
+        _lib.oracle_dot_f64.restype = d
+        _lib.oracle_dot_f32.argtypes = [i, p, p]
+        _lib.oracle_dot_f32.restype = f
+        _lib.oracle_nrm2_f64.argtypes = [i, p]
+        _lib.oracle_nrm2_f64.restype = d
+        _lib.oracle_nrm2_f32.argtypes = [i, p]
+        _lib.oracle_nrm2_f32.restype = f
+        _lib.oracle_gemv_f64.argtypes = [i, i, i, d, p, i, p, d, p]
+        _lib.oracle_gemv_f32.argtypes = [i, i, i, f, p, i, p, f, p]
+        _lib.oracle_trsv_upper_f64.argtypes = [i, p, i, p]
+        _lib.oracle_trsv_upper_f32.argtypes = [i, p, i, p]
+        _lib.oracle_rotg_f64.argtypes = [p, p, p, p]
+        _lib.oracle_rotg_f32.argtypes = [p, p, p, p]
+        _lib.oracle_jacobi_f64.argtypes = [i, p, p, p, p]
+        _lib.oracle_jacobi_f32.argtypes = [i, p, p, p, p]
+    return _lib
+
+
+def backend() -> str:
+    return lib().oracle_backend().decode()
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def solve(mpg, A, b, x_true=None, **opts):
+    """Run the oracle on the same mpg_solve_args the HIP path takes."""
+    opts = dict(opts)
+    opts.pop("engine", None)
+    args, keep = mpg.make_args(A, b, x_true, **opts)
+    fn = lib().oracle_solve
+    fn.argtypes = [C.POINTER(type(args)), C.POINTER(mpg.SolveResult)]
+    return mpg.run_solve(fn, args, A.nrows)
+
+
+def spmv(A, x: np.ndarray, alpha=1.0, beta=0.0, y=None, dtype=np.float64) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=dtype)
+    y = np.zeros(A.nrows, dtype=dtype) if y is None else np.array(y, dtype=dtype)
+    v = np.ascontiguousarray(A.val, dtype=dtype)
+    fn = lib().oracle_spmv_f64 if dtype == np.float64 else lib().oracle_spmv_f32
+    fn(A.nrows, _ptr(A.rowptr), _ptr(A.col), _ptr(v), alpha, _ptr(x), beta, _ptr(y))
+    return y
+
+
+def dot(x: np.ndarray, y: np.ndarray):
+    if x.dtype == np.float64:
+        return lib().oracle_dot_f64(len(x), _ptr(x), _ptr(y))
+    return lib().oracle_dot_f32(len(x), _ptr(x), _ptr(y))
+
+
+def nrm2(x: np.ndarray):
+    if x.dtype == np.float64:
+        return lib().oracle_nrm2_f64(len(x), _ptr(x))
+    return lib().oracle_nrm2_f32(len(x), _ptr(x))
+
+
+def gemv(trans: bool, A: np.ndarray, x: np.ndarray, alpha=1.0, beta=0.0, y=None) -> np.ndarray:
+    """A given as a Fortran-ordered 2-D array (column-major, lda = rows)."""
+    A = np.asfortranarray(A)
+    rows, cols = A.shape
+    out_len = cols if trans else rows
+    y = np.zeros(out_len, dtype=A.dtype) if y is None else np.array(y, dtype=A.dtype)
+    x = np.ascontiguousarray(x, dtype=A.dtype)
+    fn = lib().oracle_gemv_f64 if A.dtype == np.float64 else lib().oracle_gemv_f32
+    fn(int(trans), rows, cols, alpha, _ptr(A), rows, _ptr(x), beta, _ptr(y))
+    return y
+
+
+def trsv_upper(H: np.ndarray, y: np.ndarray) -> np.ndarray:
+    H = np.asfortranarray(H)
+    y = np.array(y, dtype=H.dtype)
+    fn = lib().oracle_trsv_upper_f64 if H.dtype == np.float64 else lib().oracle_trsv_upper_f32
+    fn(H.shape[0], _ptr(H), H.shape[0], _ptr(y))
+    return y
+
+
+def rotg(a, b, dtype=np.float64):
+    v = np.array([a, b, 0, 0], dtype=dtype)
+    fn = lib().oracle_rotg_f64 if dtype == np.float64 else lib().oracle_rotg_f32
+    it = v.itemsize
+    base = v.ctypes.data
+    fn(base, base + it, base + 2 * it, base + 3 * it)
+    return v  # r, 0, c, s
+
+
+def jacobi(A, dtype=np.float64) -> np.ndarray:
+    d = np.zeros(A.nrows, dtype=dtype)
+    fn = lib().oracle_jacobi_f64 if dtype == np.float64 else lib().oracle_jacobi_f32
+    fn(A.nrows, _ptr(A.rowptr), _ptr(A.col), _ptr(A.val), _ptr(d))
+    return d

@@ -1,0 +1,225 @@
+// ORACLE — test infrastructure only. Never linked into the product.
+// Run-time binding of the MKL runtime (or plain loops); see cpu_blas.hpp.
+#include "cpu_blas.hpp"
+
+#include <dlfcn.h>
+
+#include <cmath>
+#include <cstdlib>
+#include <mutex>
+
+namespace oracle {
+
+namespace {
+
+MklApi g_api;
+std::once_flag g_once;
+
+template <class F>
+void bind(void* h, F& fn, const char* name, bool& ok) {
+    fn = reinterpret_cast<F>(dlsym(h, name));
+    if (!fn) ok = false;
+}
+
+void load() {
+    const char* force = std::getenv("MPG_ORACLE_BACKEND");
+    if (force && std::string(force) == "loops") return;
+    const char* env = std::getenv("MPG_MKL_PATH");
+    const char* candidates[] = {env, "/opt/conda/lib/libmkl_rt.so.1", "/opt/conda/lib/libmkl_rt.so", "libmkl_rt.so.1",
+                                "libmkl_rt.so"};
+    void* h = nullptr;
+    std::string used;
+    for (const char* c : candidates) {
+        if (!c) continue;
+        h = dlopen(c, RTLD_NOW | RTLD_GLOBAL);
+        if (h) {
+            used = c;
+            break;
+        }
+    }
+    if (!h) return;
+    // GNU OpenMP threading layer, as the reference links mkl_gnu_thread (Makefile:13)
+    if (auto set_layer = reinterpret_cast<int (*)(int)>(dlsym(h, "MKL_Set_Threading_Layer"))) set_layer(3);
+    bool ok = true;
+    MklApi& a = g_api;
+    bind(h, a.ddot, "cblas_ddot", ok);
+    bind(h, a.sdot, "cblas_sdot", ok);
+    bind(h, a.dnrm2, "cblas_dnrm2", ok);
+    bind(h, a.snrm2, "cblas_snrm2", ok);
+    bind(h, a.daxpy, "cblas_daxpy", ok);
+    bind(h, a.saxpy, "cblas_saxpy", ok);
+    bind(h, a.dscal, "cblas_dscal", ok);
+    bind(h, a.sscal, "cblas_sscal", ok);
+    bind(h, a.drotg, "cblas_drotg", ok);
+    bind(h, a.srotg, "cblas_srotg", ok);
+    bind(h, a.drot, "cblas_drot", ok);
+    bind(h, a.srot, "cblas_srot", ok);
+    bind(h, a.dgemv, "cblas_dgemv", ok);
+    bind(h, a.sgemv, "cblas_sgemv", ok);
+    bind(h, a.dtrsv, "cblas_dtrsv", ok);
+    bind(h, a.strsv, "cblas_strsv", ok);
+    bind(h, a.d_create_csr, "mkl_sparse_d_create_csr", ok);
+    bind(h, a.s_create_csr, "mkl_sparse_s_create_csr", ok);
+    bind(h, a.d_mv, "mkl_sparse_d_mv", ok);
+    bind(h, a.s_mv, "mkl_sparse_s_mv", ok);
+    bind(h, a.destroy, "mkl_sparse_destroy", ok);
+    bind(h, a.set_num_threads, "MKL_Set_Num_Threads", ok);
+    bind(h, a.get_max_threads, "MKL_Get_Max_Threads", ok);
+    a.loaded = ok;
+    a.path = used;
+}
+
+// classic reference-BLAS ?rotg for the loop backend
+template <class T>
+void rotg_loops(T* a, T* b, T* c, T* s) {
+    const T av = *a, bv = *b;
+    const T roe = std::fabs(av) > std::fabs(bv) ? av : bv;
+    const T scale = std::fabs(av) + std::fabs(bv);
+    T r, z;
+    if (scale == T(0)) {
+        *c = 1;
+        *s = 0;
+        r = 0;
+        z = 0;
+    } else {
+        const T as = av / scale, bs = bv / scale;
+        r = scale * std::sqrt(as * as + bs * bs);
+        r = roe >= T(0) ? r : -r;
+        *c = av / r;
+        *s = bv / r;
+        z = 1;
+        if (std::fabs(av) > std::fabs(bv)) z = *s;
+        if (std::fabs(bv) >= std::fabs(av) && *c != T(0)) z = T(1) / *c;
+    }
+    *a = r;
+    *b = z;
+}
+
+template <class T>
+void gemv_loops(bool trans, int rows, int cols, T alpha, const T* A, int lda, const T* x, T beta, T* y) {
+    if (trans) {
+#pragma omp parallel for schedule(static)
+        for (int j = 0; j < cols; ++j) {
+            double acc = 0;
+            for (int i = 0; i < rows; ++i) acc += (double)A[(size_t)j * lda + i] * x[i];
+            const T t = (T)acc;
+            y[j] = beta == T(0) ? alpha * t : alpha * t + beta * y[j];
+        }
+    } else {
+#pragma omp parallel for schedule(static)
+        for (int i = 0; i < rows; ++i) {
+            double acc = 0;
+            for (int j = 0; j < cols; ++j) acc += (double)A[(size_t)j * lda + i] * x[j];
+            const T t = (T)acc;
+            y[i] = beta == T(0) ? alpha * t : alpha * t + beta * y[i];
+        }
+    }
+}
+
+template <class T>
+void trsv_upper_loops(int n, const T* A, int lda, T* x) {
+    for (int j = n - 1; j >= 0; --j) {
+        if (x[j] == T(0)) continue;
+        x[j] = x[j] / A[(size_t)j * lda + j];
+        const T t = x[j];
+        for (int i = j - 1; i >= 0; --i) x[i] = x[i] - t * A[(size_t)j * lda + i];
+    }
+}
+
+}  // namespace
+
+const MklApi& mkl() {
+    std::call_once(g_once, load);
+    return g_api;
+}
+
+const char* backend_name() { return mkl().loaded ? "mkl" : "loops"; }
+
+void set_threads(int threads) {
+    if (threads <= 0) return;
+    if (mkl().loaded) mkl().set_num_threads(threads);
+}
+
+int max_threads() { return mkl().loaded ? mkl().get_max_threads() : 1; }
+
+double dot(int n, const double* x, const double* y) {
+    if (mkl().loaded) return mkl().ddot(n, x, 1, y, 1);
+    double s = 0;
+    for (int i = 0; i < n; ++i) s += x[i] * y[i];
+    return s;
+}
+float dot(int n, const float* x, const float* y) {
+    if (mkl().loaded) return mkl().sdot(n, x, 1, y, 1);
+    double s = 0;
+    for (int i = 0; i < n; ++i) s += (double)x[i] * y[i];
+    return (float)s;
+}
+double nrm2(int n, const double* x) {
+    if (mkl().loaded) return mkl().dnrm2(n, x, 1);
+    double s = 0;
+    for (int i = 0; i < n; ++i) s += x[i] * x[i];
+    return std::sqrt(s);
+}
+float nrm2(int n, const float* x) {
+    if (mkl().loaded) return mkl().snrm2(n, x, 1);
+    double s = 0;
+    for (int i = 0; i < n; ++i) s += (double)x[i] * x[i];
+    return (float)std::sqrt(s);
+}
+void axpy(int n, double a, const double* x, double* y) {
+    if (mkl().loaded) return mkl().daxpy(n, a, x, 1, y, 1);
+    for (int i = 0; i < n; ++i) y[i] += a * x[i];
+}
+void axpy(int n, float a, const float* x, float* y) {
+    if (mkl().loaded) return mkl().saxpy(n, a, x, 1, y, 1);
+    for (int i = 0; i < n; ++i) y[i] += a * x[i];
+}
+void scal(int n, double a, double* x) {
+    if (mkl().loaded) return mkl().dscal(n, a, x, 1);
+    for (int i = 0; i < n; ++i) x[i] *= a;
+}
+void scal(int n, float a, float* x) {
+    if (mkl().loaded) return mkl().sscal(n, a, x, 1);
+    for (int i = 0; i < n; ++i) x[i] *= a;
+}
+void rotg(double* a, double* b, double* c, double* s) {
+    if (mkl().loaded) return mkl().drotg(a, b, c, s);
+    rotg_loops(a, b, c, s);
+}
+void rotg(float* a, float* b, float* c, float* s) {
+    if (mkl().loaded) return mkl().srotg(a, b, c, s);
+    rotg_loops(a, b, c, s);
+}
+void rot1(double* x, double* y, double c, double s) {
+    if (mkl().loaded) return mkl().drot(1, x, 1, y, 1, c, s);
+    const double t = c * *x + s * *y;
+    *y = c * *y - s * *x;
+    *x = t;
+}
+void rot1(float* x, float* y, float c, float s) {
+    if (mkl().loaded) return mkl().srot(1, x, 1, y, 1, c, s);
+    const float t = c * *x + s * *y;
+    *y = c * *y - s * *x;
+    *x = t;
+}
+void gemv(bool trans, int rows, int cols, double alpha, const double* A, int lda, const double* x, double beta,
+          double* y) {
+    if (mkl().loaded)
+        return mkl().dgemv(kColMajor, trans ? kTrans : kNoTrans, rows, cols, alpha, A, lda, x, 1, beta, y, 1);
+    gemv_loops(trans, rows, cols, alpha, A, lda, x, beta, y);
+}
+void gemv(bool trans, int rows, int cols, float alpha, const float* A, int lda, const float* x, float beta, float* y) {
+    if (mkl().loaded)
+        return mkl().sgemv(kColMajor, trans ? kTrans : kNoTrans, rows, cols, alpha, A, lda, x, 1, beta, y, 1);
+    gemv_loops(trans, rows, cols, alpha, A, lda, x, beta, y);
+}
+void trsv_upper(int n, const double* A, int lda, double* x) {
+    if (mkl().loaded) return mkl().dtrsv(kColMajor, kUpper, kNoTrans, kNonUnit, n, A, lda, x, 1);
+    trsv_upper_loops(n, A, lda, x);
+}
+void trsv_upper(int n, const float* A, int lda, float* x) {
+    if (mkl().loaded) return mkl().strsv(kColMajor, kUpper, kNoTrans, kNonUnit, n, A, lda, x, 1);
+    trsv_upper_loops(n, A, lda, x);
+}
+
+}  // namespace oracle
