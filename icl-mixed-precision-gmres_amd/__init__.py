@@ -81,6 +81,15 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_host_spmv.argtypes = [C.POINTER(HostCsr), C.POINTER(C.c_double), C.POINTER(C.c_double)]
     lib.mpg_host_csr_free.argtypes = [C.POINTER(HostCsr)]
     lib.mpg_host_csr_free.restype = None
+    lib.mpg_engine_create.argtypes = [C.POINTER(SolveArgs), C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
+    lib.mpg_engine_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+    lib.mpg_engine_sync.argtypes = [C.c_void_p]
+    lib.mpg_engine_total_iters.argtypes = [C.c_void_p]
+    lib.mpg_engine_total_iters.restype = C.c_int64
+    lib.mpg_engine_time_phase.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    lib.mpg_engine_phase_bytes.argtypes = [C.c_void_p, C.c_int]
+    lib.mpg_engine_phase_bytes.restype = C.c_double
+    lib.mpg_engine_destroy.argtypes = [C.c_void_p]
 
 
 # (name, argtypes) for the kernel-level C-ABI, used by the per-kernel tests
@@ -314,3 +323,54 @@ def solve(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, **opts) ->
     """Restarted GMRES(m) on the MI355X (mpg_solve). Options as make_args."""
     args, keep = make_args(A, b, x_true, **opts)
     return run_solve(host_lib().mpg_solve, args, A.nrows)
+
+
+class Engine:
+    """Stepped fused engine (mpg_engine_*): set up once, then advance the
+    restarted solve cycle by cycle — what bench.py times."""
+
+    PHASES = {"spmv": 0, "prologue": 1, "cgs_update": 2}
+
+    def __init__(self, A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, **opts):
+        opts.pop("engine", None)
+        self._args, self._keep = make_args(A, b, x_true, engine="fused", **opts)
+        self._lib = host_lib()
+        self._h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        if self._lib.mpg_engine_create(C.byref(self._args), C.byref(self._h), err, 512):
+            raise RuntimeError(f"mpg_engine_create: {err.value.decode()}")
+
+    def run(self, cycles: int) -> tuple:
+        done = C.c_int(0)
+        ran = self._lib.mpg_engine_run(self._h, cycles, C.byref(done))
+        if ran < 0:
+            raise RuntimeError(f"mpg_engine_run failed ({ran})")
+        return ran, bool(done.value)
+
+    def sync(self) -> None:
+        if self._lib.mpg_engine_sync(self._h):
+            raise RuntimeError("mpg_engine_sync failed")
+
+    @property
+    def total_iters(self) -> int:
+        return int(self._lib.mpg_engine_total_iters(self._h))
+
+    def time_phase(self, phase: str, reps: int = 20) -> float:
+        ms = C.c_double()
+        if self._lib.mpg_engine_time_phase(self._h, self.PHASES[phase], reps, C.byref(ms)):
+            raise RuntimeError("mpg_engine_time_phase failed")
+        return ms.value
+
+    def phase_bytes(self, phase: str) -> float:
+        return float(self._lib.mpg_engine_phase_bytes(self._h, self.PHASES[phase]))
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.mpg_engine_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

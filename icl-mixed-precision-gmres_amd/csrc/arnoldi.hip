@@ -1,0 +1,615 @@
+// Fused Arnoldi phase kernels for gfx950 (include/mpgmres/arnoldi.h).
+//
+// One restart cycle of GMRES(m) becomes a fixed program of phase kernels
+// with no host round trip: the prologue (true residual + preconditioner +
+// norms), per step an SpMV that normalises the previous vector on the fly
+// and emits the Gram-Schmidt dot partials, the CGS/MGS update kernels that
+// emit the next partials, a one-lane Givens kernel, and the solution update.
+// Global sums are two-stage and deterministic (per-workgroup fp64 partials,
+// then k_reduce_partials in a fixed order), which is also the seam where a
+// multi-GPU caller all-reduces across ranks.
+//
+// Numerics follow the operator surface exactly where the reference fixes
+// an order (reciprocal-then-multiply normalisation, y = alpha*t + beta*y
+// forms, Givens on rounded products); every dot/norm/gemv/SpMV accumulates in
+// fp64 and is rounded once to the working precision — the same rounding the
+// stand-alone kernels (blas1/blas2/spmv) apply, so the fused engine and the
+// operator-surface driver agree to the last bit in most steps.
+#include "internal.hpp"
+#include "mpgmres/arnoldi.h"
+
+#include <new>
+
+using namespace mpg;
+
+namespace {
+
+constexpr int kNnzCap = 2048;  // must match spmv.hip
+constexpr int kNC = 32;        // dot columns carried in registers per pass
+constexpr int kGroups = 1024;  // max workgroups of the row-block phase kernels
+constexpr int kOrthMGS = 1, kOrthCGSR = 2;  // mpg_orth_t (include/mpgmres/solve.h)
+
+struct half_v {
+    uint16_t bits;
+};
+
+template <class V>
+__device__ __forceinline__ double ld_val(const V* v, int64_t i) { return (double)v[i]; }
+template <>
+__device__ __forceinline__ double ld_val<half_v>(const half_v* v, int64_t i) { return (double)to_float(v[i].bits); }
+
+// Jacobi / identity preconditioner in precision P applied to a T value:
+// typesafe_apply (gmres.cpp:12-22) + gdmv(1, d, w, 0, w) (kernels.hpp:141-144).
+template <class T, class P>
+__device__ __forceinline__ T precond(T w, const P* __restrict__ d, int64_t i) {
+    P p = (P)w;
+    if (d) p = P(0) * p + P(1) * d[i] * p;
+    return (T)p;
+}
+
+// Walk the row blocks [rb] of the CSR-adaptive schedule assigned to this
+// workgroup. For every row: sum_j val_j * xval(col_j) in fp64 (products
+// staged in LDS for multi-row blocks), then epi(row, sum) on one lane.
+template <class V, class XF, class EPI>
+__device__ __forceinline__ void for_rows(const int32_t* __restrict__ blocks, int nblocks,
+                                         const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                         const V* __restrict__ val, XF xval, EPI epi, double* prod,
+                                         double* scratch) {
+    for (int b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        const int r0 = blocks[b], r1 = blocks[b + 1];
+        const int s = rowptr[r0], e = rowptr[r1];
+        if (r1 - r0 == 1) {
+            double acc = 0.0;
+            for (int i = s + threadIdx.x; i < e; i += kBlock) acc += ld_val(val, i) * xval(col[i]);
+            double sum = block_sum<kBlock>(acc, scratch);
+            if (threadIdx.x == 0) epi(r0, sum);
+            continue;
+        }
+        const int nnz = e - s;
+        for (int i = threadIdx.x; i < nnz; i += kBlock) prod[i] = ld_val(val, s + i) * xval(col[s + i]);
+        __syncthreads();
+        for (int r = threadIdx.x; r < r1 - r0; r += kBlock) {
+            const int a = rowptr[r0 + r] - s, z = rowptr[r0 + r + 1] - s;
+            double acc = 0.0;
+            for (int j = a; j < z; ++j) acc += prod[j];
+            epi(r0 + r, acc);
+        }
+        __syncthreads();
+    }
+}
+
+// Block-reduce NCOL fp64 accumulators and store them as partial[c*G + blk].
+template <int NCOL>
+__device__ __forceinline__ void store_partials(double (&acc)[NCOL], int ncols, double* __restrict__ partial) {
+    __shared__ double red[kBlock / kWave][NCOL];
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) {
+        if (c < ncols) {
+            double v = wave_sum(acc[c]);
+            if (lane == 0) red[wid][c] = v;
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < ncols; c += kBlock) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kBlock / kWave; ++w) s += red[w][c];
+        partial[(size_t)c * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+// ---------------------------------------------------------------- prologue
+// r = b - A x (X), w = M(T(r)); partials: ||T(r)||^2, ||w||^2, ||x||^2
+template <class T, class X, class P>
+__global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__ blocks, int nblocks,
+                                                     const int32_t* __restrict__ rowptr,
+                                                     const int32_t* __restrict__ col, const X* __restrict__ val,
+                                                     const X* __restrict__ x, const X* __restrict__ b,
+                                                     const P* __restrict__ diag, T* __restrict__ w,
+                                                     double* __restrict__ partial) {
+    __shared__ double prod[kNnzCap];
+    __shared__ double scratch[kBlock / kWave];
+    double acc[3] = {0.0, 0.0, 0.0};
+    for_rows(
+        blocks, nblocks, rowptr, col, val, [&](int c) { return (double)x[c]; },
+        [&](int i, double sum) {
+            const X t = (X)sum;
+            const X r = b[i] - t;  // copy(b, w); spmv(-1, A, x, 1, w)
+            T wi = (T)r;
+            acc[0] += (double)wi * (double)wi;
+            wi = precond<T, P>(wi, diag, i);
+            acc[1] += (double)wi * (double)wi;
+            acc[2] += (double)x[i] * (double)x[i];
+            w[i] = wi;
+        },
+        prod, scratch);
+    store_partials<3>(acc, 3, partial);
+}
+
+template <class T, class X>
+__global__ void k_prologue_finish(const double* __restrict__ sums, int m, T* __restrict__ s, T* __restrict__ inv,
+                                  double* __restrict__ report) {
+    const T r_norm = (T)sqrt(sums[0]);
+    const T beta = (T)sqrt(sums[1]);
+    const X x_norm = (X)sqrt(sums[2]);
+    const T iv = beta != T(0) ? T(1) / beta : T(0);  // first_vector: zero fill when beta == 0
+    if (threadIdx.x == 0) {
+        report[0] = (double)r_norm;
+        report[1] = (double)beta;
+        report[2] = (double)x_norm;
+        report[3] = (double)iv;
+        *inv = iv;
+    }
+    for (int i = threadIdx.x; i <= m; i += blockDim.x) s[i] = i == 0 ? beta : T(0);
+}
+
+// ---------------------------------------------------------------- reductions
+__global__ __launch_bounds__(kBlock) void k_reduce_partials(int G, const double* __restrict__ partial,
+                                                            double* __restrict__ sums) {
+    __shared__ double scratch[kBlock / kWave];
+    const int c = blockIdx.x;
+    double v = 0.0;
+    for (int g = threadIdx.x; g < G; g += kBlock) v += partial[(size_t)c * G + g];
+    double s = block_sum<kBlock>(v, scratch);
+    if (threadIdx.x == 0) sums[c] = s;
+}
+
+// ---------------------------------------------------------------- step: SpMV
+// v_k = T(w_prev * inv) (local rows stored to V[:,k]); w = M(A v_k);
+// partials <v_j, w> for j in [0, ndots)
+template <class T, class P, class VI>
+__global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict__ blocks, int nblocks,
+                                                      const int32_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ col, const VI* __restrict__ val,
+                                                      const T* __restrict__ wprev, const T* __restrict__ inv_p,
+                                                      T* __restrict__ V, int64_t ld, int k, int ndots,
+                                                      const P* __restrict__ diag, T* __restrict__ w,
+                                                      double* __restrict__ partial) {
+    __shared__ double prod[kNnzCap];
+    __shared__ double scratch[kBlock / kWave];
+    const T inv = *inv_p;
+    double acc[kNC];
+#pragma unroll
+    for (int c = 0; c < kNC; ++c) acc[c] = 0.0;
+    T* __restrict__ Vk = V + (int64_t)k * ld;
+    for_rows(
+        blocks, nblocks, rowptr, col, val, [&](int c) { return (double)(T)(wprev[c] * inv); },
+        [&](int i, double sum) {
+            const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
+            const T wi = precond<T, P>(t, diag, i);
+            w[i] = wi;
+            const T vki = wprev[i] * inv;
+            Vk[i] = vki;
+#pragma unroll
+            for (int j = 0; j < kNC; ++j) {
+                if (j < ndots) {
+                    const T vj = j == k ? vki : V[(int64_t)j * ld + i];
+                    acc[j] += (double)vj * (double)wi;
+                }
+            }
+        },
+        prod, scratch);
+    store_partials<kNC>(acc, ndots, partial);
+}
+
+// partial dots <v_j, w> for j in [c0, c0 + nc) over all local rows
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_panel_dots(int n, const T* __restrict__ V, int64_t ld, int c0, int nc,
+                                                       const T* __restrict__ w, double* __restrict__ partial) {
+    double acc[kNC];
+#pragma unroll
+    for (int c = 0; c < kNC; ++c) acc[c] = 0.0;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const double wi = (double)w[i];
+#pragma unroll
+        for (int c = 0; c < kNC; ++c)
+            if (c < nc) acc[c] += (double)V[(int64_t)(c0 + c) * ld + i] * wi;
+    }
+    store_partials<kNC>(acc, nc, partial + (size_t)c0 * gridDim.x);
+}
+
+// ---------------------------------------------------------------- step: CGS
+// coef = T(sums[0..k]); w = w - T(V coef) (gemv(-1, V, h, 1, w));
+// NEXT_DOTS: partials <v_j, w'> (j <= k) else partial ||w'||^2
+template <class T, bool NEXT_DOTS>
+__global__ __launch_bounds__(kBlock) void k_cgs_update(int n, const T* __restrict__ V, int64_t ld, int k,
+                                                       const double* __restrict__ sums, T* __restrict__ coef_out,
+                                                       T* __restrict__ w, double* __restrict__ partial) {
+    __shared__ T coef[256];
+    const int nc = k + 1;
+    for (int j = threadIdx.x; j < nc; j += kBlock) {
+        coef[j] = (T)sums[j];
+        if (blockIdx.x == 0) coef_out[j] = coef[j];
+    }
+    __syncthreads();
+    double acc[NEXT_DOTS ? kNC : 1];
+#pragma unroll
+    for (int c = 0; c < (NEXT_DOTS ? kNC : 1); ++c) acc[c] = 0.0;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        double t = 0.0;
+        for (int j = 0; j < nc; ++j) t += (double)V[(int64_t)j * ld + i] * (double)coef[j];
+        const T wi = T(-1) * (T)t + T(1) * w[i];
+        w[i] = wi;
+        if (NEXT_DOTS) {
+#pragma unroll
+            for (int c = 0; c < kNC; ++c)
+                if (c < nc) acc[c] += (double)V[(int64_t)c * ld + i] * (double)wi;
+        } else {
+            acc[0] += (double)wi * (double)wi;
+        }
+    }
+    store_partials<NEXT_DOTS ? kNC : 1>(acc, NEXT_DOTS ? (nc < kNC ? nc : kNC) : 1, partial);
+}
+
+// ---------------------------------------------------------------- step: MGS
+// h_jk = T(sums[0]); w -= h_jk v_j (naxpy); partial <v_{j+1}, w> or ||w||^2
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_mgs_update(int n, const T* __restrict__ V, int64_t ld, int j, int k,
+                                                       const double* __restrict__ sums, T* __restrict__ hjk,
+                                                       T* __restrict__ w, double* __restrict__ partial) {
+    const T h = (T)sums[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *hjk = h;
+    const T* __restrict__ vj = V + (int64_t)j * ld;
+    const T* __restrict__ vn = V + (int64_t)(j + 1) * ld;
+    const bool last = j == k;
+    double acc[1] = {0.0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        T wi = w[i];
+        wi -= h * vj[i];
+        w[i] = wi;
+        acc[0] += last ? (double)wi * (double)wi : (double)vn[i] * (double)wi;
+    }
+    store_partials<1>(acc, 1, partial);
+}
+
+// ---------------------------------------------------------------- step: Givens
+#pragma clang fp contract(off)
+template <class T>
+__device__ void rot_pair(T& a, T& b, T c, T s) {
+    const T a1 = a, a2 = b;
+    a = c * a1 + s * a2;
+    b = c * a2 - s * a1;
+}
+template <class T>
+__device__ void rotg_ref(T& a, T& b, T& c, T& s) {
+    const T av = a, bv = b;
+    const T roe = fabs(av) > fabs(bv) ? av : bv;
+    const T scale = fabs(av) + fabs(bv);
+    T r;
+    if (scale == T(0)) {
+        c = T(1); s = T(0); r = T(0);
+    } else {
+        const T as = av / scale, bs = bv / scale;
+        r = scale * sqrt(as * as + bs * bs);
+        r = roe >= T(0) ? r : -r;
+        c = av / r;
+        s = bv / r;
+    }
+    a = r;
+    b = T(0);
+}
+
+// h_{k+1,k} = ||w||; (CGSR: h(0:k,k) += correction); rotations; |s(k+1)|
+template <class T>
+__global__ void k_givens(int k, int m, const double* __restrict__ sums, const T* __restrict__ corr,
+                         T* __restrict__ H, T* __restrict__ cs, T* __restrict__ sn, T* __restrict__ s,
+                         T* __restrict__ inv, double* __restrict__ report) {
+    if (threadIdx.x != 0) return;
+    const int ldh = m + 1;
+    T* col = H + (int64_t)k * ldh;
+    if (corr)
+        for (int j = 0; j <= k; ++j) col[j] = col[j] + T(1) * corr[j];  // axpy(1.0, weights, h_col)
+    const T hn = (T)sqrt(sums[0]);
+    col[k + 1] = hn;
+    *inv = T(1) / hn;  // scal(1/h_final, w, v_{k+1}) — no breakdown guard, as in the reference
+    for (int j = 0; j < k; ++j) rot_pair(col[j], col[j + 1], cs[j], sn[j]);
+    rotg_ref(col[k], col[k + 1], cs[k], sn[k]);
+    rot_pair(s[k], s[k + 1], cs[k], sn[k]);
+    report[4 + k] = (double)fabs(s[k + 1]);
+}
+
+// upper-triangular solve y = H(0:k,0:k)^-1 s(0:k), in place on s (one lane per
+// row of the axpy sweep; k <= m is small)
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_trsv_upper(int k, int ldh, const T* __restrict__ H, T* __restrict__ y) {
+    __shared__ T ys[1024];
+    __shared__ T temp_s;
+    for (int i = threadIdx.x; i < k; i += kBlock) ys[i] = y[i];
+    __syncthreads();
+    for (int j = k - 1; j >= 0; --j) {
+        if (threadIdx.x == 0) {
+            T yj = ys[j];
+            if (yj != T(0)) yj = yj / H[(int64_t)j * ldh + j];
+            ys[j] = yj;
+            temp_s = yj;
+        }
+        __syncthreads();
+        const T t = temp_s;
+        if (t != T(0))
+            for (int i = threadIdx.x; i < j; i += kBlock) ys[i] = ys[i] - t * H[(int64_t)j * ldh + i];
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < k; i += kBlock) y[i] = ys[i];
+}
+#pragma clang fp contract(on)
+
+// x += X(T(V y)): mixed form gemv(1, V, y, 0, tmp); copy; axpy(1, tmp, x)
+// (same-precision form gemv(1, V, y, 1, x) gives the same fl(t + x))
+template <class T, class X>
+__global__ __launch_bounds__(kBlock) void k_update_x(int n, const T* __restrict__ V, int64_t ld, int k,
+                                                     const T* __restrict__ y, X* __restrict__ x) {
+    __shared__ T ys[1024];
+    for (int j = threadIdx.x; j < k; j += kBlock) ys[j] = y[j];
+    __syncthreads();
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        double t = 0.0;
+        for (int j = 0; j < k; ++j) t += (double)V[(int64_t)j * ld + i] * (double)ys[j];
+        x[i] = x[i] + (X)(T)t;
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- plan object
+struct mpg_arnoldi {
+    mpg_ctx* ctx = nullptr;
+    mpg_arnoldi_desc d{};
+    int combo = 0;    // type combination (see dispatch below)
+    int G = 1;        // workgroups of the phase kernels
+    int64_t ld = 0;   // leading dimension of V (elements)
+    size_t tsize = 8;
+    void* V = nullptr;
+    void* H = nullptr;      // (m+1) x m
+    void* small = nullptr;  // cs, sn, s (m+1 each), inv, corr (m+1), coef scratch
+    void* w[2] = {nullptr, nullptr};
+    double* partial = nullptr;  // (kNC + 4) x G
+    double* sums = nullptr;     // m + 4
+    double* report = nullptr;   // 4 + m
+
+    char* small_at(int slot) const { return static_cast<char*>(small) + (size_t)slot * (d.m + 1) * tsize; }
+    void* cs() const { return small_at(0); }
+    void* sn() const { return small_at(1); }
+    void* s() const { return small_at(2); }
+    void* corr() const { return small_at(3); }
+    void* inv() const { return small_at(4); }
+};
+
+namespace {
+
+// combos: 0 baseline <d,d,d,d>; 1 single-prec <d,d,f,d>; 2 single <f,f,f,f>;
+//         3 mixed <f,d,f,f>; 4 mixed-half <f,d,f,h>
+int combo_of(const mpg_arnoldi_desc& d) {
+    if (d.vec_type == MPG_F64 && d.outer_type == MPG_F64 && d.inner_val == MPG_F64)
+        return d.prec_type == MPG_F64 ? 0 : (d.prec_type == MPG_F32 ? 1 : -1);
+    if (d.vec_type == MPG_F32 && d.prec_type == MPG_F32) {
+        if (d.outer_type == MPG_F32 && d.inner_val == MPG_F32) return 2;
+        if (d.outer_type == MPG_F64 && d.inner_val == MPG_F32) return 3;
+        if (d.outer_type == MPG_F64 && d.inner_val == MPG_F16) return 4;
+    }
+    return -1;
+}
+
+template <class F>
+int dispatch(int combo, F&& f) {
+    switch (combo) {
+        case 0: return f(double(), double(), double(), double());
+        case 1: return f(double(), double(), float(), double());
+        case 2: return f(float(), float(), float(), float());
+        case 3: return f(float(), double(), float(), float());
+        case 4: return f(float(), double(), float(), half_v());
+        default: return MPG_ERR_UNSUPPORTED;
+    }
+}
+
+int row_grid(const mpg_arnoldi* a) { return a->G; }
+
+}  // namespace
+
+extern "C" {
+
+int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_t* out) {
+    if (!ctx || !desc || !out || !desc->A || desc->n < 0 || desc->n_ext < desc->n || desc->m < 1 ||
+        desc->m > 1000 || desc->orth < 0 || desc->orth > 2)
+        return MPG_ERR_ARG;
+    *out = nullptr;
+    int combo = combo_of(*desc);
+    if (combo < 0) return MPG_ERR_UNSUPPORTED;
+    if (desc->A->rows != desc->n || desc->A->cols > desc->n_ext) return MPG_ERR_ARG;
+    mpg_arnoldi* a = new (std::nothrow) mpg_arnoldi();
+    if (!a) return MPG_ERR_ALLOC;
+    a->ctx = ctx;
+    a->d = *desc;
+    a->combo = combo;
+    a->tsize = desc->vec_type == MPG_F64 ? 8 : 4;
+    a->G = desc->A->nblocks < kGroups ? (desc->A->nblocks > 0 ? desc->A->nblocks : 1) : kGroups;
+    const size_t align = 256 / a->tsize;
+    a->ld = ((int64_t)desc->n + align - 1) / align * align;
+    if (a->ld == 0) a->ld = align;
+    const int m = desc->m;
+    auto alloc = [&](void** p, size_t bytes) {
+        if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) return false;
+        return hipMemsetAsync(*p, 0, bytes ? bytes : 16, ctx->stream) == hipSuccess;
+    };
+    bool ok = alloc(&a->V, (size_t)a->ld * (m + 1) * a->tsize) && alloc(&a->H, (size_t)(m + 1) * m * a->tsize) &&
+              alloc(&a->small, (size_t)6 * (m + 1) * a->tsize) &&
+              alloc(&a->w[0], (size_t)(desc->n_ext + 64) * a->tsize) &&
+              alloc(&a->w[1], (size_t)(desc->n_ext + 64) * a->tsize) &&
+              alloc((void**)&a->partial, (size_t)(kNC + 4) * a->G * sizeof(double) +
+                                             (size_t)(m + 1) * a->G * sizeof(double)) &&
+              alloc((void**)&a->sums, (size_t)(m + 8) * sizeof(double)) &&
+              alloc((void**)&a->report, (size_t)(m + 8) * sizeof(double));
+    if (!ok) {
+        mpg_arnoldi_destroy(a);
+        return MPG_ERR_ALLOC;
+    }
+    *out = a;
+    return MPG_OK;
+}
+
+int mpg_arnoldi_destroy(mpg_arnoldi_t a) {
+    if (!a) return MPG_OK;
+    if (a->ctx) (void)hipStreamSynchronize(a->ctx->stream);
+    void* ps[] = {a->V, a->H, a->small, a->w[0], a->w[1], a->partial, a->sums, a->report};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    delete a;
+    return MPG_OK;
+}
+
+int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
+    if (!a) return MPG_ERR_ARG;
+    const mpg_csr* A = a->d.A;
+    int st = dispatch(a->combo, [&](auto t, auto x, auto p, auto) {
+        using T = decltype(t);
+        using X = decltype(x);
+        using P = decltype(p);
+        k_prologue<T, X, P><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+            A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const X*>(a->d.val_outer),
+            static_cast<const X*>(a->d.x), static_cast<const X*>(a->d.b),
+            a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr, static_cast<T*>(a->w[0]), a->partial);
+        return MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a) {
+    if (!a) return MPG_ERR_ARG;
+    int st = dispatch(a->combo, [&](auto t, auto x, auto, auto) {
+        using T = decltype(t);
+        using X = decltype(x);
+        k_prologue_finish<T, X><<<1, 64, 0, a->ctx->stream>>>(a->sums, a->d.m, static_cast<T*>(a->s()),
+                                                                static_cast<T*>(a->inv()), a->report);
+        return MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols) {
+    if (!a || ncols < 1 || ncols > a->d.m + 4) return MPG_ERR_ARG;
+    k_reduce_partials<<<ncols, kBlock, 0, a->ctx->stream>>>(a->G, a->partial, a->sums);
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k) {
+    if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
+    const mpg_csr* A = a->d.A;
+    const int ndots_all = a->d.orth == kOrthMGS ? 1 : k + 1;
+    const int ndots_fused = ndots_all < kNC ? ndots_all : kNC;
+    int st = dispatch(a->combo, [&](auto t, auto, auto p, auto vi) {
+        using T = decltype(t);
+        using P = decltype(p);
+        using VI = decltype(vi);
+        k_step_spmv<T, P, VI><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+            A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner),
+            static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,
+            ndots_fused, a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr, static_cast<T*>(a->w[(k + 1) & 1]),
+            a->partial);
+        for (int c0 = kNC; c0 < ndots_all; c0 += kNC) {
+            const int nc = ndots_all - c0 < kNC ? ndots_all - c0 : kNC;
+            k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, c0, nc, static_cast<const T*>(a->w[(k + 1) & 1]),
+                a->partial);
+        }
+        return MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass) {
+    if (!a || k < 0 || k >= a->d.m || pass < 0 || pass > 1 || k + 1 > 256) return MPG_ERR_ARG;
+    const bool cgsr = a->d.orth == kOrthCGSR;
+    const bool next_dots = cgsr && pass == 0;
+    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
+        using T = decltype(t);
+        T* coef_out = pass == 0 ? static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) : static_cast<T*>(a->corr());
+        T* w = static_cast<T*>(a->w[(k + 1) & 1]);
+        if (next_dots) {
+            k_cgs_update<T, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, a->sums, coef_out, w, a->partial);
+            for (int c0 = kNC; c0 < k + 1; c0 += kNC) {
+                const int nc = k + 1 - c0 < kNC ? k + 1 - c0 : kNC;
+                k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->V),
+                                                                            a->ld, c0, nc, w, a->partial);
+            }
+        } else {
+            k_cgs_update<T, false><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, a->sums, coef_out, w, a->partial);
+        }
+        return MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j) {
+    if (!a || k < 0 || k >= a->d.m || j < 0 || j > k) return MPG_ERR_ARG;
+    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
+        using T = decltype(t);
+        T* hjk = static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) + j;
+        k_mgs_update<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->V), a->ld, j,
+                                                                    k, a->sums, hjk,
+                                                                    static_cast<T*>(a->w[(k + 1) & 1]), a->partial);
+        return MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_givens(mpg_arnoldi_t a, int k) {
+    if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
+    const bool cgsr = a->d.orth == kOrthCGSR;
+    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
+        using T = decltype(t);
+        k_givens<T><<<1, 64, 0, a->ctx->stream>>>(k, a->d.m, a->sums, cgsr ? static_cast<const T*>(a->corr()) : nullptr,
+                                                  static_cast<T*>(a->H), static_cast<T*>(a->cs()),
+                                                  static_cast<T*>(a->sn()), static_cast<T*>(a->s()),
+                                                  static_cast<T*>(a->inv()), a->report);
+        return MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_update(mpg_arnoldi_t a, int k) {
+    if (!a || k < 0 || k > a->d.m || k > 1024) return MPG_ERR_ARG;
+    if (k == 0) return MPG_OK;
+    int st = dispatch(a->combo, [&](auto t, auto x, auto, auto) {
+        using T = decltype(t);
+        using X = decltype(x);
+        k_trsv_upper<T><<<1, kBlock, 0, a->ctx->stream>>>(k, a->d.m + 1, static_cast<const T*>(a->H),
+                                                          static_cast<T*>(a->s()));
+        k_update_x<T, X><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->V), a->ld, k,
+                                                                     static_cast<const T*>(a->s()),
+                                                                     static_cast<X*>(a->d.x));
+        return MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+double* mpg_arnoldi_sums_dev(mpg_arnoldi_t a) { return a ? a->sums : nullptr; }
+void* mpg_arnoldi_wprev_dev(mpg_arnoldi_t a, int k) { return a ? a->w[k & 1] : nullptr; }
+int mpg_arnoldi_vec_bytes(mpg_arnoldi_t a) { return a ? (int)a->tsize : 0; }
+const double* mpg_arnoldi_report_dev(mpg_arnoldi_t a) { return a ? a->report : nullptr; }
+int mpg_arnoldi_report_len(mpg_arnoldi_t a) { return a ? a->d.m + 4 : 0; }
+const void* mpg_arnoldi_basis_dev(mpg_arnoldi_t a, int64_t* ld) {
+    if (!a) return nullptr;
+    if (ld) *ld = a->ld;
+    return a->V;
+}
+const void* mpg_arnoldi_hessenberg_dev(mpg_arnoldi_t a) { return a ? a->H : nullptr; }
+int mpg_arnoldi_num_groups(mpg_arnoldi_t a) { return a ? a->G : 0; }
+
+}  // extern "C"

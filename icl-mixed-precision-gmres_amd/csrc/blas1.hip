@@ -219,6 +219,24 @@ int mpg_nrm2_f64(mpg_ctx_t c, int64_t n, const double* x, double* r) { return re
 int mpg_nrm2_f32(mpg_ctx_t c, int64_t n, const float* x, float* r) { return reduce<float, true>(c, n, x, x, r); }
 int mpg_nrm2_f64_host(mpg_ctx_t c, int64_t n, const double* x, double* r) { return reduce_host<double, true>(c, n, x, x, r); }
 int mpg_nrm2_f32_host(mpg_ctx_t c, int64_t n, const float* x, float* r) { return reduce_host<float, true>(c, n, x, x, r); }
+int mpg_dot_acc_f64(mpg_ctx_t c, int64_t n, const double* x, const double* y, double* acc) {
+    if (!c || n < 0) return MPG_ERR_ARG;
+    int g = grid_for(n, 4, kMaxRedBlocks);
+    k_reduce_stage1<double, false><<<g, kBlock, 0, c->stream>>>(n, x, y, c->red_ws);
+    MPG_LAUNCH_CHECK(c);
+    k_reduce_stage2<double, false><<<1, 1024, 0, c->stream>>>(g, c->red_ws, acc);
+    MPG_LAUNCH_CHECK(c);
+    return MPG_OK;
+}
+int mpg_dot_acc_f32(mpg_ctx_t c, int64_t n, const float* x, const float* y, double* acc) {
+    if (!c || n < 0) return MPG_ERR_ARG;
+    int g = grid_for(n, 4, kMaxRedBlocks);
+    k_reduce_stage1<float, false><<<g, kBlock, 0, c->stream>>>(n, x, y, c->red_ws);
+    MPG_LAUNCH_CHECK(c);
+    k_reduce_stage2<double, false><<<1, 1024, 0, c->stream>>>(g, c->red_ws, acc);
+    MPG_LAUNCH_CHECK(c);
+    return MPG_OK;
+}
 
 int mpg_axpy_f64(mpg_ctx_t c, int64_t n, double a, const double* x, double* y) { return axpy_impl<double, false, false>(c, n, a, nullptr, x, y); }
 int mpg_axpy_f32(mpg_ctx_t c, int64_t n, float a, const float* x, float* y) { return axpy_impl<float, false, false>(c, n, a, nullptr, x, y); }

@@ -22,15 +22,6 @@
 
 using namespace mpg;
 
-struct mpg_csr {
-    mpg_ctx* ctx = nullptr;
-    int32_t rows = 0, cols = 0;
-    int64_t nnz = 0;
-    const int32_t* rowptr = nullptr;  // device, borrowed
-    const int32_t* col = nullptr;     // device, borrowed
-    int32_t* blocks = nullptr;        // device, owned: nblocks+1 row starts
-    int nblocks = 0;
-};
 
 namespace {
 

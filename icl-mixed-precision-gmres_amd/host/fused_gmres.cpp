@@ -1,9 +1,597 @@
+// Fused Arnoldi engine (see fused_gmres.hpp) and its C-ABI (mpg_engine_*,
+// mpg_solve with engine = MPG_ENGINE_FUSED).
 #include "fused_gmres.hpp"
 
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
 #include <stdexcept>
 
+#include "gmres.hpp"
+#include "types_hip.hpp"
+
 namespace mpg {
-int solve_fused(const mpg_solve_args&, mpg_solve_result*) {
-    throw std::invalid_argument("fused engine not built yet");
+
+// ---------------------------------------------------------------- DevMem
+DevMem::DevMem(mpg_ctx_t c, size_t b) : ctx(c), bytes(b) { check(mpg_malloc(c, b, &p), "mpg_malloc", c); }
+DevMem::~DevMem() {
+    if (p) mpg_free(ctx, p);
 }
+DevMem& DevMem::operator=(DevMem&& o) noexcept {
+    if (this != &o) {
+        if (p) mpg_free(ctx, p);
+        ctx = o.ctx;
+        p = o.p;
+        bytes = o.bytes;
+        o.p = nullptr;
+        o.bytes = 0;
+    }
+    return *this;
+}
+
+namespace {
+
+using clk = std::chrono::steady_clock;
+
+void hipck(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("mpgmres: ") + what + ": " + hipGetErrorString(e));
+}
+
+// the driver's working types for a mode (gmres_perf_test.cpp:240-305)
+struct ModeTypes {
+    int T, X, P, VI;  // mpg_dtype_t
+    bool single_scalars;  // host scalars in float (mode single)
+};
+ModeTypes types_for(int mode) {
+    switch (mode) {
+        case MPG_MODE_MIXED: return {MPG_F32, MPG_F64, MPG_F32, MPG_F32, false};
+        case MPG_MODE_MIXED_HALF: return {MPG_F32, MPG_F64, MPG_F32, MPG_F16, false};
+        case MPG_MODE_BASELINE: return {MPG_F64, MPG_F64, MPG_F64, MPG_F64, false};
+        case MPG_MODE_SINGLE_PREC: return {MPG_F64, MPG_F64, MPG_F32, MPG_F64, false};
+        case MPG_MODE_SINGLE: return {MPG_F32, MPG_F32, MPG_F32, MPG_F32, true};
+        default: throw std::invalid_argument("unknown mode");
+    }
+}
+size_t dsize(int t) { return t == MPG_F64 ? 8 : t == MPG_F32 ? 4 : 2; }
+
+}  // namespace
+
+struct FusedEngine::Impl {
+    mpg_ctx_t ctx = nullptr;
+    mpg_solve_args args{};
+    Comm* comm = nullptr;
+    ModeTypes ty{};
+    int n = 0, n_ext = 0, m = 0, orth = 0;
+    int64_t nnz = 0;
+    DevMem rowptr, col, val64, val_outer_own, val_inner_own, diag, b, x, tmp_t, tmp_p, scal;
+    const void* val_outer = nullptr;
+    const void* val_inner = nullptr;
+    mpg_csr_t csr = nullptr;
+    mpg_arnoldi_t arn = nullptr;
+    double* report_host = nullptr;  // pinned
+    int report_len = 0;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    bool use_graph = true;
+    std::vector<int32_t> rowptr_host;
+
+    ~Impl() {
+        if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+        if (graph) (void)hipGraphDestroy(graph);
+        if (arn) mpg_arnoldi_destroy(arn);
+        if (csr) mpg_csr_destroy(csr);
+        if (report_host) (void)hipHostFree(report_host);
+    }
+    hipStream_t stream() const { return static_cast<hipStream_t>(mpg_ctx_stream(ctx)); }
+
+    // cast-copy between device arrays of runtime dtypes
+    void cast(const void* src, int st, void* dst, int dt, int64_t count) {
+        if (count == 0) return;
+        if (st == MPG_F64 && dt == MPG_F64) check(mpg_copy_f64f64(ctx, count, (const double*)src, (double*)dst), "copy", ctx);
+        else if (st == MPG_F64 && dt == MPG_F32) check(mpg_copy_f64f32(ctx, count, (const double*)src, (float*)dst), "copy", ctx);
+        else if (st == MPG_F32 && dt == MPG_F64) check(mpg_copy_f32f64(ctx, count, (const float*)src, (double*)dst), "copy", ctx);
+        else if (st == MPG_F32 && dt == MPG_F32) check(mpg_copy_f32f32(ctx, count, (const float*)src, (float*)dst), "copy", ctx);
+        else if (st == MPG_F64 && dt == MPG_F16) check(mpg_copy_f64f16(ctx, count, (const double*)src, (uint16_t*)dst), "copy", ctx);
+        else throw std::invalid_argument("unsupported cast");
+    }
+    // fp64 accumulator of <u, v> over local rows, summed across ranks
+    double dot_acc(const void* u, const void* v, int t, int64_t count) {
+        double* acc = scal.as<double>();
+        if (t == MPG_F64) check(mpg_dot_acc_f64(ctx, count, (const double*)u, (const double*)v, acc), "dot", ctx);
+        else check(mpg_dot_acc_f32(ctx, count, (const float*)u, (const float*)v, acc), "dot", ctx);
+        if (comm) comm->allreduce_sum(acc, 1, stream());
+        double h = 0;
+        check(mpg_memcpy_d2h(ctx, &h, acc, sizeof h), "d2h", ctx);
+        return h;
+    }
+    // nrm2 rounded to the vector's precision
+    double nrm2(const void* u, int t, int64_t count) {
+        const double s = std::sqrt(dot_acc(u, u, t, count));
+        return t == MPG_F64 ? s : (double)(float)s;
+    }
+};
+
+FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int n_ext) : p_(new Impl) {
+    auto t0 = clk::now();
+    Impl& I = *p_;
+    I.ctx = ctx;
+    I.args = a;
+    I.comm = comm;
+    I.ty = types_for(a.mode);
+    I.n = a.n;
+    I.n_ext = n_ext < 0 ? a.n : n_ext;
+    I.m = a.rlen;
+    I.orth = a.orth;
+    I.nnz = a.nnz;
+    if (a.prec != MPG_PREC_IDENTITY && a.prec != MPG_PREC_JACOBI)
+        throw std::invalid_argument("ILU / ILU-Jacobi preconditioners are not implemented on the Hip backend yet");
+    if (a.orthloss && a.rtol != 0)
+        throw std::invalid_argument("the LostOrthogonality restart needs v_{k+1} on the host: use engine=surface");
+    if (a.rowptr[a.n] != a.nnz) throw std::invalid_argument("rowptr[n] != nnz");
+
+    // structure + analysed schedule
+    const size_t n1 = (size_t)I.n + 1, nz = (size_t)I.nnz;
+    I.rowptr = DevMem(ctx, n1 * 4);
+    I.col = DevMem(ctx, std::max<size_t>(nz, 1) * 4);
+    check(mpg_memcpy_h2d(ctx, I.rowptr.p, a.rowptr, n1 * 4), "h2d", ctx);
+    if (nz) check(mpg_memcpy_h2d(ctx, I.col.p, a.col, nz * 4), "h2d", ctx);
+    check(mpg_csr_create(ctx, I.n, I.n_ext, I.nnz, a.rowptr, I.rowptr.as<int32_t>(), I.col.as<int32_t>(), &I.csr),
+          "mpg_csr_create", ctx);
+
+    // values: the original fp64 A, the residual matrix (outer type) and the
+    // Arnoldi matrix (inner type) — gmres_perf_test.cpp:66 (baseline solves with
+    // double(float(A))) and :136 (mixed: fp64 residual, fp32 Arnoldi)
+    I.val64 = DevMem(ctx, std::max<size_t>(nz, 1) * 8);
+    if (nz) check(mpg_memcpy_h2d(ctx, I.val64.p, a.val, nz * 8), "h2d", ctx);
+    const ModeTypes& ty = I.ty;
+    const bool rounded_outer = a.mode != MPG_MODE_MIXED && a.mode != MPG_MODE_MIXED_HALF;
+    if (rounded_outer) {
+        DevMem f32(ctx, std::max<size_t>(nz, 1) * 4);
+        I.cast(I.val64.p, MPG_F64, f32.p, MPG_F32, (int64_t)nz);
+        if (ty.X == MPG_F64) {
+            I.val_outer_own = DevMem(ctx, std::max<size_t>(nz, 1) * 8);
+            I.cast(f32.p, MPG_F32, I.val_outer_own.p, MPG_F64, (int64_t)nz);
+        } else {
+            I.val_outer_own = std::move(f32);
+        }
+        I.val_outer = I.val_outer_own.p;
+        I.val_inner = I.val_outer;  // the same matrix drives the Arnoldi cycle
+    } else {
+        I.val_outer = I.val64.p;
+        I.val_inner_own = DevMem(ctx, std::max<size_t>(nz, 1) * dsize(ty.VI));
+        I.cast(I.val64.p, MPG_F64, I.val_inner_own.p, ty.VI, (int64_t)nz);
+        I.val_inner = I.val_inner_own.p;
+    }
+
+    // Jacobi<P>(A): fp64 original A for P = double (baseline), else the A
+    // converted to float (types.hpp:393-431 on SparseMatrix<P>)
+    if (a.prec == MPG_PREC_JACOBI) {
+        I.diag = DevMem(ctx, (size_t)I.n * dsize(ty.P) + 16);
+        if (ty.P == MPG_F64) {
+            check(mpg_jacobi_setup_f64(ctx, I.csr, I.val64.as<double>(), I.diag.as<double>()), "jacobi", ctx);
+        } else {
+            DevMem f32(ctx, std::max<size_t>(nz, 1) * 4);
+            I.cast(I.val64.p, MPG_F64, f32.p, MPG_F32, (int64_t)nz);
+            check(mpg_jacobi_setup_f32(ctx, I.csr, f32.as<float>(), I.diag.as<float>()), "jacobi", ctx);
+            check(mpg_ctx_sync(ctx), "sync", ctx);
+        }
+        if (comm && comm->size() > 1)
+            throw std::invalid_argument("Jacobi on a row-partitioned matrix needs a global ||A||_inf (not yet)");
+    }
+
+    // b (outer type), x = 0 (outer type, with halo tail)
+    I.scal = DevMem(ctx, 64);
+    DevMem b64(ctx, (size_t)I.n * 8 + 8);
+    check(mpg_memcpy_h2d(ctx, b64.p, a.b, (size_t)I.n * 8), "h2d", ctx);
+    if (ty.X == MPG_F64) {
+        I.b = std::move(b64);
+    } else {
+        I.b = DevMem(ctx, (size_t)I.n * 4 + 8);
+        I.cast(b64.p, MPG_F64, I.b.p, MPG_F32, I.n);
+    }
+    I.x = DevMem(ctx, (size_t)I.n_ext * dsize(ty.X) + 64);
+
+    // one-time norms of the drivers (gmres.cpp:51-58, 162-168)
+    b_norm = I.nrm2(I.b.p, ty.X, I.n);
+    {
+        I.tmp_t = DevMem(ctx, (size_t)I.n * dsize(ty.T) + 64);
+        I.cast(I.b.p, ty.X, I.tmp_t.p, ty.T, I.n);  // copy(b, w)
+        if (ty.P != ty.T) {                             // typesafe_apply
+            I.tmp_p = DevMem(ctx, (size_t)I.n * dsize(ty.P) + 64);
+            I.cast(I.tmp_t.p, ty.T, I.tmp_p.p, ty.P, I.n);
+        }
+        void* wp = ty.P != ty.T ? I.tmp_p.p : I.tmp_t.p;
+        if (a.prec == MPG_PREC_JACOBI) {
+            if (ty.P == MPG_F64)
+                check(mpg_gdmv_f64(ctx, I.n, 1.0, I.diag.as<double>(), (double*)wp, 0.0, (double*)wp), "gdmv", ctx);
+            else
+                check(mpg_gdmv_f32(ctx, I.n, 1.0f, I.diag.as<float>(), (float*)wp, 0.0f, (float*)wp), "gdmv", ctx);
+        }
+        if (ty.P != ty.T) I.cast(I.tmp_p.p, ty.P, I.tmp_t.p, ty.T, I.n);
+        minvb_norm = I.nrm2(I.tmp_t.p, ty.T, I.n);
+    }
+    // ||A||_F of the matrix the driver was given (A_single in mixed mode)
+    {
+        const bool mixed = !rounded_outer;
+        const void* av = mixed ? nullptr : I.val_outer;
+        int at = ty.X;
+        DevMem f32;
+        if (mixed) {  // A_single values (fp32) even in mixed-half mode
+            f32 = DevMem(ctx, std::max<size_t>(nz, 1) * 4);
+            I.cast(I.val64.p, MPG_F64, f32.p, MPG_F32, (int64_t)nz);
+            av = f32.p;
+            at = MPG_F32;
+        }
+        a_norm = I.nrm2(av, at, (int64_t)nz);
+    }
+
+    mpg_arnoldi_desc d{};
+    d.n = I.n;
+    d.n_ext = I.n_ext;
+    d.m = I.m;
+    d.orth = I.orth;
+    d.vec_type = ty.T;
+    d.outer_type = ty.X;
+    d.prec_type = ty.P;
+    d.inner_val = ty.VI;
+    d.jacobi = a.prec == MPG_PREC_JACOBI;
+    d.A = I.csr;
+    d.val_outer = I.val_outer;
+    d.val_inner = I.val_inner;
+    d.diag = d.jacobi ? I.diag.p : nullptr;
+    d.b = I.b.p;
+    d.x = I.x.p;
+    check(mpg_arnoldi_create(ctx, &d, &I.arn), "mpg_arnoldi_create", ctx);
+    I.report_len = mpg_arnoldi_report_len(I.arn);
+    hipck(hipHostMalloc((void**)&I.report_host, (size_t)I.report_len * sizeof(double), 0), "hipHostMalloc");
+
+    // convergence strategy (gmres_perf_test.cpp:185-196)
+    const size_t mm = (size_t)a.rlen, mr = (size_t)a.max_restarts;
+    if (a.rtol == 0) conv_ = std::make_unique<Convergence<double, void>>(a.tol, mm, mr);
+    else if (a.repeat_iter) conv_ = std::make_unique<RepeatIteration_Convergence<double, void>>(a.tol, a.rtol, mm, mr);
+    else conv_ = std::make_unique<RelPrecRes_Convergence<double, void>>(a.tol, a.rtol, mm, mr);
+    conv_->total_iters = 0;
+
+    const char* env = std::getenv("MPG_NO_GRAPH");
+    I.use_graph = !(env && *env == '1');
+    check(mpg_ctx_sync(ctx), "sync", ctx);
+    setup_seconds = std::chrono::duration<double>(clk::now() - t0).count();
+    prologue();
+    read_report(4);
+}
+
+FusedEngine::~FusedEngine() = default;
+
+void FusedEngine::sync() { check(mpg_ctx_sync(p_->ctx), "sync", p_->ctx); }
+
+void FusedEngine::prologue() {
+    Impl& I = *p_;
+    if (I.comm) I.comm->halo(I.x.p, (int)dsize(I.ty.X), I.stream());
+    check(mpg_arnoldi_prologue(I.arn), "prologue", I.ctx);
+    check(mpg_arnoldi_reduce(I.arn, 3), "reduce", I.ctx);
+    if (I.comm) I.comm->allreduce_sum(mpg_arnoldi_sums_dev(I.arn), 3, I.stream());
+    check(mpg_arnoldi_prologue_finish(I.arn), "prologue_finish", I.ctx);
+}
+
+void FusedEngine::step(int k) {
+    Impl& I = *p_;
+    auto reduce = [&](int nc) {
+        check(mpg_arnoldi_reduce(I.arn, nc), "reduce", I.ctx);
+        if (I.comm) I.comm->allreduce_sum(mpg_arnoldi_sums_dev(I.arn), nc, I.stream());
+    };
+    if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
+    check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
+    if (I.orth == MPG_ORTH_MGS) {
+        reduce(1);
+        for (int j = 0; j <= k; ++j) {
+            check(mpg_arnoldi_mgs(I.arn, k, j), "mgs", I.ctx);
+            reduce(1);
+        }
+    } else {
+        reduce(k + 1);
+        if (I.orth == MPG_ORTH_CGSR) {
+            check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
+            reduce(k + 1);
+            check(mpg_arnoldi_cgs(I.arn, k, 1), "cgs", I.ctx);
+        } else {
+            check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
+        }
+        reduce(1);
+    }
+    check(mpg_arnoldi_givens(I.arn, k), "givens", I.ctx);
+}
+
+void FusedEngine::update(int k) { check(mpg_arnoldi_update(p_->arn, k), "update", p_->ctx); }
+
+void FusedEngine::read_report(int count) {
+    Impl& I = *p_;
+    hipck(hipMemcpyAsync(I.report_host, mpg_arnoldi_report_dev(I.arn), (size_t)count * sizeof(double),
+                         hipMemcpyDeviceToHost, I.stream()),
+          "report d2h");
+    hipck(hipStreamSynchronize(I.stream()), "report sync");
+}
+
+// steps 0..m-1, solution update with k = m, next residual prologue
+void FusedEngine::cycle_program() {
+    Impl& I = *p_;
+    for (int k = 0; k < I.m; ++k) step(k);
+    update(I.m);
+    prologue();
+}
+
+// check_initial on the report of the last prologue (gmres.cpp:171-190)
+bool FusedEngine::check_start(int64_t i) {
+    Impl& I = *p_;
+    const double* r = I.report_host;
+    double r_norm = r[0], beta = r[1], x_norm = r[2];
+    double normalization;
+    if (I.ty.single_scalars) normalization = (double)((float)b_norm + (float)a_norm * (float)x_norm);
+    else normalization = b_norm + a_norm * x_norm;
+    cycles.push_back(CycleRecord{r_norm, normalization, beta, minvb_norm});
+    restarts = i;
+    switch (conv_->check_initial(r_norm, normalization, beta, minvb_norm)) {
+        case iteration_converged: {
+            const double rel = I.ty.single_scalars ? (double)(float)((float)beta / (float)minvb_norm)
+                             : I.ty.T == MPG_F64 ? beta / minvb_norm
+                                                 : (double)((float)beta / minvb_norm);
+            out() << "Found solution with rel prec res norm = " << rel << " when k = 0 and i = " << i << std::endl;
+            out() << "  total iterations = " << conv_->total_iterations() << std::endl;
+            status = MPG_RESULT_CONVERGED;
+            return true;
+        }
+        case iteration_aborted:
+            out() << "Aborting after " << conv_->total_iterations() << " iterations" << std::endl;
+            status = MPG_RESULT_ABORTED;
+            return true;
+        default: return false;
+    }
+}
+
+int FusedEngine::run(int max_cycles, bool& done) {
+    Impl& I = *p_;
+    done = false;
+    int ran = 0;
+    const bool stepwise = conv_->needs_arnoldi_residual();
+    for (; ran < max_cycles; ++ran) {
+        const int64_t i = (int64_t)cycles.size();
+        if (check_start(i)) {
+            done = true;
+            return ran;
+        }
+        if (!stepwise) {
+            if (I.use_graph) {
+                if (!I.graph_exec) {
+                    hipck(hipStreamBeginCapture(I.stream(), hipStreamCaptureModeThreadLocal), "begin capture");
+                    cycle_program();
+                    hipck(hipStreamEndCapture(I.stream(), &I.graph), "end capture");
+                    hipck(hipGraphInstantiate(&I.graph_exec, I.graph, nullptr, nullptr, 0), "graph instantiate");
+                }
+                hipck(hipGraphLaunch(I.graph_exec, I.stream()), "graph launch");
+            } else {
+                cycle_program();
+            }
+            read_report(I.report_len);
+            for (int k = 0; k < I.m; ++k) {
+                const double res = I.report_host[4 + k];
+                step_res.push_back(res);
+                step_cycle.push_back((int)i);
+                conv_->check((size_t)k + 1, res, minvb_norm);  // base strategy: counts, restarts at m
+            }
+            continue;
+        }
+        // adaptive restart strategies: one host read of |s(k+1)| per step
+        for (int k = 0;; ++k) {
+            step(k);
+            read_report(4 + k + 1);
+            const double res = I.report_host[4 + k];
+            step_res.push_back(res);
+            step_cycle.push_back((int)i);
+            const iteration_action act = conv_->check((size_t)k + 1, res, minvb_norm);
+            if (act == iteration_converged) {
+                update(k + 1);
+                out() << "Found solution with rel prec res norm = " << res / minvb_norm << " when k = " << k + 1
+                      << " and i = " << i << std::endl;
+                out() << "  total iterations = " << conv_->total_iterations() << std::endl;
+                status = MPG_RESULT_CONVERGED;
+                inner_k = k + 1;
+                done = true;
+                sync();
+                return ran + 1;
+            }
+            if (act == iteration_aborted) {
+                out() << "Aborting after " << conv_->total_iterations() << " iterations" << std::endl;
+                status = MPG_RESULT_ABORTED;
+                done = true;
+                return ran + 1;
+            }
+            if (act == iteration_restart) {
+                update(k + 1);
+                prologue();
+                read_report(4);
+                break;
+            }
+        }
+    }
+    return ran;
+}
+
+void FusedEngine::finish_report(mpg_solve_result* r) {
+    Impl& I = *p_;
+    const int n = I.n;
+    // x and b widened to fp64 (DoBaselineProblem copies x_type / b_type to double)
+    DevMem x64(I.ctx, (size_t)I.n_ext * 8 + 8), r64(I.ctx, (size_t)n * 8 + 8), b64(I.ctx, (size_t)n * 8 + 8);
+    I.cast(I.x.p, I.ty.X, x64.p, MPG_F64, n);
+    I.cast(I.b.p, I.ty.X, b64.p, MPG_F64, n);
+    if (r->x_out) check(mpg_memcpy_d2h(I.ctx, r->x_out, x64.p, (size_t)n * 8), "d2h", I.ctx);
+    if (I.comm) I.comm->halo(x64.p, 8, I.stream());
+    check(mpg_memcpy_d2d(I.ctx, r64.p, b64.p, (size_t)n * 8), "d2d", I.ctx);
+    check(mpg_csr_spmv_f64(I.ctx, I.csr, -1.0, I.val64.as<double>(), x64.as<double>(), 1.0, r64.as<double>()), "spmv",
+          I.ctx);
+    r->res_norm = std::sqrt(I.dot_acc(r64.p, r64.p, MPG_F64, n));
+    if (I.args.x_true) {
+        DevMem xt(I.ctx, (size_t)n * 8 + 8);
+        check(mpg_memcpy_h2d(I.ctx, xt.p, I.args.x_true, (size_t)n * 8), "h2d", I.ctx);
+        check(mpg_axpy_f64(I.ctx, n, -1.0, xt.as<double>(), x64.as<double>()), "axpy", I.ctx);
+        r->err_norm = std::sqrt(I.dot_acc(x64.p, x64.p, MPG_F64, n));
+    }
+}
+
+double FusedEngine::phase_bytes(int which) const {
+    const Impl& I = *p_;
+    const double n = I.n, z = (double)I.nnz, sT = (double)dsize(I.ty.T), sX = (double)dsize(I.ty.X);
+    const double sV = (double)dsize(I.ty.VI), sP = (double)dsize(I.ty.P);
+    const double jac = I.args.prec == MPG_PREC_JACOBI ? 1.0 : 0.0;
+    if (which == 0) {
+        // mean over k of: CSR (values + int32 columns + row pointers), gathered
+        // v_k (read once), w and V(:,k) written, dot partners V(:,0..k-1)
+        double dots = 0;
+        for (int k = 0; k < I.m; ++k) dots += (I.orth == MPG_ORTH_MGS ? (k > 0 ? 1 : 0) : k);
+        dots /= I.m;
+        return z * (sV + 4) + (n + 1) * 4 + 3 * n * sT + dots * n * sT + jac * n * sP;
+    }
+    if (which == 1) return z * (sX + 4) + (n + 1) * 4 + 3 * n * sX + n * sT + jac * n * sP;
+    // CGS update at mean k: read V(:,0..k), read + write w
+    return ((I.m - 1) / 2.0 + 1) * n * sT + 2 * n * sT;
+}
+
+double FusedEngine::time_phase(int which, int reps) {
+    Impl& I = *p_;
+    hipEvent_t e0, e1;
+    hipck(hipEventCreate(&e0), "event");
+    hipck(hipEventCreate(&e1), "event");
+    float total_ms = 0;
+    int launches = 0;
+    const int ks = which == 1 ? 1 : I.m;
+    for (int k = 0; k < ks; ++k) {
+        hipck(hipEventRecord(e0, I.stream()), "record");
+        for (int r = 0; r < reps; ++r) {
+            if (which == 0) check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
+            else if (which == 1) check(mpg_arnoldi_prologue(I.arn), "prologue", I.ctx);
+            else check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
+        }
+        hipck(hipEventRecord(e1, I.stream()), "record");
+        hipck(hipEventSynchronize(e1), "sync");
+        float ms = 0;
+        hipck(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+        total_ms += ms;
+        launches += reps;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return total_ms / launches;
+}
+
+// ---------------------------------------------------------------- mpg_solve (fused)
+int solve_fused(const mpg_solve_args& a, mpg_solve_result* r) {
+    mpg_ctx_t ctx = current_ctx();
+    const char* banner = a.mode == MPG_MODE_MIXED || a.mode == MPG_MODE_MIXED_HALF ? "Doing Mixed Precision test"
+                                                                                     : "Doing Baseline test";
+    out() << banner << std::endl;
+    FusedEngine e(ctx, a);
+    auto t1 = clk::now();
+    bool done = false;
+    while (!done) e.run(1 << 20, done);
+    e.sync();
+    const double gmres_s = std::chrono::duration<double>(clk::now() - t1).count();
+    r->status = e.status;
+    r->restarts = e.restarts;
+    r->inner_k = e.inner_k;
+    r->total_iters = (int64_t)e.total_iters();
+    r->minvb_norm = e.minvb_norm;
+    r->n_cycles = (int64_t)e.cycles.size();
+    for (size_t c = 0; c < e.cycles.size() && (int64_t)c < r->cycle_cap; ++c) {
+        if (r->cyc_r_norm) r->cyc_r_norm[c] = e.cycles[c].r_norm;
+        if (r->cyc_normalization) r->cyc_normalization[c] = e.cycles[c].normalization;
+        if (r->cyc_beta) r->cyc_beta[c] = e.cycles[c].beta;
+    }
+    r->n_steps = (int64_t)e.step_res.size();
+    for (size_t s = 0; s < e.step_res.size() && (int64_t)s < r->step_cap; ++s) {
+        if (r->step_res) r->step_res[s] = e.step_res[s];
+        if (r->step_cycle) r->step_cycle[s] = e.step_cycle[s];
+    }
+    r->setup_seconds = e.setup_seconds;
+    r->gmres_seconds = gmres_s;
+    e.finish_report(r);
+    out() << "  ilu took " << (float)r->setup_seconds << "s; gmres took " << (float)gmres_s << "s" << std::endl;
+    out() << "  resNorm = " << r->res_norm << "; errNorm = " << r->err_norm << std::endl;
+    return 0;
+}
+
 }  // namespace mpg
+
+// ---------------------------------------------------------------- engine C-ABI
+struct mpg_engine {
+    mpg_ctx_t ctx = nullptr;
+    std::unique_ptr<mpg::FusedEngine> eng;
+};
+
+extern "C" {
+
+int mpg_engine_create(const mpg_solve_args* a, mpg_engine_t* out, char* err, int errlen) {
+    if (!a || !out) return MPG_ERR_ARG;
+    *out = nullptr;
+    auto* e = new mpg_engine();
+    try {
+        mpg::set_quiet(!a->verbose);
+        mpg::check(mpg_ctx_create(a->device, &e->ctx), "mpg_ctx_create");
+        mpg::ScopedContext scope(e->ctx);
+        e->eng = std::make_unique<mpg::FusedEngine>(e->ctx, *a);
+    } catch (const std::exception& ex) {
+        if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", ex.what());
+        mpg_engine_destroy(e);
+        return MPG_ERR_ARG;
+    }
+    *out = e;
+    return MPG_OK;
+}
+
+int mpg_engine_run(mpg_engine_t e, int max_cycles, int* done) {
+    if (!e || !e->eng) return MPG_ERR_ARG;
+    try {
+        mpg::ScopedContext scope(e->ctx);
+        bool d = false;
+        int ran = e->eng->run(max_cycles, d);
+        if (done) *done = d ? 1 : 0;
+        return ran;
+    } catch (const std::exception&) {
+        return MPG_ERR_HIP;
+    }
+}
+
+int mpg_engine_sync(mpg_engine_t e) {
+    if (!e) return MPG_ERR_ARG;
+    return mpg_ctx_sync(e->ctx);
+}
+
+int64_t mpg_engine_total_iters(mpg_engine_t e) { return e && e->eng ? (int64_t)e->eng->total_iters() : -1; }
+
+int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms) {
+    if (!e || !e->eng || !avg_ms || reps < 1 || which < 0 || which > 2) return MPG_ERR_ARG;
+    try {
+        mpg::ScopedContext scope(e->ctx);
+        *avg_ms = e->eng->time_phase(which, reps);
+        return MPG_OK;
+    } catch (const std::exception&) {
+        return MPG_ERR_HIP;
+    }
+}
+
+double mpg_engine_phase_bytes(mpg_engine_t e, int which) {
+    return e && e->eng ? e->eng->phase_bytes(which) : 0.0;
+}
+
+int mpg_engine_destroy(mpg_engine_t e) {
+    if (!e) return MPG_OK;
+    if (e->ctx) {
+        {
+            mpg::ScopedContext scope(e->ctx);
+            e->eng.reset();
+        }
+        mpg_ctx_destroy(e->ctx);
+    }
+    delete e;
+    return MPG_OK;
+}
+
+}  // extern "C"

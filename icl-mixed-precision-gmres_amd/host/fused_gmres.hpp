@@ -1,11 +1,100 @@
-// Fused Arnoldi engine (see fused_gmres.cpp).
+// Fused Arnoldi engine: restarted GMRES(m) on one GPU (or one rank of a
+// row-partitioned solve) with one host synchronisation per restart cycle.
+//
+// Same outer control flow as the drivers in gmres_impl.hpp (and the
+// reference gmres.cpp:24-245): check_initial on the true residual at every
+// restart, m Arnoldi steps, solution update. The cycle itself is the phase
+// program of include/mpgmres/arnoldi.h, captured once into a hipGraph and
+// replayed every cycle (steps 0..m-1, the solution update and the next
+// residual prologue); the host reads back one small report block per cycle
+// (r_norm, beta, ||x||, |s(k+1)| for every step). Strategies that look at
+// |s(k+1)| inside a cycle run the same program step by step instead.
 #ifndef MPGMRES_FUSED_GMRES_HPP
 #define MPGMRES_FUSED_GMRES_HPP
 
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "IterUtil.hpp"
+#include "mpgmres/arnoldi.h"
+#include "mpgmres/capi.h"
 #include "mpgmres/solve.h"
 
 namespace mpg {
+
+// Communication seam of the row-partitioned solve: a single-GPU engine has
+// no communicator; a multi-GPU rank supplies one (see comm.hpp).
+class Comm {
+public:
+    virtual ~Comm() {}
+    virtual int size() const = 0;
+    virtual int rank() const = 0;
+    // in-place sum of `count` doubles across ranks (bit-identical on every rank)
+    virtual void allreduce_sum(double* dev, int count, hipStream_t s) = 0;
+    // fill the halo tail [n, n_ext) of a vector of `elem_bytes` elements
+    virtual void halo(void* dev_vec, int elem_bytes, hipStream_t s) = 0;
+};
+
+// RAII device buffer through the C-ABI allocator
+struct DevMem {
+    mpg_ctx_t ctx = nullptr;
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevMem() = default;
+    DevMem(mpg_ctx_t c, size_t b);
+    ~DevMem();
+    DevMem(const DevMem&) = delete;
+    DevMem& operator=(const DevMem&) = delete;
+    DevMem(DevMem&& o) noexcept { *this = std::move(o); }
+    DevMem& operator=(DevMem&& o) noexcept;
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+class FusedEngine {
+public:
+    // `rows`/`halo` describe the local row block of a partitioned matrix
+    // (global columns already remapped to [0, n_ext)); a single GPU passes the
+    // whole matrix and no communicator.
+    FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& args, Comm* comm = nullptr, int n_ext = -1);
+    ~FusedEngine();
+
+    // Advance the solve by up to max_cycles outer iterations; returns the
+    // number run. `done` is set on convergence or abort.
+    int run(int max_cycles, bool& done);
+    void finish_report(mpg_solve_result* r);  // resNorm/errNorm + x with the original fp64 A
+
+    size_t total_iters() const { return conv_->total_iterations(); }
+    double time_phase(int which, int reps);
+    double phase_bytes(int which) const;
+    void sync();
+
+    // history (per restart / per step)
+    std::vector<CycleRecord> cycles;
+    std::vector<double> step_res;
+    std::vector<int> step_cycle;
+    int status = 0;          // MPG_RESULT_*
+    int64_t restarts = 0;
+    int64_t inner_k = 0;
+    double minvb_norm = 0, b_norm = 0, a_norm = 0;
+    double setup_seconds = 0;
+
+private:
+    struct Impl;
+    std::unique_ptr<Impl> p_;
+    std::unique_ptr<Convergence<double, void>> conv_;
+    void prologue();
+    void step(int k);
+    void update(int k);
+    void read_report(int count);
+    void cycle_program();
+    bool check_start(int64_t i);
+};
+
 int solve_fused(const mpg_solve_args& args, mpg_solve_result* result);
+
 }  // namespace mpg
 
 #endif  // MPGMRES_FUSED_GMRES_HPP

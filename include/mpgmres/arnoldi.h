@@ -1,0 +1,99 @@
+/*
+ * mpgmres fused-Arnoldi C-ABI (libmpgmres_hip.so) — the performance form of
+ * one restarted GMRES(m) cycle on gfx950, with no host synchronisation
+ * inside a cycle.
+ *
+ * Replaces, for one restart cycle of gmres_singleUpdate / gmres_baseline
+ * (gmres.cpp:160-242, 51-130), the per-operator calls of the reference
+ * (spmv, M->apply, orth.add_vector, rot/rotg/rot, fence + s.access,
+ * solution_update) by a short program of fused phase kernels:
+ *
+ *   prologue   r = b - A x (outer precision), w = M(T(r)), partial sums of
+ *              ||T(r)||^2, ||w||^2, ||x||^2            (types.hpp:230-448, gmres.cpp:171-180)
+ *   finish     r_norm, beta, x_norm -> report; 1/beta; s = [beta, 0, ...]
+ *   spmv(k)    v_k = w_prev * (1/h_{k,k-1}) formed on the fly (written to V
+ *              for local rows), w = M(A v_k), and per-workgroup partial dots
+ *              <v_j, w> for j <= k (CGS / CGSR) or j = 0 (MGS)
+ *              (Orthogonalization.hpp:56-59, 83-87, 99-105)
+ *   cgs(k,p)   coefficients c = T(sums); w -= V c; partials of ||w||^2 (last
+ *              pass) or of <v_j, w> (first CGSR pass)
+ *   mgs(k,j)   h_jk = T(sum); w -= h_jk v_j; partial <v_{j+1}, w> or ||w||^2
+ *   givens(k)  h_{k+1,k} = ||w||; 1/h for the next step; rotations on column
+ *              k, rotg, rotation of s; |s(k+1)| -> report   (gmres.cpp:217-226)
+ *   update(k)  y = H(0:k,0:k)^-1 s(0:k); x += V(:,0:k) y  (gmres.cpp:276-290)
+ *
+ * Every global reduction is two-stage: phase kernels write per-workgroup
+ * fp64 partials, mpg_arnoldi_reduce sums them in a fixed order into
+ * `sums` (fp64). A row-partitioned multi-GPU caller all-reduces `sums`
+ * across ranks between the two (mpg_arnoldi_sums_dev), and exchanges the
+ * halo entries of w_prev / x (mpg_arnoldi_halo_*), before the consumers
+ * read them — every rank then holds bit-identical scalars and takes the same
+ * decisions.
+ */
+#ifndef MPGMRES_ARNOLDI_H
+#define MPGMRES_ARNOLDI_H
+
+#include <stdint.h>
+
+#include "mpgmres/capi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum { MPG_F64 = 0, MPG_F32 = 1, MPG_F16 = 2 } mpg_dtype_t;
+
+typedef struct mpg_arnoldi* mpg_arnoldi_t;
+
+typedef struct {
+    int32_t n;             /* local rows */
+    int32_t n_ext;         /* local rows + halo entries (== n on one GPU) */
+    int32_t m;             /* restart length */
+    int32_t orth;          /* 0 CGS, 1 MGS, 2 CGSR(2) — mpg_orth_t */
+    int32_t vec_type;      /* T: Krylov basis, w, H, Givens (MPG_F64 | MPG_F32) */
+    int32_t outer_type;    /* X: x, b, residual (MPG_F64 | MPG_F32) */
+    int32_t prec_type;     /* P: preconditioner arithmetic (MPG_F64 | MPG_F32) */
+    int32_t inner_val;     /* value type of the Arnoldi SpMV (MPG_F64 | MPG_F32 | MPG_F16) */
+    int32_t jacobi;        /* 1: w = d∘w (gdmv), 0: identity */
+    mpg_csr_t A;           /* analysed local CSR, columns in [0, n_ext) */
+    const void* val_outer; /* residual values, outer_type */
+    const void* val_inner; /* Arnoldi values, inner_val */
+    const void* diag;      /* Jacobi inverse diagonal (prec_type) or NULL */
+    const void* b;         /* outer_type, n */
+    void* x;               /* outer_type, n_ext (halo tail filled by the caller) */
+} mpg_arnoldi_desc;
+
+/* Allocates the basis V (n x (m+1), leading dimension padded to 256 B),
+ * H, Givens state, two w buffers (n_ext), partials and the report block. */
+int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_t* out);
+int mpg_arnoldi_destroy(mpg_arnoldi_t a);
+
+int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
+int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);
+int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k);           /* partials: k+1 (CGS/CGSR) or 1 (MGS) */
+int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass);  /* pass 0: h; pass 1: CGSR correction */
+int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j);
+int mpg_arnoldi_givens(mpg_arnoldi_t a, int k);
+int mpg_arnoldi_update(mpg_arnoldi_t a, int k);
+/* sums[c] = sum over workgroups of partial column c, c < ncols */
+int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols);
+
+/* Device pointers for a multi-GPU caller. */
+double* mpg_arnoldi_sums_dev(mpg_arnoldi_t a);          /* fp64 [m + 4] */
+void* mpg_arnoldi_wprev_dev(mpg_arnoldi_t a, int k);    /* input vector of step k, n_ext of T */
+int mpg_arnoldi_vec_bytes(mpg_arnoldi_t a);             /* sizeof(T) */
+/* report block (fp64, device): [0] r_norm [1] beta [2] x_norm [3] inv_beta
+ * [4 + k] |s(k+1)| after step k */
+const double* mpg_arnoldi_report_dev(mpg_arnoldi_t a);
+int mpg_arnoldi_report_len(mpg_arnoldi_t a);
+/* The Krylov basis (for tests): V column j of T, ld elements apart */
+const void* mpg_arnoldi_basis_dev(mpg_arnoldi_t a, int64_t* ld);
+const void* mpg_arnoldi_hessenberg_dev(mpg_arnoldi_t a);  /* (m+1) x m, column-major, T */
+
+/* Number of workgroups of the row-block phase kernels (partials per column). */
+int mpg_arnoldi_num_groups(mpg_arnoldi_t a);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPGMRES_ARNOLDI_H */

@@ -77,6 +77,10 @@ int mpg_nrm2_f64(mpg_ctx_t ctx, int64_t n, const double* x, double* result_dev);
 int mpg_nrm2_f32(mpg_ctx_t ctx, int64_t n, const float* x, float* result_dev);
 int mpg_nrm2_f64_host(mpg_ctx_t ctx, int64_t n, const double* x, double* result_host);
 int mpg_nrm2_f32_host(mpg_ctx_t ctx, int64_t n, const float* x, float* result_host);
+/* the unrounded fp64 accumulator of <x, y> (one rank's share of a
+ * distributed dot / squared norm, summed across ranks before rounding) */
+int mpg_dot_acc_f64(mpg_ctx_t ctx, int64_t n, const double* x, const double* y, double* acc_dev);
+int mpg_dot_acc_f32(mpg_ctx_t ctx, int64_t n, const float* x, const float* y, double* acc_dev);
 /* y += alpha*x, alpha on host (kernels_mkl.cpp:118-128) */
 int mpg_axpy_f64(mpg_ctx_t ctx, int64_t n, double alpha, const double* x, double* y);
 int mpg_axpy_f32(mpg_ctx_t ctx, int64_t n, float alpha, const float* x, float* y);

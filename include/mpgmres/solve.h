@@ -37,7 +37,7 @@ typedef enum { MPG_PREC_ILU = 0, MPG_PREC_ILU_JACOBI = 1, MPG_PREC_JACOBI = 2, M
 typedef enum {
     MPG_ENGINE_SURFACE = 0,  /* generic driver over the kernels.hpp operator surface */
     MPG_ENGINE_FUSED = 1     /* fused Arnoldi kernels, device-side Givens, graph-captured cycles */
-} mpg_engine_t;
+} mpg_engine_kind_t;
 
 typedef enum { MPG_RESULT_CONVERGED = 1, MPG_RESULT_ABORTED = 3, MPG_RESULT_ERROR = -1 } mpg_result_status_t;
 
@@ -88,6 +88,26 @@ typedef struct {
 /* HIP path (libmpgmres_host.so). Returns 0 on success (result->status tells
  * converged/aborted), < 0 on error (result->message). */
 int mpg_solve(const mpg_solve_args* args, mpg_solve_result* result);
+
+/* ---- stepped access to the fused engine (benchmarks, multi-GPU ranks) ----
+ * mpg_engine_create uploads the problem, builds the preconditioner, zeroes
+ * x and runs the first residual prologue. mpg_engine_run advances the
+ * restarted solve by up to `max_cycles` outer iterations exactly as
+ * mpg_solve does (check_initial on the host once per cycle, graph-replayed
+ * cycle on the device) and returns the number of cycles run; *done is set
+ * when the solve converged or aborted. All timing is left to the caller. */
+typedef struct mpg_engine* mpg_engine_t;
+int mpg_engine_create(const mpg_solve_args* args, mpg_engine_t* out, char* err, int errlen);
+int mpg_engine_run(mpg_engine_t e, int max_cycles, int* done);
+int mpg_engine_sync(mpg_engine_t e);
+int64_t mpg_engine_total_iters(mpg_engine_t e);
+/* device-event timing of one phase kernel replayed `reps` times on the
+ * engine's stream, back to back (which: 0 = Arnoldi SpMV of step m/2,
+ * 1 = fp64 residual prologue, 2 = CGS update of step m/2) */
+int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms);
+/* algorithmic bytes of one launch of phase `which` */
+double mpg_engine_phase_bytes(mpg_engine_t e, int which);
+int mpg_engine_destroy(mpg_engine_t e);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,278 @@
+"""Per-kernel parity of the gfx950 HIP kernels (through the C-ABI) against
+the CPU oracle (MKL semantics of kernels_mkl.cpp) and an fp64 NumPy
+reference.
+
+Tolerances (stated per kernel): the HIP reductions accumulate in fp64, so
+fp32 results are within ~1 ulp of the exactly rounded value; MKL's fp32
+reductions are not (their error grows with n), hence fp32 comparisons are
+made against the fp64 reference with an ulp bound and against the oracle
+with a looser relative bound. Elementwise kernels are bit-exact.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+F32_EPS = np.finfo(np.float32).eps
+F64_EPS = np.finfo(np.float64).eps
+
+SIZES = [0, 1, 63, 64, 65, 1000, 4097, 1_000_003]
+
+
+def rng(seed=0):
+    return np.random.default_rng(seed)
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("t", ["f64", "f32"])
+def test_dot_nrm2(hip, oracle, n, t):
+    dt = np.float64 if t == "f64" else np.float32
+    g = rng(n)
+    x = g.uniform(-1, 1, n).astype(dt)
+    y = g.uniform(-1, 1, n).astype(dt)
+    dx, dy, out = hip.buf(x), hip.buf(y), hip.buf(2, dt)
+    hip.call(f"mpg_dot_{t}", n, dx.p, dy.p, out.at(0))
+    hip.call(f"mpg_nrm2_{t}", n, dx.p, out.at(1))
+    got = out.get()
+    ref_dot = float(np.dot(x.astype(np.longdouble), y.astype(np.longdouble)))
+    ref_nrm = float(np.sqrt(np.sum(x.astype(np.longdouble) ** 2)))
+    scale = float(np.sum(np.abs(x.astype(np.float64) * y)))
+    if t == "f64":
+        assert abs(got[0] - ref_dot) <= 1e-14 * max(scale, 1e-300) + 1e-300
+        assert abs(got[1] - ref_nrm) <= 1e-14 * max(ref_nrm, 1e-300)
+        if n:
+            assert abs(got[0] - oracle.dot(x, y)) <= 1e-12 * max(scale, 1e-300)
+            assert abs(got[1] - oracle.nrm2(x)) <= 1e-12 * ref_nrm
+    else:
+        # fp64 accumulation, one rounding: within 1 ulp (+ fp64 sum error)
+        assert abs(got[0] - ref_dot) <= F32_EPS * abs(ref_dot) + 1e-13 * scale + 1e-38
+        assert abs(got[1] - ref_nrm) <= F32_EPS * ref_nrm + 1e-38
+        if n:
+            assert abs(got[0] - oracle.dot(x, y)) <= 1e-5 * max(scale, 1e-30)
+            assert abs(got[1] - oracle.nrm2(x)) <= 1e-5 * ref_nrm
+    # host-result variants agree bit for bit with the device-result ones
+    import ctypes as C
+
+    hv = (C.c_double if t == "f64" else C.c_float)()
+    hip.call(f"mpg_dot_{t}_host", n, dx.p, dy.p, C.byref(hv))
+    assert dt(hv.value) == got[0]
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
+def test_blas1_elementwise_bitexact(hip, t):
+    dt = np.float64 if t == "f64" else np.float32
+    n = 100_003
+    g = rng(1)
+    x = g.uniform(-1, 1, n).astype(dt)
+    y = g.uniform(-1, 1, n).astype(dt)
+    a = dt(0.7312)
+    dx, dy, da = hip.buf(x), hip.buf(y), hip.buf(np.array([a], dt))
+    hip.call(f"mpg_axpy_{t}", n, a, dx.p, dy.p)
+    with np.errstate(all="ignore"):
+        exp = (y + a * x).astype(dt)
+    assert np.array_equal(dy.get(), exp)
+    dy2 = hip.buf(y)
+    hip.call(f"mpg_naxpy_dev_{t}", n, da.p, dx.p, dy2.p)
+    assert np.array_equal(dy2.get(), (y - a * x).astype(dt))
+    dy3 = hip.buf(y)
+    hip.call(f"mpg_axpy_dev_{t}", n, da.p, dx.p, dy3.p)
+    assert np.array_equal(dy3.get(), exp)
+    dz = hip.buf(n, dt)
+    hip.call(f"mpg_scal_copy_{t}", n, a, dx.p, dz.p)
+    assert np.array_equal(dz.get(), (a * x).astype(dt))
+    hip.call(f"mpg_scal_recip_copy_dev_{t}", n, da.p, dx.p, dz.p)
+    assert np.array_equal(dz.get(), ((dt(1) / a) * x).astype(dt))
+    hip.call(f"mpg_scal_{t}", n, a, dx.p)
+    assert np.array_equal(dx.get(), (a * x).astype(dt))
+    # gdmv: y = beta*y + alpha*d*x, in place (Jacobi apply)
+    d = g.uniform(0.5, 2, n).astype(dt)
+    dd, dw = hip.buf(d), hip.buf(y)
+    hip.call(f"mpg_gdmv_{t}", n, dt(1), dd.p, dw.p, dt(0), dw.p)
+    assert np.array_equal(dw.get(), (dt(0) * y + dt(1) * d * y).astype(dt))
+
+
+def test_copy_casts_and_fill(hip):
+    n = 5001
+    x = rng(2).normal(size=n) * 1e3
+    dx = hip.buf(x)
+    d32, d64, d16 = hip.buf(n, np.float32), hip.buf(n, np.float64), hip.buf(n, np.uint16)
+    hip.call("mpg_copy_f64f32", n, dx.p, d32.p)
+    assert np.array_equal(d32.get(), x.astype(np.float32))
+    hip.call("mpg_copy_f32f64", n, d32.p, d64.p)
+    assert np.array_equal(d64.get(), x.astype(np.float32).astype(np.float64))
+    hip.call("mpg_copy_f64f16", n, dx.p, d16.p)
+    assert np.array_equal(d16.get().view(np.float16), x.astype(np.float16))
+    # strided fill of a 7 x 5 block with lda 9
+    blk = hip.buf(9 * 5, np.float64)
+    hip.call("mpg_fill_f64", blk.p, 7, 5, 9, 2.5)
+    got = blk.get().reshape(5, 9)
+    assert np.all(got[:, :7] == 2.5) and np.all(got[:, 7:] == 0)
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
+def test_givens(hip, oracle, t):
+    dt = np.float64 if t == "f64" else np.float32
+    cases = [(3.0, 4.0), (-3.0, 4.0), (1e-3, -2.0), (0.0, 0.0), (5.0, 0.0), (0.0, -7.0), (1.5, 1.5)]
+    for a, b in cases:
+        buf = hip.buf(np.array([a, b, 0, 0], dt))
+        hip.call(f"mpg_rotg_{t}", buf.at(0), buf.at(1), buf.at(2), buf.at(3))
+        got = buf.get()
+        ref = oracle.rotg(a, b, dt)
+        tol = 4 * (F64_EPS if t == "f64" else F32_EPS)
+        assert got[1] == 0
+        assert np.allclose(got, ref, rtol=tol, atol=0), (a, b, got, ref)
+    # column rotation: k previous rotations applied to a[0..k]
+    k = 9
+    g = rng(3)
+    col = g.normal(size=k + 1).astype(dt)
+    th = g.uniform(0, 2 * np.pi, k)
+    c, s = np.cos(th).astype(dt), np.sin(th).astype(dt)
+    dcol, dc, ds = hip.buf(col), hip.buf(c), hip.buf(s)
+    hip.call(f"mpg_rot_vec_{t}", k, dcol.p, dc.p, ds.p)
+    exp = col.copy()
+    for j in range(k):
+        a1, a2 = exp[j], exp[j + 1]
+        exp[j] = dt(dt(c[j] * a1) + dt(s[j] * a2))
+        exp[j + 1] = dt(dt(c[j] * a2) - dt(s[j] * a1))
+    assert np.array_equal(dcol.get(), exp)
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
+@pytest.mark.parametrize("rows,cols", [(1_000_000, 31), (100_003, 1), (5000, 40), (31, 31), (7, 3)])
+def test_gemv_panels(hip, oracle, t, rows, cols):
+    dt = np.float64 if t == "f64" else np.float32
+    g = rng(rows + cols)
+    lda = rows + (64 if rows > 64 else 0)
+    Afull = np.zeros((lda, cols), dt, order="F")
+    Afull[:rows] = g.uniform(-1, 1, (rows, cols))
+    A = Afull[:rows]
+    xT = g.uniform(-1, 1, rows).astype(dt)
+    xN = g.uniform(-1, 1, cols).astype(dt)
+    y0 = g.uniform(-1, 1, rows).astype(dt)
+    dA = hip.buf(Afull.ravel(order="F"))
+    dxT, dxN, dyT, dyN = hip.buf(xT), hip.buf(xN), hip.buf(cols, dt), hip.buf(y0)
+    hip.call(f"mpg_gemv_{t}", 1, rows, cols, dt(1), dA.p, lda, dxT.p, dt(0), dyT.p)
+    hip.call(f"mpg_gemv_{t}", 0, rows, cols, dt(-1), dA.p, lda, dxN.p, dt(1), dyN.p)
+    A64 = A.astype(np.float64)
+    refT = A64.T @ xT.astype(np.float64)
+    refN = y0.astype(np.float64) - A64 @ xN.astype(np.float64)
+    eps = F64_EPS if t == "f64" else F32_EPS
+    scaleT = np.abs(A64).T @ np.abs(xT.astype(np.float64))
+    scaleN = np.abs(y0) + np.abs(A64) @ np.abs(xN.astype(np.float64))
+    assert np.all(np.abs(dyT.get() - refT) <= 2 * eps * np.abs(refT) + 1e-12 * scaleT)
+    assert np.all(np.abs(dyN.get() - refN) <= 2 * eps * scaleN)
+    orefT = oracle.gemv(True, A, xT)
+    assert np.allclose(dyT.get(), orefT, rtol=0, atol=(1e-12 if t == "f64" else 1e-5) * scaleT.max())
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
+@pytest.mark.parametrize("n", [1, 2, 10, 30, 100])
+def test_trsv_upper(hip, oracle, t, n):
+    dt = np.float64 if t == "f64" else np.float32
+    g = rng(n)
+    ld = n + 1  # H(0:k, 0:k) inside an (m+1) x m array
+    H = np.zeros((ld, n), dt, order="F")
+    H[:n] = np.triu(g.uniform(-1, 1, (n, n))) + np.diag(g.uniform(2, 3, n))
+    y = g.uniform(-1, 1, n).astype(dt)
+    dH, dy = hip.buf(H.ravel(order="F")), hip.buf(y)
+    hip.call(f"mpg_trsv_{t}", 1, 0, n, dH.p, ld, dy.p)
+    got = dy.get()
+    ref = oracle.trsv_upper(np.asfortranarray(H[:n]), y)
+    tol = 64 * (F64_EPS if t == "f64" else F32_EPS)
+    assert np.allclose(got, ref, rtol=tol, atol=tol)
+    # lower and transposed forms against numpy
+    L = np.asfortranarray(np.tril(g.uniform(-1, 1, (n, n))) + np.diag(g.uniform(2, 3, n))).astype(dt)
+    for upper, trans, M in [(0, 0, L), (1, 1, np.asfortranarray(H[:n])), (0, 1, L)]:
+        dM, dv = hip.buf(M.ravel(order="F")), hip.buf(y)
+        hip.call(f"mpg_trsv_{t}", upper, trans, n, dM.p, n, dv.p)
+        op = M.T if trans else M
+        exp = np.linalg.solve(op.astype(np.float64), y.astype(np.float64))
+        assert np.allclose(dv.get(), exp, rtol=1e3 * tol, atol=1e3 * tol)
+
+
+def _spmv_case(mpg, kind):
+    if kind == "band":
+        return mpg.gen_band(200_000, 5, 4, seed=11)
+    if kind == "laplace":
+        return mpg.gen_laplace3d(40, 30, 20)
+    if kind == "longrows":  # rows longer than one LDS chunk + empty rows
+        import scipy.sparse as sp
+
+        g = rng(5)
+        n = 3000
+        dens = np.where(np.arange(n) % 500 == 0, 0.9, 0.003)
+        rows, cols = [], []
+        for i in range(n):
+            if i % 777 == 5:
+                continue  # empty row
+            c = np.nonzero(g.random(n) < dens[i])[0]
+            rows += [i] * len(c)
+            cols += list(c)
+        M = sp.csr_matrix((g.uniform(-1, 1, len(rows)), (rows, cols)), shape=(n, n))
+        M.sort_indices()
+        return mpg.Csr(n, n, M.indptr.astype(np.int32), M.indices.astype(np.int32), M.data.astype(np.float64))
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["band", "laplace", "longrows"])
+def test_spmv(hip, mpg, oracle, kind):
+    import ctypes as C
+
+    A = _spmv_case(mpg, kind)
+    n = A.nrows
+    g = rng(7)
+    x = g.uniform(-1, 1, n)
+    y0 = g.uniform(-1, 1, n)
+    drp, dci = hip.buf(A.rowptr), hip.buf(A.col)
+    csr = C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, n, A.ncols, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    try:
+        S = A.to_scipy()
+        absS = abs(S)
+        # fp64: y = -A x + y0 (the residual form)
+        dv, dx, dy = hip.buf(A.val), hip.buf(x), hip.buf(y0)
+        hip.call("mpg_csr_spmv_f64", csr, -1.0, dv.p, dx.p, 1.0, dy.p)
+        ref = y0 - S @ x
+        scale = np.abs(y0) + absS @ np.abs(x)
+        assert np.all(np.abs(dy.get() - ref) <= 4 * F64_EPS * scale)
+        assert np.allclose(dy.get(), oracle.spmv(A, x, -1.0, 1.0, y0), rtol=0, atol=1e-13 * scale.max())
+        # fp32: y = A x (Arnoldi form); fp64 accumulation, one rounding
+        v32, x32 = A.val.astype(np.float32), x.astype(np.float32)
+        dv32, dx32, dy32 = hip.buf(v32), hip.buf(x32), hip.buf(n, np.float32)
+        hip.call("mpg_csr_spmv_f32", csr, np.float32(1), dv32.p, dx32.p, np.float32(0), dy32.p)
+        S32 = S.copy()
+        S32.data = v32.astype(np.float64)
+        ref32 = S32 @ x32.astype(np.float64)
+        sc32 = abs(S32) @ np.abs(x32.astype(np.float64))
+        assert np.all(np.abs(dy32.get() - ref32) <= F32_EPS * np.abs(ref32) + 1e-14 * sc32)
+        orc = oracle.spmv(A, x32, 1.0, 0.0, dtype=np.float32)
+        assert np.allclose(dy32.get(), orc, rtol=0, atol=1e-5 * max(sc32.max(), 1e-30))
+        # fp16 values, fp32 vectors
+        v16 = A.val.astype(np.float16)
+        dv16, dyh = hip.buf(v16.view(np.uint16)), hip.buf(n, np.float32)
+        hip.call("mpg_csr_spmv_f16f32", csr, np.float32(1), dv16.p, dx32.p, np.float32(0), dyh.p)
+        S16 = S.copy()
+        S16.data = v16.astype(np.float64)
+        ref16 = S16 @ x32.astype(np.float64)
+        assert np.all(np.abs(dyh.get() - ref16) <= F32_EPS * np.abs(ref16) + 1e-14 * (abs(S16) @ np.abs(x32)))
+    finally:
+        hip.lib.mpg_csr_destroy(csr)
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
+def test_jacobi_setup(hip, mpg, oracle, t):
+    import ctypes as C
+
+    dt = np.float64 if t == "f64" else np.float32
+    A = mpg.gen_band(50_000, 3, 2, seed=3)
+    A.val[::97] *= 1e-9  # tiny diagonals get boosted to eps*||A||_inf
+    n = A.nrows
+    drp, dci = hip.buf(A.rowptr), hip.buf(A.col)
+    csr = C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, n, n, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    try:
+        dv, dd = hip.buf(A.val.astype(dt)), hip.buf(n, dt)
+        hip.call(f"mpg_jacobi_setup_{t}", csr, dv.p, dd.p)
+        assert np.array_equal(dd.get(), oracle.jacobi(A, dt))
+    finally:
+        hip.lib.mpg_csr_destroy(csr)

@@ -1,0 +1,87 @@
+"""CPU checks of the oracle itself (no GPU).
+
+The reference holds no tests or golden vectors for this path, so the oracle
+is pinned by (1) the reference's own seeded input generator, whose first
+values are known (mt19937(42) + uniform_real_distribution<float>,
+gmres_perf_test.cpp:39-51), (2) agreement with an independent NumPy
+restatement of the algorithm, and (3) the committed golden records it
+produced (tolerances of tests/parity.py, since MKL's vector code paths differ
+between host CPUs).
+"""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import gmres_np
+from tests.golden.make_golden import convdiff, inputs
+from tests.parity import as_ref, compare
+
+GOLDEN = json.loads((Path(__file__).parent / "golden" / "gmres_golden.json").read_text())
+
+
+def test_rand_vect_matches_reference_sequence(mpg):
+    x = mpg.rand_vect(5, 42)
+    assert np.allclose(x, [0.37454012, 0.796543002, 0.95071429, 0.183434784, 0.731993914], rtol=0, atol=5e-9)
+    # values are floats widened to double
+    assert np.all(x.astype(np.float32).astype(np.float64) == x)
+
+
+def test_backend_reported(oracle):
+    assert oracle.backend() in ("mkl", "loops")
+
+
+@pytest.mark.parametrize("mode", ["mixed", "baseline", "single-prec", "single"])
+@pytest.mark.parametrize("orth", ["cgs", "mgs", "cgsr"])
+@pytest.mark.parametrize("prec", ["identity", "jacobi"])
+def test_oracle_vs_numpy_restatement(mpg, oracle, mode, orth, prec):
+    A = convdiff(mpg, 16)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    tol = 1e-5 if mode == "single" else 1e-10
+    r = oracle.solve(mpg, A, b, xt, mode=mode, orth=orth, prec=prec, rlen=12, tol=tol, max_restarts=300)
+    q = gmres_np.solve(A, b, mode=mode, orth=orth, prec=prec, rlen=12, tol=tol, max_restarts=300)
+    q["step_cycle"] = np.repeat(np.arange(len(q["cyc_r_norm"])), 12)[: len(q["step_res"])]
+    # the NumPy run plays "got", the oracle record plays "ref"
+    ns = type("R", (), {})()
+    for k in ("status", "restarts", "total_iters", "step_res", "step_cycle", "cyc_r_norm", "cyc_normalization"):
+        setattr(ns, k, q[k])
+    compare(as_ref(r), ns, mode, tol, 12, f"np-vs-oracle {mode}/{orth}/{prec}")
+
+
+def test_oracle_reproduces_golden(mpg, oracle):
+    mats = inputs(mpg)
+    for name, meta in GOLDEN["inputs"].items():
+        A = mats[name]
+        assert A.nrows == meta["n"] and A.nnz == meta["checksum"][2]
+        assert int(A.col.astype(np.int64).sum()) == meta["checksum"][1]
+        assert abs(A.val.sum() - meta["checksum"][0]) <= 1e-9 * abs(meta["checksum"][0])
+    for rec in GOLDEN["cases"][::5]:
+        case = dict(rec["case"])
+        A = mats[case.pop("matrix")]
+        xt = mpg.rand_vect(A.nrows, 42)
+        b = mpg.host_spmv(A, xt)
+        r = oracle.solve(mpg, A, b, xt, threads=1, **case)
+        compare(rec, r, case["mode"], case["tol"], case["rlen"], str(rec["case"]))
+
+
+def test_oracle_abort_semantics(mpg, oracle):
+    A = mpg.gen_laplace3d(8)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    r = oracle.solve(mpg, A, b, xt, mode="mixed", orth="cgs", prec="identity", rlen=30, tol=0.0, max_restarts=2)
+    assert r.status == "aborted" and r.total_iters == 60 and len(r.cyc_r_norm) == 3
+
+
+def test_oracle_adaptive_restart_strategies(mpg, oracle):
+    """RelPrecRes / RepeatIteration / LostOrthogonality (IterUtil.hpp:84-227) run and
+    restart earlier than the fixed-length strategy."""
+    A = convdiff(mpg, 24)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    base = oracle.solve(mpg, A, b, xt, mode="mixed", orth="mgs", prec="identity", rlen=40, tol=1e-9)
+    for extra in (dict(rtol=1e-3), dict(rtol=1e-3, repeat_iter=True), dict(rtol=1e-2, orthloss=True)):
+        r = oracle.solve(mpg, A, b, xt, mode="mixed", orth="mgs", prec="identity", rlen=40, tol=1e-9, **extra)
+        assert r.status == "converged"
+        assert r.restarts >= base.restarts

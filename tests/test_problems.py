@@ -1,0 +1,74 @@
+"""Host-side problem construction (CPU): generators, Matrix Market loader
+semantics (LoadMatrix.hpp:17-154), the seeded vector, host SpMV."""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+
+def test_band_shape_and_dominance(mpg):
+    A = mpg.gen_band(100_000, 5, 4, seed=7)
+    assert A.nnz == 10 * 100_000 - 25  # BAND-10M at n=1e6 has 9,999,975
+    S = A.to_scipy()
+    d = S.diagonal()
+    off = np.asarray(abs(S).sum(axis=1)).ravel() - d
+    assert np.all(d == 1 + off) or np.allclose(d, 1 + off, rtol=1e-15)
+    assert np.all(A.val[A.col != np.repeat(np.arange(A.nrows), np.diff(A.rowptr))] < 0)
+    # rows sorted, in range
+    for i in (0, 1, 50_000, 99_999):
+        c = A.col[A.rowptr[i]:A.rowptr[i + 1]]
+        assert np.all(np.diff(c) > 0) and c.min() >= 0 and c.max() < A.ncols
+
+
+def test_band_row_slices_match_whole(mpg):
+    A = mpg.gen_band(5000, 5, 4, seed=3)
+    parts = [mpg.gen_band(5000, 5, 4, seed=3, row_begin=r0, row_end=r1) for r0, r1 in ((0, 1234), (1234, 5000))]
+    assert parts[0].ncols == 5000
+    assert np.array_equal(np.concatenate([parts[0].col, parts[1].col]), A.col)
+    assert np.array_equal(np.concatenate([parts[0].val, parts[1].val]), A.val)
+
+
+def test_laplace_counts(mpg):
+    A = mpg.gen_laplace3d(10)
+    assert A.nrows == 1000 and A.nnz == 7 * 1000 - 6 * 100
+    S = A.to_scipy()
+    assert (S - S.T).nnz == 0
+    assert np.all(S.diagonal() == 6)
+    # 100^3 count quoted in SURVEY §8d: 6,940,000
+    assert 7 * 100**3 - 6 * 100**2 == 6_940_000
+
+
+def test_mtx_loader_reference_semantics(mpg):
+    A = mpg.load_mtx(str(Path(__file__).parent / "golden" / "small_quirks.mtx"))
+    assert A.nrows == 6
+    D = A.to_scipy().toarray()
+    exp = np.zeros((6, 6))
+    ent = [(0, 0, 4), (1, 0, -1), (1, 1, 6), (3, 1, -2), (2, 1, 1), (4, 4, 7), (5, 4, -3), (5, 0, 2), (3, 3, 3),
+           (5, 5, 9)]
+    for r, c, v in ent:
+        exp[r, c] = v
+        exp[c, r] = v
+    assert np.array_equal(D, exp)
+    # every row carries an explicit diagonal slot, even row 3 (index 2) which the file omits
+    for i in range(6):
+        cols = A.col[A.rowptr[i]:A.rowptr[i + 1]]
+        assert i in cols and np.all(np.diff(cols) > 0)
+    assert A.nnz == 6 + 2 * 5  # 6 diagonal slots + 5 mirrored off-diagonal pairs
+
+
+def test_mtx_loader_errors(mpg, tmp_path):
+    p = tmp_path / "bad.mtx"
+    p.write_text("%%MatrixMarket matrix coordinate complex general\n2 2 1\n1 1 1.0 0.0\n")
+    with pytest.raises(ValueError, match="Unsupported matrix type"):
+        mpg.load_mtx(str(p))
+    with pytest.raises(ValueError, match="Could not access file"):
+        mpg.load_mtx(str(tmp_path / "missing.mtx"))
+    p.write_text("not a banner\n")
+    with pytest.raises(ValueError):
+        mpg.load_mtx(str(p))
+
+
+def test_host_spmv_matches_scipy(mpg):
+    A = mpg.gen_band(20_000, 5, 4, seed=1)
+    x = mpg.rand_vect(A.nrows, 42)
+    assert np.allclose(mpg.host_spmv(A, x), A.to_scipy() @ x, rtol=1e-14, atol=1e-14)
