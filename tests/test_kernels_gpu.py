@@ -23,6 +23,13 @@ def rng(seed=0):
     return np.random.default_rng(seed)
 
 
+def assert_ulp(got, exp, ulps=1):
+    """|got - exp| <= ulps * ulp(exp): axpy may be contracted to one FMA
+    (single rounding, as MKL's and cuBLAS's vector axpy), numpy rounds twice."""
+    exp = np.asarray(exp)
+    assert np.all(np.abs(got - exp) <= ulps * np.spacing(np.maximum(np.abs(exp), np.abs(got))))
+
+
 @pytest.mark.parametrize("n", SIZES)
 @pytest.mark.parametrize("t", ["f64", "f32"])
 def test_dot_nrm2(hip, oracle, n, t):
@@ -59,7 +66,7 @@ def test_dot_nrm2(hip, oracle, n, t):
 
 
 @pytest.mark.parametrize("t", ["f64", "f32"])
-def test_blas1_elementwise_bitexact(hip, t):
+def test_blas1_elementwise(hip, t):
     dt = np.float64 if t == "f64" else np.float32
     n = 100_003
     g = rng(1)
@@ -70,13 +77,13 @@ def test_blas1_elementwise_bitexact(hip, t):
     hip.call(f"mpg_axpy_{t}", n, a, dx.p, dy.p)
     with np.errstate(all="ignore"):
         exp = (y + a * x).astype(dt)
-    assert np.array_equal(dy.get(), exp)
+    assert_ulp(dy.get(), exp)
     dy2 = hip.buf(y)
     hip.call(f"mpg_naxpy_dev_{t}", n, da.p, dx.p, dy2.p)
-    assert np.array_equal(dy2.get(), (y - a * x).astype(dt))
+    assert_ulp(dy2.get(), (y - a * x).astype(dt))
     dy3 = hip.buf(y)
     hip.call(f"mpg_axpy_dev_{t}", n, da.p, dx.p, dy3.p)
-    assert np.array_equal(dy3.get(), exp)
+    assert np.array_equal(dy3.get(), dy.get())
     dz = hip.buf(n, dt)
     hip.call(f"mpg_scal_copy_{t}", n, a, dx.p, dz.p)
     assert np.array_equal(dz.get(), (a * x).astype(dt))
@@ -160,7 +167,8 @@ def test_gemv_panels(hip, oracle, t, rows, cols):
     scaleT = np.abs(A64).T @ np.abs(xT.astype(np.float64))
     scaleN = np.abs(y0) + np.abs(A64) @ np.abs(xN.astype(np.float64))
     assert np.all(np.abs(dyT.get() - refT) <= 2 * eps * np.abs(refT) + 1e-12 * scaleT)
-    assert np.all(np.abs(dyN.get() - refN) <= 2 * eps * scaleN)
+    # fp64 sum of `cols` products, rounded to T, then y - t rounded again
+    assert np.all(np.abs(dyN.get() - refN) <= (2 * eps + cols * F64_EPS) * scaleN)
     orefT = oracle.gemv(True, A, xT)
     assert np.allclose(dyT.get(), orefT, rtol=0, atol=(1e-12 if t == "f64" else 1e-5) * scaleT.max())
 
