@@ -329,7 +329,7 @@ class Engine:
     """Stepped fused engine (mpg_engine_*): set up once, then advance the
     restarted solve cycle by cycle — what bench.py times."""
 
-    PHASES = {"spmv": 0, "prologue": 1, "cgs_update": 2}
+    PHASES = {"spmv": 0, "prologue": 1, "cgs_update": 2, "dots": 3}
 
     def __init__(self, A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, **opts):
         opts.pop("engine", None)

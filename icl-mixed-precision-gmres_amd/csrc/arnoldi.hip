@@ -15,6 +15,7 @@
 // fp64 and is rounded once to the working precision — the same rounding the
 // stand-alone kernels (blas1/blas2/spmv) apply, so the fused engine and the
 // operator-surface driver agree to the last bit in most steps.
+#include "csr_tile.hpp"
 #include "internal.hpp"
 #include "mpgmres/arnoldi.h"
 
@@ -24,19 +25,9 @@ using namespace mpg;
 
 namespace {
 
-constexpr int kNnzCap = 2048;  // must match spmv.hip
 constexpr int kNC = 32;        // dot columns carried in registers per pass
 constexpr int kGroups = 1024;  // max workgroups of the row-block phase kernels
 constexpr int kOrthMGS = 1, kOrthCGSR = 2;  // mpg_orth_t (include/mpgmres/solve.h)
-
-struct half_v {
-    uint16_t bits;
-};
-
-template <class V>
-__device__ __forceinline__ double ld_val(const V* v, int64_t i) { return (double)v[i]; }
-template <>
-__device__ __forceinline__ double ld_val<half_v>(const half_v* v, int64_t i) { return (double)to_float(v[i].bits); }
 
 // Jacobi / identity preconditioner in precision P applied to a T value:
 // typesafe_apply (gmres.cpp:12-22) + gdmv(1, d, w, 0, w) (kernels.hpp:141-144).
@@ -47,35 +38,23 @@ __device__ __forceinline__ T precond(T w, const P* __restrict__ d, int64_t i) {
     return (T)p;
 }
 
-// Walk the row blocks [rb] of the CSR-adaptive schedule assigned to this
-// workgroup. For every row: sum_j val_j * xval(col_j) in fp64 (products
-// staged in LDS for multi-row blocks), then epi(row, sum) on one lane.
+// This workgroup's contiguous run of row blocks [rb0, rb1) — contiguous so
+// that its rows form one range [blocks[rb0], blocks[rb1]) for the dot pass.
+__device__ __forceinline__ void my_blocks(int nblocks, int& rb0, int& rb1) {
+    rb0 = (int)((int64_t)blockIdx.x * nblocks / gridDim.x);
+    rb1 = (int)((int64_t)(blockIdx.x + 1) * nblocks / gridDim.x);
+}
+
+// For every row of this workgroup's row blocks: fp64 sum of val * xval(col)
+// (csr_tile.hpp), then epi(row, sum) on one lane.
 template <class V, class XF, class EPI>
 __device__ __forceinline__ void for_rows(const int32_t* __restrict__ blocks, int nblocks,
                                          const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                                         const V* __restrict__ val, XF xval, EPI epi, double* prod,
+                                         const V* __restrict__ val, int64_t nnz, XF xval, EPI epi, double* prod,
                                          double* scratch) {
-    for (int b = blockIdx.x; b < nblocks; b += gridDim.x) {
-        const int r0 = blocks[b], r1 = blocks[b + 1];
-        const int s = rowptr[r0], e = rowptr[r1];
-        if (r1 - r0 == 1) {
-            double acc = 0.0;
-            for (int i = s + threadIdx.x; i < e; i += kBlock) acc += ld_val(val, i) * xval(col[i]);
-            double sum = block_sum<kBlock>(acc, scratch);
-            if (threadIdx.x == 0) epi(r0, sum);
-            continue;
-        }
-        const int nnz = e - s;
-        for (int i = threadIdx.x; i < nnz; i += kBlock) prod[i] = ld_val(val, s + i) * xval(col[s + i]);
-        __syncthreads();
-        for (int r = threadIdx.x; r < r1 - r0; r += kBlock) {
-            const int a = rowptr[r0 + r] - s, z = rowptr[r0 + r + 1] - s;
-            double acc = 0.0;
-            for (int j = a; j < z; ++j) acc += prod[j];
-            epi(r0 + r, acc);
-        }
-        __syncthreads();
-    }
+    int rb0, rb1;
+    my_blocks(nblocks, rb0, rb1);
+    for (int b = rb0; b < rb1; ++b) csr_row_block(blocks[b], blocks[b + 1], rowptr, col, val, nnz, xval, epi, prod, scratch);
 }
 
 // Block-reduce NCOL fp64 accumulators and store them as partial[c*G + blk].
@@ -105,14 +84,14 @@ template <class T, class X, class P>
 __global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__ blocks, int nblocks,
                                                      const int32_t* __restrict__ rowptr,
                                                      const int32_t* __restrict__ col, const X* __restrict__ val,
-                                                     const X* __restrict__ x, const X* __restrict__ b,
+                                                     int64_t nnz, const X* __restrict__ x, const X* __restrict__ b,
                                                      const P* __restrict__ diag, T* __restrict__ w,
                                                      double* __restrict__ partial) {
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
     double acc[3] = {0.0, 0.0, 0.0};
     for_rows(
-        blocks, nblocks, rowptr, col, val, [&](int c) { return (double)x[c]; },
+        blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)x[c]; },
         [&](int i, double sum) {
             const X t = (X)sum;
             const X r = b[i] - t;  // copy(b, w); spmv(-1, A, x, 1, w)
@@ -145,66 +124,139 @@ __global__ void k_prologue_finish(const double* __restrict__ sums, int m, T* __r
 }
 
 // ---------------------------------------------------------------- reductions
-__global__ __launch_bounds__(kBlock) void k_reduce_partials(int G, const double* __restrict__ partial,
-                                                            double* __restrict__ sums) {
-    __shared__ double scratch[kBlock / kWave];
-    const int c = blockIdx.x;
-    double v = 0.0;
-    for (int g = threadIdx.x; g < G; g += kBlock) v += partial[(size_t)c * G + g];
-    double s = block_sum<kBlock>(v, scratch);
-    if (threadIdx.x == 0) sums[c] = s;
+// sum of G partials in a fixed order (identical in every workgroup that
+// calls it with the same G); result valid in thread 0
+template <int BS>
+__device__ __forceinline__ double sum_partials(const double* __restrict__ p, int G, double* scratch) {
+    double v0 = 0.0, v1 = 0.0;
+    int g = threadIdx.x;
+    for (; g + BS < G; g += 2 * BS) {
+        v0 += p[g];
+        v1 += p[g + BS];
+    }
+    if (g < G) v0 += p[g];
+    return block_sum<BS>(v0 + v1, scratch);
+}
+
+__global__ __launch_bounds__(1024) void k_reduce_partials(int G, const double* __restrict__ partial,
+                                                          double* __restrict__ sums) {
+    __shared__ double scratch[1024 / kWave];
+    const double s = sum_partials<1024>(partial + (size_t)blockIdx.x * G, G, scratch);
+    if (threadIdx.x == 0) sums[blockIdx.x] = s;
 }
 
 // ---------------------------------------------------------------- step: SpMV
-// v_k = T(w_prev * inv) (local rows stored to V[:,k]); w = M(A v_k);
-// partials <v_j, w> for j in [0, ndots)
+// v_k = T(w_prev * inv) (local rows stored to V[:,k]); w = M(A v_k); then
+// the Gram-Schmidt partials <v_j, w> (j < ndots <= kNC) over this
+// workgroup's rows. The dot pass keeps one column chunk live at a time and
+// folds each column with a wave64 shuffle reduction straight away, so it
+// adds few registers to this gather-bound kernel (a full fp64 accumulator
+// bank here dropped it to 3 waves/SIMD). ndots == 0: k_panel_dots follows.
+constexpr int kDotChunk = 16;
+constexpr bool kFuseDots = false;
+
 template <class T, class P, class VI>
 __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict__ blocks, int nblocks,
                                                       const int32_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ col, const VI* __restrict__ val,
-                                                      const T* __restrict__ wprev, const T* __restrict__ inv_p,
-                                                      T* __restrict__ V, int64_t ld, int k, int ndots,
-                                                      const P* __restrict__ diag, T* __restrict__ w,
-                                                      double* __restrict__ partial) {
+                                                      int64_t nnz, const T* __restrict__ wprev,
+                                                      const T* __restrict__ inv_p, T* __restrict__ V, int64_t ld,
+                                                      int k, const P* __restrict__ diag, T* __restrict__ w,
+                                                      int ndots, double* __restrict__ partial) {
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
+    __shared__ double red[kBlock / kWave][kNC];
     const T inv = *inv_p;
-    double acc[kNC];
-#pragma unroll
-    for (int c = 0; c < kNC; ++c) acc[c] = 0.0;
     T* __restrict__ Vk = V + (int64_t)k * ld;
     for_rows(
-        blocks, nblocks, rowptr, col, val, [&](int c) { return (double)(T)(wprev[c] * inv); },
+        blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)(T)(wprev[c] * inv); },
         [&](int i, double sum) {
             const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
-            const T wi = precond<T, P>(t, diag, i);
-            w[i] = wi;
-            const T vki = wprev[i] * inv;
-            Vk[i] = vki;
-#pragma unroll
-            for (int j = 0; j < kNC; ++j) {
-                if (j < ndots) {
-                    const T vj = j == k ? vki : V[(int64_t)j * ld + i];
-                    acc[j] += (double)vj * (double)wi;
-                }
-            }
+            w[i] = precond<T, P>(t, diag, i);
+            Vk[i] = wprev[i] * inv;
         },
         prod, scratch);
-    store_partials<kNC>(acc, ndots, partial);
+    if (ndots <= 0) return;
+    int rb0, rb1;
+    my_blocks(nblocks, rb0, rb1);
+    const int i0 = blocks[rb0], i1 = blocks[rb1];
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    for (int j0 = 0; j0 < ndots; j0 += kDotChunk) {
+        double a[kDotChunk];
+#pragma unroll
+        for (int c = 0; c < kDotChunk; ++c) a[c] = 0.0;
+        for (int i = i0 + threadIdx.x; i < i1; i += kBlock) {
+            const double wi = (double)w[i];
+            T v[kDotChunk];
+#pragma unroll
+            for (int c = 0; c < kDotChunk; ++c) v[c] = j0 + c < ndots ? V[(int64_t)(j0 + c) * ld + i] : T(0);
+#pragma unroll
+            for (int c = 0; c < kDotChunk; ++c) a[c] += (double)v[c] * wi;
+        }
+#pragma unroll
+        for (int c = 0; c < kDotChunk; ++c) {
+            if (j0 + c < ndots) {
+                const double s = wave_sum(a[c]);
+                if (lane == 0) red[wid][j0 + c] = s;
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < ndots; c += kBlock) {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < kBlock / kWave; ++q) s += red[q][c];
+        partial[(size_t)c * gridDim.x + blockIdx.x] = s;
+    }
 }
 
-// partial dots <v_j, w> for j in [c0, c0 + nc) over all local rows
+// 4 consecutive entries (i a multiple of 4, 16-B aligned for fp32) widened to fp64
+template <class T> struct Row4;
+template <> struct Row4<float> {
+    static __device__ __forceinline__ void load(const float* p, double (&o)[4]) {
+        const float4 v = *reinterpret_cast<const float4*>(p);
+        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    }
+};
+template <> struct Row4<double> {
+    static __device__ __forceinline__ void load(const double* p, double (&o)[4]) {
+        const double2 a = *reinterpret_cast<const double2*>(p);
+        const double2 b = *reinterpret_cast<const double2*>(p + 2);
+        o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
+    }
+};
+
+// Tall-skinny panel reduction: partial <v_j, w> for j in [c0, c0 + nc),
+// nc <= kNC, over all local rows. Each lane owns 4 consecutive rows per
+// iteration (16-B loads of every column: V's leading dimension is padded to
+// 256 B), issues all column loads before its FMAs, and keeps one fp64
+// accumulator per column; store_partials does the wave64/LDS combine.
 template <class T>
 __global__ __launch_bounds__(kBlock) void k_panel_dots(int n, const T* __restrict__ V, int64_t ld, int c0, int nc,
                                                        const T* __restrict__ w, double* __restrict__ partial) {
     double acc[kNC];
 #pragma unroll
     for (int c = 0; c < kNC; ++c) acc[c] = 0.0;
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const int n4 = n & ~3;
+    const T* __restrict__ Vb = V + (int64_t)c0 * ld;
+    for (int i = 4 * (blockIdx.x * kBlock + threadIdx.x); i < n4; i += 4 * gridDim.x * kBlock) {
+        double wv[4];
+        Row4<T>::load(w + i, wv);
+#pragma unroll
+        for (int c = 0; c < kNC; ++c) {
+            if (c < nc) {
+                double v[4];
+                Row4<T>::load(Vb + (int64_t)c * ld + i, v);
+                acc[c] += v[0] * wv[0] + v[1] * wv[1] + v[2] * wv[2] + v[3] * wv[3];
+            }
+        }
+    }
+    // tail rows (n not a multiple of 4)
+    for (int i = n4 + blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         const double wi = (double)w[i];
 #pragma unroll
         for (int c = 0; c < kNC; ++c)
-            if (c < nc) acc[c] += (double)V[(int64_t)(c0 + c) * ld + i] * wi;
+            if (c < nc) acc[c] += (double)Vb[(int64_t)c * ld + i] * wi;
     }
     store_partials<kNC>(acc, nc, partial + (size_t)c0 * gridDim.x);
 }
@@ -290,23 +342,43 @@ __device__ void rotg_ref(T& a, T& b, T& c, T& s) {
     b = T(0);
 }
 
-// h_{k+1,k} = ||w||; (CGSR: h(0:k,k) += correction); rotations; |s(k+1)|
+// h_{k+1,k} = ||w||; (CGSR: h(0:k,k) += correction); rotations; |s(k+1)|.
+// norm2 = the squared norm: sums[0] (nparts == 0) or, on one GPU, the sum
+// of `nparts` workgroup partials reduced here (saves a launch per step).
 template <class T>
-__global__ void k_givens(int k, int m, const double* __restrict__ sums, const T* __restrict__ corr,
-                         T* __restrict__ H, T* __restrict__ cs, T* __restrict__ sn, T* __restrict__ s,
-                         T* __restrict__ inv, double* __restrict__ report) {
-    if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(kBlock) void k_givens(int k, int m, const double* __restrict__ norm2, int nparts,
+                                                   const T* __restrict__ corr, T* __restrict__ H,
+                                                   T* __restrict__ cs, T* __restrict__ sn, T* __restrict__ s,
+                                                   T* __restrict__ inv, double* __restrict__ report) {
+    // stage the column and the previous rotations in LDS with all lanes, so
+    // the serial rotation chain runs on LDS instead of global latency
+    __shared__ T col[1026], c_s[1026], s_s[1026];
+    __shared__ double scratch[kBlock / kWave];
+    const double nrm2sq = nparts > 0 ? sum_partials<kBlock>(norm2, nparts, scratch) : norm2[0];
     const int ldh = m + 1;
-    T* col = H + (int64_t)k * ldh;
-    if (corr)
-        for (int j = 0; j <= k; ++j) col[j] = col[j] + T(1) * corr[j];  // axpy(1.0, weights, h_col)
-    const T hn = (T)sqrt(sums[0]);
-    col[k + 1] = hn;
-    *inv = T(1) / hn;  // scal(1/h_final, w, v_{k+1}) — no breakdown guard, as in the reference
-    for (int j = 0; j < k; ++j) rot_pair(col[j], col[j + 1], cs[j], sn[j]);
-    rotg_ref(col[k], col[k + 1], cs[k], sn[k]);
-    rot_pair(s[k], s[k + 1], cs[k], sn[k]);
-    report[4 + k] = (double)fabs(s[k + 1]);
+    T* gcol = H + (int64_t)k * ldh;
+    for (int j = threadIdx.x; j <= k; j += blockDim.x) {
+        col[j] = corr ? gcol[j] + T(1) * corr[j] : gcol[j];  // axpy(1.0, weights, h_col)
+        c_s[j] = cs[j];
+        s_s[j] = sn[j];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const T hn = (T)sqrt(nrm2sq);
+        col[k + 1] = hn;
+        *inv = T(1) / hn;  // scal(1/h_final, w, v_{k+1}) — no breakdown guard, as in the reference
+        for (int j = 0; j < k; ++j) rot_pair(col[j], col[j + 1], c_s[j], s_s[j]);
+        rotg_ref(col[k], col[k + 1], c_s[k], s_s[k]);
+        T sk = s[k], sk1 = s[k + 1];
+        rot_pair(sk, sk1, c_s[k], s_s[k]);
+        s[k] = sk;
+        s[k + 1] = sk1;
+        cs[k] = c_s[k];
+        sn[k] = s_s[k];
+        report[4 + k] = (double)fabs(sk1);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j <= k + 1; j += blockDim.x) gcol[j] = col[j];
 }
 
 // upper-triangular solve y = H(0:k,0:k)^-1 s(0:k), in place on s (one lane per
@@ -356,7 +428,10 @@ struct mpg_arnoldi {
     mpg_ctx* ctx = nullptr;
     mpg_arnoldi_desc d{};
     int combo = 0;    // type combination (see dispatch below)
-    int G = 1;        // workgroups of the phase kernels
+    int G = 1;        // workgroups of the row-parallel panel kernels
+    int Grb = 1;      // workgroups of the row-block (SpMV) kernels: one per row block
+    int last_G = 1;   // partial count per column written by the last producer
+    bool dots_pending = false;  // mpg_arnoldi_dots still has to form the partials
     int64_t ld = 0;   // leading dimension of V (elements)
     size_t tsize = 8;
     void* V = nullptr;
@@ -403,6 +478,7 @@ int dispatch(int combo, F&& f) {
 }
 
 int row_grid(const mpg_arnoldi* a) { return a->G; }
+int rb_grid(const mpg_arnoldi* a) { return a->Grb; }
 
 }  // namespace
 
@@ -423,6 +499,7 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
     a->combo = combo;
     a->tsize = desc->vec_type == MPG_F64 ? 8 : 4;
     a->G = desc->A->nblocks < kGroups ? (desc->A->nblocks > 0 ? desc->A->nblocks : 1) : kGroups;
+    a->Grb = desc->A->nblocks > 0 ? desc->A->nblocks : 1;
     const size_t align = 256 / a->tsize;
     a->ld = ((int64_t)desc->n + align - 1) / align * align;
     if (a->ld == 0) a->ld = align;
@@ -435,8 +512,8 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
               alloc(&a->small, (size_t)6 * (m + 1) * a->tsize) &&
               alloc(&a->w[0], (size_t)(desc->n_ext + 64) * a->tsize) &&
               alloc(&a->w[1], (size_t)(desc->n_ext + 64) * a->tsize) &&
-              alloc((void**)&a->partial, (size_t)(kNC + 4) * a->G * sizeof(double) +
-                                             (size_t)(m + 1) * a->G * sizeof(double)) &&
+              alloc((void**)&a->partial, std::max<size_t>((size_t)(kNC + 4) * a->Grb, (size_t)(m + 4) * a->G) *
+                                             sizeof(double)) &&
               alloc((void**)&a->sums, (size_t)(m + 8) * sizeof(double)) &&
               alloc((void**)&a->report, (size_t)(m + 8) * sizeof(double));
     if (!ok) {
@@ -464,12 +541,13 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
         using T = decltype(t);
         using X = decltype(x);
         using P = decltype(p);
-        k_prologue<T, X, P><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-            A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const X*>(a->d.val_outer),
+        k_prologue<T, X, P><<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(
+            A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const X*>(a->d.val_outer), A->nnz,
             static_cast<const X*>(a->d.x), static_cast<const X*>(a->d.b),
             a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr, static_cast<T*>(a->w[0]), a->partial);
         return MPG_OK;
     });
+    a->last_G = rb_grid(a);
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
@@ -491,7 +569,7 @@ int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a) {
 
 int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols) {
     if (!a || ncols < 1 || ncols > a->d.m + 4) return MPG_ERR_ARG;
-    k_reduce_partials<<<ncols, kBlock, 0, a->ctx->stream>>>(a->G, a->partial, a->sums);
+    k_reduce_partials<<<ncols, 1024, 0, a->ctx->stream>>>(a->last_G, a->partial, a->sums);
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
 }
@@ -500,17 +578,34 @@ int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
     const mpg_csr* A = a->d.A;
     const int ndots_all = a->d.orth == kOrthMGS ? 1 : k + 1;
-    const int ndots_fused = ndots_all < kNC ? ndots_all : kNC;
     int st = dispatch(a->combo, [&](auto t, auto, auto p, auto vi) {
         using T = decltype(t);
         using P = decltype(p);
         using VI = decltype(vi);
-        k_step_spmv<T, P, VI><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-            A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner),
+        // dots inside the SpMV launch measured 71 us vs 30 + 20 us split
+        // (BAND-10M fp32, k = 0..29 mean): keep the separate panel kernel
+        const bool fused = kFuseDots && ndots_all <= kNC;
+        k_step_spmv<T, P, VI><<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(
+            A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,
             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,
-            ndots_fused, a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr, static_cast<T*>(a->w[(k + 1) & 1]),
-            a->partial);
-        for (int c0 = kNC; c0 < ndots_all; c0 += kNC) {
+            a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr, static_cast<T*>(a->w[(k + 1) & 1]),
+            fused ? ndots_all : 0, a->partial);
+        a->last_G = rb_grid(a);
+        a->dots_pending = !fused;
+        return MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_dots(mpg_arnoldi_t a, int k) {
+    if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
+    if (!a->dots_pending) return MPG_OK;  // formed inside the SpMV launch (kFuseDots)
+    const int ndots_all = a->d.orth == kOrthMGS ? 1 : k + 1;
+    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
+        using T = decltype(t);
+        for (int c0 = 0; c0 < ndots_all; c0 += kNC) {
             const int nc = ndots_all - c0 < kNC ? ndots_all - c0 : kNC;
             k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, c0, nc, static_cast<const T*>(a->w[(k + 1) & 1]),
@@ -518,6 +613,7 @@ int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k) {
         }
         return MPG_OK;
     });
+    a->last_G = row_grid(a);
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
@@ -545,6 +641,7 @@ int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass) {
         }
         return MPG_OK;
     });
+    a->last_G = row_grid(a);
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
@@ -560,26 +657,30 @@ int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j) {
                                                                     static_cast<T*>(a->w[(k + 1) & 1]), a->partial);
         return MPG_OK;
     });
+    a->last_G = row_grid(a);
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
 }
 
-int mpg_arnoldi_givens(mpg_arnoldi_t a, int k) {
+static int givens_impl(mpg_arnoldi_t a, int k, bool from_partials) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
     const bool cgsr = a->d.orth == kOrthCGSR;
     int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
         using T = decltype(t);
-        k_givens<T><<<1, 64, 0, a->ctx->stream>>>(k, a->d.m, a->sums, cgsr ? static_cast<const T*>(a->corr()) : nullptr,
-                                                  static_cast<T*>(a->H), static_cast<T*>(a->cs()),
-                                                  static_cast<T*>(a->sn()), static_cast<T*>(a->s()),
-                                                  static_cast<T*>(a->inv()), a->report);
+        k_givens<T><<<1, kBlock, 0, a->ctx->stream>>>(
+            k, a->d.m, from_partials ? a->partial : a->sums, from_partials ? a->last_G : 0,
+            cgsr ? static_cast<const T*>(a->corr()) : nullptr, static_cast<T*>(a->H), static_cast<T*>(a->cs()),
+            static_cast<T*>(a->sn()), static_cast<T*>(a->s()), static_cast<T*>(a->inv()), a->report);
         return MPG_OK;
     });
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
 }
+
+int mpg_arnoldi_givens(mpg_arnoldi_t a, int k) { return givens_impl(a, k, false); }
+int mpg_arnoldi_givens_partials(mpg_arnoldi_t a, int k) { return givens_impl(a, k, true); }
 
 int mpg_arnoldi_update(mpg_arnoldi_t a, int k) {
     if (!a || k < 0 || k > a->d.m || k > 1024) return MPG_ERR_ARG;

@@ -1,0 +1,137 @@
+// CSR-adaptive row-block tile, shared by the stand-alone SpMV (spmv.hip) and
+// the fused Arnoldi phases (arnoldi.hip).
+//
+// A row block is either a run of short rows holding at most kNnzCap
+// nonzeros (stream mode) or one row (row mode). Stream mode loads the
+// block's (col, val) pairs with 16-byte vector loads — the block start is
+// rounded down to a 4-element boundary and the extra lanes are masked — and
+// issues every load of a lane before its first use: two int4 column loads,
+// the matching value loads, then all eight gathers of x. The fp64 products
+// land in LDS, one lane per row then sums its segment in column order.
+#pragma once
+
+#include "internal.hpp"
+
+namespace mpg {
+
+constexpr int kNnzCap = 2040;                       // nnz per stream-mode row block
+constexpr int kRowCap = 2048;                       // rows per stream-mode row block
+constexpr int kTileVec = (kNnzCap + 3) / 4 + 1;     // 16-B index vectors per tile (<= 512)
+constexpr int kVecPerLane = (kTileVec + kBlock - 1) / kBlock;  // = 2
+
+struct half_v {
+    uint16_t bits;
+};
+
+// 4 consecutive values (element index i, a multiple of 4) widened to fp64
+template <class V> struct Vec4Load;
+template <> struct Vec4Load<float> {
+    static __device__ __forceinline__ void load(const float* p, int64_t i, double (&o)[4]) {
+        const float4 v = *reinterpret_cast<const float4*>(p + i);
+        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    }
+};
+template <> struct Vec4Load<double> {
+    static __device__ __forceinline__ void load(const double* p, int64_t i, double (&o)[4]) {
+        const double2 a = *reinterpret_cast<const double2*>(p + i);
+        const double2 b = *reinterpret_cast<const double2*>(p + i + 2);
+        o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
+    }
+};
+template <> struct Vec4Load<half_v> {
+    static __device__ __forceinline__ void load(const half_v* p, int64_t i, double (&o)[4]) {
+        const ushort4 v = *reinterpret_cast<const ushort4*>(p + i);
+        o[0] = to_float(v.x); o[1] = to_float(v.y); o[2] = to_float(v.z); o[3] = to_float(v.w);
+    }
+};
+template <> struct Vec4Load<uint16_t> {
+    static __device__ __forceinline__ void load(const uint16_t* p, int64_t i, double (&o)[4]) {
+        const ushort4 v = *reinterpret_cast<const ushort4*>(p + i);
+        o[0] = to_float(v.x); o[1] = to_float(v.y); o[2] = to_float(v.z); o[3] = to_float(v.w);
+    }
+};
+
+template <class V>
+__device__ __forceinline__ double scalar_val(const V* p, int64_t i) { return (double)p[i]; }
+template <>
+__device__ __forceinline__ double scalar_val<half_v>(const half_v* p, int64_t i) { return (double)to_float(p[i].bits); }
+template <>
+__device__ __forceinline__ double scalar_val<uint16_t>(const uint16_t* p, int64_t i) { return (double)to_float(p[i]); }
+
+// Stage the fp64 products val[i] * xval(col[i]) for i in [s, e) into prod[i - s].
+// nnz_total bounds the vector loads at the end of the arrays.
+template <class V, class XF>
+__device__ __forceinline__ void stage_products(int s, int e, int64_t nnz_total, const int32_t* __restrict__ col,
+                                               const V* __restrict__ val, XF xval, double* __restrict__ prod) {
+    const int base = s & ~3;
+    int4 c[kVecPerLane];
+    double v[kVecPerLane][4];
+    bool live[kVecPerLane];
+#pragma unroll
+    for (int u = 0; u < kVecPerLane; ++u) {
+        const int idx = base + 4 * (threadIdx.x + u * kBlock);
+        live[u] = idx < e;
+        if (live[u]) {
+            if (idx + 3 < nnz_total) {
+                c[u] = *reinterpret_cast<const int4*>(col + idx);
+                Vec4Load<V>::load(val, idx, v[u]);
+            } else {
+                int cc[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const bool in = idx + q < nnz_total;
+                    cc[q] = in ? col[idx + q] : 0;
+                    v[u][q] = in ? scalar_val(val, idx + q) : 0.0;
+                }
+                c[u] = make_int4(cc[0], cc[1], cc[2], cc[3]);
+            }
+        }
+    }
+    double x[kVecPerLane][4];
+#pragma unroll
+    for (int u = 0; u < kVecPerLane; ++u) {
+        const int idx = base + 4 * (threadIdx.x + u * kBlock);
+        const int cc[4] = {c[u].x, c[u].y, c[u].z, c[u].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = idx + q;
+            x[u][q] = (live[u] && i >= s && i < e) ? xval(cc[q]) : 0.0;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kVecPerLane; ++u) {
+        const int idx = base + 4 * (threadIdx.x + u * kBlock);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = idx + q;
+            if (live[u] && i >= s && i < e) prod[i - s] = v[u][q] * x[u][q];
+        }
+    }
+}
+
+// Row sums of one row block: epi(row, fp64 sum) is called once per row.
+template <class V, class XF, class EPI>
+__device__ __forceinline__ void csr_row_block(int r0, int r1, const int32_t* __restrict__ rowptr,
+                                              const int32_t* __restrict__ col, const V* __restrict__ val,
+                                              int64_t nnz_total, XF xval, EPI epi, double* prod, double* scratch) {
+    const int s = rowptr[r0], e = rowptr[r1];
+    if (r1 - r0 == 1) {
+        double acc = 0.0;
+        for (int i = s + threadIdx.x; i < e; i += kBlock) acc += scalar_val(val, i) * xval(col[i]);
+        const double sum = block_sum<kBlock>(acc, scratch);
+        if (threadIdx.x == 0) epi(r0, sum);
+        __syncthreads();  // the row's outputs are visible to the whole workgroup
+        return;
+    }
+    stage_products(s, e, nnz_total, col, val, xval, prod);
+    __syncthreads();
+    for (int r = threadIdx.x; r < r1 - r0; r += kBlock) {
+        const int a = rowptr[r0 + r] - s, z = rowptr[r0 + r + 1] - s;
+        double acc = 0.0;
+        for (int j = a; j < z; ++j) acc += prod[j];
+        epi(r0 + r, acc);
+    }
+    __syncthreads();
+}
+
+}  // namespace mpg

@@ -14,6 +14,7 @@
 // Products and sums are fp64 for every precision (exact products for fp32
 // and fp16 values); the row sum is rounded once to the vector type, then
 // y = alpha*sum (+ beta*y when beta != 0).
+#include "csr_tile.hpp"
 #include "internal.hpp"
 
 #include <cfloat>
@@ -25,59 +26,30 @@ using namespace mpg;
 
 namespace {
 
-constexpr int kNnzCap = 2048;   // nonzeros staged per stream-mode row block
-constexpr int kRowCap = 2048;   // rows per stream-mode row block
-
-template <class V>
-__device__ __forceinline__ double val_as_double(const V* v, int64_t i) { return (double)v[i]; }
-template <>
-__device__ __forceinline__ double val_as_double<uint16_t>(const uint16_t* v, int64_t i) {
-    return (double)to_float(v[i]);
-}
-
 template <class V, class X>
 __global__ __launch_bounds__(kBlock) void k_csr_adaptive(const int32_t* __restrict__ blocks,
                                                          const int32_t* __restrict__ rowptr,
                                                          const int32_t* __restrict__ col,
-                                                         const V* __restrict__ val,
+                                                         const V* __restrict__ val, int64_t nnz,
                                                          const X* __restrict__ x, X alpha, X beta,
                                                          X* __restrict__ y) {
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
     const int b = blockIdx.x;
-    const int r0 = blocks[b], r1 = blocks[b + 1];
-    const int nrows = r1 - r0;
-    const int s = rowptr[r0];
-    const int e = rowptr[r1];
-    if (nrows == 1) {
-        double acc = 0.0;
-        for (int i = s + threadIdx.x; i < e; i += kBlock) acc += val_as_double(val, i) * (double)x[col[i]];
-        double sum = block_sum<kBlock>(acc, scratch);
-        if (threadIdx.x == 0) {
-            X t = (X)sum;
-            y[r0] = beta == X(0) ? alpha * t : alpha * t + beta * y[r0];
-        }
-        return;
-    }
-    const int nnz = e - s;
-    for (int i = threadIdx.x; i < nnz; i += kBlock)
-        prod[i] = val_as_double(val, s + i) * (double)x[col[s + i]];
-    __syncthreads();
-    for (int r = threadIdx.x; r < nrows; r += kBlock) {
-        const int a = rowptr[r0 + r] - s;
-        const int z = rowptr[r0 + r + 1] - s;
-        double acc = 0.0;
-        for (int j = a; j < z; ++j) acc += prod[j];
-        X t = (X)acc;
-        y[r0 + r] = beta == X(0) ? alpha * t : alpha * t + beta * y[r0 + r];
-    }
+    csr_row_block(
+        blocks[b], blocks[b + 1], rowptr, col, val, nnz, [&](int c) { return (double)x[c]; },
+        [&](int i, double sum) {
+            const X t = (X)sum;
+            y[i] = beta == X(0) ? alpha * t : alpha * t + beta * y[i];
+        },
+        prod, scratch);
 }
 
 template <class V, class X>
 int spmv_impl(mpg_ctx* ctx, mpg_csr* A, X alpha, const V* vals, const X* x, X beta, X* y) {
     if (!ctx || !A) return MPG_ERR_ARG;
     if (A->rows == 0) return MPG_OK;
-    k_csr_adaptive<V, X><<<A->nblocks, kBlock, 0, ctx->stream>>>(A->blocks, A->rowptr, A->col, vals, x,
+    k_csr_adaptive<V, X><<<A->nblocks, kBlock, 0, ctx->stream>>>(A->blocks, A->rowptr, A->col, vals, A->nnz, x,
                                                                  alpha, beta, y);
     MPG_LAUNCH_CHECK(ctx);
     return MPG_OK;

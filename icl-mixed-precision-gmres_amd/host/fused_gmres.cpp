@@ -282,11 +282,12 @@ void FusedEngine::step(int k) {
     };
     if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
     check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
+    check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
     if (I.orth == MPG_ORTH_MGS) {
         reduce(1);
         for (int j = 0; j <= k; ++j) {
             check(mpg_arnoldi_mgs(I.arn, k, j), "mgs", I.ctx);
-            reduce(1);
+            if (j < k) reduce(1);
         }
     } else {
         reduce(k + 1);
@@ -297,9 +298,15 @@ void FusedEngine::step(int k) {
         } else {
             check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
         }
-        reduce(1);
     }
-    check(mpg_arnoldi_givens(I.arn, k), "givens", I.ctx);
+    // ||w||^2: one GPU folds the partial sums into the Givens kernel; ranks of
+    // a partitioned solve reduce + all-reduce first
+    if (I.comm) {
+        reduce(1);
+        check(mpg_arnoldi_givens(I.arn, k), "givens", I.ctx);
+    } else {
+        check(mpg_arnoldi_givens_partials(I.arn, k), "givens", I.ctx);
+    }
 }
 
 void FusedEngine::update(int k) { check(mpg_arnoldi_update(p_->arn, k), "update", p_->ctx); }
@@ -443,14 +450,17 @@ double FusedEngine::phase_bytes(int which) const {
     const double sV = (double)dsize(I.ty.VI), sP = (double)dsize(I.ty.P);
     const double jac = I.args.prec == MPG_PREC_JACOBI ? 1.0 : 0.0;
     if (which == 0) {
-        // mean over k of: CSR (values + int32 columns + row pointers), gathered
-        // v_k (read once), w and V(:,k) written, dot partners V(:,0..k-1)
-        double dots = 0;
-        for (int k = 0; k < I.m; ++k) dots += (I.orth == MPG_ORTH_MGS ? (k > 0 ? 1 : 0) : k);
-        dots /= I.m;
-        return z * (sV + 4) + (n + 1) * 4 + 3 * n * sT + dots * n * sT + jac * n * sP;
+        // CSR (values + int32 columns + row pointers), v_k gathered (read
+        // once), w and V(:,k) written, Jacobi diagonal read
+        return z * (sV + 4) + (n + 1) * 4 + 3 * n * sT + jac * n * sP;
     }
     if (which == 1) return z * (sX + 4) + (n + 1) * 4 + 3 * n * sX + n * sT + jac * n * sP;
+    if (which == 3) {
+        // panel dots, mean over k: V(:,0..k) and w read
+        double cols = 0;
+        for (int k = 0; k < I.m; ++k) cols += (I.orth == MPG_ORTH_MGS ? 1 : k + 1);
+        return (cols / I.m + 1) * n * sT;
+    }
     // CGS update at mean k: read V(:,0..k), read + write w
     return ((I.m - 1) / 2.0 + 1) * n * sT + 2 * n * sT;
 }
@@ -468,6 +478,7 @@ double FusedEngine::time_phase(int which, int reps) {
         for (int r = 0; r < reps; ++r) {
             if (which == 0) check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
             else if (which == 1) check(mpg_arnoldi_prologue(I.arn), "prologue", I.ctx);
+            else if (which == 3) check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
             else check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
         }
         hipck(hipEventRecord(e1, I.stream()), "record");
@@ -567,7 +578,7 @@ int mpg_engine_sync(mpg_engine_t e) {
 int64_t mpg_engine_total_iters(mpg_engine_t e) { return e && e->eng ? (int64_t)e->eng->total_iters() : -1; }
 
 int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms) {
-    if (!e || !e->eng || !avg_ms || reps < 1 || which < 0 || which > 2) return MPG_ERR_ARG;
+    if (!e || !e->eng || !avg_ms || reps < 1 || which < 0 || which > 3) return MPG_ERR_ARG;
     try {
         mpg::ScopedContext scope(e->ctx);
         *avg_ms = e->eng->time_phase(which, reps);

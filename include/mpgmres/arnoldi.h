@@ -70,10 +70,14 @@ int mpg_arnoldi_destroy(mpg_arnoldi_t a);
 
 int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
 int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);
-int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k);           /* partials: k+1 (CGS/CGSR) or 1 (MGS) */
+int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k);           /* w = M(A v_k), V(:,k) */
+int mpg_arnoldi_dots(mpg_arnoldi_t a, int k);           /* partials: k+1 (CGS/CGSR) or 1 (MGS) */
 int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass);  /* pass 0: h; pass 1: CGSR correction */
 int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j);
 int mpg_arnoldi_givens(mpg_arnoldi_t a, int k);
+/* single-GPU form: the Givens kernel sums the ||w||^2 partials of the last
+ * producer itself, saving one mpg_arnoldi_reduce launch per step */
+int mpg_arnoldi_givens_partials(mpg_arnoldi_t a, int k);
 int mpg_arnoldi_update(mpg_arnoldi_t a, int k);
 /* sums[c] = sum over workgroups of partial column c, c < ncols */
 int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols);

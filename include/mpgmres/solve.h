@@ -102,8 +102,9 @@ int mpg_engine_run(mpg_engine_t e, int max_cycles, int* done);
 int mpg_engine_sync(mpg_engine_t e);
 int64_t mpg_engine_total_iters(mpg_engine_t e);
 /* device-event timing of one phase kernel replayed `reps` times on the
- * engine's stream, back to back (which: 0 = Arnoldi SpMV of step m/2,
- * 1 = fp64 residual prologue, 2 = CGS update of step m/2) */
+ * engine's stream, back to back, averaged over the steps k = 0..m-1 of a
+ * cycle (which: 0 = Arnoldi SpMV k_step_spmv, 1 = residual prologue,
+ * 2 = CGS update, 3 = Gram-Schmidt panel dots) */
 int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms);
 /* algorithmic bytes of one launch of phase `which` */
 double mpg_engine_phase_bytes(mpg_engine_t e, int which);
