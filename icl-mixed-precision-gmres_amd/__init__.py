@@ -90,6 +90,22 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_phase_bytes.argtypes = [C.c_void_p, C.c_int]
     lib.mpg_engine_phase_bytes.restype = C.c_double
     lib.mpg_engine_destroy.argtypes = [C.c_void_p]
+    P64 = C.POINTER(C.c_int64)
+    P32 = C.POINTER(C.c_int32)
+    lib.mpg_halo_analyze.argtypes = [_I32, _I32, P64, _I32, P32, P32, C.POINTER(C.c_void_p)]
+    lib.mpg_halo_n_ext.argtypes = [C.c_void_p]
+    lib.mpg_halo_n_ext.restype = _I32
+    lib.mpg_halo_recv_count.argtypes = [C.c_void_p, _I32]
+    lib.mpg_halo_recv_count.restype = _I32
+    lib.mpg_halo_recv_rows.argtypes = [C.c_void_p, _I32, P64]
+    lib.mpg_halo_set_send.argtypes = [C.c_void_p, _I32, _I32, P64]
+    lib.mpg_halo_local_cols.argtypes = [C.c_void_p, P32]
+    lib.mpg_halo_free.argtypes = [C.c_void_p]
+    lib.mpg_halo_free.restype = None
+    lib.mpg_rccl_unique_id.argtypes = [C.c_char_p, C.c_int]
+    lib.mpg_engine_create_dist.argtypes = [C.POINTER(SolveArgs), C.c_void_p, C.c_char_p, _I32, _I32,
+                                           C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
+    lib.mpg_solve_loopback.argtypes = [C.POINTER(SolveArgs), _I32, C.POINTER(SolveResult)]
 
 
 # (name, argtypes) for the kernel-level C-ABI, used by the per-kernel tests
@@ -325,20 +341,115 @@ def solve(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, **opts) ->
     return run_solve(host_lib().mpg_solve, args, A.nrows)
 
 
+def row_slice(A: Csr, r0: int, r1: int) -> Csr:
+    """Rows [r0, r1) of A with global column ids (one rank's share)."""
+    base = int(A.rowptr[r0])
+    rp = (A.rowptr[r0:r1 + 1] - base).astype(np.int32)
+    end = int(A.rowptr[r1])
+    return Csr(r1 - r0, A.ncols, rp, A.col[base:end].copy(), A.val[base:end].copy())
+
+
+def nnz_balanced_starts(A: Csr, nranks: int) -> np.ndarray:
+    """Row offsets splitting A into nranks blocks of about equal nnz."""
+    nnz = A.nnz
+    starts = [0]
+    for q in range(1, nranks):
+        starts.append(max(int(np.searchsorted(A.rowptr, nnz * q // nranks, side="left")), starts[-1]))
+    starts.append(A.nrows)
+    return np.array(starts, dtype=np.int64)
+
+
+class HaloPlan:
+    """Halo exchange plan of one rank (include/mpgmres/dist.h). Build with
+    the rank's rows (global columns), exchange recv_rows() with the peers by
+    any transport, then set_send() what each peer needs from this rank."""
+
+    def __init__(self, rank: int, nranks: int, row_starts: np.ndarray, A_local: Csr):
+        self._lib = host_lib()
+        self.rank, self.nranks = rank, nranks
+        self.row_starts = np.ascontiguousarray(row_starts, dtype=np.int64)
+        self.A = A_local
+        self._h = C.c_void_p()
+        st = self._lib.mpg_halo_analyze(rank, nranks, self.row_starts.ctypes.data_as(C.POINTER(C.c_int64)),
+                                        A_local.nrows, A_local.rowptr.ctypes.data_as(C.POINTER(C.c_int32)),
+                                        A_local.col.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(self._h))
+        if st:
+            raise ValueError(f"mpg_halo_analyze failed ({st})")
+
+    @property
+    def n_ext(self) -> int:
+        return int(self._lib.mpg_halo_n_ext(self._h))
+
+    def recv_rows(self, peer: int) -> np.ndarray:
+        cnt = self._lib.mpg_halo_recv_count(self._h, peer)
+        out = np.zeros(max(cnt, 1), dtype=np.int64)
+        self._lib.mpg_halo_recv_rows(self._h, peer, out.ctypes.data_as(C.POINTER(C.c_int64)))
+        return out[:cnt]
+
+    def set_send(self, peer: int, rows) -> None:
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        if self._lib.mpg_halo_set_send(self._h, peer, len(rows), rows.ctypes.data_as(C.POINTER(C.c_int64))):
+            raise ValueError("mpg_halo_set_send: rows outside this rank's block")
+
+    def local_cols(self) -> np.ndarray:
+        out = np.zeros(max(self.A.nnz, 1), dtype=np.int32)
+        self._lib.mpg_halo_local_cols(self._h, out.ctypes.data_as(C.POINTER(C.c_int32)))
+        return out[:self.A.nnz]
+
+    def close(self):
+        if self._h:
+            self._lib.mpg_halo_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def rccl_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    if host_lib().mpg_rccl_unique_id(buf, 128):
+        raise RuntimeError("ncclGetUniqueId failed")
+    return buf.raw
+
+
+def solve_loopback(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, nranks: int = 2, **opts) -> Result:
+    """The row-partitioned engine with `nranks` ranks as threads on one GPU."""
+    opts.pop("engine", None)
+    args, keep = make_args(A, b, x_true, engine="fused", **opts)
+    lib = host_lib()
+    return run_solve(lambda a, r: lib.mpg_solve_loopback(a, nranks, r), args, A.nrows)
+
+
 class Engine:
     """Stepped fused engine (mpg_engine_*): set up once, then advance the
-    restarted solve cycle by cycle — what bench.py times."""
+    restarted solve cycle by cycle — what bench.py times. Engine.distributed
+    builds one rank of a row-partitioned solve over RCCL."""
 
     PHASES = {"spmv": 0, "prologue": 1, "cgs_update": 2, "dots": 3}
 
-    def __init__(self, A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, **opts):
+    def __init__(self, A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, _dist=None, **opts):
         opts.pop("engine", None)
         self._args, self._keep = make_args(A, b, x_true, engine="fused", **opts)
         self._lib = host_lib()
         self._h = C.c_void_p()
         err = C.create_string_buffer(512)
-        if self._lib.mpg_engine_create(C.byref(self._args), C.byref(self._h), err, 512):
+        if _dist is None:
+            st = self._lib.mpg_engine_create(C.byref(self._args), C.byref(self._h), err, 512)
+        else:
+            plan, uid, nranks, rank = _dist
+            self._plan = plan
+            st = self._lib.mpg_engine_create_dist(C.byref(self._args), plan._h, uid, nranks, rank,
+                                                  C.byref(self._h), err, 512)
+        if st:
             raise RuntimeError(f"mpg_engine_create: {err.value.decode()}")
+
+    @classmethod
+    def distributed(cls, A_local: Csr, b_local, x_true_local, plan: HaloPlan, uid: bytes, nranks: int, rank: int,
+                    **opts):
+        return cls(A_local, b_local, x_true_local, _dist=(plan, uid, nranks, rank), **opts)
 
     def run(self, cycles: int) -> tuple:
         done = C.c_int(0)

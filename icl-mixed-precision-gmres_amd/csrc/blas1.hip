@@ -93,6 +93,22 @@ __global__ __launch_bounds__(kBlock) void k_copy_half(int64_t n, const S* __rest
         y[i] = __half_as_ushort(__float2half_rn((float)x[i]));
 }
 
+template <class E>
+__global__ __launch_bounds__(kBlock) void k_gather(int64_t n, const int32_t* __restrict__ idx, const E* __restrict__ x,
+                                                   E* __restrict__ y) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) y[i] = x[idx[i]];
+}
+
+template <class E>
+int gather_impl(mpg_ctx* ctx, int64_t n, const int32_t* idx, const void* x, void* y) {
+    if (!ctx || n < 0) return MPG_ERR_ARG;
+    if (n == 0) return MPG_OK;
+    k_gather<E><<<grid_for(n, 1), kBlock, 0, ctx->stream>>>(n, idx, static_cast<const E*>(x), static_cast<E*>(y));
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
 template <class T>
 __global__ __launch_bounds__(kBlock) void k_fill(T* x, int64_t rows, int64_t cols, int64_t ld, T v) {
     const int64_t total = rows * cols;
@@ -273,6 +289,8 @@ int mpg_copy_f32f16(mpg_ctx_t c, int64_t n, const float* x, uint16_t* y) {
     return MPG_OK;
 }
 
+int mpg_gather_b32(mpg_ctx_t c, int64_t n, const int32_t* idx, const void* x, void* y) { return gather_impl<uint32_t>(c, n, idx, x, y); }
+int mpg_gather_b64(mpg_ctx_t c, int64_t n, const int32_t* idx, const void* x, void* y) { return gather_impl<uint64_t>(c, n, idx, x, y); }
 int mpg_fill_f64(mpg_ctx_t c, double* x, int64_t r, int64_t cl, int64_t ld, double v) { return fill_impl(c, x, r, cl, ld, v); }
 int mpg_fill_f32(mpg_ctx_t c, float* x, int64_t r, int64_t cl, int64_t ld, float v) { return fill_impl(c, x, r, cl, ld, v); }
 int mpg_gdmv_f64(mpg_ctx_t c, int64_t n, double a, const double* d, const double* x, double b, double* y) { return gdmv_impl(c, n, a, d, x, b, y); }

@@ -71,28 +71,29 @@ __global__ __launch_bounds__(kBlock) void k_rowabs_max(int32_t rows, const int32
     if (threadIdx.x == 0) partial[blockIdx.x] = bm;
 }
 
-template <class T>
-__global__ __launch_bounds__(1024) void k_alpha(int nparts, const double* __restrict__ partial, T* __restrict__ alpha_out) {
+__global__ __launch_bounds__(1024) void k_rowmax_final(int nparts, const double* __restrict__ partial,
+                                                       double* __restrict__ out) {
     __shared__ double scratch[1024 / kWave];
     double v = threadIdx.x < nparts ? partial[threadIdx.x] : 0.0;
     double m = block_max<1024>(v, scratch);
-    if (threadIdx.x == 0) {
-        T a = (T)m;                 // exact: m is one of the T row sums
-        a *= (T)FLT_EPSILON;        // alpha *= numeric_limits<float>::epsilon()
-        *alpha_out = a;
-    }
+    if (threadIdx.x == 0) *out = m;  // exact: one of the row sums
 }
 
+// rows are the local rows; columns >= rows are halo entries (row-partitioned
+// matrix), which sort before the own columns when their global id is lower
 template <class T>
 __global__ __launch_bounds__(kBlock) void k_jacobi_diag(int32_t rows, int64_t nnz, const int32_t* __restrict__ rowptr,
                                                         const int32_t* __restrict__ col, const T* __restrict__ val,
-                                                        const T* __restrict__ alpha_p, T* __restrict__ diag) {
-    const T alpha = *alpha_p;
+                                                        const double* __restrict__ rowmax, T* __restrict__ diag) {
+    T alpha = (T)*rowmax;
+    alpha *= (T)FLT_EPSILON;  // alpha *= numeric_limits<float>::epsilon() (types.hpp:417)
     const int stride = gridDim.x * kBlock;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < rows; i += stride) {
         int64_t j = rowptr[i];
-        // `while (inds(j) < i) ++j;` — bounded here so a row without a
-        // diagonal cannot run off the end of the arrays.
+        // `while (inds(j) < i) ++j;` (types.hpp:422-425), bounded so a row
+        // without a diagonal cannot run off the arrays; a leading run of
+        // lower-numbered halo columns is skipped first
+        while (j < nnz - 1 && j < rowptr[i + 1] - 1 && col[j] >= rows) ++j;
         while (j < nnz - 1 && col[j] < i) ++j;
         const T v = val[j];
         if (v >= T(0)) diag[i] = T(1) / ((v < alpha) ? alpha : v);
@@ -101,19 +102,34 @@ __global__ __launch_bounds__(kBlock) void k_jacobi_diag(int32_t rows, int64_t nn
 }
 
 template <class T>
+int rowmax_impl(mpg_ctx* ctx, mpg_csr* A, const T* vals, double* out) {
+    if (!ctx || !A || !out) return MPG_ERR_ARG;
+    int g = grid_for(A->rows > 0 ? A->rows : 1, 1, kMaxRedBlocks);
+    k_rowabs_max<T><<<g, kBlock, 0, ctx->stream>>>(A->rows, A->rowptr, vals, ctx->red_ws);
+    MPG_LAUNCH_CHECK(ctx);
+    k_rowmax_final<<<1, 1024, 0, ctx->stream>>>(g, ctx->red_ws, out);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+template <class T>
+int jdiag_impl(mpg_ctx* ctx, mpg_csr* A, const T* vals, const double* rowmax, T* diag) {
+    if (!ctx || !A || !rowmax) return MPG_ERR_ARG;
+    if (A->rows == 0) return MPG_OK;
+    k_jacobi_diag<T><<<grid_for(A->rows, 1), kBlock, 0, ctx->stream>>>(A->rows, A->nnz, A->rowptr, A->col, vals,
+                                                                      rowmax, diag);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+template <class T>
 int jacobi_impl(mpg_ctx* ctx, mpg_csr* A, const T* vals, T* diag) {
     if (!ctx || !A) return MPG_ERR_ARG;
     if (A->rows == 0) return MPG_OK;
-    int g = grid_for(A->rows, 1, kMaxRedBlocks);
-    k_rowabs_max<T><<<g, kBlock, 0, ctx->stream>>>(A->rows, A->rowptr, vals, ctx->red_ws);
-    MPG_LAUNCH_CHECK(ctx);
-    T* alpha = reinterpret_cast<T*>(ctx->red_ws + (size_t)kMaxRedBlocks * kGemvMaxCols + 16);
-    k_alpha<T><<<1, 1024, 0, ctx->stream>>>(g, ctx->red_ws, alpha);
-    MPG_LAUNCH_CHECK(ctx);
-    k_jacobi_diag<T><<<grid_for(A->rows, 1), kBlock, 0, ctx->stream>>>(A->rows, A->nnz, A->rowptr, A->col, vals,
-                                                                      alpha, diag);
-    MPG_LAUNCH_CHECK(ctx);
-    return MPG_OK;
+    double* rowmax = ctx->red_ws + (size_t)kMaxRedBlocks * kGemvMaxCols + 16;
+    int st = rowmax_impl<T>(ctx, A, vals, rowmax);
+    if (st) return st;
+    return jdiag_impl<T>(ctx, A, vals, rowmax, diag);
 }
 
 }  // namespace
@@ -179,6 +195,10 @@ int mpg_csr_spmv_f16f32(mpg_ctx_t c, mpg_csr_t A, float alpha, const uint16_t* v
     return spmv_impl<uint16_t, float>(c, A, alpha, vals, x, beta, y);
 }
 
+int mpg_jacobi_rowmax_f64(mpg_ctx_t c, mpg_csr_t A, const double* vals, double* out) { return rowmax_impl<double>(c, A, vals, out); }
+int mpg_jacobi_rowmax_f32(mpg_ctx_t c, mpg_csr_t A, const float* vals, double* out) { return rowmax_impl<float>(c, A, vals, out); }
+int mpg_jacobi_diag_f64(mpg_ctx_t c, mpg_csr_t A, const double* vals, const double* rm, double* d) { return jdiag_impl<double>(c, A, vals, rm, d); }
+int mpg_jacobi_diag_f32(mpg_ctx_t c, mpg_csr_t A, const float* vals, const double* rm, float* d) { return jdiag_impl<float>(c, A, vals, rm, d); }
 int mpg_jacobi_setup_f64(mpg_ctx_t c, mpg_csr_t A, const double* vals, double* diag) { return jacobi_impl<double>(c, A, vals, diag); }
 int mpg_jacobi_setup_f32(mpg_ctx_t c, mpg_csr_t A, const float* vals, float* diag) { return jacobi_impl<float>(c, A, vals, diag); }
 

@@ -1,0 +1,417 @@
+// Row-partitioned multi-GPU support (include/mpgmres/dist.h): halo plan,
+// RCCL communicator, single-device loopback communicator (P ranks as
+// threads, for tests), and the distributed engine entry points.
+#include "mpgmres/dist.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "fused_gmres.hpp"
+#include "gmres.hpp"
+#include "types_hip.hpp"
+
+struct mpg_halo {
+    int rank = 0, nranks = 1;
+    std::vector<int64_t> row_starts;
+    int n_local = 0;
+    std::vector<int32_t> col_local;
+    std::vector<int64_t> halo_global;             // sorted external columns
+    std::vector<int32_t> recv_off, recv_cnt;      // per peer, into the halo segment
+    std::vector<std::vector<int32_t>> send_local; // per peer, local rows to send
+    std::vector<bool> send_set;
+};
+
+namespace mpg {
+namespace {
+
+void nck(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(r));
+}
+void hck(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// ---------------------------------------------------------------- RCCL
+class RcclComm : public Comm {
+    ncclComm_t comm_ = nullptr;
+    int rank_, size_, n_local_;
+    mpg_ctx_t ctx_;
+    std::vector<int32_t> recv_off_, recv_cnt_;
+    std::vector<std::unique_ptr<DevMem>> send_idx_, send_buf_;
+    std::vector<int32_t> send_cnt_;
+
+public:
+    RcclComm(mpg_ctx_t ctx, const mpg_halo& h, const char* id, int nranks, int rank)
+        : rank_(rank), size_(nranks), n_local_(h.n_local), ctx_(ctx), recv_off_(h.recv_off), recv_cnt_(h.recv_cnt) {
+        ncclUniqueId uid;
+        std::memcpy(&uid, id, sizeof uid);
+        nck(ncclCommInitRank(&comm_, nranks, uid, rank), "ncclCommInitRank");
+        send_cnt_.assign(nranks, 0);
+        send_idx_.resize(nranks);
+        send_buf_.resize(nranks);
+        for (int q = 0; q < nranks; ++q) {
+            const auto& rows = h.send_local[q];
+            send_cnt_[q] = (int32_t)rows.size();
+            if (rows.empty()) continue;
+            send_idx_[q] = std::make_unique<DevMem>(ctx, rows.size() * 4);
+            check(mpg_memcpy_h2d(ctx, send_idx_[q]->p, rows.data(), rows.size() * 4), "h2d", ctx);
+            send_buf_[q] = std::make_unique<DevMem>(ctx, rows.size() * 8);
+        }
+    }
+    ~RcclComm() override {
+        if (comm_) ncclCommDestroy(comm_);
+    }
+    int size() const override { return size_; }
+    int rank() const override { return rank_; }
+    bool capturable() const override { return true; }
+    void allreduce_sum(double* dev, int count, hipStream_t s) override {
+        nck(ncclAllReduce(dev, dev, (size_t)count, ncclFloat64, ncclSum, comm_, s), "allreduce");
+    }
+    void allreduce_max(double* dev, int count, hipStream_t s) override {
+        nck(ncclAllReduce(dev, dev, (size_t)count, ncclFloat64, ncclMax, comm_, s), "allreduce max");
+    }
+    void halo(void* vec, int eb, hipStream_t s) override {
+        for (int q = 0; q < size_; ++q) {
+            if (!send_cnt_[q]) continue;
+            const int st = eb == 8 ? mpg_gather_b64(ctx_, send_cnt_[q], send_idx_[q]->as<int32_t>(), vec, send_buf_[q]->p)
+                                   : mpg_gather_b32(ctx_, send_cnt_[q], send_idx_[q]->as<int32_t>(), vec, send_buf_[q]->p);
+            check(st, "halo pack", ctx_);
+        }
+        nck(ncclGroupStart(), "group start");
+        for (int q = 0; q < size_; ++q) {
+            if (send_cnt_[q]) nck(ncclSend(send_buf_[q]->p, (size_t)send_cnt_[q] * eb, ncclUint8, q, comm_, s), "send");
+            if (recv_cnt_[q]) {
+                char* dst = static_cast<char*>(vec) + ((size_t)n_local_ + recv_off_[q]) * eb;
+                nck(ncclRecv(dst, (size_t)recv_cnt_[q] * eb, ncclUint8, q, comm_, s), "recv");
+            }
+        }
+        nck(ncclGroupEnd(), "group end");
+    }
+};
+
+// ---------------------------------------------------------------- loopback
+struct Hub {
+    int P;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    int64_t generation = 0;
+    bool aborted = false;
+    std::vector<void*> ptrs;
+    std::vector<std::vector<double>> staging;
+    explicit Hub(int p) : P(p), ptrs(p), staging(p) {}
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (aborted) throw std::runtime_error("loopback: another rank failed");
+        const int64_t gen = generation;
+        if (++arrived == P) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != gen || aborted; });
+            if (aborted) throw std::runtime_error("loopback: another rank failed");
+        }
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(mu);
+        aborted = true;
+        cv.notify_all();
+    }
+};
+
+class LoopbackComm : public Comm {
+    Hub& hub_;
+    int rank_, n_local_;
+    mpg_ctx_t ctx_;
+    std::vector<int32_t> recv_off_, recv_cnt_;
+    std::vector<std::unique_ptr<DevMem>> src_idx_;  // per peer: indices in the peer's numbering
+
+public:
+    LoopbackComm(Hub& hub, mpg_ctx_t ctx, const mpg_halo& h)
+        : hub_(hub), rank_(h.rank), n_local_(h.n_local), ctx_(ctx), recv_off_(h.recv_off), recv_cnt_(h.recv_cnt) {
+        src_idx_.resize(h.nranks);
+        for (int q = 0; q < h.nranks; ++q) {
+            if (!recv_cnt_[q]) continue;
+            std::vector<int32_t> idx(recv_cnt_[q]);
+            for (int i = 0; i < recv_cnt_[q]; ++i)
+                idx[i] = (int32_t)(h.halo_global[recv_off_[q] + i] - h.row_starts[q]);
+            src_idx_[q] = std::make_unique<DevMem>(ctx, idx.size() * 4);
+            check(mpg_memcpy_h2d(ctx, src_idx_[q]->p, idx.data(), idx.size() * 4), "h2d", ctx);
+        }
+    }
+    int size() const override { return hub_.P; }
+    int rank() const override { return rank_; }
+    bool capturable() const override { return false; }
+    void allreduce_sum(double* dev, int count, hipStream_t s) override { reduce(dev, count, s, false); }
+    void allreduce_max(double* dev, int count, hipStream_t s) override { reduce(dev, count, s, true); }
+    void halo(void* vec, int eb, hipStream_t s) override {
+        hck(hipStreamSynchronize(s), "sync");
+        hub_.ptrs[rank_] = vec;
+        hub_.barrier();
+        for (int q = 0; q < hub_.P; ++q) {
+            if (!recv_cnt_[q]) continue;
+            char* dst = static_cast<char*>(vec) + ((size_t)n_local_ + recv_off_[q]) * eb;
+            const int st = eb == 8 ? mpg_gather_b64(ctx_, recv_cnt_[q], src_idx_[q]->as<int32_t>(), hub_.ptrs[q], dst)
+                                   : mpg_gather_b32(ctx_, recv_cnt_[q], src_idx_[q]->as<int32_t>(), hub_.ptrs[q], dst);
+            check(st, "loopback halo", ctx_);
+        }
+        hck(hipStreamSynchronize(s), "sync");
+        hub_.barrier();
+    }
+
+private:
+    void reduce(double* dev, int count, hipStream_t s, bool max) {
+        auto& mine = hub_.staging[rank_];
+        mine.resize((size_t)count);
+        hck(hipMemcpyAsync(mine.data(), dev, (size_t)count * 8, hipMemcpyDeviceToHost, s), "d2h");
+        hck(hipStreamSynchronize(s), "sync");
+        hub_.barrier();
+        std::vector<double> out(hub_.staging[0]);
+        for (int q = 1; q < hub_.P; ++q)  // rank order: identical on every rank
+            for (int c = 0; c < count; ++c)
+                out[(size_t)c] = max ? std::max(out[(size_t)c], hub_.staging[q][(size_t)c])
+                                     : out[(size_t)c] + hub_.staging[q][(size_t)c];
+        hub_.barrier();
+        hck(hipMemcpyAsync(dev, out.data(), (size_t)count * 8, hipMemcpyHostToDevice, s), "h2d");
+        hck(hipStreamSynchronize(s), "sync");
+    }
+};
+
+std::vector<int64_t> nnz_balanced_starts(int n, const int32_t* rowptr, int P) {
+    std::vector<int64_t> st((size_t)P + 1, 0);
+    const int64_t nnz = rowptr[n];
+    int r = 0;
+    for (int q = 1; q < P; ++q) {
+        const int64_t target = nnz * q / P;
+        while (r < n && rowptr[r] < target) ++r;
+        st[(size_t)q] = std::max<int64_t>(r, st[(size_t)q - 1]);
+    }
+    st[(size_t)P] = n;
+    return st;
+}
+
+}  // namespace
+}  // namespace mpg
+
+using namespace mpg;
+
+extern "C" {
+
+int mpg_halo_analyze(int32_t rank, int32_t nranks, const int64_t* row_starts, int32_t n_local, const int32_t* rowptr,
+                     const int32_t* col_global, mpg_halo_t* out) {
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks || !row_starts || !rowptr || n_local < 0) return MPG_ERR_ARG;
+    auto* h = new mpg_halo();
+    h->rank = rank;
+    h->nranks = nranks;
+    h->row_starts.assign(row_starts, row_starts + nranks + 1);
+    h->n_local = n_local;
+    const int64_t r0 = row_starts[rank], r1 = row_starts[rank + 1];
+    if (r1 - r0 != n_local) {
+        delete h;
+        return MPG_ERR_ARG;
+    }
+    const int64_t nnz = rowptr[n_local];
+    for (int64_t k = 0; k < nnz; ++k) {
+        const int64_t c = col_global[k];
+        if (c < r0 || c >= r1) h->halo_global.push_back(c);
+    }
+    std::sort(h->halo_global.begin(), h->halo_global.end());
+    h->halo_global.erase(std::unique(h->halo_global.begin(), h->halo_global.end()), h->halo_global.end());
+    h->col_local.resize((size_t)nnz);
+    for (int64_t k = 0; k < nnz; ++k) {
+        const int64_t c = col_global[k];
+        if (c >= r0 && c < r1) {
+            h->col_local[(size_t)k] = (int32_t)(c - r0);
+        } else {
+            const auto it = std::lower_bound(h->halo_global.begin(), h->halo_global.end(), c);
+            h->col_local[(size_t)k] = n_local + (int32_t)(it - h->halo_global.begin());
+        }
+    }
+    h->recv_off.assign(nranks, 0);
+    h->recv_cnt.assign(nranks, 0);
+    size_t pos = 0;
+    for (int q = 0; q < nranks; ++q) {
+        h->recv_off[q] = (int32_t)pos;
+        while (pos < h->halo_global.size() && h->halo_global[pos] < row_starts[q + 1]) ++pos;
+        h->recv_cnt[q] = (int32_t)(pos - h->recv_off[q]);
+    }
+    h->send_local.assign(nranks, {});
+    h->send_set.assign(nranks, false);
+    h->send_set[rank] = true;
+    *out = h;
+    return MPG_OK;
+}
+
+int32_t mpg_halo_n_ext(mpg_halo_t h) { return h ? h->n_local + (int32_t)h->halo_global.size() : -1; }
+int32_t mpg_halo_recv_count(mpg_halo_t h, int32_t q) {
+    return h && q >= 0 && q < h->nranks ? h->recv_cnt[q] : -1;
+}
+int mpg_halo_recv_rows(mpg_halo_t h, int32_t q, int64_t* rows) {
+    if (!h || q < 0 || q >= h->nranks || (!rows && h->recv_cnt[q])) return MPG_ERR_ARG;
+    for (int i = 0; i < h->recv_cnt[q]; ++i) rows[i] = h->halo_global[(size_t)h->recv_off[q] + i];
+    return MPG_OK;
+}
+int mpg_halo_set_send(mpg_halo_t h, int32_t q, int32_t count, const int64_t* rows) {
+    if (!h || q < 0 || q >= h->nranks || count < 0 || (count && !rows)) return MPG_ERR_ARG;
+    const int64_t r0 = h->row_starts[h->rank], r1 = h->row_starts[h->rank + 1];
+    auto& v = h->send_local[q];
+    v.resize((size_t)count);
+    for (int i = 0; i < count; ++i) {
+        if (rows[i] < r0 || rows[i] >= r1) return MPG_ERR_ARG;
+        v[(size_t)i] = (int32_t)(rows[i] - r0);
+    }
+    h->send_set[q] = true;
+    return MPG_OK;
+}
+int mpg_halo_local_cols(mpg_halo_t h, int32_t* out) {
+    if (!h || !out) return MPG_ERR_ARG;
+    std::copy(h->col_local.begin(), h->col_local.end(), out);
+    return MPG_OK;
+}
+void mpg_halo_free(mpg_halo_t h) { delete h; }
+
+int mpg_rccl_unique_id(char* id_out, int len) {
+    if (!id_out || len < (int)sizeof(ncclUniqueId)) return MPG_ERR_ARG;
+    ncclUniqueId uid;
+    if (ncclGetUniqueId(&uid) != ncclSuccess) return MPG_ERR_RCCL;
+    std::memcpy(id_out, &uid, sizeof uid);
+    return MPG_OK;
+}
+
+int mpg_engine_create_dist(const mpg_solve_args* a, mpg_halo_t plan, const char* id, int32_t nranks, int32_t rank,
+                           mpg_engine_t* out, char* err, int errlen) {
+    if (!a || !plan || !id || !out || plan->nranks != nranks || plan->rank != rank || plan->n_local != a->n)
+        return MPG_ERR_ARG;
+    for (int q = 0; q < nranks; ++q)
+        if (!plan->send_set[q]) {
+            if (err) std::snprintf(err, (size_t)errlen, "halo plan: send list of peer %d not set", q);
+            return MPG_ERR_ARG;
+        }
+    *out = nullptr;
+    auto* e = new mpg_engine();
+    try {
+        set_quiet(!a->verbose || rank != 0);
+        check(mpg_ctx_create(a->device, &e->ctx), "mpg_ctx_create");
+        ScopedContext scope(e->ctx);
+        e->comm = std::make_unique<RcclComm>(e->ctx, *plan, id, nranks, rank);
+        mpg_solve_args local = *a;
+        local.col = plan->col_local.data();
+        e->eng = std::make_unique<FusedEngine>(e->ctx, local, e->comm.get(), mpg_halo_n_ext(plan));
+    } catch (const std::exception& ex) {
+        if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", ex.what());
+        mpg_engine_destroy(e);
+        return MPG_ERR_RCCL;
+    }
+    *out = e;
+    return MPG_OK;
+}
+
+int mpg_solve_loopback(const mpg_solve_args* a, int32_t P, mpg_solve_result* r) {
+    if (!a || !r || P < 1 || a->n < P) return MPG_ERR_ARG;
+    r->status = MPG_RESULT_ERROR;
+    r->message[0] = 0;
+    const int n = a->n;
+    const auto starts = nnz_balanced_starts(n, a->rowptr, P);
+    // per-rank row slices and halo plans
+    std::vector<std::vector<int32_t>> rp(P), cg(P);
+    std::vector<mpg_halo_t> plans(P, nullptr);
+    for (int q = 0; q < P; ++q) {
+        const int64_t r0 = starts[q], r1 = starts[q + 1];
+        const int32_t base = a->rowptr[r0];
+        rp[q].resize((size_t)(r1 - r0) + 1);
+        for (int64_t i = r0; i <= r1; ++i) rp[q][(size_t)(i - r0)] = a->rowptr[i] - base;
+        cg[q].assign(a->col + base, a->col + a->rowptr[r1]);
+        if (mpg_halo_analyze(q, P, starts.data(), (int32_t)(r1 - r0), rp[q].data(), cg[q].data(), &plans[q]))
+            return MPG_ERR_ARG;
+    }
+    for (int q = 0; q < P; ++q)
+        for (int p = 0; p < P; ++p) {
+            if (p == q) continue;
+            const int c = mpg_halo_recv_count(plans[p], q);  // what p needs from q
+            std::vector<int64_t> rows((size_t)c);
+            mpg_halo_recv_rows(plans[p], q, rows.data());
+            mpg_halo_set_send(plans[q], p, c, rows.data());
+        }
+    Hub hub(P);
+    std::vector<std::string> errors(P);
+    std::vector<std::thread> th;
+    for (int q = 0; q < P; ++q) {
+        th.emplace_back([&, q] {
+            mpg_ctx_t ctx = nullptr;
+            try {
+                check(mpg_ctx_create(a->device, &ctx), "mpg_ctx_create");
+                ScopedContext scope(ctx);
+                {
+                    LoopbackComm comm(hub, ctx, *plans[q]);
+                    const int64_t r0 = starts[q], r1 = starts[q + 1];
+                    const int32_t base = a->rowptr[r0];
+                    mpg_solve_args la = *a;
+                    la.n = (int32_t)(r1 - r0);
+                    la.nnz = rp[q].back();
+                    la.rowptr = rp[q].data();
+                    la.col = plans[q]->col_local.data();
+                    la.val = a->val + base;
+                    la.b = a->b + r0;
+                    la.x_true = a->x_true ? a->x_true + r0 : nullptr;
+                    if (q != 0) la.verbose = 0;
+                    FusedEngine e(ctx, la, &comm, mpg_halo_n_ext(plans[q]));
+                    bool done = false;
+                    while (!done) e.run(1 << 20, done);
+                    e.sync();
+                    mpg_solve_result mine{};
+                    mine.x_out = r->x_out ? r->x_out + r0 : nullptr;
+                    e.finish_report(&mine);
+                    if (q == 0) {
+                        r->status = e.status;
+                        r->restarts = e.restarts;
+                        r->inner_k = e.inner_k;
+                        r->total_iters = (int64_t)e.total_iters();
+                        r->minvb_norm = e.minvb_norm;
+                        r->res_norm = mine.res_norm;
+                        r->err_norm = mine.err_norm;
+                        r->setup_seconds = e.setup_seconds;
+                        r->n_cycles = (int64_t)e.cycles.size();
+                        for (size_t c = 0; c < e.cycles.size() && (int64_t)c < r->cycle_cap; ++c) {
+                            if (r->cyc_r_norm) r->cyc_r_norm[c] = e.cycles[c].r_norm;
+                            if (r->cyc_normalization) r->cyc_normalization[c] = e.cycles[c].normalization;
+                            if (r->cyc_beta) r->cyc_beta[c] = e.cycles[c].beta;
+                        }
+                        r->n_steps = (int64_t)e.step_res.size();
+                        for (size_t s = 0; s < e.step_res.size() && (int64_t)s < r->step_cap; ++s) {
+                            if (r->step_res) r->step_res[s] = e.step_res[s];
+                            if (r->step_cycle) r->step_cycle[s] = e.step_cycle[s];
+                        }
+                    }
+                }
+            } catch (const std::exception& ex) {
+                errors[q] = ex.what();
+                hub.abort();
+            }
+            if (ctx) mpg_ctx_destroy(ctx);
+        });
+    }
+    for (auto& t : th) t.join();
+    for (auto p : plans) mpg_halo_free(p);
+    for (int q = 0; q < P; ++q)
+        if (!errors[q].empty()) {
+            r->status = MPG_RESULT_ERROR;
+            std::snprintf(r->message, sizeof r->message, "rank %d: %s", q, errors[q].c_str());
+            return MPG_ERR_ARG;
+        }
+    return MPG_OK;
+}
+
+}  // extern "C"

@@ -166,22 +166,26 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
 
     // Jacobi<P>(A): fp64 original A for P = double (baseline), else the A
     // converted to float (types.hpp:393-431 on SparseMatrix<P>)
+    // (max row sum all-reduced across ranks: ||A||_inf of the whole matrix)
+    I.scal = DevMem(ctx, 64);
     if (a.prec == MPG_PREC_JACOBI) {
         I.diag = DevMem(ctx, (size_t)I.n * dsize(ty.P) + 16);
+        double* rowmax = I.scal.as<double>() + 4;
         if (ty.P == MPG_F64) {
-            check(mpg_jacobi_setup_f64(ctx, I.csr, I.val64.as<double>(), I.diag.as<double>()), "jacobi", ctx);
+            check(mpg_jacobi_rowmax_f64(ctx, I.csr, I.val64.as<double>(), rowmax), "jacobi", ctx);
+            if (comm) comm->allreduce_max(rowmax, 1, I.stream());
+            check(mpg_jacobi_diag_f64(ctx, I.csr, I.val64.as<double>(), rowmax, I.diag.as<double>()), "jacobi", ctx);
         } else {
             DevMem f32(ctx, std::max<size_t>(nz, 1) * 4);
             I.cast(I.val64.p, MPG_F64, f32.p, MPG_F32, (int64_t)nz);
-            check(mpg_jacobi_setup_f32(ctx, I.csr, f32.as<float>(), I.diag.as<float>()), "jacobi", ctx);
+            check(mpg_jacobi_rowmax_f32(ctx, I.csr, f32.as<float>(), rowmax), "jacobi", ctx);
+            if (comm) comm->allreduce_max(rowmax, 1, I.stream());
+            check(mpg_jacobi_diag_f32(ctx, I.csr, f32.as<float>(), rowmax, I.diag.as<float>()), "jacobi", ctx);
             check(mpg_ctx_sync(ctx), "sync", ctx);
         }
-        if (comm && comm->size() > 1)
-            throw std::invalid_argument("Jacobi on a row-partitioned matrix needs a global ||A||_inf (not yet)");
     }
 
     // b (outer type), x = 0 (outer type, with halo tail)
-    I.scal = DevMem(ctx, 64);
     DevMem b64(ctx, (size_t)I.n * 8 + 8);
     check(mpg_memcpy_h2d(ctx, b64.p, a.b, (size_t)I.n * 8), "h2d", ctx);
     if (ty.X == MPG_F64) {
@@ -254,7 +258,7 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     conv_->total_iters = 0;
 
     const char* env = std::getenv("MPG_NO_GRAPH");
-    I.use_graph = !(env && *env == '1');
+    I.use_graph = !(env && *env == '1') && (!comm || comm->capturable());
     check(mpg_ctx_sync(ctx), "sync", ctx);
     setup_seconds = std::chrono::duration<double>(clk::now() - t0).count();
     prologue();
@@ -532,10 +536,6 @@ int solve_fused(const mpg_solve_args& a, mpg_solve_result* r) {
 }  // namespace mpg
 
 // ---------------------------------------------------------------- engine C-ABI
-struct mpg_engine {
-    mpg_ctx_t ctx = nullptr;
-    std::unique_ptr<mpg::FusedEngine> eng;
-};
 
 extern "C" {
 
@@ -598,6 +598,7 @@ int mpg_engine_destroy(mpg_engine_t e) {
         {
             mpg::ScopedContext scope(e->ctx);
             e->eng.reset();
+            e->comm.reset();
         }
         mpg_ctx_destroy(e->ctx);
     }

@@ -32,10 +32,13 @@ public:
     virtual ~Comm() {}
     virtual int size() const = 0;
     virtual int rank() const = 0;
-    // in-place sum of `count` doubles across ranks (bit-identical on every rank)
+    // in-place sum / max of `count` doubles across ranks (bit-identical on every rank)
     virtual void allreduce_sum(double* dev, int count, hipStream_t s) = 0;
+    virtual void allreduce_max(double* dev, int count, hipStream_t s) = 0;
     // fill the halo tail [n, n_ext) of a vector of `elem_bytes` elements
     virtual void halo(void* dev_vec, int elem_bytes, hipStream_t s) = 0;
+    // whether the collectives may be captured into a hipGraph (no host waits)
+    virtual bool capturable() const = 0;
 };
 
 // RAII device buffer through the C-ABI allocator
@@ -96,5 +99,12 @@ private:
 int solve_fused(const mpg_solve_args& args, mpg_solve_result* result);
 
 }  // namespace mpg
+
+// handle behind mpg_engine_t (solve.h / dist.h)
+struct mpg_engine {
+    mpg_ctx_t ctx = nullptr;
+    std::unique_ptr<mpg::Comm> comm;          // declared first: destroyed after eng
+    std::unique_ptr<mpg::FusedEngine> eng;
+};
 
 #endif  // MPGMRES_FUSED_GMRES_HPP

@@ -110,6 +110,10 @@ int mpg_copy_f64f32(mpg_ctx_t ctx, int64_t n, const double* x, float* y);
 int mpg_copy_f32f64(mpg_ctx_t ctx, int64_t n, const float* x, double* y);
 int mpg_copy_f64f16(mpg_ctx_t ctx, int64_t n, const double* x, uint16_t* y_half);
 int mpg_copy_f32f16(mpg_ctx_t ctx, int64_t n, const float* x, uint16_t* y_half);
+/* y[i] = x[idx[i]] for i < n, elements of 4 or 8 bytes (halo packing of a
+ * row-partitioned vector before the neighbour exchange) */
+int mpg_gather_b32(mpg_ctx_t ctx, int64_t n, const int32_t* idx, const void* x, void* y);
+int mpg_gather_b64(mpg_ctx_t ctx, int64_t n, const int32_t* idx, const void* x, void* y);
 /* fill (kernels.hpp:88-101): strided 2-D form covers Scalar/Vect/MultiVect */
 int mpg_fill_f64(mpg_ctx_t ctx, double* x, int64_t rows, int64_t cols, int64_t ld, double value);
 int mpg_fill_f32(mpg_ctx_t ctx, float* x, int64_t rows, int64_t cols, int64_t ld, float value);
@@ -173,6 +177,12 @@ int mpg_csr_spmv_f16f32(mpg_ctx_t ctx, mpg_csr_t A, float alpha, const uint16_t*
  * entry of row i whose column >= i (types.hpp:422-425). */
 int mpg_jacobi_setup_f64(mpg_ctx_t ctx, mpg_csr_t A, const double* vals, double* diag_out);
 int mpg_jacobi_setup_f32(mpg_ctx_t ctx, mpg_csr_t A, const float* vals, float* diag_out);
+/* the two halves, for a row-partitioned matrix whose max row sum is
+ * all-reduced (max) between them; columns >= rows are halo entries */
+int mpg_jacobi_rowmax_f64(mpg_ctx_t ctx, mpg_csr_t A, const double* vals, double* rowmax_dev);
+int mpg_jacobi_rowmax_f32(mpg_ctx_t ctx, mpg_csr_t A, const float* vals, double* rowmax_dev);
+int mpg_jacobi_diag_f64(mpg_ctx_t ctx, mpg_csr_t A, const double* vals, const double* rowmax_dev, double* diag_out);
+int mpg_jacobi_diag_f32(mpg_ctx_t ctx, mpg_csr_t A, const float* vals, const double* rowmax_dev, float* diag_out);
 
 #ifdef __cplusplus
 }

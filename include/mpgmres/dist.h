@@ -1,0 +1,67 @@
+/*
+ * mpgmres row-partitioned multi-GPU C-ABI (libmpgmres_host.so).
+ *
+ * The reference runs on one device only (no MPI/NCCL). Here the
+ * CSR matrix is split into contiguous row blocks, one per rank (one process
+ * and one GPU per rank). Each rank keeps its rows with columns remapped to
+ * [0, n_local) for its own rows and [n_local, n_ext) for the "halo" entries
+ * owned by other ranks. Per Arnoldi step a rank exchanges only those halo
+ * entries with the ranks that own them (RCCL grouped send/recv over xGMI —
+ * for a banded matrix a handful of values per neighbour) and all-reduces the
+ * fp64 partial sums of the Gram-Schmidt dots and norms, so every rank holds
+ * bit-identical H, Givens and convergence scalars and takes the same
+ * decisions.
+ *
+ * Building the plan is transport-neutral and needs no GPU:
+ *   mpg_halo_analyze        this rank's rows -> which rows it needs from whom
+ *   (exchange the needs with any transport: torch.distributed, MPI, ...)
+ *   mpg_halo_set_send       what each peer needs from this rank
+ *   mpg_halo_local_cols     the remapped column array
+ * then mpg_engine_create_dist builds the fused engine with an RCCL
+ * communicator. mpg_solve_loopback runs P ranks as threads sharing one GPU
+ * (device-to-device copies instead of RCCL) to test the partitioned path on
+ * a single device.
+ */
+#ifndef MPGMRES_DIST_H
+#define MPGMRES_DIST_H
+
+#include <stdint.h>
+
+#include "mpgmres/solve.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mpg_halo* mpg_halo_t;
+
+/* row_starts: nranks + 1 global row offsets; rowptr/col_global: this rank's
+ * n_local rows with global column ids (sorted per row). */
+int mpg_halo_analyze(int32_t rank, int32_t nranks, const int64_t* row_starts, int32_t n_local,
+                     const int32_t* rowptr, const int32_t* col_global, mpg_halo_t* out);
+int32_t mpg_halo_n_ext(mpg_halo_t h);
+int32_t mpg_halo_recv_count(mpg_halo_t h, int32_t peer);
+/* global ids (ascending) of the rows this rank needs from `peer` */
+int mpg_halo_recv_rows(mpg_halo_t h, int32_t peer, int64_t* rows_out);
+/* global ids of this rank's rows that `peer` needs (its recv list for us) */
+int mpg_halo_set_send(mpg_halo_t h, int32_t peer, int32_t count, const int64_t* rows);
+/* column array remapped to local ids (nnz entries) */
+int mpg_halo_local_cols(mpg_halo_t h, int32_t* col_local_out);
+void mpg_halo_free(mpg_halo_t h);
+
+/* RCCL unique id (128 bytes) made by one rank and broadcast by the caller */
+int mpg_rccl_unique_id(char* id_out, int len);
+
+/* args: this rank's rows with GLOBAL column ids, local b and x_true; the
+ * plan must have every peer's send list set. Collective over all ranks. */
+int mpg_engine_create_dist(const mpg_solve_args* args, mpg_halo_t plan, const char* rccl_id, int32_t nranks,
+                           int32_t rank, mpg_engine_t* out, char* err, int errlen);
+
+/* P ranks as threads on one device, rows split evenly by nnz; the result
+ * (history, counts, norms, x gathered) matches mpg_solve's. */
+int mpg_solve_loopback(const mpg_solve_args* args, int32_t nranks, mpg_solve_result* result);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPGMRES_DIST_H */
