@@ -85,8 +85,15 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # MPG_BENCH_SHARED_GPU=1 rehearses the multi-rank path with every rank on
+        # device 0 (torch side on gloo); the default is one GPU per rank over RCCL
+        if os.environ.get("MPG_BENCH_SHARED_GPU") == "1":
+            local_rank = 0
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     # global BAND matrix of world * n_local rows; this rank owns one row block
     n = args.n_local * world
@@ -129,7 +136,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     iters = eng.total_iters - it0

@@ -371,17 +371,30 @@ int FusedEngine::run(int max_cycles, bool& done) {
             return ran;
         }
         if (!stepwise) {
-            if (I.use_graph) {
-                if (!I.graph_exec) {
-                    hipck(hipStreamBeginCapture(I.stream(), hipStreamCaptureModeThreadLocal), "begin capture");
+            if (I.use_graph && !I.graph_exec) {
+                // capture once; if the runtime refuses (e.g. a collective that
+                // cannot be captured) fall back to eager launches for good
+                hipck(hipStreamBeginCapture(I.stream(), hipStreamCaptureModeThreadLocal), "begin capture");
+                bool ok = true;
+                try {
                     cycle_program();
-                    hipck(hipStreamEndCapture(I.stream(), &I.graph), "end capture");
-                    hipck(hipGraphInstantiate(&I.graph_exec, I.graph, nullptr, nullptr, 0), "graph instantiate");
+                } catch (const std::exception& ex) {
+                    ok = false;
+                    std::fprintf(stderr, "mpgmres: cycle capture failed (%s); running eagerly\n", ex.what());
                 }
-                hipck(hipGraphLaunch(I.graph_exec, I.stream()), "graph launch");
-            } else {
-                cycle_program();
+                hipGraph_t g = nullptr;
+                const hipError_t ec = hipStreamEndCapture(I.stream(), &g);
+                if (ok && ec == hipSuccess &&
+                    hipGraphInstantiate(&I.graph_exec, g, nullptr, nullptr, 0) == hipSuccess) {
+                    I.graph = g;
+                } else {
+                    if (g) (void)hipGraphDestroy(g);
+                    (void)hipGetLastError();
+                    I.use_graph = false;
+                }
             }
+            if (I.use_graph) hipck(hipGraphLaunch(I.graph_exec, I.stream()), "graph launch");
+            else cycle_program();
             read_report(I.report_len);
             for (int k = 0; k < I.m; ++k) {
                 const double res = I.report_host[4 + k];

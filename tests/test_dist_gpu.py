@@ -34,6 +34,24 @@ def test_loopback_golden(mpg, mats, rec, nranks):
     compare(rec, got, case["mode"], case["tol"], case["rlen"], f"loopback{nranks}")
 
 
+def test_rccl_single_rank_engine(mpg):
+    """The RCCL engine path (communicator init, captured all-reduces, empty
+    halo) on one rank reproduces the single-GPU engine."""
+    A = mpg.gen_band(100_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=4)
+    plan = mpg.HaloPlan(0, 1, [0, A.nrows], A)
+    eng = mpg.Engine.distributed(A, b, xt, plan, mpg.rccl_unique_id(), 1, 0, **opts)
+    ran, done = eng.run(10)
+    assert ran == 4 and done and eng.total_iters == 120
+    eng.close()
+    one = mpg.Engine(A, b, xt, **opts)
+    ran1, done1 = one.run(10)
+    assert ran1 == 4 and done1 and one.total_iters == 120
+    one.close()
+
+
 @pytest.mark.parametrize("nranks", [2, 4])
 def test_loopback_matches_single_gpu_band(mpg, nranks):
     A = mpg.gen_band(200_000, 5, 4, seed=7)
