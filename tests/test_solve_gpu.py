@@ -51,6 +51,21 @@ def test_live_oracle_band(mpg, oracle, engine, mode):
         assert abs(got.res_norm - ref.res_norm) <= 0.5 * ref.res_norm + 1e-12 * np.linalg.norm(b)
 
 
+@pytest.mark.parametrize("prec", ["identity", "jacobi"])
+def test_mixed_half_values_converge(mpg, prec):
+    """Low-precision cast path (BASELINE config 5): fp16 matrix values in the
+    Arnoldi SpMV, fp32 vectors, fp64 residual/update. The reference has no
+    fp16 mode, so parity is the final backward error <= tol."""
+    A = mpg.gen_band(300_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    got = mpg.solve(A, b, xt, engine="fused", mode="mixed-half", orth="cgs", prec=prec, rlen=30, tol=1e-10,
+                    max_restarts=100)
+    assert got.status == "converged"
+    assert got.backward_error[-1] <= 1e-10
+    assert got.err_norm <= 1e-6 * np.linalg.norm(xt)
+
+
 @pytest.mark.parametrize("engine", ["surface", "fused"])
 def test_aborts_at_max_restarts(mpg, engine):
     """tol = 0 never converges: exactly max_restarts cycles of m steps, then abort
