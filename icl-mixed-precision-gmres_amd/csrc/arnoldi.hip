@@ -57,18 +57,43 @@ __device__ __forceinline__ void for_rows(const int32_t* __restrict__ blocks, int
     for (int b = rb0; b < rb1; ++b) csr_row_block(blocks[b], blocks[b + 1], rowptr, col, val, nnz, xval, epi, prod, scratch);
 }
 
+// One transpose round on the first 2H accumulators: lanes with the MASK bit
+// set keep the upper half, the others the lower half; recursion keeps every
+// index a compile-time constant (a runtime index sends acc to scratch).
+template <int H, int MASK, int N>
+__device__ __forceinline__ void butterfly_round(double (&acc)[N], int lane) {
+    if constexpr (H >= 1) {
+        const bool upper = (lane & MASK) != 0;
+#pragma unroll
+        for (int i = 0; i < H; ++i) {
+            const double keep = upper ? acc[i + H] : acc[i];
+            const double send = upper ? acc[i] : acc[i + H];
+            acc[i] = keep + __shfl_xor(send, MASK, kWave);
+        }
+        butterfly_round<H / 2, MASK / 2>(acc, lane);
+    }
+}
+
 // Block-reduce NCOL fp64 accumulators and store them as partial[c*G + blk].
+//
+// Wave stage = transpose (butterfly) reduction: in round r every lane trades
+// half of its remaining columns with the lane 32>>r away and keeps the sum
+// of the other half, so after log2(NCOL) rounds lane l holds one column
+// (l >> (6 - log2 NCOL)) summed over 2^rounds lanes; plain xor shuffles
+// finish the remaining lanes. 32 columns cost 32 shuffles instead of the
+// 192 of one 6-level reduction per column. Fixed order: deterministic.
 template <int NCOL>
 __device__ __forceinline__ void store_partials(double (&acc)[NCOL], int ncols, double* __restrict__ partial) {
+    static_assert((NCOL & (NCOL - 1)) == 0 && NCOL <= 32, "NCOL: power of two <= 32");
     __shared__ double red[kBlock / kWave][NCOL];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    constexpr int rounds = NCOL == 1 ? 0 : NCOL == 2 ? 1 : NCOL == 4 ? 2 : NCOL == 8 ? 3 : NCOL == 16 ? 4 : 5;
+    butterfly_round<NCOL / 2, 32>(acc, lane);
+    double v = acc[0];
 #pragma unroll
-    for (int c = 0; c < NCOL; ++c) {
-        if (c < ncols) {
-            double v = wave_sum(acc[c]);
-            if (lane == 0) red[wid][c] = v;
-        }
-    }
+    for (int mask = 32 >> rounds; mask >= 1; mask >>= 1) v += __shfl_xor(v, mask, kWave);
+    constexpr int shift = 6 - rounds;
+    if ((lane & ((1 << shift) - 1)) == 0) red[wid][lane >> shift] = v;
     __syncthreads();
     for (int c = threadIdx.x; c < ncols; c += kBlock) {
         double s = 0.0;
@@ -89,7 +114,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__
                                                      double* __restrict__ partial) {
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
-    double acc[3] = {0.0, 0.0, 0.0};
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
     for_rows(
         blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)x[c]; },
         [&](int i, double sum) {
@@ -103,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__
             w[i] = wi;
         },
         prod, scratch);
-    store_partials<3>(acc, 3, partial);
+    store_partials<4>(acc, 3, partial);
 }
 
 template <class T, class X>
@@ -217,12 +242,19 @@ template <> struct Row4<float> {
         const float4 v = *reinterpret_cast<const float4*>(p);
         o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
     }
+    static __device__ __forceinline__ void store(float* p, const float (&o)[4]) {
+        *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+    }
 };
 template <> struct Row4<double> {
     static __device__ __forceinline__ void load(const double* p, double (&o)[4]) {
         const double2 a = *reinterpret_cast<const double2*>(p);
         const double2 b = *reinterpret_cast<const double2*>(p + 2);
         o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
+    }
+    static __device__ __forceinline__ void store(double* p, const double (&o)[4]) {
+        *reinterpret_cast<double2*>(p) = make_double2(o[0], o[1]);
+        *reinterpret_cast<double2*>(p + 2) = make_double2(o[2], o[3]);
     }
 };
 
@@ -263,35 +295,83 @@ __global__ __launch_bounds__(kBlock) void k_panel_dots(int n, const T* __restric
 
 // ---------------------------------------------------------------- step: CGS
 // coef = T(sums[0..k]); w = w - T(V coef) (gemv(-1, V, h, 1, w));
-// NEXT_DOTS: partials <v_j, w'> (j <= k) else partial ||w'||^2
+// NEXT_DOTS: partials <v_j, w'> (j <= k) else partial ||w'||^2.
+// Each lane owns 4 consecutive rows (16-B loads of every basis column), and
+// issues the loads of 8 columns before their FMAs; the row sum t runs over
+// j = 0..k in order in fp64, as the scalar form did.
 template <class T, bool NEXT_DOTS>
 __global__ __launch_bounds__(kBlock) void k_cgs_update(int n, const T* __restrict__ V, int64_t ld, int k,
                                                        const double* __restrict__ sums, T* __restrict__ coef_out,
                                                        T* __restrict__ w, double* __restrict__ partial) {
-    __shared__ T coef[256];
+    __shared__ double coef[256];
     const int nc = k + 1;
     for (int j = threadIdx.x; j < nc; j += kBlock) {
-        coef[j] = (T)sums[j];
-        if (blockIdx.x == 0) coef_out[j] = coef[j];
+        const T c = (T)sums[j];
+        coef[j] = (double)c;
+        if (blockIdx.x == 0) coef_out[j] = c;
     }
     __syncthreads();
-    double acc[NEXT_DOTS ? kNC : 1];
+    constexpr int NA = NEXT_DOTS ? kNC : 1;
+    double acc[NA];
 #pragma unroll
-    for (int c = 0; c < (NEXT_DOTS ? kNC : 1); ++c) acc[c] = 0.0;
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    for (int c = 0; c < NA; ++c) acc[c] = 0.0;
+    const int n4 = n & ~3;
+    for (int i = 4 * (blockIdx.x * kBlock + threadIdx.x); i < n4; i += 4 * gridDim.x * kBlock) {
+        double t[4] = {0.0, 0.0, 0.0, 0.0};
+        int j = 0;
+        for (; j + 8 <= nc; j += 8) {
+            double v[8][4];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) Row4<T>::load(V + (int64_t)(j + u) * ld + i, v[u]);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) t[r] += v[u][r] * coef[j + u];
+        }
+        for (; j < nc; ++j) {
+            double v[4];
+            Row4<T>::load(V + (int64_t)j * ld + i, v);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[r] += v[r] * coef[j];
+        }
+        double wv[4];
+        Row4<T>::load(w + i, wv);
+        T wo[4];
+        double wd[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            wo[r] = T(-1) * (T)t[r] + T(1) * (T)wv[r];
+            wd[r] = (double)wo[r];
+        }
+        Row4<T>::store(w + i, wo);
+        if (NEXT_DOTS) {
+#pragma unroll
+            for (int c = 0; c < NA; ++c) {
+                if (c < nc) {
+                    double v[4];
+                    Row4<T>::load(V + (int64_t)c * ld + i, v);
+                    acc[c] += v[0] * wd[0] + v[1] * wd[1] + v[2] * wd[2] + v[3] * wd[3];
+                }
+            }
+        } else {
+            acc[0] += wd[0] * wd[0] + wd[1] * wd[1] + wd[2] * wd[2] + wd[3] * wd[3];
+        }
+    }
+    // tail rows (n not a multiple of 4)
+    for (int i = n4 + blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         double t = 0.0;
-        for (int j = 0; j < nc; ++j) t += (double)V[(int64_t)j * ld + i] * (double)coef[j];
+        for (int j = 0; j < nc; ++j) t += (double)V[(int64_t)j * ld + i] * coef[j];
         const T wi = T(-1) * (T)t + T(1) * w[i];
         w[i] = wi;
         if (NEXT_DOTS) {
 #pragma unroll
-            for (int c = 0; c < kNC; ++c)
+            for (int c = 0; c < NA; ++c)
                 if (c < nc) acc[c] += (double)V[(int64_t)c * ld + i] * (double)wi;
         } else {
             acc[0] += (double)wi * (double)wi;
         }
     }
-    store_partials<NEXT_DOTS ? kNC : 1>(acc, NEXT_DOTS ? (nc < kNC ? nc : kNC) : 1, partial);
+    store_partials<NA>(acc, NEXT_DOTS ? (nc < kNC ? nc : kNC) : 1, partial);
 }
 
 // ---------------------------------------------------------------- step: MGS
