@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--cpu-cycles", type=int, default=4, help="restart cycles in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-reps", type=int, default=10)
+    ap.add_argument("--spmv-format", default="auto", choices=["auto", "csr", "sell"],
+                    help="Arnoldi SpMV storage (auto: SELL-64 when its padding is small)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -106,7 +108,7 @@ def main():
     log(f"[bench] rank {rank}: BAND rows {r0}..{r1} of {n}, local nnz={A.nnz}, built in {time.time() - t0:.1f}s")
 
     opts = dict(mode=args.mode, orth=args.orth, prec=args.prec, rlen=args.rlen, tol=0.0,
-                max_restarts=args.warmup + args.steps + 10, device=local_rank)
+                max_restarts=args.warmup + args.steps + 10, device=local_rank, spmv_format=args.spmv_format)
     if world == 1:
         eng = mpg.Engine(A, b, xt, **opts)
     else:
@@ -146,16 +148,18 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     log(f"[bench] {args.steps} cycles, {iters} iterations in {elapsed:.4f}s -> {iters / elapsed:.1f} it/s")
 
-    # roofline of the dominant kernel: Arnoldi SpMV phase (k_step_spmv), mean over k
+    # roofline of the dominant kernel: the Arnoldi SpMV phase, mean over k
+    layout = eng.spmv_layout()
+    kernel = "k_step_sell" if layout["format"] == "sell" else "k_step_spmv"
     avg_ms = eng.time_phase("spmv", args.roofline_reps)
     bytes_per_launch = eng.phase_bytes("spmv")
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(REPO / "profiles", "k_step_spmv")
+    traffic = pmc_traffic(REPO / "profiles", kernel)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_step_spmv", "avg_launch_ms": round(avg_ms, 5),
+                "kernel": kernel, "avg_launch_ms": round(avg_ms, 5),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch)}
-    log(f"[bench] k_step_spmv {avg_ms * 1e3:.1f} us/launch, {achieved:.0f} GB/s algorithmic")
+    log(f"[bench] {kernel} {avg_ms * 1e3:.1f} us/launch, {achieved:.0f} GB/s algorithmic, storage {layout}")
     eng.close()
 
     cpu = None
@@ -185,6 +189,7 @@ def main():
                        "step": f"one restart cycle = {args.rlen} iterations",
                        "value_counts": "GMRES iterations x 10M-nnz row blocks (one per GPU) per second",
                        "rows_per_gpu": args.n_local, "nnz": global_nnz,
+                       "spmv_storage": layout,
                        "parallelism": f"row-partition x{world} (halo send/recv + fp64 all-reduce over RCCL)"},
         }
         print(json.dumps(line), flush=True)

@@ -22,7 +22,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._abi import ENGINES, MODES, ORTHS, PRECS, STATUS, HostCsr, SolveArgs, SolveResult
+from ._abi import ENGINES, MODES, ORTHS, PRECS, SPMV_FORMATS, STATUS, HostCsr, SolveArgs, SolveResult
 
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
@@ -90,6 +90,8 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_phase_bytes.argtypes = [C.c_void_p, C.c_int]
     lib.mpg_engine_phase_bytes.restype = C.c_double
     lib.mpg_engine_destroy.argtypes = [C.c_void_p]
+    lib.mpg_engine_spmv_layout.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                           C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
     P64 = C.POINTER(C.c_int64)
     P32 = C.POINTER(C.c_int32)
     lib.mpg_halo_analyze.argtypes = [_I32, _I32, P64, _I32, P32, P32, C.POINTER(C.c_void_p)]
@@ -293,7 +295,8 @@ class Result:
 
 def make_args(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, mode="mixed", orth="mgs",
               prec="identity", rlen=30, tol=1e-6, max_restarts=1_000_000, rtol=0.0, repeat_iter=False,
-              orthloss=False, jacobi_steps=1, engine="fused", verbose=False, device=0, threads=0):
+              orthloss=False, jacobi_steps=1, engine="fused", verbose=False, device=0, threads=0,
+              spmv_format="auto"):
     """Build mpg_solve_args (shared by mpg_solve and the CPU oracle)."""
     b = np.ascontiguousarray(b, dtype=np.float64)
     keep = [A.rowptr, A.col, A.val, b]
@@ -311,6 +314,7 @@ def make_args(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, mod
     a.rlen, a.tol, a.max_restarts, a.rtol = rlen, tol, max_restarts, rtol
     a.repeat_iter, a.orthloss, a.jacobi_steps = int(repeat_iter), int(orthloss), jacobi_steps
     a.verbose, a.device, a.threads = int(verbose), device, threads
+    a.spmv_format = SPMV_FORMATS[spmv_format]
     return a, keep
 
 
@@ -474,6 +478,15 @@ class Engine:
 
     def phase_bytes(self, phase: str) -> float:
         return float(self._lib.mpg_engine_phase_bytes(self._h, self.PHASES[phase]))
+
+    def spmv_layout(self) -> dict:
+        """Storage of the Arnoldi SpMV: {"format": "csr"|"sell", "vec_width",
+        "col_bytes", "stored"} (mpg_engine_spmv_layout)."""
+        f, w, cb, st = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+        if self._lib.mpg_engine_spmv_layout(self._h, C.byref(f), C.byref(w), C.byref(cb), C.byref(st)):
+            raise RuntimeError("mpg_engine_spmv_layout failed")
+        return {"format": {1: "csr", 2: "sell"}[f.value], "vec_width": w.value, "col_bytes": cb.value,
+                "stored": st.value}
 
     def close(self) -> None:
         if self._h:

@@ -8,6 +8,7 @@ MODES = {"mixed": 0, "baseline": 1, "single-prec": 2, "single": 3, "mixed-half":
 ORTHS = {"cgs": 0, "mgs": 1, "cgsr": 2}
 PRECS = {"ilu": 0, "ilu_jacobi": 1, "jacobi": 2, "identity": 3}
 ENGINES = {"surface": 0, "fused": 1}
+SPMV_FORMATS = {"auto": 0, "csr": 1, "sell": 2}
 STATUS = {1: "converged", 3: "aborted", -1: "error"}
 
 
@@ -34,6 +35,7 @@ class SolveArgs(C.Structure):
         ("verbose", C.c_int32),
         ("device", C.c_int32),
         ("threads", C.c_int32),
+        ("spmv_format", C.c_int32),
     ]
 
 

@@ -16,10 +16,13 @@
 // stand-alone kernels (blas1/blas2/spmv) apply, so the fused engine and the
 // operator-surface driver agree to the last bit in most steps.
 #include "csr_tile.hpp"
+#include "sell_tile.hpp"
 #include "internal.hpp"
 #include "mpgmres/arnoldi.h"
 
 #include <new>
+#include <algorithm>
+#include <vector>
 
 using namespace mpg;
 
@@ -232,6 +235,74 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
 #pragma unroll
         for (int q = 0; q < kBlock / kWave; ++q) s += red[q][c];
         partial[(size_t)c * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+// ---------------------------------------------------------------- step: SpMV (SELL-64)
+// Same contract as k_step_spmv on the sliced-ELL copy (sell_tile.hpp): one
+// wave per slice, one lane per row, no LDS; v_k and w are written coalesced.
+template <class T, class P, class VI, class CI, int W>
+__global__ __launch_bounds__(kBlock) void k_step_sell(int n, int nslices, const int64_t* __restrict__ off,
+                                                      const CI* __restrict__ col,
+                                                      const typename SellStore<VI>::type* __restrict__ val,
+                                                      const T* __restrict__ wprev, const T* __restrict__ inv_p,
+                                                      T* __restrict__ V, int64_t ld, int k,
+                                                      const P* __restrict__ diag, T* __restrict__ w) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int s = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    if (s >= nslices) return;
+    const T inv = *inv_p;
+    const double sum = sell_row_sum<typename SellStore<VI>::type, CI, W>(
+        s, lane, off, col, val, [&](int c) { return (double)(T)(wprev[c] * inv); });
+    const int i = s * kWave + lane;
+    if (i < n) {
+        const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
+        w[i] = precond<T, P>(t, diag, i);
+        V[(int64_t)k * ld + i] = wprev[i] * inv;
+    }
+}
+
+// largest |col - first row of its slice| over the matrix (int16 eligibility)
+__global__ void k_sell_span(int n, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                            unsigned* __restrict__ out) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned m = 0;
+    if (r < n) {
+        const int row0 = r & ~(kWave - 1);
+        for (int j = rowptr[r]; j < rowptr[r + 1]; ++j) {
+            const int d = col[j] - row0;
+            m = max(m, (unsigned)(d < 0 ? -d : d));
+        }
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & (kWave - 1)) == 0) atomicMax(out, m);
+}
+
+template <class VI> __device__ __forceinline__ typename SellStore<VI>::type sell_raw(VI v) { return v; }
+template <> __device__ __forceinline__ uint16_t sell_raw<half_v>(half_v v) { return v.bits; }
+
+// scatter the CSR (col, val) of row 64 s + lane into its slice; pads get the sentinel
+template <class VI, class CI, int W>
+__global__ void k_sell_fill(int n, int nslices, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                            const VI* __restrict__ val, const int64_t* __restrict__ off, CI* __restrict__ scol,
+                            typename SellStore<VI>::type* __restrict__ sval) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = (int)(t / kWave), lane = (int)(t % kWave);
+    if (s >= nslices) return;
+    const int r = s * kWave + lane;
+    const int64_t o = off[s];
+    const int width = (int)((off[s + 1] - o) / kWave);
+    const int b = r < n ? rowptr[r] : 0, len = r < n ? rowptr[r + 1] - b : 0;
+    for (int j = 0; j < width; ++j) {
+        const int64_t pos = o + (int64_t)(j / W) * kWave * W + lane * W + (j % W);
+        if (j < len) {
+            const int c = col[b + j];
+            scol[pos] = sizeof(CI) == 2 ? (CI)(c - s * kWave) : (CI)c;
+            sval[pos] = sell_raw(val[b + j]);
+        } else {
+            scol[pos] = SellCol<CI>::kPad;
+            sval[pos] = typename SellStore<VI>::type(0);
+        }
     }
 }
 
@@ -521,6 +592,15 @@ struct mpg_arnoldi {
     double* partial = nullptr;  // (kNC + 4) x G
     double* sums = nullptr;     // m + 4
     double* report = nullptr;   // 4 + m
+    // sliced-ELL copy of the Arnoldi matrix (nslices == 0: CSR row blocks)
+    struct {
+        int nslices = 0, W = 1;
+        bool c16 = false;
+        int64_t padded = 0;
+        int64_t* off = nullptr;
+        void* col = nullptr;
+        void* val = nullptr;
+    } sell;
 
     char* small_at(int slot) const { return static_cast<char*>(small) + (size_t)slot * (d.m + 1) * tsize; }
     void* cs() const { return small_at(0); }
@@ -559,6 +639,85 @@ int dispatch(int combo, F&& f) {
 
 int row_grid(const mpg_arnoldi* a) { return a->G; }
 int rb_grid(const mpg_arnoldi* a) { return a->Grb; }
+
+template <class F>
+int sell_dispatch(int W, bool c16, F&& f) {
+    auto with_w = [&](auto ci) {
+        switch (W) {
+            case 1: return f(ci, std::integral_constant<int, 1>());
+            case 2: return f(ci, std::integral_constant<int, 2>());
+            case 4: return f(ci, std::integral_constant<int, 4>());
+            default: return (int)MPG_ERR_UNSUPPORTED;
+        }
+    };
+    return c16 ? with_w(int16_t()) : with_w(int32_t());
+}
+
+// Build the SELL-64 copy (format: 0 auto, 1 never, 2 always). Auto takes it
+// when padding adds at most 20% to the stored entries; W is the widest
+// vector (4, 2, 1) with the least padding.
+int sell_build(mpg_arnoldi* a, int format) {
+    const mpg_csr* A = a->d.A;
+    const int n = A->rows;
+    if (format == 1 || n == 0 || A->nnz == 0) return MPG_OK;
+    std::vector<int32_t> rp((size_t)n + 1);
+    if (hipMemcpyAsync(rp.data(), A->rowptr, rp.size() * 4, hipMemcpyDeviceToHost, a->ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(a->ctx->stream) != hipSuccess)
+        return MPG_ERR_HIP;
+    const int ns = (n + kWave - 1) / kWave;
+    std::vector<int> width((size_t)ns, 0);
+    for (int r = 0; r < n; ++r) width[r / kWave] = std::max(width[r / kWave], rp[r + 1] - rp[r]);
+    int best_w = 1;
+    int64_t best = -1;
+    for (int W : {4, 2, 1}) {
+        int64_t p = 0;
+        for (int s = 0; s < ns; ++s) p += (int64_t)kWave * ((width[s] + W - 1) / W * W);
+        if (best < 0 || p < best) best = p, best_w = W;
+    }
+    if (format == 0 && (double)best > 1.2 * (double)A->nnz) return MPG_OK;
+    if (best >= ((int64_t)1 << 31) * 4) return format == 2 ? MPG_ERR_UNSUPPORTED : MPG_OK;
+    std::vector<int64_t> off((size_t)ns + 1, 0);
+    for (int s = 0; s < ns; ++s)
+        off[s + 1] = off[s] + (int64_t)kWave * ((width[s] + best_w - 1) / best_w * best_w);
+
+    unsigned* span = nullptr;
+    unsigned span_h = 0;
+    if (hipMalloc((void**)&span, sizeof(unsigned)) != hipSuccess) return MPG_ERR_ALLOC;
+    bool ok = hipMemsetAsync(span, 0, sizeof(unsigned), a->ctx->stream) == hipSuccess;
+    if (ok) {
+        k_sell_span<<<(n + kBlock - 1) / kBlock, kBlock, 0, a->ctx->stream>>>(n, A->rowptr, A->col, span);
+        ok = hipMemcpyAsync(&span_h, span, sizeof(unsigned), hipMemcpyDeviceToHost, a->ctx->stream) == hipSuccess &&
+             hipStreamSynchronize(a->ctx->stream) == hipSuccess;
+    }
+    (void)hipFree(span);
+    if (!ok) return MPG_ERR_HIP;
+    const bool c16 = span_h <= 32767u;
+    const size_t vsize = a->d.inner_val == MPG_F64 ? 8 : a->d.inner_val == MPG_F32 ? 4 : 2;
+    auto& S = a->sell;
+    if (hipMalloc((void**)&S.off, off.size() * 8) != hipSuccess ||
+        hipMalloc(&S.col, (size_t)best * (c16 ? 2 : 4) + 256) != hipSuccess ||
+        hipMalloc(&S.val, (size_t)best * vsize + 256) != hipSuccess)
+        return MPG_ERR_ALLOC;
+    if (hipMemcpyAsync(S.off, off.data(), off.size() * 8, hipMemcpyHostToDevice, a->ctx->stream) != hipSuccess)
+        return MPG_ERR_HIP;
+    S.nslices = ns;
+    S.W = best_w;
+    S.c16 = c16;
+    S.padded = best;
+    const int grid = (int)(((int64_t)ns * kWave + kBlock - 1) / kBlock);
+    int st = dispatch(a->combo, [&](auto, auto, auto, auto vi) {
+        using VI = decltype(vi);
+        return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
+            using CI = decltype(ci);
+            k_sell_fill<VI, CI, decltype(wc)::value><<<grid, kBlock, 0, a->ctx->stream>>>(
+                n, ns, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), S.off, static_cast<CI*>(S.col),
+                static_cast<typename SellStore<VI>::type*>(S.val));
+            return (int)MPG_OK;
+        });
+    });
+    if (st) return st;
+    return hipStreamSynchronize(a->ctx->stream) == hipSuccess ? MPG_OK : MPG_ERR_HIP;
+}
 
 }  // namespace
 
@@ -600,14 +759,34 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
         mpg_arnoldi_destroy(a);
         return MPG_ERR_ALLOC;
     }
+    if (desc->spmv_format < 0 || desc->spmv_format > 2) {
+        mpg_arnoldi_destroy(a);
+        return MPG_ERR_ARG;
+    }
+    if (int st = sell_build(a, desc->spmv_format)) {
+        mpg_arnoldi_destroy(a);
+        return st;
+    }
     *out = a;
+    return MPG_OK;
+}
+
+int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
+                            int64_t* stored) {
+    if (!a) return MPG_ERR_ARG;
+    const bool sell = a->sell.nslices > 0;
+    if (format) *format = sell ? 2 : 1;
+    if (vec_width) *vec_width = sell ? a->sell.W : 4;
+    if (col_bytes) *col_bytes = sell && a->sell.c16 ? 2 : 4;
+    if (stored) *stored = sell ? a->sell.padded : a->d.A->nnz;
     return MPG_OK;
 }
 
 int mpg_arnoldi_destroy(mpg_arnoldi_t a) {
     if (!a) return MPG_OK;
     if (a->ctx) (void)hipStreamSynchronize(a->ctx->stream);
-    void* ps[] = {a->V, a->H, a->small, a->w[0], a->w[1], a->partial, a->sums, a->report};
+    void* ps[] = {a->V, a->H, a->small, a->w[0], a->w[1], a->partial, a->sums, a->report,
+                  a->sell.off, a->sell.col, a->sell.val};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete a;
@@ -662,17 +841,31 @@ int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k) {
         using T = decltype(t);
         using P = decltype(p);
         using VI = decltype(vi);
+        const P* diag = a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr;
+        if (a->sell.nslices > 0) {
+            const auto& S = a->sell;
+            a->dots_pending = true;
+            return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
+                using CI = decltype(ci);
+                const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
+                k_step_sell<T, P, VI, CI, decltype(wc)::value><<<grid, kBlock, 0, a->ctx->stream>>>(
+                    a->d.n, S.nslices, S.off, static_cast<const CI*>(S.col),
+                    static_cast<const typename SellStore<VI>::type*>(S.val), static_cast<const T*>(a->w[k & 1]),
+                    static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k, diag,
+                    static_cast<T*>(a->w[(k + 1) & 1]));
+                return (int)MPG_OK;
+            });
+        }
         // dots inside the SpMV launch measured 71 us vs 30 + 20 us split
         // (BAND-10M fp32, k = 0..29 mean): keep the separate panel kernel
         const bool fused = kFuseDots && ndots_all <= kNC;
         k_step_spmv<T, P, VI><<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(
             A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,
             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,
-            a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr, static_cast<T*>(a->w[(k + 1) & 1]),
-            fused ? ndots_all : 0, a->partial);
+            diag, static_cast<T*>(a->w[(k + 1) & 1]), fused ? ndots_all : 0, a->partial);
         a->last_G = rb_grid(a);
         a->dots_pending = !fused;
-        return MPG_OK;
+        return (int)MPG_OK;
     });
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);

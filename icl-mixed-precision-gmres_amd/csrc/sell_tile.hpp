@@ -1,0 +1,97 @@
+// Sliced-ELL (SELL-64) copy of a CSR matrix for the Arnoldi SpMV.
+//
+// A slice is 64 consecutive rows = one wave64; lane l owns row 64 s + l.
+// The slice is padded to its longest row, rounded up to W, and stored as
+// steps of W entries per lane, lane-major inside a step:
+//
+//   element j of row 64 s + l  ->  off[s] + (j / W) * 64 W + l W + (j % W)
+//
+// so one wave-wide W-vector load per step moves 64 W contiguous entries
+// and needs no LDS, no segmented reduction and no row pointers. Columns are
+// int32, or int16 deltas against the slice's first row when every entry of
+// the matrix is within +-32767 of it (banded/stencil matrices: half the
+// index bytes). Padding carries a sentinel column and is skipped, so an
+// Inf/NaN in x never meets a padded zero. Within a row the entries keep CSR
+// order and the fp64 sum runs in that order.
+#pragma once
+
+#include "internal.hpp"
+#include "csr_tile.hpp"
+
+namespace mpg {
+
+template <class CI> struct SellCol;
+template <> struct SellCol<int32_t> {
+    static constexpr int32_t kPad = -1;
+    static __device__ __forceinline__ bool live(int32_t c) { return c >= 0; }
+    static __device__ __forceinline__ int decode(int32_t c, int /*row0*/) { return c; }
+};
+template <> struct SellCol<int16_t> {
+    static constexpr int16_t kPad = INT16_MIN;
+    static __device__ __forceinline__ bool live(int16_t c) { return c != INT16_MIN; }
+    static __device__ __forceinline__ int decode(int16_t c, int row0) { return row0 + (int)c; }
+};
+
+// raw storage of a value type inside the slices
+template <class V> struct SellStore { using type = V; };
+template <> struct SellStore<half_v> { using type = uint16_t; };
+
+template <class S> __device__ __forceinline__ double widen(S v) { return (double)v; }
+template <> __device__ __forceinline__ double widen<uint16_t>(uint16_t v) { return (double)to_float(v); }
+
+// W consecutive elements with one aligned vector load
+template <class S, int W> struct VecW {
+    typedef S vtype __attribute__((ext_vector_type(W)));
+    static __device__ __forceinline__ void load(const S* p, S (&o)[W]) {
+        const vtype v = *reinterpret_cast<const vtype*>(p);
+#pragma unroll
+        for (int e = 0; e < W; ++e) o[e] = v[e];
+    }
+};
+template <class S> struct VecW<S, 1> {
+    static __device__ __forceinline__ void load(const S* p, S (&o)[1]) { o[0] = *p; }
+};
+
+// steps per batch: every load of a batch is issued before its gathers
+template <int W> constexpr int sell_unroll() { return W >= 8 ? 1 : 8 / W; }
+
+// fp64 row sum of row 64 s + lane (lane valid or not: all lanes take part).
+template <class S, class CI, int W, class XF>
+__device__ __forceinline__ double sell_row_sum(int s, int lane, const int64_t* __restrict__ off,
+                                               const CI* __restrict__ col, const S* __restrict__ val, XF xval) {
+    constexpr int U = sell_unroll<W>();
+    const int64_t o = off[s];
+    const int steps = (int)((off[s + 1] - o) / (kWave * W));
+    const int row0 = s * kWave;
+    const CI* __restrict__ cp = col + o + lane * W;
+    const S* __restrict__ vp = val + o + lane * W;
+    double acc = 0.0;
+    for (int q = 0; q < steps; q += U) {
+        CI c[U][W];
+        S v[U][W];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (q + u < steps) {
+                VecW<CI, W>::load(cp + (int64_t)(q + u) * kWave * W, c[u]);
+                VecW<S, W>::load(vp + (int64_t)(q + u) * kWave * W, v[u]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < W; ++e) c[u][e] = SellCol<CI>::kPad;
+            }
+        }
+        double x[U][W];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < W; ++e)
+                x[u][e] = SellCol<CI>::live(c[u][e]) ? xval(SellCol<CI>::decode(c[u][e], row0)) : 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < W; ++e)
+                if (SellCol<CI>::live(c[u][e])) acc += widen(v[u][e]) * x[u][e];
+    }
+    return acc;
+}
+
+}  // namespace mpg

@@ -246,6 +246,7 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     d.diag = d.jacobi ? I.diag.p : nullptr;
     d.b = I.b.p;
     d.x = I.x.p;
+    d.spmv_format = a.spmv_format;
     check(mpg_arnoldi_create(ctx, &d, &I.arn), "mpg_arnoldi_create", ctx);
     I.report_len = mpg_arnoldi_report_len(I.arn);
     hipck(hipHostMalloc((void**)&I.report_host, (size_t)I.report_len * sizeof(double), 0), "hipHostMalloc");
@@ -467,9 +468,14 @@ double FusedEngine::phase_bytes(int which) const {
     const double sV = (double)dsize(I.ty.VI), sP = (double)dsize(I.ty.P);
     const double jac = I.args.prec == MPG_PREC_JACOBI ? 1.0 : 0.0;
     if (which == 0) {
-        // CSR (values + int32 columns + row pointers), v_k gathered (read
-        // once), w and V(:,k) written, Jacobi diagonal read
-        return z * (sV + 4) + (n + 1) * 4 + 3 * n * sT + jac * n * sP;
+        // matrix (CSR: values + int32 columns + row pointers; SELL-64:
+        // values + int32/int16 columns + slice offsets, padding not
+        // counted), v_k gathered (read once), w and V(:,k) written, Jacobi
+        // diagonal read
+        int32_t fmt = 1, cb = 4;
+        mpg_arnoldi_spmv_layout(I.arn, &fmt, nullptr, &cb, nullptr);
+        const double mat = fmt == 2 ? z * (sV + cb) + ((n + 63) / 64 + 1) * 8 : z * (sV + 4) + (n + 1) * 4;
+        return mat + 3 * n * sT + jac * n * sP;
     }
     if (which == 1) return z * (sX + 4) + (n + 1) * 4 + 3 * n * sX + n * sT + jac * n * sP;
     if (which == 3) {
@@ -481,6 +487,8 @@ double FusedEngine::phase_bytes(int which) const {
     // CGS update at mean k: read V(:,0..k), read + write w
     return ((I.m - 1) / 2.0 + 1) * n * sT + 2 * n * sT;
 }
+
+mpg_arnoldi_t FusedEngine::arnoldi() const { return p_->arn; }
 
 double FusedEngine::time_phase(int which, int reps) {
     Impl& I = *p_;
@@ -603,6 +611,12 @@ int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms) {
 
 double mpg_engine_phase_bytes(mpg_engine_t e, int which) {
     return e && e->eng ? e->eng->phase_bytes(which) : 0.0;
+}
+
+int mpg_engine_spmv_layout(mpg_engine_t e, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
+                           int64_t* stored) {
+    if (!e || !e->eng) return MPG_ERR_ARG;
+    return mpg_arnoldi_spmv_layout(e->eng->arnoldi(), format, vec_width, col_bytes, stored);
 }
 
 int mpg_engine_destroy(mpg_engine_t e) {

@@ -72,6 +72,7 @@ public:
     size_t total_iters() const { return conv_->total_iterations(); }
     double time_phase(int which, int reps);
     double phase_bytes(int which) const;
+    mpg_arnoldi_t arnoldi() const;
     void sync();
 
     // history (per restart / per step)

@@ -61,12 +61,21 @@ typedef struct {
     const void* diag;      /* Jacobi inverse diagonal (prec_type) or NULL */
     const void* b;         /* outer_type, n */
     void* x;               /* outer_type, n_ext (halo tail filled by the caller) */
+    int32_t spmv_format;   /* Arnoldi SpMV storage: 0 auto, 1 CSR row blocks, 2 sliced ELL (SELL-64) */
 } mpg_arnoldi_desc;
 
 /* Allocates the basis V (n x (m+1), leading dimension padded to 256 B),
  * H, Givens state, two w buffers (n_ext), partials and the report block. */
 int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_t* out);
 int mpg_arnoldi_destroy(mpg_arnoldi_t a);
+
+/* Storage the Arnoldi SpMV runs on: *format 1 = CSR row blocks (cuSPARSE
+ * csrmv's input, types_cuda.hpp:53-60), 2 = SELL-64 copy made at create
+ * (64-row slices, vec_width entries per lane load, col_bytes 4 = int32
+ * columns or 2 = int16 offsets from the slice's first row); *stored = stored
+ * entries including padding (nnz for CSR). Any output may be NULL. */
+int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
+                            int64_t* stored);
 
 int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
 int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);

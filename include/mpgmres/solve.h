@@ -61,6 +61,7 @@ typedef struct {
     int32_t verbose;       /* print the reference's stdout lines */
     int32_t device;        /* HIP device (mpg_solve only) */
     int32_t threads;       /* host threads (oracle only; 0 = default) */
+    int32_t spmv_format;   /* fused engine Arnoldi SpMV: 0 auto, 1 CSR row blocks, 2 SELL-64 */
 } mpg_solve_args;
 
 typedef struct {
@@ -108,6 +109,9 @@ int64_t mpg_engine_total_iters(mpg_engine_t e);
 int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms);
 /* algorithmic bytes of one launch of phase `which` */
 double mpg_engine_phase_bytes(mpg_engine_t e, int which);
+/* storage of the engine's Arnoldi SpMV (mpg_arnoldi_spmv_layout) */
+int mpg_engine_spmv_layout(mpg_engine_t e, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
+                           int64_t* stored);
 int mpg_engine_destroy(mpg_engine_t e);
 
 #ifdef __cplusplus

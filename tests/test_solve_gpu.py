@@ -25,18 +25,68 @@ def _case_id(c):
     return f"{k['matrix']}-{k['mode']}-{k['orth']}-{k['prec']}-m{k['rlen']}"
 
 
-@pytest.mark.parametrize("engine", ["surface", "fused"])
+# fused engine on both Arnoldi SpMV storages: CSR row blocks and SELL-64
+ENGINES = {"surface": ("surface", "auto"), "fused-csr": ("fused", "csr"), "fused-sell": ("fused", "sell")}
+
+
+@pytest.mark.parametrize("engine", list(ENGINES))
 @pytest.mark.parametrize("rec", GOLDEN["cases"], ids=_case_id)
 def test_golden(mpg, mats, rec, engine):
     case = dict(rec["case"])
     A = mats[case.pop("matrix")]
     xt = mpg.rand_vect(A.nrows, 42)
     b = mpg.host_spmv(A, xt)
-    got = mpg.solve(A, b, xt, engine=engine, **case)
+    eng, fmt = ENGINES[engine]
+    got = mpg.solve(A, b, xt, engine=eng, spmv_format=fmt, **case)
     compare(rec, got, case["mode"], case["tol"], case["rlen"], _case_id(rec) + "/" + engine)
 
 
-@pytest.mark.parametrize("engine", ["surface", "fused"])
+def _arrow(mpg, n):
+    """Diagonally dominant arrow matrix: a dense first row and column, so
+    one slice would pad every row to n (auto keeps CSR)."""
+    rows = [[(0, float(n + 1))] + [(j, 0.5) for j in range(1, n)]]
+    for i in range(1, n):
+        rows.append([(0, 0.25), (i, 4.0)] + ([(i + 1, -1.0)] if i + 1 < n else []))
+    rowptr = np.zeros(n + 1, dtype=np.int32)
+    cols, vals = [], []
+    for i, r in enumerate(rows):
+        rowptr[i + 1] = rowptr[i] + len(r)
+        cols += [c for c, _ in r]
+        vals += [v for _, v in r]
+    return mpg.Csr(n, n, rowptr, np.array(cols, dtype=np.int32), np.array(vals))
+
+
+def test_spmv_layout_choice(mpg):
+    """Auto picks SELL-64 with int16 offsets and 2-wide loads for the band,
+    CSR for the arrow matrix; forcing either storage gives the same solve."""
+    A = mpg.gen_band(20_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    e = mpg.Engine(A, b, xt, mode="mixed", orth="cgs", prec="identity", rlen=30, tol=0.0, max_restarts=2)
+    try:  # 10 entries per row, 64-row slices, the last one half full
+        assert e.spmv_layout() == {"format": "sell", "vec_width": 2, "col_bytes": 2,
+                                   "stored": -(-A.nrows // 64) * 64 * 10}
+    finally:
+        e.close()
+    B = _arrow(mpg, 3000)
+    xb = mpg.rand_vect(B.nrows, 42)
+    bb = mpg.host_spmv(B, xb)
+    e = mpg.Engine(B, bb, xb, mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=2)
+    try:
+        assert e.spmv_layout()["format"] == "csr"
+    finally:
+        e.close()
+    res = {}
+    for fmt in ("csr", "sell"):
+        got = mpg.solve(B, bb, xb, engine="fused", spmv_format=fmt, mode="mixed", orth="cgs", prec="jacobi",
+                        rlen=30, tol=1e-10, max_restarts=50)
+        assert got.status == "converged"
+        res[fmt] = got
+    assert res["csr"].total_iters == res["sell"].total_iters
+    np.testing.assert_allclose(res["csr"].step_res, res["sell"].step_res, rtol=1e-4)
+
+
+@pytest.mark.parametrize("engine", list(ENGINES))
 @pytest.mark.parametrize("mode", ["mixed", "baseline"])
 def test_live_oracle_band(mpg, oracle, engine, mode):
     """Larger input than the fixtures: BAND n=200k, GMRES(30), live oracle."""
@@ -45,7 +95,8 @@ def test_live_oracle_band(mpg, oracle, engine, mode):
     b = mpg.host_spmv(A, xt)
     opts = dict(mode=mode, orth="cgs", prec="jacobi", rlen=30, tol=1e-9, max_restarts=40)
     ref = oracle.solve(mpg, A, b, xt, **opts)
-    got = mpg.solve(A, b, xt, engine=engine, **opts)
+    eng, fmt = ENGINES[engine]
+    got = mpg.solve(A, b, xt, engine=eng, spmv_format=fmt, **opts)
     compare(as_ref(ref), got, mode, opts["tol"], 30, f"band200k-{mode}-{engine}")
     if mode == "baseline":  # same restart count -> comparable final residuals
         assert abs(got.res_norm - ref.res_norm) <= 0.5 * ref.res_norm + 1e-12 * np.linalg.norm(b)
