@@ -30,6 +30,8 @@ namespace {
 
 constexpr int kNC = 32;        // dot columns carried in registers per pass
 constexpr int kGroups = 1024;  // max workgroups of the row-block phase kernels
+constexpr int kCombineBlock = 1024;  // threads per workgroup of the combining panel dots
+constexpr int kCombineGroups = 256;  // its workgroups: one per CU
 constexpr int kOrthMGS = 1, kOrthCGSR = 2;  // mpg_orth_t (include/mpgmres/solve.h)
 
 // Jacobi / identity preconditioner in precision P applied to a T value:
@@ -77,7 +79,42 @@ __device__ __forceinline__ void butterfly_round(double (&acc)[N], int lane) {
     }
 }
 
-// Block-reduce NCOL fp64 accumulators and store them as partial[c*G + blk].
+// ---------------------------------------------------------------- in-launch combine
+// Last-arriver hand-off (one GPU): every workgroup stores its partials
+// write-through (sc1, so no release fence is needed for them), drains its
+// stores, and one lane draws a ticket; the workgroup that draws the last one
+// takes an agent-scope acquire and combines all partials in a fixed order
+// (deterministic, placement-independent). The counter is re-armed by the
+// last arriver; it starts zeroed (hipMemset at plan creation).
+typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+__device__ __forceinline__ void store_wt(double* p, double v) {
+    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// true in every thread of the last-arriving workgroup (after its acquire)
+__device__ __forceinline__ bool last_arriver(unsigned* cnt) {
+    __shared__ int last_s;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = t == gridDim.x - 1;
+        if (last) {
+            __hip_atomic_store((gu32*)cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        last_s = last;
+    }
+    __syncthreads();
+    return last_s != 0;
+}
+
+// Block-reduce NCOL fp64 accumulators and store them as partial[c*G + blk]
+// (write-through when WT: the last-arriver combine reads them).
 //
 // Wave stage = transpose (butterfly) reduction: in round r every lane trades
 // half of its remaining columns with the lane 32>>r away and keeps the sum
@@ -85,10 +122,10 @@ __device__ __forceinline__ void butterfly_round(double (&acc)[N], int lane) {
 // (l >> (6 - log2 NCOL)) summed over 2^rounds lanes; plain xor shuffles
 // finish the remaining lanes. 32 columns cost 32 shuffles instead of the
 // 192 of one 6-level reduction per column. Fixed order: deterministic.
-template <int NCOL>
+template <int NCOL, int BS = kBlock, bool WT = false>
 __device__ __forceinline__ void store_partials(double (&acc)[NCOL], int ncols, double* __restrict__ partial) {
     static_assert((NCOL & (NCOL - 1)) == 0 && NCOL <= 32, "NCOL: power of two <= 32");
-    __shared__ double red[kBlock / kWave][NCOL];
+    __shared__ double red[BS / kWave][NCOL];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     constexpr int rounds = NCOL == 1 ? 0 : NCOL == 2 ? 1 : NCOL == 4 ? 2 : NCOL == 8 ? 3 : NCOL == 16 ? 4 : 5;
     butterfly_round<NCOL / 2, 32>(acc, lane);
@@ -98,12 +135,28 @@ __device__ __forceinline__ void store_partials(double (&acc)[NCOL], int ncols, d
     constexpr int shift = 6 - rounds;
     if ((lane & ((1 << shift) - 1)) == 0) red[wid][lane >> shift] = v;
     __syncthreads();
-    for (int c = threadIdx.x; c < ncols; c += kBlock) {
+    for (int c = threadIdx.x; c < ncols; c += BS) {
         double s = 0.0;
 #pragma unroll
-        for (int w = 0; w < kBlock / kWave; ++w) s += red[w][c];
-        partial[(size_t)c * gridDim.x + blockIdx.x] = s;
+        for (int w = 0; w < BS / kWave; ++w) s += red[w][c];
+        if (WT) store_wt(partial + (size_t)c * gridDim.x + blockIdx.x, s);
+        else partial[(size_t)c * gridDim.x + blockIdx.x] = s;
     }
+}
+
+// Combine in the last arriver: sums[c] = sum over g of partial[c*G + g] for
+// c < ncols <= BS/32; 32 lanes per column, each a strided run in g order,
+// then a 32-lane xor tree (fixed order).
+template <int BS>
+__device__ __forceinline__ void combine_columns(const double* __restrict__ partial, int G, int ncols,
+                                                double* __restrict__ sums) {
+    const int c = threadIdx.x / 32, sub = threadIdx.x % 32;
+    double v = 0.0;
+    if (c < ncols)
+        for (int g = sub; g < G; g += 32) v += partial[(size_t)c * G + g];
+#pragma unroll
+    for (int mask = 16; mask >= 1; mask >>= 1) v += __shfl_xor(v, mask, kWave);
+    if (c < ncols && sub == 0) sums[c] = v;
 }
 
 // ---------------------------------------------------------------- prologue
@@ -173,16 +226,124 @@ __global__ __launch_bounds__(1024) void k_reduce_partials(int G, const double* _
     if (threadIdx.x == 0) sums[blockIdx.x] = s;
 }
 
-// ---------------------------------------------------------------- step: SpMV
-// v_k = T(w_prev * inv) (local rows stored to V[:,k]); w = M(A v_k); then
-// the Gram-Schmidt partials <v_j, w> (j < ndots <= kNC) over this
-// workgroup's rows. The dot pass keeps one column chunk live at a time and
-// folds each column with a wave64 shuffle reduction straight away, so it
-// adds few registers to this gather-bound kernel (a full fp64 accumulator
-// bank here dropped it to 3 waves/SIMD). ndots == 0: k_panel_dots follows.
-constexpr int kDotChunk = 16;
-constexpr bool kFuseDots = false;
+// ---------------------------------------------------------------- step: Givens
+#pragma clang fp contract(off)
+template <class T>
+__device__ void rot_pair(T& a, T& b, T c, T s) {
+    const T a1 = a, a2 = b;
+    a = c * a1 + s * a2;
+    b = c * a2 - s * a1;
+}
+template <class T>
+__device__ void rotg_ref(T& a, T& b, T& c, T& s) {
+    const T av = a, bv = b;
+    const T roe = fabs(av) > fabs(bv) ? av : bv;
+    const T scale = fabs(av) + fabs(bv);
+    T r;
+    if (scale == T(0)) {
+        c = T(1); s = T(0); r = T(0);
+    } else {
+        const T as = av / scale, bs = bv / scale;
+        r = scale * sqrt(as * as + bs * bs);
+        r = roe >= T(0) ? r : -r;
+        c = av / r;
+        s = bv / r;
+    }
+    a = r;
+    b = T(0);
+}
 
+// h_{k+1,k} = ||w||; (CGSR: h(0:k,k) += correction); rotations; |s(k+1)|.
+// norm2 = the squared norm: sums[0] (nparts == 0) or, on one GPU, the sum
+// of `nparts` workgroup partials reduced here (saves a launch per step).
+// Givens step k on one workgroup (gmres.cpp:217-226): col/c_s/s_s are LDS
+// arrays of at least k + 2 entries; nrm2sq (= ||w||^2) is read in thread 0.
+template <class T>
+struct GivensArgs {
+    int k, m;
+    const T* corr;  // CGSR correction (h += corr) or nullptr
+    T *H, *cs, *sn, *s, *inv;
+    double* report;
+};
+
+template <class T>
+__device__ void givens_block(const GivensArgs<T>& g, double nrm2sq, T* col, T* c_s, T* s_s) {
+    // stage the column and the previous rotations in LDS with all lanes, so
+    // the serial rotation chain runs on LDS instead of global latency
+    const int k = g.k;
+    T* gcol = g.H + (int64_t)k * (g.m + 1);
+    for (int j = threadIdx.x; j <= k; j += blockDim.x) {
+        col[j] = g.corr ? gcol[j] + T(1) * g.corr[j] : gcol[j];  // axpy(1.0, weights, h_col)
+        c_s[j] = g.cs[j];
+        s_s[j] = g.sn[j];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const T hn = (T)sqrt(nrm2sq);
+        col[k + 1] = hn;
+        *g.inv = T(1) / hn;  // scal(1/h_final, w, v_{k+1}) — no breakdown guard, as in the reference
+        for (int j = 0; j < k; ++j) rot_pair(col[j], col[j + 1], c_s[j], s_s[j]);
+        rotg_ref(col[k], col[k + 1], c_s[k], s_s[k]);
+        T sk = g.s[k], sk1 = g.s[k + 1];
+        rot_pair(sk, sk1, c_s[k], s_s[k]);
+        g.s[k] = sk;
+        g.s[k + 1] = sk1;
+        g.cs[k] = c_s[k];
+        g.sn[k] = s_s[k];
+        g.report[4 + k] = (double)fabs(sk1);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j <= k + 1; j += blockDim.x) gcol[j] = col[j];
+}
+
+// the scale 1/h_{k+1,k} exactly as givens_block forms it
+template <class T>
+__device__ __forceinline__ T inv_of_norm2(double nrm2sq) {
+    return T(1) / (T)sqrt(nrm2sq);
+}
+
+// norm2 = the squared norm: sums[0] (nparts == 0) or, on one GPU, the sum
+// of `nparts` workgroup partials reduced here (saves a launch per step).
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_givens(GivensArgs<T> g, const double* __restrict__ norm2, int nparts) {
+    __shared__ T col[1026], c_s[1026], s_s[1026];
+    __shared__ double scratch[kBlock / kWave];
+    const double nrm2sq = nparts > 0 ? sum_partials<kBlock>(norm2, nparts, scratch) : norm2[0];
+    givens_block(g, nrm2sq, col, c_s, s_s);
+}
+
+// Givens step k-1 folded into the SpMV launch of step k (restart length
+// <= kFoldMaxM): every workgroup sums the ||w||^2 partials in the same
+// fixed order and forms 1/h_{k,k-1} itself; workgroup 0 also runs the
+// rotation step. Returns the scale for v_k in every thread.
+constexpr int kFoldMaxM = 64;
+template <class T>
+struct GivensFold {
+    const double* norm2;  // nullptr: not folded (use *inv_p)
+    int nparts;
+    GivensArgs<T> g;
+};
+
+template <class T>
+__device__ __forceinline__ T fold_givens(const GivensFold<T>& f, const T* __restrict__ inv_p) {
+    if (!f.norm2) return *inv_p;
+    __shared__ T col[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
+    __shared__ double scratch[kBlock / kWave];
+    __shared__ T inv_s;
+    const double nrm2sq = f.nparts > 0 ? sum_partials<kBlock>(f.norm2, f.nparts, scratch) : f.norm2[0];
+    if (threadIdx.x == 0) inv_s = inv_of_norm2<T>(nrm2sq);
+    if (blockIdx.x == 0) givens_block(f.g, nrm2sq, col, c_s, s_s);
+    __syncthreads();
+    return inv_s;
+}
+#pragma clang fp contract(on)
+
+// ---------------------------------------------------------------- step: SpMV
+// v_k = T(w_prev * inv) (local rows stored to V[:,k]); w = M(A v_k).
+// inv = 1/h_{k,k-1} from the previous Givens kernel, or formed here with
+// that Givens step folded in (fold.norm2 != nullptr). The Gram-Schmidt dots
+// follow in k_panel_dots (measured: dots inside this gather-bound launch
+// cost more than the separate pass, 71 us vs 30 + 20 us on BAND-10M).
 template <class T, class P, class VI>
 __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict__ blocks, int nblocks,
                                                       const int32_t* __restrict__ rowptr,
@@ -190,11 +351,10 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
                                                       int64_t nnz, const T* __restrict__ wprev,
                                                       const T* __restrict__ inv_p, T* __restrict__ V, int64_t ld,
                                                       int k, const P* __restrict__ diag, T* __restrict__ w,
-                                                      int ndots, double* __restrict__ partial) {
+                                                      GivensFold<T> fold) {
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
-    __shared__ double red[kBlock / kWave][kNC];
-    const T inv = *inv_p;
+    const T inv = fold_givens(fold, inv_p);
     T* __restrict__ Vk = V + (int64_t)k * ld;
     for_rows(
         blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)(T)(wprev[c] * inv); },
@@ -204,38 +364,6 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
             Vk[i] = wprev[i] * inv;
         },
         prod, scratch);
-    if (ndots <= 0) return;
-    int rb0, rb1;
-    my_blocks(nblocks, rb0, rb1);
-    const int i0 = blocks[rb0], i1 = blocks[rb1];
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    for (int j0 = 0; j0 < ndots; j0 += kDotChunk) {
-        double a[kDotChunk];
-#pragma unroll
-        for (int c = 0; c < kDotChunk; ++c) a[c] = 0.0;
-        for (int i = i0 + threadIdx.x; i < i1; i += kBlock) {
-            const double wi = (double)w[i];
-            T v[kDotChunk];
-#pragma unroll
-            for (int c = 0; c < kDotChunk; ++c) v[c] = j0 + c < ndots ? V[(int64_t)(j0 + c) * ld + i] : T(0);
-#pragma unroll
-            for (int c = 0; c < kDotChunk; ++c) a[c] += (double)v[c] * wi;
-        }
-#pragma unroll
-        for (int c = 0; c < kDotChunk; ++c) {
-            if (j0 + c < ndots) {
-                const double s = wave_sum(a[c]);
-                if (lane == 0) red[wid][j0 + c] = s;
-            }
-        }
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < ndots; c += kBlock) {
-        double s = 0.0;
-#pragma unroll
-        for (int q = 0; q < kBlock / kWave; ++q) s += red[q][c];
-        partial[(size_t)c * gridDim.x + blockIdx.x] = s;
-    }
 }
 
 // ---------------------------------------------------------------- step: SpMV (SELL-64)
@@ -247,11 +375,12 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int nslices, const 
                                                       const typename SellStore<VI>::type* __restrict__ val,
                                                       const T* __restrict__ wprev, const T* __restrict__ inv_p,
                                                       T* __restrict__ V, int64_t ld, int k,
-                                                      const P* __restrict__ diag, T* __restrict__ w) {
+                                                      const P* __restrict__ diag, T* __restrict__ w,
+                                                      GivensFold<T> fold) {
+    const T inv = fold_givens(fold, inv_p);  // block-wide: before any lane leaves
     const int lane = threadIdx.x & (kWave - 1);
     const int s = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
     if (s >= nslices) return;
-    const T inv = *inv_p;
     const double sum = sell_row_sum<typename SellStore<VI>::type, CI, W>(
         s, lane, off, col, val, [&](int c) { return (double)(T)(wprev[c] * inv); });
     const int i = s * kWave + lane;
@@ -334,15 +463,20 @@ template <> struct Row4<double> {
 // iteration (16-B loads of every column: V's leading dimension is padded to
 // 256 B), issues all column loads before its FMAs, and keeps one fp64
 // accumulator per column; store_partials does the wave64/LDS combine.
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_panel_dots(int n, const T* __restrict__ V, int64_t ld, int c0, int nc,
-                                                       const T* __restrict__ w, double* __restrict__ partial) {
+// BS threads per workgroup. COMBINE (one GPU, nc <= kNC, c0 == 0): the
+// partials go write-through and the last-arriving workgroup sums them into
+// sums[0..nc) itself — no separate reduce launch (BS = 1024, so one
+// workgroup per CU keeps the partial count at 256 per column).
+template <class T, int BS = kBlock, bool COMBINE = false>
+__global__ __launch_bounds__(BS) void k_panel_dots(int n, const T* __restrict__ V, int64_t ld, int c0, int nc,
+                                                   const T* __restrict__ w, double* __restrict__ partial,
+                                                   unsigned* __restrict__ cnt, double* __restrict__ sums) {
     double acc[kNC];
 #pragma unroll
     for (int c = 0; c < kNC; ++c) acc[c] = 0.0;
     const int n4 = n & ~3;
     const T* __restrict__ Vb = V + (int64_t)c0 * ld;
-    for (int i = 4 * (blockIdx.x * kBlock + threadIdx.x); i < n4; i += 4 * gridDim.x * kBlock) {
+    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
         double wv[4];
         Row4<T>::load(w + i, wv);
 #pragma unroll
@@ -355,13 +489,16 @@ __global__ __launch_bounds__(kBlock) void k_panel_dots(int n, const T* __restric
         }
     }
     // tail rows (n not a multiple of 4)
-    for (int i = n4 + blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
         const double wi = (double)w[i];
 #pragma unroll
         for (int c = 0; c < kNC; ++c)
             if (c < nc) acc[c] += (double)Vb[(int64_t)c * ld + i] * wi;
     }
-    store_partials<kNC>(acc, nc, partial + (size_t)c0 * gridDim.x);
+    store_partials<kNC, BS, COMBINE>(acc, nc, partial + (size_t)c0 * gridDim.x);
+    if constexpr (COMBINE) {
+        if (last_arriver(cnt)) combine_columns<BS>(partial, gridDim.x, nc, sums);
+    }
 }
 
 // ---------------------------------------------------------------- step: CGS
@@ -370,10 +507,15 @@ __global__ __launch_bounds__(kBlock) void k_panel_dots(int n, const T* __restric
 // Each lane owns 4 consecutive rows (16-B loads of every basis column), and
 // issues the loads of 8 columns before their FMAs; the row sum t runs over
 // j = 0..k in order in fp64, as the scalar form did.
-template <class T, bool NEXT_DOTS>
+// GIVENS (one GPU, last pass, m <= kFoldMaxM): the ||w'||^2 partials go
+// write-through and the last-arriving workgroup sums them and runs the
+// Givens step k (givens_block) — no separate Givens launch.
+template <class T, bool NEXT_DOTS, bool GIVENS = false>
 __global__ __launch_bounds__(kBlock) void k_cgs_update(int n, const T* __restrict__ V, int64_t ld, int k,
                                                        const double* __restrict__ sums, T* __restrict__ coef_out,
-                                                       T* __restrict__ w, double* __restrict__ partial) {
+                                                       T* __restrict__ w, double* __restrict__ partial,
+                                                       unsigned* __restrict__ cnt, GivensArgs<T> g) {
+    static_assert(!(NEXT_DOTS && GIVENS), "the Givens step follows the last pass");
     __shared__ double coef[256];
     const int nc = k + 1;
     for (int j = threadIdx.x; j < nc; j += kBlock) {
@@ -442,7 +584,15 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update(int n, const T* __restric
             acc[0] += (double)wi * (double)wi;
         }
     }
-    store_partials<NA>(acc, NEXT_DOTS ? (nc < kNC ? nc : kNC) : 1, partial);
+    store_partials<NA, kBlock, GIVENS>(acc, NEXT_DOTS ? (nc < kNC ? nc : kNC) : 1, partial);
+    if constexpr (GIVENS) {
+        if (last_arriver(cnt)) {
+            __shared__ T col[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
+            __shared__ double scratch[kBlock / kWave];
+            const double nrm2sq = sum_partials<kBlock>(partial, gridDim.x, scratch);
+            givens_block(g, nrm2sq, col, c_s, s_s);
+        }
+    }
 }
 
 // ---------------------------------------------------------------- step: MGS
@@ -466,72 +616,7 @@ __global__ __launch_bounds__(kBlock) void k_mgs_update(int n, const T* __restric
     store_partials<1>(acc, 1, partial);
 }
 
-// ---------------------------------------------------------------- step: Givens
 #pragma clang fp contract(off)
-template <class T>
-__device__ void rot_pair(T& a, T& b, T c, T s) {
-    const T a1 = a, a2 = b;
-    a = c * a1 + s * a2;
-    b = c * a2 - s * a1;
-}
-template <class T>
-__device__ void rotg_ref(T& a, T& b, T& c, T& s) {
-    const T av = a, bv = b;
-    const T roe = fabs(av) > fabs(bv) ? av : bv;
-    const T scale = fabs(av) + fabs(bv);
-    T r;
-    if (scale == T(0)) {
-        c = T(1); s = T(0); r = T(0);
-    } else {
-        const T as = av / scale, bs = bv / scale;
-        r = scale * sqrt(as * as + bs * bs);
-        r = roe >= T(0) ? r : -r;
-        c = av / r;
-        s = bv / r;
-    }
-    a = r;
-    b = T(0);
-}
-
-// h_{k+1,k} = ||w||; (CGSR: h(0:k,k) += correction); rotations; |s(k+1)|.
-// norm2 = the squared norm: sums[0] (nparts == 0) or, on one GPU, the sum
-// of `nparts` workgroup partials reduced here (saves a launch per step).
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_givens(int k, int m, const double* __restrict__ norm2, int nparts,
-                                                   const T* __restrict__ corr, T* __restrict__ H,
-                                                   T* __restrict__ cs, T* __restrict__ sn, T* __restrict__ s,
-                                                   T* __restrict__ inv, double* __restrict__ report) {
-    // stage the column and the previous rotations in LDS with all lanes, so
-    // the serial rotation chain runs on LDS instead of global latency
-    __shared__ T col[1026], c_s[1026], s_s[1026];
-    __shared__ double scratch[kBlock / kWave];
-    const double nrm2sq = nparts > 0 ? sum_partials<kBlock>(norm2, nparts, scratch) : norm2[0];
-    const int ldh = m + 1;
-    T* gcol = H + (int64_t)k * ldh;
-    for (int j = threadIdx.x; j <= k; j += blockDim.x) {
-        col[j] = corr ? gcol[j] + T(1) * corr[j] : gcol[j];  // axpy(1.0, weights, h_col)
-        c_s[j] = cs[j];
-        s_s[j] = sn[j];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const T hn = (T)sqrt(nrm2sq);
-        col[k + 1] = hn;
-        *inv = T(1) / hn;  // scal(1/h_final, w, v_{k+1}) — no breakdown guard, as in the reference
-        for (int j = 0; j < k; ++j) rot_pair(col[j], col[j + 1], c_s[j], s_s[j]);
-        rotg_ref(col[k], col[k + 1], c_s[k], s_s[k]);
-        T sk = s[k], sk1 = s[k + 1];
-        rot_pair(sk, sk1, c_s[k], s_s[k]);
-        s[k] = sk;
-        s[k + 1] = sk1;
-        cs[k] = c_s[k];
-        sn[k] = s_s[k];
-        report[4 + k] = (double)fabs(sk1);
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j <= k + 1; j += blockDim.x) gcol[j] = col[j];
-}
-
 // upper-triangular solve y = H(0:k,0:k)^-1 s(0:k), in place on s (one lane per
 // row of the axpy sweep; k <= m is small)
 template <class T>
@@ -582,7 +667,6 @@ struct mpg_arnoldi {
     int G = 1;        // workgroups of the row-parallel panel kernels
     int Grb = 1;      // workgroups of the row-block (SpMV) kernels: one per row block
     int last_G = 1;   // partial count per column written by the last producer
-    bool dots_pending = false;  // mpg_arnoldi_dots still has to form the partials
     int64_t ld = 0;   // leading dimension of V (elements)
     size_t tsize = 8;
     void* V = nullptr;
@@ -592,6 +676,8 @@ struct mpg_arnoldi {
     double* partial = nullptr;  // (kNC + 4) x G
     double* sums = nullptr;     // m + 4
     double* report = nullptr;   // 4 + m
+    unsigned* counters = nullptr;  // last-arriver tickets: [0] dots, [32] CGS + Givens (zeroed at create)
+    int Gd = 1;                    // workgroups (kCombineBlock threads) of the combining panel dots
     // sliced-ELL copy of the Arnoldi matrix (nslices == 0: CSR row blocks)
     struct {
         int nslices = 0, W = 1;
@@ -639,6 +725,19 @@ int dispatch(int combo, F&& f) {
 
 int row_grid(const mpg_arnoldi* a) { return a->G; }
 int rb_grid(const mpg_arnoldi* a) { return a->Grb; }
+
+template <class T>
+GivensArgs<T> givens_args(const mpg_arnoldi* a, int k) {
+    return GivensArgs<T>{k,
+                         a->d.m,
+                         a->d.orth == kOrthCGSR ? static_cast<const T*>(a->corr()) : nullptr,
+                         static_cast<T*>(a->H),
+                         static_cast<T*>(a->cs()),
+                         static_cast<T*>(a->sn()),
+                         static_cast<T*>(a->s()),
+                         static_cast<T*>(a->inv()),
+                         a->report};
+}
 
 template <class F>
 int sell_dispatch(int W, bool c16, F&& f) {
@@ -739,6 +838,8 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
     a->tsize = desc->vec_type == MPG_F64 ? 8 : 4;
     a->G = desc->A->nblocks < kGroups ? (desc->A->nblocks > 0 ? desc->A->nblocks : 1) : kGroups;
     a->Grb = desc->A->nblocks > 0 ? desc->A->nblocks : 1;
+    a->Gd = (int)std::min<int64_t>(kCombineGroups, std::max<int64_t>(1, ((int64_t)desc->n + 4 * kCombineBlock - 1) /
+                                                                          (4 * kCombineBlock)));
     const size_t align = 256 / a->tsize;
     a->ld = ((int64_t)desc->n + align - 1) / align * align;
     if (a->ld == 0) a->ld = align;
@@ -754,7 +855,8 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
               alloc((void**)&a->partial, std::max<size_t>((size_t)(kNC + 4) * a->Grb, (size_t)(m + 4) * a->G) *
                                              sizeof(double)) &&
               alloc((void**)&a->sums, (size_t)(m + 8) * sizeof(double)) &&
-              alloc((void**)&a->report, (size_t)(m + 8) * sizeof(double));
+              alloc((void**)&a->report, (size_t)(m + 8) * sizeof(double)) &&
+              alloc((void**)&a->counters, 256);
     if (!ok) {
         mpg_arnoldi_destroy(a);
         return MPG_ERR_ALLOC;
@@ -786,7 +888,7 @@ int mpg_arnoldi_destroy(mpg_arnoldi_t a) {
     if (!a) return MPG_OK;
     if (a->ctx) (void)hipStreamSynchronize(a->ctx->stream);
     void* ps[] = {a->V, a->H, a->small, a->w[0], a->w[1], a->partial, a->sums, a->report,
-                  a->sell.off, a->sell.col, a->sell.val};
+                  a->counters, a->sell.off, a->sell.col, a->sell.val};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete a;
@@ -833,18 +935,20 @@ int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols) {
     return MPG_OK;
 }
 
-int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k) {
+// fold: 0 plain; 1 Givens(k-1) folded, ||w||^2 from sums[0]; 2 from the partials
+static int spmv_impl(mpg_arnoldi_t a, int k, int fold) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
+    if (fold && (k < 1 || a->d.m > kFoldMaxM)) return MPG_ERR_ARG;
     const mpg_csr* A = a->d.A;
-    const int ndots_all = a->d.orth == kOrthMGS ? 1 : k + 1;
     int st = dispatch(a->combo, [&](auto t, auto, auto p, auto vi) {
         using T = decltype(t);
         using P = decltype(p);
         using VI = decltype(vi);
         const P* diag = a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr;
+        GivensFold<T> gf{nullptr, 0, {}};
+        if (fold) gf = GivensFold<T>{fold == 2 ? a->partial : a->sums, fold == 2 ? a->last_G : 0, givens_args<T>(a, k - 1)};
         if (a->sell.nslices > 0) {
             const auto& S = a->sell;
-            a->dots_pending = true;
             return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
                 using CI = decltype(ci);
                 const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
@@ -852,19 +956,14 @@ int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k) {
                     a->d.n, S.nslices, S.off, static_cast<const CI*>(S.col),
                     static_cast<const typename SellStore<VI>::type*>(S.val), static_cast<const T*>(a->w[k & 1]),
                     static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k, diag,
-                    static_cast<T*>(a->w[(k + 1) & 1]));
+                    static_cast<T*>(a->w[(k + 1) & 1]), gf);
                 return (int)MPG_OK;
             });
         }
-        // dots inside the SpMV launch measured 71 us vs 30 + 20 us split
-        // (BAND-10M fp32, k = 0..29 mean): keep the separate panel kernel
-        const bool fused = kFuseDots && ndots_all <= kNC;
         k_step_spmv<T, P, VI><<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(
             A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,
             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,
-            diag, static_cast<T*>(a->w[(k + 1) & 1]), fused ? ndots_all : 0, a->partial);
-        a->last_G = rb_grid(a);
-        a->dots_pending = !fused;
+            diag, static_cast<T*>(a->w[(k + 1) & 1]), gf);
         return (int)MPG_OK;
     });
     if (st) return st;
@@ -872,19 +971,67 @@ int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k) {
     return MPG_OK;
 }
 
-int mpg_arnoldi_dots(mpg_arnoldi_t a, int k) {
+int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 0); }
+int mpg_arnoldi_givens_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 1); }
+int mpg_arnoldi_givens_partials_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 2); }
+int mpg_arnoldi_fold_max_m(void) { return kFoldMaxM; }
+
+static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
-    if (!a->dots_pending) return MPG_OK;  // formed inside the SpMV launch (kFuseDots)
     const int ndots_all = a->d.orth == kOrthMGS ? 1 : k + 1;
+    if (combine && ndots_all > kNC) return MPG_ERR_ARG;
     int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
         using T = decltype(t);
+        if (combine) {
+            k_panel_dots<T, kCombineBlock, true><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, 0, ndots_all, static_cast<const T*>(a->w[(k + 1) & 1]),
+                a->partial, a->counters, a->sums);
+            return (int)MPG_OK;
+        }
         for (int c0 = 0; c0 < ndots_all; c0 += kNC) {
             const int nc = ndots_all - c0 < kNC ? ndots_all - c0 : kNC;
             k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, c0, nc, static_cast<const T*>(a->w[(k + 1) & 1]),
-                a->partial);
+                a->partial, nullptr, nullptr);
         }
-        return MPG_OK;
+        return (int)MPG_OK;
+    });
+    a->last_G = combine ? a->Gd : row_grid(a);
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_dots(mpg_arnoldi_t a, int k) { return dots_impl(a, k, false); }
+int mpg_arnoldi_dots_sums(mpg_arnoldi_t a, int k) { return dots_impl(a, k, true); }
+
+static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens) {
+    if (!a || k < 0 || k >= a->d.m || pass < 0 || pass > 1 || k + 1 > 256) return MPG_ERR_ARG;
+    const bool cgsr = a->d.orth == kOrthCGSR;
+    const bool next_dots = cgsr && pass == 0;
+    if (givens && (next_dots || a->d.m > kFoldMaxM)) return MPG_ERR_ARG;
+    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
+        using T = decltype(t);
+        T* coef_out = pass == 0 ? static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) : static_cast<T*>(a->corr());
+        T* w = static_cast<T*>(a->w[(k + 1) & 1]);
+        const GivensArgs<T> g = givens_args<T>(a, k);
+        if (next_dots) {
+            k_cgs_update<T, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, a->sums, coef_out, w, a->partial, nullptr, g);
+            for (int c0 = kNC; c0 < k + 1; c0 += kNC) {
+                const int nc = k + 1 - c0 < kNC ? k + 1 - c0 : kNC;
+                k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                    a->d.n, static_cast<const T*>(a->V), a->ld, c0, nc, w, a->partial, nullptr, nullptr);
+            }
+        } else if (givens) {
+            k_cgs_update<T, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, a->sums, coef_out, w, a->partial, a->counters + 32,
+                g);
+        } else {
+            k_cgs_update<T, false><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, a->sums, coef_out, w, a->partial, nullptr, g);
+        }
+        return (int)MPG_OK;
     });
     a->last_G = row_grid(a);
     if (st) return st;
@@ -892,33 +1039,8 @@ int mpg_arnoldi_dots(mpg_arnoldi_t a, int k) {
     return MPG_OK;
 }
 
-int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass) {
-    if (!a || k < 0 || k >= a->d.m || pass < 0 || pass > 1 || k + 1 > 256) return MPG_ERR_ARG;
-    const bool cgsr = a->d.orth == kOrthCGSR;
-    const bool next_dots = cgsr && pass == 0;
-    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
-        using T = decltype(t);
-        T* coef_out = pass == 0 ? static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) : static_cast<T*>(a->corr());
-        T* w = static_cast<T*>(a->w[(k + 1) & 1]);
-        if (next_dots) {
-            k_cgs_update<T, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, a->sums, coef_out, w, a->partial);
-            for (int c0 = kNC; c0 < k + 1; c0 += kNC) {
-                const int nc = k + 1 - c0 < kNC ? k + 1 - c0 : kNC;
-                k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->V),
-                                                                            a->ld, c0, nc, w, a->partial);
-            }
-        } else {
-            k_cgs_update<T, false><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, a->sums, coef_out, w, a->partial);
-        }
-        return MPG_OK;
-    });
-    a->last_G = row_grid(a);
-    if (st) return st;
-    MPG_LAUNCH_CHECK(a->ctx);
-    return MPG_OK;
-}
+int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, false); }
+int mpg_arnoldi_cgs_givens(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, true); }
 
 int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j) {
     if (!a || k < 0 || k >= a->d.m || j < 0 || j > k) return MPG_ERR_ARG;
@@ -938,13 +1060,10 @@ int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j) {
 
 static int givens_impl(mpg_arnoldi_t a, int k, bool from_partials) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
-    const bool cgsr = a->d.orth == kOrthCGSR;
     int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
         using T = decltype(t);
-        k_givens<T><<<1, kBlock, 0, a->ctx->stream>>>(
-            k, a->d.m, from_partials ? a->partial : a->sums, from_partials ? a->last_G : 0,
-            cgsr ? static_cast<const T*>(a->corr()) : nullptr, static_cast<T*>(a->H), static_cast<T*>(a->cs()),
-            static_cast<T*>(a->sn()), static_cast<T*>(a->s()), static_cast<T*>(a->inv()), a->report);
+        k_givens<T><<<1, kBlock, 0, a->ctx->stream>>>(givens_args<T>(a, k), from_partials ? a->partial : a->sums,
+                                                      from_partials ? a->last_G : 0);
         return MPG_OK;
     });
     if (st) return st;

@@ -52,8 +52,13 @@ template <class S> struct VecW<S, 1> {
     static __device__ __forceinline__ void load(const S* p, S (&o)[1]) { o[0] = *p; }
 };
 
-// steps per batch: every load of a batch is issued before its gathers
-template <int W> constexpr int sell_unroll() { return W >= 8 ? 1 : 8 / W; }
+// entries per lane per batch: every load of a batch is issued before its
+// gathers, so a row of up to kSellBatch entries costs one load round trip
+#ifndef MPG_SELL_BATCH
+#define MPG_SELL_BATCH 16
+#endif
+constexpr int kSellBatch = MPG_SELL_BATCH;
+template <int W> constexpr int sell_unroll() { return W >= kSellBatch ? 1 : kSellBatch / W; }
 
 // fp64 row sum of row 64 s + lane (lane valid or not: all lanes take part).
 template <class S, class CI, int W, class XF>

@@ -74,6 +74,8 @@ struct FusedEngine::Impl {
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     bool use_graph = true;
+    bool fold = false;     // Givens step folded into the next SpMV launch
+    bool combine = false;  // last-arriver combines in the dots and CGS launches
     std::vector<int32_t> rowptr_host;
 
     ~Impl() {
@@ -260,6 +262,15 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
 
     const char* env = std::getenv("MPG_NO_GRAPH");
     I.use_graph = !(env && *env == '1') && (!comm || comm->capturable());
+    // Launch-count experiments, both off by default (BAND-10M, one MI355X):
+    // MPG_FOLD_GIVENS=1 folds Givens(k-1) into SpMV(k) — every SpMV workgroup
+    // sums the ||w||^2 partials itself: 18.0-18.3k vs 18.0k it/s, within noise;
+    // MPG_COMBINE=1 (one GPU, CGS/CGSR) does last-arriver combines in the dots
+    // and CGS launches: 15.1k it/s (1024 tickets on one counter serialise).
+    const char* cenv = std::getenv("MPG_COMBINE");
+    I.combine = !comm && cenv && *cenv == '1' && I.orth != MPG_ORTH_MGS && I.m <= mpg_arnoldi_fold_max_m();
+    const char* fenv = std::getenv("MPG_FOLD_GIVENS");
+    I.fold = !I.combine && fenv && *fenv == '1' && I.m <= mpg_arnoldi_fold_max_m();
     check(mpg_ctx_sync(ctx), "sync", ctx);
     setup_seconds = std::chrono::duration<double>(clk::now() - t0).count();
     prologue();
@@ -279,39 +290,65 @@ void FusedEngine::prologue() {
     check(mpg_arnoldi_prologue_finish(I.arn), "prologue_finish", I.ctx);
 }
 
-void FusedEngine::step(int k) {
+void FusedEngine::reduce(int nc) {
     Impl& I = *p_;
-    auto reduce = [&](int nc) {
-        check(mpg_arnoldi_reduce(I.arn, nc), "reduce", I.ctx);
-        if (I.comm) I.comm->allreduce_sum(mpg_arnoldi_sums_dev(I.arn), nc, I.stream());
-    };
-    if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
-    check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
-    check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
-    if (I.orth == MPG_ORTH_MGS) {
-        reduce(1);
-        for (int j = 0; j <= k; ++j) {
-            check(mpg_arnoldi_mgs(I.arn, k, j), "mgs", I.ctx);
-            if (j < k) reduce(1);
-        }
-    } else {
-        reduce(k + 1);
-        if (I.orth == MPG_ORTH_CGSR) {
-            check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
-            reduce(k + 1);
-            check(mpg_arnoldi_cgs(I.arn, k, 1), "cgs", I.ctx);
-        } else {
-            check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
-        }
-    }
-    // ||w||^2: one GPU folds the partial sums into the Givens kernel; ranks of
-    // a partitioned solve reduce + all-reduce first
+    check(mpg_arnoldi_reduce(I.arn, nc), "reduce", I.ctx);
+    if (I.comm) I.comm->allreduce_sum(mpg_arnoldi_sums_dev(I.arn), nc, I.stream());
+}
+
+// ||w||^2: one GPU folds the partial sums into the Givens kernel; ranks of a
+// partitioned solve reduce + all-reduce first
+void FusedEngine::givens(int k) {
+    Impl& I = *p_;
     if (I.comm) {
         reduce(1);
         check(mpg_arnoldi_givens(I.arn, k), "givens", I.ctx);
     } else {
         check(mpg_arnoldi_givens_partials(I.arn, k), "givens", I.ctx);
     }
+}
+
+// Arnoldi step k. fold: the Givens step k-1 rides in this step's SpMV
+// launch (k >= 1) and step k's own Givens is left to step k+1 / the caller.
+void FusedEngine::step(int k, bool fold) {
+    Impl& I = *p_;
+    if (fold && k > 0) {
+        if (I.comm) reduce(1);
+        if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
+        check(I.comm ? mpg_arnoldi_givens_spmv(I.arn, k) : mpg_arnoldi_givens_partials_spmv(I.arn, k), "givens+spmv",
+              I.ctx);
+    } else {
+        if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
+        check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
+    }
+    if (I.orth == MPG_ORTH_MGS) {
+        check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
+        reduce(1);
+        for (int j = 0; j <= k; ++j) {
+            check(mpg_arnoldi_mgs(I.arn, k, j), "mgs", I.ctx);
+            if (j < k) reduce(1);
+        }
+    } else {
+        // one GPU: the dots' last workgroup writes the sums, the last CGS
+        // pass's last workgroup runs the Givens step (no reduce / Givens launch)
+        if (I.combine && k + 1 <= 32) {
+            check(mpg_arnoldi_dots_sums(I.arn, k), "dots+sums", I.ctx);
+        } else {
+            check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
+            reduce(k + 1);
+        }
+        const int last_pass = I.orth == MPG_ORTH_CGSR ? 1 : 0;
+        if (last_pass == 1) {
+            check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
+            reduce(k + 1);
+        }
+        if (I.combine) {
+            check(mpg_arnoldi_cgs_givens(I.arn, k, last_pass), "cgs+givens", I.ctx);
+            return;
+        }
+        check(mpg_arnoldi_cgs(I.arn, k, last_pass), "cgs", I.ctx);
+    }
+    if (!fold) givens(k);
 }
 
 void FusedEngine::update(int k) { check(mpg_arnoldi_update(p_->arn, k), "update", p_->ctx); }
@@ -327,7 +364,9 @@ void FusedEngine::read_report(int count) {
 // steps 0..m-1, solution update with k = m, next residual prologue
 void FusedEngine::cycle_program() {
     Impl& I = *p_;
-    for (int k = 0; k < I.m; ++k) step(k);
+    const bool fold = I.fold;
+    for (int k = 0; k < I.m; ++k) step(k, fold);
+    if (fold) givens(I.m - 1);
     update(I.m);
     prologue();
 }
@@ -407,7 +446,7 @@ int FusedEngine::run(int max_cycles, bool& done) {
         }
         // adaptive restart strategies: one host read of |s(k+1)| per step
         for (int k = 0;; ++k) {
-            step(k);
+            step(k, false);
             read_report(4 + k + 1);
             const double res = I.report_host[4 + k];
             step_res.push_back(res);
@@ -468,14 +507,11 @@ double FusedEngine::phase_bytes(int which) const {
     const double sV = (double)dsize(I.ty.VI), sP = (double)dsize(I.ty.P);
     const double jac = I.args.prec == MPG_PREC_JACOBI ? 1.0 : 0.0;
     if (which == 0) {
-        // matrix (CSR: values + int32 columns + row pointers; SELL-64:
-        // values + int32/int16 columns + slice offsets, padding not
-        // counted), v_k gathered (read once), w and V(:,k) written, Jacobi
-        // diagonal read
-        int32_t fmt = 1, cb = 4;
-        mpg_arnoldi_spmv_layout(I.arn, &fmt, nullptr, &cb, nullptr);
-        const double mat = fmt == 2 ? z * (sV + cb) + ((n + 63) / 64 + 1) * 8 : z * (sV + 4) + (n + 1) * 4;
-        return mat + 3 * n * sT + jac * n * sP;
+        // SURVEY §8(d) B_spmv, the same for every storage: CSR values + int32
+        // columns + row pointers, x read once, y written (the SELL-64 copy
+        // moves fewer bytes; profiles/ PMC traffic shows the actual ones),
+        // plus the Jacobi diagonal when the preconditioner is fused in
+        return z * (sV + 4) + (n + 1) * 4 + 2 * n * sT + jac * n * sP;
     }
     if (which == 1) return z * (sX + 4) + (n + 1) * 4 + 3 * n * sX + n * sT + jac * n * sP;
     if (which == 3) {
@@ -498,12 +534,18 @@ double FusedEngine::time_phase(int which, int reps) {
     float total_ms = 0;
     int launches = 0;
     const int ks = which == 1 ? 1 : I.m;
+    const bool fold = I.fold;  // the form cycle_program launches
     for (int k = 0; k < ks; ++k) {
         hipck(hipEventRecord(e0, I.stream()), "record");
         for (int r = 0; r < reps; ++r) {
-            if (which == 0) check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
+            if (which == 0 && fold && k > 0)
+                check(I.comm ? mpg_arnoldi_givens_spmv(I.arn, k) : mpg_arnoldi_givens_partials_spmv(I.arn, k),
+                      "givens+spmv", I.ctx);
+            else if (which == 0) check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
             else if (which == 1) check(mpg_arnoldi_prologue(I.arn), "prologue", I.ctx);
+            else if (which == 3 && I.combine && k + 1 <= 32) check(mpg_arnoldi_dots_sums(I.arn, k), "dots", I.ctx);
             else if (which == 3) check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
+            else if (I.combine && I.orth == MPG_ORTH_CGS) check(mpg_arnoldi_cgs_givens(I.arn, k, 0), "cgs", I.ctx);
             else check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
         }
         hipck(hipEventRecord(e1, I.stream()), "record");

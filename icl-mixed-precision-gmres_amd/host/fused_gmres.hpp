@@ -90,7 +90,9 @@ private:
     std::unique_ptr<Impl> p_;
     std::unique_ptr<Convergence<double, void>> conv_;
     void prologue();
-    void step(int k);
+    void step(int k, bool fold);
+    void reduce(int nc);
+    void givens(int k);
     void update(int k);
     void read_report(int count);
     void cycle_program();

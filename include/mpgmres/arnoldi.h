@@ -87,6 +87,23 @@ int mpg_arnoldi_givens(mpg_arnoldi_t a, int k);
 /* single-GPU form: the Givens kernel sums the ||w||^2 partials of the last
  * producer itself, saving one mpg_arnoldi_reduce launch per step */
 int mpg_arnoldi_givens_partials(mpg_arnoldi_t a, int k);
+/* Givens step k-1 folded into the SpMV launch of step k (1 <= k < m, m <=
+ * mpg_arnoldi_fold_max_m()): every workgroup forms 1/h_{k,k-1} from the
+ * ||w||^2 sum itself and workgroup 0 runs the rotation step — one launch
+ * boundary fewer per Arnoldi step. _partials_ reads the last producer's
+ * workgroup partials (one GPU), the other form sums[0] (after an all-reduce).
+ * The last step's Givens (k = m-1) stays a separate mpg_arnoldi_givens*. */
+int mpg_arnoldi_givens_spmv(mpg_arnoldi_t a, int k);
+/* One-GPU combined forms (no separate reduce / Givens launch): the phase's
+ * workgroup partials are written through to memory and the last workgroup
+ * to finish sums them in a fixed order. dots_sums: panel dots for k+1 <= 32
+ * columns straight into sums (replaces dots + reduce); cgs_givens: the last
+ * CGS pass (pass 0 for CGS, 1 for CGSR) followed by the Givens step k
+ * (replaces cgs + givens_partials; m <= mpg_arnoldi_fold_max_m()). */
+int mpg_arnoldi_dots_sums(mpg_arnoldi_t a, int k);
+int mpg_arnoldi_cgs_givens(mpg_arnoldi_t a, int k, int pass);
+int mpg_arnoldi_givens_partials_spmv(mpg_arnoldi_t a, int k);
+int mpg_arnoldi_fold_max_m(void);
 int mpg_arnoldi_update(mpg_arnoldi_t a, int k);
 /* sums[c] = sum over workgroups of partial column c, c < ncols */
 int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols);

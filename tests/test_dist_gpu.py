@@ -23,9 +23,11 @@ def mats(mpg):
     return inputs(mpg)
 
 
+@pytest.mark.parametrize("fold", ["0", "1"], ids=["givens", "fold"])
 @pytest.mark.parametrize("nranks", [2, 3])
 @pytest.mark.parametrize("rec", PICK, ids=lambda c: "-".join(str(c["case"][k]) for k in ("matrix", "mode", "orth", "prec")))
-def test_loopback_golden(mpg, mats, rec, nranks):
+def test_loopback_golden(mpg, mats, rec, nranks, fold, monkeypatch):
+    monkeypatch.setenv("MPG_FOLD_GIVENS", fold)
     case = dict(rec["case"])
     A = mats[case.pop("matrix")]
     xt = mpg.rand_vect(A.nrows, 42)

@@ -25,19 +25,30 @@ def _case_id(c):
     return f"{k['matrix']}-{k['mode']}-{k['orth']}-{k['prec']}-m{k['rlen']}"
 
 
-# fused engine on both Arnoldi SpMV storages: CSR row blocks and SELL-64
-ENGINES = {"surface": ("surface", "auto"), "fused-csr": ("fused", "csr"), "fused-sell": ("fused", "sell")}
+# fused engine on both Arnoldi SpMV storages (CSR row blocks, SELL-64), and
+# with the two launch-count variants: the Givens step folded into the next
+# SpMV launch, and the one-GPU last-arriver combines
+# (engine, storage, MPG_COMBINE, MPG_FOLD_GIVENS)
+ENGINES = {"surface": ("surface", "auto", "0", "0"), "fused-csr": ("fused", "csr", "0", "0"),
+           "fused-sell": ("fused", "sell", "0", "0"), "fused-fold": ("fused", "auto", "0", "1"),
+           "fused-combine": ("fused", "auto", "1", "0")}
+
+
+def _engine(monkeypatch, engine):
+    eng, fmt, combine, fold = ENGINES[engine]
+    monkeypatch.setenv("MPG_COMBINE", combine)
+    monkeypatch.setenv("MPG_FOLD_GIVENS", fold)
+    return dict(engine=eng, spmv_format=fmt)
 
 
 @pytest.mark.parametrize("engine", list(ENGINES))
 @pytest.mark.parametrize("rec", GOLDEN["cases"], ids=_case_id)
-def test_golden(mpg, mats, rec, engine):
+def test_golden(mpg, mats, rec, engine, monkeypatch):
     case = dict(rec["case"])
     A = mats[case.pop("matrix")]
     xt = mpg.rand_vect(A.nrows, 42)
     b = mpg.host_spmv(A, xt)
-    eng, fmt = ENGINES[engine]
-    got = mpg.solve(A, b, xt, engine=eng, spmv_format=fmt, **case)
+    got = mpg.solve(A, b, xt, **_engine(monkeypatch, engine), **case)
     compare(rec, got, case["mode"], case["tol"], case["rlen"], _case_id(rec) + "/" + engine)
 
 
@@ -88,15 +99,14 @@ def test_spmv_layout_choice(mpg):
 
 @pytest.mark.parametrize("engine", list(ENGINES))
 @pytest.mark.parametrize("mode", ["mixed", "baseline"])
-def test_live_oracle_band(mpg, oracle, engine, mode):
+def test_live_oracle_band(mpg, oracle, engine, mode, monkeypatch):
     """Larger input than the fixtures: BAND n=200k, GMRES(30), live oracle."""
     A = mpg.gen_band(200_000, 5, 4, seed=7)
     xt = mpg.rand_vect(A.nrows, 42)
     b = mpg.host_spmv(A, xt)
     opts = dict(mode=mode, orth="cgs", prec="jacobi", rlen=30, tol=1e-9, max_restarts=40)
     ref = oracle.solve(mpg, A, b, xt, **opts)
-    eng, fmt = ENGINES[engine]
-    got = mpg.solve(A, b, xt, engine=eng, spmv_format=fmt, **opts)
+    got = mpg.solve(A, b, xt, **_engine(monkeypatch, engine), **opts)
     compare(as_ref(ref), got, mode, opts["tol"], 30, f"band200k-{mode}-{engine}")
     if mode == "baseline":  # same restart count -> comparable final residuals
         assert abs(got.res_norm - ref.res_norm) <= 0.5 * ref.res_norm + 1e-12 * np.linalg.norm(b)
