@@ -45,6 +45,9 @@ def lib() -> C.CDLL:
         _lib.oracle_rotg_f32.argtypes = [p, p, p, p]
         _lib.oracle_jacobi_f64.argtypes = [i, p, p, p, p]
         _lib.oracle_jacobi_f32.argtypes = [i, p, p, p, p]
+        for t in ("f64", "f32"):
+            getattr(_lib, f"oracle_ilu0_{t}").argtypes = [i, p, p, p, p, p]
+            getattr(_lib, f"oracle_ilu_apply_{t}").argtypes = [i, p, p, p, i, i, p]
     return _lib
 
 
@@ -121,3 +124,26 @@ def jacobi(A, dtype=np.float64) -> np.ndarray:
     fn = lib().oracle_jacobi_f64 if dtype == np.float64 else lib().oracle_jacobi_f32
     fn(A.nrows, _ptr(A.rowptr), _ptr(A.col), _ptr(A.val), _ptr(d))
     return d
+
+
+def ilu0(A, dtype=np.float64):
+    """ILU(0) factors (CSR order) and diagonal positions of A (oracle ilu0)."""
+    lu = np.zeros(A.nnz, dtype=dtype)
+    di = np.zeros(A.nrows, dtype=np.int32)
+    fn = lib().oracle_ilu0_f64 if dtype == np.float64 else lib().oracle_ilu0_f32
+    if fn(A.nrows, _ptr(A.rowptr), _ptr(A.col), _ptr(np.ascontiguousarray(A.val, dtype=np.float64)), _ptr(lu),
+          _ptr(di)):
+        raise ValueError("oracle ilu0 failed")
+    return lu, di
+
+
+def ilu_apply(A, x: np.ndarray, kind="ilu", steps=1, dtype=np.float64) -> np.ndarray:
+    """One preconditioner apply M^-1 x with M = ILU(0)(A) ("ilu": exact
+    triangular solves; "ilu_jacobi": `steps` Jacobi sweeps per factor)."""
+    kinds = {"ilu": 0, "ilu_jacobi": 1}
+    x = np.array(x, dtype=dtype)
+    fn = lib().oracle_ilu_apply_f64 if dtype == np.float64 else lib().oracle_ilu_apply_f32
+    if fn(A.nrows, _ptr(A.rowptr), _ptr(A.col), _ptr(np.ascontiguousarray(A.val, dtype=np.float64)), kinds[kind],
+          steps, _ptr(x)):
+        raise ValueError("oracle ILU apply failed")
+    return x

@@ -62,6 +62,8 @@ void load() {
     bind(h, a.s_create_csr, "mkl_sparse_s_create_csr", ok);
     bind(h, a.d_mv, "mkl_sparse_d_mv", ok);
     bind(h, a.s_mv, "mkl_sparse_s_mv", ok);
+    bind(h, a.d_trsv, "mkl_sparse_d_trsv", ok);
+    bind(h, a.s_trsv, "mkl_sparse_s_trsv", ok);
     bind(h, a.destroy, "mkl_sparse_destroy", ok);
     bind(h, a.set_num_threads, "MKL_Set_Num_Threads", ok);
     bind(h, a.get_max_threads, "MKL_Get_Max_Threads", ok);

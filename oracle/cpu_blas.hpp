@@ -18,7 +18,8 @@ namespace oracle {
 
 // CBLAS / MKL sparse enum values (LP64 interface)
 enum { kColMajor = 102, kNoTrans = 111, kTrans = 112, kUpper = 121, kLower = 122, kNonUnit = 131 };
-enum { kSparseOpNoTrans = 10, kSparseTypeGeneral = 20, kSparseIndexZero = 0 };
+enum { kSparseOpNoTrans = 10, kSparseTypeGeneral = 20, kSparseTypeTriangular = 23, kSparseIndexZero = 0 };
+enum { kSparseFillLower = 40, kSparseFillUpper = 41, kSparseDiagNonUnit = 50, kSparseDiagUnit = 51 };
 struct SparseDescr {
     int type, mode, diag;
 };
@@ -46,6 +47,8 @@ struct MklApi {
     int (*s_create_csr)(void**, int, int, int, int*, int*, int*, float*) = nullptr;
     int (*d_mv)(int, double, void*, SparseDescr, const double*, double, double*) = nullptr;
     int (*s_mv)(int, float, void*, SparseDescr, const float*, float, float*) = nullptr;
+    int (*d_trsv)(int, double, void*, SparseDescr, const double*, double*) = nullptr;
+    int (*s_trsv)(int, float, void*, SparseDescr, const float*, float*) = nullptr;
     int (*destroy)(void*) = nullptr;
     void (*set_num_threads)(int) = nullptr;
     int (*get_max_threads)() = nullptr;

@@ -114,26 +114,167 @@ void cast(const std::vector<S>& x, std::vector<D>& y) {
     for (size_t i = 0; i < x.size(); ++i) y[i] = (D)x[i];
 }
 
-// ---- preconditioners (types.hpp:374-448) ----
+// ---- preconditioners (types.hpp:251-448, kernels.hpp:168-248) ----
+
+// ILU(0) of the fp64 matrix (ilu0_impl, kernels_mkl.cpp:416-500), with the
+// one change that makes it an ILU: the reference allocates diag_inds (448)
+// but never fills it, so every pivot lookup reads entry 0; here
+// diag_inds[i] is the position of a_ii. Everything else is as written there:
+// rows 1..n-1 in order (row 0 is neither eliminated nor boosted), the
+// sorted merge of row i with the upper part of row k, pivots pushed away
+// from zero to +-alpha (sign kept), alpha = max_i sum_j |a_ij| * eps(T).
+// (cuSPARSE csrilu02's numeric boost, kernels_cuda.cpp:745-746, replaces a
+// small pivot by +alpha in every row; the two agree whenever no pivot is
+// smaller than alpha.) Returns the factors in fp64; the caller rounds to T.
+template <class T>
+void ilu0(int n, const int* rp, const int* ci, const double* v64, std::vector<double>& lu, std::vector<int>& di) {
+    double alpha = 0;
+    for (int i = 0; i < n; ++i) {
+        double sum = 0;
+        for (int k = rp[i]; k < rp[i + 1]; ++k) sum += std::fabs(v64[k]);
+        if (alpha < sum) alpha = sum;
+    }
+    alpha *= std::numeric_limits<T>::epsilon();
+    lu.assign(v64, v64 + rp[n]);
+    di.assign((size_t)n, -1);
+    for (int i = 0; i < n; ++i)
+        for (int k = rp[i]; k < rp[i + 1]; ++k)
+            if (ci[k] == i) {
+                di[(size_t)i] = k;
+                break;
+            }
+    for (int i = 0; i < n; ++i)
+        if (di[(size_t)i] < 0) throw std::invalid_argument("ILU(0) needs an explicit diagonal entry in every row");
+    for (int i = 1; i < n; ++i) {
+        const int rowEnd = rp[i + 1];
+        for (int k_ind = rp[i]; ci[k_ind] < i; ++k_ind) {
+            const int k = ci[k_ind];
+            int prev_ind = di[(size_t)k];
+            const int prev_end = rp[k + 1];
+            const double factor = lu[(size_t)k_ind] / lu[(size_t)prev_ind];
+            lu[(size_t)k_ind] = factor;
+            prev_ind += 1;
+            for (int j_ind = k_ind + 1; j_ind < rowEnd && prev_ind < prev_end;) {
+                if (ci[prev_ind] < ci[j_ind]) {
+                    ++prev_ind;
+                } else if (ci[prev_ind] > ci[j_ind]) {
+                    ++j_ind;
+                } else {
+                    const double p = factor * lu[(size_t)prev_ind];
+                    lu[(size_t)j_ind] -= p;
+                    ++prev_ind;
+                    ++j_ind;
+                }
+            }
+        }
+        double& d = lu[(size_t)di[(size_t)i]];
+        if (d >= 0) {
+            if (d < alpha) d = alpha;
+        } else {
+            if (d > -alpha) d = -alpha;
+        }
+    }
+}
+
 template <class T>
 struct Prec {
-    bool jacobi = false;
-    std::vector<T> d;
+    int kind = MPG_PREC_IDENTITY;
+    std::vector<T> d;  // Jacobi: inverse boosted diagonal; ILU-Jacobi: 1/u_ii (types.hpp:305-316)
+    // ILU(0) factors in one CSR (unit-lower L below the diagonal, U on and
+    // above it), precision T, with an MKL handle for the triangular solves
+    std::unique_ptr<Csr<T>> lu;
+    std::vector<int> di;
+    int steps = 1;
+    mutable std::vector<T> t1, t2;
+
     void apply(T* w, int n) const {
-        if (!jacobi) return;
-        // gdmv(1.0, diag, w, 0.0, w): y = 0*y + 1*d*x
-        for (int i = 0; i < n; ++i) w[i] = T(0) * w[i] + T(1) * d[(size_t)i] * w[i];
+        if (kind == MPG_PREC_JACOBI) {
+            // gdmv(1.0, diag, w, 0.0, w): y = 0*y + 1*d*x
+            for (int i = 0; i < n; ++i) w[i] = T(0) * w[i] + T(1) * d[(size_t)i] * w[i];
+        } else if (kind == MPG_PREC_ILU) {
+            ilusv(w, n);
+        } else if (kind == MPG_PREC_ILU_JACOBI) {
+            ilusv_jacobi(w, n);
+        }
+    }
+
+    // ilusv (kernels_mkl.cpp:355-384): L then U sparse triangular solves
+    void ilusv(T* x, int n) const {
+        if (mkl().loaded) {
+            t1.assign(x, x + n);
+            trsv_mkl(SparseDescr{kSparseTypeTriangular, kSparseFillLower, kSparseDiagUnit}, t1.data(), x);
+            t1.assign(x, x + n);
+            trsv_mkl(SparseDescr{kSparseTypeTriangular, kSparseFillUpper, kSparseDiagNonUnit}, t1.data(), x);
+            return;
+        }
+        const auto& A = *lu;
+        for (int i = 0; i < n; ++i) {
+            double s = x[i];
+            for (int k = A.rp[i]; k < di[(size_t)i]; ++k) s -= (double)A.v[(size_t)k] * (double)x[A.ci[k]];
+            x[i] = (T)s;
+        }
+        for (int i = n - 1; i >= 0; --i) {
+            double s = x[i];
+            for (int k = di[(size_t)i] + 1; k < A.rp[i + 1]; ++k) s -= (double)A.v[(size_t)k] * (double)x[A.ci[k]];
+            x[i] = (T)(s / (double)A.v[(size_t)di[(size_t)i]]);
+        }
+    }
+    void trsv_mkl(SparseDescr dsc, const T* in, T* out) const;
+
+    // ilusv_jacobi (kernels.hpp:219-248) with the generic ilu_jacobi_mv
+    // (kernels.hpp:171-210): `steps` Jacobi sweeps on L, then on U
+    void ilusv_jacobi(T* x, int n) const {
+        const auto& A = *lu;
+        t1.assign(x, x + n);  // b
+        t2.resize((size_t)n);
+        for (int s = 0; s < steps; ++s) {
+            for (int i = 0; i < n; ++i) {  // temp = b; temp = 1*temp + (-1)*(x_i + L x)
+                T sum = x[i];
+                for (int j = A.rp[i]; j < di[(size_t)i]; ++j) sum += A.v[(size_t)j] * x[A.ci[j]];
+                t2[(size_t)i] = T(1) * t1[(size_t)i] + T(-1) * sum;
+            }
+            axpy(n, T(1), t2.data(), x);
+        }
+        t1.assign(x, x + n);
+        for (int s = 0; s < steps; ++s) {
+            for (int i = 0; i < n; ++i) {  // temp = b; temp = 1.0*temp + -1.0*(U x)
+                T sum = 0;
+                for (int j = di[(size_t)i]; j < A.rp[i + 1]; ++j) sum += A.v[(size_t)j] * x[A.ci[j]];
+                t2[(size_t)i] = T(1.0) * t1[(size_t)i] + T(-1.0) * sum;
+            }
+            for (int i = 0; i < n; ++i) x[i] = T(1) * x[i] + T(1) * d[(size_t)i] * t2[(size_t)i];  // gdmv
+        }
     }
 };
+template <>
+void Prec<double>::trsv_mkl(SparseDescr dsc, const double* in, double* out) const {
+    if (mkl().d_trsv(kSparseOpNoTrans, 1.0, lu->h, dsc, in, out)) throw std::runtime_error("mkl_sparse_d_trsv failed");
+}
+template <>
+void Prec<float>::trsv_mkl(SparseDescr dsc, const float* in, float* out) const {
+    if (mkl().s_trsv(kSparseOpNoTrans, 1.0f, lu->h, dsc, in, out)) throw std::runtime_error("mkl_sparse_s_trsv failed");
+}
 
 // Jacobi<T>(A) with A converted to T first (the implicit SparseMatrix<T>
-// conversion at the call site, gmres_perf_test.cpp:80, 151).
+// conversion at the call site, gmres_perf_test.cpp:80, 151); ILU / ILU-Jacobi
+// from ilu0<T>(A) on the fp64 A (gmres_perf_test.cpp:70-79, 140-149).
 template <class T>
-Prec<T> make_prec(int kind, int n, const int* rp, const int* ci, const double* v64) {
+Prec<T> make_prec(int kind, int n, const int* rp, const int* ci, const double* v64, int steps = 1) {
     Prec<T> M;
+    M.kind = kind;
     if (kind == MPG_PREC_IDENTITY) return M;
-    if (kind != MPG_PREC_JACOBI) throw std::invalid_argument("ILU preconditioners are not part of the oracle");
-    M.jacobi = true;
+    if (kind == MPG_PREC_ILU || kind == MPG_PREC_ILU_JACOBI) {
+        std::vector<double> f;
+        ilu0<T>(n, rp, ci, v64, f, M.di);
+        M.lu = make_csr<T>(n, rp, ci, f.data());
+        M.steps = steps;
+        if (kind == MPG_PREC_ILU_JACOBI) {
+            M.d.resize((size_t)n);
+            for (int i = 0; i < n; ++i) M.d[(size_t)i] = 1 / M.lu->v[(size_t)M.di[(size_t)i]];
+        }
+        return M;
+    }
+    if (kind != MPG_PREC_JACOBI) throw std::invalid_argument("unknown preconditioner");
     M.d.resize((size_t)n);
     T alpha = 0;
     for (int i = 0; i < n; ++i) {
@@ -509,7 +650,7 @@ void run_baseline(const mpg_solve_args& a, const Csr<double>& A, mpg_solve_resul
     std::vector<float> vf;
     cast(A.v, vf);
     auto At = make_csr<T>(n, a.rowptr, a.col, vf.data());
-    Prec<P> M = make_prec<P>(a.prec, n, a.rowptr, a.col, a.val);
+    Prec<P> M = make_prec<P>(a.prec, n, a.rowptr, a.col, a.val, a.jacobi_steps);
     r->setup_seconds = since(t0);
     std::vector<T> xt((size_t)n, T(0)), bt((size_t)n);
     for (int i = 0; i < n; ++i) bt[(size_t)i] = (T)a.b[i];
@@ -532,7 +673,7 @@ void run_mixed(const mpg_solve_args& a, const Csr<double>& A, mpg_solve_result* 
     std::vector<double> x((size_t)n, 0.0), b(a.b, a.b + n);
     auto t0 = clk::now();
     auto As = make_csr<float>(n, a.rowptr, a.col, a.val);
-    Prec<float> M = make_prec<float>(a.prec, n, a.rowptr, a.col, a.val);
+    Prec<float> M = make_prec<float>(a.prec, n, a.rowptr, a.col, a.val, a.jacobi_steps);
     r->setup_seconds = since(t0);
     Strategy st = make_strategy(a);
     auto t1 = clk::now();
@@ -616,6 +757,52 @@ void oracle_jacobi_f64(int n, const int* rp, const int* ci, const double* v, dou
 void oracle_jacobi_f32(int n, const int* rp, const int* ci, const double* v, float* d) {
     auto M = oracle::make_prec<float>(MPG_PREC_JACOBI, n, rp, ci, v);
     std::memcpy(d, M.d.data(), sizeof(float) * (size_t)n);
+}
+
+// ILU(0) factors (values in CSR order, rounded to fp64 or fp32) and the
+// diagonal positions; then one apply of ILU (exact triangular solves) or of
+// ILU-Jacobi with `steps` sweeps, in place on x
+int oracle_ilu0_f64(int n, const int* rp, const int* ci, const double* v, double* lu, int* di) {
+    try {
+        std::vector<double> f;
+        std::vector<int> d;
+        oracle::ilu0<double>(n, rp, ci, v, f, d);
+        std::memcpy(lu, f.data(), sizeof(double) * f.size());
+        std::memcpy(di, d.data(), sizeof(int) * d.size());
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+int oracle_ilu0_f32(int n, const int* rp, const int* ci, const double* v, float* lu, int* di) {
+    try {
+        std::vector<double> f;
+        std::vector<int> d;
+        oracle::ilu0<float>(n, rp, ci, v, f, d);
+        for (size_t k = 0; k < f.size(); ++k) lu[k] = (float)f[k];
+        std::memcpy(di, d.data(), sizeof(int) * d.size());
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+int oracle_ilu_apply_f64(int n, const int* rp, const int* ci, const double* v, int kind, int steps, double* x) {
+    try {
+        auto M = oracle::make_prec<double>(kind, n, rp, ci, v, steps);
+        M.apply(x, n);
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+int oracle_ilu_apply_f32(int n, const int* rp, const int* ci, const double* v, int kind, int steps, float* x) {
+    try {
+        auto M = oracle::make_prec<float>(kind, n, rp, ci, v, steps);
+        M.apply(x, n);
+        return 0;
+    } catch (...) {
+        return -1;
+    }
 }
 
 }  // extern "C"

@@ -10,6 +10,7 @@ array arithmetic in the reference's precisions:
   Givens              kernels_mkl.cpp:214-260 (reference-BLAS rotg, b := 0)
   Convergence (base)  IterUtil.hpp:17-81
   Jacobi              types.hpp:393-431
+  ILU(0), ILU-Jacobi  kernels_mkl.cpp:416-500 (diag_inds filled), kernels.hpp:171-248
 Only the base restart strategy is restated here. BLAS reductions use NumPy's
 own summation order, so agreement with the MKL oracle is to round-off, not
 bitwise.
@@ -43,6 +44,62 @@ def jacobi_diag(rowptr, col, val64, dt):
         a = v[j]
         d[i] = dt(1) / (max(a, alpha) if a >= 0 else min(a, -alpha))
     return d
+
+
+def ilu0_factors(A, dt):
+    """ILU(0) by the dictionary-of-rows IKJ form (an independent restatement
+    of ilu0_impl, kernels_mkl.cpp:416-500, with diag_inds filled): rows 1..n-1,
+    eliminations in increasing column order, pivots pushed to +-alpha with
+    alpha = max row |sum| * eps(dt). Returns (L strict lower, U upper with
+    the diagonal) as scipy CSR in dt."""
+    import scipy.sparse as sp
+
+    n = A.nrows
+    rows = []
+    for i in range(n):
+        rows.append({int(c): float(v) for c, v in zip(A.col[A.rowptr[i]:A.rowptr[i + 1]],
+                                                      A.val[A.rowptr[i]:A.rowptr[i + 1]])})
+    alpha = max(sum(abs(v) for v in r.values()) for r in rows) * float(np.finfo(dt).eps)
+    for i in range(1, n):
+        ri = rows[i]
+        for k in sorted(c for c in ri if c < i):
+            f = ri[k] / rows[k][k]
+            ri[k] = f
+            for j, u in rows[k].items():
+                if j > k and j in ri:
+                    ri[j] -= f * u
+        d = ri[i]
+        ri[i] = (alpha if d < alpha else d) if d >= 0 else (-alpha if d > -alpha else d)
+    lo, up = sp.lil_matrix((n, n)), sp.lil_matrix((n, n))
+    for i, r in enumerate(rows):
+        for j, v in r.items():
+            (lo if j < i else up)[i, j] = v
+    return lo.tocsr().astype(dt), up.tocsr().astype(dt)
+
+
+def ilu_apply(Lo, Up, x, dt, kind="ilu", steps=1):
+    """M^-1 x: exact unit-lower then upper solves, or `steps` Jacobi sweeps
+    on each factor (ilusv_jacobi, kernels.hpp:219-248)."""
+    from scipy.sparse.linalg import spsolve_triangular
+
+    x = x.astype(dt)
+    if kind == "ilu":
+        n = Lo.shape[0]
+        import scipy.sparse as sp
+
+        y = spsolve_triangular((Lo + sp.identity(n, dtype=dt, format="csr")).astype(np.float64),
+                               x.astype(np.float64), lower=True, unit_diagonal=True)
+        return spsolve_triangular(Up.astype(np.float64), y, lower=False).astype(dt)
+    b = x.copy()
+    for _ in range(steps):
+        t = (b - (x + (Lo @ x).astype(dt))).astype(dt)
+        x = (x + t).astype(dt)
+    b = x.copy()
+    d = (dt(1) / Up.diagonal()).astype(dt)
+    for _ in range(steps):
+        t = (b - (Up @ x).astype(dt)).astype(dt)
+        x = (x + d * t).astype(dt)
+    return x
 
 
 class _Problem:
@@ -99,15 +156,18 @@ def _cycle(Aop, apply_m, w, m, orth, dt, minvb, history):
     return y, V
 
 
-def solve(A, b, mode="mixed", orth="mgs", prec="identity", rlen=30, tol=1e-6, max_restarts=1000):
+def solve(A, b, mode="mixed", orth="mgs", prec="identity", rlen=30, tol=1e-6, max_restarts=1000, jacobi_steps=1):
     """Returns dict(status, restarts, total_iters, cyc_r_norm, cyc_normalization, cyc_beta, step_res, x)."""
     n = A.nrows
     m = rlen
     T = np.float32 if mode in ("mixed", "single") else np.float64
     P = np.float32 if mode in ("mixed", "single", "single-prec") else np.float64
     d = jacobi_diag(A.rowptr, A.col, A.val, P) if prec == "jacobi" else None
+    lu = ilu0_factors(A, P) if prec in ("ilu", "ilu_jacobi") else None
 
     def apply_m(v, into=T):
+        if lu is not None:
+            return ilu_apply(lu[0], lu[1], v.astype(P), P, prec, jacobi_steps).astype(into)
         if d is None:
             return v.astype(into)
         return (d * v.astype(P)).astype(into)
