@@ -17,6 +17,7 @@
 // operator-surface driver agree to the last bit in most steps.
 #include "csr_tile.hpp"
 #include "sell_tile.hpp"
+#include "handoff.hpp"
 #include "internal.hpp"
 #include "mpgmres/arnoldi.h"
 
@@ -77,40 +78,6 @@ __device__ __forceinline__ void butterfly_round(double (&acc)[N], int lane) {
         }
         butterfly_round<H / 2, MASK / 2>(acc, lane);
     }
-}
-
-// ---------------------------------------------------------------- in-launch combine
-// Last-arriver hand-off (one GPU): every workgroup stores its partials
-// write-through (sc1, so no release fence is needed for them), drains its
-// stores, and one lane draws a ticket; the workgroup that draws the last one
-// takes an agent-scope acquire and combines all partials in a fixed order
-// (deterministic, placement-independent). The counter is re-armed by the
-// last arriver; it starts zeroed (hipMemset at plan creation).
-typedef __attribute__((address_space(1))) unsigned int gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-
-__device__ __forceinline__ void store_wt(double* p, double v) {
-    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// true in every thread of the last-arriving workgroup (after its acquire)
-__device__ __forceinline__ bool last_arriver(unsigned* cnt) {
-    __shared__ int last_s;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = t == gridDim.x - 1;
-        if (last) {
-            __hip_atomic_store((gu32*)cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        last_s = last;
-    }
-    __syncthreads();
-    return last_s != 0;
 }
 
 // Block-reduce NCOL fp64 accumulators and store them as partial[c*G + blk]
@@ -202,6 +169,15 @@ __global__ void k_prologue_finish(const double* __restrict__ sums, int m, T* __r
         *inv = iv;
     }
     for (int i = threadIdx.x; i <= m; i += blockDim.x) s[i] = i == 0 ? beta : T(0);
+}
+
+// ||w||^2 partials again (column 1 of the prologue's partials, same grid)
+// after a preconditioner applied outside the prologue kernel (ILU)
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_wnorm_partials(int n, const T* __restrict__ w, double* __restrict__ partial) {
+    double acc[1] = {0.0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) acc[0] += (double)w[i] * (double)w[i];
+    store_partials<1>(acc, 1, partial + gridDim.x);
 }
 
 // ---------------------------------------------------------------- reductions
@@ -909,6 +885,19 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
         return MPG_OK;
     });
     a->last_G = rb_grid(a);
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_prologue_wnorm(mpg_arnoldi_t a) {
+    if (!a) return MPG_ERR_ARG;
+    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
+        using T = decltype(t);
+        k_wnorm_partials<T><<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->w[0]),
+                                                                      a->partial);
+        return (int)MPG_OK;
+    });
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;

@@ -1,0 +1,425 @@
+// ILU(0) factorisation, sync-free triangular solves and ILU-Jacobi sweeps
+// on gfx950 (include/mpgmres/ilu.h).
+//
+// Factorisation and solves hand rows out in order through an atomic ticket:
+// a wave64 takes the next row, waits (handoff.hpp) only for the rows that
+// row reads, computes it, stores it write-through and raises the row's
+// flag. A wave only ever waits for rows taken earlier by running waves, so
+// the schedule always progresses; every wait is bounded (a fault is
+// recorded instead of hanging the GPU).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <limits>
+#include <new>
+#include <type_traits>
+
+#include "handoff.hpp"
+#include "internal.hpp"
+#include "mpgmres/ilu.h"
+
+using namespace mpg;
+
+namespace {
+
+constexpr int kRowCap = 512;                 // entries of one row staged in LDS
+constexpr int kWaves = kBlock / kWave;       // 4 rows in flight per workgroup
+constexpr int kPersistGroups = 2048;         // 8 workgroups per CU
+constexpr uint64_t kDeadline = 3000000000ull;  // 30 s of the 100 MHz clock: a wave gives up (fault 2)
+
+// sync block layout (ints): [0, n) factor / L flags, [n, 2n) U flags, then
+// tickets at 2n + 0 / 32 / 64 / 96 (separate 128-B lines), the fault word at 2n + 128
+inline size_t sync_ints(int n) { return 2 * (size_t)n + 160; }
+
+// ---------------------------------------------------------------- set-up
+__global__ void k_find_diag(int n, const int* __restrict__ rowptr, const int* __restrict__ col, int* __restrict__ diag,
+                            int* __restrict__ bad) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int d = -1;
+    for (int k = rowptr[i]; k < rowptr[i + 1]; ++k)
+        if (col[k] == i) {
+            d = k;
+            break;
+        }
+    diag[i] = d;
+    if (d < 0) atomicOr(bad, 1);
+    if (rowptr[i + 1] - rowptr[i] > kRowCap) atomicOr(bad, 2);
+}
+
+// max_i sum_j |a_ij| (rows summed in CSR order, as ilu0_impl's parallel_reduce)
+__global__ void k_abs_rowsum_max(int n, const int* __restrict__ rowptr, const double* __restrict__ v,
+                                 unsigned long long* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    double s = 0;
+    if (i < n)
+        for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) s += fabs(v[k]);
+    s = wave_max(s);
+    // non-negative doubles order like their bit patterns
+    if ((threadIdx.x & (kWave - 1)) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(s));
+}
+
+// ---------------------------------------------------------------- factorisation
+// ilu0_impl (kernels_mkl.cpp:416-500) row by row, in fp64. The row is staged
+// in LDS; its elimination steps run in column order, and step k updates each
+// later entry of the row with the matching entry of row k's upper part. The
+// sorted merge of the reference pairs equal columns in order, so the e-th
+// entry, the r-th of its column in the row's remaining run, meets the r-th
+// entry of that column in row k (duplicates handled as the merge does).
+// Products and differences are not contracted, as in the reference loop.
+#pragma clang fp contract(off)
+__global__ __launch_bounds__(kBlock) void k_ilu0_factor(int n, const int* __restrict__ rowptr,
+                                                        const int* __restrict__ col, const int* __restrict__ diag,
+                                                        double* lu, double eps,
+                                                        const unsigned long long* __restrict__ rowmax, int* done,
+                                                        unsigned* ticket, int* err) {
+    __shared__ double vs[kWaves][kRowCap];
+    __shared__ int cs[kWaves][kRowCap];
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    double* v = vs[wid];
+    int* c = cs[wid];
+    const double alpha = __longlong_as_double((long long)*rowmax) * eps;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (__builtin_amdgcn_s_memrealtime() - t_start > kDeadline) {
+            if (lane == 0) __hip_atomic_store((gu32*)err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        int row = 0;
+        if (lane == 0) row = (int)__hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        row = __shfl(row, 0, kWave);
+        if (row >= n) break;
+        const int rs = rowptr[row], len = rowptr[row + 1] - rs, dpos = diag[row] - rs;
+        for (int e = lane; e < len; e += kWave) {
+            c[e] = col[rs + e];
+            v[e] = lu[rs + e];  // this row's values: written by nobody else before its flag
+        }
+        wave_lds_sync();
+        if (row > 0) {  // the reference loop starts at row 1 (no elimination, no boost on row 0)
+            for (int e = lane; e < dpos; e += kWave) wait_flag(done + c[e], err);
+            acquire_agent();
+            for (int p = 0; p < dpos; ++p) {
+                const int k = c[p];
+                const int kd = diag[k], ke = rowptr[k + 1];
+                const double factor = v[p] / lu[kd];
+                wave_lds_sync();
+                if (lane == 0) v[p] = factor;
+                for (int e = p + 1 + lane; e < len; e += kWave) {
+                    const int cc = c[e];
+                    int f = e;
+                    while (f > p + 1 && c[f - 1] == cc) --f;
+                    int lo = kd + 1, hi = ke;
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (col[mid] < cc) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    const int t = lo + (e - f);
+                    if (t < ke && col[t] == cc) {
+                        const double prod = factor * lu[t];
+                        v[e] = v[e] - prod;
+                    }
+                }
+                wave_lds_sync();
+            }
+            if (lane == 0) {
+                double d = v[dpos];
+                if (d >= 0) {
+                    if (d < alpha) d = alpha;
+                } else {
+                    if (d > -alpha) d = -alpha;
+                }
+                v[dpos] = d;
+            }
+            wave_lds_sync();
+        }
+        for (int e = lane; e < len; e += kWave) store_wt(lu + rs + e, v[e]);
+        drain_stores();
+        if (lane == 0) set_flag(done + row);
+    }
+}
+#pragma clang fp contract(on)
+
+template <class T>
+__global__ void k_round_factors(int64_t nnz, const double* __restrict__ lu64, T* __restrict__ lu) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nnz; k += (int64_t)gridDim.x * blockDim.x)
+        lu[k] = (T)lu64[k];
+}
+
+// diag(i) = 1/vals(j) on the rounded factors (types.hpp:305-316)
+template <class T>
+__global__ void k_dinv(int n, const int* __restrict__ diag, const T* __restrict__ lu, T* __restrict__ dinv) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dinv[i] = 1 / lu[diag[i]];
+}
+
+// ---------------------------------------------------------------- triangular solves
+// x := L^-1 x (unit lower) or U^-1 x (upper), in place, sync-free: row i
+// waits for the rows its off-diagonal entries read, then
+// x_i = T((x_i - sum_j a_ij x_j) [/ u_ii]) with the sum in fp64 (lane
+// partials in CSR order, then a fixed xor tree).
+template <class T, bool UPPER>
+__global__ __launch_bounds__(kBlock) void k_ilu_trsv(int n, const int* __restrict__ rowptr,
+                                                     const int* __restrict__ col, const int* __restrict__ diag,
+                                                     const T* __restrict__ lu, T* x, int* done, unsigned* ticket,
+                                                     int* err) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (__builtin_amdgcn_s_memrealtime() - t_start > kDeadline) {
+            if (lane == 0) __hip_atomic_store((gu32*)err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        int t = 0;
+        if (lane == 0) t = (int)__hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __shfl(t, 0, kWave);
+        if (t >= n) break;
+        const int row = UPPER ? n - 1 - t : t;
+        const int d = diag[row];
+        const int j0 = UPPER ? d + 1 : rowptr[row];
+        const int j1 = UPPER ? rowptr[row + 1] : d;
+        for (int j = j0 + lane; j < j1; j += kWave) wait_flag(done + col[j], err);
+        acquire_agent();
+        double s = 0.0;
+        for (int j = j0 + lane; j < j1; j += kWave) s += (double)lu[j] * (double)x[col[j]];
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, kWave);
+        if (lane == 0) {
+            double r = (double)x[row] - s;
+            if (UPPER) r = r / (double)lu[d];
+            store_wt(x + row, (T)r);
+        }
+        drain_stores();
+        if (lane == 0) set_flag(done + row);
+    }
+}
+
+// ---------------------------------------------------------------- ILU-Jacobi
+// One Jacobi sweep on L (x_new = x + (b - (x + L_s x))) or on U
+// (x_new = x + d∘(b - U x)), with the reference's operation order
+// (ilu_jacobi_mv + axpy / gdmv, kernels.hpp:171-248); row sums in fp64.
+template <class T, bool UPPER>
+__global__ void k_ilu_jacobi_sweep(int n, const int* __restrict__ rowptr, const int* __restrict__ col,
+                                   const int* __restrict__ diag, const T* __restrict__ lu,
+                                   const T* __restrict__ dinv, const T* __restrict__ b, const T* __restrict__ xo,
+                                   T* __restrict__ xn) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int d = diag[i];
+    if (!UPPER) {
+        double s = (double)xo[i];
+        for (int j = rowptr[i]; j < d; ++j) s += (double)lu[j] * (double)xo[col[j]];
+        const T sum = (T)s;
+        const T t = T(1) * b[i] + T(-1) * sum;  // temp = beta*temp + alpha*sum
+        xn[i] = T(1) * t + xo[i];               // axpy(1.0, temp, x)
+    } else {
+        double s = 0.0;
+        for (int j = d; j < rowptr[i + 1]; ++j) s += (double)lu[j] * (double)xo[col[j]];
+        const T sum = (T)s;
+        const T t = T(1.0) * b[i] + T(-1.0) * sum;
+        xn[i] = T(1) * xo[i] + T(1) * dinv[i] * t;  // gdmv(1.0, diag, temp, 1.0, x)
+    }
+}
+
+}  // namespace
+
+struct mpg_ilu {
+    mpg_ctx* ctx = nullptr;
+    const mpg_csr* A = nullptr;
+    int n = 0;
+    int64_t nnz = 0;
+    int type = 0;                // 0 fp64, 1 fp32
+    double* lu64 = nullptr;      // fp64 factors
+    float* lu32 = nullptr;       // fp32 factors (type 1)
+    int* diag = nullptr;
+    void* dinv = nullptr;
+    int* sync = nullptr;
+    void* w[2] = {nullptr, nullptr};  // ILU-Jacobi: right-hand side and the second sweep buffer
+    unsigned long long* scratch = nullptr;
+
+    size_t tsize() const { return type == 0 ? 8 : 4; }
+    void* values() const { return type == 0 ? (void*)lu64 : (void*)lu32; }
+    unsigned* ticket(int which) { return reinterpret_cast<unsigned*>(sync + 2 * (size_t)n + 32 * which); }
+    int* err() { return sync + 2 * (size_t)n + 128; }
+};
+
+namespace {
+
+template <class F>
+int by_type(int type, F&& f) {
+    if (type == 0) return f(double());
+    if (type == 1) return f(float());
+    return MPG_ERR_UNSUPPORTED;
+}
+
+int reset_sync(mpg_ilu* L) {
+    // flags and tickets (the fault word, past them, stays sticky)
+    MPG_HIP(L->ctx, hipMemsetAsync(L->sync, 0, (2 * (size_t)L->n + 128) * sizeof(int), L->ctx->stream));
+    return MPG_OK;
+}
+
+int persist_grid(int n) { return std::max(1, std::min(kPersistGroups, (n + kWaves - 1) / kWaves)); }
+
+}  // namespace
+
+extern "C" {
+
+int mpg_ilu_row_cap(void) { return kRowCap; }
+
+int mpg_ilu0_create(mpg_ctx_t ctx, mpg_csr_t A, const double* val64, int type, mpg_ilu_t* out) {
+    if (!ctx || !A || !out || (type != 0 && type != 1) || A->rows != A->cols || (A->nnz > 0 && !val64))
+        return MPG_ERR_ARG;
+    *out = nullptr;
+    mpg_ilu* L = new (std::nothrow) mpg_ilu();
+    if (!L) return MPG_ERR_ALLOC;
+    L->ctx = ctx;
+    L->A = A;
+    L->n = A->rows;
+    L->nnz = A->nnz;
+    L->type = type;
+    const int n = L->n;
+    hipStream_t s = ctx->stream;
+    auto fail = [&](int st) {
+        mpg_ilu_destroy(L);
+        return st;
+    };
+    auto ok = [](hipError_t e) { return e == hipSuccess; };
+    const size_t nb = std::max<size_t>(1, (size_t)n), zb = std::max<size_t>(1, (size_t)L->nnz);
+    if (!ok(hipMalloc((void**)&L->lu64, zb * 8)) || !ok(hipMalloc((void**)&L->diag, nb * 4)) ||
+        !ok(hipMalloc(&L->dinv, nb * L->tsize())) || !ok(hipMalloc((void**)&L->sync, sync_ints(n) * 4)) ||
+        !ok(hipMalloc(&L->w[0], nb * L->tsize())) || !ok(hipMalloc(&L->w[1], nb * L->tsize())) ||
+        !ok(hipMalloc((void**)&L->scratch, 64)) || (type == 1 && !ok(hipMalloc((void**)&L->lu32, zb * 4))))
+        return fail(MPG_ERR_ALLOC);
+    if (!ok(hipMemsetAsync(L->sync, 0, sync_ints(n) * 4, s)) || !ok(hipMemsetAsync(L->scratch, 0, 64, s)))
+        return fail(MPG_ERR_HIP);
+    if (n == 0) {
+        *out = L;
+        return MPG_OK;
+    }
+    if (L->nnz && !ok(hipMemcpyAsync(L->lu64, val64, (size_t)L->nnz * 8, hipMemcpyDeviceToDevice, s)))
+        return fail(MPG_ERR_HIP);
+    int* bad = reinterpret_cast<int*>(L->scratch) + 4;
+    const int g = (n + kBlock - 1) / kBlock;
+    k_find_diag<<<g, kBlock, 0, s>>>(n, A->rowptr, A->col, L->diag, bad);
+    k_abs_rowsum_max<<<g, kBlock, 0, s>>>(n, A->rowptr, L->lu64, L->scratch);
+    int bad_h = 0;
+    if (!ok(hipMemcpyAsync(&bad_h, bad, 4, hipMemcpyDeviceToHost, s)) || !ok(hipStreamSynchronize(s)))
+        return fail(MPG_ERR_HIP);
+    if (bad_h) return fail(MPG_ERR_UNSUPPORTED);  // a row without its diagonal, or longer than kRowCap
+    const double eps = type == 0 ? (double)std::numeric_limits<double>::epsilon()
+                                 : (double)std::numeric_limits<float>::epsilon();
+    k_ilu0_factor<<<persist_grid(n), kBlock, 0, s>>>(n, A->rowptr, A->col, L->diag, L->lu64, eps, L->scratch,
+                                                     L->sync, L->ticket(0), L->err());
+    int st = by_type(type, [&](auto t) {
+        using T = decltype(t);
+        T* lu = static_cast<T*>(L->values());
+        if (std::is_same<T, float>::value)
+            k_round_factors<T><<<grid_for(L->nnz, 4), kBlock, 0, s>>>(L->nnz, L->lu64, lu);
+        k_dinv<T><<<g, kBlock, 0, s>>>(n, L->diag, lu, static_cast<T*>(L->dinv));
+        return (int)MPG_OK;
+    });
+    if (st) return fail(st);
+    if (!ok(hipGetLastError())) return fail(MPG_ERR_HIP);
+    if (int f = mpg_ilu_fault(L)) {
+        if (std::getenv("MPG_ILU_DEBUG")) {
+            int32_t st4[4];
+            mpg_ilu_debug_state(L, st4);
+            std::fprintf(stderr, "mpg_ilu0_create: fault %d, tickets %d %d %d, n %d\n", f, st4[0], st4[1], st4[2], n);
+        }
+        return fail(MPG_ERR_BREAKDOWN);
+    }
+    *out = L;
+    return MPG_OK;
+}
+
+int mpg_ilu_destroy(mpg_ilu_t L) {
+    if (!L) return MPG_OK;
+    if (L->ctx) (void)hipStreamSynchronize(L->ctx->stream);
+    void* ps[] = {L->lu64, L->lu32, L->diag, L->dinv, L->sync, L->w[0], L->w[1], L->scratch};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    delete L;
+    return MPG_OK;
+}
+
+int mpg_ilu_solve(mpg_ctx_t ctx, mpg_ilu_t L, void* x) {
+    if (!ctx || !L || (!x && L->n)) return MPG_ERR_ARG;
+    if (L->n == 0) return MPG_OK;
+    if (int st = reset_sync(L)) return st;
+    const int n = L->n, g = persist_grid(n);
+    int st = by_type(L->type, [&](auto t) {
+        using T = decltype(t);
+        const T* lu = static_cast<const T*>(L->values());
+        T* xv = static_cast<T*>(x);
+        k_ilu_trsv<T, false><<<g, kBlock, 0, ctx->stream>>>(n, L->A->rowptr, L->A->col, L->diag, lu, xv, L->sync,
+                                                             L->ticket(1), L->err());
+        k_ilu_trsv<T, true><<<g, kBlock, 0, ctx->stream>>>(n, L->A->rowptr, L->A->col, L->diag, lu, xv,
+                                                            L->sync + n, L->ticket(2), L->err());
+        return (int)MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+int mpg_ilu_jacobi_solve(mpg_ctx_t ctx, mpg_ilu_t L, int steps, void* x) {
+    if (!ctx || !L || steps < 0 || (!x && L->n)) return MPG_ERR_ARG;
+    const int n = L->n;
+    if (n == 0) return MPG_OK;
+    const int g = (n + kBlock - 1) / kBlock;
+    const size_t bytes = (size_t)n * L->tsize();
+    hipStream_t s = ctx->stream;
+    int st = by_type(L->type, [&](auto t) {
+        using T = decltype(t);
+        const T* lu = static_cast<const T*>(L->values());
+        const T* dinv = static_cast<const T*>(L->dinv);
+        T* b = static_cast<T*>(L->w[0]);
+        T* cur = static_cast<T*>(x);
+        T* nxt = static_cast<T*>(L->w[1]);
+        if (hipMemcpyAsync(b, cur, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess) return (int)MPG_ERR_HIP;
+        for (int i = 0; i < steps; ++i) {
+            k_ilu_jacobi_sweep<T, false><<<g, kBlock, 0, s>>>(n, L->A->rowptr, L->A->col, L->diag, lu, dinv, b, cur,
+                                                               nxt);
+            std::swap(cur, nxt);
+        }
+        if (hipMemcpyAsync(b, cur, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess) return (int)MPG_ERR_HIP;
+        for (int i = 0; i < steps; ++i) {
+            k_ilu_jacobi_sweep<T, true><<<g, kBlock, 0, s>>>(n, L->A->rowptr, L->A->col, L->diag, lu, dinv, b, cur,
+                                                              nxt);
+            std::swap(cur, nxt);
+        }
+        if (cur != static_cast<T*>(x) && hipMemcpyAsync(x, cur, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return (int)MPG_ERR_HIP;
+        return (int)MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+const void* mpg_ilu_values_dev(mpg_ilu_t L) { return L ? L->values() : nullptr; }
+const int32_t* mpg_ilu_diag_dev(mpg_ilu_t L) { return L ? L->diag : nullptr; }
+const void* mpg_ilu_dinv_dev(mpg_ilu_t L) { return L ? L->dinv : nullptr; }
+
+int mpg_ilu_debug_state(mpg_ilu_t L, int32_t* out4) {
+    if (!L || !out4 || !L->sync) return MPG_ERR_ARG;
+    int v[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 3; ++k)
+        if (hipMemcpyAsync(v + k, L->ticket(k), 4, hipMemcpyDeviceToHost, L->ctx->stream) != hipSuccess) return MPG_ERR_HIP;
+    if (hipMemcpyAsync(v + 3, L->err(), 4, hipMemcpyDeviceToHost, L->ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(L->ctx->stream) != hipSuccess)
+        return MPG_ERR_HIP;
+    for (int k = 0; k < 4; ++k) out4[k] = v[k];
+    return MPG_OK;
+}
+
+int mpg_ilu_fault(mpg_ilu_t L) {
+    if (!L || !L->sync) return 0;
+    int e = 0;
+    if (hipMemcpyAsync(&e, L->err(), 4, hipMemcpyDeviceToHost, L->ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(L->ctx->stream) != hipSuccess)
+        return -1;
+    return e;
+}
+
+}  // extern "C"

@@ -77,8 +77,10 @@ struct FusedEngine::Impl {
     bool fold = false;     // Givens step folded into the next SpMV launch
     bool combine = false;  // last-arriver combines in the dots and CGS launches
     std::vector<int32_t> rowptr_host;
+    mpg_ilu_t ilu = nullptr;  // ILU(0) factors (prec ilu / ilu_jacobi), applied between phase kernels
 
     ~Impl() {
+        if (ilu) mpg_ilu_destroy(ilu);
         if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
         if (graph) (void)hipGraphDestroy(graph);
         if (arn) mpg_arnoldi_destroy(arn);
@@ -107,6 +109,21 @@ struct FusedEngine::Impl {
         check(mpg_memcpy_d2h(ctx, &h, acc, sizeof h), "d2h", ctx);
         return h;
     }
+    // M^-1 w for the ILU preconditioners, with typesafe_apply's casts when
+    // the preconditioner precision differs (gmres.cpp:12-22)
+    void apply_ilu(void* w) {
+        void* wp = w;
+        if (ty.P != ty.T) {
+            cast(w, ty.T, tmp_p.p, ty.P, n);
+            wp = tmp_p.p;
+        }
+        solve_ilu(wp);
+        if (ty.P != ty.T) cast(tmp_p.p, ty.P, w, ty.T, n);
+    }
+    void solve_ilu(void* wp) {
+        if (args.prec == MPG_PREC_ILU) check(mpg_ilu_solve(ctx, ilu, wp), "ilusv", ctx);
+        else check(mpg_ilu_jacobi_solve(ctx, ilu, args.jacobi_steps, wp), "ilusv_jacobi", ctx);
+    }
     // nrm2 rounded to the vector's precision
     double nrm2(const void* u, int t, int64_t count) {
         const double s = std::sqrt(dot_acc(u, u, t, count));
@@ -126,8 +143,10 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     I.m = a.rlen;
     I.orth = a.orth;
     I.nnz = a.nnz;
-    if (a.prec != MPG_PREC_IDENTITY && a.prec != MPG_PREC_JACOBI)
-        throw std::invalid_argument("ILU / ILU-Jacobi preconditioners are not implemented on the Hip backend yet");
+    const bool ilu = a.prec == MPG_PREC_ILU || a.prec == MPG_PREC_ILU_JACOBI;
+    if (ilu && comm)
+        throw std::invalid_argument("ILU / ILU-Jacobi factor the whole matrix: not available on a row-partitioned solve");
+    if (!ilu && a.prec != MPG_PREC_IDENTITY && a.prec != MPG_PREC_JACOBI) throw std::invalid_argument("Unknown prec type");
     if (a.orthloss && a.rtol != 0)
         throw std::invalid_argument("the LostOrthogonality restart needs v_{k+1} on the host: use engine=surface");
     if (a.rowptr[a.n] != a.nnz) throw std::invalid_argument("rowptr[n] != nnz");
@@ -187,6 +206,9 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
         }
     }
 
+    // ILU(0) of the fp64 A in the preconditioner precision (gmres_perf_test.cpp:70-79, 140-149)
+    if (ilu) check(mpg_ilu0_create(ctx, I.csr, I.val64.as<double>(), ty.P == MPG_F64 ? 0 : 1, &I.ilu), "ilu0", ctx);
+
     // b (outer type), x = 0 (outer type, with halo tail)
     DevMem b64(ctx, (size_t)I.n * 8 + 8);
     check(mpg_memcpy_h2d(ctx, b64.p, a.b, (size_t)I.n * 8), "h2d", ctx);
@@ -214,6 +236,7 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
             else
                 check(mpg_gdmv_f32(ctx, I.n, 1.0f, I.diag.as<float>(), (float*)wp, 0.0f, (float*)wp), "gdmv", ctx);
         }
+        if (I.ilu) I.solve_ilu(wp);
         if (ty.P != ty.T) I.cast(I.tmp_p.p, ty.P, I.tmp_t.p, ty.T, I.n);
         minvb_norm = I.nrm2(I.tmp_t.p, ty.T, I.n);
     }
@@ -285,6 +308,10 @@ void FusedEngine::prologue() {
     Impl& I = *p_;
     if (I.comm) I.comm->halo(I.x.p, (int)dsize(I.ty.X), I.stream());
     check(mpg_arnoldi_prologue(I.arn), "prologue", I.ctx);
+    if (I.ilu) {  // w = M(T(r)) outside the kernel, then ||w||^2 again
+        I.apply_ilu(mpg_arnoldi_wprev_dev(I.arn, 0));
+        check(mpg_arnoldi_prologue_wnorm(I.arn), "prologue wnorm", I.ctx);
+    }
     check(mpg_arnoldi_reduce(I.arn, 3), "reduce", I.ctx);
     if (I.comm) I.comm->allreduce_sum(mpg_arnoldi_sums_dev(I.arn), 3, I.stream());
     check(mpg_arnoldi_prologue_finish(I.arn), "prologue_finish", I.ctx);
@@ -321,6 +348,7 @@ void FusedEngine::step(int k, bool fold) {
         if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
         check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
     }
+    if (I.ilu) I.apply_ilu(mpg_arnoldi_wprev_dev(I.arn, k + 1));  // w = M(A v_k)
     if (I.orth == MPG_ORTH_MGS) {
         check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
         reduce(1);

@@ -126,6 +126,16 @@ void spmv(ScalarType alpha, SparseMatrix<Type, Device> matrix, Vect<Type, Device
 template <class Type, class Device>
 void jacobi_diag(SparseMatrix<Type, Device> A, Vect<Type, Device> diag);
 
+// ILU(0) of the fp64 matrix in precision Type (kernels.hpp:155-156), its
+// triangular solves (kernels.hpp:168-169) and the Jacobi-sweep
+// approximation of them (ilusv_jacobi, kernels.hpp:219-248).
+template <class Type, class Device>
+ILU<Type, Device> ilu0(SparseMatrix<double, Device> matrix);
+template <class Type, class Device>
+void ilusv(ILU<Type, Device> ilu, Vect<Type, Device> rhs);
+template <class Type, class Device>
+void ilusv_jacobi(ILU_Jacobi<Type, Device> ilu, Vect<Type, Device> x);
+
 // Jacobi preconditioner M = D^-1 (types.hpp:381-448).
 template <class Type, class Device>
 class Jacobi : public LinearOperator<Type, Device> {

@@ -294,4 +294,28 @@ template <> void jacobi_diag<float, Hip>(SparseMatrix<float, Hip> A, Vect<float,
     check(mpg_jacobi_setup_f32(C, A.csr(), A.vals_data(), d.data()), "jacobi setup");
 }
 
+// ---- ILU(0) / ILU-Jacobi (kernels_mkl.cpp:355-506, kernels_cuda.cpp:617-791) ----
+namespace {
+template <class T>
+ILU<T, Hip> make_ilu(SparseMatrix<double, Hip> A, int type) {
+    mpg_ilu_t h = nullptr;
+    check(mpg_ilu0_create(C, A.csr(), A.vals_data(), type, &h), "ilu0");
+    return ILU<T, Hip>(std::shared_ptr<mpg_ilu>(h, [](mpg_ilu* p) { mpg_ilu_destroy(p); }), A.nrows(), A.nnz());
+}
+}  // namespace
+template <> ILU<double, Hip> ilu0<double, Hip>(SparseMatrix<double, Hip> A) { return make_ilu<double>(A, 0); }
+template <> ILU<float, Hip> ilu0<float, Hip>(SparseMatrix<double, Hip> A) { return make_ilu<float>(A, 1); }
+template <> void ilusv<double, Hip>(ILU<double, Hip> ilu, Vect<double, Hip> x) {
+    check(mpg_ilu_solve(C, ilu.handle(), x.data()), "ilusv");
+}
+template <> void ilusv<float, Hip>(ILU<float, Hip> ilu, Vect<float, Hip> x) {
+    check(mpg_ilu_solve(C, ilu.handle(), x.data()), "ilusv");
+}
+template <> void ilusv_jacobi<double, Hip>(ILU_Jacobi<double, Hip> ilu, Vect<double, Hip> x) {
+    check(mpg_ilu_jacobi_solve(C, ilu.handle(), ilu.steps(), x.data()), "ilusv_jacobi");
+}
+template <> void ilusv_jacobi<float, Hip>(ILU_Jacobi<float, Hip> ilu, Vect<float, Hip> x) {
+    check(mpg_ilu_jacobi_solve(C, ilu.handle(), ilu.steps(), x.data()), "ilusv_jacobi");
+}
+
 #undef C

@@ -41,14 +41,16 @@ std::unique_ptr<Convergence<T, Hip>> make_convergence(const mpg_solve_args& a) {
     return std::make_unique<RelPrecRes_Convergence<T, Hip>>(a.tol, a.rtol, m, (size_t)a.max_restarts);
 }
 
+// gmres_perf_test.cpp:69-89, 139-159 (ILU from the fp64 A; Jacobi from A
+// converted to the preconditioner precision)
 template <class P>
-std::unique_ptr<LinearOperator<P, Hip>> make_preconditioner(int prec, const SparseMatrix<double, Hip>& A) {
+std::unique_ptr<LinearOperator<P, Hip>> make_preconditioner(int prec, const SparseMatrix<double, Hip>& A,
+                                                            int jacobi_steps) {
     switch (prec) {
         case MPG_PREC_IDENTITY: return std::make_unique<Identity<P, Hip>>();
         case MPG_PREC_JACOBI: return std::make_unique<Jacobi<P, Hip>>(A);
-        case MPG_PREC_ILU:
-        case MPG_PREC_ILU_JACOBI:
-            throw std::invalid_argument("ILU / ILU-Jacobi preconditioners are not implemented on the Hip backend yet");
+        case MPG_PREC_ILU: return std::make_unique<ILU<P, Hip>>(ilu0<P, Hip>(A));
+        case MPG_PREC_ILU_JACOBI: return std::make_unique<ILU_Jacobi<P, Hip>>(ilu0<P, Hip>(A), jacobi_steps);
         default: throw std::invalid_argument("Unknown prec type");
     }
 }
@@ -107,7 +109,7 @@ void do_baseline(const mpg_solve_args& a, const SparseMatrix<double, Hip>& A, Ve
     // fp32-rounded copy, widened back for Type = double.
     const SparseMatrix<float, Hip> A_f32(A);
     const SparseMatrix<Type, Hip> A_type(A_f32);
-    auto M = make_preconditioner<PrecType>(a.prec, A);
+    auto M = make_preconditioner<PrecType>(a.prec, A, a.jacobi_steps);
     Hip::fence();
     const double prec_s = seconds_since(t0);
 
@@ -139,7 +141,7 @@ void do_mixed(const mpg_solve_args& a, const SparseMatrix<double, Hip>& A, Vect<
     Vect<double, Hip> x(n);
     auto t0 = clk::now();
     const SparseMatrix<float, Hip> A_single(A);
-    auto M = make_preconditioner<float>(a.prec, A);
+    auto M = make_preconditioner<float>(a.prec, A, a.jacobi_steps);
     Hip::fence();
     const double prec_s = seconds_since(t0);
 

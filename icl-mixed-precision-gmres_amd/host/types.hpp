@@ -215,6 +215,13 @@ public:
 template <class Type, class Device>
 class SparseMatrix {};
 
+// Device-specialised ILU(0) factors and their Jacobi-sweep variant
+// (types.hpp:243-372; types_mkl.hpp:110-240; types_cuda.hpp:155-260).
+template <class Type, class Device>
+class ILU {};
+template <class Type, class Device>
+class ILU_Jacobi {};
+
 // M = I (types.hpp:374-378).
 template <class Type, class Device>
 class Identity : public LinearOperator<Type, Device> {

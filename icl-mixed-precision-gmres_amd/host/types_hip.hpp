@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "mpgmres/capi.h"
+#include "mpgmres/ilu.h"
 #include "kernels.hpp"
 #include "types.hpp"
 
@@ -108,6 +109,40 @@ public:
     mpg_csr_t csr() const { return s_->csr.get(); }
     Vect<Type, Hip> vals_vect() const { return vals_; }
     bool is_transposed() const { return false; }
+};
+
+// ILU(0) factors on the device (types_mkl.hpp:110-190, types_cuda.hpp:155-240):
+// a handle to the factor values in the matrix's CSR pattern, the pivot
+// positions and the sync-free solve state (include/mpgmres/ilu.h).
+template <class Type>
+class ILU<Type, Hip> : public LinearOperator<Type, Hip> {
+    std::shared_ptr<mpg_ilu> h_;
+    int n_ = 0;
+    int64_t nnz_ = 0;
+
+public:
+    ILU() = default;
+    ILU(std::shared_ptr<mpg_ilu> h, int n, int64_t nnz) : h_(std::move(h)), n_(n), nnz_(nnz) {}
+    int n() const { return n_; }
+    int64_t nnz() const { return nnz_; }
+    mpg_ilu_t handle() const { return h_.get(); }
+    const Type* vals_data() const { return static_cast<const Type*>(mpg_ilu_values_dev(h_.get())); }
+    void apply(Vect<Type, Hip> rhs) override { ilusv(*this, rhs); }
+};
+
+// ILU-Jacobi (types.hpp:251-372): the same factors, `steps` Jacobi sweeps
+// per triangular factor instead of the exact solves.
+template <class Type>
+class ILU_Jacobi<Type, Hip> : public LinearOperator<Type, Hip> {
+    ILU<Type, Hip> ilu_;
+    int steps_ = 1;
+
+public:
+    ILU_Jacobi(ILU<Type, Hip> ilu, int steps) : ilu_(std::move(ilu)), steps_(steps) {}
+    int n() const { return ilu_.n(); }
+    int steps() const { return steps_; }
+    mpg_ilu_t handle() const { return ilu_.handle(); }
+    void apply(Vect<Type, Hip> rhs) override { ilusv_jacobi(*this, rhs); }
 };
 
 #endif  // MPGMRES_TYPES_HIP_HPP

@@ -79,6 +79,9 @@ int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width
 
 int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
 int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);
+/* recompute the ||w||^2 partials of the prologue (column 1) after the
+ * caller preconditioned w (mpg_arnoldi_wprev_dev(a, 0)) itself — ILU */
+int mpg_arnoldi_prologue_wnorm(mpg_arnoldi_t a);
 int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k);           /* w = M(A v_k), V(:,k) */
 int mpg_arnoldi_dots(mpg_arnoldi_t a, int k);           /* partials: k+1 (CGS/CGSR) or 1 (MGS) */
 int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass);  /* pass 0: h; pass 1: CGSR correction */

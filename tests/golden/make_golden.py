@@ -74,6 +74,13 @@ for mat in ("lap10", "band2000", "convdiff32"):
                 for m in (10, 30):
                     tol = 1e-5 if mode == "single" else 1e-10
                     CASES.append(dict(matrix=mat, mode=mode, orth=orth, prec=prec, rlen=m, tol=tol, max_restarts=200))
+# ILU(0) / ILU-Jacobi (3 sweeps per factor): SURVEY §8f #2
+for mat in ("lap10", "band2000", "convdiff32"):
+    for mode in ("mixed", "baseline", "single-prec", "single"):
+        for prec in ("ilu", "ilu_jacobi"):
+            tol = 1e-5 if mode == "single" else 1e-10
+            CASES.append(dict(matrix=mat, mode=mode, orth="cgs", prec=prec, rlen=30, tol=tol, max_restarts=200,
+                              jacobi_steps=3))
 
 
 def main():

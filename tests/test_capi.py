@@ -11,7 +11,7 @@ def test_every_declared_symbol_is_exported(mpg):
     assert len(declared) > 60
     missing = []
     for header, name in declared:
-        lib = hip if header == "capi.h" else host
+        lib = hip if header in ("capi.h", "arnoldi.h", "ilu.h") else host
         try:
             getattr(lib, name)
         except AttributeError:
