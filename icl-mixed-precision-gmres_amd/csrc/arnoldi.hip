@@ -490,14 +490,34 @@ template <class T, bool NEXT_DOTS, bool GIVENS = false>
 __global__ __launch_bounds__(kBlock) void k_cgs_update(int n, const T* __restrict__ V, int64_t ld, int k,
                                                        const double* __restrict__ sums, T* __restrict__ coef_out,
                                                        T* __restrict__ w, double* __restrict__ partial,
-                                                       unsigned* __restrict__ cnt, GivensArgs<T> g) {
+                                                       unsigned* __restrict__ cnt, GivensArgs<T> g, int part_G) {
     static_assert(!(NEXT_DOTS && GIVENS), "the Givens step follows the last pass");
     __shared__ double coef[256];
     const int nc = k + 1;
-    for (int j = threadIdx.x; j < nc; j += kBlock) {
-        const T c = (T)sums[j];
-        coef[j] = (double)c;
-        if (blockIdx.x == 0) coef_out[j] = c;
+    if (part_G > 0) {
+        // sums straight from the panel-dots partials (nc <= kNC, part_G per
+        // column): 8 lanes per column, each a strided run in g order, then an
+        // xor tree — the same fixed order in every workgroup
+        const int j = threadIdx.x >> 3, sub = threadIdx.x & 7;
+        double v = 0.0;
+        if (j < nc) {
+#pragma unroll 8
+            for (int gi = sub; gi < part_G; gi += 8) v += sums[(size_t)j * part_G + gi];
+        }
+        v += __shfl_xor(v, 4, kWave);
+        v += __shfl_xor(v, 2, kWave);
+        v += __shfl_xor(v, 1, kWave);
+        if (j < nc && sub == 0) {
+            const T c = (T)v;
+            coef[j] = (double)c;
+            if (blockIdx.x == 0) coef_out[j] = c;
+        }
+    } else {
+        for (int j = threadIdx.x; j < nc; j += kBlock) {
+            const T c = (T)sums[j];
+            coef[j] = (double)c;
+            if (blockIdx.x == 0) coef_out[j] = c;
+        }
     }
     __syncthreads();
     constexpr int NA = NEXT_DOTS ? kNC : 1;
@@ -643,6 +663,7 @@ struct mpg_arnoldi {
     int G = 1;        // workgroups of the row-parallel panel kernels
     int Grb = 1;      // workgroups of the row-block (SpMV) kernels: one per row block
     int last_G = 1;   // partial count per column written by the last producer
+    double* last_part = nullptr;  // ... and the buffer it wrote (partial or dpart)
     int64_t ld = 0;   // leading dimension of V (elements)
     size_t tsize = 8;
     void* V = nullptr;
@@ -650,6 +671,7 @@ struct mpg_arnoldi {
     void* small = nullptr;  // cs, sn, s (m+1 each), inv, corr (m+1), coef scratch
     void* w[2] = {nullptr, nullptr};
     double* partial = nullptr;  // (kNC + 4) x G
+    double* dpart = nullptr;    // kNC x Gd: one-panel dots partials (read by the CGS update that writes `partial`)
     double* sums = nullptr;     // m + 4
     double* report = nullptr;   // 4 + m
     unsigned* counters = nullptr;  // last-arriver tickets: [0] dots, [32] CGS + Givens (zeroed at create)
@@ -832,11 +854,13 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
                                              sizeof(double)) &&
               alloc((void**)&a->sums, (size_t)(m + 8) * sizeof(double)) &&
               alloc((void**)&a->report, (size_t)(m + 8) * sizeof(double)) &&
+              alloc((void**)&a->dpart, (size_t)kNC * kCombineGroups * sizeof(double)) &&
               alloc((void**)&a->counters, 256);
     if (!ok) {
         mpg_arnoldi_destroy(a);
         return MPG_ERR_ALLOC;
     }
+    a->last_part = a->partial;
     if (desc->spmv_format < 0 || desc->spmv_format > 2) {
         mpg_arnoldi_destroy(a);
         return MPG_ERR_ARG;
@@ -863,7 +887,7 @@ int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width
 int mpg_arnoldi_destroy(mpg_arnoldi_t a) {
     if (!a) return MPG_OK;
     if (a->ctx) (void)hipStreamSynchronize(a->ctx->stream);
-    void* ps[] = {a->V, a->H, a->small, a->w[0], a->w[1], a->partial, a->sums, a->report,
+    void* ps[] = {a->V, a->H, a->small, a->w[0], a->w[1], a->partial, a->dpart, a->sums, a->report,
                   a->counters, a->sell.off, a->sell.col, a->sell.val};
     for (void* p : ps)
         if (p) (void)hipFree(p);
@@ -885,6 +909,7 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
         return MPG_OK;
     });
     a->last_G = rb_grid(a);
+    a->last_part = a->partial;
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
@@ -919,7 +944,7 @@ int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a) {
 
 int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols) {
     if (!a || ncols < 1 || ncols > a->d.m + 4) return MPG_ERR_ARG;
-    k_reduce_partials<<<ncols, 1024, 0, a->ctx->stream>>>(a->last_G, a->partial, a->sums);
+    k_reduce_partials<<<ncols, 1024, 0, a->ctx->stream>>>(a->last_G, a->last_part, a->sums);
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
 }
@@ -935,7 +960,8 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold) {
         using VI = decltype(vi);
         const P* diag = a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr;
         GivensFold<T> gf{nullptr, 0, {}};
-        if (fold) gf = GivensFold<T>{fold == 2 ? a->partial : a->sums, fold == 2 ? a->last_G : 0, givens_args<T>(a, k - 1)};
+        if (fold)
+            gf = GivensFold<T>{fold == 2 ? a->last_part : a->sums, fold == 2 ? a->last_G : 0, givens_args<T>(a, k - 1)};
         if (a->sell.nslices > 0) {
             const auto& S = a->sell;
             return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
@@ -977,6 +1003,12 @@ static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
                 a->partial, a->counters, a->sums);
             return (int)MPG_OK;
         }
+        if (ndots_all <= kNC) {  // one panel: 1024-thread workgroups, one per CU -> Gd partials per column
+            k_panel_dots<T, kCombineBlock, false><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, 0, ndots_all, static_cast<const T*>(a->w[(k + 1) & 1]),
+                a->dpart, nullptr, nullptr);
+            return (int)MPG_OK;
+        }
         for (int c0 = 0; c0 < ndots_all; c0 += kNC) {
             const int nc = ndots_all - c0 < kNC ? ndots_all - c0 : kNC;
             k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
@@ -985,7 +1017,8 @@ static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
         }
         return (int)MPG_OK;
     });
-    a->last_G = combine ? a->Gd : row_grid(a);
+    a->last_G = combine || ndots_all <= kNC ? a->Gd : row_grid(a);
+    a->last_part = !combine && ndots_all <= kNC ? a->dpart : a->partial;
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
@@ -994,11 +1027,16 @@ static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
 int mpg_arnoldi_dots(mpg_arnoldi_t a, int k) { return dots_impl(a, k, false); }
 int mpg_arnoldi_dots_sums(mpg_arnoldi_t a, int k) { return dots_impl(a, k, true); }
 
-static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens) {
+static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_partials = false) {
     if (!a || k < 0 || k >= a->d.m || pass < 0 || pass > 1 || k + 1 > 256) return MPG_ERR_ARG;
     const bool cgsr = a->d.orth == kOrthCGSR;
     const bool next_dots = cgsr && pass == 0;
     if (givens && (next_dots || a->d.m > kFoldMaxM)) return MPG_ERR_ARG;
+    // from_partials: the coefficients are summed from the preceding one-panel
+    // dots' partials inside this launch (no reduce launch)
+    if (from_partials && (pass != 0 || k + 1 > kNC || a->last_part != a->dpart)) return MPG_ERR_ARG;
+    const double* src = from_partials ? a->dpart : a->sums;
+    const int part_G = from_partials ? a->Gd : 0;
     int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
         using T = decltype(t);
         T* coef_out = pass == 0 ? static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) : static_cast<T*>(a->corr());
@@ -1006,7 +1044,7 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens) {
         const GivensArgs<T> g = givens_args<T>(a, k);
         if (next_dots) {
             k_cgs_update<T, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, a->sums, coef_out, w, a->partial, nullptr, g);
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, part_G);
             for (int c0 = kNC; c0 < k + 1; c0 += kNC) {
                 const int nc = k + 1 - c0 < kNC ? k + 1 - c0 : kNC;
                 k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
@@ -1014,21 +1052,23 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens) {
             }
         } else if (givens) {
             k_cgs_update<T, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, a->sums, coef_out, w, a->partial, a->counters + 32,
-                g);
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, a->counters + 32, g,
+                part_G);
         } else {
             k_cgs_update<T, false><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, a->sums, coef_out, w, a->partial, nullptr, g);
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, part_G);
         }
         return (int)MPG_OK;
     });
     a->last_G = row_grid(a);
+    a->last_part = a->partial;
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
 }
 
 int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, false); }
+int mpg_arnoldi_cgs_partials(mpg_arnoldi_t a, int k) { return cgs_impl(a, k, 0, false, true); }
 int mpg_arnoldi_cgs_givens(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, true); }
 
 int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j) {
@@ -1042,6 +1082,7 @@ int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j) {
         return MPG_OK;
     });
     a->last_G = row_grid(a);
+    a->last_part = a->partial;
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
@@ -1051,7 +1092,7 @@ static int givens_impl(mpg_arnoldi_t a, int k, bool from_partials) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
     int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
         using T = decltype(t);
-        k_givens<T><<<1, kBlock, 0, a->ctx->stream>>>(givens_args<T>(a, k), from_partials ? a->partial : a->sums,
+        k_givens<T><<<1, kBlock, 0, a->ctx->stream>>>(givens_args<T>(a, k), from_partials ? a->last_part : a->sums,
                                                       from_partials ? a->last_G : 0);
         return MPG_OK;
     });

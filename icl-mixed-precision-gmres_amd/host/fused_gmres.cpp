@@ -76,6 +76,7 @@ struct FusedEngine::Impl {
     bool use_graph = true;
     bool fold = false;     // Givens step folded into the next SpMV launch
     bool combine = false;  // last-arriver combines in the dots and CGS launches
+    bool cgs_partials = false;  // CGS update sums the dots partials in-launch
     std::vector<int32_t> rowptr_host;
     mpg_ilu_t ilu = nullptr;  // ILU(0) factors (prec ilu / ilu_jacobi), applied between phase kernels
 
@@ -289,9 +290,14 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     // MPG_FOLD_GIVENS=1 folds Givens(k-1) into SpMV(k) — every SpMV workgroup
     // sums the ||w||^2 partials itself: 18.0-18.3k vs 18.0k it/s, within noise;
     // MPG_COMBINE=1 (one GPU, CGS/CGSR) does last-arriver combines in the dots
-    // and CGS launches: 15.1k it/s (1024 tickets on one counter serialise).
+    // and CGS launches: 15.1k it/s (1024 tickets on one counter serialise);
+    // MPG_CGS_PARTIALS=1: every CGS workgroup sums the 256 dots partials per
+    // column itself instead of the reduce launch: 17.5k it/s (+4 us per CGS
+    // launch against the 4.9 us reduce it removes).
     const char* cenv = std::getenv("MPG_COMBINE");
     I.combine = !comm && cenv && *cenv == '1' && I.orth != MPG_ORTH_MGS && I.m <= mpg_arnoldi_fold_max_m();
+    const char* penv = std::getenv("MPG_CGS_PARTIALS");
+    I.cgs_partials = !comm && !I.combine && penv && *penv == '1' && I.orth != MPG_ORTH_MGS;
     const char* fenv = std::getenv("MPG_FOLD_GIVENS");
     I.fold = !I.combine && fenv && *fenv == '1' && I.m <= mpg_arnoldi_fold_max_m();
     check(mpg_ctx_sync(ctx), "sync", ctx);
@@ -357,18 +363,29 @@ void FusedEngine::step(int k, bool fold) {
             if (j < k) reduce(1);
         }
     } else {
-        // one GPU: the dots' last workgroup writes the sums, the last CGS
-        // pass's last workgroup runs the Givens step (no reduce / Givens launch)
-        if (I.combine && k + 1 <= 32) {
+        // MPG_CGS_PARTIALS=1 (one GPU, k+1 <= 32): the CGS update sums the dots
+        // partials itself; MPG_COMBINE=1: the dots' last workgroup writes the
+        // sums and the last CGS pass's last workgroup runs the Givens step
+        const bool small = k + 1 <= 32;
+        const int last_pass = I.orth == MPG_ORTH_CGSR ? 1 : 0;
+        bool pass0_done = false;
+        if (I.combine && small) {
             check(mpg_arnoldi_dots_sums(I.arn, k), "dots+sums", I.ctx);
         } else {
             check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
-            reduce(k + 1);
+            if (I.cgs_partials && small) {
+                check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx);
+                pass0_done = true;
+            } else {
+                reduce(k + 1);
+            }
         }
-        const int last_pass = I.orth == MPG_ORTH_CGSR ? 1 : 0;
         if (last_pass == 1) {
-            check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
+            if (!pass0_done) check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
             reduce(k + 1);
+        } else if (pass0_done) {
+            if (!fold) givens(k);
+            return;
         }
         if (I.combine) {
             check(mpg_arnoldi_cgs_givens(I.arn, k, last_pass), "cgs+givens", I.ctx);

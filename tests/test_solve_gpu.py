@@ -28,16 +28,16 @@ def _case_id(c):
 # fused engine on both Arnoldi SpMV storages (CSR row blocks, SELL-64), and
 # with the two launch-count variants: the Givens step folded into the next
 # SpMV launch, and the one-GPU last-arriver combines
-# (engine, storage, MPG_COMBINE, MPG_FOLD_GIVENS)
-ENGINES = {"surface": ("surface", "auto", "0", "0"), "fused-csr": ("fused", "csr", "0", "0"),
-           "fused-sell": ("fused", "sell", "0", "0"), "fused-fold": ("fused", "auto", "0", "1"),
-           "fused-combine": ("fused", "auto", "1", "0")}
+# (engine, storage, experiment flag set to 1: MPG_COMBINE / MPG_FOLD_GIVENS / MPG_CGS_PARTIALS)
+ENGINES = {"surface": ("surface", "auto", None), "fused-csr": ("fused", "csr", None),
+           "fused-sell": ("fused", "sell", None), "fused-fold": ("fused", "auto", "MPG_FOLD_GIVENS"),
+           "fused-combine": ("fused", "auto", "MPG_COMBINE"), "fused-cgspart": ("fused", "auto", "MPG_CGS_PARTIALS")}
 
 
 def _engine(monkeypatch, engine):
-    eng, fmt, combine, fold = ENGINES[engine]
-    monkeypatch.setenv("MPG_COMBINE", combine)
-    monkeypatch.setenv("MPG_FOLD_GIVENS", fold)
+    eng, fmt, flag = ENGINES[engine]
+    for f in ("MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS"):
+        monkeypatch.setenv(f, "1" if f == flag else "0")
     return dict(engine=eng, spmv_format=fmt)
 
 
