@@ -91,7 +91,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_phase_bytes.restype = C.c_double
     lib.mpg_engine_destroy.argtypes = [C.c_void_p]
     lib.mpg_engine_spmv_layout.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
-                                           C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
+                                           C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
     P64 = C.POINTER(C.c_int64)
     P32 = C.POINTER(C.c_int32)
     lib.mpg_halo_analyze.argtypes = [_I32, _I32, P64, _I32, P32, P32, C.POINTER(C.c_void_p)]
@@ -482,11 +482,11 @@ class Engine:
     def spmv_layout(self) -> dict:
         """Storage of the Arnoldi SpMV: {"format": "csr"|"sell", "vec_width",
         "col_bytes", "stored"} (mpg_engine_spmv_layout)."""
-        f, w, cb, st = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
-        if self._lib.mpg_engine_spmv_layout(self._h, C.byref(f), C.byref(w), C.byref(cb), C.byref(st)):
+        f, w, cb, st, win = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64(), C.c_int32()
+        if self._lib.mpg_engine_spmv_layout(self._h, C.byref(f), C.byref(w), C.byref(cb), C.byref(st), C.byref(win)):
             raise RuntimeError("mpg_engine_spmv_layout failed")
         return {"format": {1: "csr", 2: "sell"}[f.value], "vec_width": w.value, "col_bytes": cb.value,
-                "stored": st.value}
+                "stored": st.value, "window": bool(win.value)}
 
     def close(self) -> None:
         if self._h:

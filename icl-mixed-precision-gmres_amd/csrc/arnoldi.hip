@@ -21,6 +21,7 @@
 #include "internal.hpp"
 #include "mpgmres/arnoldi.h"
 
+#include <cstdlib>
 #include <new>
 #include <algorithm>
 #include <vector>
@@ -344,22 +345,43 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
 
 // ---------------------------------------------------------------- step: SpMV (SELL-64)
 // Same contract as k_step_spmv on the sliced-ELL copy (sell_tile.hpp): one
-// wave per slice, one lane per row, no LDS; v_k and w are written coalesced.
-template <class T, class P, class VI, class CI, int W>
-__global__ __launch_bounds__(kBlock) void k_step_sell(int n, int nslices, const int64_t* __restrict__ off,
+// wave per slice, one lane per row; v_k and w are written coalesced.
+// WIN (every column of a slice within [row0 - kWinLo, row0 + 64 + kWinHi),
+// checked when the copy is built): the slice's window of v_k is formed once
+// in LDS with three coalesced loads per lane and the gathers read LDS —
+// 10 scattered global loads per row become LDS reads (-20 % on BAND-10M,
+// tools/sell_bench.hip). Values are the same T(w_prev * inv) either way.
+constexpr int kWinLo = 64, kWinHi = 64, kWinLen = kWinLo + kWave + kWinHi;
+
+template <class T, class P, class VI, class CI, int W, bool WIN>
+__global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col,
                                                       const typename SellStore<VI>::type* __restrict__ val,
                                                       const T* __restrict__ wprev, const T* __restrict__ inv_p,
                                                       T* __restrict__ V, int64_t ld, int k,
                                                       const P* __restrict__ diag, T* __restrict__ w,
                                                       GivensFold<T> fold) {
+    __shared__ T win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const T inv = fold_givens(fold, inv_p);  // block-wide: before any lane leaves
-    const int lane = threadIdx.x & (kWave - 1);
-    const int s = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int s = blockIdx.x * (kBlock / kWave) + wid;
     if (s >= nslices) return;
-    const double sum = sell_row_sum<typename SellStore<VI>::type, CI, W>(
-        s, lane, off, col, val, [&](int c) { return (double)(T)(wprev[c] * inv); });
-    const int i = s * kWave + lane;
+    const int row0 = s * kWave;
+    double sum;
+    if constexpr (WIN) {
+#pragma unroll
+        for (int q = 0; q < kWinLen / kWave; ++q) {
+            const int c = row0 - kWinLo + q * kWave + lane;
+            win[wid][q * kWave + lane] = (c >= 0 && c < n_ext) ? (T)(wprev[c] * inv) : T(0);
+        }
+        wave_lds_sync();
+        sum = sell_row_sum<typename SellStore<VI>::type, CI, W>(
+            s, lane, off, col, val, [&](int c) { return (double)win[wid][c - row0 + kWinLo]; });
+    } else {
+        sum = sell_row_sum<typename SellStore<VI>::type, CI, W>(
+            s, lane, off, col, val, [&](int c) { return (double)(T)(wprev[c] * inv); });
+    }
+    const int i = row0 + lane;
     if (i < n) {
         const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
         w[i] = precond<T, P>(t, diag, i);
@@ -367,20 +389,24 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int nslices, const 
     }
 }
 
-// largest |col - first row of its slice| over the matrix (int16 eligibility)
+// min and max of (col - first row of its slice) over the matrix: int16
+// column eligibility and the LDS window of k_step_sell
 __global__ void k_sell_span(int n, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                            unsigned* __restrict__ out) {
+                            int* __restrict__ out) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned m = 0;
+    int lo = INT32_MAX, hi = INT32_MIN;
     if (r < n) {
         const int row0 = r & ~(kWave - 1);
         for (int j = rowptr[r]; j < rowptr[r + 1]; ++j) {
             const int d = col[j] - row0;
-            m = max(m, (unsigned)(d < 0 ? -d : d));
+            lo = min(lo, d);
+            hi = max(hi, d);
         }
     }
-    m = wave_max(m);
-    if ((threadIdx.x & (kWave - 1)) == 0) atomicMax(out, m);
+    if (r < n && rowptr[r] < rowptr[r + 1]) {
+        atomicMin(out, lo);
+        atomicMax(out + 1, hi);
+    }
 }
 
 template <class VI> __device__ __forceinline__ typename SellStore<VI>::type sell_raw(VI v) { return v; }
@@ -680,6 +706,7 @@ struct mpg_arnoldi {
     struct {
         int nslices = 0, W = 1;
         bool c16 = false;
+        bool win = false;  // every slice's columns inside the LDS window
         int64_t padded = 0;
         int64_t* off = nullptr;
         void* col = nullptr;
@@ -749,6 +776,10 @@ int sell_dispatch(int W, bool c16, F&& f) {
     };
     return c16 ? with_w(int16_t()) : with_w(int32_t());
 }
+template <class F>
+int sell_dispatch_win(bool win, F&& f) {
+    return win ? f(std::true_type()) : f(std::false_type());
+}
 
 // Build the SELL-64 copy (format: 0 auto, 1 never, 2 always). Auto takes it
 // when padding adds at most 20% to the stored entries; W is the widest
@@ -777,18 +808,20 @@ int sell_build(mpg_arnoldi* a, int format) {
     for (int s = 0; s < ns; ++s)
         off[s + 1] = off[s] + (int64_t)kWave * ((width[s] + best_w - 1) / best_w * best_w);
 
-    unsigned* span = nullptr;
-    unsigned span_h = 0;
-    if (hipMalloc((void**)&span, sizeof(unsigned)) != hipSuccess) return MPG_ERR_ALLOC;
-    bool ok = hipMemsetAsync(span, 0, sizeof(unsigned), a->ctx->stream) == hipSuccess;
+    int* span = nullptr;
+    int span_h[2] = {INT32_MAX, INT32_MIN};
+    if (hipMalloc((void**)&span, 2 * sizeof(int)) != hipSuccess) return MPG_ERR_ALLOC;
+    bool ok = hipMemcpyAsync(span, span_h, 2 * sizeof(int), hipMemcpyHostToDevice, a->ctx->stream) == hipSuccess;
     if (ok) {
         k_sell_span<<<(n + kBlock - 1) / kBlock, kBlock, 0, a->ctx->stream>>>(n, A->rowptr, A->col, span);
-        ok = hipMemcpyAsync(&span_h, span, sizeof(unsigned), hipMemcpyDeviceToHost, a->ctx->stream) == hipSuccess &&
+        ok = hipMemcpyAsync(span_h, span, 2 * sizeof(int), hipMemcpyDeviceToHost, a->ctx->stream) == hipSuccess &&
              hipStreamSynchronize(a->ctx->stream) == hipSuccess;
     }
     (void)hipFree(span);
     if (!ok) return MPG_ERR_HIP;
-    const bool c16 = span_h <= 32767u;
+    const bool c16 = span_h[0] >= -32767 && span_h[1] <= 32767;
+    const char* wenv = std::getenv("MPG_SELL_WINDOW");  // 0: always gather from global memory
+    const bool win = !(wenv && *wenv == '0') && span_h[0] >= -kWinLo && span_h[1] < kWave + kWinHi;
     const size_t vsize = a->d.inner_val == MPG_F64 ? 8 : a->d.inner_val == MPG_F32 ? 4 : 2;
     auto& S = a->sell;
     if (hipMalloc((void**)&S.off, off.size() * 8) != hipSuccess ||
@@ -800,6 +833,7 @@ int sell_build(mpg_arnoldi* a, int format) {
     S.nslices = ns;
     S.W = best_w;
     S.c16 = c16;
+    S.win = win;
     S.padded = best;
     const int grid = (int)(((int64_t)ns * kWave + kBlock - 1) / kBlock);
     int st = dispatch(a->combo, [&](auto, auto, auto, auto vi) {
@@ -874,13 +908,14 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
 }
 
 int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
-                            int64_t* stored) {
+                            int64_t* stored, int32_t* window) {
     if (!a) return MPG_ERR_ARG;
     const bool sell = a->sell.nslices > 0;
     if (format) *format = sell ? 2 : 1;
     if (vec_width) *vec_width = sell ? a->sell.W : 4;
     if (col_bytes) *col_bytes = sell && a->sell.c16 ? 2 : 4;
     if (stored) *stored = sell ? a->sell.padded : a->d.A->nnz;
+    if (window) *window = sell && a->sell.win ? 1 : 0;
     return MPG_OK;
 }
 
@@ -967,12 +1002,15 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold) {
             return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
                 using CI = decltype(ci);
                 const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
-                k_step_sell<T, P, VI, CI, decltype(wc)::value><<<grid, kBlock, 0, a->ctx->stream>>>(
-                    a->d.n, S.nslices, S.off, static_cast<const CI*>(S.col),
-                    static_cast<const typename SellStore<VI>::type*>(S.val), static_cast<const T*>(a->w[k & 1]),
-                    static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k, diag,
-                    static_cast<T*>(a->w[(k + 1) & 1]), gf);
-                return (int)MPG_OK;
+                return sell_dispatch_win(S.win, [&](auto wn) {
+                    k_step_sell<T, P, VI, CI, decltype(wc)::value, decltype(wn)::value>
+                        <<<grid, kBlock, 0, a->ctx->stream>>>(
+                            a->d.n, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
+                            static_cast<const typename SellStore<VI>::type*>(S.val),
+                            static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
+                            static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf);
+                    return (int)MPG_OK;
+                });
             });
         }
         k_step_spmv<T, P, VI><<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(

@@ -701,9 +701,9 @@ double mpg_engine_phase_bytes(mpg_engine_t e, int which) {
 }
 
 int mpg_engine_spmv_layout(mpg_engine_t e, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
-                           int64_t* stored) {
+                           int64_t* stored, int32_t* window) {
     if (!e || !e->eng) return MPG_ERR_ARG;
-    return mpg_arnoldi_spmv_layout(e->eng->arnoldi(), format, vec_width, col_bytes, stored);
+    return mpg_arnoldi_spmv_layout(e->eng->arnoldi(), format, vec_width, col_bytes, stored, window);
 }
 
 int mpg_engine_destroy(mpg_engine_t e) {

@@ -73,9 +73,11 @@ int mpg_arnoldi_destroy(mpg_arnoldi_t a);
  * csrmv's input, types_cuda.hpp:53-60), 2 = SELL-64 copy made at create
  * (64-row slices, vec_width entries per lane load, col_bytes 4 = int32
  * columns or 2 = int16 offsets from the slice's first row); *stored = stored
- * entries including padding (nnz for CSR). Any output may be NULL. */
+ * entries including padding (nnz for CSR); *window = 1 when every slice's
+ * columns lie within [row0 - 64, row0 + 128) and the SpMV reads v_k from an
+ * LDS window instead of gathering from memory. Any output may be NULL. */
 int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
-                            int64_t* stored);
+                            int64_t* stored, int32_t* window);
 
 int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
 int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);

@@ -111,7 +111,7 @@ int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms);
 double mpg_engine_phase_bytes(mpg_engine_t e, int which);
 /* storage of the engine's Arnoldi SpMV (mpg_arnoldi_spmv_layout) */
 int mpg_engine_spmv_layout(mpg_engine_t e, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
-                           int64_t* stored);
+                           int64_t* stored, int32_t* window);
 int mpg_engine_destroy(mpg_engine_t e);
 
 #ifdef __cplusplus

@@ -25,19 +25,21 @@ def _case_id(c):
     return f"{k['matrix']}-{k['mode']}-{k['orth']}-{k['prec']}-m{k['rlen']}"
 
 
-# fused engine on both Arnoldi SpMV storages (CSR row blocks, SELL-64), and
-# with the two launch-count variants: the Givens step folded into the next
-# SpMV launch, and the one-GPU last-arriver combines
-# (engine, storage, experiment flag set to 1: MPG_COMBINE / MPG_FOLD_GIVENS / MPG_CGS_PARTIALS)
-ENGINES = {"surface": ("surface", "auto", None), "fused-csr": ("fused", "csr", None),
-           "fused-sell": ("fused", "sell", None), "fused-fold": ("fused", "auto", "MPG_FOLD_GIVENS"),
-           "fused-combine": ("fused", "auto", "MPG_COMBINE"), "fused-cgspart": ("fused", "auto", "MPG_CGS_PARTIALS")}
+# (engine, storage, environment): the fused engine on both Arnoldi SpMV
+# storages (CSR row blocks, SELL-64);: MPG_SELL_WINDOW=0 gathers v_k from memory
+# instead of the LDS window; the others are launch-count experiments
+FLAGS = ("MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS", "MPG_SELL_WINDOW")
+ENGINES = {"surface": ("surface", "auto", {}), "fused-csr": ("fused", "csr", {}),
+           "fused-sell": ("fused", "sell", {}), "fused-gather": ("fused", "sell", {"MPG_SELL_WINDOW": "0"}),
+           "fused-fold": ("fused", "auto", {"MPG_FOLD_GIVENS": "1"}),
+           "fused-combine": ("fused", "auto", {"MPG_COMBINE": "1"}),
+           "fused-cgspart": ("fused", "auto", {"MPG_CGS_PARTIALS": "1"})}
 
 
 def _engine(monkeypatch, engine):
-    eng, fmt, flag = ENGINES[engine]
-    for f in ("MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS"):
-        monkeypatch.setenv(f, "1" if f == flag else "0")
+    eng, fmt, env = ENGINES[engine]
+    for f in FLAGS:
+        monkeypatch.setenv(f, env.get(f, "1" if f == "MPG_SELL_WINDOW" else "0"))
     return dict(engine=eng, spmv_format=fmt)
 
 
@@ -76,7 +78,7 @@ def test_spmv_layout_choice(mpg):
     e = mpg.Engine(A, b, xt, mode="mixed", orth="cgs", prec="identity", rlen=30, tol=0.0, max_restarts=2)
     try:  # 10 entries per row, 64-row slices, the last one half full
         assert e.spmv_layout() == {"format": "sell", "vec_width": 2, "col_bytes": 2,
-                                   "stored": -(-A.nrows // 64) * 64 * 10}
+                                   "stored": -(-A.nrows // 64) * 64 * 10, "window": True}
     finally:
         e.close()
     B = _arrow(mpg, 3000)
