@@ -301,17 +301,20 @@ struct GivensFold {
     GivensArgs<T> g;
 };
 
-template <class T>
+template <bool FOLD, class T>
 __device__ __forceinline__ T fold_givens(const GivensFold<T>& f, const T* __restrict__ inv_p) {
-    if (!f.norm2) return *inv_p;
-    __shared__ T col[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
-    __shared__ double scratch[kBlock / kWave];
-    __shared__ T inv_s;
-    const double nrm2sq = f.nparts > 0 ? sum_partials<kBlock>(f.norm2, f.nparts, scratch) : f.norm2[0];
-    if (threadIdx.x == 0) inv_s = inv_of_norm2<T>(nrm2sq);
-    if (blockIdx.x == 0) givens_block(f.g, nrm2sq, col, c_s, s_s);
-    __syncthreads();
-    return inv_s;
+    if constexpr (!FOLD) {
+        return *inv_p;
+    } else {
+        __shared__ T col[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
+        __shared__ double scratch[kBlock / kWave];
+        __shared__ T inv_s;
+        const double nrm2sq = f.nparts > 0 ? sum_partials<kBlock>(f.norm2, f.nparts, scratch) : f.norm2[0];
+        if (threadIdx.x == 0) inv_s = inv_of_norm2<T>(nrm2sq);
+        if (blockIdx.x == 0) givens_block(f.g, nrm2sq, col, c_s, s_s);
+        __syncthreads();
+        return inv_s;
+    }
 }
 #pragma clang fp contract(on)
 
@@ -321,7 +324,7 @@ __device__ __forceinline__ T fold_givens(const GivensFold<T>& f, const T* __rest
 // that Givens step folded in (fold.norm2 != nullptr). The Gram-Schmidt dots
 // follow in k_panel_dots (measured: dots inside this gather-bound launch
 // cost more than the separate pass, 71 us vs 30 + 20 us on BAND-10M).
-template <class T, class P, class VI>
+template <class T, class P, class VI, bool FOLD>
 __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict__ blocks, int nblocks,
                                                       const int32_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ col, const VI* __restrict__ val,
@@ -331,7 +334,7 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
                                                       GivensFold<T> fold) {
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
-    const T inv = fold_givens(fold, inv_p);
+    const T inv = fold_givens<FOLD>(fold, inv_p);
     T* __restrict__ Vk = V + (int64_t)k * ld;
     for_rows(
         blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)(T)(wprev[c] * inv); },
@@ -353,7 +356,7 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
 // tools/sell_bench.hip). Values are the same T(w_prev * inv) either way.
 constexpr int kWinLo = 64, kWinHi = 64, kWinLen = kWinLo + kWave + kWinHi;
 
-template <class T, class P, class VI, class CI, int W, bool WIN>
+template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD>
 __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col,
                                                       const typename SellStore<VI>::type* __restrict__ val,
@@ -362,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
                                                       const P* __restrict__ diag, T* __restrict__ w,
                                                       GivensFold<T> fold) {
     __shared__ T win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
-    const T inv = fold_givens(fold, inv_p);  // block-wide: before any lane leaves
+    const T inv = fold_givens<FOLD>(fold, inv_p);  // block-wide: before any lane leaves
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     const int s = blockIdx.x * (kBlock / kWave) + wid;
     if (s >= nslices) return;
@@ -512,8 +515,8 @@ __global__ __launch_bounds__(BS) void k_panel_dots(int n, const T* __restrict__ 
 // GIVENS (one GPU, last pass, m <= kFoldMaxM): the ||w'||^2 partials go
 // write-through and the last-arriving workgroup sums them and runs the
 // Givens step k (givens_block) — no separate Givens launch.
-template <class T, bool NEXT_DOTS, bool GIVENS = false>
-__global__ __launch_bounds__(kBlock) void k_cgs_update(int n, const T* __restrict__ V, int64_t ld, int k,
+template <class T, bool NEXT_DOTS, bool GIVENS = false, int BS = kBlock>
+__global__ __launch_bounds__(BS) void k_cgs_update(int n, const T* __restrict__ V, int64_t ld, int k,
                                                        const double* __restrict__ sums, T* __restrict__ coef_out,
                                                        T* __restrict__ w, double* __restrict__ partial,
                                                        unsigned* __restrict__ cnt, GivensArgs<T> g, int part_G) {
@@ -539,7 +542,7 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update(int n, const T* __restric
             if (blockIdx.x == 0) coef_out[j] = c;
         }
     } else {
-        for (int j = threadIdx.x; j < nc; j += kBlock) {
+        for (int j = threadIdx.x; j < nc; j += BS) {
             const T c = (T)sums[j];
             coef[j] = (double)c;
             if (blockIdx.x == 0) coef_out[j] = c;
@@ -551,7 +554,7 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update(int n, const T* __restric
 #pragma unroll
     for (int c = 0; c < NA; ++c) acc[c] = 0.0;
     const int n4 = n & ~3;
-    for (int i = 4 * (blockIdx.x * kBlock + threadIdx.x); i < n4; i += 4 * gridDim.x * kBlock) {
+    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
         double t[4] = {0.0, 0.0, 0.0, 0.0};
         int j = 0;
         for (; j + 8 <= nc; j += 8) {
@@ -593,7 +596,7 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update(int n, const T* __restric
         }
     }
     // tail rows (n not a multiple of 4)
-    for (int i = n4 + blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
         double t = 0.0;
         for (int j = 0; j < nc; ++j) t += (double)V[(int64_t)j * ld + i] * coef[j];
         const T wi = T(-1) * (T)t + T(1) * w[i];
@@ -606,12 +609,12 @@ __global__ __launch_bounds__(kBlock) void k_cgs_update(int n, const T* __restric
             acc[0] += (double)wi * (double)wi;
         }
     }
-    store_partials<NA, kBlock, GIVENS>(acc, NEXT_DOTS ? (nc < kNC ? nc : kNC) : 1, partial);
+    store_partials<NA, BS, GIVENS>(acc, NEXT_DOTS ? (nc < kNC ? nc : kNC) : 1, partial);
     if constexpr (GIVENS) {
         if (last_arriver(cnt)) {
             __shared__ T col[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
-            __shared__ double scratch[kBlock / kWave];
-            const double nrm2sq = sum_partials<kBlock>(partial, gridDim.x, scratch);
+            __shared__ double scratch[BS / kWave];
+            const double nrm2sq = sum_partials<BS>(partial, gridDim.x, scratch);
             givens_block(g, nrm2sq, col, c_s, s_s);
         }
     }
@@ -1003,8 +1006,9 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold) {
                 using CI = decltype(ci);
                 const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
                 return sell_dispatch_win(S.win, [&](auto wn) {
-                    k_step_sell<T, P, VI, CI, decltype(wc)::value, decltype(wn)::value>
-                        <<<grid, kBlock, 0, a->ctx->stream>>>(
+                    auto kern = fold ? k_step_sell<T, P, VI, CI, decltype(wc)::value, decltype(wn)::value, true>
+                                     : k_step_sell<T, P, VI, CI, decltype(wc)::value, decltype(wn)::value, false>;
+                    kern<<<grid, kBlock, 0, a->ctx->stream>>>(
                             a->d.n, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
@@ -1013,7 +1017,8 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold) {
                 });
             });
         }
-        k_step_spmv<T, P, VI><<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(
+        auto kern = fold ? k_step_spmv<T, P, VI, true> : k_step_spmv<T, P, VI, false>;
+        kern<<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(
             A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,
             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,
             diag, static_cast<T*>(a->w[(k + 1) & 1]), gf);
@@ -1092,13 +1097,13 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
             k_cgs_update<T, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, a->counters + 32, g,
                 part_G);
-        } else {
-            k_cgs_update<T, false><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+        } else {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
+            k_cgs_update<T, false, false, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, part_G);
         }
         return (int)MPG_OK;
     });
-    a->last_G = row_grid(a);
+    a->last_G = next_dots || givens ? row_grid(a) : a->Gd;
     a->last_part = a->partial;
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);

@@ -77,6 +77,8 @@ struct FusedEngine::Impl {
     bool fold = false;     // Givens step folded into the next SpMV launch
     bool combine = false;  // last-arriver combines in the dots and CGS launches
     bool cgs_partials = false;  // CGS update sums the dots partials in-launch
+    int timed = -1;                  // phase whose launches time_phase brackets with events
+    std::vector<hipEvent_t> marks;   // ... begin/end pairs
     std::vector<int32_t> rowptr_host;
     mpg_ilu_t ilu = nullptr;  // ILU(0) factors (prec ilu / ilu_jacobi), applied between phase kernels
 
@@ -286,9 +288,10 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
 
     const char* env = std::getenv("MPG_NO_GRAPH");
     I.use_graph = !(env && *env == '1') && (!comm || comm->capturable());
-    // Launch-count experiments, both off by default (BAND-10M, one MI355X):
-    // MPG_FOLD_GIVENS=1 folds Givens(k-1) into SpMV(k) — every SpMV workgroup
-    // sums the ||w||^2 partials itself: 18.0-18.3k vs 18.0k it/s, within noise;
+    // Givens(k-1) is folded into SpMV(k) by default (MPG_FOLD_GIVENS=0: its
+    // own launch): every SpMV workgroup sums the 256 ||w||^2 partials of the
+    // 1024-thread CGS update itself (+1.9 us per SpMV, -4.6 us Givens launch
+    // and its boundary: 19.3k vs 18.7k it/s on BAND-10M). Experiments, off:
     // MPG_COMBINE=1 (one GPU, CGS/CGSR) does last-arriver combines in the dots
     // and CGS launches: 15.1k it/s (1024 tickets on one counter serialise);
     // MPG_CGS_PARTIALS=1: every CGS workgroup sums the 256 dots partials per
@@ -299,7 +302,7 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     const char* penv = std::getenv("MPG_CGS_PARTIALS");
     I.cgs_partials = !comm && !I.combine && penv && *penv == '1' && I.orth != MPG_ORTH_MGS;
     const char* fenv = std::getenv("MPG_FOLD_GIVENS");
-    I.fold = !I.combine && fenv && *fenv == '1' && I.m <= mpg_arnoldi_fold_max_m();
+    I.fold = !I.combine && !(fenv && *fenv == '0') && I.m <= mpg_arnoldi_fold_max_m();
     check(mpg_ctx_sync(ctx), "sync", ctx);
     setup_seconds = std::chrono::duration<double>(clk::now() - t0).count();
     prologue();
@@ -313,6 +316,7 @@ void FusedEngine::sync() { check(mpg_ctx_sync(p_->ctx), "sync", p_->ctx); }
 void FusedEngine::prologue() {
     Impl& I = *p_;
     if (I.comm) I.comm->halo(I.x.p, (int)dsize(I.ty.X), I.stream());
+    timed(1, [&] { check(mpg_arnoldi_prologue(I.arn), "prologue", I.ctx); });
     check(mpg_arnoldi_prologue(I.arn), "prologue", I.ctx);
     if (I.ilu) {  // w = M(T(r)) outside the kernel, then ||w||^2 again
         I.apply_ilu(mpg_arnoldi_wprev_dev(I.arn, 0));
@@ -348,10 +352,12 @@ void FusedEngine::step(int k, bool fold) {
     if (fold && k > 0) {
         if (I.comm) reduce(1);
         if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
+        timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
         check(I.comm ? mpg_arnoldi_givens_spmv(I.arn, k) : mpg_arnoldi_givens_partials_spmv(I.arn, k), "givens+spmv",
               I.ctx);
     } else {
         if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
+        timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
         check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
     }
     if (I.ilu) I.apply_ilu(mpg_arnoldi_wprev_dev(I.arn, k + 1));  // w = M(A v_k)
@@ -372,6 +378,7 @@ void FusedEngine::step(int k, bool fold) {
         if (I.combine && small) {
             check(mpg_arnoldi_dots_sums(I.arn, k), "dots+sums", I.ctx);
         } else {
+            timed(3, [&] { check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx); });
             check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
             if (I.cgs_partials && small) {
                 check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx);
@@ -391,6 +398,7 @@ void FusedEngine::step(int k, bool fold) {
             check(mpg_arnoldi_cgs_givens(I.arn, k, last_pass), "cgs+givens", I.ctx);
             return;
         }
+        timed(2, [&] { check(mpg_arnoldi_cgs(I.arn, k, last_pass), "cgs", I.ctx); });
         check(mpg_arnoldi_cgs(I.arn, k, last_pass), "cgs", I.ctx);
     }
     if (!fold) givens(k);
@@ -571,38 +579,45 @@ double FusedEngine::phase_bytes(int which) const {
 
 mpg_arnoldi_t FusedEngine::arnoldi() const { return p_->arn; }
 
+// Device-event time of one phase kernel in its place in the cycle: `reps`
+// restart cycles run eagerly in cycle order, and at every launch of phase
+// `which` the plain form of that kernel is first replayed kTimedReplays
+// times back to back between one event pair (amortising the dispatch
+// latency an event pair around a single launch would include), then the
+// cycle's own launch follows. Replays of the non-idempotent CGS update leave
+// the engine's state meaningless: time_phase is for measurement only.
+constexpr int kTimedReplays = 10;
+
 double FusedEngine::time_phase(int which, int reps) {
     Impl& I = *p_;
-    hipEvent_t e0, e1;
-    hipck(hipEventCreate(&e0), "event");
-    hipck(hipEventCreate(&e1), "event");
+    I.timed = which;
+    I.marks.clear();
+    for (int r = 0; r < reps; ++r) cycle_program();
+    I.timed = -1;
+    hipck(hipStreamSynchronize(I.stream()), "sync");
     float total_ms = 0;
-    int launches = 0;
-    const int ks = which == 1 ? 1 : I.m;
-    const bool fold = I.fold;  // the form cycle_program launches
-    for (int k = 0; k < ks; ++k) {
-        hipck(hipEventRecord(e0, I.stream()), "record");
-        for (int r = 0; r < reps; ++r) {
-            if (which == 0 && fold && k > 0)
-                check(I.comm ? mpg_arnoldi_givens_spmv(I.arn, k) : mpg_arnoldi_givens_partials_spmv(I.arn, k),
-                      "givens+spmv", I.ctx);
-            else if (which == 0) check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
-            else if (which == 1) check(mpg_arnoldi_prologue(I.arn), "prologue", I.ctx);
-            else if (which == 3 && I.combine && k + 1 <= 32) check(mpg_arnoldi_dots_sums(I.arn, k), "dots", I.ctx);
-            else if (which == 3) check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
-            else if (I.combine && I.orth == MPG_ORTH_CGS) check(mpg_arnoldi_cgs_givens(I.arn, k, 0), "cgs", I.ctx);
-            else check(mpg_arnoldi_cgs(I.arn, k, 0), "cgs", I.ctx);
-        }
-        hipck(hipEventRecord(e1, I.stream()), "record");
-        hipck(hipEventSynchronize(e1), "sync");
+    const size_t pairs = I.marks.size() / 2;
+    for (size_t q = 0; q < pairs; ++q) {
         float ms = 0;
-        hipck(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+        hipck(hipEventElapsedTime(&ms, I.marks[2 * q], I.marks[2 * q + 1]), "elapsed");
         total_ms += ms;
-        launches += reps;
     }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    return total_ms / launches;
+    for (hipEvent_t e : I.marks) (void)hipEventDestroy(e);
+    I.marks.clear();
+    return pairs ? total_ms / (pairs * kTimedReplays) : 0.0;
+}
+
+template <class F>
+void FusedEngine::timed(int phase, F&& launch) {
+    Impl& I = *p_;
+    if (I.timed != phase) return;
+    hipEvent_t e[2];
+    for (auto& x : e) hipck(hipEventCreate(&x), "event");
+    hipck(hipEventRecord(e[0], I.stream()), "record");
+    for (int r = 0; r < kTimedReplays; ++r) launch();
+    hipck(hipEventRecord(e[1], I.stream()), "record");
+    I.marks.push_back(e[0]);
+    I.marks.push_back(e[1]);
 }
 
 // ---------------------------------------------------------------- mpg_solve (fused)

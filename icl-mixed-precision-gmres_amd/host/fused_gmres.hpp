@@ -93,6 +93,8 @@ private:
     void step(int k, bool fold);
     void reduce(int nc);
     void givens(int k);
+    template <class F>
+    void timed(int phase, F&& launch);
     void update(int k);
     void read_report(int count);
     void cycle_program();
