@@ -621,24 +621,54 @@ __global__ __launch_bounds__(BS) void k_cgs_update(int n, const T* __restrict__ 
 }
 
 // ---------------------------------------------------------------- step: MGS
-// h_jk = T(sums[0]); w -= h_jk v_j (naxpy); partial <v_{j+1}, w> or ||w||^2
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_mgs_update(int n, const T* __restrict__ V, int64_t ld, int j, int k,
-                                                       const double* __restrict__ sums, T* __restrict__ hjk,
-                                                       T* __restrict__ w, double* __restrict__ partial) {
-    const T h = (T)sums[0];
+// h_jk = T(sums[0]); w -= h_jk v_j (naxpy); partial <v_{j+1}, w> or ||w||^2.
+// src_G > 0: h_jk is summed here from the src_G partials of the previous
+// launch (the dots or the previous MGS update, one GPU), in the same fixed
+// order in every workgroup — one launch per j instead of reduce + update.
+// Each lane owns 4 consecutive rows (16-B loads).
+template <class T, int BS>
+__global__ __launch_bounds__(BS) void k_mgs_update(int n, const T* __restrict__ V, int64_t ld, int j, int k,
+                                                   const double* __restrict__ src, int src_G, T* __restrict__ hjk,
+                                                   T* __restrict__ w, double* __restrict__ partial) {
+    __shared__ double scratch[BS / kWave];
+    __shared__ T h_s;
+    if (src_G > 0) {
+        const double sum = sum_partials<BS>(src, src_G, scratch);
+        if (threadIdx.x == 0) h_s = (T)sum;
+        __syncthreads();
+    } else if (threadIdx.x == 0) {
+        h_s = (T)src[0];
+    }
+    __syncthreads();
+    const T h = h_s;
     if (blockIdx.x == 0 && threadIdx.x == 0) *hjk = h;
     const T* __restrict__ vj = V + (int64_t)j * ld;
     const T* __restrict__ vn = V + (int64_t)(j + 1) * ld;
     const bool last = j == k;
     double acc[1] = {0.0};
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const int n4 = n & ~3;
+    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
+        double wv[4], vv[4], nv[4] = {0.0, 0.0, 0.0, 0.0};
+        Row4<T>::load(w + i, wv);
+        Row4<T>::load(vj + i, vv);
+        if (!last) Row4<T>::load(vn + i, nv);
+        T wo[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            T wi = (T)wv[r];
+            wi -= h * (T)vv[r];
+            wo[r] = wi;
+            acc[0] += last ? (double)wi * (double)wi : nv[r] * (double)wi;
+        }
+        Row4<T>::store(w + i, wo);
+    }
+    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
         T wi = w[i];
         wi -= h * vj[i];
         w[i] = wi;
         acc[0] += last ? (double)wi * (double)wi : (double)vn[i] * (double)wi;
     }
-    store_partials<1>(acc, 1, partial);
+    store_partials<1, BS>(acc, 1, partial);
 }
 
 #pragma clang fp contract(off)
@@ -1114,22 +1144,31 @@ int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pa
 int mpg_arnoldi_cgs_partials(mpg_arnoldi_t a, int k) { return cgs_impl(a, k, 0, false, true); }
 int mpg_arnoldi_cgs_givens(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, true); }
 
-int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j) {
+static int mgs_impl(mpg_arnoldi_t a, int k, int j, bool from_partials) {
     if (!a || k < 0 || k >= a->d.m || j < 0 || j > k) return MPG_ERR_ARG;
+    // from_partials: h_jk from the previous launch's partials; the update
+    // writes into the other partial buffer (the previous one is still read)
+    const double* src = from_partials ? a->last_part : a->sums;
+    const int src_G = from_partials ? a->last_G : 0;
+    double* dst = from_partials && a->last_part == a->partial ? a->dpart : a->partial;
+    if (from_partials && src_G > kCombineGroups * 4) return MPG_ERR_ARG;
     int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
         using T = decltype(t);
         T* hjk = static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) + j;
-        k_mgs_update<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->V), a->ld, j,
-                                                                    k, a->sums, hjk,
-                                                                    static_cast<T*>(a->w[(k + 1) & 1]), a->partial);
-        return MPG_OK;
+        k_mgs_update<T, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+            a->d.n, static_cast<const T*>(a->V), a->ld, j, k, src, src_G, hjk, static_cast<T*>(a->w[(k + 1) & 1]),
+            dst);
+        return (int)MPG_OK;
     });
-    a->last_G = row_grid(a);
-    a->last_part = a->partial;
+    a->last_G = a->Gd;
+    a->last_part = dst;
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
 }
+
+int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j) { return mgs_impl(a, k, j, false); }
+int mpg_arnoldi_mgs_partials(mpg_arnoldi_t a, int k, int j) { return mgs_impl(a, k, j, true); }
 
 static int givens_impl(mpg_arnoldi_t a, int k, bool from_partials) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;

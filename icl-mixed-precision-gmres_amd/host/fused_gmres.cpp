@@ -363,10 +363,14 @@ void FusedEngine::step(int k, bool fold) {
     if (I.ilu) I.apply_ilu(mpg_arnoldi_wprev_dev(I.arn, k + 1));  // w = M(A v_k)
     if (I.orth == MPG_ORTH_MGS) {
         check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
-        reduce(1);
-        for (int j = 0; j <= k; ++j) {
-            check(mpg_arnoldi_mgs(I.arn, k, j), "mgs", I.ctx);
-            if (j < k) reduce(1);
+        if (!I.comm) {  // one GPU: each update sums the previous launch's partials itself
+            for (int j = 0; j <= k; ++j) check(mpg_arnoldi_mgs_partials(I.arn, k, j), "mgs", I.ctx);
+        } else {
+            reduce(1);
+            for (int j = 0; j <= k; ++j) {
+                check(mpg_arnoldi_mgs(I.arn, k, j), "mgs", I.ctx);
+                if (j < k) reduce(1);
+            }
         }
     } else {
         // MPG_CGS_PARTIALS=1 (one GPU, k+1 <= 32): the CGS update sums the dots

@@ -92,6 +92,10 @@ int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass);  /* pass 0: h; pass 1: CG
  * mpg_arnoldi_reduce + mpg_arnoldi_cgs(a, k, 0) */
 int mpg_arnoldi_cgs_partials(mpg_arnoldi_t a, int k);
 int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j);
+/* one GPU: MGS update j taking h_jk from the partials of the previous launch
+ * (mpg_arnoldi_dots for j = 0, the previous update otherwise) — replaces
+ * mpg_arnoldi_reduce + mpg_arnoldi_mgs */
+int mpg_arnoldi_mgs_partials(mpg_arnoldi_t a, int k, int j);
 int mpg_arnoldi_givens(mpg_arnoldi_t a, int k);
 /* single-GPU form: the Givens kernel sums the ||w||^2 partials of the last
  * producer itself, saving one mpg_arnoldi_reduce launch per step */
