@@ -828,13 +828,19 @@ int sell_build(mpg_arnoldi* a, int format) {
     const int ns = (n + kWave - 1) / kWave;
     std::vector<int> width((size_t)ns, 0);
     for (int r = 0; r < n; ++r) width[r / kWave] = std::max(width[r / kWave], rp[r + 1] - rp[r]);
+    // the widest vector whose padding stays within 15 % of the least padded
+    // layout: narrow (2-4 B per lane) index loads cost more than the padding
+    int64_t padded[5] = {0, 0, 0, 0, 0};
+    for (int W : {4, 2, 1})
+        for (int s = 0; s < ns; ++s) padded[W] += (int64_t)kWave * ((width[s] + W - 1) / W * W);
+    const int64_t least = std::min(padded[1], std::min(padded[2], padded[4]));
     int best_w = 1;
-    int64_t best = -1;
-    for (int W : {4, 2, 1}) {
-        int64_t p = 0;
-        for (int s = 0; s < ns; ++s) p += (int64_t)kWave * ((width[s] + W - 1) / W * W);
-        if (best < 0 || p < best) best = p, best_w = W;
-    }
+    for (int W : {4, 2, 1})
+        if ((double)padded[W] <= 1.15 * (double)least) {
+            best_w = W;
+            break;
+        }
+    const int64_t best = padded[best_w];
     if (format == 0 && (double)best > 1.2 * (double)A->nnz) return MPG_OK;
     if (best >= ((int64_t)1 << 31) * 4) return format == 2 ? MPG_ERR_UNSUPPORTED : MPG_OK;
     std::vector<int64_t> off((size_t)ns + 1, 0);
