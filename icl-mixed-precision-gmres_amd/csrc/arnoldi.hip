@@ -695,15 +695,47 @@ __global__ __launch_bounds__(kBlock) void k_trsv_upper(int k, int ldh, const T* 
     }
     for (int i = threadIdx.x; i < k; i += kBlock) y[i] = ys[i];
 }
+// The same upper solve by one wave64 (k <= 64): lane i holds y_i, the
+// column sweep's scalar is broadcast with a shuffle, H(0:k,0:k) is in LDS
+// (column j at Hs[j * 64]). No barrier inside the sweep.
+template <class T>
+__device__ __forceinline__ T trsv_upper_wave(int k, const T* Hs, T y, int lane) {
+    for (int j = k - 1; j >= 0; --j) {
+        T yj = __shfl(y, j, kWave);
+        if (yj != T(0)) yj = yj / Hs[j * kWave + j];
+        if (lane == j) y = yj;
+        if (yj != T(0) && lane < j) y = y - yj * Hs[j * kWave + lane];
+    }
+    return y;
+}
 #pragma clang fp contract(on)
 
 // x += X(T(V y)): mixed form gemv(1, V, y, 0, tmp); copy; axpy(1, tmp, x)
 // (same-precision form gemv(1, V, y, 1, x) gives the same fl(t + x))
-template <class T, class X>
+// SOLVE (k <= 64): y = H(0:k,0:k)^-1 s(0:k) is formed first by every
+// workgroup (trsv_upper_wave) — one launch per restart instead of two. s is
+// not overwritten (the next prologue resets it).
+template <class T, class X, bool SOLVE>
 __global__ __launch_bounds__(kBlock) void k_update_x(int n, const T* __restrict__ V, int64_t ld, int k,
-                                                     const T* __restrict__ y, X* __restrict__ x) {
-    __shared__ T ys[1024];
-    for (int j = threadIdx.x; j < k; j += kBlock) ys[j] = y[j];
+                                                     const T* __restrict__ y, const T* __restrict__ H, int ldh,
+                                                     X* __restrict__ x) {
+    __shared__ T ys[SOLVE ? kWave : 1024];
+    if constexpr (SOLVE) {
+        __shared__ T Hs[kWave * kWave];
+        for (int e = threadIdx.x; e < k * kWave; e += kBlock) {
+            const int j = e / kWave, i = e % kWave;
+            Hs[e] = i <= j ? H[(int64_t)j * ldh + i] : T(0);
+        }
+        __syncthreads();
+        if (threadIdx.x < kWave) {
+            const int lane = threadIdx.x;
+            T yv = lane < k ? y[lane] : T(0);
+            yv = trsv_upper_wave(k, Hs, yv, lane);
+            ys[lane] = yv;  // (s itself is left as is: every workgroup reads it)
+        }
+    } else {
+        for (int j = threadIdx.x; j < k; j += kBlock) ys[j] = y[j];
+    }
     __syncthreads();
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         double t = 0.0;
@@ -1198,11 +1230,17 @@ int mpg_arnoldi_update(mpg_arnoldi_t a, int k) {
     int st = dispatch(a->combo, [&](auto t, auto x, auto, auto) {
         using T = decltype(t);
         using X = decltype(x);
-        k_trsv_upper<T><<<1, kBlock, 0, a->ctx->stream>>>(k, a->d.m + 1, static_cast<const T*>(a->H),
-                                                          static_cast<T*>(a->s()));
-        k_update_x<T, X><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->V), a->ld, k,
-                                                                     static_cast<const T*>(a->s()),
-                                                                     static_cast<X*>(a->d.x));
+        if (k <= kWave) {
+            k_update_x<T, X, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, static_cast<const T*>(a->s()),
+                static_cast<const T*>(a->H), a->d.m + 1, static_cast<X*>(a->d.x));
+        } else {
+            k_trsv_upper<T><<<1, kBlock, 0, a->ctx->stream>>>(k, a->d.m + 1, static_cast<const T*>(a->H),
+                                                              static_cast<T*>(a->s()));
+            k_update_x<T, X, false><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, static_cast<const T*>(a->s()), nullptr, 0,
+                static_cast<X*>(a->d.x));
+        }
         return MPG_OK;
     });
     if (st) return st;
