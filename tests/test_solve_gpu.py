@@ -140,3 +140,21 @@ def test_aborts_at_max_restarts(mpg, engine):
                     max_restarts=3)
     assert got.status == "aborted"
     assert got.total_iters == 90 and len(got.step_res) == 90 and len(got.cyc_r_norm) == 4
+
+
+@pytest.mark.parametrize("engine", ["surface", "fused"])
+@pytest.mark.parametrize("n", [1, 2, 3, 65])
+def test_tiny_systems_match_oracle(mpg, oracle, engine, n):
+    """Restart length above n: the Krylov space is exhausted, h_{k+1,k}
+    collapses to (near) zero and, with no breakdown guard in the reference,
+    the cycle can turn non-finite. The GPU path must take the same restart
+    decisions as the oracle on the same inputs."""
+    A = mpg.gen_band(n, 1, 1, seed=5)
+    xt = mpg.rand_vect(n, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode="baseline", orth="cgs", prec="identity", rlen=30, tol=1e-12, max_restarts=5)
+    ref = oracle.solve(mpg, A, b, xt, **opts)
+    got = mpg.solve(A, b, xt, engine=engine, **opts)
+    assert got.status == ref.status
+    assert got.restarts == ref.restarts and got.total_iters == ref.total_iters
+    assert np.array_equal(np.isfinite(got.step_res), np.isfinite(ref.step_res))
