@@ -196,10 +196,11 @@ __device__ __forceinline__ double sum_partials(const double* __restrict__ p, int
     return block_sum<BS>(v0 + v1, scratch);
 }
 
-__global__ __launch_bounds__(1024) void k_reduce_partials(int G, const double* __restrict__ partial,
-                                                          double* __restrict__ sums) {
-    __shared__ double scratch[1024 / kWave];
-    const double s = sum_partials<1024>(partial + (size_t)blockIdx.x * G, G, scratch);
+template <int BS>
+__global__ __launch_bounds__(BS) void k_reduce_partials(int G, const double* __restrict__ partial,
+                                                        double* __restrict__ sums) {
+    __shared__ double scratch[BS / kWave];
+    const double s = sum_partials<BS>(partial + (size_t)blockIdx.x * G, G, scratch);
     if (threadIdx.x == 0) sums[blockIdx.x] = s;
 }
 
@@ -1050,7 +1051,10 @@ int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a) {
 
 int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols) {
     if (!a || ncols < 1 || ncols > a->d.m + 4) return MPG_ERR_ARG;
-    k_reduce_partials<<<ncols, 1024, 0, a->ctx->stream>>>(a->last_G, a->last_part, a->sums);
+    // one column per workgroup: 256 threads when the producer left <= 512
+    // partials per column (one or two loads per thread), else 1024
+    if (a->last_G <= 2 * kBlock) k_reduce_partials<kBlock><<<ncols, kBlock, 0, a->ctx->stream>>>(a->last_G, a->last_part, a->sums);
+    else k_reduce_partials<1024><<<ncols, 1024, 0, a->ctx->stream>>>(a->last_G, a->last_part, a->sums);
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
 }
