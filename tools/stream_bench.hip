@@ -69,6 +69,37 @@ __global__ __launch_bounds__(256) void k_dots(int n, const float* __restrict__ V
     if ((threadIdx.x & 63) == 0) part[blockIdx.x * 4 + threadIdx.x / 64] = s;
 }
 
+// panel dots variant: BS threads, R float4 row groups per lane per iteration
+template <int NC, int BS, int R>
+__global__ __launch_bounds__(BS) void k_dots2(int n, const float* __restrict__ V, size_t ld, int nc,
+                                              const float* __restrict__ w, double* __restrict__ part) {
+    double acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+    for (int i = 4 * R * (blockIdx.x * BS) + 4 * threadIdx.x; i < n; i += 4 * R * gridDim.x * BS) {
+        float4 wv[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) wv[r] = *reinterpret_cast<const float4*>(w + i + 4 * BS * r);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c < nc) {
+                float4 v[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[r] = *reinterpret_cast<const float4*>(V + c * ld + i + 4 * BS * r);
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    acc[c] += (double)v[r].x * wv[r].x + (double)v[r].y * wv[r].y + (double)v[r].z * wv[r].z +
+                              (double)v[r].w * wv[r].w;
+            }
+        }
+    }
+    double s = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) s += acc[c];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) part[blockIdx.x * (BS / 64) + threadIdx.x / 64] = s;
+}
+
 // PMC calibration: read `bytes` with W-byte loads per lane (k_calib_4/8/16),
 // so FETCH_SIZE per dispatch can be compared with a known byte count
 template <class V>
@@ -133,6 +164,19 @@ int main() {
         });
         std::printf("  G=%5d           %7.2f us  %7.0f GB/s\n", G, ms * 1e3, (bytes + ld * 4) / (ms * 1e-3) / 1e9);
     }
+    std::printf("panel dots variants (BS threads, R row groups of 4 per lane)\n");
+    auto dv = [&](auto kern, int G, int BS, const char* tag) {
+        float ms = time_it(reps, [&](int r) { kern<<<G, BS>>>(n, bufs[r % kCopies], ld, cols, ws[r % kCopies], part); });
+        std::printf("  G=%5d %-12s %7.2f us  %7.0f GB/s\n", G, tag, ms * 1e3, (bytes + ld * 4) / (ms * 1e-3) / 1e9);
+    };
+    dv(k_dots2<32, 1024, 1>, 256, 1024, "bs1024 r1");
+    dv(k_dots2<32, 1024, 2>, 128, 1024, "bs1024 r2");
+    dv(k_dots2<32, 512, 1>, 512, 512, "bs512 r1");
+    dv(k_dots2<32, 512, 2>, 256, 512, "bs512 r2");
+    dv(k_dots2<32, 512, 2>, 512, 512, "bs512 r2");
+    dv(k_dots2<32, 256, 2>, 512, 256, "bs256 r2");
+    dv(k_dots2<32, 256, 2>, 1024, 256, "bs256 r2");
+    dv(k_dots2<32, 256, 4>, 512, 256, "bs256 r4");
     std::printf("same, one copy only (MALL-resident after the first pass)\n");
     for (int G : {1024}) {
         float ms = time_it(reps, [&](int) { k_dots<32><<<G, 256>>>(n, bufs[0], ld, cols, ws[0], part); });
