@@ -21,6 +21,14 @@
  * communicator. mpg_solve_loopback runs P ranks as threads sharing one GPU
  * (device-to-device copies instead of RCCL) to test the partitioned path on
  * a single device.
+ *
+ * Reference correspondence (what each exchange distributes): the halo
+ * exchange feeds the Arnoldi spmv (gmres.cpp:213, kernels_cuda.cpp:576-614)
+ * and the residual spmv (gmres.cpp:174); the fp64 all-reduces carry the
+ * CGS/CGSR gemv^T panels (Orthogonalization.hpp:83-87, 109-136), the MGS
+ * dots (Orthogonalization.hpp:99-105), nrm2 (Orthogonalization.hpp:56) and
+ * the restart norms (gmres.cpp:168-180); the Jacobi ||A||_inf boost
+ * (types.hpp:404-430) is an all-reduce max.
  */
 #ifndef MPGMRES_DIST_H
 #define MPGMRES_DIST_H

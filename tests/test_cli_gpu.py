@@ -36,3 +36,13 @@ def test_cli_rejects_like_the_reference(mpg):
     assert r.returncode == 1 and "Unknown Orthogonalization" in r.stdout
     r = subprocess.run([str(mpg.CLI), "--rlen", "10"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "No value suplied for A" in r.stdout
+
+
+def test_cli_default_preconditioner_is_ilu(mpg):
+    """With no --prec the reference CLI uses ILU(0) (gmres_perf_test.cpp:322);
+    the run converges and prints the harness lines."""
+    out = subprocess.run([str(mpg.CLI), "--matrix", "laplace:10", "--rlen", "30", "--mode", "mixed", "--tol", "1e-9",
+                          "--gpu"], capture_output=True, text=True, timeout=120, check=True).stdout
+    m = SUMMARY.search(out)
+    assert m, out
+    assert float(m.group(1)) <= 1e-9
