@@ -22,8 +22,12 @@ def per_kernel(d, counter):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
-            m = re.search(r"(k_\w+)", r["Kernel_Name"])
+            m = re.search(r"(k_\w+)(<[^(]*>)?", r["Kernel_Name"])
             name = m.group(1) if m else r["Kernel_Name"][:40]
+            # the Arnoldi SpMVs come in a plain and a Givens-folded (FOLD =
+            # last template argument true) instantiation: keep them apart
+            if m and name in ("k_step_sell", "k_step_spmv") and m.group(2) and m.group(2).endswith("true>"):
+                name += ":fold"
             vals[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
