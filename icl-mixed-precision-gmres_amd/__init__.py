@@ -75,6 +75,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_solve.restype = C.c_int
     lib.mpg_gen_band.argtypes = [_I64, _I32, _I32, C.c_uint64, _I64, _I64, C.POINTER(HostCsr)]
     lib.mpg_gen_laplace3d.argtypes = [_I32, _I32, _I32, C.POINTER(HostCsr)]
+    lib.mpg_gen_stencil27.argtypes = [_I32, _I32, _I32, _I32, C.c_uint64, C.POINTER(HostCsr)]
     lib.mpg_load_mtx.argtypes = [C.c_char_p, C.POINTER(HostCsr), C.c_char_p, C.c_int]
     lib.mpg_load_mtx_vector.argtypes = [C.c_char_p, _I32, C.POINTER(C.c_double), _I64, C.c_char_p, C.c_int]
     lib.mpg_rand_vect.argtypes = [_I64, C.c_uint32, C.POINTER(C.c_double)]
@@ -240,6 +241,16 @@ def gen_laplace3d(nx: int, ny: Optional[int] = None, nz: Optional[int] = None) -
     st = host_lib().mpg_gen_laplace3d(nx, ny or nx, nz or nx, C.byref(h))
     if st:
         raise ValueError(f"mpg_gen_laplace3d failed ({st})")
+    return _take_csr(h)
+
+
+def gen_stencil27(nx: int, dof: int = 3, seed: int = 11) -> Csr:
+    """27-point 3-D stencil, `dof` unknowns per node (the Queen_4147 stand-in
+    at nx = 111, dof = 3)."""
+    h = HostCsr()
+    st = host_lib().mpg_gen_stencil27(nx, nx, nx, dof, seed, C.byref(h))
+    if st:
+        raise ValueError(f"mpg_gen_stencil27 failed ({st})")
     return _take_csr(h)
 
 

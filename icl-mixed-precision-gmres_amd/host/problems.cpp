@@ -183,6 +183,51 @@ int mpg_gen_laplace3d(int32_t nx, int32_t ny, int32_t nz, mpg_host_csr* out) {
     return emit(out, (int32_t)n, (int32_t)n, rp, ci, va);
 }
 
+int mpg_gen_stencil27(int32_t nx, int32_t ny, int32_t nz, int32_t dof, uint64_t seed, mpg_host_csr* out) {
+    if (!out || nx <= 0 || ny <= 0 || nz <= 0 || dof <= 0 || dof > 8) return -2;
+    const int64_t nodes = (int64_t)nx * ny * nz, n = nodes * dof;
+    if (n > INT32_MAX || n * 27 * dof > INT32_MAX) return -2;
+    std::vector<int32_t> rp((size_t)n + 1), ci;
+    std::vector<double> va;
+    ci.reserve((size_t)n * 27 * dof);
+    va.reserve((size_t)n * 27 * dof);
+    for (int32_t z = 0; z < nz; ++z)
+        for (int32_t y = 0; y < ny; ++y)
+            for (int32_t x = 0; x < nx; ++x) {
+                const int64_t node = x + (int64_t)nx * (y + (int64_t)ny * z);
+                for (int32_t d = 0; d < dof; ++d) {
+                    const int64_t i = node * dof + d;
+                    rp[(size_t)i] = (int32_t)ci.size();
+                    double offsum = 0.0;
+                    size_t diag_slot = 0;
+                    // neighbours in lexicographic order (z, y, x), so columns come sorted
+                    for (int dz = -1; dz <= 1; ++dz)
+                        for (int dy = -1; dy <= 1; ++dy)
+                            for (int dx = -1; dx <= 1; ++dx) {
+                                const int32_t X = x + dx, Y = y + dy, Z = z + dz;
+                                if (X < 0 || X >= nx || Y < 0 || Y >= ny || Z < 0 || Z >= nz) continue;
+                                const int64_t nb = X + (int64_t)nx * (Y + (int64_t)ny * Z);
+                                for (int32_t e = 0; e < dof; ++e) {
+                                    const int64_t c = nb * dof + e;
+                                    ci.push_back((int32_t)c);
+                                    if (c == i) {
+                                        diag_slot = va.size();
+                                        va.push_back(0.0);
+                                    } else {  // symmetric: keyed on the unordered pair
+                                        const int64_t a = std::min(i, c), b = std::max(i, c);
+                                        const double v = -unit_double(seed ^ (uint64_t)b, a, 0);
+                                        offsum += std::fabs(v);
+                                        va.push_back(v);
+                                    }
+                                }
+                            }
+                    va[diag_slot] = 1.0 + offsum;
+                }
+            }
+    rp[(size_t)n] = (int32_t)ci.size();
+    return emit(out, (int32_t)n, (int32_t)n, rp, ci, va);
+}
+
 int mpg_load_mtx(const char* path, mpg_host_csr* out, char* err, int errlen) {
     if (!out || !path) return -2;
     FILE* f = std::fopen(path, "r");

@@ -38,6 +38,14 @@ int mpg_gen_band(int64_t n, int32_t lo, int32_t hi, uint64_t seed, int64_t row_b
  * (x fastest), diagonal 6, off-diagonals -1 (100^3: n = 1e6, nnz = 6,940,000). */
 int mpg_gen_laplace3d(int32_t nx, int32_t ny, int32_t nz, mpg_host_csr* out);
 
+/* 27-point 3-D stencil with `dof` unknowns per node (every unknown of a
+ * node coupled to every unknown of its <= 27 neighbours), lexicographic
+ * node order, symmetric off-diagonals -u (u from a counter-based hash of
+ * the unordered pair), diagonal 1 + sum|off| (SPD, diagonally dominant).
+ * The Queen_4147 stand-in of SURVEY §8(d): 111^3 nodes x 3 dof = 4,102,893
+ * rows, ~3.2e8 nnz. */
+int mpg_gen_stencil27(int32_t nx, int32_t ny, int32_t nz, int32_t dof, uint64_t seed, mpg_host_csr* out);
+
 /* Matrix Market coordinate real|integer, general|symmetric, loaded as
  * LoadMatrix.hpp:17-154 does: an explicit diagonal slot in every row (0 if
  * the file has none; a diagonal entry in the file overwrites it), symmetric

@@ -72,3 +72,22 @@ def test_host_spmv_matches_scipy(mpg):
     A = mpg.gen_band(20_000, 5, 4, seed=1)
     x = mpg.rand_vect(A.nrows, 42)
     assert np.allclose(mpg.host_spmv(A, x), A.to_scipy() @ x, rtol=1e-14, atol=1e-14)
+
+
+def test_stencil27_counts_symmetry_dominance(mpg):
+    """The Queen_4147 stand-in generator (27-point stencil, 3 dof/node)."""
+    nx, dof = 7, 3
+    A = mpg.gen_stencil27(nx, dof)
+    assert A.nrows == nx**3 * dof
+    # node-pair couplings: each dimension contributes (3 nx - 2) neighbour pairs per line
+    assert A.nnz == (3 * nx - 2) ** 3 * dof * dof
+    S = A.to_scipy()
+    assert abs(S - S.T).max() == 0
+    d = S.diagonal()
+    off = np.asarray(abs(S).sum(axis=1)).ravel() - d
+    assert np.allclose(d, 1 + off, rtol=1e-15)
+    for i in (0, 17, A.nrows - 1):
+        c = A.col[A.rowptr[i]:A.rowptr[i + 1]]
+        assert np.all(np.diff(c) > 0)
+    # Queen_4147 scale: 111^3 x 3 = 4,102,893 rows
+    assert 111**3 * 3 == 4_102_893

@@ -5,11 +5,13 @@ tol = 0 (fixed work), the Arnoldi SpMV's achieved algorithmic GB/s
 solve. Synthetic inputs:
   C2  LAP-1M   7-point 3-D Laplacian 100^3, fp64 GMRES(30) (baseline mode)
   C3  LAP-1M   fp32 Arnoldi + fp64 residual/update (mixed mode)
+  C4  Queen_4147 stand-in: 27-point 3-D stencil, 3 dof/node, 111^3 nodes
+      (n = 4.1M, 3.26e8 nnz), fp32 Arnoldi (mixed mode)
   C5  BAND-100M at one GPU: n = 1e7, fp16 Arnoldi values (mixed-half)
       (BASELINE quotes it on 8 GPUs; here one GPU holds the whole matrix)
 Prints one JSON line per case; `--out FILE` also writes them to FILE.
 
-usage: python tools/bench_configs.py [--cycles 10] [--cpu-cycles 2] [--out profiles/r01_configs.jsonl]
+usage: python tools/bench_configs.py [--cycles 10] [--cpu-cycles 2] [--only C4] [--out profiles/r01_configs.jsonl]
 """
 import argparse
 import json
@@ -28,6 +30,7 @@ CASES = [
     dict(name="C3 LAP-1M mixed CGS", matrix=("laplace", 100), mode="mixed", orth="cgs"),
     dict(name="C3 LAP-1M mixed MGS", matrix=("laplace", 100), mode="mixed", orth="mgs"),
     dict(name="C3 LAP-1M mixed CGSR", matrix=("laplace", 100), mode="mixed", orth="cgsr"),
+    dict(name="C4 Queen-stand-in mixed CGS", matrix=("stencil27", 111), mode="mixed", orth="cgs"),
     dict(name="C5 BAND-100M mixed-half CGS (1 GPU)", matrix=("band", 10_000_000), mode="mixed-half", orth="cgs"),
 ]
 
@@ -37,6 +40,7 @@ def main():
     ap.add_argument("--cycles", type=int, default=10)
     ap.add_argument("--cpu-cycles", type=int, default=2)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default=None, help="comma-separated case prefixes, e.g. C4,C5")
     args = ap.parse_args()
     from __graft_entry__ import _load
 
@@ -44,10 +48,15 @@ def main():
     from oracle import binding
 
     lines = []
+    only = tuple(args.only.split(",")) if args.only else None
+    gens = {"laplace": mpg.gen_laplace3d, "stencil27": lambda s: mpg.gen_stencil27(s, 3),
+            "band": lambda s: mpg.gen_band(s, 5, 4, seed=7)}
     for case in CASES:
+        if only and not case["name"].startswith(only):
+            continue
         kind, size = case["matrix"]
         t0 = time.time()
-        A = mpg.gen_laplace3d(size) if kind == "laplace" else mpg.gen_band(size, 5, 4, seed=7)
+        A = gens[kind](size)
         xt = mpg.rand_vect(A.nrows, 42)
         b = mpg.host_spmv(A, xt)
         opts = dict(mode=case["mode"], orth=case["orth"], prec="identity", rlen=30, tol=0.0,
@@ -66,7 +75,7 @@ def main():
         layout = eng.spmv_layout()
         eng.close()
         cpu = None
-        if kind == "laplace":  # (the 100M-nnz CPU sample would take minutes)
+        if kind == "laplace":  # (the 1e8-nnz-scale CPU samples would take minutes)
             r = binding.solve(mpg, A, b, xt, **dict(opts, max_restarts=args.cpu_cycles))
             cpu = {"it_s": round(r.total_iters / r.gmres_seconds, 2),
                    "threads": binding.lib().oracle_max_threads(), "backend": binding.backend()}
