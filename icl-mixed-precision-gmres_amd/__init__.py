@@ -22,7 +22,8 @@ from typing import Optional
 
 import numpy as np
 
-from ._abi import ENGINES, MODES, ORTHS, PRECS, SPMV_FORMATS, STATUS, HostCsr, SolveArgs, SolveResult
+from ._abi import (ENGINES, MODES, ORTHS, PRECS, SPMV_FORMATS, STATUS, CondestResult, HostCsr, SolveArgs, SolveResult,
+                   condest_args, condest_dict)
 
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
@@ -75,6 +76,8 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_solve.restype = C.c_int
     lib.mpg_gen_band.argtypes = [_I64, _I32, _I32, C.c_uint64, _I64, _I64, C.POINTER(HostCsr)]
     lib.mpg_gen_laplace3d.argtypes = [_I32, _I32, _I32, C.POINTER(HostCsr)]
+    lib.mpg_gen_spec.argtypes = [C.c_char_p, C.POINTER(HostCsr), C.c_char_p, C.c_int]
+    lib.mpg_condest.restype = C.c_int
     lib.mpg_gen_stencil27.argtypes = [_I32, _I32, _I32, _I32, C.c_uint64, C.POINTER(HostCsr)]
     lib.mpg_load_mtx.argtypes = [C.c_char_p, C.POINTER(HostCsr), C.c_char_p, C.c_int]
     lib.mpg_load_mtx_vector.argtypes = [C.c_char_p, _I32, C.POINTER(C.c_double), _I64, C.c_char_p, C.c_int]
@@ -124,6 +127,9 @@ _HIP_DECLS = {
     "mpg_memcpy_h2d": ([_P, _P, _P, C.c_size_t], C.c_int),
     "mpg_memcpy_d2h": ([_P, _P, _P, C.c_size_t], C.c_int),
     "mpg_csr_create": ([_P, _I32, _I32, _I64, _P, _P, _P, C.POINTER(_P)], C.c_int),
+    "mpg_csr_transpose": ([_P, _I32, _I32, _I64, _P, _P, _P, _P, _P], C.c_int),
+    "mpg_gather_b32": ([_P, _I64, _P, _P, _P], C.c_int),
+    "mpg_gather_b64": ([_P, _I64, _P, _P, _P], C.c_int),
     "mpg_csr_destroy": ([_P], C.c_int),
     "mpg_csr_num_blocks": ([_P], C.c_int),
 }
@@ -252,6 +258,25 @@ def gen_stencil27(nx: int, dof: int = 3, seed: int = 11) -> Csr:
     if st:
         raise ValueError(f"mpg_gen_stencil27 failed ({st})")
     return _take_csr(h)
+
+
+def gen_spec(spec: str) -> Csr:
+    """A generator by its CLI spec (mpg_gen_spec: band:..., laplace:..., stencil27:...)."""
+    h = HostCsr()
+    err = C.create_string_buffer(256)
+    if host_lib().mpg_gen_spec(spec.encode(), C.byref(h), err, 256):
+        raise ValueError(err.value.decode())
+    return _take_csr(h)
+
+
+def condest(A: Csr, rand_seed: int = 42, max_iters: int = 100000, verbose: bool = False, device: int = 0) -> dict:
+    """Condition-number estimate of square A on the GPU (include/mpgmres/condest.h;
+    the reference's condest.cpp:34-150): sigma_max, sigma_min, cond, iters, ..."""
+    a = condest_args(A, rand_seed, max_iters, verbose, device)
+    r = CondestResult()
+    if host_lib().mpg_condest(C.byref(a), C.byref(r)):
+        raise RuntimeError(f"mpg_condest failed: {r.message.decode()}")
+    return condest_dict(r)
 
 
 def load_mtx(path: str) -> Csr:

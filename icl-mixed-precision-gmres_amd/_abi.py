@@ -73,3 +73,51 @@ class HostCsr(C.Structure):
         ("col", C.POINTER(C.c_int32)),
         ("val", C.POINTER(C.c_double)),
     ]
+
+
+class CondestArgs(C.Structure):  # include/mpgmres/condest.h
+    _fields_ = [
+        ("n", C.c_int32),
+        ("nnz", C.c_int64),
+        ("rowptr", C.POINTER(C.c_int32)),
+        ("col", C.POINTER(C.c_int32)),
+        ("val", C.POINTER(C.c_double)),
+        ("rand_seed", C.c_int32),
+        ("max_iters", C.c_int64),
+        ("verbose", C.c_int32),
+        ("device", C.c_int32),
+        ("threads", C.c_int32),
+    ]
+
+
+class CondestResult(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32),
+        ("sigma_max", C.c_double),
+        ("sigma_min", C.c_double),
+        ("cond", C.c_double),
+        ("power_iters", C.c_int64),
+        ("iters", C.c_int64),
+        ("finish_t", C.c_int64),
+        ("stop_reason", C.c_int32),
+        ("seconds", C.c_double),
+        ("message", C.c_char * 256),
+    ]
+
+
+def condest_args(A, rand_seed: int = 42, max_iters: int = 100000, verbose: bool = False, device: int = 0,
+                 threads: int = 0) -> CondestArgs:
+    """Arguments for mpg_condest / oracle_condest; keeps references to A's
+    arrays on the struct so they outlive the call."""
+    a = CondestArgs()
+    a.n, a.nnz = A.nrows, A.nnz
+    a.rowptr = A.rowptr.ctypes.data_as(C.POINTER(C.c_int32))
+    a.col = A.col.ctypes.data_as(C.POINTER(C.c_int32))
+    a.val = A.val.ctypes.data_as(C.POINTER(C.c_double))
+    a.rand_seed, a.max_iters, a.verbose, a.device, a.threads = rand_seed, max_iters, int(verbose), device, threads
+    a._keep = A
+    return a
+
+
+def condest_dict(r: CondestResult) -> dict:
+    return {k: getattr(r, k) for k, _ in CondestResult._fields_ if k != "message"}

@@ -5,8 +5,9 @@
 // --tol --max-restarts --rand --mode {mixed,baseline,single-prec,single}
 // --orth {cgs,mgs,cgsr} --prec {ilu,identity,jacobi,ilu_jacobi}
 // --jacobi-steps --gpu (accepted; this build always runs on the GPU).
-// Additions: --matrix band:N[:LO:HI[:SEED]] | laplace:NX[:NY:NZ] (synthetic
-// input instead of --Apath), --mode mixed-half, --engine {fused,surface},
+// Additions: --matrix band:N[:LO:HI[:SEED]] | laplace:NX[:NY:NZ] |
+// stencil27:NX[:DOF[:SEED]] (synthetic input instead of --Apath,
+// mpg_gen_spec), --mode mixed-half, --engine {fused,surface},
 // --device D.
 #include <cmath>
 #include <cstdio>
@@ -25,34 +26,6 @@ double host_nrm2(const double* v, int64_t n) {
     double s = 0;
     for (int64_t i = 0; i < n; ++i) s += v[i] * v[i];
     return std::sqrt(s);
-}
-
-bool parse_synthetic(const std::string& spec, mpg_host_csr* A, std::string& err) {
-    std::vector<std::string> f;
-    size_t p = 0;
-    while (true) {
-        size_t q = spec.find(':', p);
-        f.push_back(spec.substr(p, q == std::string::npos ? std::string::npos : q - p));
-        if (q == std::string::npos) break;
-        p = q + 1;
-    }
-    if (f[0] == "band" && f.size() >= 2) {
-        long long n = std::atoll(f[1].c_str());
-        int lo = f.size() > 2 ? std::atoi(f[2].c_str()) : 5;
-        int hi = f.size() > 3 ? std::atoi(f[3].c_str()) : 4;
-        unsigned long long seed = f.size() > 4 ? std::strtoull(f[4].c_str(), nullptr, 10) : 7;
-        if (mpg_gen_band(n, lo, hi, seed, 0, n, A) != 0) { err = "bad band spec"; return false; }
-        return true;
-    }
-    if (f[0] == "laplace" && f.size() >= 2) {
-        int nx = std::atoi(f[1].c_str());
-        int ny = f.size() > 2 ? std::atoi(f[2].c_str()) : nx;
-        int nz = f.size() > 3 ? std::atoi(f[3].c_str()) : nx;
-        if (mpg_gen_laplace3d(nx, ny, nz, A) != 0) { err = "bad laplace spec"; return false; }
-        return true;
-    }
-    err = "unknown --matrix spec (band:N[:LO:HI[:SEED]] or laplace:NX[:NY:NZ])";
-    return false;
 }
 
 }  // namespace
@@ -148,8 +121,8 @@ int main(int argc, char* argv[]) {
             return 1;
         }
     } else {
-        std::string e;
-        if (!parse_synthetic(synthetic, &A, e)) {
+        char e[256];
+        if (mpg_gen_spec(synthetic.c_str(), &A, e, sizeof e) != 0) {
             std::cerr << e << std::endl;
             return 1;
         }

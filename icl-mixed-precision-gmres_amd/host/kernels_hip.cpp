@@ -53,6 +53,39 @@ mpg_ctx_t current_ctx() {
 ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) { tl_ctx = ctx; }
 ScopedContext::~ScopedContext() { tl_ctx = prev_; }
 
+void build_transpose(CsrStructure& s) {
+    if (s.transposed) return;
+    mpg_ctx_t C = current_ctx();
+    auto t = std::make_shared<CsrStructure>();
+    t->m = s.n;
+    t->n = s.m;
+    t->nnz = s.nnz;
+    const size_t ib = sizeof(int) * ((size_t)s.n + 1), jb = sizeof(int) * (size_t)s.nnz;
+    t->row_map = device_alloc<Hip>(ib);
+    t->inds = device_alloc<Hip>(jb ? jb : sizeof(int));
+    auto perm = device_alloc<Hip>(jb ? jb : sizeof(int));
+    check(mpg_csr_transpose(C, s.m, s.n, s.nnz, static_cast<const int32_t*>(s.row_map.get()),
+                            static_cast<const int32_t*>(s.inds.get()), static_cast<int32_t*>(t->row_map.get()),
+                            static_cast<int32_t*>(t->inds.get()), static_cast<int32_t*>(perm.get())),
+          "mpg_csr_transpose", C);
+    std::vector<int32_t> rp_host((size_t)s.n + 1);
+    Hip::to_host(rp_host.data(), t->row_map.get(), ib);
+    mpg_csr_t csr = nullptr;
+    check(mpg_csr_create(C, t->m, t->n, t->nnz, rp_host.data(), static_cast<const int32_t*>(t->row_map.get()),
+                         static_cast<const int32_t*>(t->inds.get()), &csr),
+          "mpg_csr_create (transpose)", C);
+    t->csr = std::shared_ptr<mpg_csr>(csr, [](mpg_csr* p) { mpg_csr_destroy(p); });
+    s.perm = std::move(perm);
+    s.transposed = std::move(t);
+}
+
+void gather_entries(const CsrStructure& s, const void* vals, void* out, size_t elem_bytes) {
+    mpg_ctx_t C = current_ctx();
+    const auto* perm = static_cast<const int32_t*>(s.perm.get());
+    check(elem_bytes == 8 ? mpg_gather_b64(C, s.nnz, perm, vals, out) : mpg_gather_b32(C, s.nnz, perm, vals, out),
+          "gather (transpose values)", C);
+}
+
 }  // namespace mpg
 
 using mpg::check;
@@ -277,15 +310,20 @@ template <> void gdmv<float, Hip>(float alpha, Vect<float, Hip> d, Vect<float, H
 }
 
 // ---------------- sparse ----------------
+// A transposed matrix runs the same CSR-adaptive kernel on A^T's own CSR
+// (SparseMatrix::set_transpose); nrows()/ncols() stay A's, as in the
+// reference, so the extents swap here.
 template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Vect<double, Hip> x, double beta,
                                    Vect<double, Hip> y) {
-    assert((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n());
-    check(mpg_csr_spmv_f64(C, A.csr(), alpha, A.vals_data(), x.data(), beta, y.data()), "spmv");
+    assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
+                             : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
+    check(mpg_csr_spmv_f64(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
 }
 template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<float, Hip> x, float beta,
                                   Vect<float, Hip> y) {
-    assert((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n());
-    check(mpg_csr_spmv_f32(C, A.csr(), alpha, A.vals_data(), x.data(), beta, y.data()), "spmv");
+    assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
+                             : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
+    check(mpg_csr_spmv_f32(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
 }
 template <> void jacobi_diag<double, Hip>(SparseMatrix<double, Hip> A, Vect<double, Hip> d) {
     check(mpg_jacobi_setup_f64(C, A.csr(), A.vals_data(), d.data()), "jacobi setup");

@@ -228,6 +228,41 @@ int mpg_gen_stencil27(int32_t nx, int32_t ny, int32_t nz, int32_t dof, uint64_t 
     return emit(out, (int32_t)n, (int32_t)n, rp, ci, va);
 }
 
+int mpg_gen_spec(const char* spec, mpg_host_csr* out, char* err, int errlen) {
+    auto fail = [&](const char* what) {
+        if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", what);
+        return -2;
+    };
+    if (!spec || !out) return fail("null argument");
+    std::vector<std::string> f;
+    std::string s(spec);
+    for (size_t p = 0;;) {
+        const size_t q = s.find(':', p);
+        f.push_back(s.substr(p, q == std::string::npos ? std::string::npos : q - p));
+        if (q == std::string::npos) break;
+        p = q + 1;
+    }
+    auto num = [&](size_t i, long long def) { return f.size() > i ? std::atoll(f[i].c_str()) : def; };
+    if (f[0] == "band" && f.size() >= 2) {
+        const long long n = num(1, 0);
+        if (mpg_gen_band(n, (int)num(2, 5), (int)num(3, 4), (uint64_t)num(4, 7), 0, n, out) != 0)
+            return fail("bad band spec");
+        return 0;
+    }
+    if (f[0] == "laplace" && f.size() >= 2) {
+        const int nx = (int)num(1, 0);
+        if (mpg_gen_laplace3d(nx, (int)num(2, nx), (int)num(3, nx), out) != 0) return fail("bad laplace spec");
+        return 0;
+    }
+    if (f[0] == "stencil27" && f.size() >= 2) {
+        const int nx = (int)num(1, 0);
+        if (mpg_gen_stencil27(nx, nx, nx, (int)num(2, 3), (uint64_t)num(3, 11), out) != 0)
+            return fail("bad stencil27 spec");
+        return 0;
+    }
+    return fail("unknown --matrix spec (band:N[:LO:HI[:SEED]], laplace:NX[:NY:NZ] or stencil27:NX[:DOF[:SEED]])");
+}
+
 int mpg_load_mtx(const char* path, mpg_host_csr* out, char* err, int errlen) {
     if (!out || !path) return -2;
     FILE* f = std::fopen(path, "r");

@@ -42,7 +42,16 @@ struct CsrStructure {
     int64_t nnz = 0;
     std::shared_ptr<void> row_map, inds;  // device int32
     std::shared_ptr<mpg_csr> csr;        // analysed CSR-adaptive schedule
+    // A^T as its own CSR (mpg_csr_transpose), built on the first
+    // set_transpose(true) of any SparseMatrix sharing this structure
+    std::shared_ptr<CsrStructure> transposed;
+    std::shared_ptr<void> perm;  // device int32[nnz]: source entry of each A^T entry
 };
+
+// Builds s.transposed / s.perm once (synchronises).
+void build_transpose(CsrStructure& s);
+// out[t] = vals[perm[t]] (the values of A^T in its CSR order)
+void gather_entries(const CsrStructure& s, const void* vals, void* out, size_t elem_bytes);
 
 }  // namespace mpg
 
@@ -92,12 +101,32 @@ public:
     }
 
     // Precision-converting copy: shares the structure, casts the values on
-    // the device (types_mkl.hpp:46-62, types_cuda.hpp:82-101). Implicit, as
-    // in the reference — DoBaselineProblem relies on it (§0.1-2 of SURVEY).
+    // the device, keeps the transpose flag (types_mkl.hpp:46-62,
+    // types_cuda.hpp:82-101). Implicit, as in the reference —
+    // DoBaselineProblem relies on it (§0.1-2 of SURVEY).
     template <class OldType>
     SparseMatrix(SparseMatrix<OldType, Hip> old) : s_(old.s_), vals_((size_t)old.s_->nnz) {
         copy(old.vals_, vals_);
+        set_transpose(old.trans_);
     }
+
+    // spmv then applies A^T (types_cuda.hpp:145-151; cusparse?csrmv with
+    // CUSPARSE_OPERATION_TRANSPOSE, kernels_cuda.cpp:588-596). Copies share
+    // the values, as the reference's do (condest.cpp:49-50: A_trans = A),
+    // so the values are taken in A^T's order here, once; the structure of
+    // A^T is built on first use and shared by every precision.
+    void set_transpose(bool t) {
+        trans_ = t;
+        if (t && tvals_.n() != (size_t)s_->nnz) {
+            mpg::build_transpose(*s_);
+            tvals_ = Vect<Type, Hip>((size_t)s_->nnz);
+            if (s_->nnz) mpg::gather_entries(*s_, vals_.data(), tvals_.data(), sizeof(Type));
+        }
+    }
+    bool is_transposed() const { return trans_; }
+    // the CSR and values spmv reads (A's, or A^T's when transposed)
+    mpg_csr_t applied_csr() const { return trans_ ? s_->transposed->csr.get() : csr(); }
+    Type* applied_vals() const { return trans_ ? tvals_.data() : vals_.data(); }
 
     const std::shared_ptr<mpg::CsrStructure>& structure() const { return s_; }
     int nrows() const { return s_->m; }
@@ -108,7 +137,10 @@ public:
     Type* vals_data() const { return vals_.data(); }
     mpg_csr_t csr() const { return s_->csr.get(); }
     Vect<Type, Hip> vals_vect() const { return vals_; }
-    bool is_transposed() const { return false; }
+
+private:
+    bool trans_ = false;
+    Vect<Type, Hip> tvals_;  // values in A^T's CSR order (set_transpose)
 };
 
 // ILU(0) factors on the device (types_mkl.hpp:110-190, types_cuda.hpp:155-240):

@@ -171,6 +171,16 @@ int mpg_csr_spmv_f32(mpg_ctx_t ctx, mpg_csr_t A, float alpha, const float* vals,
 int mpg_csr_spmv_f16f32(mpg_ctx_t ctx, mpg_csr_t A, float alpha, const uint16_t* vals_half,
                         const float* x, float beta, float* y);
 
+/* A^T as its own CSR (SparseMatrix::set_transpose, types_cuda.hpp:145-151;
+ * cusparse?csrmv TRANSPOSE, kernels_cuda.cpp:588-596; condest.cpp:49-50).
+ * Device outputs: rowptr_t[cols+1]; col_t[nnz] = the source rows; perm[nnz]
+ * = the source entry of each transposed entry (values of any precision:
+ * mpg_gather_b64/b32 with perm). Stable: a transposed row lists its entries
+ * in increasing source row (source entry order for duplicates), so the
+ * result is deterministic. Synchronises. */
+int mpg_csr_transpose(mpg_ctx_t ctx, int32_t rows, int32_t cols, int64_t nnz, const int32_t* rowptr_dev,
+                      const int32_t* col_dev, int32_t* rowptr_t_dev, int32_t* col_t_dev, int32_t* perm_dev);
+
 /* ---- Jacobi preconditioner setup (types.hpp:393-431) ----
  * alpha = max_i sum_j |a_ij| (summed in the values' precision) *
  * FLT_EPSILON; d_i = 1 / boost(a_ii) where the diagonal entry is the first

@@ -46,6 +46,11 @@ int mpg_gen_laplace3d(int32_t nx, int32_t ny, int32_t nz, mpg_host_csr* out);
  * rows, ~3.2e8 nnz. */
 int mpg_gen_stencil27(int32_t nx, int32_t ny, int32_t nz, int32_t dof, uint64_t seed, mpg_host_csr* out);
 
+/* One of the generators above from a CLI spec: "band:N[:LO:HI[:SEED]]"
+ * (defaults 5, 4, 7), "laplace:NX[:NY:NZ]", "stencil27:NX[:DOF[:SEED]]"
+ * (defaults 3, 11). Returns 0, or -2 with a message in err. */
+int mpg_gen_spec(const char* spec, mpg_host_csr* out, char* err, int errlen);
+
 /* Matrix Market coordinate real|integer, general|symmetric, loaded as
  * LoadMatrix.hpp:17-154 does: an explicit diagonal slot in every row (0 if
  * the file has none; a diagonal entry in the file overwrites it), symmetric

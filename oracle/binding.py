@@ -45,6 +45,7 @@ def lib() -> C.CDLL:
         _lib.oracle_rotg_f32.argtypes = [p, p, p, p]
         _lib.oracle_jacobi_f64.argtypes = [i, p, p, p, p]
         _lib.oracle_jacobi_f32.argtypes = [i, p, p, p, p]
+        _lib.oracle_condest.restype = C.c_int
         for t in ("f64", "f32"):
             getattr(_lib, f"oracle_ilu0_{t}").argtypes = [i, p, p, p, p, p]
             getattr(_lib, f"oracle_ilu_apply_{t}").argtypes = [i, p, p, p, i, i, p]
@@ -147,3 +148,16 @@ def ilu_apply(A, x: np.ndarray, kind="ilu", steps=1, dtype=np.float64) -> np.nda
           steps, _ptr(x)):
         raise ValueError("oracle ILU apply failed")
     return x
+
+
+def condest(mpg, A, rand_seed: int = 42, max_iters: int = 100000, verbose: bool = False, threads: int = 0) -> dict:
+    """The CPU restatement of condest.cpp:34-150 (oracle/cpu_condest.cpp);
+    same argument/result structs as mpg.condest."""
+    from importlib import import_module
+
+    abi = import_module(mpg.__name__ + "._abi")
+    a = abi.condest_args(A, rand_seed, max_iters, verbose, 0, threads)
+    r = abi.CondestResult()
+    if lib().oracle_condest(C.byref(a), C.byref(r)):
+        raise RuntimeError(f"oracle_condest failed: {r.message.decode()}")
+    return abi.condest_dict(r)
