@@ -23,30 +23,47 @@ struct half_v {
     uint16_t bits;
 };
 
+// Cache policy of the matrix streams (col + val). MPG_CSR_NT=1 loads them
+// non-temporally, so a once-per-cycle CSR pass (the fp64 residual) does not
+// displace the Krylov basis from the Infinity Cache.
+#ifndef MPG_CSR_NT
+#define MPG_CSR_NT 0
+#endif
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef double f64x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x4_t __attribute__((ext_vector_type(4)));
+
+template <bool NT, class V> __device__ __forceinline__ V ld_policy(const V* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <class V> __device__ __forceinline__ V ld_mat(const V* p) { return ld_policy<MPG_CSR_NT != 0>(p); }
+
 // 4 consecutive values (element index i, a multiple of 4) widened to fp64
 template <class V> struct Vec4Load;
 template <> struct Vec4Load<float> {
     static __device__ __forceinline__ void load(const float* p, int64_t i, double (&o)[4]) {
-        const float4 v = *reinterpret_cast<const float4*>(p + i);
+        const f32x4_t v = ld_mat(reinterpret_cast<const f32x4_t*>(p + i));
         o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
     }
 };
 template <> struct Vec4Load<double> {
     static __device__ __forceinline__ void load(const double* p, int64_t i, double (&o)[4]) {
-        const double2 a = *reinterpret_cast<const double2*>(p + i);
-        const double2 b = *reinterpret_cast<const double2*>(p + i + 2);
+        const f64x2_t a = ld_mat(reinterpret_cast<const f64x2_t*>(p + i));
+        const f64x2_t b = ld_mat(reinterpret_cast<const f64x2_t*>(p + i + 2));
         o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
     }
 };
 template <> struct Vec4Load<half_v> {
     static __device__ __forceinline__ void load(const half_v* p, int64_t i, double (&o)[4]) {
-        const ushort4 v = *reinterpret_cast<const ushort4*>(p + i);
+        const u16x4_t v = ld_mat(reinterpret_cast<const u16x4_t*>(p + i));
         o[0] = to_float(v.x); o[1] = to_float(v.y); o[2] = to_float(v.z); o[3] = to_float(v.w);
     }
 };
 template <> struct Vec4Load<uint16_t> {
     static __device__ __forceinline__ void load(const uint16_t* p, int64_t i, double (&o)[4]) {
-        const ushort4 v = *reinterpret_cast<const ushort4*>(p + i);
+        const u16x4_t v = ld_mat(reinterpret_cast<const u16x4_t*>(p + i));
         o[0] = to_float(v.x); o[1] = to_float(v.y); o[2] = to_float(v.z); o[3] = to_float(v.w);
     }
 };
@@ -73,7 +90,8 @@ __device__ __forceinline__ void stage_products(int s, int e, int64_t nnz_total, 
         live[u] = idx < e;
         if (live[u]) {
             if (idx + 3 < nnz_total) {
-                c[u] = *reinterpret_cast<const int4*>(col + idx);
+                const i32x4_t cv = ld_mat(reinterpret_cast<const i32x4_t*>(col + idx));
+                c[u] = make_int4(cv.x, cv.y, cv.z, cv.w);
                 Vec4Load<V>::load(val, idx, v[u]);
             } else {
                 int cc[4];

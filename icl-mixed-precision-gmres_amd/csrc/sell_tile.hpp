@@ -39,17 +39,22 @@ template <> struct SellStore<half_v> { using type = uint16_t; };
 template <class S> __device__ __forceinline__ double widen(S v) { return (double)v; }
 template <> __device__ __forceinline__ double widen<uint16_t>(uint16_t v) { return (double)to_float(v); }
 
+// Cache policy of the slices (MPG_SELL_NT=1: non-temporal loads)
+#ifndef MPG_SELL_NT
+#define MPG_SELL_NT 0
+#endif
+
 // W consecutive elements with one aligned vector load
 template <class S, int W> struct VecW {
     typedef S vtype __attribute__((ext_vector_type(W)));
     static __device__ __forceinline__ void load(const S* p, S (&o)[W]) {
-        const vtype v = *reinterpret_cast<const vtype*>(p);
+        const vtype v = ld_policy<MPG_SELL_NT != 0>(reinterpret_cast<const vtype*>(p));
 #pragma unroll
         for (int e = 0; e < W; ++e) o[e] = v[e];
     }
 };
 template <class S> struct VecW<S, 1> {
-    static __device__ __forceinline__ void load(const S* p, S (&o)[1]) { o[0] = *p; }
+    static __device__ __forceinline__ void load(const S* p, S (&o)[1]) { o[0] = ld_policy<MPG_SELL_NT != 0>(p); }
 };
 
 // entries per lane per batch: every load of a batch is issued before its
