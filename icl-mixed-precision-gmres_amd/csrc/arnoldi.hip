@@ -53,15 +53,17 @@ __device__ __forceinline__ void my_blocks(int nblocks, int& rb0, int& rb1) {
 }
 
 // For every row of this workgroup's row blocks: fp64 sum of val * xval(col)
-// (csr_tile.hpp), then epi(row, sum) on one lane.
-template <class V, class XF, class EPI>
+// (csr_tile.hpp), then epi(row, sum) on one lane. NT: non-temporal matrix
+// loads (a pass that runs once per restart cycle).
+template <bool NT = false, class V, class XF, class EPI>
 __device__ __forceinline__ void for_rows(const int32_t* __restrict__ blocks, int nblocks,
                                          const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                          const V* __restrict__ val, int64_t nnz, XF xval, EPI epi, double* prod,
                                          double* scratch) {
     int rb0, rb1;
     my_blocks(nblocks, rb0, rb1);
-    for (int b = rb0; b < rb1; ++b) csr_row_block(blocks[b], blocks[b + 1], rowptr, col, val, nnz, xval, epi, prod, scratch);
+    for (int b = rb0; b < rb1; ++b)
+        csr_row_block<NT>(blocks[b], blocks[b + 1], rowptr, col, val, nnz, xval, epi, prod, scratch);
 }
 
 // One transpose round on the first 2H accumulators: lanes with the MASK bit
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for_rows(
+    for_rows<true>(  // once per cycle: keep V and the Arnoldi matrix cached
         blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)x[c]; },
         [&](int i, double sum) {
             const X t = (X)sum;
@@ -516,7 +518,7 @@ __global__ __launch_bounds__(BS) void k_panel_dots(int n, const T* __restrict__ 
 // GIVENS (one GPU, last pass, m <= kFoldMaxM): the ||w'||^2 partials go
 // write-through and the last-arriving workgroup sums them and runs the
 // Givens step k (givens_block) — no separate Givens launch.
-template <class T, bool NEXT_DOTS, bool GIVENS = false, int BS = kBlock>
+template <class T, bool NEXT_DOTS, bool GIVENS = false, int BS = kBlock, bool FROM_PARTS = false>
 __global__ __launch_bounds__(BS) void k_cgs_update(int n, const T* __restrict__ V, int64_t ld, int k,
                                                        const double* __restrict__ sums, T* __restrict__ coef_out,
                                                        T* __restrict__ w, double* __restrict__ partial,
@@ -524,19 +526,38 @@ __global__ __launch_bounds__(BS) void k_cgs_update(int n, const T* __restrict__ 
     static_assert(!(NEXT_DOTS && GIVENS), "the Givens step follows the last pass");
     __shared__ double coef[256];
     const int nc = k + 1;
-    if (part_G > 0) {
+    const int n4 = n & ~3;
+    const int i_first = 4 * (blockIdx.x * BS + threadIdx.x);
+    // part_G > 0: this lane's first row group (the first kPre columns and w)
+    // is loaded BEFORE the coefficient sums, so the partial loads below
+    // travel with it and their latency hides behind the basis stream
+    constexpr int kPre = 8;
+    const int npre = nc < kPre ? nc : kPre;
+    const bool pre = FROM_PARTS && i_first < n4;
+    double pv[kPre][4], pw[4];
+    if (pre) {
+#pragma unroll
+        for (int u = 0; u < kPre; ++u)
+            if (u < npre) Row4<T>::load(V + (int64_t)u * ld + i_first, pv[u]);
+        Row4<T>::load(w + i_first, pw);
+    }
+    if (FROM_PARTS) {
         // sums straight from the panel-dots partials (nc <= kNC, part_G per
-        // column): 8 lanes per column, each a strided run in g order, then an
-        // xor tree — the same fixed order in every workgroup
-        const int j = threadIdx.x >> 3, sub = threadIdx.x & 7;
+        // column): LPC lanes per column, each summing part_G / LPC partials
+        // (all loads issued first) in g order, then an xor tree — the same
+        // fixed order in every workgroup
+        constexpr int LPC = BS / kNC;
+        const int j = threadIdx.x / LPC, sub = threadIdx.x % LPC;
+        const int per = (part_G + LPC - 1) / LPC;
         double v = 0.0;
         if (j < nc) {
+            const double* src = sums + (size_t)j * part_G + sub;
 #pragma unroll 8
-            for (int gi = sub; gi < part_G; gi += 8) v += sums[(size_t)j * part_G + gi];
+            for (int q = 0; q < per; ++q)
+                if (q * LPC + sub < part_G) v += src[q * LPC];
         }
-        v += __shfl_xor(v, 4, kWave);
-        v += __shfl_xor(v, 2, kWave);
-        v += __shfl_xor(v, 1, kWave);
+#pragma unroll
+        for (int o = LPC / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
         if (j < nc && sub == 0) {
             const T c = (T)v;
             coef[j] = (double)c;
@@ -554,10 +575,18 @@ __global__ __launch_bounds__(BS) void k_cgs_update(int n, const T* __restrict__ 
     double acc[NA];
 #pragma unroll
     for (int c = 0; c < NA; ++c) acc[c] = 0.0;
-    const int n4 = n & ~3;
-    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
+    for (int i = i_first; i < n4; i += 4 * gridDim.x * BS) {
         double t[4] = {0.0, 0.0, 0.0, 0.0};
         int j = 0;
+        const bool use_pre = pre && i == i_first;
+        if (use_pre) {
+#pragma unroll
+            for (int u = 0; u < kPre; ++u)
+                if (u < npre)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) t[r] += pv[u][r] * coef[u];
+            j = npre;
+        }
         for (; j + 8 <= nc; j += 8) {
             double v[8][4];
 #pragma unroll
@@ -574,7 +603,12 @@ __global__ __launch_bounds__(BS) void k_cgs_update(int n, const T* __restrict__ 
             for (int r = 0; r < 4; ++r) t[r] += v[r] * coef[j];
         }
         double wv[4];
-        Row4<T>::load(w + i, wv);
+        if (use_pre) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) wv[r] = pw[r];
+        } else {
+            Row4<T>::load(w + i, wv);
+        }
         T wo[4];
         double wd[4];
 #pragma unroll
@@ -1146,7 +1180,7 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
     if (!a || k < 0 || k >= a->d.m || pass < 0 || pass > 1 || k + 1 > 256) return MPG_ERR_ARG;
     const bool cgsr = a->d.orth == kOrthCGSR;
     const bool next_dots = cgsr && pass == 0;
-    if (givens && (next_dots || a->d.m > kFoldMaxM)) return MPG_ERR_ARG;
+    if (givens && (next_dots || a->d.m > kFoldMaxM || from_partials)) return MPG_ERR_ARG;
     // from_partials: the coefficients are summed from the preceding one-panel
     // dots' partials inside this launch (no reduce launch)
     if (from_partials && (pass != 0 || k + 1 > kNC || a->last_part != a->dpart)) return MPG_ERR_ARG;
@@ -1158,8 +1192,12 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
         T* w = static_cast<T*>(a->w[(k + 1) & 1]);
         const GivensArgs<T> g = givens_args<T>(a, k);
         if (next_dots) {
-            k_cgs_update<T, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, part_G);
+            if (from_partials)
+                k_cgs_update<T, true, false, kBlock, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                    a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, part_G);
+            else
+                k_cgs_update<T, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                    a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, 0);
             for (int c0 = kNC; c0 < k + 1; c0 += kNC) {
                 const int nc = k + 1 - c0 < kNC ? k + 1 - c0 : kNC;
                 k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
@@ -1167,11 +1205,13 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
             }
         } else if (givens) {
             k_cgs_update<T, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, a->counters + 32, g,
-                part_G);
-        } else {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
-            k_cgs_update<T, false, false, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, a->counters + 32, g, 0);
+        } else if (from_partials) {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
+            k_cgs_update<T, false, false, kCombineBlock, true><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, part_G);
+        } else {
+            k_cgs_update<T, false, false, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, 0);
         }
         return (int)MPG_OK;
     });

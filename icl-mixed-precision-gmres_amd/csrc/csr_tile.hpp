@@ -23,9 +23,11 @@ struct half_v {
     uint16_t bits;
 };
 
-// Cache policy of the matrix streams (col + val). MPG_CSR_NT=1 loads them
-// non-temporally, so a once-per-cycle CSR pass (the fp64 residual) does not
-// displace the Krylov basis from the Infinity Cache.
+// Cache policy of the matrix streams (col + val): NT loads them
+// non-temporally, so a once-per-cycle CSR pass (the fp64 residual of the
+// fused engine's prologue) does not displace the Krylov basis and the
+// Arnoldi matrix from the Infinity Cache (+2 % GMRES it/s on BAND-10M,
+// tools/policy_experiment.sh). MPG_CSR_NT=1 forces it for every CSR tile.
 #ifndef MPG_CSR_NT
 #define MPG_CSR_NT 0
 #endif
@@ -38,32 +40,38 @@ template <bool NT, class V> __device__ __forceinline__ V ld_policy(const V* p) {
     if constexpr (NT) return __builtin_nontemporal_load(p);
     else return *p;
 }
-template <class V> __device__ __forceinline__ V ld_mat(const V* p) { return ld_policy<MPG_CSR_NT != 0>(p); }
+template <bool NT, class V> __device__ __forceinline__ V ld_mat(const V* p) {
+    return ld_policy<NT || MPG_CSR_NT != 0>(p);
+}
 
 // 4 consecutive values (element index i, a multiple of 4) widened to fp64
 template <class V> struct Vec4Load;
 template <> struct Vec4Load<float> {
+    template <bool NT = false>
     static __device__ __forceinline__ void load(const float* p, int64_t i, double (&o)[4]) {
-        const f32x4_t v = ld_mat(reinterpret_cast<const f32x4_t*>(p + i));
+        const f32x4_t v = ld_mat<NT>(reinterpret_cast<const f32x4_t*>(p + i));
         o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
     }
 };
 template <> struct Vec4Load<double> {
+    template <bool NT = false>
     static __device__ __forceinline__ void load(const double* p, int64_t i, double (&o)[4]) {
-        const f64x2_t a = ld_mat(reinterpret_cast<const f64x2_t*>(p + i));
-        const f64x2_t b = ld_mat(reinterpret_cast<const f64x2_t*>(p + i + 2));
+        const f64x2_t a = ld_mat<NT>(reinterpret_cast<const f64x2_t*>(p + i));
+        const f64x2_t b = ld_mat<NT>(reinterpret_cast<const f64x2_t*>(p + i + 2));
         o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
     }
 };
 template <> struct Vec4Load<half_v> {
+    template <bool NT = false>
     static __device__ __forceinline__ void load(const half_v* p, int64_t i, double (&o)[4]) {
-        const u16x4_t v = ld_mat(reinterpret_cast<const u16x4_t*>(p + i));
+        const u16x4_t v = ld_mat<NT>(reinterpret_cast<const u16x4_t*>(p + i));
         o[0] = to_float(v.x); o[1] = to_float(v.y); o[2] = to_float(v.z); o[3] = to_float(v.w);
     }
 };
 template <> struct Vec4Load<uint16_t> {
+    template <bool NT = false>
     static __device__ __forceinline__ void load(const uint16_t* p, int64_t i, double (&o)[4]) {
-        const u16x4_t v = ld_mat(reinterpret_cast<const u16x4_t*>(p + i));
+        const u16x4_t v = ld_mat<NT>(reinterpret_cast<const u16x4_t*>(p + i));
         o[0] = to_float(v.x); o[1] = to_float(v.y); o[2] = to_float(v.z); o[3] = to_float(v.w);
     }
 };
@@ -77,7 +85,7 @@ __device__ __forceinline__ double scalar_val<uint16_t>(const uint16_t* p, int64_
 
 // Stage the fp64 products val[i] * xval(col[i]) for i in [s, e) into prod[i - s].
 // nnz_total bounds the vector loads at the end of the arrays.
-template <class V, class XF>
+template <bool NT = false, class V, class XF>
 __device__ __forceinline__ void stage_products(int s, int e, int64_t nnz_total, const int32_t* __restrict__ col,
                                                const V* __restrict__ val, XF xval, double* __restrict__ prod) {
     const int base = s & ~3;
@@ -90,9 +98,9 @@ __device__ __forceinline__ void stage_products(int s, int e, int64_t nnz_total, 
         live[u] = idx < e;
         if (live[u]) {
             if (idx + 3 < nnz_total) {
-                const i32x4_t cv = ld_mat(reinterpret_cast<const i32x4_t*>(col + idx));
+                const i32x4_t cv = ld_mat<NT>(reinterpret_cast<const i32x4_t*>(col + idx));
                 c[u] = make_int4(cv.x, cv.y, cv.z, cv.w);
-                Vec4Load<V>::load(val, idx, v[u]);
+                Vec4Load<V>::template load<NT>(val, idx, v[u]);
             } else {
                 int cc[4];
 #pragma unroll
@@ -128,7 +136,7 @@ __device__ __forceinline__ void stage_products(int s, int e, int64_t nnz_total, 
 }
 
 // Row sums of one row block: epi(row, fp64 sum) is called once per row.
-template <class V, class XF, class EPI>
+template <bool NT = false, class V, class XF, class EPI>
 __device__ __forceinline__ void csr_row_block(int r0, int r1, const int32_t* __restrict__ rowptr,
                                               const int32_t* __restrict__ col, const V* __restrict__ val,
                                               int64_t nnz_total, XF xval, EPI epi, double* prod, double* scratch) {
@@ -141,7 +149,7 @@ __device__ __forceinline__ void csr_row_block(int r0, int r1, const int32_t* __r
         __syncthreads();  // the row's outputs are visible to the whole workgroup
         return;
     }
-    stage_products(s, e, nnz_total, col, val, xval, prod);
+    stage_products<NT>(s, e, nnz_total, col, val, xval, prod);
     __syncthreads();
     for (int r = threadIdx.x; r < r1 - r0; r += kBlock) {
         const int a = rowptr[r0 + r] - s, z = rowptr[r0 + r + 1] - s;
