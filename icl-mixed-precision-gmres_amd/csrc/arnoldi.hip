@@ -509,6 +509,138 @@ __global__ __launch_bounds__(BS) void k_panel_dots(int n, const T* __restrict__ 
     }
 }
 
+// The one-panel forms of the dots and the CGS update with the column count
+// NC a compile-time constant (the captured cycle knows k at every step):
+// every column index is static, so the loads of a batch of columns issue
+// back to back and the accumulators stay in registers. With a runtime
+// count the compiler guarded each column's load with its own branch and
+// waited for it before the next (one memory latency per column: t(k) =
+// 8.6 + 0.50 k us for the dots on BAND-10M, tools/per_step.py).
+template <int N> struct Pow2Ceil {
+    static constexpr int v = N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : N <= 16 ? 16 : 32;
+};
+// columns per load batch: 32 VGPRs of raw column data per batch
+template <class T> constexpr int kColBatch = sizeof(T) == 4 ? 8 : 4;
+
+// 4 consecutive entries kept in their storage type until used (a batch of
+// raw loads costs half the registers of widened fp32 values)
+template <class T> struct Raw4;
+template <> struct Raw4<float> {
+    float4 v;
+    __device__ __forceinline__ void load(const float* p) { v = *reinterpret_cast<const float4*>(p); }
+    __device__ __forceinline__ double operator[](int r) const {
+        return (double)(r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w);
+    }
+};
+template <> struct Raw4<double> {
+    double2 a, b;
+    __device__ __forceinline__ void load(const double* p) {
+        a = *reinterpret_cast<const double2*>(p);
+        b = *reinterpret_cast<const double2*>(p + 2);
+    }
+    __device__ __forceinline__ double operator[](int r) const { return r == 0 ? a.x : r == 1 ? a.y : r == 2 ? b.x : b.y; }
+};
+
+template <class T, int BS, int NC>
+__global__ __launch_bounds__(BS) void k_dots_nc(int n, const T* __restrict__ V, int64_t ld,
+                                                const T* __restrict__ w, double* __restrict__ partial) {
+    static_assert(NC >= 1 && NC <= kNC, "one panel");
+    constexpr int NP = Pow2Ceil<NC>::v;
+    constexpr int B = kColBatch<T>;
+    double acc[NP];
+#pragma unroll
+    for (int c = 0; c < NP; ++c) acc[c] = 0.0;
+    const int n4 = n & ~3;
+    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
+        double wv[4];
+        Row4<T>::load(w + i, wv);
+#pragma unroll
+        for (int c0 = 0; c0 < NC; c0 += B) {
+            Raw4<T> v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) v[u].load(V + (int64_t)(c0 + u) * ld + i);
+            __builtin_amdgcn_sched_barrier(0);  // keep the batch's loads issued back to back
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) acc[c0 + u] += v[u][0] * wv[0] + v[u][1] * wv[1] + v[u][2] * wv[2] + v[u][3] * wv[3];
+        }
+    }
+    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
+        const double wi = (double)w[i];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c] += (double)V[(int64_t)c * ld + i] * wi;
+    }
+    store_partials<NP, BS>(acc, NC, partial);
+}
+
+// coef = T(sums[0..NC)); w = w - T(V coef); partial ||w'||^2 (the last
+// CGS pass; same arithmetic and order as k_cgs_update)
+template <class T, int BS, int NC>
+__global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict__ V, int64_t ld,
+                                                      const double* __restrict__ sums, T* __restrict__ coef_out,
+                                                      T* __restrict__ w, double* __restrict__ partial) {
+    static_assert(NC >= 1 && NC <= kNC, "one panel");
+    constexpr int B = kColBatch<T>;
+    __shared__ double coef[NC];
+    if (threadIdx.x < NC) {
+        const T c = (T)sums[threadIdx.x];
+        coef[threadIdx.x] = (double)c;
+        if (blockIdx.x == 0) coef_out[threadIdx.x] = c;
+    }
+    __syncthreads();
+    double acc[1] = {0.0};
+    const int n4 = n & ~3;
+    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
+        double wv[4];
+        Row4<T>::load(w + i, wv);
+        double t[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c0 = 0; c0 < NC; c0 += B) {
+            Raw4<T> v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) v[u].load(V + (int64_t)(c0 + u) * ld + i);
+            __builtin_amdgcn_sched_barrier(0);  // keep the batch's loads issued back to back
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) {
+                    const double cu = coef[c0 + u];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) t[r] += v[u][r] * cu;
+                }
+        }
+        T wo[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            wo[r] = T(-1) * (T)t[r] + T(1) * (T)wv[r];
+            const double wd = (double)wo[r];
+            acc[0] += wd * wd;
+        }
+        Row4<T>::store(w + i, wo);
+    }
+    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) t += (double)V[(int64_t)j * ld + i] * coef[j];
+        const T wi = T(-1) * (T)t + T(1) * w[i];
+        w[i] = wi;
+        acc[0] += (double)wi * (double)wi;
+    }
+    store_partials<1, BS>(acc, 1, partial);
+}
+
+// f(integral_constant<int, nc>) for 1 <= nc <= N
+template <int N, class F>
+int with_nc(int nc, F&& f) {
+    if constexpr (N == 0) {
+        return MPG_ERR_ARG;
+    } else {
+        if (nc == N) return f(std::integral_constant<int, N>());
+        return with_nc<N - 1>(nc, f);
+    }
+}
+
 // ---------------------------------------------------------------- step: CGS
 // coef = T(sums[0..k]); w = w - T(V coef) (gemv(-1, V, h, 1, w));
 // NEXT_DOTS: partials <v_j, w'> (j <= k) else partial ||w'||^2.
@@ -1153,10 +1285,11 @@ static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
             return (int)MPG_OK;
         }
         if (ndots_all <= kNC) {  // one panel: 1024-thread workgroups, one per CU -> Gd partials per column
-            k_panel_dots<T, kCombineBlock, false><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, 0, ndots_all, static_cast<const T*>(a->w[(k + 1) & 1]),
-                a->dpart, nullptr, nullptr);
-            return (int)MPG_OK;
+            return with_nc<kNC>(ndots_all, [&](auto nc) {
+                k_dots_nc<T, kCombineBlock, decltype(nc)::value><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+                    a->d.n, static_cast<const T*>(a->V), a->ld, static_cast<const T*>(a->w[(k + 1) & 1]), a->dpart);
+                return (int)MPG_OK;
+            });
         }
         for (int c0 = 0; c0 < ndots_all; c0 += kNC) {
             const int nc = ndots_all - c0 < kNC ? ndots_all - c0 : kNC;
@@ -1209,6 +1342,12 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
         } else if (from_partials) {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
             k_cgs_update<T, false, false, kCombineBlock, true><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, part_G);
+        } else if (k + 1 <= kNC) {
+            return with_nc<kNC>(k + 1, [&](auto nc) {
+                k_cgs_update_nc<T, kCombineBlock, decltype(nc)::value><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+                    a->d.n, static_cast<const T*>(a->V), a->ld, src, coef_out, w, a->partial);
+                return (int)MPG_OK;
+            });
         } else {
             k_cgs_update<T, false, false, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, 0);
