@@ -575,15 +575,43 @@ __global__ __launch_bounds__(BS) void k_dots_nc(int n, const T* __restrict__ V, 
 }
 
 // coef = T(sums[0..NC)); w = w - T(V coef); partial ||w'||^2 (the last
-// CGS pass; same arithmetic and order as k_cgs_update)
-template <class T, int BS, int NC>
+// CGS pass; same arithmetic and order as k_cgs_update).
+// FROM_PARTS (one GPU): the coefficients are summed here from the one-panel
+// dots' part_G <= kCombineGroups partials per column (32 lanes per column,
+// each summing its 8 strided partials in g order, then a 32-lane xor tree:
+// the same fixed order in every workgroup) instead of a reduce launch. The 8
+// loads per lane are branch-free so they issue together: one latency.
+template <class T, int BS, int NC, bool FROM_PARTS = false>
 __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict__ V, int64_t ld,
-                                                      const double* __restrict__ sums, T* __restrict__ coef_out,
-                                                      T* __restrict__ w, double* __restrict__ partial) {
+                                                      const double* __restrict__ sums, int part_G,
+                                                      T* __restrict__ coef_out, T* __restrict__ w,
+                                                      double* __restrict__ partial) {
     static_assert(NC >= 1 && NC <= kNC, "one panel");
+    static_assert(!FROM_PARTS || BS >= 32 * NC, "32 lanes per column");
     constexpr int B = kColBatch<T>;
     __shared__ double coef[NC];
-    if (threadIdx.x < NC) {
+    if constexpr (FROM_PARTS) {
+        const int j = threadIdx.x / 32, sub = threadIdx.x % 32;
+        const int jc = j < NC ? j : NC - 1;
+        constexpr int Q = kCombineGroups / 32;
+        double pp[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int g = sub + 32 * q;
+            pp[q] = sums[(size_t)jc * part_G + (g < part_G ? g : 0)];
+        }
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            if (sub + 32 * q < part_G) v += pp[q];
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+        if (j < NC && sub == 0) {
+            const T c = (T)v;
+            coef[j] = (double)c;
+            if (blockIdx.x == 0) coef_out[j] = c;
+        }
+    } else if (threadIdx.x < NC) {
         const T c = (T)sums[threadIdx.x];
         coef[threadIdx.x] = (double)c;
         if (blockIdx.x == 0) coef_out[threadIdx.x] = c;
@@ -592,8 +620,8 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
     double acc[1] = {0.0};
     const int n4 = n & ~3;
     for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
-        double wv[4];
-        Row4<T>::load(w + i, wv);
+        Raw4<T> wr;
+        wr.load(w + i);
         double t[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int c0 = 0; c0 < NC; c0 += B) {
@@ -613,7 +641,7 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
         T wo[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            wo[r] = T(-1) * (T)t[r] + T(1) * (T)wv[r];
+            wo[r] = T(-1) * (T)t[r] + T(1) * (T)wr[r];
             const double wd = (double)wo[r];
             acc[0] += wd * wd;
         }
@@ -799,26 +827,61 @@ __global__ __launch_bounds__(BS) void k_mgs_update(int n, const T* __restrict__ 
                                                    T* __restrict__ w, double* __restrict__ partial) {
     __shared__ double scratch[BS / kWave];
     __shared__ T h_s;
-    if (src_G > 0) {
-        const double sum = sum_partials<BS>(src, src_G, scratch);
-        if (threadIdx.x == 0) h_s = (T)sum;
-        __syncthreads();
-    } else if (threadIdx.x == 0) {
-        h_s = (T)src[0];
-    }
-    __syncthreads();
-    const T h = h_s;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *hjk = h;
     const T* __restrict__ vj = V + (int64_t)j * ld;
     const T* __restrict__ vn = V + (int64_t)(j + 1) * ld;
     const bool last = j == k;
-    double acc[1] = {0.0};
     const int n4 = n & ~3;
-    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
+    // this lane's first row group is loaded before h_jk is known, so its
+    // latency overlaps the partial sum's instead of following it
+    const int i_first = 4 * (blockIdx.x * BS + threadIdx.x);
+    const bool pre = i_first < n4;
+    // raw and unconditional (a clamped address when this lane has no row
+    // group): a guarded load would be widened to fp64 inside its branch,
+    // i.e. waited for right here. Column j + 1 <= m exists; unused when last.
+    // The partial (src_G <= BS: one per lane) is loaded FIRST: vmcnt retires
+    // in order, so waiting for it must not wait for the row group behind it.
+    static_assert(BS >= kCombineGroups * 4, "one partial per lane");
+    double part = src[threadIdx.x < src_G ? threadIdx.x : 0];
+    if (threadIdx.x >= src_G) part = 0.0;
+    __builtin_amdgcn_sched_barrier(0);
+    const int ip = pre ? i_first : 0;
+    Raw4<T> pw, pv, pn;
+    pw.load(w + ip);
+    pv.load(vj + ip);
+    pn.load(vn + ip);
+    __builtin_amdgcn_sched_barrier(0);
+    // LDS-only barriers: the first row group's loads stay in flight. The
+    // block sum runs unconditionally so the partial load is not sunk below
+    // the row group's loads.
+    {
+        const double v = wave_sum(part + 0.0);  // = sum_partials' order for src_G <= BS
+        if ((threadIdx.x & (kWave - 1)) == 0) scratch[threadIdx.x / kWave] = v;
+        lds_barrier();
+        if (threadIdx.x == 0) {
+            double r = 0.0;
+#pragma unroll
+            for (int q = 0; q < BS / kWave; ++q) r += scratch[q];
+            h_s = src_G > 0 ? (T)r : (T)src[0];
+        }
+    }
+    lds_barrier();
+    const T h = h_s;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *hjk = h;
+    double acc[1] = {0.0};
+    for (int i = i_first; i < n4; i += 4 * gridDim.x * BS) {
         double wv[4], vv[4], nv[4] = {0.0, 0.0, 0.0, 0.0};
-        Row4<T>::load(w + i, wv);
-        Row4<T>::load(vj + i, vv);
-        if (!last) Row4<T>::load(vn + i, nv);
+        if (i == i_first) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                wv[r] = pw[r];
+                vv[r] = pv[r];
+                nv[r] = last ? 0.0 : pn[r];
+            }
+        } else {
+            Row4<T>::load(w + i, wv);
+            Row4<T>::load(vj + i, vv);
+            if (!last) Row4<T>::load(vn + i, nv);
+        }
         T wo[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1339,13 +1402,15 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
         } else if (givens) {
             k_cgs_update<T, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, a->counters + 32, g, 0);
-        } else if (from_partials) {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
-            k_cgs_update<T, false, false, kCombineBlock, true><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, part_G);
-        } else if (k + 1 <= kNC) {
+        } else if (k + 1 <= kNC) {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
             return with_nc<kNC>(k + 1, [&](auto nc) {
-                k_cgs_update_nc<T, kCombineBlock, decltype(nc)::value><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                    a->d.n, static_cast<const T*>(a->V), a->ld, src, coef_out, w, a->partial);
+                constexpr int NC = decltype(nc)::value;
+                if (from_partials)
+                    k_cgs_update_nc<T, kCombineBlock, NC, true><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+                        a->d.n, static_cast<const T*>(a->V), a->ld, src, part_G, coef_out, w, a->partial);
+                else
+                    k_cgs_update_nc<T, kCombineBlock, NC, false><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+                        a->d.n, static_cast<const T*>(a->V), a->ld, src, 0, coef_out, w, a->partial);
                 return (int)MPG_OK;
             });
         } else {

@@ -82,6 +82,17 @@ __device__ __forceinline__ T wave_max(T v) {
     return v;
 }
 
+// Workgroup barrier that waits for this wave's LDS operations only:
+// __syncthreads() also waits for every outstanding global load (its
+// workgroup-scope release), which would drain loads issued ahead on purpose.
+// The signal fences keep the compiler from moving memory accesses across.
+__device__ __forceinline__ void lds_barrier() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt and expcnt at their maxima (no wait)
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 // Block-wide sum for blockDim.x == BS (multiple of 64). Result valid in
 // thread 0. `scratch` must hold BS/64 elements.
 template <int BS, class T>
