@@ -359,6 +359,16 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
 // tools/sell_bench.hip). Values are the same T(w_prev * inv) either way.
 constexpr int kWinLo = 64, kWinHi = 64, kWinLen = kWinLo + kWave + kWinHi;
 
+//
+// Load order (vmcnt retires in order, so what is needed first is issued
+// first, and nothing is waited for before everything is in flight): the
+// slice's offsets, the folded Givens step's partial (one per lane), the
+// window of w_prev (raw,
+// clamped addresses), the slice's first batch of (col, val); then the
+// partial sum behind LDS-only barriers, the scaled window into LDS, the
+// gathers. A guarded load would be widened inside its branch and waited
+// for right there — the previous form waited for each window load and each
+// step's loads in turn.
 template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD>
 __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col,
@@ -367,31 +377,96 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
                                                       T* __restrict__ V, int64_t ld, int k,
                                                       const P* __restrict__ diag, T* __restrict__ w,
                                                       GivensFold<T> fold) {
+    using S = typename SellStore<VI>::type;
+    constexpr int NQ = kWinLen / kWave;
     __shared__ T win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
-    const T inv = fold_givens<FOLD>(fold, inv_p);  // block-wide: before any lane leaves
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     const int s = blockIdx.x * (kBlock / kWave) + wid;
-    if (s >= nslices) return;
+    const bool live = s < nslices;  // a dead wave still joins the fold's barriers
     const int row0 = s * kWave;
-    double sum;
+    const int i = row0 + lane;
+    // 0. the slice's offsets
+    SellRow<S, CI, W> row;
+    row.init_load(live ? s : 0, off);
+    __builtin_amdgcn_sched_barrier(0);
+    // 1. the fold's ||w||^2 partial (nparts <= kBlock, checked at launch: one per lane)
+    double part = 0.0;
+    if constexpr (FOLD) {
+        part = fold.norm2[threadIdx.x < fold.nparts ? threadIdx.x : 0];
+        if (threadIdx.x >= fold.nparts) part = 0.0;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // 2. w_prev window (or this row's own w_prev), raw
+    T wr[WIN ? NQ : 1];
     if constexpr (WIN) {
 #pragma unroll
-        for (int q = 0; q < kWinLen / kWave; ++q) {
+        for (int q = 0; q < NQ; ++q) {
             const int c = row0 - kWinLo + q * kWave + lane;
-            win[wid][q * kWave + lane] = (c >= 0 && c < n_ext) ? (T)(wprev[c] * inv) : T(0);
+            wr[q] = wprev[c >= 0 && c < n_ext ? c : 0];
+        }
+    } else {
+        wr[0] = wprev[i < n ? i : 0];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // 3. the slice's first batch
+    row.init_finish(lane, col, val);
+    row.load(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // the scale 1/h_{k,k-1}: the folded Givens step, or the Givens kernel's
+    T inv;
+    if constexpr (FOLD) {
+        __shared__ T col_s[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
+        __shared__ double scratch[kBlock / kWave];
+        __shared__ T inv_s;
+        double nrm2sq;
+        if (fold.nparts > 0) {
+            const double v = wave_sum(part + 0.0);  // the same fixed order in every workgroup
+            if (lane == 0) scratch[wid] = v;
+            lds_barrier();
+            double r = 0.0;
+#pragma unroll
+            for (int q = 0; q < kBlock / kWave; ++q) r += scratch[q];
+            nrm2sq = r;
+        } else {
+            nrm2sq = fold.norm2[0];
+        }
+        if (threadIdx.x == 0) inv_s = inv_of_norm2<T>(nrm2sq);
+        if (blockIdx.x == 0) givens_block(fold.g, nrm2sq, col_s, c_s, s_s);
+        lds_barrier();
+        inv = inv_s;
+    } else {
+        inv = *inv_p;
+    }
+    if (!live) return;
+    double sum = 0.0;
+    T vk;  // v_k(i) = T(w_prev(i) * inv)
+    if constexpr (WIN) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int c = row0 - kWinLo + q * kWave + lane;
+            win[wid][q * kWave + lane] = (c >= 0 && c < n_ext) ? (T)(wr[q] * inv) : T(0);
         }
         wave_lds_sync();
-        sum = sell_row_sum<typename SellStore<VI>::type, CI, W>(
-            s, lane, off, col, val, [&](int c) { return (double)win[wid][c - row0 + kWinLo]; });
+        auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
+        row.sum(0, xv, sum);
+        for (int q = row.U; q < row.steps; q += row.U) {
+            row.load(q);
+            row.sum(q, xv, sum);
+        }
+        vk = win[wid][lane + kWinLo];
     } else {
-        sum = sell_row_sum<typename SellStore<VI>::type, CI, W>(
-            s, lane, off, col, val, [&](int c) { return (double)(T)(wprev[c] * inv); });
+        auto xv = [&](int c) { return (double)(T)(wprev[c] * inv); };
+        row.sum(0, xv, sum);
+        for (int q = row.U; q < row.steps; q += row.U) {
+            row.load(q);
+            row.sum(q, xv, sum);
+        }
+        vk = (T)(wr[0] * inv);
     }
-    const int i = row0 + lane;
     if (i < n) {
         const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
         w[i] = precond<T, P>(t, diag, i);
-        V[(int64_t)k * ld + i] = wprev[i] * inv;
+        V[(int64_t)k * ld + i] = vk;
     }
 }
 
@@ -1303,6 +1378,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold) {
             gf = GivensFold<T>{fold == 2 ? a->last_part : a->sums, fold == 2 ? a->last_G : 0, givens_args<T>(a, k - 1)};
         if (a->sell.nslices > 0) {
             const auto& S = a->sell;
+            if (fold == 2 && a->last_G > kBlock) return (int)MPG_ERR_ARG;  // k_step_sell folds <= kBlock partials
             return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
                 using CI = decltype(ci);
                 const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);

@@ -104,4 +104,66 @@ __device__ __forceinline__ double sell_row_sum(int s, int lane, const int64_t* _
     return acc;
 }
 
+// The same row sum split into load and sum halves, so a kernel can issue a
+// batch of slice loads early (before loads it needs sooner have returned,
+// or before a barrier) and consume it later. Loads are unconditional: steps
+// past the slice's width re-read its last step (cache hits) and are masked
+// by step index at use, so nothing widens or selects a loaded value at load
+// time (which would wait for it on the spot). An empty slice points at
+// offset 0 of the arrays.
+template <class S, class CI, int W>
+struct SellRow {
+    static constexpr int U = sell_unroll<W>();
+    CI c[U][W];
+    S v[U][W];
+    int steps, row0;
+    const CI* __restrict__ cp;
+    const S* __restrict__ vp;
+
+    int64_t o0, o1;
+    // the slice's offsets: issue first (everything else needs them), use later
+    __device__ __forceinline__ void init_load(int s, const int64_t* __restrict__ off) {
+        o0 = off[s];
+        o1 = off[s + 1];
+        row0 = s * kWave;
+    }
+    __device__ __forceinline__ void init_finish(int lane, const CI* __restrict__ col, const S* __restrict__ val) {
+        steps = (int)((o1 - o0) / (kWave * W));
+        const int64_t base = steps > 0 ? o0 + lane * W : 0;
+        cp = col + base;
+        vp = val + base;
+    }
+    __device__ __forceinline__ void init(int s, int lane, const int64_t* __restrict__ off, const CI* __restrict__ col,
+                                         const S* __restrict__ val) {
+        init_load(s, off);
+        init_finish(lane, col, val);
+    }
+    __device__ __forceinline__ void load(int q) {
+        const int last = steps > 0 ? steps - 1 : 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int qq = q + u < last ? q + u : last;
+            VecW<CI, W>::load(cp + (int64_t)qq * kWave * W, c[u]);
+            VecW<S, W>::load(vp + (int64_t)qq * kWave * W, v[u]);
+        }
+    }
+    // acc += the batch loaded at step q, in CSR order. Every gather is issued
+    // (padding and steps past the width read x at row0, a valid index) and
+    // masked at the sum, so the gathers of a batch are in flight together.
+    template <class XF>
+    __device__ __forceinline__ void sum(int q, XF xval, double& acc) const {
+        double x[U][W];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < W; ++e)
+                x[u][e] = xval(SellCol<CI>::live(c[u][e]) ? SellCol<CI>::decode(c[u][e], row0) : row0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < W; ++e)
+                if (q + u < steps && SellCol<CI>::live(c[u][e])) acc += widen(v[u][e]) * x[u][e];
+    }
+};
+
 }  // namespace mpg

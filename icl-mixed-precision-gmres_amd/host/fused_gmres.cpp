@@ -293,14 +293,15 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     // 1024-thread CGS update itself (+1.9 us per SpMV, -4.6 us Givens launch
     // and its boundary: 19.3k vs 18.7k it/s on BAND-10M). Experiments, off:
     // MPG_COMBINE=1 (one GPU, CGS/CGSR) does last-arriver combines in the dots
-    // and CGS launches: 15.1k it/s (1024 tickets on one counter serialise);
-    // MPG_CGS_PARTIALS=1: every CGS workgroup sums the 256 dots partials per
-    // column itself instead of the reduce launch: 17.5k it/s (+4 us per CGS
-    // launch against the 4.9 us reduce it removes).
+    // and CGS launches: 15.1k it/s (1024 tickets on one counter serialise).
+    // One GPU, by default (MPG_CGS_PARTIALS=0: off): every CGS workgroup sums
+    // the 256 dots partials per column itself (8 branch-free loads per lane,
+    // one latency) instead of the reduce launch: 21.6k vs 21.1k it/s on
+    // BAND-10M (tools/ab_bench.sh, 4 interleaved runs each).
     const char* cenv = std::getenv("MPG_COMBINE");
     I.combine = !comm && cenv && *cenv == '1' && I.orth != MPG_ORTH_MGS && I.m <= mpg_arnoldi_fold_max_m();
     const char* penv = std::getenv("MPG_CGS_PARTIALS");
-    I.cgs_partials = !comm && !I.combine && penv && *penv == '1' && I.orth != MPG_ORTH_MGS;
+    I.cgs_partials = !comm && !I.combine && !(penv && *penv == '0') && I.orth != MPG_ORTH_MGS;
     const char* fenv = std::getenv("MPG_FOLD_GIVENS");
     I.fold = !I.combine && !(fenv && *fenv == '0') && I.m <= mpg_arnoldi_fold_max_m();
     check(mpg_ctx_sync(ctx), "sync", ctx);

@@ -52,7 +52,7 @@ def main():
     gens = {"laplace": mpg.gen_laplace3d, "stencil27": lambda s: mpg.gen_stencil27(s, 3),
             "band": lambda s: mpg.gen_band(s, 5, 4, seed=7)}
     for case in CASES:
-        if only and not case["name"].startswith(only):
+        if only and not any(case["name"].startswith(o) for o in only.split(",")):
             continue
         kind, size = case["matrix"]
         t0 = time.time()
@@ -75,7 +75,7 @@ def main():
         layout = eng.spmv_layout()
         eng.close()
         cpu = None
-        if kind == "laplace":  # (the 1e8-nnz-scale CPU samples would take minutes)
+        if kind == "laplace" and args.cpu_cycles > 0:  # (the 1e8-nnz-scale CPU samples would take minutes)
             r = binding.solve(mpg, A, b, xt, **dict(opts, max_restarts=args.cpu_cycles))
             cpu = {"it_s": round(r.total_iters / r.gmres_seconds, 2),
                    "threads": binding.lib().oracle_max_threads(), "backend": binding.backend()}
