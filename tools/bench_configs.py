@@ -52,7 +52,7 @@ def main():
     gens = {"laplace": mpg.gen_laplace3d, "stencil27": lambda s: mpg.gen_stencil27(s, 3),
             "band": lambda s: mpg.gen_band(s, 5, 4, seed=7)}
     for case in CASES:
-        if only and not any(case["name"].startswith(o) for o in only.split(",")):
+        if only and not case["name"].startswith(only):
             continue
         kind, size = case["matrix"]
         t0 = time.time()
