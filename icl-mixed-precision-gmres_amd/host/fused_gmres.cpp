@@ -301,7 +301,10 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     const char* cenv = std::getenv("MPG_COMBINE");
     I.combine = !comm && cenv && *cenv == '1' && I.orth != MPG_ORTH_MGS && I.m <= mpg_arnoldi_fold_max_m();
     const char* penv = std::getenv("MPG_CGS_PARTIALS");
-    I.cgs_partials = !comm && !I.combine && !(penv && *penv == '0') && I.orth != MPG_ORTH_MGS;
+    // (CGSR's first pass also emits the next dots: its in-launch form is the
+    // older runtime-count kernel, slower than reduce + update; on only with =1)
+    I.cgs_partials = !comm && !I.combine && I.orth != MPG_ORTH_MGS &&
+                     (I.orth == MPG_ORTH_CGSR ? (penv && *penv == '1') : !(penv && *penv == '0'));
     const char* fenv = std::getenv("MPG_FOLD_GIVENS");
     I.fold = !I.combine && !(fenv && *fenv == '0') && I.m <= mpg_arnoldi_fold_max_m();
     check(mpg_ctx_sync(ctx), "sync", ctx);
