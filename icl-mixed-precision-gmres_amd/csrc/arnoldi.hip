@@ -1260,7 +1260,9 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
               alloc(&a->small, (size_t)6 * (m + 1) * a->tsize) &&
               alloc(&a->w[0], (size_t)(desc->n_ext + 64) * a->tsize) &&
               alloc(&a->w[1], (size_t)(desc->n_ext + 64) * a->tsize) &&
-              alloc((void**)&a->partial, std::max<size_t>((size_t)(kNC + 4) * a->Grb, (size_t)(m + 4) * a->G) *
+              alloc((void**)&a->partial, std::max<size_t>(std::max<size_t>((size_t)(kNC + 4) * a->Grb,
+                                                                           (size_t)(m + 4) * a->G),
+                                                          (size_t)kNC * kCombineGroups) *  // uniform groups
                                              sizeof(double)) &&
               alloc((void**)&a->sums, (size_t)(m + 8) * sizeof(double)) &&
               alloc((void**)&a->report, (size_t)(m + 8) * sizeof(double)) &&
@@ -1584,5 +1586,14 @@ const void* mpg_arnoldi_basis_dev(mpg_arnoldi_t a, int64_t* ld) {
 }
 const void* mpg_arnoldi_hessenberg_dev(mpg_arnoldi_t a) { return a ? a->H : nullptr; }
 int mpg_arnoldi_num_groups(mpg_arnoldi_t a) { return a ? a->G : 0; }
+double* mpg_arnoldi_partials_dev(mpg_arnoldi_t a) { return a ? a->last_part : nullptr; }
+// the last producer wrote last_G partials per column; the one-column
+// producers (CGS/MGS updates, MGS dots) are what a caller all-reduces
+int mpg_arnoldi_partials_count(mpg_arnoldi_t a) { return a ? a->last_G : 0; }
+int mpg_arnoldi_uniform_groups(mpg_arnoldi_t a) {
+    if (!a) return MPG_ERR_ARG;
+    a->Gd = kCombineGroups;
+    return MPG_OK;
+}
 
 }  // extern "C"

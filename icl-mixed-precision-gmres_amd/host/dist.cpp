@@ -51,6 +51,7 @@ class RcclComm : public Comm {
     std::vector<int32_t> recv_off_, recv_cnt_;
     std::vector<std::unique_ptr<DevMem>> send_idx_, send_buf_;
     std::vector<int32_t> send_cnt_;
+    std::vector<int32_t> send_first_;  // >= 0: the rows sent to q are [first, first + cnt) (sent in place, no pack)
 
 public:
     RcclComm(mpg_ctx_t ctx, const mpg_halo& h, const char* id, int nranks, int rank)
@@ -59,12 +60,19 @@ public:
         std::memcpy(&uid, id, sizeof uid);
         nck(ncclCommInitRank(&comm_, nranks, uid, rank), "ncclCommInitRank");
         send_cnt_.assign(nranks, 0);
+        send_first_.assign(nranks, -1);
         send_idx_.resize(nranks);
         send_buf_.resize(nranks);
         for (int q = 0; q < nranks; ++q) {
             const auto& rows = h.send_local[q];
             send_cnt_[q] = (int32_t)rows.size();
             if (rows.empty()) continue;
+            bool contiguous = true;  // banded matrices: a run at either end of the block
+            for (size_t i = 1; i < rows.size() && contiguous; ++i) contiguous = rows[i] == rows[i - 1] + 1;
+            if (contiguous) {
+                send_first_[q] = rows[0];
+                continue;
+            }
             send_idx_[q] = std::make_unique<DevMem>(ctx, rows.size() * 4);
             check(mpg_memcpy_h2d(ctx, send_idx_[q]->p, rows.data(), rows.size() * 4), "h2d", ctx);
             send_buf_[q] = std::make_unique<DevMem>(ctx, rows.size() * 8);
@@ -82,16 +90,29 @@ public:
     void allreduce_max(double* dev, int count, hipStream_t s) override {
         nck(ncclAllReduce(dev, dev, (size_t)count, ncclFloat64, ncclMax, comm_, s), "allreduce max");
     }
-    void halo(void* vec, int eb, hipStream_t s) override {
+    void halo(void* vec, int eb, hipStream_t s) override { exchange(nullptr, 0, vec, eb, s); }
+    void allreduce_sum_and_halo(double* dev, int count, void* vec, int eb, hipStream_t s) override {
+        exchange(dev, count, vec, eb, s);
+    }
+
+private:
+    // halo send/recv (rows that are not one contiguous run are packed
+    // first), with the optional all-reduce in the same RCCL group
+    void exchange(double* dev, int count, void* vec, int eb, hipStream_t s) {
         for (int q = 0; q < size_; ++q) {
-            if (!send_cnt_[q]) continue;
+            if (!send_cnt_[q] || send_first_[q] >= 0) continue;
             const int st = eb == 8 ? mpg_gather_b64(ctx_, send_cnt_[q], send_idx_[q]->as<int32_t>(), vec, send_buf_[q]->p)
                                    : mpg_gather_b32(ctx_, send_cnt_[q], send_idx_[q]->as<int32_t>(), vec, send_buf_[q]->p);
             check(st, "halo pack", ctx_);
         }
         nck(ncclGroupStart(), "group start");
+        if (dev) nck(ncclAllReduce(dev, dev, (size_t)count, ncclFloat64, ncclSum, comm_, s), "allreduce");
         for (int q = 0; q < size_; ++q) {
-            if (send_cnt_[q]) nck(ncclSend(send_buf_[q]->p, (size_t)send_cnt_[q] * eb, ncclUint8, q, comm_, s), "send");
+            if (send_cnt_[q]) {
+                const void* src = send_first_[q] >= 0 ? static_cast<const char*>(vec) + (size_t)send_first_[q] * eb
+                                                      : send_buf_[q]->p;
+                nck(ncclSend(src, (size_t)send_cnt_[q] * eb, ncclUint8, q, comm_, s), "send");
+            }
             if (recv_cnt_[q]) {
                 char* dst = static_cast<char*>(vec) + ((size_t)n_local_ + recv_off_[q]) * eb;
                 nck(ncclRecv(dst, (size_t)recv_cnt_[q] * eb, ncclUint8, q, comm_, s), "recv");

@@ -276,6 +276,8 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     d.x = I.x.p;
     d.spmv_format = a.spmv_format;
     check(mpg_arnoldi_create(ctx, &d, &I.arn), "mpg_arnoldi_create", ctx);
+    // ranks all-reduce per-workgroup partials in place: same count on every rank
+    if (comm) check(mpg_arnoldi_uniform_groups(I.arn), "uniform groups", ctx);
     I.report_len = mpg_arnoldi_report_len(I.arn);
     hipck(hipHostMalloc((void**)&I.report_host, (size_t)I.report_len * sizeof(double), 0), "hipHostMalloc");
 
@@ -331,6 +333,13 @@ void FusedEngine::prologue() {
     check(mpg_arnoldi_prologue_finish(I.arn), "prologue_finish", I.ctx);
 }
 
+// ranks: sum the last kernel's per-workgroup partials across ranks in place
+// (bit-identical on every rank), for a consumer that sums them itself
+void FusedEngine::allreduce_partials() {
+    Impl& I = *p_;
+    I.comm->allreduce_sum(mpg_arnoldi_partials_dev(I.arn), mpg_arnoldi_partials_count(I.arn), I.stream());
+}
+
 void FusedEngine::reduce(int nc) {
     Impl& I = *p_;
     check(mpg_arnoldi_reduce(I.arn, nc), "reduce", I.ctx);
@@ -354,11 +363,12 @@ void FusedEngine::givens(int k) {
 void FusedEngine::step(int k, bool fold) {
     Impl& I = *p_;
     if (fold && k > 0) {
-        if (I.comm) reduce(1);
-        if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
+        if (I.comm)  // the ||w||^2 partials' all-reduce and the w_prev halo in one RCCL group
+            I.comm->allreduce_sum_and_halo(mpg_arnoldi_partials_dev(I.arn), mpg_arnoldi_partials_count(I.arn),
+                                           mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn),
+                                           I.stream());
         timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
-        check(I.comm ? mpg_arnoldi_givens_spmv(I.arn, k) : mpg_arnoldi_givens_partials_spmv(I.arn, k), "givens+spmv",
-              I.ctx);
+        check(mpg_arnoldi_givens_partials_spmv(I.arn, k), "givens+spmv", I.ctx);
     } else {
         if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
         timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
@@ -369,11 +379,10 @@ void FusedEngine::step(int k, bool fold) {
         check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
         if (!I.comm) {  // one GPU: each update sums the previous launch's partials itself
             for (int j = 0; j <= k; ++j) check(mpg_arnoldi_mgs_partials(I.arn, k, j), "mgs", I.ctx);
-        } else {
-            reduce(1);
+        } else {  // ranks: all-reduce the 256 partials in place, then the same in-launch sums
             for (int j = 0; j <= k; ++j) {
-                check(mpg_arnoldi_mgs(I.arn, k, j), "mgs", I.ctx);
-                if (j < k) reduce(1);
+                allreduce_partials();
+                check(mpg_arnoldi_mgs_partials(I.arn, k, j), "mgs", I.ctx);
             }
         }
     } else {

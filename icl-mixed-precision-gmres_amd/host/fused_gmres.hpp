@@ -37,6 +37,12 @@ public:
     virtual void allreduce_max(double* dev, int count, hipStream_t s) = 0;
     // fill the halo tail [n, n_ext) of a vector of `elem_bytes` elements
     virtual void halo(void* dev_vec, int elem_bytes, hipStream_t s) = 0;
+    // allreduce_sum and halo together (independent inputs): one RCCL group,
+    // i.e. one collective launch per Arnoldi step instead of two
+    virtual void allreduce_sum_and_halo(double* dev, int count, void* dev_vec, int elem_bytes, hipStream_t s) {
+        allreduce_sum(dev, count, s);
+        halo(dev_vec, elem_bytes, s);
+    }
     // whether the collectives may be captured into a hipGraph (no host waits)
     virtual bool capturable() const = 0;
 };
@@ -92,6 +98,7 @@ private:
     void prologue();
     void step(int k, bool fold);
     void reduce(int nc);
+    void allreduce_partials();
     void givens(int k);
     template <class F>
     void timed(int phase, F&& launch);

@@ -136,6 +136,17 @@ const void* mpg_arnoldi_hessenberg_dev(mpg_arnoldi_t a);  /* (m+1) x m, column-m
 /* Number of workgroups of the row-block phase kernels (partials per column). */
 int mpg_arnoldi_num_groups(mpg_arnoldi_t a);
 
+/* The per-workgroup fp64 partials the last phase kernel wrote, and their
+ * count (columns x workgroups): a multi-GPU caller may all-reduce them in
+ * place and let the next kernel sum them (mpg_arnoldi_givens_partials_spmv,
+ * mpg_arnoldi_mgs_partials) instead of a reduce launch + a scalar
+ * all-reduce. Every rank must then have the same partial count: call
+ * mpg_arnoldi_uniform_groups once after create (the one-per-CU panel
+ * kernels then always run 256 workgroups; those without rows write zeros). */
+double* mpg_arnoldi_partials_dev(mpg_arnoldi_t a);
+int mpg_arnoldi_partials_count(mpg_arnoldi_t a);
+int mpg_arnoldi_uniform_groups(mpg_arnoldi_t a);
+
 #ifdef __cplusplus
 }
 #endif
