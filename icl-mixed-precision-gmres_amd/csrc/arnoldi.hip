@@ -656,7 +656,9 @@ __global__ __launch_bounds__(BS) void k_dots_nc(int n, const T* __restrict__ V, 
 // each summing its 8 strided partials in g order, then a 32-lane xor tree:
 // the same fixed order in every workgroup) instead of a reduce launch. The 8
 // loads per lane are branch-free so they issue together: one latency.
-template <class T, int BS, int NC, bool FROM_PARTS = false>
+// NEXT_DOTS (CGSR's first pass): the partials of <v_j, w'> for j < NC
+// instead of ||w'||^2, from a second batched pass over the lane's columns.
+template <class T, int BS, int NC, bool FROM_PARTS = false, bool NEXT_DOTS = false>
 __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict__ V, int64_t ld,
                                                       const double* __restrict__ sums, int part_G,
                                                       T* __restrict__ coef_out, T* __restrict__ w,
@@ -692,7 +694,10 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
         if (blockIdx.x == 0) coef_out[threadIdx.x] = c;
     }
     __syncthreads();
-    double acc[1] = {0.0};
+    constexpr int NA = NEXT_DOTS ? Pow2Ceil<NC>::v : 1;
+    double acc[NA];
+#pragma unroll
+    for (int c = 0; c < NA; ++c) acc[c] = 0.0;
     const int n4 = n & ~3;
     for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
         Raw4<T> wr;
@@ -714,13 +719,28 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
                 }
         }
         T wo[4];
+        double wd[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             wo[r] = T(-1) * (T)t[r] + T(1) * (T)wr[r];
-            const double wd = (double)wo[r];
-            acc[0] += wd * wd;
+            wd[r] = (double)wo[r];
+            if (!NEXT_DOTS) acc[0] += wd[r] * wd[r];
         }
         Row4<T>::store(w + i, wo);
+        if constexpr (NEXT_DOTS) {
+#pragma unroll
+            for (int c0 = 0; c0 < NC; c0 += B) {
+                Raw4<T> v[B];
+#pragma unroll
+                for (int u = 0; u < B; ++u)
+                    if (c0 + u < NC) v[u].load(V + (int64_t)(c0 + u) * ld + i);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < B; ++u)
+                    if (c0 + u < NC)
+                        acc[c0 + u] += v[u][0] * wd[0] + v[u][1] * wd[1] + v[u][2] * wd[2] + v[u][3] * wd[3];
+            }
+        }
     }
     for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
         double t = 0.0;
@@ -728,9 +748,14 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
         for (int j = 0; j < NC; ++j) t += (double)V[(int64_t)j * ld + i] * coef[j];
         const T wi = T(-1) * (T)t + T(1) * w[i];
         w[i] = wi;
-        acc[0] += (double)wi * (double)wi;
+        if constexpr (NEXT_DOTS) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[c] += (double)V[(int64_t)c * ld + i] * (double)wi;
+        } else {
+            acc[0] += (double)wi * (double)wi;
+        }
     }
-    store_partials<1, BS>(acc, 1, partial);
+    store_partials<NA, BS>(acc, NEXT_DOTS ? NC : 1, partial);
 }
 
 // f(integral_constant<int, nc>) for 1 <= nc <= N
@@ -1465,7 +1490,15 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
         T* coef_out = pass == 0 ? static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) : static_cast<T*>(a->corr());
         T* w = static_cast<T*>(a->w[(k + 1) & 1]);
         const GivensArgs<T> g = givens_args<T>(a, k);
-        if (next_dots) {
+        if (next_dots && k + 1 <= kNC && !from_partials) {
+            // 256-thread workgroups (the NC fp64 dot accumulators need more
+            // than the 128 VGPRs of a 1024-thread one) -> row_grid partials
+            return with_nc<kNC>(k + 1, [&](auto nc) {
+                k_cgs_update_nc<T, kBlock, decltype(nc)::value, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
+                    a->d.n, static_cast<const T*>(a->V), a->ld, src, 0, coef_out, w, a->partial);
+                return (int)MPG_OK;
+            });
+        } else if (next_dots) {
             if (from_partials)
                 k_cgs_update<T, true, false, kBlock, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
                     a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, part_G);
