@@ -1074,6 +1074,63 @@ __global__ __launch_bounds__(kBlock) void k_update_x(int n, const T* __restrict_
     }
 }
 
+// k_update_x<T, X, true> with the column count NC = k <= kNC a compile-time
+// constant: each lane owns 4 rows and loads the basis in batches (the
+// runtime-k form waited for every few columns in turn). Same arithmetic:
+// t = sum_j V_ij y_j in fp64 in j order, x_i = x_i + X(T(t)).
+template <class T, class X, int NC>
+__global__ __launch_bounds__(kCombineBlock) void k_update_x_nc(int n, const T* __restrict__ V, int64_t ld,
+                                                                const T* __restrict__ y, const T* __restrict__ H,
+                                                                int ldh, X* __restrict__ x) {
+    static_assert(NC >= 1 && NC <= kNC, "one panel");
+    constexpr int BS = kCombineBlock, B = kColBatch<T>;
+    __shared__ T Hs[NC * kWave];
+    __shared__ double ys[NC];
+    for (int e = threadIdx.x; e < NC * kWave; e += BS) {
+        const int j = e / kWave, i = e % kWave;
+        Hs[e] = i <= j && i < NC ? H[(int64_t)j * ldh + i] : T(0);
+    }
+    __syncthreads();
+    if (threadIdx.x < kWave) {
+        const int lane = threadIdx.x;
+        T yv = lane < NC ? y[lane] : T(0);
+        yv = trsv_upper_wave(NC, Hs, yv, lane);
+        if (lane < NC) ys[lane] = (double)yv;
+    }
+    __syncthreads();
+    const int n4 = n & ~3;
+    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
+        Raw4<X> xr;
+        xr.load(x + i);
+        double t[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c0 = 0; c0 < NC; c0 += B) {
+            Raw4<T> v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) v[u].load(V + (int64_t)(c0 + u) * ld + i);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) {
+                    const double yu = ys[c0 + u];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) t[r] += v[u][r] * yu;
+                }
+        }
+        X xo[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xo[r] = (X)xr[r] + (X)(T)t[r];
+        Row4<X>::store(x + i, xo);
+    }
+    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) t += (double)V[(int64_t)j * ld + i] * ys[j];
+        x[i] = x[i] + (X)(T)t;
+    }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- plan object
@@ -1589,7 +1646,14 @@ int mpg_arnoldi_update(mpg_arnoldi_t a, int k) {
     int st = dispatch(a->combo, [&](auto t, auto x, auto, auto) {
         using T = decltype(t);
         using X = decltype(x);
-        if (k <= kWave) {
+        if (k <= kNC) {  // x is an aligned allocation: row groups of 4 are 16/32-B aligned
+            return with_nc<kNC>(k, [&](auto nc) {
+                k_update_x_nc<T, X, decltype(nc)::value><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+                    a->d.n, static_cast<const T*>(a->V), a->ld, static_cast<const T*>(a->s()),
+                    static_cast<const T*>(a->H), a->d.m + 1, static_cast<X*>(a->d.x));
+                return (int)MPG_OK;
+            });
+        } else if (k <= kWave) {
             k_update_x<T, X, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, static_cast<const T*>(a->s()),
                 static_cast<const T*>(a->H), a->d.m + 1, static_cast<X*>(a->d.x));
@@ -1600,7 +1664,7 @@ int mpg_arnoldi_update(mpg_arnoldi_t a, int k) {
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, static_cast<const T*>(a->s()), nullptr, 0,
                 static_cast<X*>(a->d.x));
         }
-        return MPG_OK;
+        return (int)MPG_OK;
     });
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);

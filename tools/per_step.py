@@ -35,7 +35,7 @@ def main():
         if cur is None:
             continue
         cur.append((k, d))
-        if k == "k_update_x":
+        if k.startswith("k_update_x"):
             cycles.append(cur)
             cur = None
     # keep the cycles of the most common shape (drops eagerly timed cycles
