@@ -158,3 +158,24 @@ def test_tiny_systems_match_oracle(mpg, oracle, engine, n):
     assert got.status == ref.status
     assert got.restarts == ref.restarts and got.total_iters == ref.total_iters
     assert np.array_equal(np.isfinite(got.step_res), np.isfinite(ref.step_res))
+
+
+@pytest.mark.parametrize("engine", ["fused", "fused-cgspart", "surface"])
+@pytest.mark.parametrize("orth", ["cgs", "mgs", "cgsr"])
+@pytest.mark.parametrize("mode", ["mixed", "baseline"])
+@pytest.mark.parametrize("rlen", [32, 33, 40, 70])
+def test_long_restart_matches_oracle(mpg, oracle, engine, orth, mode, rlen, monkeypatch):
+    """Restart lengths around and past the one-panel kernels' 32 columns:
+    m = 32 is the last compile-time column count, m > 32 runs the multi-panel
+    dots and the runtime-count CGS update / solution update, m > 64 also the
+    separate trsv and an unfolded Givens launch. Live oracle, same inputs."""
+    A = mpg.gen_band(3000, 5, 4, seed=11)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=rlen, tol=1e-10, max_restarts=30)
+    ref = oracle.solve(mpg, A, b, xt, **opts)
+    env = {"fused": {}, "fused-cgspart": {"MPG_CGS_PARTIALS": "1"}, "surface": {}}[engine]
+    for f in FLAGS:
+        monkeypatch.setenv(f, env.get(f, "1" if f in ("MPG_SELL_WINDOW", "MPG_FOLD_GIVENS") else "0"))
+    got = mpg.solve(A, b, xt, engine="surface" if engine == "surface" else "fused", **opts)
+    compare(as_ref(ref), got, mode, opts["tol"], rlen, f"band3000-{mode}-{orth}-m{rlen}-{engine}")
