@@ -144,13 +144,18 @@ __global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__
     for_rows<true>(  // once per cycle: keep V and the Arnoldi matrix cached
         blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)x[c]; },
         [&](int i, double sum) {
+            // the row's operands first (one latency, not one per operand)
+            const X bi = b[i], xi = x[i];
+            const P di = diag ? diag[i] : P(0);
             const X t = (X)sum;
-            const X r = b[i] - t;  // copy(b, w); spmv(-1, A, x, 1, w)
+            const X r = bi - t;  // copy(b, w); spmv(-1, A, x, 1, w)
             T wi = (T)r;
             acc[0] += (double)wi * (double)wi;
-            wi = precond<T, P>(wi, diag, i);
+            P pw = (P)wi;  // = precond<T, P> (typesafe_apply's rounding to P included)
+            if (diag) pw = P(0) * pw + P(1) * di * pw;
+            wi = (T)pw;
             acc[1] += (double)wi * (double)wi;
-            acc[2] += (double)x[i] * (double)x[i];
+            acc[2] += (double)xi * (double)xi;
             w[i] = wi;
         },
         prod, scratch);

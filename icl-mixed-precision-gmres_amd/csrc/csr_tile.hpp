@@ -135,6 +135,80 @@ __device__ __forceinline__ void stage_products(int s, int e, int64_t nnz_total, 
     }
 }
 
+// 4 consecutive values kept in their storage type until used (a raw load
+// into its final registers is not waited for until a consumer reads it)
+template <class V> struct RawVal4;
+template <> struct RawVal4<double> {
+    f64x2_t a, b;
+    template <bool NT> __device__ __forceinline__ void load(const double* p, int64_t i) {
+        a = ld_mat<NT>(reinterpret_cast<const f64x2_t*>(p + i));
+        b = ld_mat<NT>(reinterpret_cast<const f64x2_t*>(p + i + 2));
+    }
+    __device__ __forceinline__ double operator[](int q) const { return q == 0 ? a.x : q == 1 ? a.y : q == 2 ? b.x : b.y; }
+};
+template <> struct RawVal4<float> {
+    f32x4_t v;
+    template <bool NT> __device__ __forceinline__ void load(const float* p, int64_t i) {
+        v = ld_mat<NT>(reinterpret_cast<const f32x4_t*>(p + i));
+    }
+    __device__ __forceinline__ double operator[](int q) const {
+        return (double)(q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w);
+    }
+};
+template <> struct RawVal4<uint16_t> {
+    u16x4_t v;
+    template <bool NT> __device__ __forceinline__ void load(const uint16_t* p, int64_t i) {
+        v = ld_mat<NT>(reinterpret_cast<const u16x4_t*>(p + i));
+    }
+    __device__ __forceinline__ double operator[](int q) const {
+        return (double)to_float(q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w);
+    }
+};
+template <> struct RawVal4<half_v> : RawVal4<uint16_t> {
+    template <bool NT> __device__ __forceinline__ void load(const half_v* p, int64_t i) {
+        RawVal4<uint16_t>::load<NT>(reinterpret_cast<const uint16_t*>(p), i);
+    }
+};
+
+// stage_products for a block whose every 16-B vector lies inside the arrays
+// (e + 3 < nnz_total): every lane's loads are unconditional, at an address
+// clamped to the block's last vector, and every gather uses a loaded column
+// (an entry of the matrix, so a valid index); positions outside [s, e) are
+// masked at the store. Nothing is waited for until all loads are in flight
+// (a guarded load is widened or copied inside its branch, i.e. waited for
+// there).
+template <bool NT, class V, class XF>
+__device__ __forceinline__ void stage_products_interior(int s, int e, const int32_t* __restrict__ col,
+                                                        const V* __restrict__ val, XF xval,
+                                                        double* __restrict__ prod) {
+    const int base = s & ~3;
+    const int lastv = (e - 1) & ~3;
+    i32x4_t c[kVecPerLane];
+    RawVal4<V> v[kVecPerLane];
+#pragma unroll
+    for (int u = 0; u < kVecPerLane; ++u) {
+        const int idx = base + 4 * (threadIdx.x + u * kBlock);
+        const int idc = idx < lastv ? idx : lastv;
+        c[u] = ld_mat<NT>(reinterpret_cast<const i32x4_t*>(col + idc));
+        v[u].template load<NT>(val, idc);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double x[kVecPerLane][4];
+#pragma unroll
+    for (int u = 0; u < kVecPerLane; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[u][q] = xval(c[u][q]);
+#pragma unroll
+    for (int u = 0; u < kVecPerLane; ++u) {
+        const int idx = base + 4 * (threadIdx.x + u * kBlock);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = idx + q;
+            if (i >= s && i < e) prod[i - s] = v[u][q] * x[u][q];
+        }
+    }
+}
+
 // Row sums of one row block: epi(row, fp64 sum) is called once per row.
 template <bool NT = false, class V, class XF, class EPI>
 __device__ __forceinline__ void csr_row_block(int r0, int r1, const int32_t* __restrict__ rowptr,
@@ -149,10 +223,16 @@ __device__ __forceinline__ void csr_row_block(int r0, int r1, const int32_t* __r
         __syncthreads();  // the row's outputs are visible to the whole workgroup
         return;
     }
-    stage_products<NT>(s, e, nnz_total, col, val, xval, prod);
+    // this lane's first row bounds, loaded ahead of the tile
+    const int rf = r0 + (threadIdx.x < r1 - r0 ? threadIdx.x : 0);
+    const int ra = rowptr[rf], rz = rowptr[rf + 1];
+    __builtin_amdgcn_sched_barrier(0);
+    if (e > s && (int64_t)e + 3 < nnz_total) stage_products_interior<NT>(s, e, col, val, xval, prod);
+    else stage_products<NT>(s, e, nnz_total, col, val, xval, prod);
     __syncthreads();
     for (int r = threadIdx.x; r < r1 - r0; r += kBlock) {
-        const int a = rowptr[r0 + r] - s, z = rowptr[r0 + r + 1] - s;
+        const int a = (r == threadIdx.x ? ra : rowptr[r0 + r]) - s;
+        const int z = (r == threadIdx.x ? rz : rowptr[r0 + r + 1]) - s;
         double acc = 0.0;
         for (int j = a; j < z; ++j) acc += prod[j];
         epi(r0 + r, acc);
