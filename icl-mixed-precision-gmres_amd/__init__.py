@@ -160,6 +160,12 @@ for _t, _ct in (("f64", C.c_double), ("f32", C.c_float)):
     })
 _HIP_DECLS.update({
     "mpg_csr_spmv_f16f32": ([_P, _P, C.c_float, _P, _P, C.c_float, _P], C.c_int),
+    "mpg_sell_create": ([_P, _P, _I32, _P, _I32, C.POINTER(_P)], C.c_int),
+    "mpg_sell_destroy": ([_P], C.c_int),
+    "mpg_sell_layout": ([_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I64), C.POINTER(_I32)], C.c_int),
+    "mpg_sell_spmv_f64": ([_P, _P, C.c_double, _P, C.c_double, _P], C.c_int),
+    "mpg_sell_spmv_f32": ([_P, _P, C.c_float, _P, C.c_float, _P], C.c_int),
+    "mpg_sell_spmv_f16f32": ([_P, _P, C.c_float, _P, C.c_float, _P], C.c_int),
     "mpg_copy_f64f64": ([_P, _I64, _P, _P], C.c_int),
     "mpg_copy_f32f32": ([_P, _I64, _P, _P], C.c_int),
     "mpg_copy_f64f32": ([_P, _I64, _P, _P], C.c_int),

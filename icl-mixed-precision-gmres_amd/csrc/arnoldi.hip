@@ -362,7 +362,6 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
 // in LDS with three coalesced loads per lane and the gathers read LDS —
 // 10 scattered global loads per row become LDS reads (-20 % on BAND-10M,
 // tools/sell_bench.hip). Values are the same T(w_prev * inv) either way.
-constexpr int kWinLo = 64, kWinHi = 64, kWinLen = kWinLo + kWave + kWinHi;
 
 //
 // Load order (vmcnt retires in order, so what is needed first is issued
@@ -472,54 +471,6 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
         const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
         w[i] = precond<T, P>(t, diag, i);
         V[(int64_t)k * ld + i] = vk;
-    }
-}
-
-// min and max of (col - first row of its slice) over the matrix: int16
-// column eligibility and the LDS window of k_step_sell
-__global__ void k_sell_span(int n, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                            int* __restrict__ out) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    int lo = INT32_MAX, hi = INT32_MIN;
-    if (r < n) {
-        const int row0 = r & ~(kWave - 1);
-        for (int j = rowptr[r]; j < rowptr[r + 1]; ++j) {
-            const int d = col[j] - row0;
-            lo = min(lo, d);
-            hi = max(hi, d);
-        }
-    }
-    if (r < n && rowptr[r] < rowptr[r + 1]) {
-        atomicMin(out, lo);
-        atomicMax(out + 1, hi);
-    }
-}
-
-template <class VI> __device__ __forceinline__ typename SellStore<VI>::type sell_raw(VI v) { return v; }
-template <> __device__ __forceinline__ uint16_t sell_raw<half_v>(half_v v) { return v.bits; }
-
-// scatter the CSR (col, val) of row 64 s + lane into its slice; pads get the sentinel
-template <class VI, class CI, int W>
-__global__ void k_sell_fill(int n, int nslices, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                            const VI* __restrict__ val, const int64_t* __restrict__ off, CI* __restrict__ scol,
-                            typename SellStore<VI>::type* __restrict__ sval) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int s = (int)(t / kWave), lane = (int)(t % kWave);
-    if (s >= nslices) return;
-    const int r = s * kWave + lane;
-    const int64_t o = off[s];
-    const int width = (int)((off[s + 1] - o) / kWave);
-    const int b = r < n ? rowptr[r] : 0, len = r < n ? rowptr[r + 1] - b : 0;
-    for (int j = 0; j < width; ++j) {
-        const int64_t pos = o + (int64_t)(j / W) * kWave * W + lane * W + (j % W);
-        if (j < len) {
-            const int c = col[b + j];
-            scol[pos] = sizeof(CI) == 2 ? (CI)(c - s * kWave) : (CI)c;
-            sval[pos] = sell_raw(val[b + j]);
-        } else {
-            scol[pos] = SellCol<CI>::kPad;
-            sval[pos] = typename SellStore<VI>::type(0);
-        }
     }
 }
 
@@ -1159,16 +1110,7 @@ struct mpg_arnoldi {
     double* report = nullptr;   // 4 + m
     unsigned* counters = nullptr;  // last-arriver tickets: [0] dots, [32] CGS + Givens (zeroed at create)
     int Gd = 1;                    // workgroups (kCombineBlock threads) of the combining panel dots
-    // sliced-ELL copy of the Arnoldi matrix (nslices == 0: CSR row blocks)
-    struct {
-        int nslices = 0, W = 1;
-        bool c16 = false;
-        bool win = false;  // every slice's columns inside the LDS window
-        int64_t padded = 0;
-        int64_t* off = nullptr;
-        void* col = nullptr;
-        void* val = nullptr;
-    } sell;
+    SellCopy sell;  // sliced-ELL copy of the Arnoldi matrix (nslices == 0: CSR row blocks)
 
     char* small_at(int slot) const { return static_cast<char*>(small) + (size_t)slot * (d.m + 1) * tsize; }
     void* cs() const { return small_at(0); }
@@ -1221,96 +1163,9 @@ GivensArgs<T> givens_args(const mpg_arnoldi* a, int k) {
                          a->report};
 }
 
-template <class F>
-int sell_dispatch(int W, bool c16, F&& f) {
-    auto with_w = [&](auto ci) {
-        switch (W) {
-            case 1: return f(ci, std::integral_constant<int, 1>());
-            case 2: return f(ci, std::integral_constant<int, 2>());
-            case 4: return f(ci, std::integral_constant<int, 4>());
-            default: return (int)MPG_ERR_UNSUPPORTED;
-        }
-    };
-    return c16 ? with_w(int16_t()) : with_w(int32_t());
-}
-template <class F>
-int sell_dispatch_win(bool win, F&& f) {
-    return win ? f(std::true_type()) : f(std::false_type());
-}
-
-// Build the SELL-64 copy (format: 0 auto, 1 never, 2 always). Auto takes it
-// when padding adds at most 20% to the stored entries; W is the widest
-// vector (4, 2, 1) with the least padding.
-int sell_build(mpg_arnoldi* a, int format) {
-    const mpg_csr* A = a->d.A;
-    const int n = A->rows;
-    if (format == 1 || n == 0 || A->nnz == 0) return MPG_OK;
-    std::vector<int32_t> rp((size_t)n + 1);
-    if (hipMemcpyAsync(rp.data(), A->rowptr, rp.size() * 4, hipMemcpyDeviceToHost, a->ctx->stream) != hipSuccess ||
-        hipStreamSynchronize(a->ctx->stream) != hipSuccess)
-        return MPG_ERR_HIP;
-    const int ns = (n + kWave - 1) / kWave;
-    std::vector<int> width((size_t)ns, 0);
-    for (int r = 0; r < n; ++r) width[r / kWave] = std::max(width[r / kWave], rp[r + 1] - rp[r]);
-    // the widest vector whose padding stays within 15 % of the least padded
-    // layout: narrow (2-4 B per lane) index loads cost more than the padding
-    int64_t padded[5] = {0, 0, 0, 0, 0};
-    for (int W : {4, 2, 1})
-        for (int s = 0; s < ns; ++s) padded[W] += (int64_t)kWave * ((width[s] + W - 1) / W * W);
-    const int64_t least = std::min(padded[1], std::min(padded[2], padded[4]));
-    int best_w = 1;
-    for (int W : {4, 2, 1})
-        if ((double)padded[W] <= 1.15 * (double)least) {
-            best_w = W;
-            break;
-        }
-    const int64_t best = padded[best_w];
-    if (format == 0 && (double)best > 1.2 * (double)A->nnz) return MPG_OK;
-    if (best >= ((int64_t)1 << 31) * 4) return format == 2 ? MPG_ERR_UNSUPPORTED : MPG_OK;
-    std::vector<int64_t> off((size_t)ns + 1, 0);
-    for (int s = 0; s < ns; ++s)
-        off[s + 1] = off[s] + (int64_t)kWave * ((width[s] + best_w - 1) / best_w * best_w);
-
-    int* span = nullptr;
-    int span_h[2] = {INT32_MAX, INT32_MIN};
-    if (hipMalloc((void**)&span, 2 * sizeof(int)) != hipSuccess) return MPG_ERR_ALLOC;
-    bool ok = hipMemcpyAsync(span, span_h, 2 * sizeof(int), hipMemcpyHostToDevice, a->ctx->stream) == hipSuccess;
-    if (ok) {
-        k_sell_span<<<(n + kBlock - 1) / kBlock, kBlock, 0, a->ctx->stream>>>(n, A->rowptr, A->col, span);
-        ok = hipMemcpyAsync(span_h, span, 2 * sizeof(int), hipMemcpyDeviceToHost, a->ctx->stream) == hipSuccess &&
-             hipStreamSynchronize(a->ctx->stream) == hipSuccess;
-    }
-    (void)hipFree(span);
-    if (!ok) return MPG_ERR_HIP;
-    const bool c16 = span_h[0] >= -32767 && span_h[1] <= 32767;
-    const char* wenv = std::getenv("MPG_SELL_WINDOW");  // 0: always gather from global memory
-    const bool win = !(wenv && *wenv == '0') && span_h[0] >= -kWinLo && span_h[1] < kWave + kWinHi;
-    const size_t vsize = a->d.inner_val == MPG_F64 ? 8 : a->d.inner_val == MPG_F32 ? 4 : 2;
-    auto& S = a->sell;
-    if (hipMalloc((void**)&S.off, off.size() * 8) != hipSuccess ||
-        hipMalloc(&S.col, (size_t)best * (c16 ? 2 : 4) + 256) != hipSuccess ||
-        hipMalloc(&S.val, (size_t)best * vsize + 256) != hipSuccess)
-        return MPG_ERR_ALLOC;
-    if (hipMemcpyAsync(S.off, off.data(), off.size() * 8, hipMemcpyHostToDevice, a->ctx->stream) != hipSuccess)
-        return MPG_ERR_HIP;
-    S.nslices = ns;
-    S.W = best_w;
-    S.c16 = c16;
-    S.win = win;
-    S.padded = best;
-    const int grid = (int)(((int64_t)ns * kWave + kBlock - 1) / kBlock);
-    int st = dispatch(a->combo, [&](auto, auto, auto, auto vi) {
-        using VI = decltype(vi);
-        return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
-            using CI = decltype(ci);
-            k_sell_fill<VI, CI, decltype(wc)::value><<<grid, kBlock, 0, a->ctx->stream>>>(
-                n, ns, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), S.off, static_cast<CI*>(S.col),
-                static_cast<typename SellStore<VI>::type*>(S.val));
-            return (int)MPG_OK;
-        });
-    });
-    if (st) return st;
-    return hipStreamSynchronize(a->ctx->stream) == hipSuccess ? MPG_OK : MPG_ERR_HIP;
+// the Arnoldi SpMV's SELL copy of the inner-precision values
+int arnoldi_sell_build(mpg_arnoldi* a, int format) {
+    return sell_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, format, a->sell);
 }
 
 }  // namespace
@@ -1364,7 +1219,7 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
         mpg_arnoldi_destroy(a);
         return MPG_ERR_ARG;
     }
-    if (int st = sell_build(a, desc->spmv_format)) {
+    if (int st = arnoldi_sell_build(a, desc->spmv_format)) {
         mpg_arnoldi_destroy(a);
         return st;
     }
@@ -1388,9 +1243,10 @@ int mpg_arnoldi_destroy(mpg_arnoldi_t a) {
     if (!a) return MPG_OK;
     if (a->ctx) (void)hipStreamSynchronize(a->ctx->stream);
     void* ps[] = {a->V, a->H, a->small, a->w[0], a->w[1], a->partial, a->dpart, a->sums, a->report,
-                  a->counters, a->sell.off, a->sell.col, a->sell.val};
+                  a->counters};
     for (void* p : ps)
         if (p) (void)hipFree(p);
+    sell_free(a->sell);
     delete a;
     return MPG_OK;
 }

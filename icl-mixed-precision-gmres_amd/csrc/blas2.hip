@@ -46,6 +46,86 @@ __global__ __launch_bounds__(kBlock) void k_gemv_t_stage1(int64_t rows, int ncol
     }
 }
 
+// k_gemv_t_stage1 with the column count a compile-time constant (the
+// driver's gemv calls have k+1 <= 32 columns): every column index is static,
+// so a batch of columns' loads issues back to back instead of one guarded
+// load (and one memory latency) per column. One row per lane with scalar
+// loads: no alignment assumption on A, lda or x.
+template <class T, int NC>
+__global__ __launch_bounds__(kBlock) void k_gemv_t_nc(int64_t rows, const T* __restrict__ A, int64_t lda,
+                                                      const T* __restrict__ x, double* __restrict__ partial) {
+    constexpr int B = 16;
+    __shared__ double scratch[kBlock / kWave][NC];
+    double acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < rows; i += stride) {
+        const T xr = x[i];
+#pragma unroll
+        for (int c0 = 0; c0 < NC; c0 += B) {
+            T v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) v[u] = A[(int64_t)(c0 + u) * lda + i];
+            __builtin_amdgcn_sched_barrier(0);  // the batch's loads back to back
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) acc[c0 + u] += (double)v[u] * (double)xr;
+        }
+    }
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const double v = wave_sum(acc[c]);
+        if (lane == 0) scratch[wid][c] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NC) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kBlock / kWave; ++w) s += scratch[w][threadIdx.x];
+        partial[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+// k_gemv_n with a compile-time column count (batched loads, same order)
+template <class T, int NC>
+__global__ __launch_bounds__(kBlock) void k_gemv_n_nc(int64_t rows, T alpha, const T* __restrict__ A, int64_t lda,
+                                                      const T* __restrict__ x, T beta, T* __restrict__ y) {
+    constexpr int B = 16;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < rows; i += stride) {
+        const T yi = beta == T(0) ? T(0) : y[i];
+        double acc = 0.0;
+#pragma unroll
+        for (int c0 = 0; c0 < NC; c0 += B) {
+            T v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) v[u] = A[(int64_t)(c0 + u) * lda + i];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) acc += (double)v[u] * (double)x[c0 + u];
+        }
+        const T t = (T)acc;
+        y[i] = beta == T(0) ? alpha * t : alpha * t + beta * yi;
+    }
+}
+
+// f(integral_constant<int, nc>) for 1 <= nc <= N
+template <int N, class F>
+int with_cols(int nc, F&& f) {
+    if constexpr (N == 0) {
+        return MPG_ERR_ARG;
+    } else {
+        if (nc == N) return f(std::integral_constant<int, N>());
+        return with_cols<N - 1>(nc, f);
+    }
+}
+
 template <class T>
 __global__ __launch_bounds__(1024) void k_gemv_t_stage2(int nparts, const double* __restrict__ partial,
                                                         T alpha, T beta, T* __restrict__ y) {
@@ -78,7 +158,16 @@ int gemv_impl(mpg_ctx* ctx, int trans, int64_t rows, int64_t cols, T alpha, cons
     if (!ctx || rows < 0 || cols < 0 || (cols > 0 && lda < (rows > 0 ? rows : 1))) return MPG_ERR_ARG;
     if (!trans) {
         if (rows == 0) return MPG_OK;
-        k_gemv_n<T><<<grid_for(rows, 1), kBlock, 0, ctx->stream>>>(rows, cols, alpha, A, lda, x, beta, y);
+        if (cols >= 1 && cols <= kGemvMaxCols) {
+            const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto nc) {
+                k_gemv_n_nc<T, decltype(nc)::value><<<grid_for(rows, 1), kBlock, 0, ctx->stream>>>(
+                    rows, alpha, A, lda, x, beta, y);
+                return (int)MPG_OK;
+            });
+            if (st) return st;
+        } else {
+            k_gemv_n<T><<<grid_for(rows, 1), kBlock, 0, ctx->stream>>>(rows, cols, alpha, A, lda, x, beta, y);
+        }
         MPG_LAUNCH_CHECK(ctx);
         return MPG_OK;
     }
@@ -86,7 +175,12 @@ int gemv_impl(mpg_ctx* ctx, int trans, int64_t rows, int64_t cols, T alpha, cons
     int g = grid_for(rows, 4, kMaxRedBlocks);
     for (int64_t c0 = 0; c0 < cols; c0 += kGemvMaxCols) {
         int nc = (int)((cols - c0) < kGemvMaxCols ? (cols - c0) : kGemvMaxCols);
-        k_gemv_t_stage1<T><<<g, kBlock, 0, ctx->stream>>>(rows, nc, A + c0 * lda, lda, x, ctx->red_ws);
+        const int st = with_cols<kGemvMaxCols>(nc, [&](auto ncc) {
+            k_gemv_t_nc<T, decltype(ncc)::value><<<g, kBlock, 0, ctx->stream>>>(rows, A + c0 * lda, lda, x,
+                                                                               ctx->red_ws);
+            return (int)MPG_OK;
+        });
+        if (st) return st;
         MPG_LAUNCH_CHECK(ctx);
         k_gemv_t_stage2<T><<<nc, 1024, 0, ctx->stream>>>(g, ctx->red_ws, alpha, beta, y + c0);
         MPG_LAUNCH_CHECK(ctx);

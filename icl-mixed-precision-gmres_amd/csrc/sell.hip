@@ -1,0 +1,317 @@
+// SELL-64 copies of a CSR matrix (sell_tile.hpp) and the stand-alone SELL
+// SpMV behind the operator surface (replaces mkl_sparse_?_mv,
+// kernels_mkl.cpp:326-352, like mpg_csr_spmv, on the sliced copy).
+//
+// The builder is shared with the fused Arnoldi engine (arnoldi.hip), whose
+// SpMV phase runs on the same copy. A copy is worth it when padding the
+// slices to their longest row adds little (banded and stencil matrices);
+// the builder reports "no copy" otherwise and the caller keeps CSR.
+//
+// The SpMV issues its loads in the order they are needed (vmcnt retires in
+// issue order): the slice's offsets, the window of x (raw, clamped), y when
+// beta != 0, the first batch of (column, value) steps; nothing is waited for
+// before all of them are in flight. Sums are fp64 in CSR order, rounded
+// once to the vector type: y = alpha*t (+ beta*y), as spmv.hip.
+#include "sell_tile.hpp"
+#include "handoff.hpp"
+#include "internal.hpp"
+#include "mpgmres/arnoldi.h"
+#include "mpgmres/capi.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <new>
+#include <vector>
+
+using namespace mpg;
+
+namespace {
+
+// min and max of (col - first row of its slice) over the matrix: int16
+// column eligibility and the LDS window
+__global__ void k_sell_span(int n, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                            int* __restrict__ out) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    int lo = INT32_MAX, hi = INT32_MIN;
+    if (r < n) {
+        const int row0 = r & ~(kWave - 1);
+        for (int j = rowptr[r]; j < rowptr[r + 1]; ++j) {
+            const int d = col[j] - row0;
+            lo = min(lo, d);
+            hi = max(hi, d);
+        }
+    }
+    if (r < n && rowptr[r] < rowptr[r + 1]) {
+        atomicMin(out, lo);
+        atomicMax(out + 1, hi);
+    }
+}
+
+// scatter the CSR (col, val) of row 64 s + lane into its slice; pads get the
+// sentinel column and a zero value (S: stored value type, half as raw bits)
+template <class S, class CI, int W>
+__global__ void k_sell_fill(int n, int nslices, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                            const S* __restrict__ val, const int64_t* __restrict__ off, CI* __restrict__ scol,
+                            S* __restrict__ sval) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = (int)(t / kWave), lane = (int)(t % kWave);
+    if (s >= nslices) return;
+    const int r = s * kWave + lane;
+    const int64_t o = off[s];
+    const int width = (int)((off[s + 1] - o) / kWave);
+    const int b = r < n ? rowptr[r] : 0, len = r < n ? rowptr[r + 1] - b : 0;
+    for (int j = 0; j < width; ++j) {
+        const int64_t pos = o + (int64_t)(j / W) * kWave * W + lane * W + (j % W);
+        if (j < len) {
+            const int c = col[b + j];
+            scol[pos] = sizeof(CI) == 2 ? (CI)(c - s * kWave) : (CI)c;
+            sval[pos] = val[b + j];
+        } else {
+            scol[pos] = SellCol<CI>::kPad;
+            sval[pos] = S(0);
+        }
+    }
+}
+
+template <class F>
+int with_store(int vtype, F&& f) {
+    switch (vtype) {
+        case MPG_F64: return f(double());
+        case MPG_F32: return f(float());
+        case MPG_F16: return f(uint16_t());
+        default: return MPG_ERR_UNSUPPORTED;
+    }
+}
+
+// y = alpha * T(A x) (+ beta * y) on the sliced copy; one wave per slice
+template <class X, class S, class CI, int W, bool WIN>
+__global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslices, const int64_t* __restrict__ off,
+                                                      const CI* __restrict__ col, const S* __restrict__ val,
+                                                      const X* __restrict__ x, X alpha, X beta,
+                                                      X* __restrict__ y) {
+    constexpr int NQ = kWinLen / kWave;
+    __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int s = blockIdx.x * (kBlock / kWave) + wid;
+    if (s >= nslices) return;  // no workgroup barrier below: a dead wave may leave
+    const int row0 = s * kWave;
+    const int i = row0 + lane;
+    SellRow<S, CI, W> row;
+    row.init_load(s, off);
+    __builtin_amdgcn_sched_barrier(0);
+    X xr[WIN ? NQ : 1];
+    if constexpr (WIN) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int c = row0 - kWinLo + q * kWave + lane;
+            xr[q] = x[c >= 0 && c < cols ? c : 0];
+        }
+    }
+    const X yi = beta != X(0) ? y[i < n ? i : 0] : X(0);
+    __builtin_amdgcn_sched_barrier(0);
+    row.init_finish(lane, col, val);
+    row.load(0);
+    __builtin_amdgcn_sched_barrier(0);
+    double sum = 0.0;
+    if constexpr (WIN) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int c = row0 - kWinLo + q * kWave + lane;
+            win[wid][q * kWave + lane] = (c >= 0 && c < cols) ? xr[q] : X(0);
+        }
+        wave_lds_sync();
+        auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
+        row.sum(0, xv, sum);
+        for (int q = row.U; q < row.steps; q += row.U) {
+            row.load(q);
+            row.sum(q, xv, sum);
+        }
+    } else {
+        auto xv = [&](int c) { return (double)x[c]; };
+        row.sum(0, xv, sum);
+        for (int q = row.U; q < row.steps; q += row.U) {
+            row.load(q);
+            row.sum(q, xv, sum);
+        }
+    }
+    if (i < n) {
+        const X t = (X)sum;
+        y[i] = beta == X(0) ? alpha * t : alpha * t + beta * yi;
+    }
+}
+
+}  // namespace
+
+namespace mpg {
+
+int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int format, SellCopy& S) {
+    S = SellCopy{};
+    const int n = A->rows;
+    if (format == 1 || n == 0 || A->nnz == 0) return MPG_OK;
+    hipStream_t stream = ctx->stream;
+    std::vector<int32_t> rp((size_t)n + 1);
+    if (hipMemcpyAsync(rp.data(), A->rowptr, rp.size() * 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+        return MPG_ERR_HIP;
+    const int ns = (n + kWave - 1) / kWave;
+    std::vector<int> width((size_t)ns, 0);
+    for (int r = 0; r < n; ++r) width[r / kWave] = std::max(width[r / kWave], rp[r + 1] - rp[r]);
+    // the widest vector whose padding stays within 15 % of the least padded
+    // layout: narrow (2-4 B per lane) index loads cost more than the padding
+    int64_t padded[5] = {0, 0, 0, 0, 0};
+    for (int W : {4, 2, 1})
+        for (int s = 0; s < ns; ++s) padded[W] += (int64_t)kWave * ((width[s] + W - 1) / W * W);
+    const int64_t least = std::min(padded[1], std::min(padded[2], padded[4]));
+    int best_w = 1;
+    for (int W : {4, 2, 1})
+        if ((double)padded[W] <= 1.15 * (double)least) {
+            best_w = W;
+            break;
+        }
+    const int64_t best = padded[best_w];
+    if (format == 0 && (double)best > 1.2 * (double)A->nnz) return MPG_OK;
+    if (best >= ((int64_t)1 << 31) * 4) return format == 2 ? MPG_ERR_UNSUPPORTED : MPG_OK;
+    std::vector<int64_t> off((size_t)ns + 1, 0);
+    for (int s = 0; s < ns; ++s)
+        off[s + 1] = off[s] + (int64_t)kWave * ((width[s] + best_w - 1) / best_w * best_w);
+
+    int* span = nullptr;
+    int span_h[2] = {INT32_MAX, INT32_MIN};
+    if (hipMalloc((void**)&span, 2 * sizeof(int)) != hipSuccess) return MPG_ERR_ALLOC;
+    bool ok = hipMemcpyAsync(span, span_h, 2 * sizeof(int), hipMemcpyHostToDevice, stream) == hipSuccess;
+    if (ok) {
+        k_sell_span<<<(n + kBlock - 1) / kBlock, kBlock, 0, stream>>>(n, A->rowptr, A->col, span);
+        ok = hipMemcpyAsync(span_h, span, 2 * sizeof(int), hipMemcpyDeviceToHost, stream) == hipSuccess &&
+             hipStreamSynchronize(stream) == hipSuccess;
+    }
+    (void)hipFree(span);
+    if (!ok) return MPG_ERR_HIP;
+    const bool c16 = span_h[0] >= -32767 && span_h[1] <= 32767;
+    const char* wenv = std::getenv("MPG_SELL_WINDOW");  // 0: always gather from global memory
+    const bool win = !(wenv && *wenv == '0') && span_h[0] >= -kWinLo && span_h[1] < kWave + kWinHi;
+    const size_t vsize = vtype == MPG_F64 ? 8 : vtype == MPG_F32 ? 4 : 2;
+    if (hipMalloc((void**)&S.off, off.size() * 8) != hipSuccess ||
+        hipMalloc(&S.col, (size_t)best * (c16 ? 2 : 4) + 256) != hipSuccess ||
+        hipMalloc(&S.val, (size_t)best * vsize + 256) != hipSuccess) {
+        sell_free(S);
+        return MPG_ERR_ALLOC;
+    }
+    if (hipMemcpyAsync(S.off, off.data(), off.size() * 8, hipMemcpyHostToDevice, stream) != hipSuccess) {
+        sell_free(S);
+        return MPG_ERR_HIP;
+    }
+    S.n = n;
+    S.nslices = ns;
+    S.W = best_w;
+    S.vtype = vtype;
+    S.c16 = c16;
+    S.win = win;
+    S.padded = best;
+    const int grid = (int)(((int64_t)ns * kWave + kBlock - 1) / kBlock);
+    int st = with_store(vtype, [&](auto sv) {
+        using St = decltype(sv);
+        return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
+            using CI = decltype(ci);
+            k_sell_fill<St, CI, decltype(wc)::value><<<grid, kBlock, 0, stream>>>(
+                n, ns, A->rowptr, A->col, static_cast<const St*>(val), S.off, static_cast<CI*>(S.col),
+                static_cast<St*>(S.val));
+            return (int)MPG_OK;
+        });
+    });
+    if (!st && hipStreamSynchronize(stream) != hipSuccess) st = MPG_ERR_HIP;
+    if (st) sell_free(S);
+    return st;
+}
+
+void sell_free(SellCopy& S) {
+    if (S.off) (void)hipFree(S.off);
+    if (S.col) (void)hipFree(S.col);
+    if (S.val) (void)hipFree(S.val);
+    S = SellCopy{};
+}
+
+}  // namespace mpg
+
+struct mpg_sell {
+    mpg_ctx* ctx = nullptr;
+    int cols = 0;
+    SellCopy S;
+};
+
+namespace {
+
+template <class X, class St>
+int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y) {
+    if (!ctx || !A) return MPG_ERR_ARG;
+    const SellCopy& S = A->S;
+    if (S.nslices == 0) return MPG_OK;
+    const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
+    int st = sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
+        using CI = decltype(ci);
+        return sell_dispatch_win(S.win, [&](auto wn) {
+            k_sell_spmv<X, St, CI, decltype(wc)::value, decltype(wn)::value><<<grid, kBlock, 0, ctx->stream>>>(
+                S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val), x,
+                alpha, beta, y);
+            return (int)MPG_OK;
+        });
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpg_sell_create(mpg_ctx_t ctx, mpg_csr_t A, int32_t vtype, const void* vals, int32_t format, mpg_sell_t* out) {
+    if (!ctx || !A || !out || (A->nnz > 0 && !vals) || format < 0 || format > 2) return MPG_ERR_ARG;
+    if (vtype != MPG_F64 && vtype != MPG_F32 && vtype != MPG_F16) return MPG_ERR_UNSUPPORTED;
+    *out = nullptr;
+    mpg_sell* h = new (std::nothrow) mpg_sell();
+    if (!h) return MPG_ERR_ALLOC;
+    h->ctx = ctx;
+    h->cols = A->cols;
+    if (int st = sell_build(ctx, A, vtype, vals, format, h->S)) {
+        delete h;
+        return st;
+    }
+    if (h->S.nslices == 0) {  // padding would not pay: keep CSR
+        delete h;
+        return MPG_OK;
+    }
+    *out = h;
+    return MPG_OK;
+}
+
+int mpg_sell_destroy(mpg_sell_t A) {
+    if (!A) return MPG_OK;
+    if (A->ctx) (void)hipStreamSynchronize(A->ctx->stream);
+    sell_free(A->S);
+    delete A;
+    return MPG_OK;
+}
+
+int mpg_sell_layout(mpg_sell_t A, int32_t* vec_width, int32_t* col_bytes, int64_t* stored, int32_t* window) {
+    if (!A) return MPG_ERR_ARG;
+    if (vec_width) *vec_width = A->S.W;
+    if (col_bytes) *col_bytes = A->S.c16 ? 2 : 4;
+    if (stored) *stored = A->S.padded;
+    if (window) *window = A->S.win ? 1 : 0;
+    return MPG_OK;
+}
+
+int mpg_sell_spmv_f64(mpg_ctx_t c, mpg_sell_t A, double alpha, const double* x, double beta, double* y) {
+    if (A && A->S.vtype != MPG_F64) return MPG_ERR_ARG;
+    return sell_spmv_impl<double, double>(c, A, alpha, x, beta, y);
+}
+int mpg_sell_spmv_f32(mpg_ctx_t c, mpg_sell_t A, float alpha, const float* x, float beta, float* y) {
+    if (A && A->S.vtype != MPG_F32) return MPG_ERR_ARG;
+    return sell_spmv_impl<float, float>(c, A, alpha, x, beta, y);
+}
+int mpg_sell_spmv_f16f32(mpg_ctx_t c, mpg_sell_t A, float alpha, const float* x, float beta, float* y) {
+    if (A && A->S.vtype != MPG_F16) return MPG_ERR_ARG;
+    return sell_spmv_impl<float, uint16_t>(c, A, alpha, x, beta, y);
+}
+
+}  // extern "C"

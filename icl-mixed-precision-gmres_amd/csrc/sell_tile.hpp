@@ -18,6 +18,8 @@
 #include "internal.hpp"
 #include "csr_tile.hpp"
 
+#include <type_traits>
+
 namespace mpg {
 
 template <class CI> struct SellCol;
@@ -165,5 +167,46 @@ struct SellRow {
                 if (q + u < steps && SellCol<CI>::live(c[u][e])) acc += widen(v[u][e]) * x[u][e];
     }
 };
+
+// LDS window of x for a slice (SELL SpMVs): every column of every slice
+// within [row0 - kWinLo, row0 + 64 + kWinHi) lets the gathers read LDS
+constexpr int kWinLo = 64, kWinHi = 64, kWinLen = kWinLo + kWave + kWinHi;
+
+// A SELL-64 copy of one CSR value array (device memory owned by the copy).
+// nslices == 0: no copy (the CSR storage runs).
+struct SellCopy {
+    int n = 0, nslices = 0, W = 1;
+    int vtype = 0;     // mpg_dtype_t of the stored values (MPG_F64 | MPG_F32 | MPG_F16)
+    bool c16 = false;  // int16 slice-relative columns
+    bool win = false;  // every slice's columns inside the LDS window
+    int64_t padded = 0;
+    int64_t* off = nullptr;
+    void* col = nullptr;
+    void* val = nullptr;
+};
+
+// Build the copy from the CSR structure and `val` (vtype; F16 = raw IEEE
+// half bits). format: 0 auto (only when padding adds <= 20 % to the stored
+// entries), 1 never, 2 always. Synchronises the context's stream.
+int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int format, SellCopy& S);
+void sell_free(SellCopy& S);
+
+// f(column type, integral_constant<int, W>) for the copy's layout
+template <class F>
+int sell_dispatch(int W, bool c16, F&& f) {
+    auto with_w = [&](auto ci) {
+        switch (W) {
+            case 1: return f(ci, std::integral_constant<int, 1>());
+            case 2: return f(ci, std::integral_constant<int, 2>());
+            case 4: return f(ci, std::integral_constant<int, 4>());
+            default: return (int)MPG_ERR_UNSUPPORTED;
+        }
+    };
+    return c16 ? with_w(int16_t()) : with_w(int32_t());
+}
+template <class F>
+int sell_dispatch_win(bool win, F&& f) {
+    return win ? f(std::true_type()) : f(std::false_type());
+}
 
 }  // namespace mpg

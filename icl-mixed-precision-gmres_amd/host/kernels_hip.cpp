@@ -40,6 +40,12 @@ void check(int status, const char* what, mpg_ctx_t ctx) {
     throw std::runtime_error(os.str());
 }
 
+// MPG_SURFACE_SELL=0 keeps the operator surface's spmv on CSR
+bool surface_sell_enabled() {
+    const char* env = std::getenv("MPG_SURFACE_SELL");
+    return !(env && *env == '0');
+}
+
 mpg_ctx_t current_ctx() {
     if (!tl_ctx) {
         const char* env = std::getenv("MPG_DEVICE");
@@ -317,13 +323,15 @@ template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Ve
                                    Vect<double, Hip> y) {
     assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
                              : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
-    check(mpg_csr_spmv_f64(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
+    if (mpg_sell_t s = A.sell()) check(mpg_sell_spmv_f64(C, s, alpha, x.data(), beta, y.data()), "spmv");
+    else check(mpg_csr_spmv_f64(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
 }
 template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<float, Hip> x, float beta,
                                   Vect<float, Hip> y) {
     assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
                              : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
-    check(mpg_csr_spmv_f32(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
+    if (mpg_sell_t s = A.sell()) check(mpg_sell_spmv_f32(C, s, alpha, x.data(), beta, y.data()), "spmv");
+    else check(mpg_csr_spmv_f32(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
 }
 template <> void jacobi_diag<double, Hip>(SparseMatrix<double, Hip> A, Vect<double, Hip> d) {
     check(mpg_jacobi_setup_f64(C, A.csr(), A.vals_data(), d.data()), "jacobi setup");

@@ -36,6 +36,22 @@ public:
     ScopedContext& operator=(const ScopedContext&) = delete;
 };
 
+// The SELL-64 copy of one SparseMatrix's values (mpg_sell_create), shared by
+// the copies of that matrix (spmv takes A by value) and built on its first
+// non-transposed spmv, when the values are final. Absent (h == nullptr) when
+// slicing would not pay (format 0: padding > 20 %) or MPG_SURFACE_SELL=0.
+struct SellHolder {
+    bool tried = false;
+    mpg_sell_t h = nullptr;
+    SellHolder() = default;
+    SellHolder(const SellHolder&) = delete;
+    SellHolder& operator=(const SellHolder&) = delete;
+    ~SellHolder() {
+        if (h) mpg_sell_destroy(h);
+    }
+};
+bool surface_sell_enabled();
+
 // Device CSR structure shared by every precision of one matrix.
 struct CsrStructure {
     int m = 0, n = 0;
@@ -138,7 +154,21 @@ public:
     mpg_csr_t csr() const { return s_->csr.get(); }
     Vect<Type, Hip> vals_vect() const { return vals_; }
 
+    // the sliced copy spmv runs on, or nullptr (CSR): A only, not A^T
+    mpg_sell_t sell() const {
+        if (trans_ || !sell_) return nullptr;
+        if (!sell_->tried) {
+            sell_->tried = true;
+            if (mpg::surface_sell_enabled() && s_->nnz > 0)
+                mpg::check(mpg_sell_create(mpg::current_ctx(), csr(), sizeof(Type) == 8 ? 0 : 1, vals_.data(), 0,
+                                           &sell_->h),
+                           "mpg_sell_create");
+        }
+        return sell_->h;
+    }
+
 private:
+    std::shared_ptr<mpg::SellHolder> sell_ = std::make_shared<mpg::SellHolder>();
     bool trans_ = false;
     Vect<Type, Hip> tvals_;  // values in A^T's CSR order (set_transpose)
 };

@@ -43,6 +43,7 @@ typedef enum {
 
 typedef struct mpg_ctx* mpg_ctx_t;   /* one per (GPU, host thread) */
 typedef struct mpg_csr* mpg_csr_t;   /* analysed CSR structure (row blocks) */
+typedef struct mpg_sell* mpg_sell_t; /* SELL-64 copy of one CSR value array */
 
 const char* mpg_error_string(int status);
 /* Last HIP error text recorded in this context (for diagnostics). */
@@ -170,6 +171,22 @@ int mpg_csr_spmv_f32(mpg_ctx_t ctx, mpg_csr_t A, float alpha, const float* vals,
                      const float* x, float beta, float* y);
 int mpg_csr_spmv_f16f32(mpg_ctx_t ctx, mpg_csr_t A, float alpha, const uint16_t* vals_half,
                         const float* x, float beta, float* y);
+
+/* ---- SELL-64 SpMV: the same y = alpha*A x + beta*y (kernels_mkl.cpp:326-352)
+ * on a sliced-ELL copy (64-row slices padded to their longest row, int16
+ * slice-relative columns when they fit). mpg_sell_create copies one value
+ * array (vtype MPG_F64 | MPG_F32 | MPG_F16 raw half bits) of an analysed
+ * CSR; format 0 = only when padding adds <= 20 % to the stored entries
+ * (*out = NULL otherwise: keep mpg_csr_spmv), 2 = always. The copy owns its
+ * device memory and does not borrow vals afterwards; it synchronises. The
+ * spmv entry must match the copy's vtype (f64 / f32 / f16f32). */
+int mpg_sell_create(mpg_ctx_t ctx, mpg_csr_t A, int32_t vtype, const void* vals, int32_t format,
+                    mpg_sell_t* out);
+int mpg_sell_destroy(mpg_sell_t A);
+int mpg_sell_layout(mpg_sell_t A, int32_t* vec_width, int32_t* col_bytes, int64_t* stored, int32_t* window);
+int mpg_sell_spmv_f64(mpg_ctx_t ctx, mpg_sell_t A, double alpha, const double* x, double beta, double* y);
+int mpg_sell_spmv_f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y);
+int mpg_sell_spmv_f16f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y);
 
 /* A^T as its own CSR (SparseMatrix::set_transpose, types_cuda.hpp:145-151;
  * cusparse?csrmv TRANSPOSE, kernels_cuda.cpp:588-596; condest.cpp:49-50).

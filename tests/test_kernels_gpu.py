@@ -270,6 +270,60 @@ def test_spmv(hip, mpg, oracle, kind):
         hip.lib.mpg_csr_destroy(csr)
 
 
+@pytest.mark.parametrize("kind", ["band", "laplace", "longrows"])
+def test_sell_spmv(hip, mpg, oracle, kind):
+    """The SELL-64 copy (format 2: always, so the irregular longrows case is
+    sliced too) against the CSR SpMV on the same inputs. Both sum in fp64 in
+    CSR order and round once; for fp32/fp16 values the fp64 products are
+    exact, so the results agree to the last bit. With fp64 values the SELL
+    sum contracts product and add into one FMA while the CSR tile rounds the
+    product it stages in LDS: a few ulps of the row's scale apart."""
+    import ctypes as C
+
+    A = _spmv_case(mpg, kind)
+    n = A.nrows
+    g = rng(9)
+    x = g.uniform(-1, 1, A.ncols)
+    y0 = g.uniform(-1, 1, n)
+    drp, dci = hip.buf(A.rowptr), hip.buf(A.col)
+    csr = C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, n, A.ncols, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    sells = []
+    try:
+        v32 = A.val.astype(np.float32)
+        v16 = A.val.astype(np.float16).view(np.uint16)
+        cases = [("f64", 0, A.val, np.float64, -1.0, 1.0), ("f32", 1, v32, np.float32, 1.0, 0.0),
+                 ("f16f32", 2, v16, np.float32, 2.0, -0.5)]
+        for name, vt, vals, xdt, alpha, beta in cases:
+            dv = hip.buf(vals)
+            sell = C.c_void_p()
+            hip.check(hip.lib.mpg_sell_create(hip.ctx, csr, vt, dv.p, 2, C.byref(sell)))
+            assert sell.value
+            sells.append(sell)
+            dx = hip.buf(x.astype(xdt))
+            dy_sell, dy_csr = hip.buf(y0.astype(xdt)), hip.buf(y0.astype(xdt))
+            hip.call(f"mpg_sell_spmv_{name}", sell, xdt(alpha), dx.p, xdt(beta), dy_sell.p)
+            hip.call(f"mpg_csr_spmv_{name}", csr, xdt(alpha), dv.p, dx.p, xdt(beta), dy_csr.p)
+            if name == "f64":
+                scale = np.abs(y0) + abs(A.to_scipy()) @ np.abs(x)
+                assert np.all(np.abs(dy_sell.get() - dy_csr.get()) <= 4 * F64_EPS * scale), name
+            else:
+                assert np.array_equal(dy_sell.get(), dy_csr.get()), name
+        # format 0 declines the slices when padding would not pay
+        auto = C.c_void_p()
+        dv = hip.buf(A.val)
+        hip.check(hip.lib.mpg_sell_create(hip.ctx, csr, 0, dv.p, 0, C.byref(auto)))
+        if kind == "longrows":
+            assert not auto.value
+        else:
+            assert auto.value
+            sells.append(auto)
+    finally:
+        for h in sells:
+            hip.lib.mpg_sell_destroy(h)
+        hip.lib.mpg_csr_destroy(csr)
+
+
 @pytest.mark.parametrize("t", ["f64", "f32"])
 def test_jacobi_setup(hip, mpg, oracle, t):
     import ctypes as C

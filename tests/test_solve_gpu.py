@@ -28,8 +28,10 @@ def _case_id(c):
 # (engine, storage, environment): the fused engine on both Arnoldi SpMV
 # storages (CSR row blocks, SELL-64);: MPG_SELL_WINDOW=0 gathers v_k from memory
 # instead of the LDS window; the others are launch-count experiments
-FLAGS = ("MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS", "MPG_SELL_WINDOW")
-ENGINES = {"surface": ("surface", "auto", {}), "fused-csr": ("fused", "csr", {}),
+FLAGS = ("MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS", "MPG_SELL_WINDOW", "MPG_SURFACE_SELL")
+ON_BY_DEFAULT = ("MPG_SELL_WINDOW", "MPG_SURFACE_SELL")
+ENGINES = {"surface": ("surface", "auto", {}), "surface-csr": ("surface", "auto", {"MPG_SURFACE_SELL": "0"}),
+           "fused-csr": ("fused", "csr", {}),
            "fused-sell": ("fused", "sell", {}), "fused-gather": ("fused", "sell", {"MPG_SELL_WINDOW": "0"}),
            "fused-fold": ("fused", "auto", {"MPG_FOLD_GIVENS": "1"}),
            "fused-combine": ("fused", "auto", {"MPG_COMBINE": "1"}),
@@ -39,7 +41,7 @@ ENGINES = {"surface": ("surface", "auto", {}), "fused-csr": ("fused", "csr", {})
 def _engine(monkeypatch, engine):
     eng, fmt, env = ENGINES[engine]
     for f in FLAGS:
-        monkeypatch.setenv(f, env.get(f, "1" if f == "MPG_SELL_WINDOW" else "0"))
+        monkeypatch.setenv(f, env.get(f, "1" if f in ON_BY_DEFAULT else "0"))
     return dict(engine=eng, spmv_format=fmt)
 
 
@@ -176,6 +178,6 @@ def test_long_restart_matches_oracle(mpg, oracle, engine, orth, mode, rlen, monk
     ref = oracle.solve(mpg, A, b, xt, **opts)
     env = {"fused": {}, "fused-cgspart": {"MPG_CGS_PARTIALS": "1"}, "surface": {}}[engine]
     for f in FLAGS:
-        monkeypatch.setenv(f, env.get(f, "1" if f in ("MPG_SELL_WINDOW", "MPG_FOLD_GIVENS") else "0"))
+        monkeypatch.setenv(f, env.get(f, "1" if f in ON_BY_DEFAULT + ("MPG_FOLD_GIVENS",) else "0"))
     got = mpg.solve(A, b, xt, engine="surface" if engine == "surface" else "fused", **opts)
     compare(as_ref(ref), got, mode, opts["tol"], rlen, f"band3000-{mode}-{orth}-m{rlen}-{engine}")

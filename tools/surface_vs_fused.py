@@ -1,0 +1,33 @@
+"""GMRES it/s of the operator-surface driver (the reference gmres.cpp control
+flow over kernels_hip.cpp) against the fused engine on BAND-10M, mixed
+GMRES(30), 5 restart cycles each.
+
+usage: python tools/surface_vs_fused.py [orth ...] [--engines surface,fused]"""
+import sys
+
+sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+from __graft_entry__ import _load
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    engines = ["surface", "fused"]
+    for a in sys.argv[1:]:
+        if a.startswith("--engines="):
+            engines = a.split("=", 1)[1].split(",")
+    orths = args or ["cgs", "mgs"]
+    mpg = _load()
+    A = mpg.gen_band(1_000_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    for orth in orths:
+        for eng in engines:
+            opts = dict(engine=eng, mode="mixed", orth=orth, prec="identity", rlen=30, tol=0.0)
+            mpg.solve(A, b, xt, max_restarts=1, **opts)
+            r = mpg.solve(A, b, xt, max_restarts=5, **opts)
+            print(orth, eng, r.total_iters, "iters", round(r.gmres_seconds, 4), "s",
+                  round(r.total_iters / r.gmres_seconds, 1), "it/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
