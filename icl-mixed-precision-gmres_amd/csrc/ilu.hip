@@ -13,6 +13,7 @@
 #include <limits>
 #include <new>
 #include <type_traits>
+#include <vector>
 
 #include "handoff.hpp"
 #include "internal.hpp"
@@ -25,6 +26,13 @@ namespace {
 constexpr int kRowCap = 512;                 // entries of one row staged in LDS
 constexpr int kWaves = kBlock / kWave;       // 4 rows in flight per workgroup
 constexpr int kPersistGroups = 2048;         // 8 workgroups per CU
+// level-scheduled solves: few spinning waves. 64 workgroups (one per CU on a
+// quarter of the chip, 256 waves) solve LAP-1M's L and U in 3.0 ms; 2048
+// workgroups flood the memory system with flag polls (waits past 2 s at
+// 90^3 and up), 512: 5.1 ms, 256: 3.6 ms (tools/ilu_debug.py). Loading the
+// rows' values with sc1 loads instead of the wave's one agent acquire gained
+// 4 %: a hop (drain, flag, poll, loads) is ~5 us either way.
+constexpr int kSolveGroups = 64;
 constexpr uint64_t kDeadline = 3000000000ull;  // 30 s of the 100 MHz clock: a wave gives up (fault 2)
 
 // sync block layout (ints): [0, n) factor / L flags, [n, 2n) U flags, then
@@ -154,12 +162,22 @@ __global__ void k_dinv(int n, const int* __restrict__ diag, const T* __restrict_
 }
 
 // ---------------------------------------------------------------- triangular solves
-// x := L^-1 x (unit lower) or U^-1 x (upper), in place, sync-free: row i
-// waits for the rows its off-diagonal entries read, then
-// x_i = T((x_i - sum_j a_ij x_j) [/ u_ii]) with the sum in fp64 (lane
-// partials in CSR order, then a fixed xor tree).
+// x := L^-1 x (unit lower) or U^-1 x (upper), in place, level-scheduled and
+// sync-free. mpg_ilu0_create sorts the rows by dependency level (a row's
+// level is one more than the highest level among the rows its off-diagonal
+// entries read) and cuts every level into chunks of <= 64 rows, so the rows
+// of a chunk never depend on each other. A wave takes the next chunk from an
+// atomic ticket (chunks in level order: a wave only waits for rows of
+// earlier chunks, taken by running waves, so the schedule always
+// progresses), and each lane solves one row: it waits for the flags of the
+// rows it reads, the wave takes one agent-scope acquire, then the lane
+// forms x_i = T((x_i - sum_j a_ij x_j) [/ u_ii]) with the sum in fp64 in CSR
+// order, stores it write-through, drains, and raises the row's flag.
+// One row per lane (the previous form took one row per wave, one ticket per
+// row, 2048 workgroups): LAP-1M's L + U solves from ~40 ms to 3.0 ms.
 template <class T, bool UPPER>
-__global__ __launch_bounds__(kBlock) void k_ilu_trsv(int n, const int* __restrict__ rowptr,
+__global__ __launch_bounds__(kBlock) void k_ilu_trsv(int nchunks, const int* __restrict__ chunk,
+                                                     const int* __restrict__ ord, const int* __restrict__ rowptr,
                                                      const int* __restrict__ col, const int* __restrict__ diag,
                                                      const T* __restrict__ lu, T* x, int* done, unsigned* ticket,
                                                      int* err) {
@@ -173,24 +191,27 @@ __global__ __launch_bounds__(kBlock) void k_ilu_trsv(int n, const int* __restric
         int t = 0;
         if (lane == 0) t = (int)__hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t = __shfl(t, 0, kWave);
-        if (t >= n) break;
-        const int row = UPPER ? n - 1 - t : t;
-        const int d = diag[row];
-        const int j0 = UPPER ? d + 1 : rowptr[row];
-        const int j1 = UPPER ? rowptr[row + 1] : d;
-        for (int j = j0 + lane; j < j1; j += kWave) wait_flag(done + col[j], err);
+        if (t >= nchunks) break;
+        const int c0 = chunk[t], cnt = chunk[t + 1] - c0;
+        const bool live = lane < cnt;
+        int row = 0, d = 0, j0 = 0, j1 = 0;
+        if (live) {
+            row = ord[c0 + lane];
+            d = diag[row];
+            j0 = UPPER ? d + 1 : rowptr[row];
+            j1 = UPPER ? rowptr[row + 1] : d;
+            for (int j = j0; j < j1; ++j) wait_flag(done + col[j], err);
+        }
         acquire_agent();
-        double s = 0.0;
-        for (int j = j0 + lane; j < j1; j += kWave) s += (double)lu[j] * (double)x[col[j]];
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, kWave);
-        if (lane == 0) {
+        if (live) {
+            double s = 0.0;
+            for (int j = j0; j < j1; ++j) s += (double)lu[j] * (double)x[col[j]];
             double r = (double)x[row] - s;
             if (UPPER) r = r / (double)lu[d];
             store_wt(x + row, (T)r);
         }
         drain_stores();
-        if (lane == 0) set_flag(done + row);
+        if (live) set_flag(done + row);
     }
 }
 
@@ -236,6 +257,12 @@ struct mpg_ilu {
     int* sync = nullptr;
     void* w[2] = {nullptr, nullptr};  // ILU-Jacobi: right-hand side and the second sweep buffer
     unsigned long long* scratch = nullptr;
+    // level schedules of the two triangular solves: rows by level, and
+    // chunk starts (<= 64 rows, never across a level) into that order
+    int* ord[2] = {nullptr, nullptr};
+    int* chunk[2] = {nullptr, nullptr};
+    int nchunks[2] = {0, 0};
+    int levels[2] = {0, 0};
 
     size_t tsize() const { return type == 0 ? 8 : 4; }
     void* values() const { return type == 0 ? (void*)lu64 : (void*)lu32; }
@@ -259,6 +286,35 @@ int reset_sync(mpg_ilu* L) {
 }
 
 int persist_grid(int n) { return std::max(1, std::min(kPersistGroups, (n + kWaves - 1) / kWaves)); }
+
+// Level schedule of one triangular solve from host copies of the structure
+// (upper: the rows after the diagonal, solved last row first).
+void level_schedule(int n, const std::vector<int>& rp, const std::vector<int>& ci, const std::vector<int>& dg,
+                    bool upper, std::vector<int>& ord, std::vector<int>& chunk, int& nlev) {
+    std::vector<int> lev((size_t)n, 0);
+    nlev = 0;
+    for (int t = 0; t < n; ++t) {
+        const int i = upper ? n - 1 - t : t;
+        const int j0 = upper ? dg[i] + 1 : rp[i], j1 = upper ? rp[i + 1] : dg[i];
+        int l = 0;
+        for (int j = j0; j < j1; ++j) l = std::max(l, lev[ci[j]] + 1);
+        lev[i] = l;
+        nlev = std::max(nlev, l + 1);
+    }
+    std::vector<int> start((size_t)nlev + 1, 0);
+    for (int i = 0; i < n; ++i) ++start[(size_t)lev[i] + 1];
+    for (int l = 0; l < nlev; ++l) start[(size_t)l + 1] += start[l];
+    ord.assign((size_t)n, 0);
+    std::vector<int> fill(start.begin(), start.end() - 1);
+    for (int t = 0; t < n; ++t) {
+        const int i = upper ? n - 1 - t : t;
+        ord[(size_t)fill[lev[i]]++] = i;
+    }
+    chunk.clear();
+    for (int l = 0; l < nlev; ++l)
+        for (int c = start[l]; c < start[(size_t)l + 1]; c += kWave) chunk.push_back(c);
+    chunk.push_back(n);
+}
 
 }  // namespace
 
@@ -306,6 +362,25 @@ int mpg_ilu0_create(mpg_ctx_t ctx, mpg_csr_t A, const double* val64, int type, m
     if (!ok(hipMemcpyAsync(&bad_h, bad, 4, hipMemcpyDeviceToHost, s)) || !ok(hipStreamSynchronize(s)))
         return fail(MPG_ERR_HIP);
     if (bad_h) return fail(MPG_ERR_UNSUPPORTED);  // a row without its diagonal, or longer than kRowCap
+    {  // level schedules of the two triangular solves (host, O(nnz), once)
+        std::vector<int> rp((size_t)n + 1), ci((size_t)std::max<int64_t>(L->nnz, 1)), dg((size_t)n);
+        if (!ok(hipMemcpyAsync(rp.data(), A->rowptr, rp.size() * 4, hipMemcpyDeviceToHost, s)) ||
+            (L->nnz && !ok(hipMemcpyAsync(ci.data(), A->col, (size_t)L->nnz * 4, hipMemcpyDeviceToHost, s))) ||
+            !ok(hipMemcpyAsync(dg.data(), L->diag, dg.size() * 4, hipMemcpyDeviceToHost, s)) ||
+            !ok(hipStreamSynchronize(s)))
+            return fail(MPG_ERR_HIP);
+        for (int u = 0; u < 2; ++u) {
+            std::vector<int> ord, chunk;
+            level_schedule(n, rp, ci, dg, u == 1, ord, chunk, L->levels[u]);
+            L->nchunks[u] = (int)chunk.size() - 1;
+            if (!ok(hipMalloc((void**)&L->ord[u], ord.size() * 4)) ||
+                !ok(hipMalloc((void**)&L->chunk[u], chunk.size() * 4)) ||
+                !ok(hipMemcpyAsync(L->ord[u], ord.data(), ord.size() * 4, hipMemcpyHostToDevice, s)) ||
+                !ok(hipMemcpyAsync(L->chunk[u], chunk.data(), chunk.size() * 4, hipMemcpyHostToDevice, s)) ||
+                !ok(hipStreamSynchronize(s)))
+                return fail(MPG_ERR_ALLOC);
+        }
+    }
     const double eps = type == 0 ? (double)std::numeric_limits<double>::epsilon()
                                  : (double)std::numeric_limits<float>::epsilon();
     k_ilu0_factor<<<persist_grid(n), kBlock, 0, s>>>(n, A->rowptr, A->col, L->diag, L->lu64, eps, L->scratch,
@@ -335,7 +410,8 @@ int mpg_ilu0_create(mpg_ctx_t ctx, mpg_csr_t A, const double* val64, int type, m
 int mpg_ilu_destroy(mpg_ilu_t L) {
     if (!L) return MPG_OK;
     if (L->ctx) (void)hipStreamSynchronize(L->ctx->stream);
-    void* ps[] = {L->lu64, L->lu32, L->diag, L->dinv, L->sync, L->w[0], L->w[1], L->scratch};
+    void* ps[] = {L->lu64,   L->lu32,   L->diag,     L->dinv,     L->sync,    L->w[0],
+                  L->w[1],   L->scratch, L->ord[0],  L->ord[1],   L->chunk[0], L->chunk[1]};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete L;
@@ -346,15 +422,23 @@ int mpg_ilu_solve(mpg_ctx_t ctx, mpg_ilu_t L, void* x) {
     if (!ctx || !L || (!x && L->n)) return MPG_ERR_ARG;
     if (L->n == 0) return MPG_OK;
     if (int st = reset_sync(L)) return st;
-    const int n = L->n, g = persist_grid(n);
+    const int n = L->n;
+    // one wave per chunk in flight at most: a wave per 64 rows, <= 8 workgroups per CU
+    static const int cap = [] {
+        const char* e = std::getenv("MPG_ILU_GROUPS");  // experiment: cap on the solve grid
+        return e && std::atoi(e) > 0 ? std::atoi(e) : kSolveGroups;
+    }();
+    auto grid = [&](int u) { return std::max(1, std::min(cap, (L->nchunks[u] + kWaves - 1) / kWaves)); };
     int st = by_type(L->type, [&](auto t) {
         using T = decltype(t);
         const T* lu = static_cast<const T*>(L->values());
         T* xv = static_cast<T*>(x);
-        k_ilu_trsv<T, false><<<g, kBlock, 0, ctx->stream>>>(n, L->A->rowptr, L->A->col, L->diag, lu, xv, L->sync,
-                                                             L->ticket(1), L->err());
-        k_ilu_trsv<T, true><<<g, kBlock, 0, ctx->stream>>>(n, L->A->rowptr, L->A->col, L->diag, lu, xv,
-                                                            L->sync + n, L->ticket(2), L->err());
+        k_ilu_trsv<T, false><<<grid(0), kBlock, 0, ctx->stream>>>(L->nchunks[0], L->chunk[0], L->ord[0],
+                                                                    L->A->rowptr, L->A->col, L->diag, lu, xv, L->sync,
+                                                                    L->ticket(1), L->err());
+        k_ilu_trsv<T, true><<<grid(1), kBlock, 0, ctx->stream>>>(L->nchunks[1], L->chunk[1], L->ord[1], L->A->rowptr,
+                                                                  L->A->col, L->diag, lu, xv, L->sync + n,
+                                                                  L->ticket(2), L->err());
         return (int)MPG_OK;
     });
     if (st) return st;
