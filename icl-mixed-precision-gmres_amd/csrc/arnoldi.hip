@@ -55,15 +55,17 @@ __device__ __forceinline__ void my_blocks(int nblocks, int& rb0, int& rb1) {
 // For every row of this workgroup's row blocks: fp64 sum of val * xval(col)
 // (csr_tile.hpp), then epi(row, sum) on one lane. NT: non-temporal matrix
 // loads (a pass that runs once per restart cycle).
-template <bool NT = false, class V, class XF, class EPI>
+template <bool NT = false, class V, class XF, class PF, class EPI>
 __device__ __forceinline__ void for_rows(const int32_t* __restrict__ blocks, int nblocks,
                                          const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                                         const V* __restrict__ val, int64_t nnz, XF xval, EPI epi, double* prod,
-                                         double* scratch) {
+                                         const V* __restrict__ val, int64_t nnz, XF xval, PF pre, EPI epi,
+                                         double* prod, double* scratch) {
+    const int32_t* __restrict__ bnnz = blocks + nblocks + 1;  // mpg_csr's nnz starts follow the row starts
     int rb0, rb1;
     my_blocks(nblocks, rb0, rb1);
     for (int b = rb0; b < rb1; ++b)
-        csr_row_block<NT>(blocks[b], blocks[b + 1], rowptr, col, val, nnz, xval, epi, prod, scratch);
+        csr_row_block<NT>(blocks[b], blocks[b + 1], bnnz[b], bnnz[b + 1], rowptr, col, val, nnz, xval, pre, epi, prod,
+                          scratch);
 }
 
 // One transpose round on the first 2H accumulators: lanes with the MASK bit
@@ -141,12 +143,16 @@ __global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    struct Ops {
+        X b, x;
+        P d;
+    };
     for_rows<true>(  // once per cycle: keep V and the Arnoldi matrix cached
         blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)x[c]; },
-        [&](int i, double sum) {
-            // the row's operands first (one latency, not one per operand)
-            const X bi = b[i], xi = x[i];
-            const P di = diag ? diag[i] : P(0);
+        [&](int i) { return Ops{b[i], x[i], diag ? diag[i] : P(0)}; },
+        [&](int i, double sum, const Ops& o) {
+            const X bi = o.b, xi = o.x;
+            const P di = o.d;
             const X t = (X)sum;
             const X r = bi - t;  // copy(b, w); spmv(-1, A, x, 1, w)
             T wi = (T)r;
@@ -344,12 +350,19 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
     __shared__ double scratch[kBlock / kWave];
     const T inv = fold_givens<FOLD>(fold, inv_p);
     T* __restrict__ Vk = V + (int64_t)k * ld;
+    struct Ops {
+        T wp;
+        P d;
+    };
     for_rows(
         blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)(T)(wprev[c] * inv); },
-        [&](int i, double sum) {
+        [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0)}; },
+        [&](int i, double sum, const Ops& o) {
             const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
-            w[i] = precond<T, P>(t, diag, i);
-            Vk[i] = wprev[i] * inv;
+            P pw = (P)t;         // = precond<T, P> with the diagonal loaded ahead
+            if (diag) pw = P(0) * pw + P(1) * o.d * pw;
+            w[i] = (T)pw;
+            Vk[i] = o.wp * inv;
         },
         prod, scratch);
 }

@@ -209,33 +209,38 @@ __device__ __forceinline__ void stage_products_interior(int s, int e, const int3
     }
 }
 
-// Row sums of one row block: epi(row, fp64 sum) is called once per row.
-template <bool NT = false, class V, class XF, class EPI>
-__device__ __forceinline__ void csr_row_block(int r0, int r1, const int32_t* __restrict__ rowptr,
+// Row sums of one row block: epi(row, fp64 sum, pre(row)) is called once per
+// row. pre(row) loads the row's epilogue operands; for this lane's first row
+// it is issued ahead of the tile, so its latency hides under the tile's.
+template <bool NT = false, class V, class XF, class PF, class EPI>
+__device__ __forceinline__ void csr_row_block(int r0, int r1, int s, int e, const int32_t* __restrict__ rowptr,
                                               const int32_t* __restrict__ col, const V* __restrict__ val,
-                                              int64_t nnz_total, XF xval, EPI epi, double* prod, double* scratch) {
-    const int s = rowptr[r0], e = rowptr[r1];
+                                              int64_t nnz_total, XF xval, PF pre, EPI epi, double* prod,
+                                              double* scratch) {
+    // s, e = rowptr[r0], rowptr[r1] (the analysis' nnz starts of the block)
     if (r1 - r0 == 1) {
         double acc = 0.0;
         for (int i = s + threadIdx.x; i < e; i += kBlock) acc += scalar_val(val, i) * xval(col[i]);
         const double sum = block_sum<kBlock>(acc, scratch);
-        if (threadIdx.x == 0) epi(r0, sum);
+        if (threadIdx.x == 0) epi(r0, sum, pre(r0));
         __syncthreads();  // the row's outputs are visible to the whole workgroup
         return;
     }
-    // this lane's first row bounds, loaded ahead of the tile
+    // this lane's first row: bounds and epilogue operands, loaded ahead of the tile
     const int rf = r0 + (threadIdx.x < r1 - r0 ? threadIdx.x : 0);
     const int ra = rowptr[rf], rz = rowptr[rf + 1];
+    const auto pf = pre(rf);
     __builtin_amdgcn_sched_barrier(0);
     if (e > s && (int64_t)e + 3 < nnz_total) stage_products_interior<NT>(s, e, col, val, xval, prod);
     else stage_products<NT>(s, e, nnz_total, col, val, xval, prod);
     __syncthreads();
     for (int r = threadIdx.x; r < r1 - r0; r += kBlock) {
-        const int a = (r == threadIdx.x ? ra : rowptr[r0 + r]) - s;
-        const int z = (r == threadIdx.x ? rz : rowptr[r0 + r + 1]) - s;
+        const bool first = r == threadIdx.x;
+        const int a = (first ? ra : rowptr[r0 + r]) - s;
+        const int z = (first ? rz : rowptr[r0 + r + 1]) - s;
         double acc = 0.0;
         for (int j = a; j < z; ++j) acc += prod[j];
-        epi(r0 + r, acc);
+        epi(r0 + r, acc, first ? pf : pre(r0 + r));
     }
     __syncthreads();
 }

@@ -27,7 +27,8 @@ struct mpg_csr {
     int64_t nnz = 0;
     const int32_t* rowptr = nullptr;  // device, borrowed
     const int32_t* col = nullptr;     // device, borrowed
-    int32_t* blocks = nullptr;        // device, owned: nblocks+1 row starts
+    int32_t* blocks = nullptr;        // device, owned: nblocks+1 row starts, then nblocks+1 nnz starts
+    int32_t* bnnz = nullptr;          // = blocks + nblocks + 1: rowptr[blocks[b]] (one load, not two dependent)
     int nblocks = 0;
 };
 

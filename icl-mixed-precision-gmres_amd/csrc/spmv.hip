@@ -28,6 +28,7 @@ namespace {
 
 template <class V, class X>
 __global__ __launch_bounds__(kBlock) void k_csr_adaptive(const int32_t* __restrict__ blocks,
+                                                         const int32_t* __restrict__ bnnz,
                                                          const int32_t* __restrict__ rowptr,
                                                          const int32_t* __restrict__ col,
                                                          const V* __restrict__ val, int64_t nnz,
@@ -37,10 +38,11 @@ __global__ __launch_bounds__(kBlock) void k_csr_adaptive(const int32_t* __restri
     __shared__ double scratch[kBlock / kWave];
     const int b = blockIdx.x;
     csr_row_block(
-        blocks[b], blocks[b + 1], rowptr, col, val, nnz, [&](int c) { return (double)x[c]; },
-        [&](int i, double sum) {
+        blocks[b], blocks[b + 1], bnnz[b], bnnz[b + 1], rowptr, col, val, nnz, [&](int c) { return (double)x[c]; },
+        [&](int i) { return beta == X(0) ? X(0) : y[i]; },
+        [&](int i, double sum, X yi) {
             const X t = (X)sum;
-            y[i] = beta == X(0) ? alpha * t : alpha * t + beta * y[i];
+            y[i] = beta == X(0) ? alpha * t : alpha * t + beta * yi;
         },
         prod, scratch);
 }
@@ -49,7 +51,7 @@ template <class V, class X>
 int spmv_impl(mpg_ctx* ctx, mpg_csr* A, X alpha, const V* vals, const X* x, X beta, X* y) {
     if (!ctx || !A) return MPG_ERR_ARG;
     if (A->rows == 0) return MPG_OK;
-    k_csr_adaptive<V, X><<<A->nblocks, kBlock, 0, ctx->stream>>>(A->blocks, A->rowptr, A->col, vals, A->nnz, x,
+    k_csr_adaptive<V, X><<<A->nblocks, kBlock, 0, ctx->stream>>>(A->blocks, A->bnnz, A->rowptr, A->col, vals, A->nnz, x,
                                                                  alpha, beta, y);
     MPG_LAUNCH_CHECK(ctx);
     return MPG_OK;
@@ -163,9 +165,12 @@ int mpg_csr_create(mpg_ctx_t ctx, int32_t rows, int32_t cols, int64_t nnz, const
     A->rowptr = rowptr_dev;
     A->col = col_dev;
     A->nblocks = (int)starts.size() - 1;
+    const size_t nb = starts.size();
+    for (size_t b = 0; b < nb; ++b) starts.push_back(rowptr_host[starts[b]]);  // nnz start of each block
     hipError_t e = hipMalloc(&A->blocks, starts.size() * sizeof(int32_t));
     if (e == hipSuccess)
         e = hipMemcpy(A->blocks, starts.data(), starts.size() * sizeof(int32_t), hipMemcpyHostToDevice);
+    A->bnnz = A->blocks + nb;
     if (e != hipSuccess) {
         if (A->blocks) (void)hipFree(A->blocks);
         delete A;
