@@ -69,8 +69,15 @@ struct FusedEngine::Impl {
     const void* val_inner = nullptr;
     mpg_csr_t csr = nullptr;
     mpg_arnoldi_t arn = nullptr;
-    double* report_host = nullptr;  // pinned
+    double* rep[2] = {nullptr, nullptr};  // pinned report buffers (two: pipelined cycles)
+    double* report_host = nullptr;       // = rep[0] or rep[1]: the report the host works on
     int report_len = 0;
+    // pipelined cycles: the next cycle's graph is launched before this
+    // cycle's report is read; it starts by saving x, so a cycle launched past
+    // a stop decision is undone by restoring x
+    bool pipeline = true;
+    DevMem x_snap;
+    hipEvent_t report_ev[2] = {nullptr, nullptr};
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     bool use_graph = true;
@@ -88,7 +95,10 @@ struct FusedEngine::Impl {
         if (graph) (void)hipGraphDestroy(graph);
         if (arn) mpg_arnoldi_destroy(arn);
         if (csr) mpg_csr_destroy(csr);
-        if (report_host) (void)hipHostFree(report_host);
+        for (double* r : rep)
+            if (r) (void)hipHostFree(r);
+        for (hipEvent_t e : report_ev)
+            if (e) (void)hipEventDestroy(e);
     }
     hipStream_t stream() const { return static_cast<hipStream_t>(mpg_ctx_stream(ctx)); }
 
@@ -279,7 +289,12 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     // ranks all-reduce per-workgroup partials in place: same count on every rank
     if (comm) check(mpg_arnoldi_uniform_groups(I.arn), "uniform groups", ctx);
     I.report_len = mpg_arnoldi_report_len(I.arn);
-    hipck(hipHostMalloc((void**)&I.report_host, (size_t)I.report_len * sizeof(double), 0), "hipHostMalloc");
+    for (double*& r : I.rep) hipck(hipHostMalloc((void**)&r, (size_t)I.report_len * sizeof(double), 0), "hipHostMalloc");
+    I.report_host = I.rep[0];
+    for (hipEvent_t& e : I.report_ev) hipck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+    const char* qenv = std::getenv("MPG_PIPELINE");  // 0: read each cycle's report before the next launch
+    I.pipeline = !(qenv && *qenv == '0');
+    if (I.pipeline) I.x_snap = DevMem(ctx, (size_t)I.n_ext * dsize(ty.X) + 64);
 
     // convergence strategy (gmres_perf_test.cpp:185-196)
     const size_t mm = (size_t)a.rlen, mr = (size_t)a.max_restarts;
@@ -434,6 +449,8 @@ void FusedEngine::read_report(int count) {
 // steps 0..m-1, solution update with k = m, next residual prologue
 void FusedEngine::cycle_program() {
     Impl& I = *p_;
+    if (I.pipeline)  // the cycle may run past a stop decision: keep the x it started from
+        hipck(hipMemcpyAsync(I.x_snap.p, I.x.p, I.x.bytes, hipMemcpyDeviceToDevice, I.stream()), "x snapshot");
     const bool fold = I.fold;
     for (int k = 0; k < I.m; ++k) step(k, fold);
     if (fold) givens(I.m - 1);
@@ -469,11 +486,94 @@ bool FusedEngine::check_start(int64_t i) {
     }
 }
 
+// capture the cycle program once; if the runtime refuses (e.g. a collective
+// that cannot be captured) fall back to eager launches for good
+void FusedEngine::ensure_graph() {
+    Impl& I = *p_;
+    if (!I.use_graph || I.graph_exec) return;
+    hipck(hipStreamBeginCapture(I.stream(), hipStreamCaptureModeThreadLocal), "begin capture");
+    bool ok = true;
+    try {
+        cycle_program();
+    } catch (const std::exception& ex) {
+        ok = false;
+        std::fprintf(stderr, "mpgmres: cycle capture failed (%s); running eagerly\n", ex.what());
+    }
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(I.stream(), &g);
+    if (ok && ec == hipSuccess && hipGraphInstantiate(&I.graph_exec, g, nullptr, nullptr, 0) == hipSuccess) {
+        I.graph = g;
+    } else {
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        I.use_graph = false;
+    }
+}
+
+// the base strategy's per-step bookkeeping for one cycle's report
+void FusedEngine::record_steps(int64_t i) {
+    Impl& I = *p_;
+    for (int k = 0; k < I.m; ++k) {
+        const double res = I.report_host[4 + k];
+        step_res.push_back(res);
+        step_cycle.push_back((int)i);
+        conv_->check((size_t)k + 1, res, minvb_norm);  // base strategy: counts, restarts at m
+    }
+}
+
+// Graph cycles with the host round trip hidden: cycle i+1 is launched before
+// cycle i's report is read, so the GPU never waits for the host's
+// check_initial (≈ 38 us per cycle on BAND-10M: the report copy, the
+// stream synchronisation and the next launch). A cycle launched past a stop
+// decision (converged or aborted at check_initial) is undone by restoring the
+// x it started from (it cannot have changed anything else the result reads);
+// no cycle is ever left in flight when run() returns.
+int FusedEngine::run_pipelined(int max_cycles, bool& done) {
+    Impl& I = *p_;
+    int64_t i = (int64_t)cycles.size();
+    if (check_start(i)) {
+        done = true;
+        return 0;
+    }
+    if (max_cycles <= 0) return 0;
+    // one replay of the captured cycle, then its report into rep[p], marked by report_ev[p]
+    auto launch = [&](int p) {
+        hipck(hipGraphLaunch(I.graph_exec, I.stream()), "graph launch");
+        hipck(hipMemcpyAsync(I.rep[p], mpg_arnoldi_report_dev(I.arn), (size_t)I.report_len * sizeof(double),
+                             hipMemcpyDeviceToHost, I.stream()),
+              "report d2h");
+        hipck(hipEventRecord(I.report_ev[p], I.stream()), "event record");
+    };
+    // the buffer not holding the report check_start just read
+    int p = I.report_host == I.rep[0] ? 1 : 0, ran = 0;
+    launch(p);
+    for (;;) {
+        const bool more = ran + 1 < max_cycles;
+        if (more) launch(p ^ 1);  // speculative: decided by this cycle's report
+        hipck(hipEventSynchronize(I.report_ev[p]), "report wait");
+        I.report_host = I.rep[p];
+        record_steps(i);
+        ++ran;
+        ++i;
+        if (!more) return ran;
+        if (check_start(i)) {  // stop: undo the cycle launched past it
+            done = true;
+            sync();
+            hipck(hipMemcpyAsync(I.x.p, I.x_snap.p, I.x.bytes, hipMemcpyDeviceToDevice, I.stream()), "x restore");
+            sync();
+            return ran;
+        }
+        p ^= 1;
+    }
+}
+
 int FusedEngine::run(int max_cycles, bool& done) {
     Impl& I = *p_;
     done = false;
     int ran = 0;
     const bool stepwise = conv_->needs_arnoldi_residual();
+    if (!stepwise) ensure_graph();
+    if (!stepwise && I.use_graph && I.pipeline) return run_pipelined(max_cycles, done);
     for (; ran < max_cycles; ++ran) {
         const int64_t i = (int64_t)cycles.size();
         if (check_start(i)) {
@@ -481,37 +581,10 @@ int FusedEngine::run(int max_cycles, bool& done) {
             return ran;
         }
         if (!stepwise) {
-            if (I.use_graph && !I.graph_exec) {
-                // capture once; if the runtime refuses (e.g. a collective that
-                // cannot be captured) fall back to eager launches for good
-                hipck(hipStreamBeginCapture(I.stream(), hipStreamCaptureModeThreadLocal), "begin capture");
-                bool ok = true;
-                try {
-                    cycle_program();
-                } catch (const std::exception& ex) {
-                    ok = false;
-                    std::fprintf(stderr, "mpgmres: cycle capture failed (%s); running eagerly\n", ex.what());
-                }
-                hipGraph_t g = nullptr;
-                const hipError_t ec = hipStreamEndCapture(I.stream(), &g);
-                if (ok && ec == hipSuccess &&
-                    hipGraphInstantiate(&I.graph_exec, g, nullptr, nullptr, 0) == hipSuccess) {
-                    I.graph = g;
-                } else {
-                    if (g) (void)hipGraphDestroy(g);
-                    (void)hipGetLastError();
-                    I.use_graph = false;
-                }
-            }
             if (I.use_graph) hipck(hipGraphLaunch(I.graph_exec, I.stream()), "graph launch");
             else cycle_program();
             read_report(I.report_len);
-            for (int k = 0; k < I.m; ++k) {
-                const double res = I.report_host[4 + k];
-                step_res.push_back(res);
-                step_cycle.push_back((int)i);
-                conv_->check((size_t)k + 1, res, minvb_norm);  // base strategy: counts, restarts at m
-            }
+            record_steps(i);
             continue;
         }
         // adaptive restart strategies: one host read of |s(k+1)| per step

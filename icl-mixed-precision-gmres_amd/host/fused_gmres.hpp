@@ -105,6 +105,9 @@ private:
     void update(int k);
     void read_report(int count);
     void cycle_program();
+    void ensure_graph();
+    void record_steps(int64_t i);
+    int run_pipelined(int max_cycles, bool& done);
     bool check_start(int64_t i);
 };
 
