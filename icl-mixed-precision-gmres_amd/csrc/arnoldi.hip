@@ -168,6 +168,82 @@ __global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__
     store_partials<4>(acc, 3, partial);
 }
 
+// The same prologue on a SELL-64 copy of the outer-precision values (one
+// wave per slice, one lane per row; loads issued in need order as in
+// k_step_sell): r = b - A x (X), w = M(T(r)), partials ||T(r)||^2,
+// ||w||^2, ||x||^2 per workgroup.
+template <class T, class X, class P, class CI, int W, bool WIN>
+__global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_ext, int nslices, const int64_t* __restrict__ off,
+                                                          const CI* __restrict__ col, const X* __restrict__ val,
+                                                          const X* __restrict__ x, const X* __restrict__ b,
+                                                          const P* __restrict__ diag, T* __restrict__ w,
+                                                          double* __restrict__ partial) {
+    constexpr int NQ = kWinLen / kWave;
+    __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int s = blockIdx.x * (kBlock / kWave) + wid;
+    const bool live = s < nslices;  // a dead wave still joins the partials' barrier
+    const int row0 = s * kWave;
+    const int i = row0 + lane;
+    const bool own = live && i < n;
+    SellRow<X, CI, W, true> row;  // once per cycle: non-temporal slices
+    row.init_load(live ? s : 0, off);
+    __builtin_amdgcn_sched_barrier(0);
+    X xr[WIN ? NQ : 1];
+    if constexpr (WIN) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int c = row0 - kWinLo + q * kWave + lane;
+            xr[q] = x[c >= 0 && c < n_ext ? c : 0];
+        }
+    }
+    const int ic = own ? i : 0;
+    const X bi = b[ic], xi = x[ic];
+    const P di = diag ? diag[ic] : P(0);
+    __builtin_amdgcn_sched_barrier(0);
+    row.init_finish(lane, col, val);
+    row.load(0);
+    __builtin_amdgcn_sched_barrier(0);
+    double sum = 0.0;
+    if (live) {
+        if constexpr (WIN) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int c = row0 - kWinLo + q * kWave + lane;
+                win[wid][q * kWave + lane] = (c >= 0 && c < n_ext) ? xr[q] : X(0);
+            }
+            wave_lds_sync();
+            auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
+            row.sum(0, xv, sum);
+            for (int q = row.U; q < row.steps; q += row.U) {
+                row.load(q);
+                row.sum(q, xv, sum);
+            }
+        } else {
+            auto xv = [&](int c) { return (double)x[c]; };
+            row.sum(0, xv, sum);
+            for (int q = row.U; q < row.steps; q += row.U) {
+                row.load(q);
+                row.sum(q, xv, sum);
+            }
+        }
+    }
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (own) {
+        const X t = (X)sum;
+        const X r = bi - t;  // copy(b, w); spmv(-1, A, x, 1, w)
+        T wi = (T)r;
+        acc[0] = (double)wi * (double)wi;
+        P pw = (P)wi;  // = precond<T, P>
+        if (diag) pw = P(0) * pw + P(1) * di * pw;
+        wi = (T)pw;
+        acc[1] = (double)wi * (double)wi;
+        acc[2] = (double)xi * (double)xi;
+        w[i] = wi;
+    }
+    store_partials<4>(acc, 3, partial);
+}
+
 template <class T, class X>
 __global__ void k_prologue_finish(const double* __restrict__ sums, int m, T* __restrict__ s, T* __restrict__ inv,
                                   double* __restrict__ report) {
@@ -1124,6 +1200,8 @@ struct mpg_arnoldi {
     unsigned* counters = nullptr;  // last-arriver tickets: [0] dots, [32] CGS + Givens (zeroed at create)
     int Gd = 1;                    // workgroups (kCombineBlock threads) of the combining panel dots
     SellCopy sell;  // sliced-ELL copy of the Arnoldi matrix (nslices == 0: CSR row blocks)
+    SellCopy sell_outer;        // ... of the outer-precision values, for the residual prologue
+    bool outer_is_inner = false;  // the prologue runs on `sell` (baseline / single modes)
 
     char* small_at(int slot) const { return static_cast<char*>(small) + (size_t)slot * (d.m + 1) * tsize; }
     void* cs() const { return small_at(0); }
@@ -1178,7 +1256,13 @@ GivensArgs<T> givens_args(const mpg_arnoldi* a, int k) {
 
 // the Arnoldi SpMV's SELL copy of the inner-precision values
 int arnoldi_sell_build(mpg_arnoldi* a, int format) {
-    return sell_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, format, a->sell);
+    if (int st = sell_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, format, a->sell)) return st;
+    if (a->sell.nslices == 0) return MPG_OK;
+    // the residual prologue on the same slicing: shared when the residual and
+    // Arnoldi matrices are the same array, else a copy of the outer values
+    a->outer_is_inner = a->d.val_outer == a->d.val_inner && a->d.outer_type == a->d.inner_val;
+    if (a->outer_is_inner) return MPG_OK;
+    return sell_build(a->ctx, a->d.A, a->d.outer_type, a->d.val_outer, 2, a->sell_outer);
 }
 
 }  // namespace
@@ -1260,6 +1344,7 @@ int mpg_arnoldi_destroy(mpg_arnoldi_t a) {
     for (void* p : ps)
         if (p) (void)hipFree(p);
     sell_free(a->sell);
+    sell_free(a->sell_outer);
     delete a;
     return MPG_OK;
 }
@@ -1271,13 +1356,30 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
         using T = decltype(t);
         using X = decltype(x);
         using P = decltype(p);
+        const P* diag = a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr;
+        const SellCopy* S = a->outer_is_inner ? &a->sell : &a->sell_outer;
+        if (S->nslices > 0 && S->vtype == a->d.outer_type) {
+            const int grid = (S->nslices + kBlock / kWave - 1) / (kBlock / kWave);
+            a->last_G = grid;
+            return sell_dispatch(S->W, S->c16, [&](auto ci, auto wc) {
+                using CI = decltype(ci);
+                return sell_dispatch_win(S->win, [&](auto wn) {
+                    k_prologue_sell<T, X, P, CI, decltype(wc)::value, decltype(wn)::value>
+                        <<<grid, kBlock, 0, a->ctx->stream>>>(
+                            a->d.n, a->d.n_ext, S->nslices, S->off, static_cast<const CI*>(S->col),
+                            static_cast<const X*>(S->val), static_cast<const X*>(a->d.x),
+                            static_cast<const X*>(a->d.b), diag, static_cast<T*>(a->w[0]), a->partial);
+                    return (int)MPG_OK;
+                });
+            });
+        }
+        a->last_G = rb_grid(a);
         k_prologue<T, X, P><<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(
             A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const X*>(a->d.val_outer), A->nnz,
-            static_cast<const X*>(a->d.x), static_cast<const X*>(a->d.b),
-            a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr, static_cast<T*>(a->w[0]), a->partial);
-        return MPG_OK;
+            static_cast<const X*>(a->d.x), static_cast<const X*>(a->d.b), diag, static_cast<T*>(a->w[0]),
+            a->partial);
+        return (int)MPG_OK;
     });
-    a->last_G = rb_grid(a);
     a->last_part = a->partial;
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
@@ -1288,8 +1390,9 @@ int mpg_arnoldi_prologue_wnorm(mpg_arnoldi_t a) {
     if (!a) return MPG_ERR_ARG;
     int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
         using T = decltype(t);
-        k_wnorm_partials<T><<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->w[0]),
-                                                                      a->partial);
+        // the prologue's grid (CSR row blocks or SELL slices): column 1 of its partials
+        k_wnorm_partials<T><<<a->last_G, kBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->w[0]),
+                                                                     a->partial);
         return (int)MPG_OK;
     });
     if (st) return st;

@@ -46,17 +46,17 @@ template <> __device__ __forceinline__ double widen<uint16_t>(uint16_t v) { retu
 #define MPG_SELL_NT 0
 #endif
 
-// W consecutive elements with one aligned vector load
-template <class S, int W> struct VecW {
+// W consecutive elements with one aligned vector load (NT: non-temporal)
+template <class S, int W, bool NT = (MPG_SELL_NT != 0)> struct VecW {
     typedef S vtype __attribute__((ext_vector_type(W)));
     static __device__ __forceinline__ void load(const S* p, S (&o)[W]) {
-        const vtype v = ld_policy<MPG_SELL_NT != 0>(reinterpret_cast<const vtype*>(p));
+        const vtype v = ld_policy<NT>(reinterpret_cast<const vtype*>(p));
 #pragma unroll
         for (int e = 0; e < W; ++e) o[e] = v[e];
     }
 };
-template <class S> struct VecW<S, 1> {
-    static __device__ __forceinline__ void load(const S* p, S (&o)[1]) { o[0] = ld_policy<MPG_SELL_NT != 0>(p); }
+template <class S, bool NT> struct VecW<S, 1, NT> {
+    static __device__ __forceinline__ void load(const S* p, S (&o)[1]) { o[0] = ld_policy<NT>(p); }
 };
 
 // entries per lane per batch: every load of a batch is issued before its
@@ -113,7 +113,9 @@ __device__ __forceinline__ double sell_row_sum(int s, int lane, const int64_t* _
 // by step index at use, so nothing widens or selects a loaded value at load
 // time (which would wait for it on the spot). An empty slice points at
 // offset 0 of the arrays.
-template <class S, class CI, int W>
+// NT: non-temporal slice loads (a pass that runs once per restart cycle, so
+// the slices the Arnoldi steps re-read stay in the Infinity Cache)
+template <class S, class CI, int W, bool NT = (MPG_SELL_NT != 0)>
 struct SellRow {
     static constexpr int U = sell_unroll<W>();
     CI c[U][W];
@@ -145,8 +147,8 @@ struct SellRow {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int qq = q + u < last ? q + u : last;
-            VecW<CI, W>::load(cp + (int64_t)qq * kWave * W, c[u]);
-            VecW<S, W>::load(vp + (int64_t)qq * kWave * W, v[u]);
+            VecW<CI, W, NT>::load(cp + (int64_t)qq * kWave * W, c[u]);
+            VecW<S, W, NT>::load(vp + (int64_t)qq * kWave * W, v[u]);
         }
     }
     // acc += the batch loaded at step q, in CSR order. Every gather is issued
