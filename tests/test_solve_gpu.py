@@ -181,3 +181,26 @@ def test_long_restart_matches_oracle(mpg, oracle, engine, orth, mode, rlen, monk
         monkeypatch.setenv(f, env.get(f, "1" if f in ON_BY_DEFAULT + ("MPG_FOLD_GIVENS",) else "0"))
     got = mpg.solve(A, b, xt, engine="surface" if engine == "surface" else "fused", **opts)
     compare(as_ref(ref), got, mode, opts["tol"], rlen, f"band3000-{mode}-{orth}-m{rlen}-{engine}")
+
+
+@pytest.mark.parametrize("mode", ["mixed", "baseline"])
+@pytest.mark.parametrize("stop", ["converged", "aborted"])
+def test_pipelined_cycles_match_serial(mpg, mode, stop, monkeypatch):
+    """The pipelined cycle loop (the next cycle's graph is launched before
+    this cycle's report is read; a cycle launched past the stop decision is
+    undone by restoring x) gives bit-identical results to the serial loop,
+    for a solve that converges and one that aborts at max_restarts."""
+    A = mpg.gen_band(50_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(engine="fused", mode=mode, orth="cgs", prec="jacobi", rlen=30,
+                tol=1e-9 if stop == "converged" else 0.0, max_restarts=40 if stop == "converged" else 3)
+    got = {}
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("MPG_PIPELINE", pipe)
+        got[pipe] = mpg.solve(A, b, xt, **opts)
+    p, s = got["1"], got["0"]
+    assert p.status == s.status == stop
+    assert p.total_iters == s.total_iters and p.restarts == s.restarts
+    assert np.array_equal(p.step_res, s.step_res)
+    assert p.res_norm == s.res_norm and p.err_norm == s.err_norm
