@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <limits>
 #include <new>
 #include <type_traits>
@@ -215,6 +216,118 @@ __global__ __launch_bounds__(kBlock) void k_ilu_trsv(int nchunks, const int* __r
     }
 }
 
+// The same solve for matrices whose dependency levels hold few rows (banded:
+// every level one row, depth n), where the level schedule pays a flag
+// hand-off (~2 us) per row: ONE workgroup runs the recurrence serially.
+// Lane 0 of wave 0 solves the rows of a stage in processing order from LDS,
+// keeping the x values it produced in an LDS ring of kRing rows
+// (eligibility: every dependency lies within kRing rows); waves 1-3 stage
+// the next stage's operands meanwhile (right-hand sides, pivots, and each
+// row's off-diagonal entries as ring slots + values, padded to a multiple of
+// kPass with zero products on a zero slot). The chain per row is then one
+// LDS round trip (the x reads, issued after the previous row's ring write)
+// plus the fp64 arithmetic: the next row's slots, values and right-hand side
+// are read while the current row finishes. The arithmetic is the level
+// kernel's -- fp64 sum in CSR order, rounded once; a padded term adds an
+// exact +0 (the sum never holds -0) -- so both modes give identical results.
+constexpr int kRing = 2048, kStageRows = 256, kStageEnt = 1536, kPass = 8;
+template <class T>
+struct SerialStage {
+    T rhs[kStageRows + 1];
+    T piv[kStageRows + 1];
+    int eend[kStageRows + 1];        // end of each row's padded entries
+    uint16_t slot[kStageEnt + kPass];  // ring slot of each entry's column (kRing: the zero slot)
+    T elu[kStageEnt + kPass];
+};
+
+template <class T, bool UPPER>
+__global__ __launch_bounds__(kBlock) void k_ilu_trsv_serial(int n, int nstages, const int* __restrict__ stage,
+                                                            const int* __restrict__ eoff,
+                                                            const int* __restrict__ rowptr,
+                                                            const int* __restrict__ col, const int* __restrict__ diag,
+                                                            const T* __restrict__ lu, T* __restrict__ x) {
+    __shared__ T ring[kRing + 1];
+    __shared__ SerialStage<T> buf[2];
+    auto row_of = [&](int p) { return UPPER ? n - 1 - p : p; };
+    // waves 1-3: the operands of stage t into buf[t & 1]
+    auto load = [&](int t) {
+        SerialStage<T>& B = buf[t & 1];
+        const int p0 = stage[t], p1 = stage[t + 1], e0 = eoff[p0];
+        for (int p = p0 + (int)threadIdx.x - kWave; p < p1; p += kBlock - kWave) {
+            const int row = row_of(p), d = diag[row];
+            const int j0 = UPPER ? d + 1 : rowptr[row], j1 = UPPER ? rowptr[row + 1] : d;
+            const int eb = eoff[p] - e0, ee = eoff[p + 1] - e0;
+            B.rhs[p - p0] = x[row];
+            if (UPPER) B.piv[p - p0] = lu[d];
+            B.eend[p - p0] = ee;
+            int e = eb;
+            for (int j = j0; j < j1; ++j, ++e) {
+                B.slot[e] = (uint16_t)(col[j] & (kRing - 1));
+                B.elu[e] = lu[j];
+            }
+            for (; e < ee; ++e) {
+                B.slot[e] = (uint16_t)kRing;
+                B.elu[e] = T(0);
+            }
+        }
+    };
+    if (threadIdx.x == 0) ring[kRing] = T(0);
+    if (threadIdx.x >= kWave) load(0);
+    __syncthreads();
+    for (int t = 0; t < nstages; ++t) {
+        if (threadIdx.x >= kWave) {
+            if (t + 1 < nstages) load(t + 1);
+        } else if (threadIdx.x == 0) {
+            const SerialStage<T>& B = buf[t & 1];
+            const int p0 = stage[t], p1 = stage[t + 1];
+            // row p's operands, read one row ahead
+            int eb = 0, ee = B.eend[0];
+            T rhs = B.rhs[0], piv = UPPER ? B.piv[0] : T(1);
+            int sl[kPass];
+            T a[kPass];
+#pragma unroll
+            for (int k = 0; k < kPass; ++k) {
+                sl[k] = B.slot[k];
+                a[k] = B.elu[k];
+            }
+            for (int p = p0; p < p1; ++p) {
+                T xv[kPass];
+#pragma unroll
+                for (int k = 0; k < kPass; ++k) xv[k] = ring[sl[k]];
+                double s = 0.0;
+#pragma unroll
+                for (int k = 0; k < kPass; ++k) s += (double)a[k] * (double)xv[k];
+                for (int e = eb + kPass; e < ee; e += kPass) {  // rows of more than kPass entries
+#pragma unroll
+                    for (int k = 0; k < kPass; ++k) xv[k] = ring[B.slot[e + k]];
+#pragma unroll
+                    for (int k = 0; k < kPass; ++k) s += (double)B.elu[e + k] * (double)xv[k];
+                }
+                // the next row's operands (past the stage's last row: unused reads within the arrays)
+                const int q = p + 1 - p0;
+                const int nb = ee, ne = B.eend[q];
+                const T nrhs = B.rhs[q], npiv = UPPER ? B.piv[q] : T(1);
+#pragma unroll
+                for (int k = 0; k < kPass; ++k) {
+                    sl[k] = B.slot[nb + k];
+                    a[k] = B.elu[nb + k];
+                }
+                double r = (double)rhs - s;
+                if (UPPER) r = r / (double)piv;
+                const int row = row_of(p);
+                const T v = (T)r;
+                ring[row & (kRing - 1)] = v;
+                x[row] = v;
+                eb = nb;
+                ee = ne;
+                rhs = nrhs;
+                piv = npiv;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------- ILU-Jacobi
 // One Jacobi sweep on L (x_new = x + (b - (x + L_s x))) or on U
 // (x_new = x + d∘(b - U x)), with the reference's operation order
@@ -263,6 +376,12 @@ struct mpg_ilu {
     int* chunk[2] = {nullptr, nullptr};
     int nchunks[2] = {0, 0};
     int levels[2] = {0, 0};
+    // serial mode (few rows per level): stage starts and off-diagonal entry
+    // offsets in processing order
+    bool serial[2] = {false, false};
+    int* stage[2] = {nullptr, nullptr};
+    int* eoff[2] = {nullptr, nullptr};
+    int nstages[2] = {0, 0};
 
     size_t tsize() const { return type == 0 ? 8 : 4; }
     void* values() const { return type == 0 ? (void*)lu64 : (void*)lu32; }
@@ -288,6 +407,35 @@ int reset_sync(mpg_ilu* L) {
 // (the factorisation keeps 8 workgroups per CU: 64 / 256 of them took
 // 0.75 / 0.22 s on LAP-1M against 0.071 s; one row per wave spins little)
 int persist_grid(int n) { return std::max(1, std::min(kPersistGroups, (n + kWaves - 1) / kWaves)); }
+
+// Serial-mode plan of one triangular solve (k_ilu_trsv_serial), or false
+// when the solve is not eligible: a level schedule with >= 16 rows per level
+// on average (the level kernel is faster), a dependency farther than kRing
+// rows, or a row with more than kStageEnt off-diagonal entries. Entry
+// offsets count each row padded to a multiple of kPass (at least kPass).
+bool serial_plan(int n, int nlev, const std::vector<int>& rp, const std::vector<int>& ci, const std::vector<int>& dg,
+                 bool upper, std::vector<int>& stage, std::vector<int>& eoff) {
+    if (n == 0 || (int64_t)n >= 16 * (int64_t)nlev) return false;
+    eoff.assign((size_t)n + 1, 0);
+    for (int p = 0; p < n; ++p) {
+        const int i = upper ? n - 1 - p : p;
+        const int j0 = upper ? dg[i] + 1 : rp[i], j1 = upper ? rp[i + 1] : dg[i];
+        const int padded = std::max(kPass, (j1 - j0 + kPass - 1) / kPass * kPass);
+        if (padded > kStageEnt) return false;
+        for (int j = j0; j < j1; ++j)
+            if (std::abs(ci[j] - i) >= kRing) return false;
+        eoff[(size_t)p + 1] = eoff[p] + padded;
+    }
+    stage.clear();
+    for (int p = 0; p < n;) {
+        stage.push_back(p);
+        int q = p;
+        while (q < n && q - p < kStageRows && eoff[(size_t)q + 1] - eoff[p] <= kStageEnt) ++q;
+        p = q;
+    }
+    stage.push_back(n);
+    return true;
+}
 
 // Level schedule of one triangular solve from host copies of the structure
 // (upper: the rows after the diagonal, solved last row first).
@@ -375,6 +523,18 @@ int mpg_ilu0_create(mpg_ctx_t ctx, mpg_csr_t A, const double* val64, int type, m
             std::vector<int> ord, chunk;
             level_schedule(n, rp, ci, dg, u == 1, ord, chunk, L->levels[u]);
             L->nchunks[u] = (int)chunk.size() - 1;
+            std::vector<int> stage, eoff;
+            const char* senv = std::getenv("MPG_ILU_SERIAL");  // 0: always the level schedule
+            if (!(senv && *senv == '0') && serial_plan(n, L->levels[u], rp, ci, dg, u == 1, stage, eoff)) {
+                L->serial[u] = true;
+                L->nstages[u] = (int)stage.size() - 1;
+                if (!ok(hipMalloc((void**)&L->stage[u], stage.size() * 4)) ||
+                    !ok(hipMalloc((void**)&L->eoff[u], eoff.size() * 4)) ||
+                    !ok(hipMemcpyAsync(L->stage[u], stage.data(), stage.size() * 4, hipMemcpyHostToDevice, s)) ||
+                    !ok(hipMemcpyAsync(L->eoff[u], eoff.data(), eoff.size() * 4, hipMemcpyHostToDevice, s)) ||
+                    !ok(hipStreamSynchronize(s)))
+                    return fail(MPG_ERR_ALLOC);
+            }
             if (!ok(hipMalloc((void**)&L->ord[u], ord.size() * 4)) ||
                 !ok(hipMalloc((void**)&L->chunk[u], chunk.size() * 4)) ||
                 !ok(hipMemcpyAsync(L->ord[u], ord.data(), ord.size() * 4, hipMemcpyHostToDevice, s)) ||
@@ -412,8 +572,9 @@ int mpg_ilu0_create(mpg_ctx_t ctx, mpg_csr_t A, const double* val64, int type, m
 int mpg_ilu_destroy(mpg_ilu_t L) {
     if (!L) return MPG_OK;
     if (L->ctx) (void)hipStreamSynchronize(L->ctx->stream);
-    void* ps[] = {L->lu64,   L->lu32,   L->diag,     L->dinv,     L->sync,    L->w[0],
-                  L->w[1],   L->scratch, L->ord[0],  L->ord[1],   L->chunk[0], L->chunk[1]};
+    void* ps[] = {L->lu64,    L->lu32,    L->diag,     L->dinv,     L->sync,     L->w[0],    L->w[1],
+                  L->scratch, L->ord[0],  L->ord[1],   L->chunk[0], L->chunk[1], L->stage[0], L->stage[1],
+                  L->eoff[0], L->eoff[1]};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete L;
@@ -435,12 +596,20 @@ int mpg_ilu_solve(mpg_ctx_t ctx, mpg_ilu_t L, void* x) {
         using T = decltype(t);
         const T* lu = static_cast<const T*>(L->values());
         T* xv = static_cast<T*>(x);
-        k_ilu_trsv<T, false><<<grid(0), kBlock, 0, ctx->stream>>>(L->nchunks[0], L->chunk[0], L->ord[0],
-                                                                    L->A->rowptr, L->A->col, L->diag, lu, xv, L->sync,
-                                                                    L->ticket(1), L->err());
-        k_ilu_trsv<T, true><<<grid(1), kBlock, 0, ctx->stream>>>(L->nchunks[1], L->chunk[1], L->ord[1], L->A->rowptr,
-                                                                  L->A->col, L->diag, lu, xv, L->sync + n,
-                                                                  L->ticket(2), L->err());
+        if (L->serial[0])
+            k_ilu_trsv_serial<T, false><<<1, kBlock, 0, ctx->stream>>>(n, L->nstages[0], L->stage[0], L->eoff[0],
+                                                                       L->A->rowptr, L->A->col, L->diag, lu, xv);
+        else
+            k_ilu_trsv<T, false><<<grid(0), kBlock, 0, ctx->stream>>>(L->nchunks[0], L->chunk[0], L->ord[0],
+                                                                        L->A->rowptr, L->A->col, L->diag, lu, xv,
+                                                                        L->sync, L->ticket(1), L->err());
+        if (L->serial[1])
+            k_ilu_trsv_serial<T, true><<<1, kBlock, 0, ctx->stream>>>(n, L->nstages[1], L->stage[1], L->eoff[1],
+                                                                      L->A->rowptr, L->A->col, L->diag, lu, xv);
+        else
+            k_ilu_trsv<T, true><<<grid(1), kBlock, 0, ctx->stream>>>(L->nchunks[1], L->chunk[1], L->ord[1],
+                                                                       L->A->rowptr, L->A->col, L->diag, lu, xv,
+                                                                       L->sync + n, L->ticket(2), L->err());
         return (int)MPG_OK;
     });
     if (st) return st;
@@ -507,5 +676,7 @@ int mpg_ilu_fault(mpg_ilu_t L) {
         return -1;
     return e;
 }
+
+int mpg_ilu_solve_mode(mpg_ilu_t L) { return L ? (L->serial[0] ? 1 : 0) | (L->serial[1] ? 2 : 0) : 0; }
 
 }  // extern "C"

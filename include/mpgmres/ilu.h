@@ -64,6 +64,10 @@ int mpg_ilu_fault(mpg_ilu_t ilu);
 /* diagnostics: tickets drawn by the factor / L / U launches and the fault
  * word (1 = a bounded wait expired, 2 = a launch passed its deadline) */
 int mpg_ilu_debug_state(mpg_ilu_t ilu, int32_t* out4);
+/* how the triangular solves run: bit 0 set = L solved serially by one
+ * workgroup (few rows per dependency level, e.g. banded), bit 1 = U; clear
+ * bits use the level schedule. MPG_ILU_SERIAL=0 at create forces levels. */
+int mpg_ilu_solve_mode(mpg_ilu_t ilu);
 
 #ifdef __cplusplus
 }

@@ -141,6 +141,30 @@ def test_ilu_large_stencil_consistent(hip, mpg):
         L.close()
 
 
+@pytest.mark.parametrize("dt", [np.float64, np.float32], ids=["f64", "f32"])
+@pytest.mark.parametrize("mat", ["band3000", "band-wide", "random2000", "lap3d-20", "grid-3000x2"])
+def test_ilu_serial_solve_matches_levels(hip, mpg, monkeypatch, mat, dt):
+    """Serial-chain solves (one workgroup, for schedules with few rows per
+    level) and level-scheduled solves give identical results: both sum each
+    row in fp64 in CSR order and round once. Banded matrices take the serial
+    path; the random pattern and the 3-D Laplacian (wide levels) and a 3000x2 grid (dependencies
+    3000 rows back, beyond the serial kernel's LDS ring) keep the levels."""
+    extra = {"band-wide": lambda: mpg.gen_band(9000, 31, 29, seed=5), "grid-3000x2": lambda: mpg.gen_laplace3d(3000, 2, 1)}
+    A = extra[mat]() if mat in extra else MATS[mat](mpg)
+    x = mpg.rand_vect(A.nrows, 7).astype(dt)
+    out = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("MPG_ILU_SERIAL", env)
+        L = Ilu(hip, A, dt)
+        try:
+            out[env] = (L.apply(x, "ilu"), hip.lib.mpg_ilu_solve_mode(L.h))
+        finally:
+            L.close()
+    assert out["0"][1] == 0
+    assert out["1"][1] == (3 if mat.startswith("band") else 0)
+    assert np.array_equal(out["1"][0], out["0"][0])
+
+
 def test_ilu_rejects_missing_diagonal(hip, mpg):
     A = mpg.Csr(3, 3, np.array([0, 1, 2, 3], np.int32), np.array([1, 1, 2], np.int32), np.ones(3))
     drp, dci, dv = hip.buf(A.rowptr), hip.buf(A.col), hip.buf(A.val)

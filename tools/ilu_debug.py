@@ -31,7 +31,7 @@ def run(A, dt, reps=3):
             t = time.time()
             st = lib.mpg_ilu_solve(hip.ctx, h, x.p)
             hip.sync()
-            print(f"  solve st={st} fault={lib.mpg_ilu_fault(h)} {1e3 * (time.time() - t):.3f} ms", flush=True)
+            print(f"  solve st={st} fault={lib.mpg_ilu_fault(h)} mode={lib.mpg_ilu_solve_mode(h)} {1e3 * (time.time() - t):.3f} ms", flush=True)
         lib.mpg_ilu_destroy(h)
     lib.mpg_csr_destroy(csr)
 
@@ -42,4 +42,6 @@ for nx in sizes:
     run(mpg.gen_laplace3d(nx), np.float64)
 print("band20000", flush=True)
 run(mpg.gen_band(20000, 5, 4, seed=3), np.float64, reps=2)
+print("band1M", flush=True)
+run(mpg.gen_band(1000000, 5, 4, seed=7), np.float64, reps=3)
 print("done", flush=True)
