@@ -4,7 +4,7 @@ each Arnoldi step k (its occurrence index within a cycle), and a least-squares
 fit t(k) = a + b*k, which separates a launch's fixed cost (a) from the cost of
 each added basis column (b).
 
-A cycle starts at k_prologue (or k_update_x closes one); k counts the
+A cycle starts at k_prologue / k_prologue_sell (or k_update_x closes one); k counts the
 occurrences of each kernel name since the cycle started.
 
 usage: python tools/per_step.py gpurun_out/prof/.../kernel_trace.csv [col_bytes]
@@ -29,7 +29,7 @@ def main():
     for r in rows:
         k = short(r["Kernel_Name"])
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        if k == "k_prologue":
+        if k in ("k_prologue", "k_prologue_sell"):
             cur = []
             continue
         if cur is None:
