@@ -462,14 +462,28 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
 // gathers. A guarded load would be widened inside its branch and waited
 // for right there — the previous form waited for each window load and each
 // step's loads in turn.
-template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD>
+// DN > 0 (one GPU, CGS, k + 1 <= DN): the panel dots <v_j, w> for j <= k
+// are formed here too, from the lane's own w(i) (no re-read of w and no dots
+// launch). Each workgroup block-reduces its products (store_partials); the
+// last arriver of each group of `gs` workgroups sums the group's partials
+// in workgroup order, so the CGS update (FROM_PARTS) sees <= 256 partials
+// per column, as from k_dots_nc. Deterministic: fixed order throughout.
+struct SellDots {
+    int nc;            // columns: k + 1
+    int gs, ng;        // workgroups per group, groups (<= kCombineGroups)
+    double* wgpart;    // [c * gridDim.x + blockIdx.x]
+    unsigned* cnt;     // one ticket per group (zero between launches)
+    double* out;       // [c * ng + g]
+};
+
+template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD, int DN = 0>
 __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col,
                                                       const typename SellStore<VI>::type* __restrict__ val,
                                                       const T* __restrict__ wprev, const T* __restrict__ inv_p,
                                                       T* __restrict__ V, int64_t ld, int k,
                                                       const P* __restrict__ diag, T* __restrict__ w,
-                                                      GivensFold<T> fold) {
+                                                      GivensFold<T> fold, SellDots dd) {
     using S = typename SellStore<VI>::type;
     constexpr int NQ = kWinLen / kWave;
     __shared__ T win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
@@ -530,36 +544,63 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
     } else {
         inv = *inv_p;
     }
-    if (!live) return;
+    if (DN == 0 && !live) return;  // with dots, a dead wave joins the partials' barriers
     double sum = 0.0;
-    T vk;  // v_k(i) = T(w_prev(i) * inv)
-    if constexpr (WIN) {
+    T vk = T(0);  // v_k(i) = T(w_prev(i) * inv)
+    if (live) {
+        if constexpr (WIN) {
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int c = row0 - kWinLo + q * kWave + lane;
-            win[wid][q * kWave + lane] = (c >= 0 && c < n_ext) ? (T)(wr[q] * inv) : T(0);
+            for (int q = 0; q < NQ; ++q) {
+                const int c = row0 - kWinLo + q * kWave + lane;
+                win[wid][q * kWave + lane] = (c >= 0 && c < n_ext) ? (T)(wr[q] * inv) : T(0);
+            }
+            wave_lds_sync();
+            auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
+            row.sum(0, xv, sum);
+            for (int q = row.U; q < row.steps; q += row.U) {
+                row.load(q);
+                row.sum(q, xv, sum);
+            }
+            vk = win[wid][lane + kWinLo];
+        } else {
+            auto xv = [&](int c) { return (double)(T)(wprev[c] * inv); };
+            row.sum(0, xv, sum);
+            for (int q = row.U; q < row.steps; q += row.U) {
+                row.load(q);
+                row.sum(q, xv, sum);
+            }
+            vk = (T)(wr[0] * inv);
         }
-        wave_lds_sync();
-        auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
-        row.sum(0, xv, sum);
-        for (int q = row.U; q < row.steps; q += row.U) {
-            row.load(q);
-            row.sum(q, xv, sum);
-        }
-        vk = win[wid][lane + kWinLo];
-    } else {
-        auto xv = [&](int c) { return (double)(T)(wprev[c] * inv); };
-        row.sum(0, xv, sum);
-        for (int q = row.U; q < row.steps; q += row.U) {
-            row.load(q);
-            row.sum(q, xv, sum);
-        }
-        vk = (T)(wr[0] * inv);
     }
-    if (i < n) {
+    T wi = T(0);
+    if (live && i < n) {
         const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
-        w[i] = precond<T, P>(t, diag, i);
+        wi = precond<T, P>(t, diag, i);
+        w[i] = wi;
         V[(int64_t)k * ld + i] = vk;
+    }
+    if constexpr (DN > 0) {
+        // the earlier basis columns at this row: clamped, branch-free loads
+        // issued together (one latency), then one product per column
+        const int ic = i < n ? i : n - 1;
+        const int kc = k > 0 ? k - 1 : 0;
+        T vc[DN];
+#pragma unroll
+        for (int c = 0; c < DN; ++c) vc[c] = V[(int64_t)(c < kc ? c : kc) * ld + ic];
+        __builtin_amdgcn_sched_barrier(0);
+        const double wd = (live && i < n) ? (double)wi : 0.0;
+        double acc[DN];
+#pragma unroll
+        for (int c = 0; c < DN; ++c) acc[c] = (c < k ? (double)vc[c] : c == k ? (double)vk : 0.0) * wd;
+        store_partials<DN, kBlock, true>(acc, dd.nc, dd.wgpart);
+        const int g = blockIdx.x / dd.gs;
+        const int m0 = g * dd.gs, m1 = m0 + dd.gs < (int)gridDim.x ? m0 + dd.gs : (int)gridDim.x;
+        if (last_arriver_of(dd.cnt + g, (unsigned)(m1 - m0)) && (int)threadIdx.x < dd.nc) {
+            const int c = threadIdx.x;
+            double v = 0.0;
+            for (int m = m0; m < m1; ++m) v += dd.wgpart[(size_t)c * gridDim.x + m];
+            dd.out[(size_t)c * dd.ng + g] = v;
+        }
     }
 }
 
@@ -1202,6 +1243,11 @@ struct mpg_arnoldi {
     SellCopy sell;  // sliced-ELL copy of the Arnoldi matrix (nslices == 0: CSR row blocks)
     SellCopy sell_outer;        // ... of the outer-precision values, for the residual prologue
     bool outer_is_inner = false;  // the prologue runs on `sell` (baseline / single modes)
+    // SELL SpMV with the panel dots fused (SellDots): per-workgroup partials,
+    // group tickets, group size and count
+    double* fd_part = nullptr;
+    unsigned* fd_cnt = nullptr;
+    int fd_gs = 0, fd_ng = 0;
 
     char* small_at(int slot) const { return static_cast<char*>(small) + (size_t)slot * (d.m + 1) * tsize; }
     void* cs() const { return small_at(0); }
@@ -1261,6 +1307,13 @@ int arnoldi_sell_build(mpg_arnoldi* a, int format) {
     // the residual prologue on the same slicing: shared when the residual and
     // Arnoldi matrices are the same array, else a copy of the outer values
     a->outer_is_inner = a->d.val_outer == a->d.val_inner && a->d.outer_type == a->d.inner_val;
+    const int grid = (a->sell.nslices + kBlock / kWave - 1) / (kBlock / kWave);
+    a->fd_gs = (grid + kCombineGroups - 1) / kCombineGroups;
+    a->fd_ng = (grid + a->fd_gs - 1) / a->fd_gs;
+    if (hipMalloc((void**)&a->fd_part, (size_t)kNC * grid * sizeof(double)) != hipSuccess ||
+        hipMalloc((void**)&a->fd_cnt, (size_t)a->fd_ng * sizeof(unsigned)) != hipSuccess ||
+        hipMemsetAsync(a->fd_cnt, 0, (size_t)a->fd_ng * sizeof(unsigned), a->ctx->stream) != hipSuccess)
+        return MPG_ERR_ALLOC;
     if (a->outer_is_inner) return MPG_OK;
     return sell_build(a->ctx, a->d.A, a->d.outer_type, a->d.val_outer, 2, a->sell_outer);
 }
@@ -1340,7 +1393,7 @@ int mpg_arnoldi_destroy(mpg_arnoldi_t a) {
     if (!a) return MPG_OK;
     if (a->ctx) (void)hipStreamSynchronize(a->ctx->stream);
     void* ps[] = {a->V, a->H, a->small, a->w[0], a->w[1], a->partial, a->dpart, a->sums, a->report,
-                  a->counters};
+                  a->counters, a->fd_part, a->fd_cnt};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     sell_free(a->sell);
@@ -1424,9 +1477,15 @@ int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols) {
     return MPG_OK;
 }
 
-// fold: 0 plain; 1 Givens(k-1) folded, ||w||^2 from sums[0]; 2 from the partials
-static int spmv_impl(mpg_arnoldi_t a, int k, int fold) {
+// fold: 0 plain; 1 Givens(k-1) folded, ||w||^2 from sums[0]; 2 from the partials.
+// dots: the panel dots fused (SellDots; MPG_ERR_UNSUPPORTED where the SELL
+// copy, an fp32 basis with fp32 values, int16 columns and the window are
+// not all present -- the caller then launches the dots itself).
+static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
+    if (dots && (a->sell.nslices == 0 || !a->sell.c16 || !a->sell.win || (a->combo != 2 && a->combo != 3) ||
+                 k + 1 > kNC || a->d.orth == kOrthMGS))
+        return MPG_ERR_UNSUPPORTED;
     if (fold && (k < 1 || a->d.m > kFoldMaxM)) return MPG_ERR_ARG;
     const mpg_csr* A = a->d.A;
     int st = dispatch(a->combo, [&](auto t, auto, auto p, auto vi) {
@@ -1442,16 +1501,34 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold) {
             if (fold == 2 && a->last_G > kBlock) return (int)MPG_ERR_ARG;  // k_step_sell folds <= kBlock partials
             return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
                 using CI = decltype(ci);
+                constexpr int Wc = decltype(wc)::value;
                 const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
-                return sell_dispatch_win(S.win, [&](auto wn) {
-                    auto kern = fold ? k_step_sell<T, P, VI, CI, decltype(wc)::value, decltype(wn)::value, true>
-                                     : k_step_sell<T, P, VI, CI, decltype(wc)::value, decltype(wn)::value, false>;
+                auto launch = [&](auto kern, SellDots dd) {
                     kern<<<grid, kBlock, 0, a->ctx->stream>>>(
                             a->d.n, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
-                            static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf);
+                            static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd);
                     return (int)MPG_OK;
+                };
+                if constexpr (std::is_same_v<T, float> && std::is_same_v<VI, float> &&
+                              std::is_same_v<CI, int16_t>) {
+                    if (dots) {
+                        const SellDots dd{k + 1, a->fd_gs, a->fd_ng, a->fd_part, a->fd_cnt, a->dpart};
+                        auto pick = [&](auto dn) {
+                            constexpr int DN = decltype(dn)::value;
+                            return fold ? launch(k_step_sell<T, P, VI, CI, Wc, true, true, DN>, dd)
+                                        : launch(k_step_sell<T, P, VI, CI, Wc, true, false, DN>, dd);
+                        };
+                        if (k + 1 <= 8) return pick(std::integral_constant<int, 8>());
+                        if (k + 1 <= 16) return pick(std::integral_constant<int, 16>());
+                        return pick(std::integral_constant<int, 32>());
+                    }
+                }
+                return sell_dispatch_win(S.win, [&](auto wn) {
+                    constexpr bool WN = decltype(wn)::value;
+                    return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true>, SellDots{})
+                                : launch(k_step_sell<T, P, VI, CI, Wc, WN, false>, SellDots{});
                 });
             });
         }
@@ -1463,11 +1540,19 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold) {
         return (int)MPG_OK;
     });
     if (st) return st;
+    if (dots) {
+        a->last_G = a->fd_ng;
+        a->last_part = a->dpart;
+    }
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
 }
 
 int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 0); }
+int mpg_arnoldi_spmv_dots(mpg_arnoldi_t a, int k, int fold) {
+    if (fold < 0 || fold > 2) return MPG_ERR_ARG;
+    return spmv_impl(a, k, fold, true);
+}
 int mpg_arnoldi_givens_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 1); }
 int mpg_arnoldi_givens_partials_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 2); }
 int mpg_arnoldi_fold_max_m(void) { return kFoldMaxM; }
@@ -1518,7 +1603,8 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
     // dots' partials inside this launch (no reduce launch)
     if (from_partials && (pass != 0 || k + 1 > kNC || a->last_part != a->dpart)) return MPG_ERR_ARG;
     const double* src = from_partials ? a->dpart : a->sums;
-    const int part_G = from_partials ? a->Gd : 0;
+    const int part_G = from_partials ? a->last_G : 0;  // Gd (k_dots_nc) or fd_ng (k_step_sell's dots)
+    if (part_G > kCombineGroups) return MPG_ERR_ARG;
     int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
         using T = decltype(t);
         T* coef_out = pass == 0 ? static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) : static_cast<T*>(a->corr());

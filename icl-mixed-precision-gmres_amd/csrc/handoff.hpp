@@ -24,14 +24,15 @@ __device__ __forceinline__ void store_wt(double* p, double v) {
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// true in every thread of the last-arriving workgroup (after its acquire)
-__device__ __forceinline__ bool last_arriver(unsigned* cnt) {
+// true in every thread of the last-arriving of `expected` workgroups that
+// share the counter (after its acquire); last_arriver: of the whole grid
+__device__ __forceinline__ bool last_arriver_of(unsigned* cnt, unsigned expected) {
     __shared__ int last_s;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned t = __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = t == gridDim.x - 1;
+        const bool last = t == expected - 1;
         if (last) {
             __hip_atomic_store((gu32*)cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -42,6 +43,7 @@ __device__ __forceinline__ bool last_arriver(unsigned* cnt) {
     __syncthreads();
     return last_s != 0;
 }
+__device__ __forceinline__ bool last_arriver(unsigned* cnt) { return last_arriver_of(cnt, gridDim.x); }
 
 
 __device__ __forceinline__ void store_wt(float* p, float v) {

@@ -84,6 +84,8 @@ struct FusedEngine::Impl {
     bool fold = false;     // Givens step folded into the next SpMV launch
     bool combine = false;  // last-arriver combines in the dots and CGS launches
     bool cgs_partials = false;  // CGS update sums the dots partials in-launch
+    bool fuse_dots = false;     // ... from dots formed in the SpMV launch
+    bool fuse_dots_required = false;
     int timed = -1;                  // phase whose launches time_phase brackets with events
     std::vector<hipEvent_t> marks;   // ... begin/end pairs
     std::vector<int32_t> rowptr_host;
@@ -322,6 +324,11 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     // older runtime-count kernel, slower than reduce + update; on only with =1)
     I.cgs_partials = !comm && !I.combine && I.orth != MPG_ORTH_MGS &&
                      (I.orth == MPG_ORTH_CGSR ? (penv && *penv == '1') : !(penv && *penv == '0'));
+    // MPG_FUSE_DOTS=1: the panel dots inside the SELL SpMV launch (SellDots)
+    const char* denv = std::getenv("MPG_FUSE_DOTS");
+    // (=2: required -- an error where the storage does not support it; tests)
+    I.fuse_dots = I.cgs_partials && I.orth == MPG_ORTH_CGS && denv && (*denv == '1' || *denv == '2');
+    I.fuse_dots_required = I.fuse_dots && *denv == '2';
     const char* fenv = std::getenv("MPG_FOLD_GIVENS");
     I.fold = !I.combine && !(fenv && *fenv == '0') && I.m <= mpg_arnoldi_fold_max_m();
     check(mpg_ctx_sync(ctx), "sync", ctx);
@@ -377,6 +384,18 @@ void FusedEngine::givens(int k) {
 // launch (k >= 1) and step k's own Givens is left to step k+1 / the caller.
 void FusedEngine::step(int k, bool fold) {
     Impl& I = *p_;
+    // SpMV and panel dots in one launch (one GPU, CGS with in-launch sums)
+    if (I.fuse_dots && !I.comm && !I.ilu && I.orth == MPG_ORTH_CGS && I.cgs_partials && !I.combine && k + 1 <= 32) {
+        timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
+        const int st = mpg_arnoldi_spmv_dots(I.arn, k, fold && k > 0 ? 2 : 0);
+        if (st == MPG_OK) {
+            check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx);
+            if (!fold) givens(k);
+            return;
+        }
+        if (st != MPG_ERR_UNSUPPORTED || I.fuse_dots_required) check(st, "spmv+dots", I.ctx);
+        I.fuse_dots = false;  // not available for this storage: the separate launches below
+    }
     if (fold && k > 0) {
         if (I.comm)  // the ||w||^2 partials' all-reduce and the w_prev halo in one RCCL group
             I.comm->allreduce_sum_and_halo(mpg_arnoldi_partials_dev(I.arn), mpg_arnoldi_partials_count(I.arn),

@@ -116,6 +116,12 @@ int mpg_arnoldi_givens_spmv(mpg_arnoldi_t a, int k);
 int mpg_arnoldi_dots_sums(mpg_arnoldi_t a, int k);
 int mpg_arnoldi_cgs_givens(mpg_arnoldi_t a, int k, int pass);
 int mpg_arnoldi_givens_partials_spmv(mpg_arnoldi_t a, int k);
+/* SpMV step k (fold as above: 0 plain, 1 from sums[0], 2 from the partials)
+ * with the panel dots <v_j, w>, j <= k, formed in the same launch: replaces
+ * spmv + dots ahead of mpg_arnoldi_cgs_partials (one GPU, CGS / CGSR,
+ * k + 1 <= 32). MPG_ERR_UNSUPPORTED unless the SpMV runs on the SELL copy
+ * with an fp32 basis, fp32 values, 16-bit columns and the v_k window. */
+int mpg_arnoldi_spmv_dots(mpg_arnoldi_t a, int k, int fold);
 int mpg_arnoldi_fold_max_m(void);
 int mpg_arnoldi_update(mpg_arnoldi_t a, int k);
 /* sums[c] = sum over workgroups of partial column c, c < ncols */

@@ -28,14 +28,17 @@ def _case_id(c):
 # (engine, storage, environment): the fused engine on both Arnoldi SpMV
 # storages (CSR row blocks, SELL-64);: MPG_SELL_WINDOW=0 gathers v_k from memory
 # instead of the LDS window; the others are launch-count experiments
-FLAGS = ("MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS", "MPG_SELL_WINDOW", "MPG_SURFACE_SELL")
+FLAGS = ("MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS", "MPG_SELL_WINDOW", "MPG_SURFACE_SELL", "MPG_FUSE_DOTS")
 ON_BY_DEFAULT = ("MPG_SELL_WINDOW", "MPG_SURFACE_SELL")
 ENGINES = {"surface": ("surface", "auto", {}), "surface-csr": ("surface", "auto", {"MPG_SURFACE_SELL": "0"}),
            "fused-csr": ("fused", "csr", {}),
            "fused-sell": ("fused", "sell", {}), "fused-gather": ("fused", "sell", {"MPG_SELL_WINDOW": "0"}),
            "fused-fold": ("fused", "auto", {"MPG_FOLD_GIVENS": "1"}),
            "fused-combine": ("fused", "auto", {"MPG_COMBINE": "1"}),
-           "fused-cgspart": ("fused", "auto", {"MPG_CGS_PARTIALS": "1"})}
+           "fused-cgspart": ("fused", "auto", {"MPG_CGS_PARTIALS": "1"}),
+           "fused-dots": ("fused", "sell", {"MPG_CGS_PARTIALS": "1", "MPG_FUSE_DOTS": "1"}),
+           "fused-dots-fold": ("fused", "sell", {"MPG_CGS_PARTIALS": "1", "MPG_FUSE_DOTS": "1",
+                                                 "MPG_FOLD_GIVENS": "1"})}
 
 
 def _engine(monkeypatch, engine):
