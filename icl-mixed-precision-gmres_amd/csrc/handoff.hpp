@@ -51,14 +51,15 @@ __device__ __forceinline__ void store_wt(float* p, float v) {
 }
 
 // Wait until *flag != 0 (lane-local; relaxed agent-scope polls with
-// s_sleep). Bounded by the 100 MHz real-time counter: after ~2 s it records
-// a fault in *err and returns false, so a scheduling fault ends the launch
-// instead of hanging the GPU.
-__device__ __forceinline__ bool wait_flag(const int* flag, int* err) {
+// s_sleep). Bounded by the 100 MHz real-time counter: after `bound` ticks
+// (default ~2 s) it records a fault in *err and returns false, so a
+// scheduling fault ends the launch instead of hanging the GPU.
+constexpr uint64_t kWaitBound = 200000000ull;
+__device__ __forceinline__ bool wait_flag(const int* flag, int* err, uint64_t bound = kWaitBound) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load((const gu32*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
         __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {
             __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }

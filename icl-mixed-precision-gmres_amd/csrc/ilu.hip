@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu_trsv(int nchunks, const int* __r
                                                      const int* __restrict__ ord, const int* __restrict__ rowptr,
                                                      const int* __restrict__ col, const int* __restrict__ diag,
                                                      const T* __restrict__ lu, T* x, int* done, unsigned* ticket,
-                                                     int* err) {
+                                                     int* err, uint64_t wait_bound) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     for (;;) {
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void k_ilu_trsv(int nchunks, const int* __r
             d = diag[row];
             j0 = UPPER ? d + 1 : rowptr[row];
             j1 = UPPER ? rowptr[row + 1] : d;
-            for (int j = j0; j < j1; ++j) wait_flag(done + col[j], err);
+            for (int j = j0; j < j1; ++j) wait_flag(done + col[j], err, wait_bound);
         }
         acquire_agent();
         if (live) {
@@ -368,6 +368,7 @@ struct mpg_ilu {
     int* diag = nullptr;
     void* dinv = nullptr;
     int* sync = nullptr;
+    uint64_t wait_bound = kWaitBound;  // per-wait bound of the level-scheduled solves (test hook)
     void* w[2] = {nullptr, nullptr};  // ILU-Jacobi: right-hand side and the second sweep buffer
     unsigned long long* scratch = nullptr;
     // level schedules of the two triangular solves: rows by level, and
@@ -565,6 +566,8 @@ int mpg_ilu0_create(mpg_ctx_t ctx, mpg_csr_t A, const double* val64, int type, m
         }
         return fail(MPG_ERR_BREAKDOWN);
     }
+    if (const char* e = std::getenv("MPG_ILU_WAIT_TICKS"))  // test hook: bound of the solves' waits
+        L->wait_bound = std::strtoull(e, nullptr, 10) ? std::strtoull(e, nullptr, 10) : kWaitBound;
     *out = L;
     return MPG_OK;
 }
@@ -602,14 +605,16 @@ int mpg_ilu_solve(mpg_ctx_t ctx, mpg_ilu_t L, void* x) {
         else
             k_ilu_trsv<T, false><<<grid(0), kBlock, 0, ctx->stream>>>(L->nchunks[0], L->chunk[0], L->ord[0],
                                                                         L->A->rowptr, L->A->col, L->diag, lu, xv,
-                                                                        L->sync, L->ticket(1), L->err());
+                                                                        L->sync, L->ticket(1), L->err(),
+                                                                        L->wait_bound);
         if (L->serial[1])
             k_ilu_trsv_serial<T, true><<<1, kBlock, 0, ctx->stream>>>(n, L->nstages[1], L->stage[1], L->eoff[1],
                                                                       L->A->rowptr, L->A->col, L->diag, lu, xv);
         else
             k_ilu_trsv<T, true><<<grid(1), kBlock, 0, ctx->stream>>>(L->nchunks[1], L->chunk[1], L->ord[1],
                                                                        L->A->rowptr, L->A->col, L->diag, lu, xv,
-                                                                       L->sync + n, L->ticket(2), L->err());
+                                                                       L->sync + n, L->ticket(2), L->err(),
+                                                                       L->wait_bound);
         return (int)MPG_OK;
     });
     if (st) return st;
@@ -675,6 +680,18 @@ int mpg_ilu_fault(mpg_ilu_t L) {
         hipStreamSynchronize(L->ctx->stream) != hipSuccess)
         return -1;
     return e;
+}
+
+int mpg_ilu_clear_fault(mpg_ilu_t L) {
+    if (!L || !L->sync) return MPG_ERR_ARG;
+    MPG_HIP(L->ctx, hipMemsetAsync(L->err(), 0, sizeof(int), L->ctx->stream));
+    return MPG_OK;
+}
+
+int mpg_ilu_set_wait_bound(mpg_ilu_t L, uint64_t ticks) {
+    if (!L) return MPG_ERR_ARG;
+    L->wait_bound = ticks ? ticks : kWaitBound;
+    return MPG_OK;
 }
 
 int mpg_ilu_solve_mode(mpg_ilu_t L) { return L ? (L->serial[0] ? 1 : 0) | (L->serial[1] ? 2 : 0) : 0; }

@@ -335,6 +335,7 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     setup_seconds = std::chrono::duration<double>(clk::now() - t0).count();
     prologue();
     read_report(4);
+    if (I.ilu) check_ilu_fault(I.ilu);
 }
 
 FusedEngine::~FusedEngine() = default;
@@ -570,6 +571,7 @@ int FusedEngine::run_pipelined(int max_cycles, bool& done) {
         const bool more = ran + 1 < max_cycles;
         if (more) launch(p ^ 1);  // speculative: decided by this cycle's report
         hipck(hipEventSynchronize(I.report_ev[p]), "report wait");
+        if (I.ilu) check_ilu_fault(I.ilu);  // every apply of this cycle is valid
         I.report_host = I.rep[p];
         record_steps(i);
         ++ran;
@@ -603,6 +605,7 @@ int FusedEngine::run(int max_cycles, bool& done) {
             if (I.use_graph) hipck(hipGraphLaunch(I.graph_exec, I.stream()), "graph launch");
             else cycle_program();
             read_report(I.report_len);
+            if (I.ilu) check_ilu_fault(I.ilu);
             record_steps(i);
             continue;
         }
@@ -610,6 +613,7 @@ int FusedEngine::run(int max_cycles, bool& done) {
         for (int k = 0;; ++k) {
             step(k, false);
             read_report(4 + k + 1);
+            if (I.ilu) check_ilu_fault(I.ilu);
             const double res = I.report_host[4 + k];
             step_res.push_back(res);
             step_cycle.push_back((int)i);
@@ -635,6 +639,7 @@ int FusedEngine::run(int max_cycles, bool& done) {
                 update(k + 1);
                 prologue();
                 read_report(4);
+                if (I.ilu) check_ilu_fault(I.ilu);
                 break;
             }
         }
@@ -797,6 +802,8 @@ int mpg_engine_run(mpg_engine_t e, int max_cycles, int* done) {
         int ran = e->eng->run(max_cycles, d);
         if (done) *done = d ? 1 : 0;
         return ran;
+    } catch (const mpg::StatusError& ex) {
+        return ex.status;
     } catch (const std::exception&) {
         return MPG_ERR_HIP;
     }

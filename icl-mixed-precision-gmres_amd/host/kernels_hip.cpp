@@ -37,7 +37,16 @@ void check(int status, const char* what, mpg_ctx_t ctx) {
         const char* e = mpg_ctx_last_error(c);
         if (e && *e) os << " (" << e << ")";
     }
-    throw std::runtime_error(os.str());
+    throw StatusError(status, os.str());
+}
+
+void check_ilu_fault(mpg_ilu_t ilu) {
+    const int f = mpg_ilu_fault(ilu);
+    if (f == 0) return;
+    if (f < 0) check(MPG_ERR_HIP, "ILU fault word read");
+    std::ostringstream os;
+    os << "mpgmres: ILU triangular solve fault " << f << " (a row waited past its bound); the solve is invalid";
+    throw StatusError(MPG_ERR_BREAKDOWN, os.str());
 }
 
 // MPG_SURFACE_SELL=0 keeps the operator surface's spmv on CSR
@@ -353,9 +362,15 @@ template <> ILU<double, Hip> ilu0<double, Hip>(SparseMatrix<double, Hip> A) { re
 template <> ILU<float, Hip> ilu0<float, Hip>(SparseMatrix<double, Hip> A) { return make_ilu<float>(A, 1); }
 template <> void ilusv<double, Hip>(ILU<double, Hip> ilu, Vect<double, Hip> x) {
     check(mpg_ilu_solve(C, ilu.handle(), x.data()), "ilusv");
+    // a level-scheduled solve can fault (a bounded wait expired): read the
+    // sticky fault word before anything consumes x (the serial chain never waits)
+    if (mpg_ilu_solve_mode(ilu.handle()) != 3) mpg::check_ilu_fault(ilu.handle());
 }
 template <> void ilusv<float, Hip>(ILU<float, Hip> ilu, Vect<float, Hip> x) {
     check(mpg_ilu_solve(C, ilu.handle(), x.data()), "ilusv");
+    // a level-scheduled solve can fault (a bounded wait expired): read the
+    // sticky fault word before anything consumes x (the serial chain never waits)
+    if (mpg_ilu_solve_mode(ilu.handle()) != 3) mpg::check_ilu_fault(ilu.handle());
 }
 template <> void ilusv_jacobi<double, Hip>(ILU_Jacobi<double, Hip> ilu, Vect<double, Hip> x) {
     check(mpg_ilu_jacobi_solve(C, ilu.handle(), ilu.steps(), x.data()), "ilusv_jacobi");

@@ -212,6 +212,10 @@ extern "C" int mpg_solve(const mpg_solve_args* args, mpg_solve_result* result) {
             mpg::check(mpg_ctx_sync(ctx), "final sync", ctx);
         }
         return st;
+    } catch (const mpg::StatusError& e) {
+        result->status = MPG_RESULT_ERROR;
+        std::snprintf(result->message, sizeof result->message, "%s", e.what());
+        return e.status;
     } catch (const std::exception& e) {
         result->status = MPG_RESULT_ERROR;
         std::snprintf(result->message, sizeof result->message, "%s", e.what());

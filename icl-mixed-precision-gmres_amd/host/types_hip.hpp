@@ -18,9 +18,17 @@
 
 namespace mpg {
 
-// Throws on a non-zero C-ABI status (the reference ignores cuBLAS statuses
-// and asserts MKL ones; we never drop an error).
+// Throws StatusError on a non-zero C-ABI status (the reference ignores cuBLAS
+// statuses and asserts MKL ones; we never drop an error). mpg_solve returns
+// the carried status.
+struct StatusError : std::runtime_error {
+    int status;
+    StatusError(int st, const std::string& msg) : std::runtime_error(msg), status(st) {}
+};
 void check(int status, const char* what, mpg_ctx_t ctx = nullptr);
+// A scheduling fault of the ILU triangular solves (the results of every
+// apply since the last check are invalid): StatusError(MPG_ERR_BREAKDOWN).
+void check_ilu_fault(mpg_ilu_t ilu);
 
 // The calling thread's current HIP context (stream + workspace). Created
 // lazily on the device named by MPG_DEVICE (default 0) unless a

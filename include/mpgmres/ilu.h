@@ -59,8 +59,16 @@ const void* mpg_ilu_values_dev(mpg_ilu_t ilu);
 const int32_t* mpg_ilu_diag_dev(mpg_ilu_t ilu);
 const void* mpg_ilu_dinv_dev(mpg_ilu_t ilu);
 /* non-zero when a row waited past its bound (a scheduling fault; results
- * are then not valid). Synchronises. */
+ * are then not valid). Synchronises. The word is sticky: every solve after
+ * a fault keeps reporting it until mpg_ilu_clear_fault. The solve engines
+ * read it at every restart-cycle boundary (fused) or after every apply
+ * (operator surface) and fail the solve with MPG_ERR_BREAKDOWN. */
 int mpg_ilu_fault(mpg_ilu_t ilu);
+int mpg_ilu_clear_fault(mpg_ilu_t ilu);
+/* per-wait bound of the level-scheduled triangular solves in ticks of the
+ * 100 MHz real-time counter (0 = the default, ~2 s). Test hook: a tiny
+ * bound makes any real wait fault. */
+int mpg_ilu_set_wait_bound(mpg_ilu_t ilu, uint64_t ticks);
 /* diagnostics: tickets drawn by the factor / L / U launches and the fault
  * word (1 = a bounded wait expired, 2 = a launch passed its deadline) */
 int mpg_ilu_debug_state(mpg_ilu_t ilu, int32_t* out4);

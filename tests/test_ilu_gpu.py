@@ -192,3 +192,23 @@ def test_ilu_solve_live_oracle(mpg, oracle, engine, mode, prec):
     got = mpg.solve(A, b, xt, engine=engine, **opts)
     assert ref.status == "converged"
     compare(as_ref(ref), got, mode, opts["tol"], 30, f"lap24-{mode}-{prec}-{engine}")
+
+
+@pytest.mark.parametrize("engine", ["surface", "fused"])
+def test_ilu_solve_fault_fails_the_solve(mpg, engine, monkeypatch):
+    """A level-scheduled triangular solve whose bounded wait expires records
+    a fault and leaves x partly solved; the engines read the sticky fault
+    word (fused: every restart-cycle boundary; surface: after every apply)
+    and fail the solve with MPG_ERR_BREAKDOWN instead of iterating on a wrong
+    M^-1 w. A 1-tick wait bound makes every real wait fault."""
+    A = mpg.gen_laplace3d(24)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode="mixed", orth="cgs", prec="ilu", rlen=30, tol=1e-10, max_restarts=60)
+    monkeypatch.setenv("MPG_ILU_SERIAL", "0")
+    monkeypatch.setenv("MPG_ILU_WAIT_TICKS", "1")
+    with pytest.raises(RuntimeError, match=r"solve failed \(-6\).*ILU triangular solve fault"):
+        mpg.solve(A, b, xt, engine=engine, **opts)
+    monkeypatch.delenv("MPG_ILU_WAIT_TICKS")
+    got = mpg.solve(A, b, xt, engine=engine, **opts)  # a fresh factor has a clear fault word
+    assert got.status == "converged"

@@ -207,3 +207,23 @@ def test_pipelined_cycles_match_serial(mpg, mode, stop, monkeypatch):
     assert p.total_iters == s.total_iters and p.restarts == s.restarts
     assert np.array_equal(p.step_res, s.step_res)
     assert p.res_norm == s.res_norm and p.err_norm == s.err_norm
+
+
+def test_engine_sequence_in_one_process(mpg, oracle):
+    """CGS surface -> CGS fused -> MGS surface -> MGS fused in one process
+    (each solve creates and destroys its own context, engine, graphs and
+    pinned report buffers). Round 1 saw a SIGSEGV on the first MGS fused
+    solve of this sequence under rocprofv3 --kernel-trace; its PC lies in
+    librocprofiler-sdk's queue intercept while HIP submits the packet-captured
+    graph, and the same sequence passes under the profiler with
+    DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 (profiles/r02_engine_sequence_*).
+    Every solve here is checked against the oracle."""
+    A = mpg.gen_band(200_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    for orth in ("cgs", "mgs"):
+        opts = dict(mode="mixed", orth=orth, prec="identity", rlen=30, tol=1e-9, max_restarts=40)
+        ref = oracle.solve(mpg, A, b, xt, **opts)
+        for engine in ("surface", "fused"):
+            got = mpg.solve(A, b, xt, engine=engine, **opts)
+            compare(as_ref(ref), got, "mixed", opts["tol"], 30, f"sequence-{orth}-{engine}")

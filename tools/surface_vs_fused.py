@@ -4,6 +4,7 @@ GMRES(30), 5 restart cycles each.
 
 usage: python tools/surface_vs_fused.py [orth ...] [--engines surface,fused]"""
 import sys
+from pathlib import Path
 
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 from __graft_entry__ import _load
@@ -20,8 +21,12 @@ def main():
     A = mpg.gen_band(1_000_000, 5, 4, seed=7)
     xt = mpg.rand_vect(A.nrows, 42)
     b = mpg.host_spmv(A, xt)
+    import os
+    maps = os.environ.get("MPG_DUMP_MAPS")  # crash triage: library map of this process
     for orth in orths:
         for eng in engines:
+            if maps:
+                Path(maps).write_text(Path("/proc/self/maps").read_text())
             opts = dict(engine=eng, mode="mixed", orth=orth, prec="identity", rlen=30, tol=0.0)
             mpg.solve(A, b, xt, max_restarts=1, **opts)
             r = mpg.solve(A, b, xt, max_restarts=5, **opts)
