@@ -1,25 +1,47 @@
 """Parity rules between a GMRES run and the oracle / golden record.
 
-Stated tolerances (the north-star's "within a stated fp tolerance"):
+Stated tolerances (the north-star's "within a stated fp tolerance"). be(c)
+is the per-restart backward error r/(||b|| + ||A||_F ||x||) of cycle c
+(IterUtil.hpp:37-61), s(k+1) the per-step Arnoldi residual.
 
 fp64 Arnoldi with an fp64 preconditioner (mode baseline):
   * same final status, same restart index i and total iteration count;
-  * per-step Arnoldi residual |s(k+1)|, cycle 0:
-        |Δ| <= 1e-8 |s_ref| + 1e-12 ||M^-1 b||
-    later cycles: |Δ| <= 1e-5 |s_ref| + 1e-10 ||M^-1 b||;
-  * per-restart backward error r/(||b|| + ||A||_F ||x||):
-        |Δ| <= 1e-5 be_ref + 1e-15.
+  * per-step |s(k+1)|, cycle 0:  |Δ| <= 1e-8 |s_ref| + 1e-12 ||M^-1 b||;
+    later cycles:               |Δ| <= 1e-5 |s_ref| + 1e-10 ||M^-1 b||;
+  * every cycle's backward error: |Δ| <= 1e-5 be_ref + 1e-15;
+  * x (first 16 entries and the sum): relative 1e-12 of max|x_ref|;
+  * final resNorm within a factor 1.2, errNorm within a factor 2.
 fp32 Arnoldi, or fp64 Arnoldi whose vectors pass through an fp32
 preconditioner every step (modes mixed, single, mixed-half, single-prec):
   * same final status; restart index within ±1;
   * cycle-0 history |Δ| <= 1e-3 |s_ref| + 1e-5 ||M^-1 b||;
+  * every cycle both runs reached (all but the last when the restart
+    counts differ): max(be, F) within a factor 3 of max(be_ref, F), with
+    the floor F = 1e-14 (fp64 residual) or 1e-6 (mode single, fp32
+    residual) — the restarts of an fp32 cycle contract the error by
+    amounts that differ with the fp32 rounding, never by more than that;
+  * x: relative 1e-9 (fp64 outer) / 1e-5 (single) of max|x_ref| on the
+    first 16 entries, 1e-7 / 1e-4 on the sum (same restart count only);
+  * final resNorm and errNorm within a factor 10;
   * when converged, the final backward error is <= tol.
+Measured margins behind these numbers: tools/parity_margins.py over the
+168 golden records on the fused and operator-surface engines
+(profiles/r02_parity_margins.txt).
 """
 import numpy as np
 
 
 def _arr(x):
     return np.asarray(x, dtype=np.float64)
+
+
+def _ratio_ok(a, b, factor):
+    a, b = float(a), float(b)
+    if a == b:
+        return True
+    if not (np.isfinite(a) and np.isfinite(b)) or a <= 0 or b <= 0:
+        return False
+    return max(a / b, b / a) <= factor
 
 
 def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
@@ -30,6 +52,8 @@ def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
     cyc = np.asarray(got.step_cycle)
     be_ref = _arr(ref["cyc_r_norm"]) / _arr(ref["cyc_normalization"])
     be_got = _arr(got.cyc_r_norm) / _arr(got.cyc_normalization)
+    x_head_ref = _arr(ref["x_head"]) if "x_head" in ref else None
+    xscale = float(np.max(np.abs(x_head_ref))) if x_head_ref is not None and len(x_head_ref) else 0.0
     if fp64:
         assert got.restarts == ref["restarts"], f"{label}: restarts {got.restarts} vs {ref['restarts']}"
         assert got.total_iters == ref["total_iters"], f"{label}: iters {got.total_iters} vs {ref['total_iters']}"
@@ -39,13 +63,33 @@ def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
         assert np.all(d[c0] <= 1e-8 * s_ref[c0] + 1e-12 * minvb), f"{label}: cycle-0 history {d[c0].max():.3e}"
         assert np.all(d[~c0] <= 1e-5 * s_ref[~c0] + 1e-10 * minvb), f"{label}: history {d[~c0].max():.3e}"
         assert np.all(np.abs(be_got - be_ref) <= 1e-5 * be_ref + 1e-15), f"{label}: backward errors"
+        x_rtol, xs_rtol, norm_factor = 1e-12, 1e-12, (1.2, 2.0)
     else:
         assert abs(got.restarts - ref["restarts"]) <= 1, f"{label}: restarts {got.restarts} vs {ref['restarts']}"
         k = min(rlen, len(s_ref), len(s_got))
         d = np.abs(s_got[:k] - s_ref[:k])
         assert np.all(d <= 1e-3 * s_ref[:k] + 1e-5 * minvb), f"{label}: cycle-0 history {d.max():.3e}"
+        floor = 1e-6 if mode == "single" else 1e-14
+        nc = min(len(be_ref), len(be_got)) - (0 if got.restarts == ref["restarts"] else 1)
+        for c in range(max(nc, 0)):
+            assert _ratio_ok(max(be_got[c], floor), max(be_ref[c], floor), 3.0), \
+                f"{label}: cycle {c} backward error {be_got[c]:.3e} vs {be_ref[c]:.3e}"
         if got.status == "converged":
             assert be_got[-1] <= tol, f"{label}: final backward error {be_got[-1]:.3e} > {tol}"
+        x_rtol, xs_rtol = (1e-5, 1e-4) if mode == "single" else (1e-9, 1e-7)
+        norm_factor = (10.0, 10.0)
+    same_cycles = got.restarts == ref["restarts"]
+    if x_head_ref is not None and same_cycles and xscale > 0:
+        dx = np.max(np.abs(_arr(got.x[:len(x_head_ref)]) - x_head_ref))
+        assert dx <= x_rtol * xscale, f"{label}: x head differs by {dx:.3e} (scale {xscale:.3e})"
+        xs_ref = float(ref["x_sum"])
+        assert abs(float(np.sum(got.x)) - xs_ref) <= xs_rtol * max(abs(xs_ref), xscale), f"{label}: x sum"
+    if "res_norm" in ref and same_cycles and hasattr(got, "res_norm"):
+        assert _ratio_ok(got.res_norm, ref["res_norm"], norm_factor[0]), \
+            f"{label}: resNorm {got.res_norm:.3e} vs {ref['res_norm']:.3e}"
+        if ref.get("err_norm"):
+            assert _ratio_ok(got.err_norm, ref["err_norm"], norm_factor[1]), \
+                f"{label}: errNorm {got.err_norm:.3e} vs {ref['err_norm']:.3e}"
 
 
 def as_ref(result) -> dict:
@@ -53,4 +97,5 @@ def as_ref(result) -> dict:
     return dict(status=result.status, restarts=result.restarts, total_iters=result.total_iters,
                 minvb_norm=result.minvb_norm, step_res=result.step_res, step_cycle=result.step_cycle,
                 cyc_r_norm=result.cyc_r_norm, cyc_normalization=result.cyc_normalization,
-                res_norm=result.res_norm, err_norm=result.err_norm)
+                res_norm=result.res_norm, err_norm=result.err_norm,
+                x_head=np.asarray(result.x[:16]), x_sum=float(np.sum(result.x)))

@@ -45,7 +45,7 @@ def test_oracle_vs_numpy_restatement(mpg, oracle, mode, orth, prec):
     q["step_cycle"] = np.repeat(np.arange(len(q["cyc_r_norm"])), 12)[: len(q["step_res"])]
     # the NumPy run plays "got", the oracle record plays "ref"
     ns = type("R", (), {})()
-    for k in ("status", "restarts", "total_iters", "step_res", "step_cycle", "cyc_r_norm", "cyc_normalization"):
+    for k in ("status", "restarts", "total_iters", "step_res", "step_cycle", "cyc_r_norm", "cyc_normalization", "x"):
         setattr(ns, k, q[k])
     compare(as_ref(r), ns, mode, tol, 12, f"np-vs-oracle {mode}/{orth}/{prec}")
 
@@ -140,7 +140,7 @@ def test_oracle_ilu_solve_vs_numpy_restatement(mpg, oracle, mode, prec):
     assert r.status == "converged"
     q["step_cycle"] = np.repeat(np.arange(len(q["cyc_r_norm"])), 12)[: len(q["step_res"])]
     ns = type("R", (), {})()
-    for k in ("status", "restarts", "total_iters", "step_res", "step_cycle", "cyc_r_norm", "cyc_normalization"):
+    for k in ("status", "restarts", "total_iters", "step_res", "step_cycle", "cyc_r_norm", "cyc_normalization", "x"):
         setattr(ns, k, q[k])
     compare(as_ref(r), ns, mode, 1e-10, 12, f"np-vs-oracle {mode}/cgs/{prec}")
     # the preconditioner does its job: fewer restarts than without it

@@ -45,5 +45,42 @@ def main():
                 res=(g.res_norm, rec["res_norm"]), err=(g.err_norm, rec["err_norm"]))), flush=True)
 
 
+
+
+def summary(path):
+    """Per-mode maxima of a parity_margins.jsonl (profiles/r02_parity_margins.txt)."""
+    gold = {}
+    for rec in json.loads((REPO / "tests/golden/gmres_golden.json").read_text())["cases"]:
+        c = rec["case"]
+        gold[f"{c['matrix']}-{c['mode']}-{c['orth']}-{c['prec']}-m{c['rlen']}"] = rec
+    per = {}
+    for line in open(path):
+        r = json.loads(line)
+        rec = gold[r["id"]]
+        mode = rec["case"]["mode"]
+        be = np.array(rec["cyc_r_norm"]) / np.array(rec["cyc_normalization"])
+        rel = np.array(r["be_rel"])
+        floor = 1e-6 if mode == "single" else 1e-14
+        above = be[:len(rel)] > floor
+        d = per.setdefault(mode, dict(runs=0, same_restarts=0, same_status=0, be_rel_above_floor=0.0,
+                                      xhead_rel=0.0, xsum_rel=0.0, res_factor=1.0, err_factor=1.0))
+        d["runs"] += 1
+        d["same_restarts"] += r["restarts"][0] == r["restarts"][1]
+        d["same_status"] += r["status"][0] == r["status"][1]
+        if above.any():
+            d["be_rel_above_floor"] = max(d["be_rel_above_floor"], float(rel[above].max()))
+        d["xhead_rel"] = max(d["xhead_rel"], r["xhead_rel"])
+        d["xsum_rel"] = max(d["xsum_rel"], r["xsum_rel"])
+        for k, key in (("res", "res_factor"), ("err", "err_factor")):
+            a, b = r[k]
+            if a > 0 and b > 0:
+                d[key] = max(d[key], a / b, b / a)
+    for mode, d in per.items():
+        print(mode, json.dumps({k: (float(f"{v:.3g}") if isinstance(v, float) else v) for k, v in d.items()}))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 3 and sys.argv[1] == "--summary":
+        summary(sys.argv[2])
+    else:
+        main()
