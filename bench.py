@@ -11,13 +11,24 @@ preconditioner, tol = 0 so the solve never stops early.
 
 One step = one restart cycle = check_initial on the host + 30 Arnoldi
 iterations + solution update + the next true-residual prologue (the fused
-engine's graph replay). value = iterations/s of the whole job; with N GPUs
-each rank owns a 1e6-row slice of an N*1e6-row BAND matrix (weak scaling)
-and value counts iterations x N shards.
+engine's graph replay).
 
-Also reported: the roofline of the dominant kernel (the Arnoldi SpMV phase,
-k_step_spmv) from HIP events on the engine's stream, and the CPU oracle
-(MKL restatement of kernels_mkl.cpp) on a bounded sample of the same solve.
+Scaling modes (one row-partitioned solve over all ranks either way):
+  weak (default)       each rank owns a 1e6-row BAND block of an N*1e6-row
+                       matrix; value = GMRES iterations x N blocks per second
+                       (the aggregate rate over 10M-nnz row blocks), and
+                       solve_iters_per_s is the one solve's iteration rate;
+  strong               --global-rows R: one R-row BAND matrix split over the
+                       N ranks (R = 1e7 is the north star's 100M-nnz matrix);
+                       value = that solve's iterations per second.
+
+Also reported (N = 1, rank 0): the roofline of the dominant kernel -- the
+Arnoldi SpMV as the cycle runs it (Givens folded), each launch timed by its
+own kernel events -- on the bytes its storage moves, against the 8 TB/s spec
+and the GPU's measured streaming peak (mpg_bw_probe, 2 GiB); the same SpMV
+on BAND-100M (a working set far past the 256 MB Infinity Cache) as the HBM
+figure; and the CPU oracle (MKL restatement of kernels_mkl.cpp) on the
+host cores, 1 warm-up + median of 5 per orthogonalisation.
 """
 import argparse
 import json
@@ -39,22 +50,35 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def stream_copy_peak(torch, nbytes=1 << 30, reps=5):
-    """Measured device-to-device copy rate (read + write bytes / s) of a
-    1 GiB fp32 buffer — larger than the 256 MB Infinity Cache, so it is HBM."""
-    src = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda").fill_(1.0)
-    dst = torch.empty_like(src)
-    dst.copy_(src)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        dst.copy_(src)
-    e1.record()
-    e1.synchronize()
-    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del src, dst
-    torch.cuda.empty_cache()
-    return gbs
+_CPU_INFO = None
+
+
+def cpu_info() -> dict:
+    """CPU model, physical cores of the machine (lscpu), and the cores this
+    process may run on (its affinity mask: the box's share of the host)."""
+    info = {"model": "unknown", "physical_cores": None, "affinity_cpus": len(os.sched_getaffinity(0))}
+    try:
+        import subprocess
+
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = {k.strip(): v.strip() for k, v in (ln.split(":", 1) for ln in out.splitlines() if ":" in ln)}
+        info["model"] = kv.get("Model name", "unknown")
+        info["physical_cores"] = int(kv.get("Core(s) per socket", "0")) * int(kv.get("Socket(s)", "1"))
+    except Exception:
+        pass
+    return info
+
+
+def cpu_threads() -> int:
+    """Threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS,
+    set to 16 per GPU on the pool), never more than the affinity mask or the
+    physical cores."""
+    info = _CPU_INFO or cpu_info()
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or info["affinity_cpus"]
+    n = min(n, info["affinity_cpus"])
+    if info["physical_cores"]:
+        n = min(n, info["physical_cores"])
+    return max(n, 1)
 
 
 def load_pkg():
@@ -63,17 +87,64 @@ def load_pkg():
     return _load()
 
 
-def pmc_traffic(profile_dir: Path, kernel_prefix: str):
+def pmc_traffic(profile_dir: Path, kernel_key: str):
     """HBM bytes per launch of the dominant kernel from a committed rocprofv3
-    PMC summary (profiles/*pmc*.json written by tools/pmc_summary.py), or None."""
+    PMC summary (profiles/pmc_traffic.json written by tools/pmc_summary.py:
+    FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or None."""
     f = profile_dir / "pmc_traffic.json"
     if not f.exists():
         return None
     try:
         d = json.loads(f.read_text())
-        return d.get(kernel_prefix, {}).get("hbm_bytes_per_launch")
+        return d.get(kernel_key, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+def spmv_roofline(eng, cycles: int) -> dict:
+    """The Arnoldi SpMV in its place in the cycle: mean kernel time over every
+    launch of `cycles` cycles (k = 0 plain, k >= 1 with the Givens step
+    folded), the bytes its storage moves, and SURVEY 8(d)'s CSR bytes."""
+    layout = eng.spmv_layout()
+    avg_ms, per = eng.time_spmv_incycle(cycles)
+    actual = eng.phase_bytes("spmv_storage")
+    csr = eng.phase_bytes("spmv")
+    return {"kernel": "k_step_sell" if layout["format"] == "sell" else "k_step_spmv", "layout": layout,
+            "avg_launch_ms": avg_ms, "launches": len(per), "min_launch_ms": min(per), "max_launch_ms": max(per),
+            "storage_bytes": actual, "csr_bytes": csr,
+            "achieved_gbs": actual / (avg_ms * 1e-3) / 1e9, "csr_equiv_gbs": csr / (avg_ms * 1e-3) / 1e9}
+
+
+def cpu_baseline(mpg, A, b, xt, opts, args):
+    """The oracle (kernels_mkl.cpp restatement over the image's MKL) on the
+    host cores: per orthogonalisation, 1 warm-up + the median of `runs`
+    solves of `cpu_cycles` restart cycles each."""
+    from oracle import binding
+
+    threads = cpu_threads()
+    info = _CPU_INFO or cpu_info()
+    by_orth = {}
+    for orth in dict.fromkeys([args.orth, "mgs"]):
+        o = dict(opts, orth=orth, max_restarts=args.cpu_cycles, threads=threads)
+        o.pop("device")
+        o.pop("spmv_format", None)
+        rates = []
+        for r in range(args.cpu_runs + 1):
+            res = binding.solve(mpg, A, b, xt, **o)
+            if r:  # run 0 is the warm-up
+                rates.append(res.total_iters / res.gmres_seconds)
+        by_orth[orth] = {"median": round(float(np.median(rates)), 2), "runs": [round(x, 2) for x in rates],
+                         "iterations_per_run": int(res.total_iters)}
+        log(f"[bench] CPU oracle {orth}: median {by_orth[orth]['median']} it/s over {args.cpu_runs} runs "
+            f"({threads} threads)")
+    return {"value": by_orth[args.orth]["median"], "unit": "GMRES it/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_cycles} restart cycles ({args.cpu_cycles * args.rlen} iterations) of the same "
+                      f"BAND-10M GMRES({args.rlen}) {args.mode}/{args.orth} solve; 1 warm-up + median of "
+                      f"{args.cpu_runs}; oracle backend {binding.backend()} (MKL restatement of kernels_mkl.cpp, "
+                      f"GNU OpenMP threading, OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, "
+                      f"OMP_PLACES={os.environ.get('OMP_PLACES')})",
+            "by_orth": by_orth, "cpu_model": info["model"], "physical_cores": info["physical_cores"],
+            "affinity_cpus": info["affinity_cpus"]}
 
 
 def main():
@@ -81,18 +152,31 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20, help="timed restart cycles")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n-local", type=int, default=1_000_000, help="rows per GPU")
+    ap.add_argument("--n-local", type=int, default=1_000_000, help="rows per GPU (weak scaling)")
+    ap.add_argument("--global-rows", type=int, default=0,
+                    help="strong scaling: one BAND matrix of this many rows split over the ranks")
     ap.add_argument("--rlen", type=int, default=30)
     ap.add_argument("--mode", default="mixed")
     ap.add_argument("--orth", default="cgs")
     ap.add_argument("--prec", default="identity")
-    ap.add_argument("--cpu-cycles", type=int, default=4, help="restart cycles in the CPU-baseline sample")
+    ap.add_argument("--cpu-cycles", type=int, default=2, help="restart cycles per CPU-baseline solve")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU-baseline solves (after 1 warm-up)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--roofline-reps", type=int, default=10)
+    ap.add_argument("--roofline-cycles", type=int, default=3)
+    ap.add_argument("--hbm-rows", type=int, default=10_000_000,
+                    help="rows of the BAND matrix of the HBM-scale SpMV figure (0: skip)")
     ap.add_argument("--spmv-format", default="auto", choices=["auto", "csr", "sell"],
                     help="Arnoldi SpMV storage (auto: SELL-64 when its padding is small)")
     args = ap.parse_args()
 
+    # the CPU facts before anything binds this thread (libgomp pins the
+    # initial thread to one place under OMP_PROC_BIND)
+    global _CPU_INFO
+    _CPU_INFO = cpu_info()
+    # the CPU baseline's OpenMP placement (automated.py:13-15); libgomp reads
+    # these when it is first loaded, which importing torch does
+    os.environ.setdefault("OMP_PROC_BIND", "spread")
+    os.environ.setdefault("OMP_PLACES", "threads")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -115,9 +199,11 @@ def main():
             torch.cuda.set_device(local_rank)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    # global BAND matrix of world * n_local rows; this rank owns one row block
-    n = args.n_local * world
-    r0, r1 = rank * args.n_local, (rank + 1) * args.n_local
+    # one BAND matrix; this rank owns one contiguous row block of it
+    strong = args.global_rows > 0
+    n = args.global_rows if strong else args.n_local * world
+    starts = [n * q // world for q in range(world + 1)] if strong else [q * args.n_local for q in range(world + 1)]
+    r0, r1 = starts[rank], starts[rank + 1]
     t0 = time.time()
     A = mpg.gen_band(n, 5, 4, seed=7, row_begin=r0, row_end=r1)
     xt = mpg.rand_vect(n, 42)
@@ -131,7 +217,6 @@ def main():
         eng = mpg.Engine(A, b, xt, **opts)
     else:
         # halo plan: exchange "rows I need from you" with every rank, then RCCL
-        starts = [q * args.n_local for q in range(world + 1)]
         plan = mpg.HaloPlan(rank, world, starts, A)
         needs = {q: plan.recv_rows(q).tolist() for q in range(world) if q != rank}
         gathered = [None] * world
@@ -162,56 +247,81 @@ def main():
         elapsed = float(tt.item())
     iters = eng.total_iters - it0
     assert ran == args.steps and iters == args.steps * args.rlen, (ran, iters)
-    value = iters * world / elapsed
+    solve_rate = iters / elapsed
+    value = solve_rate if strong else solve_rate * world
     ms_per_step = 1e3 * elapsed / args.steps
-    log(f"[bench] {args.steps} cycles, {iters} iterations in {elapsed:.4f}s -> {iters / elapsed:.1f} it/s")
+    log(f"[bench] {args.steps} cycles, {iters} iterations in {elapsed:.4f}s -> {solve_rate:.1f} it/s")
 
-    # roofline of the dominant kernel: the Arnoldi SpMV phase, mean over k
-    layout = eng.spmv_layout()
-    kernel = "k_step_sell" if layout["format"] == "sell" else "k_step_spmv"
-    avg_ms = eng.time_phase("spmv", args.roofline_reps)
-    bytes_per_launch = eng.phase_bytes("spmv")
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(REPO / "profiles", kernel)
-    stream = stream_copy_peak(torch)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": kernel, "avg_launch_ms": round(avg_ms, 5),
-                "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                "bytes_formula": "SURVEY 8(d) B_spmv = nnz*(s_v+4) + (n+1)*4 + 2*n*s_x",
-                "measured_copy_peak": round(stream, 1), "frac_of_measured": round(achieved / stream, 4)}
-    log(f"[bench] {kernel} {avg_ms * 1e3:.1f} us/launch, {achieved:.0f} GB/s algorithmic, storage {layout}; "
-        f"measured copy peak {stream:.0f} GB/s")
+    # roofline of the dominant kernel: the Arnoldi SpMV as the cycle runs it
+    sp = spmv_roofline(eng, args.roofline_cycles)
     eng.close()
-
+    log(f"[bench] {sp['kernel']} in-cycle {sp['avg_launch_ms'] * 1e3:.2f} us/launch over {sp['launches']} launches: "
+        f"{sp['achieved_gbs']:.0f} GB/s on its storage bytes, {sp['csr_equiv_gbs']:.0f} GB/s CSR-equivalent; "
+        f"{sp['layout']}")
+    roofline = None
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import binding
-
-        cpu_opts = dict(opts, max_restarts=args.cpu_cycles)
-        cpu_opts.pop("device")
-        r = binding.solve(mpg, A, b, xt, **cpu_opts)
-        cpu_its = r.total_iters / r.gmres_seconds
-        cpu = {"value": round(cpu_its, 2), "unit": "GMRES it/s", "cores": binding.lib().oracle_max_threads(),
-               "kind": "port",
-               "sample": f"{r.total_iters} iterations ({args.cpu_cycles} restart cycles) of the same BAND-10M "
-                         f"GMRES({args.rlen}) {args.mode}/{args.orth} solve, oracle backend "
-                         f"{binding.backend()} (MKL restatement of kernels_mkl.cpp)"}
-        log(f"[bench] CPU oracle: {cpu_its:.2f} it/s on {cpu['cores']} threads")
+    if rank == 0 and world == 1:
+        peak_read = mpg.bw_probe("read", 2 << 30, 3, local_rank)
+        peak_copy = mpg.bw_probe("copy", 1 << 30, 3, local_rank)
+        measured = max(peak_read, peak_copy)
+        log(f"[bench] measured streaming peak: read {peak_read:.0f} GB/s, copy {peak_copy:.0f} GB/s")
+        hbm = None
+        if args.hbm_rows > 0:
+            t1 = time.time()
+            Ah = mpg.gen_band(args.hbm_rows, 5, 4, seed=7)
+            xh = mpg.rand_vect(args.hbm_rows, 42)
+            bh = mpg.host_spmv(Ah, xh)
+            eh = mpg.Engine(Ah, bh, xh, **dict(opts, max_restarts=4))
+            eh.run(1)
+            hs = spmv_roofline(eh, 2)
+            eh.close()
+            del Ah, bh, xh
+            hbm = {"workload": f"BAND n={args.hbm_rows}, nnz={10 * args.hbm_rows - 25} (working set > 256 MB "
+                               f"Infinity Cache), same solve", "kernel": hs["kernel"],
+                   "avg_launch_ms": round(hs["avg_launch_ms"], 5), "storage_bytes_per_launch": int(hs["storage_bytes"]),
+                   "achieved": round(hs["achieved_gbs"], 1), "frac": round(hs["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                   "frac_of_measured": round(hs["achieved_gbs"] / measured, 4),
+                   "csr_equiv_gbs": round(hs["csr_equiv_gbs"], 1), "layout": hs["layout"]}
+            log(f"[bench] HBM scale ({time.time() - t1:.1f}s): {hs['avg_launch_ms'] * 1e3:.1f} us/launch, "
+                f"{hs['achieved_gbs']:.0f} GB/s on storage bytes")
+        traffic = pmc_traffic(REPO / "profiles", sp["kernel"] + ":fold")
+        roofline = {"bound": "hbm", "achieved": round(sp["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(sp["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": sp["kernel"] + " (in-cycle, Givens folded for k >= 1)",
+                    "avg_launch_ms": round(sp["avg_launch_ms"], 5), "launches_timed": sp["launches"],
+                    "timing": "hipExtLaunchKernel start/stop events of each in-cycle launch",
+                    "bytes_per_launch": int(sp["storage_bytes"]),
+                    "bytes_formula": "storage: SELL slots x (col + value bytes) + slice offsets + 3 n s_T "
+                                     "(w_prev read, v_k and w written)",
+                    "csr_equiv_bytes_per_launch": int(sp["csr_bytes"]),
+                    "csr_equiv_achieved": round(sp["csr_equiv_gbs"], 1),
+                    "csr_bytes_formula": "SURVEY 8(d) B_spmv = nnz*(s_v+4) + (n+1)*4 + 2*n*s_x",
+                    "measured_peak": round(measured, 1), "measured_peak_read": round(peak_read, 1),
+                    "measured_peak_copy": round(peak_copy, 1),
+                    "frac_of_measured": round(sp["achieved_gbs"] / measured, 4),
+                    "cache_note": "the BAND-10M Arnoldi working set (~190 MB) fits the 256 MB Infinity Cache; "
+                                  "hbm_scale is the same kernel past it",
+                    "hbm_scale": hbm}
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(mpg, A, b, xt, opts, args)
 
     if rank == 0:
+        scaling = "strong" if strong else "weak"
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GMRES iterations/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic", "roofline": roofline, "cpu_baseline": cpu,
-            "config": {"workload": f"BAND-10M per GPU: banded CSR n={n}, offsets -5..+4, nnz={global_nnz}; "
+            "solve_iters_per_s": round(solve_rate, 2),
+            "config": {"workload": f"BAND banded CSR n={n}, offsets -5..+4, nnz={global_nnz} "
+                                   f"({'split over' if strong else '1e6 rows = 10M nnz per GPU,'} {world} GPU(s)); "
                                    f"GMRES({args.rlen}) {args.mode} (fp32 Arnoldi, fp64 residual/update), "
                                    f"{args.orth}, {args.prec} preconditioner, tol=0",
                        "step": f"one restart cycle = {args.rlen} iterations",
-                       "value_counts": "GMRES iterations x 10M-nnz row blocks (one per GPU) per second",
-                       "rows_per_gpu": args.n_local, "nnz": global_nnz,
-                       "spmv_storage": layout,
+                       "value_counts": ("GMRES iterations of the one solve per second" if strong else
+                                        "GMRES iterations x 10M-nnz row blocks (one per GPU) per second; "
+                                        "solve_iters_per_s is the solve's own rate"),
+                       "rows_per_gpu": (r1 - r0), "nnz": global_nnz, "spmv_storage": sp["layout"],
                        "parallelism": f"row-partition x{world} (halo send/recv + fp64 all-reduce over RCCL)"},
         }
         print(json.dumps(line), flush=True)

@@ -91,6 +91,8 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_total_iters.argtypes = [C.c_void_p]
     lib.mpg_engine_total_iters.restype = C.c_int64
     lib.mpg_engine_time_phase.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    lib.mpg_engine_time_spmv_incycle.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double),
+                                                 C.POINTER(C.c_double), C.c_int]
     lib.mpg_engine_phase_bytes.argtypes = [C.c_void_p, C.c_int]
     lib.mpg_engine_phase_bytes.restype = C.c_double
     lib.mpg_engine_destroy.argtypes = [C.c_void_p]
@@ -454,6 +456,24 @@ class HaloPlan:
             pass
 
 
+def bw_probe(kind: str = "read", nbytes: int = 2 << 30, reps: int = 3, device: int = 0) -> float:
+    """Measured HBM streaming rate in GB/s (mpg_bw_probe): "read" counts the
+    bytes read by a float4 stream, "copy" read + written bytes."""
+    lib = hip_lib()
+    lib.mpg_bw_probe.argtypes = [C.c_void_p, C.c_int, C.c_size_t, C.c_int, C.POINTER(C.c_double)]
+    ctx = C.c_void_p()
+    if lib.mpg_ctx_create(device, C.byref(ctx)):
+        raise RuntimeError("mpg_ctx_create failed")
+    try:
+        gbs = C.c_double()
+        st = lib.mpg_bw_probe(ctx, {"read": 0, "copy": 1}[kind], nbytes, reps, C.byref(gbs))
+        if st:
+            raise RuntimeError(f"mpg_bw_probe failed ({st})")
+        return gbs.value
+    finally:
+        lib.mpg_ctx_destroy(ctx)
+
+
 def rccl_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     if host_lib().mpg_rccl_unique_id(buf, 128):
@@ -474,7 +494,7 @@ class Engine:
     restarted solve cycle by cycle — what bench.py times. Engine.distributed
     builds one rank of a row-partitioned solve over RCCL."""
 
-    PHASES = {"spmv": 0, "prologue": 1, "cgs_update": 2, "dots": 3}
+    PHASES = {"spmv": 0, "prologue": 1, "cgs_update": 2, "dots": 3, "spmv_storage": 4}
 
     def __init__(self, A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, _dist=None, **opts):
         opts.pop("engine", None)
@@ -517,6 +537,18 @@ class Engine:
         if self._lib.mpg_engine_time_phase(self._h, self.PHASES[phase], reps, C.byref(ms)):
             raise RuntimeError("mpg_engine_time_phase failed")
         return ms.value
+
+    def time_spmv_incycle(self, cycles: int = 3) -> tuple:
+        """(mean ms, per-launch ms in cycle order) of the Arnoldi SpMV as the
+        cycle runs it (Givens folded for k >= 1), each launch timed by its own
+        kernel events; measurement only (the cycles skip the restart checks)."""
+        ms = C.c_double()
+        cap = 4096
+        per = (C.c_double * cap)()
+        cnt = self._lib.mpg_engine_time_spmv_incycle(self._h, cycles, C.byref(ms), per, cap)
+        if cnt < 0:
+            raise RuntimeError(f"mpg_engine_time_spmv_incycle failed ({cnt})")
+        return ms.value, [per[i] for i in range(min(cnt, cap))]
 
     def phase_bytes(self, phase: str) -> float:
         return float(self._lib.mpg_engine_phase_bytes(self._h, self.PHASES[phase]))

@@ -1504,7 +1504,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                 constexpr int Wc = decltype(wc)::value;
                 const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
                 auto launch = [&](auto kern, SellDots dd) {
-                    kern<<<grid, kBlock, 0, a->ctx->stream>>>(
+                    launch_timed(a->ctx, kern, dim3(grid), dim3(kBlock),
                             a->d.n, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
@@ -1533,7 +1533,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
             });
         }
         auto kern = fold ? k_step_spmv<T, P, VI, true> : k_step_spmv<T, P, VI, false>;
-        kern<<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(
+        launch_timed(a->ctx, kern, dim3(rb_grid(a)), dim3(kBlock),
             A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,
             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,
             diag, static_cast<T*>(a->w[(k + 1) & 1]), gf);
@@ -1745,6 +1745,13 @@ const void* mpg_arnoldi_basis_dev(mpg_arnoldi_t a, int64_t* ld) {
     return a->V;
 }
 const void* mpg_arnoldi_hessenberg_dev(mpg_arnoldi_t a) { return a ? a->H : nullptr; }
+const void* mpg_arnoldi_inv_dev(mpg_arnoldi_t a) { return a ? a->inv() : nullptr; }
+int mpg_arnoldi_time_next_spmv(mpg_arnoldi_t a, void* start_event, void* stop_event) {
+    if (!a || !start_event || !stop_event) return MPG_ERR_ARG;
+    a->ctx->time_start = static_cast<hipEvent_t>(start_event);
+    a->ctx->time_stop = static_cast<hipEvent_t>(stop_event);
+    return MPG_OK;
+}
 int mpg_arnoldi_num_groups(mpg_arnoldi_t a) { return a ? a->G : 0; }
 double* mpg_arnoldi_partials_dev(mpg_arnoldi_t a) { return a ? a->last_part : nullptr; }
 // the last producer wrote last_G partials per column; the one-column

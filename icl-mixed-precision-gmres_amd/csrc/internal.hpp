@@ -2,8 +2,9 @@
 // Not part of the C-ABI (see include/mpgmres/capi.h).
 #pragma once
 
-#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <string>
@@ -18,6 +19,9 @@ struct mpg_ctx {
     double* red_ws = nullptr;
     size_t red_ws_elems = 0;
     std::string last_error;
+    // measurement hook (mpg_arnoldi_time_next_spmv): the next launch made
+    // through launch_timed records its own start/stop on these events
+    hipEvent_t time_start = nullptr, time_stop = nullptr;
 };
 
 // Analysed CSR structure (row blocks of the CSR-adaptive schedule).
@@ -57,6 +61,19 @@ inline int set_hip_error(mpg_ctx* ctx, hipError_t e, const char* what) {
         hipError_t mpg_e_ = hipGetLastError();                          \
         if (mpg_e_ != hipSuccess) return mpg::set_hip_error(ctx, mpg_e_, "kernel launch"); \
     } while (0)
+
+// A kernel launch on the context's stream; when a timing pair is armed it
+// goes through hipExtLaunchKernelGGL, whose events carry the kernel's own
+// start and end (no queue or dispatch time around it), and is disarmed.
+template <class K, class... A>
+inline void launch_timed(mpg_ctx* c, K kern, dim3 grid, dim3 block, A... args) {
+    if (c->time_start) {
+        hipExtLaunchKernelGGL(kern, grid, block, 0, c->stream, c->time_start, c->time_stop, 0, args...);
+        c->time_start = c->time_stop = nullptr;
+    } else {
+        kern<<<grid, block, 0, c->stream>>>(args...);
+    }
+}
 
 inline int grid_for(int64_t n, int per_thread, int cap = 2048) {
     int64_t g = (n + (int64_t)kBlock * per_thread - 1) / ((int64_t)kBlock * per_thread);

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 
 #include "gmres.hpp"
@@ -55,6 +56,32 @@ ModeTypes types_for(int mode) {
 }
 size_t dsize(int t) { return t == MPG_F64 ? 8 : t == MPG_F32 ? 4 : 2; }
 
+// LostOrthogonality (IterUtil.hpp:172-227) on the fused engine's basis. The
+// base check (count, restart at m) comes first, as in the reference; the
+// V^T v / S-column update is the engine's (orth_loss_step), which returns
+// dot(s_col, s_col) rounded to the basis precision.
+class LostOrthogonalityFused : public Convergence<double, void> {
+    using Base = Convergence<double, void>;
+    const double restart_tol_squared_;
+    double current_loss_squared_ = 0;
+
+public:
+    std::function<double(size_t)> step_loss;
+    LostOrthogonalityFused(double tol, double restart_tol, size_t m, size_t max_restarts)
+        : Base(tol, m, max_restarts), restart_tol_squared_(restart_tol * restart_tol) {}
+    iteration_action check_initial(double r, double nrm, double pr, double pb) override {
+        current_loss_squared_ = 0;
+        return Base::check_initial(r, nrm, pr, pb);
+    }
+    iteration_action check(size_t k, double res, double bnorm) override {
+        const iteration_action a = Base::check(k, res, bnorm);
+        if (a != iteration_next) return a;
+        current_loss_squared_ += step_loss(k);
+        return current_loss_squared_ >= restart_tol_squared_ ? iteration_restart : iteration_next;
+    }
+    bool needs_arnoldi_residual() const override { return true; }
+};
+
 }  // namespace
 
 struct FusedEngine::Impl {
@@ -87,9 +114,12 @@ struct FusedEngine::Impl {
     bool fuse_dots = false;     // ... from dots formed in the SpMV launch
     bool fuse_dots_required = false;
     int timed = -1;                  // phase whose launches time_phase brackets with events
+    bool timed_inplace = false;      // ... the cycle's own SpMV launch, by its kernel events
     std::vector<hipEvent_t> marks;   // ... begin/end pairs
     std::vector<int32_t> rowptr_host;
     mpg_ilu_t ilu = nullptr;  // ILU(0) factors (prec ilu / ilu_jacobi), applied between phase kernels
+    bool orthloss = false;    // LostOrthogonality: v_{k+1} stored each step, S / u below
+    DevMem loss_S, loss_u;    // (m+1) x (m+1) and m+2 of T, zero-filled (IterUtil.hpp:185-191)
 
     ~Impl() {
         if (ilu) mpg_ilu_destroy(ilu);
@@ -162,8 +192,9 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     if (ilu && comm)
         throw std::invalid_argument("ILU / ILU-Jacobi factor the whole matrix: not available on a row-partitioned solve");
     if (!ilu && a.prec != MPG_PREC_IDENTITY && a.prec != MPG_PREC_JACOBI) throw std::invalid_argument("Unknown prec type");
-    if (a.orthloss && a.rtol != 0)
-        throw std::invalid_argument("the LostOrthogonality restart needs v_{k+1} on the host: use engine=surface");
+    I.orthloss = a.orthloss && a.rtol != 0 && !a.repeat_iter;  // alloc_convergence order (gmres_perf_test.cpp:184-195)
+    if (I.orthloss && comm)
+        throw std::invalid_argument("LostOrthogonality restarts are not available on a row-partitioned solve");
     if (a.rowptr[a.n] != a.nnz) throw std::invalid_argument("rowptr[n] != nnz");
 
     // structure + analysed schedule
@@ -302,7 +333,13 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     const size_t mm = (size_t)a.rlen, mr = (size_t)a.max_restarts;
     if (a.rtol == 0) conv_ = std::make_unique<Convergence<double, void>>(a.tol, mm, mr);
     else if (a.repeat_iter) conv_ = std::make_unique<RepeatIteration_Convergence<double, void>>(a.tol, a.rtol, mm, mr);
-    else conv_ = std::make_unique<RelPrecRes_Convergence<double, void>>(a.tol, a.rtol, mm, mr);
+    else if (I.orthloss) {
+        auto lo = std::make_unique<LostOrthogonalityFused>(a.tol, a.rtol, mm, mr);
+        lo->step_loss = [this](size_t k) { return orth_loss_step(k); };
+        I.loss_S = DevMem(ctx, (size_t)(mm + 1) * (mm + 1) * dsize(ty.T));
+        I.loss_u = DevMem(ctx, (size_t)(mm + 2) * dsize(ty.T));
+        conv_ = std::move(lo);
+    } else conv_ = std::make_unique<RelPrecRes_Convergence<double, void>>(a.tol, a.rtol, mm, mr);
     conv_->total_iters = 0;
 
     const char* env = std::getenv("MPG_NO_GRAPH");
@@ -454,6 +491,52 @@ void FusedEngine::step(int k, bool fold) {
         check(mpg_arnoldi_cgs(I.arn, k, last_pass), "cgs", I.ctx);
     }
     if (!fold) givens(k);
+}
+
+// v_{k+1} = T(w * (1/h_{k+1,k})) into V(:,k+1) right after step k, as the
+// reference's add_vector does (Orthogonalization.hpp:51-60); the next SpMV
+// forms and stores the same value again. Only LostOrthogonality needs it
+// early: it reads the basis column after the newest one.
+void FusedEngine::store_next_basis(int k) {
+    Impl& I = *p_;
+    int64_t ld = 0;
+    void* V = const_cast<void*>(mpg_arnoldi_basis_dev(I.arn, &ld));
+    const void* inv = mpg_arnoldi_inv_dev(I.arn);
+    const void* w = mpg_arnoldi_wprev_dev(I.arn, k + 1);
+    const size_t off = (size_t)(k + 1) * (size_t)ld;
+    if (I.ty.T == MPG_F64)
+        check(mpg_scal_copy_dev_f64(I.ctx, I.n, (const double*)inv, (const double*)w, (double*)V + off), "v_k+1", I.ctx);
+    else
+        check(mpg_scal_copy_dev_f32(I.ctx, I.n, (const float*)inv, (const float*)w, (float*)V + off), "v_k+1", I.ctx);
+}
+
+// LostOrthogonality_Convergence::check body (IterUtil.hpp:206-216) for
+// check(k): u = V(:,0:k+1)^T V(:,k+1); s_col = S(0:k+1,k+1) = u - S(0:k+1,
+// 0:k+1) u; returns dot(s_col, s_col). V(:,k+1) is the column after the
+// newest basis vector: what an earlier cycle left there, or zeros.
+double FusedEngine::orth_loss_step(size_t kk) {
+    Impl& I = *p_;
+    const int64_t k = (int64_t)kk, ldS = I.m + 1;
+    int64_t ld = 0;
+    const void* V = mpg_arnoldi_basis_dev(I.arn, &ld);
+    if (I.ty.T == MPG_F64) {
+        const double* Vd = (const double*)V;
+        double *u = I.loss_u.as<double>(), *S = I.loss_S.as<double>(), *scol = S + (k + 1) * ldS;
+        check(mpg_gemv_f64(I.ctx, 1, I.n, k + 1, 1.0, Vd, ld, Vd + (k + 1) * ld, 0.0, u), "gemv", I.ctx);
+        check(mpg_copy_f64f64(I.ctx, k + 1, u, scol), "copy", I.ctx);
+        check(mpg_gemv_f64(I.ctx, 0, k + 1, k + 1, -1.0, S, ldS, u, 1.0, scol), "gemv", I.ctx);
+        double d = 0;
+        check(mpg_dot_f64_host(I.ctx, k + 1, scol, scol, &d), "dot", I.ctx);
+        return d;
+    }
+    const float* Vf = (const float*)V;
+    float *u = I.loss_u.as<float>(), *S = I.loss_S.as<float>(), *scol = S + (k + 1) * ldS;
+    check(mpg_gemv_f32(I.ctx, 1, I.n, k + 1, 1.0f, Vf, ld, Vf + (k + 1) * ld, 0.0f, u), "gemv", I.ctx);
+    check(mpg_copy_f32f32(I.ctx, k + 1, u, scol), "copy", I.ctx);
+    check(mpg_gemv_f32(I.ctx, 0, k + 1, k + 1, -1.0f, S, ldS, u, 1.0f, scol), "gemv", I.ctx);
+    float d = 0;
+    check(mpg_dot_f32_host(I.ctx, k + 1, scol, scol, &d), "dot", I.ctx);
+    return (double)d;
 }
 
 void FusedEngine::update(int k) { check(mpg_arnoldi_update(p_->arn, k), "update", p_->ctx); }
@@ -612,6 +695,7 @@ int FusedEngine::run(int max_cycles, bool& done) {
         // adaptive restart strategies: one host read of |s(k+1)| per step
         for (int k = 0;; ++k) {
             step(k, false);
+            if (I.orthloss) store_next_basis(k);
             read_report(4 + k + 1);
             if (I.ilu) check_ilu_fault(I.ilu);
             const double res = I.report_host[4 + k];
@@ -681,6 +765,18 @@ double FusedEngine::phase_bytes(int which) const {
         return z * (sV + 4) + (n + 1) * 4 + 2 * n * sT + jac * n * sP;
     }
     if (which == 1) return z * (sX + 4) + (n + 1) * 4 + 3 * n * sX + n * sT + jac * n * sP;
+    if (which == 4) {
+        // the bytes the Arnoldi SpMV's own storage moves per launch: SELL-64
+        // slots (column offset + value) and int64 slice offsets, or CSR
+        // values + int32 columns + row pointers; then w_prev read once, v_k
+        // stored to V(:,k), w written, the Jacobi diagonal when fused
+        int32_t fmt = 0, W = 0, cb = 0, win = 0;
+        int64_t stored = 0;
+        check(mpg_arnoldi_spmv_layout(I.arn, &fmt, &W, &cb, &stored, &win), "layout", I.ctx);
+        const double vec = 3 * n * sT + jac * n * sP;
+        if (fmt == 2) return (double)stored * (cb + sV) + std::ceil(n / 64.0) * 8 + vec;
+        return z * (sV + 4) + (n + 1) * 4 + vec;
+    }
     if (which == 3) {
         // panel dots, mean over k: V(:,0..k) and w read
         double cols = 0;
@@ -702,12 +798,15 @@ mpg_arnoldi_t FusedEngine::arnoldi() const { return p_->arn; }
 // the engine's state meaningless: time_phase is for measurement only.
 constexpr int kTimedReplays = 10;
 
-double FusedEngine::time_phase(int which, int reps) {
+double FusedEngine::time_phase(int which, int reps, bool inplace, std::vector<double>* per_launch) {
     Impl& I = *p_;
+    if (inplace && which != 0) throw std::invalid_argument("in-place timing covers the Arnoldi SpMV only");
     I.timed = which;
+    I.timed_inplace = inplace;
     I.marks.clear();
     for (int r = 0; r < reps; ++r) cycle_program();
     I.timed = -1;
+    I.timed_inplace = false;
     hipck(hipStreamSynchronize(I.stream()), "sync");
     float total_ms = 0;
     const size_t pairs = I.marks.size() / 2;
@@ -715,21 +814,29 @@ double FusedEngine::time_phase(int which, int reps) {
         float ms = 0;
         hipck(hipEventElapsedTime(&ms, I.marks[2 * q], I.marks[2 * q + 1]), "elapsed");
         total_ms += ms;
+        if (per_launch) per_launch->push_back(inplace ? ms : ms / kTimedReplays);
     }
     for (hipEvent_t e : I.marks) (void)hipEventDestroy(e);
     I.marks.clear();
-    return pairs ? total_ms / (pairs * kTimedReplays) : 0.0;
+    return pairs ? total_ms / (pairs * (inplace ? 1 : kTimedReplays)) : 0.0;
 }
 
+// replay mode: kTimedReplays plain launches between one event pair ahead of
+// the site's own launch; in-place mode (SpMV): arm the kernel events that
+// the site's own launch records (mpg_arnoldi_time_next_spmv)
 template <class F>
 void FusedEngine::timed(int phase, F&& launch) {
     Impl& I = *p_;
     if (I.timed != phase) return;
     hipEvent_t e[2];
     for (auto& x : e) hipck(hipEventCreate(&x), "event");
-    hipck(hipEventRecord(e[0], I.stream()), "record");
-    for (int r = 0; r < kTimedReplays; ++r) launch();
-    hipck(hipEventRecord(e[1], I.stream()), "record");
+    if (I.timed_inplace) {
+        check(mpg_arnoldi_time_next_spmv(I.arn, e[0], e[1]), "time spmv", I.ctx);
+    } else {
+        hipck(hipEventRecord(e[0], I.stream()), "record");
+        for (int r = 0; r < kTimedReplays; ++r) launch();
+        hipck(hipEventRecord(e[1], I.stream()), "record");
+    }
     I.marks.push_back(e[0]);
     I.marks.push_back(e[1]);
 }
@@ -822,6 +929,19 @@ int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms) {
         mpg::ScopedContext scope(e->ctx);
         *avg_ms = e->eng->time_phase(which, reps);
         return MPG_OK;
+    } catch (const std::exception&) {
+        return MPG_ERR_HIP;
+    }
+}
+
+int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, double* per_launch_ms, int cap) {
+    if (!e || !e->eng || !avg_ms || cycles < 1 || cap < 0 || (cap && !per_launch_ms)) return MPG_ERR_ARG;
+    try {
+        mpg::ScopedContext scope(e->ctx);
+        std::vector<double> t;
+        *avg_ms = e->eng->time_phase(0, cycles, true, &t);
+        for (size_t i = 0; i < t.size() && (int)i < cap; ++i) per_launch_ms[i] = t[i];
+        return (int)t.size();
     } catch (const std::exception&) {
         return MPG_ERR_HIP;
     }

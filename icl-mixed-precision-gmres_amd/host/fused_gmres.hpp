@@ -76,7 +76,7 @@ public:
     void finish_report(mpg_solve_result* r);  // resNorm/errNorm + x with the original fp64 A
 
     size_t total_iters() const { return conv_->total_iterations(); }
-    double time_phase(int which, int reps);
+    double time_phase(int which, int reps, bool inplace = false, std::vector<double>* per_launch = nullptr);
     double phase_bytes(int which) const;
     mpg_arnoldi_t arnoldi() const;
     void sync();
@@ -103,6 +103,8 @@ private:
     template <class F>
     void timed(int phase, F&& launch);
     void update(int k);
+    void store_next_basis(int k);
+    double orth_loss_step(size_t k);
     void read_report(int count);
     void cycle_program();
     void ensure_graph();

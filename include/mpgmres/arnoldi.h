@@ -138,6 +138,13 @@ int mpg_arnoldi_report_len(mpg_arnoldi_t a);
 /* The Krylov basis (for tests): V column j of T, ld elements apart */
 const void* mpg_arnoldi_basis_dev(mpg_arnoldi_t a, int64_t* ld);
 const void* mpg_arnoldi_hessenberg_dev(mpg_arnoldi_t a);  /* (m+1) x m, column-major, T */
+/* 1/h_{k+1,k} (T) written by the Givens step k for the next SpMV's
+ * normalisation (Orthogonalization.hpp:56-59 reciprocal) */
+const void* mpg_arnoldi_inv_dev(mpg_arnoldi_t a);
+/* measurement: the next Arnoldi SpMV launch (any form: plain, Givens folded,
+ * dots fused) records its own kernel start/stop on these hipEvent_t
+ * (hipExtLaunchKernel events: the kernel alone, not the queue around it) */
+int mpg_arnoldi_time_next_spmv(mpg_arnoldi_t a, void* start_event, void* stop_event);
 
 /* Number of workgroups of the row-block phase kernels (partials per column). */
 int mpg_arnoldi_num_groups(mpg_arnoldi_t a);

@@ -66,6 +66,14 @@ int mpg_memcpy_h2d(mpg_ctx_t ctx, void* dst_dev, const void* src_host, size_t by
 int mpg_memcpy_d2h(mpg_ctx_t ctx, void* dst_host, const void* src_dev, size_t bytes);
 int mpg_memcpy_d2d(mpg_ctx_t ctx, void* dst_dev, const void* src_dev, size_t bytes);
 
+/* Measured HBM streaming rate (GB/s) of this GPU: kind 0 = float4 read
+ * (bytes read), 1 = float4 copy (bytes read + written), on fresh buffers of
+ * `bytes` (>= 1 MiB; use >= 1 GiB to stay clear of the Infinity Cache); the
+ * best kernel time (hipExtLaunchKernel events) over a grid/unroll sweep with
+ * `reps` launches each. No reference counterpart: the achievable peak
+ * bench.py reports beside the 8 TB/s spec. */
+int mpg_bw_probe(mpg_ctx_t ctx, int kind, size_t bytes, int reps, double* gbs_out);
+
 /* ---- BLAS-1 (kernels.hpp:11-101; kernels_mkl.cpp:73-211) ----
  * Reductions accumulate in fp64 for both precisions and are deterministic
  * (fixed two-stage tree); *_dev variants leave the result in device memory

@@ -107,6 +107,12 @@ int64_t mpg_engine_total_iters(mpg_engine_t e);
  * cycle (which: 0 = Arnoldi SpMV k_step_spmv, 1 = residual prologue,
  * 2 = CGS update, 3 = Gram-Schmidt panel dots) */
 int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms);
+/* the Arnoldi SpMV as it runs inside the cycle (Givens folded for k >= 1),
+ * timed by each launch's own kernel events over `cycles` eager cycles:
+ * returns the launch count (m per cycle), the mean in *avg_ms and up to
+ * `cap` per-launch times in cycle order (measurement only: the cycles run
+ * without the host's restart checks) */
+int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, double* per_launch_ms, int cap);
 /* algorithmic bytes of one launch of phase `which` */
 double mpg_engine_phase_bytes(mpg_engine_t e, int which);
 /* storage of the engine's Arnoldi SpMV (mpg_arnoldi_spmv_layout) */

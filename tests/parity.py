@@ -9,8 +9,13 @@ fp64 Arnoldi with an fp64 preconditioner (mode baseline):
   * per-step |s(k+1)|, cycle 0:  |Δ| <= 1e-8 |s_ref| + 1e-12 ||M^-1 b||;
     later cycles:               |Δ| <= 1e-5 |s_ref| + 1e-10 ||M^-1 b||;
   * every cycle's backward error: |Δ| <= 1e-5 be_ref + 1e-15;
-  * x (first 16 entries and the sum): relative 1e-12 of max|x_ref|;
-  * final resNorm within a factor 1.2, errNorm within a factor 2.
+  * x, first 16 entries: |Δ| <= 1e-12 max|x_ref| + 0.5 (e_ref + e_got),
+    sum: |Δ| <= 1e-12 max(|Σx_ref|, max|x_ref|) + 0.5 sqrt(n) (e_ref + e_got),
+    where e = errNorm = ||x - x_true||_2 of each run — two solves of the
+    same system agree to within the accuracy they reached, never closer
+    than rounding (an ill-conditioned C1 differs at 2e-12 relative);
+  * final resNorm within a factor 1.2 and errNorm within a factor 2, both
+    above a floor of 64 eps (||b|| + ||A||_F ||x||) / eps-level errors.
 fp32 Arnoldi, or fp64 Arnoldi whose vectors pass through an fp32
 preconditioner every step (modes mixed, single, mixed-half, single-prec):
   * same final status; restart index within ±1;
@@ -20,9 +25,13 @@ preconditioner every step (modes mixed, single, mixed-half, single-prec):
     the floor F = 1e-14 (fp64 residual) or 1e-6 (mode single, fp32
     residual) — the restarts of an fp32 cycle contract the error by
     amounts that differ with the fp32 rounding, never by more than that;
-  * x: relative 1e-9 (fp64 outer) / 1e-5 (single) of max|x_ref| on the
-    first 16 entries, 1e-7 / 1e-4 on the sum (same restart count only);
-  * final resNorm and errNorm within a factor 10;
+  * x: the rule above with 1e-9 (fp64 outer) / 1e-5 (single) relative
+    and the error term at full weight, (e_ref + e_got) and sqrt(n) (e_ref +
+    e_got) (same restart count only): the fp32 cycle's corrections differ
+    in rounding, so the iterates agree only to the error they carry;
+  * final resNorm within a factor 10 (above the floor); errNorm at most
+    10x the reference's (a more accurate x than the oracle's is not a
+    parity failure: forward error at convergence depends on conditioning);
   * when converged, the final backward error is <= tol.
 Measured margins behind these numbers: tools/parity_margins.py over the
 168 golden records on the fused and operator-surface engines
@@ -63,7 +72,7 @@ def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
         assert np.all(d[c0] <= 1e-8 * s_ref[c0] + 1e-12 * minvb), f"{label}: cycle-0 history {d[c0].max():.3e}"
         assert np.all(d[~c0] <= 1e-5 * s_ref[~c0] + 1e-10 * minvb), f"{label}: history {d[~c0].max():.3e}"
         assert np.all(np.abs(be_got - be_ref) <= 1e-5 * be_ref + 1e-15), f"{label}: backward errors"
-        x_rtol, xs_rtol, norm_factor = 1e-12, 1e-12, (1.2, 2.0)
+        x_rtol, e_w, norm_factor = 1e-12, 0.5, (1.2, 2.0)
     else:
         assert abs(got.restarts - ref["restarts"]) <= 1, f"{label}: restarts {got.restarts} vs {ref['restarts']}"
         k = min(rlen, len(s_ref), len(s_got))
@@ -76,20 +85,30 @@ def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
                 f"{label}: cycle {c} backward error {be_got[c]:.3e} vs {be_ref[c]:.3e}"
         if got.status == "converged":
             assert be_got[-1] <= tol, f"{label}: final backward error {be_got[-1]:.3e} > {tol}"
-        x_rtol, xs_rtol = (1e-5, 1e-4) if mode == "single" else (1e-9, 1e-7)
+        x_rtol, e_w = (1e-5 if mode == "single" else 1e-9), 1.0
         norm_factor = (10.0, 10.0)
     same_cycles = got.restarts == ref["restarts"]
+    e_ref, e_got = float(ref.get("err_norm") or 0.0), float(getattr(got, "err_norm", 0.0) or 0.0)
     if x_head_ref is not None and same_cycles and xscale > 0:
         dx = np.max(np.abs(_arr(got.x[:len(x_head_ref)]) - x_head_ref))
-        assert dx <= x_rtol * xscale, f"{label}: x head differs by {dx:.3e} (scale {xscale:.3e})"
+        bound = x_rtol * xscale + e_w * (e_ref + e_got)
+        assert dx <= bound, f"{label}: x head differs by {dx:.3e} (bound {bound:.3e}, scale {xscale:.3e})"
         xs_ref = float(ref["x_sum"])
-        assert abs(float(np.sum(got.x)) - xs_ref) <= xs_rtol * max(abs(xs_ref), xscale), f"{label}: x sum"
+        ds = abs(float(np.sum(got.x)) - xs_ref)
+        bound = x_rtol * max(abs(xs_ref), xscale) + e_w * np.sqrt(len(got.x)) * (e_ref + e_got)
+        assert ds <= bound, f"{label}: x sum differs by {ds:.3e} (bound {bound:.3e})"
     if "res_norm" in ref and same_cycles and hasattr(got, "res_norm"):
-        assert _ratio_ok(got.res_norm, ref["res_norm"], norm_factor[0]), \
+        norm_last = float(_arr(ref["cyc_normalization"])[-1])
+        rf = 64 * np.finfo(np.float64).eps * norm_last
+        assert _ratio_ok(max(got.res_norm, rf), max(ref["res_norm"], rf), norm_factor[0]), \
             f"{label}: resNorm {got.res_norm:.3e} vs {ref['res_norm']:.3e}"
-        if ref.get("err_norm"):
-            assert _ratio_ok(got.err_norm, ref["err_norm"], norm_factor[1]), \
-                f"{label}: errNorm {got.err_norm:.3e} vs {ref['err_norm']:.3e}"
+        if e_ref:
+            ef = 64 * np.finfo(np.float64).eps * xscale
+            if fp64:
+                assert _ratio_ok(max(e_got, ef), max(e_ref, ef), norm_factor[1]), \
+                    f"{label}: errNorm {e_got:.3e} vs {e_ref:.3e}"
+            else:
+                assert e_got <= norm_factor[1] * max(e_ref, ef), f"{label}: errNorm {e_got:.3e} vs {e_ref:.3e}"
 
 
 def as_ref(result) -> dict:

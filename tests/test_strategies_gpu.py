@@ -10,8 +10,9 @@
 
 Both engines: the operator surface runs the reference driver with one host
 read per step; the fused engine runs the same phase kernels step by step
-(one report read per step) and, for LostOrthogonality, the reference's
-V^T v_{k+1} / S update on the same surface operators over its own basis."""
+(one report read per step) and, for LostOrthogonality, stores v_{k+1} after
+each step and runs the reference's V^T v / S-column update (gemv^T, copy,
+gemv, dot) over its own basis (fused_gmres.cpp orth_loss_step)."""
 import numpy as np
 import pytest
 
@@ -20,7 +21,12 @@ from tests.parity import as_ref, compare
 
 pytestmark = pytest.mark.gpu
 
-STRATEGIES = {"relprecres": dict(rtol=1e-3), "repeat": dict(rtol=1e-3, repeat_iter=True),
+# restart improvements at which each strategy fires on this problem (the
+# oracle: RelPrecRes cycles 4, 36, 18, ...; RepeatIteration 4 every cycle;
+# LostOrthogonality never in cycle 0 -- the column after the newest basis
+# vector is still zero there -- and at step 1 of every later cycle, where
+# that column holds an earlier cycle's vector)
+STRATEGIES = {"relprecres": dict(rtol=0.1), "repeat": dict(rtol=0.1, repeat_iter=True),
               "orthloss": dict(rtol=1e-2, orthloss=True)}
 
 
