@@ -86,6 +86,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_host_csr_free.argtypes = [C.POINTER(HostCsr)]
     lib.mpg_host_csr_free.restype = None
     lib.mpg_engine_create.argtypes = [C.POINTER(SolveArgs), C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
+    lib.mpg_cycle_program_counts.argtypes = [C.POINTER(_I64)] * 3
     lib.mpg_engine_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     lib.mpg_engine_sync.argtypes = [C.c_void_p]
     lib.mpg_engine_total_iters.argtypes = [C.c_void_p]
@@ -387,6 +388,14 @@ def solve(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, **opts) ->
     """Restarted GMRES(m) on the MI355X (mpg_solve). Options as make_args."""
     args, keep = make_args(A, b, x_true, **opts)
     return run_solve(host_lib().mpg_solve, args, A.nrows)
+
+
+def cycle_program_counts() -> dict:
+    """Operator-surface cycle programs so far in this process
+    (mpg_cycle_program_counts): recorded, replayed, voided."""
+    v = [_I64() for _ in range(3)]
+    host_lib().mpg_cycle_program_counts(*[C.byref(x) for x in v])
+    return {"recorded": v[0].value, "replayed": v[1].value, "voided": v[2].value}
 
 
 def row_slice(A: Csr, r0: int, r1: int) -> Csr:

@@ -18,6 +18,7 @@
 #include "csr_tile.hpp"
 #include "sell_tile.hpp"
 #include "handoff.hpp"
+#include "panel.hpp"
 #include "internal.hpp"
 #include "mpgmres/arnoldi.h"
 
@@ -66,54 +67,6 @@ __device__ __forceinline__ void for_rows(const int32_t* __restrict__ blocks, int
     for (int b = rb0; b < rb1; ++b)
         csr_row_block<NT>(blocks[b], blocks[b + 1], bnnz[b], bnnz[b + 1], rowptr, col, val, nnz, xval, pre, epi, prod,
                           scratch);
-}
-
-// One transpose round on the first 2H accumulators: lanes with the MASK bit
-// set keep the upper half, the others the lower half; recursion keeps every
-// index a compile-time constant (a runtime index sends acc to scratch).
-template <int H, int MASK, int N>
-__device__ __forceinline__ void butterfly_round(double (&acc)[N], int lane) {
-    if constexpr (H >= 1) {
-        const bool upper = (lane & MASK) != 0;
-#pragma unroll
-        for (int i = 0; i < H; ++i) {
-            const double keep = upper ? acc[i + H] : acc[i];
-            const double send = upper ? acc[i] : acc[i + H];
-            acc[i] = keep + __shfl_xor(send, MASK, kWave);
-        }
-        butterfly_round<H / 2, MASK / 2>(acc, lane);
-    }
-}
-
-// Block-reduce NCOL fp64 accumulators and store them as partial[c*G + blk]
-// (write-through when WT: the last-arriver combine reads them).
-//
-// Wave stage = transpose (butterfly) reduction: in round r every lane trades
-// half of its remaining columns with the lane 32>>r away and keeps the sum
-// of the other half, so after log2(NCOL) rounds lane l holds one column
-// (l >> (6 - log2 NCOL)) summed over 2^rounds lanes; plain xor shuffles
-// finish the remaining lanes. 32 columns cost 32 shuffles instead of the
-// 192 of one 6-level reduction per column. Fixed order: deterministic.
-template <int NCOL, int BS = kBlock, bool WT = false>
-__device__ __forceinline__ void store_partials(double (&acc)[NCOL], int ncols, double* __restrict__ partial) {
-    static_assert((NCOL & (NCOL - 1)) == 0 && NCOL <= 32, "NCOL: power of two <= 32");
-    __shared__ double red[BS / kWave][NCOL];
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    constexpr int rounds = NCOL == 1 ? 0 : NCOL == 2 ? 1 : NCOL == 4 ? 2 : NCOL == 8 ? 3 : NCOL == 16 ? 4 : 5;
-    butterfly_round<NCOL / 2, 32>(acc, lane);
-    double v = acc[0];
-#pragma unroll
-    for (int mask = 32 >> rounds; mask >= 1; mask >>= 1) v += __shfl_xor(v, mask, kWave);
-    constexpr int shift = 6 - rounds;
-    if ((lane & ((1 << shift) - 1)) == 0) red[wid][lane >> shift] = v;
-    __syncthreads();
-    for (int c = threadIdx.x; c < ncols; c += BS) {
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < BS / kWave; ++w) s += red[w][c];
-        if (WT) store_wt(partial + (size_t)c * gridDim.x + blockIdx.x, s);
-        else partial[(size_t)c * gridDim.x + blockIdx.x] = s;
-    }
 }
 
 // Combine in the last arriver: sums[c] = sum over g of partial[c*G + g] for
@@ -604,29 +557,6 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
     }
 }
 
-// 4 consecutive entries (i a multiple of 4, 16-B aligned for fp32) widened to fp64
-template <class T> struct Row4;
-template <> struct Row4<float> {
-    static __device__ __forceinline__ void load(const float* p, double (&o)[4]) {
-        const float4 v = *reinterpret_cast<const float4*>(p);
-        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-    }
-    static __device__ __forceinline__ void store(float* p, const float (&o)[4]) {
-        *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
-    }
-};
-template <> struct Row4<double> {
-    static __device__ __forceinline__ void load(const double* p, double (&o)[4]) {
-        const double2 a = *reinterpret_cast<const double2*>(p);
-        const double2 b = *reinterpret_cast<const double2*>(p + 2);
-        o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
-    }
-    static __device__ __forceinline__ void store(double* p, const double (&o)[4]) {
-        *reinterpret_cast<double2*>(p) = make_double2(o[0], o[1]);
-        *reinterpret_cast<double2*>(p + 2) = make_double2(o[2], o[3]);
-    }
-};
-
 // Tall-skinny panel reduction: partial <v_j, w> for j in [c0, c0 + nc),
 // nc <= kNC, over all local rows. Each lane owns 4 consecutive rows per
 // iteration (16-B loads of every column: V's leading dimension is padded to
@@ -677,31 +607,6 @@ __global__ __launch_bounds__(BS) void k_panel_dots(int n, const T* __restrict__ 
 // count the compiler guarded each column's load with its own branch and
 // waited for it before the next (one memory latency per column: t(k) =
 // 8.6 + 0.50 k us for the dots on BAND-10M, tools/per_step.py).
-template <int N> struct Pow2Ceil {
-    static constexpr int v = N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : N <= 16 ? 16 : 32;
-};
-// columns per load batch: 32 VGPRs of raw column data per batch
-template <class T> constexpr int kColBatch = sizeof(T) == 4 ? 8 : 4;
-
-// 4 consecutive entries kept in their storage type until used (a batch of
-// raw loads costs half the registers of widened fp32 values)
-template <class T> struct Raw4;
-template <> struct Raw4<float> {
-    float4 v;
-    __device__ __forceinline__ void load(const float* p) { v = *reinterpret_cast<const float4*>(p); }
-    __device__ __forceinline__ double operator[](int r) const {
-        return (double)(r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w);
-    }
-};
-template <> struct Raw4<double> {
-    double2 a, b;
-    __device__ __forceinline__ void load(const double* p) {
-        a = *reinterpret_cast<const double2*>(p);
-        b = *reinterpret_cast<const double2*>(p + 2);
-    }
-    __device__ __forceinline__ double operator[](int r) const { return r == 0 ? a.x : r == 1 ? a.y : r == 2 ? b.x : b.y; }
-};
-
 template <class T, int BS, int NC>
 __global__ __launch_bounds__(BS) void k_dots_nc(int n, const T* __restrict__ V, int64_t ld,
                                                 const T* __restrict__ w, double* __restrict__ partial) {

@@ -7,7 +7,16 @@
 // registers, reduces each across its 4 waves with wave64 shuffles, and
 // writes per-workgroup partials; stage 2 sums the partials of each column in
 // a fixed order. gemv (no transpose) is row-per-lane with fp64 accumulation.
+//
+// Panels whose columns start on 16-B granules (A, lda and the row-indexed
+// vector aligned: the padded Krylov basis of MultiVect always is) take the
+// quad forms: 1024-thread workgroups, one per CU, each lane 4 consecutive
+// rows with 16-B loads of every column issued in compile-time batches (the
+// fused cycle's panel kernels, arnoldi.hip k_dots_nc / k_cgs_update_nc).
 #include "internal.hpp"
+#include "panel.hpp"
+
+#include <algorithm>
 
 using namespace mpg;
 
@@ -115,6 +124,92 @@ __global__ __launch_bounds__(kBlock) void k_gemv_n_nc(int64_t rows, T alpha, con
     }
 }
 
+constexpr int kQuadBlock = 1024;
+constexpr int kQuadGroups = 256;
+
+// partial <A(:,c), x> per workgroup, 4 rows per lane (16-B loads)
+template <class T, int NC>
+__global__ __launch_bounds__(kQuadBlock) void k_gemv_t_quad(int64_t rows, const T* __restrict__ A, int64_t lda,
+                                                            const T* __restrict__ x, double* __restrict__ partial) {
+    constexpr int NP = Pow2Ceil<NC>::v;
+    constexpr int B = kColBatch<T>;
+    double acc[NP];
+#pragma unroll
+    for (int c = 0; c < NP; ++c) acc[c] = 0.0;
+    const int64_t n4 = rows & ~int64_t(3);
+    const int64_t step = 4 * (int64_t)gridDim.x * kQuadBlock;
+    for (int64_t i = 4 * ((int64_t)blockIdx.x * kQuadBlock + threadIdx.x); i < n4; i += step) {
+        double xv[4];
+        Row4<T>::load(x + i, xv);
+#pragma unroll
+        for (int c0 = 0; c0 < NC; c0 += B) {
+            Raw4<T> v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) v[u].load(A + (int64_t)(c0 + u) * lda + i);
+            __builtin_amdgcn_sched_barrier(0);  // the batch's loads back to back
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) acc[c0 + u] += v[u][0] * xv[0] + v[u][1] * xv[1] + v[u][2] * xv[2] + v[u][3] * xv[3];
+        }
+    }
+    for (int64_t i = n4 + (int64_t)blockIdx.x * kQuadBlock + threadIdx.x; i < rows; i += (int64_t)gridDim.x * kQuadBlock) {
+        const double xi = (double)x[i];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c] += (double)A[(int64_t)c * lda + i] * xi;
+    }
+    store_partials<NP, kQuadBlock>(acc, NC, partial);
+}
+
+// y = alpha*T(A x) + beta*y, 4 rows per lane, fp64 sums in column order
+template <class T, int NC>
+__global__ __launch_bounds__(kQuadBlock) void k_gemv_n_quad(int64_t rows, T alpha, const T* __restrict__ A,
+                                                            int64_t lda, const T* __restrict__ x, T beta,
+                                                            T* __restrict__ y) {
+    constexpr int B = kColBatch<T>;
+    __shared__ double xs[NC];
+    if (threadIdx.x < NC) xs[threadIdx.x] = (double)x[threadIdx.x];
+    __syncthreads();
+    const int64_t n4 = rows & ~int64_t(3);
+    const int64_t step = 4 * (int64_t)gridDim.x * kQuadBlock;
+    for (int64_t i = 4 * ((int64_t)blockIdx.x * kQuadBlock + threadIdx.x); i < n4; i += step) {
+        Raw4<T> yr;
+        if (beta != T(0)) yr.load(y + i);
+        double t[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c0 = 0; c0 < NC; c0 += B) {
+            Raw4<T> v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) v[u].load(A + (int64_t)(c0 + u) * lda + i);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (c0 + u < NC) {
+                    const double xu = xs[c0 + u];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) t[r] += v[u][r] * xu;
+                }
+        }
+        T out[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[r] = beta == T(0) ? alpha * (T)t[r] : alpha * (T)t[r] + beta * (T)yr[r];
+        Row4<T>::store(y + i, out);
+    }
+    for (int64_t i = n4 + (int64_t)blockIdx.x * kQuadBlock + threadIdx.x; i < rows; i += (int64_t)gridDim.x * kQuadBlock) {
+        double t = 0.0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) t += (double)A[(int64_t)c * lda + i] * xs[c];
+        const T tt = (T)t;
+        y[i] = beta == T(0) ? alpha * tt : alpha * tt + beta * y[i];
+    }
+}
+
+template <class T>
+bool quad_aligned(const T* A, int64_t lda, const T* v) {
+    return ((uintptr_t)A % 16 == 0) && ((uintptr_t)v % 16 == 0) && ((lda * (int64_t)sizeof(T)) % 16 == 0);
+}
+
 // f(integral_constant<int, nc>) for 1 <= nc <= N
 template <int N, class F>
 int with_cols(int nc, F&& f) {
@@ -158,7 +253,15 @@ int gemv_impl(mpg_ctx* ctx, int trans, int64_t rows, int64_t cols, T alpha, cons
     if (!ctx || rows < 0 || cols < 0 || (cols > 0 && lda < (rows > 0 ? rows : 1))) return MPG_ERR_ARG;
     if (!trans) {
         if (rows == 0) return MPG_OK;
-        if (cols >= 1 && cols <= kGemvMaxCols) {
+        if (cols >= 1 && cols <= kGemvMaxCols && quad_aligned(A, lda, y)) {
+            const int g = (int)std::min<int64_t>(kQuadGroups, (rows + 4 * kQuadBlock - 1) / (4 * kQuadBlock));
+            const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto nc) {
+                k_gemv_n_quad<T, decltype(nc)::value><<<g, kQuadBlock, 0, ctx->stream>>>(rows, alpha, A, lda, x,
+                                                                                        beta, y);
+                return (int)MPG_OK;
+            });
+            if (st) return st;
+        } else if (cols >= 1 && cols <= kGemvMaxCols) {
             const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto nc) {
                 k_gemv_n_nc<T, decltype(nc)::value><<<grid_for(rows, 1), kBlock, 0, ctx->stream>>>(
                     rows, alpha, A, lda, x, beta, y);
@@ -172,12 +275,18 @@ int gemv_impl(mpg_ctx* ctx, int trans, int64_t rows, int64_t cols, T alpha, cons
         return MPG_OK;
     }
     if (cols == 0) return MPG_OK;
-    int g = grid_for(rows, 4, kMaxRedBlocks);
+    const bool quad = quad_aligned(A, lda, x);
+    int g = quad ? (int)std::max<int64_t>(1, std::min<int64_t>(kQuadGroups, (rows + 4 * kQuadBlock - 1) / (4 * kQuadBlock)))
+                 : grid_for(rows, 4, kMaxRedBlocks);
     for (int64_t c0 = 0; c0 < cols; c0 += kGemvMaxCols) {
         int nc = (int)((cols - c0) < kGemvMaxCols ? (cols - c0) : kGemvMaxCols);
         const int st = with_cols<kGemvMaxCols>(nc, [&](auto ncc) {
-            k_gemv_t_nc<T, decltype(ncc)::value><<<g, kBlock, 0, ctx->stream>>>(rows, A + c0 * lda, lda, x,
-                                                                               ctx->red_ws);
+            if (quad)
+                k_gemv_t_quad<T, decltype(ncc)::value><<<g, kQuadBlock, 0, ctx->stream>>>(rows, A + c0 * lda, lda, x,
+                                                                                        ctx->red_ws);
+            else
+                k_gemv_t_nc<T, decltype(ncc)::value><<<g, kBlock, 0, ctx->stream>>>(rows, A + c0 * lda, lda, x,
+                                                                                   ctx->red_ws);
             return (int)MPG_OK;
         });
         if (st) return st;

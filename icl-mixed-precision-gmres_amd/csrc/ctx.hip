@@ -112,6 +112,64 @@ int mpg_memcpy_d2h(mpg_ctx_t ctx, void* dst_host, const void* src_dev, size_t by
     return MPG_OK;
 }
 
+struct mpg_graph {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+};
+
+int mpg_ctx_record_begin(mpg_ctx_t ctx) {
+    if (!ctx) return MPG_ERR_ARG;
+    MPG_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    return MPG_OK;
+}
+
+int mpg_ctx_record_end(mpg_ctx_t ctx, mpg_graph_t* out) {
+    if (!ctx || !out) return MPG_ERR_ARG;
+    *out = nullptr;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+    (void)hipGetLastError();  // a void recording leaves its error sticky
+    if (e != hipSuccess || !g) {
+        if (g) (void)hipGraphDestroy(g);
+        return mpg::set_hip_error(ctx, e != hipSuccess ? e : hipErrorStreamCaptureInvalidated, "hipStreamEndCapture");
+    }
+    mpg_graph* p = new (std::nothrow) mpg_graph();
+    if (!p) {
+        (void)hipGraphDestroy(g);
+        return MPG_ERR_ALLOC;
+    }
+    p->graph = g;
+    const hipError_t ei = hipGraphInstantiate(&p->exec, g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+        (void)hipGraphDestroy(g);
+        delete p;
+        return mpg::set_hip_error(ctx, ei, "hipGraphInstantiate");
+    }
+    *out = p;
+    return MPG_OK;
+}
+
+int mpg_ctx_recording(mpg_ctx_t ctx) {
+    if (!ctx) return 0;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(ctx->stream, &st) != hipSuccess) return 0;
+    return st == hipStreamCaptureStatusActive ? 1 : 0;
+}
+
+int mpg_graph_launch(mpg_ctx_t ctx, mpg_graph_t g) {
+    if (!ctx || !g || !g->exec) return MPG_ERR_ARG;
+    MPG_HIP(ctx, hipGraphLaunch(g->exec, ctx->stream));
+    return MPG_OK;
+}
+
+int mpg_graph_destroy(mpg_graph_t g) {
+    if (!g) return MPG_OK;
+    if (g->exec) (void)hipGraphExecDestroy(g->exec);
+    if (g->graph) (void)hipGraphDestroy(g->graph);
+    delete g;
+    return MPG_OK;
+}
+
 int mpg_memcpy_d2d(mpg_ctx_t ctx, void* dst_dev, const void* src_dev, size_t bytes) {
     if (!ctx) return MPG_ERR_ARG;
     if (bytes == 0) return MPG_OK;

@@ -3,7 +3,8 @@
 // Behaviour follows the reference Orthogonalization.hpp:
 //   GS::first_vector      :36-45  v0 = w * (1/beta)  (zero fill when beta == 0)
 //   GS::add_vector        :51-60  orthogonalize; h(k+1,k) = ||w|| (device);
-//                                 host read of h(k+1,k); v_{k+1} = w * (1/h)
+//                                 v_{k+1} = w * (1/h), the reciprocal formed on
+//                                 the device (the reference reads h to the host)
 //   GS::update_x          :62-73  x += V y  /  x_hi += hi(V y)
 //   CGS_Kernel            :76-89  h = V^T w ; w -= V h
 //   MGS_Kernel            :91-107 per column: h_j = <w, v_j> ; w -= h_j v_j
@@ -58,9 +59,10 @@ public:
         kernel_.orthogonalize(v, k, w, h);
         Scalar<Type, Device> h_next = h(k + 1, k);
         nrm2(w, h_next);
-        const Type h_final = h_next.access();
-        const Type inv = Type(1) / h_final;
-        scal(inv, w, Vect<Type, Device>(v, mpg::ALL, k + 1));
+        // v_{k+1} = w * (1/h): the reference reads h to the host and forms
+        // the reciprocal there (:56-59); scal_recip forms the same Type
+        // reciprocal on the device, so the step has no host read.
+        scal_recip(h_next, w, Vect<Type, Device>(v, mpg::ALL, k + 1));
     }
 
     // x += V(:, 0:k) y, all in Type

@@ -197,7 +197,7 @@ extern "C" int mpg_condest(const mpg_condest_args* a, mpg_condest_result* r) {
             mpg::check(mpg_ctx_sync(ctx), "upload", ctx);
             const auto t0 = std::chrono::steady_clock::now();
             mpg::condest<Hip>(A, a->rand_seed, a->max_iters, a->verbose != 0, r);
-            mpg::check(mpg_ctx_sync(ctx), "final sync", ctx);
+            Hip::fence();  // issues any queued scalar operators first
             r->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         }
         r->status = 0;

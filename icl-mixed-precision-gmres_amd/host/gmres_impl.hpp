@@ -76,6 +76,7 @@ void gmres_baseline(Convergence<Type, Device>& convergence, SparseMatrix<Type, D
     Vect<PrecType, Device> w_temp(std::is_same<PrecType, Type>::value ? 0 : n);
     const bool defer = !convergence.needs_arnoldi_residual();
     mpg::ArnoldiResidualLog<Type, Device> rlog(m, defer);
+    mpg::CycleProgram<Device> cycle;
 
     convergence.setup(orth);
 
@@ -110,28 +111,35 @@ void gmres_baseline(Convergence<Type, Device>& convergence, SparseMatrix<Type, D
         mpg::reset_rhs(s, beta);
 
         size_t k = 0;
-        for (bool more = true; more; ++k) {
+        if (defer) {
+            // base strategy: no decision inside the cycle, so its m steps are
+            // device-only and run as one cycle program (recorded once on Hip)
+            cycle.run([&] {
+                for (size_t j = 0; j < m; ++j) {
+                    spmv(1.0, A, orth.previous_krylov_vector(j), 0.0, w);
+                    mpg::typesafe_apply(M, w, w_temp);
+                    orth.add_vector(j, w, h);
+                    mpg::givens_step(j, h, cs, sn, s);
+                    copy(s(j + 1), rlog.buf(j));
+                }
+            });
+            Device::fence();
+            std::vector<Type> res(m);
+            Device::to_host(res.data(), rlog.buf.data(), m * sizeof(Type));
+            for (size_t j = 0; j < m; ++j) {
+                const iteration_action a = convergence.check(j + 1, std::fabs(res[j]), Minvb_norm);
+                if (a == iteration_aborted) {
+                    mpg::out() << "Aborting after " << convergence.total_iterations() << " iterations" << std::endl;
+                    return;
+                }
+            }
+            k = m;
+        }
+        for (bool more = !defer; more; ++k) {
             spmv(1.0, A, orth.previous_krylov_vector(k), 0.0, w);
             mpg::typesafe_apply(M, w, w_temp);
             orth.add_vector(k, w, h);
             mpg::givens_step(k, h, cs, sn, s);
-
-            if (defer) {
-                copy(s(k + 1), rlog.buf(k));
-                if (k + 1 < m) continue;  // base strategy: only counts, restarts at m
-                Device::fence();
-                std::vector<Type> res(m);
-                Device::to_host(res.data(), rlog.buf.data(), m * sizeof(Type));
-                for (size_t j = 0; j < m; ++j) {
-                    const iteration_action a = convergence.check(j + 1, std::fabs(res[j]), Minvb_norm);
-                    if (a == iteration_aborted) {
-                        mpg::out() << "Aborting after " << convergence.total_iterations() << " iterations" << std::endl;
-                        return;
-                    }
-                }
-                more = false;
-                continue;
-            }
 
             Device::fence();
             const Type arnoldi_residual = std::fabs(s.access(k + 1));
@@ -170,6 +178,7 @@ void gmres_singleUpdate(Convergence<float, Device>& convergence, SparseMatrix<do
     Vect<double, Device> r_accum(n);  // fp64 residual; also the widening temp of the update
     const bool defer = !convergence.needs_arnoldi_residual();
     mpg::ArnoldiResidualLog<float, Device> rlog(m, defer);
+    mpg::CycleProgram<Device> cycle;
 
     convergence.setup(orth);
 
@@ -205,29 +214,36 @@ void gmres_singleUpdate(Convergence<float, Device>& convergence, SparseMatrix<do
         mpg::reset_rhs(s, beta);
 
         size_t k = 0;
-        for (bool more = true; more; ++k) {
+        if (defer) {
+            // base strategy: no decision inside the cycle, so its m steps are
+            // device-only and run as one cycle program (recorded once on Hip)
+            cycle.run([&] {
+                for (size_t j = 0; j < m; ++j) {
+                    spmv(1.0, A_single, orth.previous_krylov_vector(j), 0.0, w);
+                    M->apply(w);
+                    orth.add_vector(j, w, h);
+                    mpg::givens_step(j, h, cs, sn, s);
+                    copy(s(j + 1), rlog.buf(j));
+                }
+            });
+            Device::fence();
+            std::vector<float> res(m);
+            Device::to_host(res.data(), rlog.buf.data(), m * sizeof(float));
+            for (size_t j = 0; j < m; ++j) {
+                const iteration_action a = convergence.check(j + 1, std::fabs(double(res[j])), Minvb_norm);
+                if (a == iteration_aborted) {
+                    mpg::out() << "Aborting after " << convergence.total_iterations() << " iterations" << std::endl;
+                    return;
+                }
+            }
+            k = m;
+        }
+        for (bool more = !defer; more; ++k) {
             spmv(1.0, A_single, orth.previous_krylov_vector(k), 0.0, w);
             M->apply(w);
             orth.add_vector(k, w, h);
             // mixed driver rotates h(0:k, k) — same k entries touched (gmres.cpp:219-220)
             mpg::givens_step(k, h, cs, sn, s);
-
-            if (defer) {
-                copy(s(k + 1), rlog.buf(k));
-                if (k + 1 < m) continue;
-                Device::fence();
-                std::vector<float> res(m);
-                Device::to_host(res.data(), rlog.buf.data(), m * sizeof(float));
-                for (size_t j = 0; j < m; ++j) {
-                    const iteration_action a = convergence.check(j + 1, std::fabs(double(res[j])), Minvb_norm);
-                    if (a == iteration_aborted) {
-                        mpg::out() << "Aborting after " << convergence.total_iterations() << " iterations" << std::endl;
-                        return;
-                    }
-                }
-                more = false;
-                continue;
-            }
 
             Device::fence();
             const double arnoldi_residual = std::fabs(s.access(k + 1));

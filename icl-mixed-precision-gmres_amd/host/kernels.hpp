@@ -65,6 +65,13 @@ void scal(ScalarType alpha, Scalar<Type, Device> x, Scalar<Type, Device> y) {
 }
 template <class Type, class Device>
 void scal(Scalar<Type, Device> alpha, Scalar<Type, Device> x, Scalar<Type, Device> y);
+// y = (1/alpha) x with the reciprocal formed in Type where alpha lives: the
+// reference's `inv = 1/h.access(); scal(inv, w, v)` (Orthogonalization.hpp:
+// 51-60) without the host read (the same two roundings, so bit-identical).
+// Addition to the reference surface; a backend without a device form can
+// define it as exactly that host read.
+template <class Type, class Device>
+void scal_recip(Scalar<Type, Device> alpha, Vect<Type, Device> x, Vect<Type, Device> y);
 
 // ---- fill (kernels.hpp:88-101) ----
 // backend primitive: x[c*ld + r] = value for r < rows, c < cols

@@ -8,11 +8,13 @@
 // the device (device pointer mode, kernels_cuda.cpp:142-150).
 #include "types_hip.hpp"
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <sstream>
 
 #include "kernels.hpp"
+#include "mpgmres/solve.h"
 
 namespace mpg {
 
@@ -49,13 +51,48 @@ void check_ilu_fault(mpg_ilu_t ilu) {
     throw StatusError(MPG_ERR_BREAKDOWN, os.str());
 }
 
+// A call that must read the device back cannot be part of a recorded cycle
+// program: refuse it before it touches the stream (CycleProgram<Hip> then
+// runs the steps eagerly).
+void no_recording(const char* what) {
+    if (tl_ctx && mpg_ctx_recording(tl_ctx))
+        throw StatusError(MPG_ERR_UNSUPPORTED, std::string("mpgmres: ") + what + " cannot be recorded");
+}
+
+bool CycleProgram<Hip>::enabled() {
+    const char* env = std::getenv("MPG_SURFACE_GRAPH");
+    return !(env && *env == '0');
+}
+
+namespace {
+std::atomic<int64_t> g_cycle_counts[3];
+}
+void CycleProgram<Hip>::count(int which) { g_cycle_counts[which].fetch_add(1, std::memory_order_relaxed); }
+
 // MPG_SURFACE_SELL=0 keeps the operator surface's spmv on CSR
 bool surface_sell_enabled() {
     const char* env = std::getenv("MPG_SURFACE_SELL");
     return !(env && *env == '0');
 }
 
-mpg_ctx_t current_ctx() {
+// ---- scalar-op batching ----
+// Consecutive scalar operators (rotg, rot, rot_vec, scalar copy/scal: the
+// Givens step and the |s(k+1)| record of every Arnoldi step) are queued and
+// issued as one mpg_scalar_program launch. Every other call reaches the
+// device through current_ctx(), which issues the queue first, so the stream
+// order of the calls is unchanged; so does every host read (to_host, fence).
+// MPG_SURFACE_BATCH=0 issues each scalar call on its own.
+namespace {
+thread_local mpg_scalar_op tl_ops[MPG_SCALAR_PROGRAM_MAX];
+thread_local int tl_nops = 0;
+thread_local mpg_ctx_t tl_ops_ctx = nullptr;
+
+bool batch_enabled() {
+    const char* env = std::getenv("MPG_SURFACE_BATCH");
+    return !(env && *env == '0');
+}
+
+mpg_ctx_t ctx_no_flush() {
     if (!tl_ctx) {
         const char* env = std::getenv("MPG_DEVICE");
         int dev = env ? std::atoi(env) : 0;
@@ -64,9 +101,47 @@ mpg_ctx_t current_ctx() {
     }
     return tl_ctx;
 }
+}  // namespace
 
-ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) { tl_ctx = ctx; }
-ScopedContext::~ScopedContext() { tl_ctx = prev_; }
+void flush_scalar_ops() {
+    if (tl_nops == 0) return;
+    const int n = tl_nops;
+    tl_nops = 0;
+    check(mpg_scalar_program(tl_ops_ctx, tl_ops, n), "scalar program", tl_ops_ctx);
+}
+
+void discard_scalar_ops() { tl_nops = 0; }
+
+// true when queued (the caller issues the op itself otherwise)
+bool queue_scalar_op(const mpg_scalar_op& op) {
+    if (!batch_enabled()) return false;
+    mpg_ctx_t c = ctx_no_flush();
+    if (tl_nops && tl_ops_ctx != c) flush_scalar_ops();
+    tl_ops_ctx = c;
+    tl_ops[tl_nops++] = op;
+    if (tl_nops == MPG_SCALAR_PROGRAM_MAX) flush_scalar_ops();
+    return true;
+}
+
+mpg_ctx_t current_ctx() {
+    if (tl_nops) flush_scalar_ops();
+    return ctx_no_flush();
+}
+
+ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) {
+    if (tl_nops) flush_scalar_ops();
+    tl_ctx = ctx;
+}
+ScopedContext::~ScopedContext() {
+    // the queue belongs to this scope's context; a failure here has already
+    // been reported by the call that follows it, or the scope is unwinding
+    if (tl_nops) {
+        const int n = tl_nops;
+        tl_nops = 0;
+        (void)mpg_scalar_program(tl_ops_ctx, tl_ops, n);
+    }
+    tl_ctx = prev_;
+}
 
 void build_transpose(CsrStructure& s) {
     if (s.transposed) return;
@@ -143,9 +218,11 @@ template <> void copy<float, double, Hip>(Vect<float, Hip> x, Vect<double, Hip> 
     check(mpg_copy_f32f64(C, x.n(), x.data(), y.data()), "copy");
 }
 template <> void copy<double, double, Hip>(Scalar<double, Hip> x, Scalar<double, Hip> y) {
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_COPY, 1, 0, 0, 0.0, {x.data(), y.data(), nullptr, nullptr}})) return;
     check(mpg_copy_f64f64(C, 1, x.data(), y.data()), "copy");
 }
 template <> void copy<float, float, Hip>(Scalar<float, Hip> x, Scalar<float, Hip> y) {
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_COPY, 0, 0, 0, 0.0, {x.data(), y.data(), nullptr, nullptr}})) return;
     check(mpg_copy_f32f32(C, 1, x.data(), y.data()), "copy");
 }
 template <> void copy<double, float, Hip>(Scalar<double, Hip> x, Scalar<float, Hip> y) {
@@ -243,16 +320,29 @@ template <> void scal<float, Hip>(Scalar<float, Hip> a, Vect<float, Hip> x, Vect
     check(mpg_scal_copy_dev_f32(C, x.n(), a.data(), x.data(), y.data()), "scal");
 }
 template <> void scal<double, Hip>(double a, Scalar<double, Hip> x, Scalar<double, Hip> y) {
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_SCAL, 1, 0, 0, (double)a, {x.data(), y.data(), nullptr, nullptr}})) return;
     check(mpg_scal_scalar_f64(C, a, x.data(), y.data()), "scal");
 }
 template <> void scal<float, Hip>(float a, Scalar<float, Hip> x, Scalar<float, Hip> y) {
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_SCAL, 0, 0, 0, (double)a, {x.data(), y.data(), nullptr, nullptr}})) return;
     check(mpg_scal_scalar_f32(C, a, x.data(), y.data()), "scal");
 }
 template <> void scal<double, Hip>(Scalar<double, Hip> a, Scalar<double, Hip> x, Scalar<double, Hip> y) {
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_SCAL_DEV, 1, 0, 0, 0.0, {x.data(), y.data(), a.data(), nullptr}})) return;
     check(mpg_scal_scalar_dev_f64(C, a.data(), x.data(), y.data()), "scal");
 }
 template <> void scal<float, Hip>(Scalar<float, Hip> a, Scalar<float, Hip> x, Scalar<float, Hip> y) {
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_SCAL_DEV, 0, 0, 0, 0.0, {x.data(), y.data(), a.data(), nullptr}})) return;
     check(mpg_scal_scalar_dev_f32(C, a.data(), x.data(), y.data()), "scal");
+}
+
+template <> void scal_recip<double, Hip>(Scalar<double, Hip> a, Vect<double, Hip> x, Vect<double, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_scal_recip_copy_dev_f64(C, x.n(), a.data(), x.data(), y.data()), "scal_recip");
+}
+template <> void scal_recip<float, Hip>(Scalar<float, Hip> a, Vect<float, Hip> x, Vect<float, Hip> y) {
+    assert(x.n() == y.n());
+    check(mpg_scal_recip_copy_dev_f32(C, x.n(), a.data(), x.data(), y.data()), "scal_recip");
 }
 
 // ---------------- fill ----------------
@@ -266,24 +356,32 @@ template <> void fill_strided<float, Hip>(float* x, size_t r, size_t c, size_t l
 // ---------------- Givens ----------------
 template <> void rotg<double, Hip>(Scalar<double, Hip> a, Scalar<double, Hip> b, Scalar<double, Hip> c,
                                    Scalar<double, Hip> s) {
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_ROTG, 1, 0, 0, 0.0, {a.data(), b.data(), c.data(), s.data()}})) return;
     check(mpg_rotg_f64(C, a.data(), b.data(), c.data(), s.data()), "rotg");
 }
 template <> void rotg<float, Hip>(Scalar<float, Hip> a, Scalar<float, Hip> b, Scalar<float, Hip> c,
-                                  Scalar<float, Hip> s) {
+                                   Scalar<float, Hip> s) {
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_ROTG, 0, 0, 0, 0.0, {a.data(), b.data(), c.data(), s.data()}})) return;
     check(mpg_rotg_f32(C, a.data(), b.data(), c.data(), s.data()), "rotg");
 }
 template <> void rot<double, Hip>(Scalar<double, Hip> a, Scalar<double, Hip> b, Scalar<double, Hip> c,
                                   Scalar<double, Hip> s) {
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_ROT, 1, 0, 0, 0.0, {a.data(), b.data(), c.data(), s.data()}})) return;
     check(mpg_rot_f64(C, a.data(), b.data(), c.data(), s.data()), "rot");
 }
 template <> void rot<float, Hip>(Scalar<float, Hip> a, Scalar<float, Hip> b, Scalar<float, Hip> c,
-                                 Scalar<float, Hip> s) {
+                                  Scalar<float, Hip> s) {
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_ROT, 0, 0, 0, 0.0, {a.data(), b.data(), c.data(), s.data()}})) return;
     check(mpg_rot_f32(C, a.data(), b.data(), c.data(), s.data()), "rot");
 }
 template <> void rot<double, Hip>(Vect<double, Hip> a, Vect<double, Hip> c, Vect<double, Hip> s) {
+    if (c.n() == 0) return;
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_ROT_VEC, 1, (int32_t)c.n(), 0, 0.0, {a.data(), nullptr, c.data(), s.data()}})) return;
     check(mpg_rot_vec_f64(C, (int)c.n(), a.data(), c.data(), s.data()), "rot");
 }
 template <> void rot<float, Hip>(Vect<float, Hip> a, Vect<float, Hip> c, Vect<float, Hip> s) {
+    if (c.n() == 0) return;
+    if (mpg::queue_scalar_op(mpg_scalar_op{MPG_SOP_ROT_VEC, 0, (int32_t)c.n(), 0, 0.0, {a.data(), nullptr, c.data(), s.data()}})) return;
     check(mpg_rot_vec_f32(C, (int)c.n(), a.data(), c.data(), s.data()), "rot");
 }
 
@@ -361,12 +459,14 @@ ILU<T, Hip> make_ilu(SparseMatrix<double, Hip> A, int type) {
 template <> ILU<double, Hip> ilu0<double, Hip>(SparseMatrix<double, Hip> A) { return make_ilu<double>(A, 0); }
 template <> ILU<float, Hip> ilu0<float, Hip>(SparseMatrix<double, Hip> A) { return make_ilu<float>(A, 1); }
 template <> void ilusv<double, Hip>(ILU<double, Hip> ilu, Vect<double, Hip> x) {
+    mpg::no_recording("ilusv (its fault check reads the device)");
     check(mpg_ilu_solve(C, ilu.handle(), x.data()), "ilusv");
     // a level-scheduled solve can fault (a bounded wait expired): read the
     // sticky fault word before anything consumes x (the serial chain never waits)
     if (mpg_ilu_solve_mode(ilu.handle()) != 3) mpg::check_ilu_fault(ilu.handle());
 }
 template <> void ilusv<float, Hip>(ILU<float, Hip> ilu, Vect<float, Hip> x) {
+    mpg::no_recording("ilusv (its fault check reads the device)");
     check(mpg_ilu_solve(C, ilu.handle(), x.data()), "ilusv");
     // a level-scheduled solve can fault (a bounded wait expired): read the
     // sticky fault word before anything consumes x (the serial chain never waits)
@@ -380,3 +480,10 @@ template <> void ilusv_jacobi<float, Hip>(ILU_Jacobi<float, Hip> ilu, Vect<float
 }
 
 #undef C
+
+extern "C" int mpg_cycle_program_counts(int64_t* recorded, int64_t* replayed, int64_t* voided) {
+    if (recorded) *recorded = mpg::g_cycle_counts[0].load();
+    if (replayed) *replayed = mpg::g_cycle_counts[1].load();
+    if (voided) *voided = mpg::g_cycle_counts[2].load();
+    return MPG_OK;
+}

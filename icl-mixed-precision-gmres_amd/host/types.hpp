@@ -42,6 +42,18 @@ std::shared_ptr<void> device_alloc(size_t bytes) {
     return std::shared_ptr<void>(p, [](void* q) { Device::deallocate(q); });
 }
 
+// The Arnoldi steps of one restart cycle when nothing inside them reads the
+// device (the driver's deferred |s(k+1)| path): a backend may record them once
+// and replay the recording every later cycle. Generic form: run them as given.
+template <class Device>
+class CycleProgram {
+public:
+    template <class F>
+    void run(F&& steps) {
+        steps();
+    }
+};
+
 }  // namespace mpg
 
 template <class Type, class Device> class Vect;

@@ -29,6 +29,12 @@ void check(int status, const char* what, mpg_ctx_t ctx = nullptr);
 // A scheduling fault of the ILU triangular solves (the results of every
 // apply since the last check are invalid): StatusError(MPG_ERR_BREAKDOWN).
 void check_ilu_fault(mpg_ilu_t ilu);
+// throws StatusError(MPG_ERR_UNSUPPORTED) while the current context records
+void no_recording(const char* what);
+// the queue of batched scalar operators (kernels_hip.cpp): issue it now /
+// drop it (a voided recording re-runs its steps, which queue them again)
+void flush_scalar_ops();
+void discard_scalar_ops();
 
 // The calling thread's current HIP context (stream + workspace). Created
 // lazily on the device named by MPG_DEVICE (default 0) unless a
@@ -90,6 +96,72 @@ struct Hip {
     using execution_space = Hip;
     using memory_space = Hip;
 };
+
+namespace mpg {
+
+// Hip cycle program: the first cycle runs eagerly (lazy set-up such as the
+// SELL copy of the Arnoldi matrix happens there), the second is recorded on
+// the context's stream (mpg_ctx_record_begin) and launched, every later one
+// is one graph launch. A step that cannot be recorded (one that synchronises,
+// e.g. the ILU solve's fault check) voids the recording: nothing recorded has
+// run, so the steps run eagerly from then on. MPG_SURFACE_GRAPH=0 disables it.
+template <>
+class CycleProgram<Hip> {
+    mpg_graph_t g_ = nullptr;
+    mpg_ctx_t ctx_ = nullptr;
+    int cycles_ = 0;
+    bool eager_;
+
+    static bool enabled();
+    static void count(int which);  // 0 recorded, 1 replayed, 2 voided
+
+public:
+    CycleProgram() : eager_(!enabled()) {}
+    ~CycleProgram() {
+        if (g_) mpg_graph_destroy(g_);
+    }
+    CycleProgram(const CycleProgram&) = delete;
+    CycleProgram& operator=(const CycleProgram&) = delete;
+
+    bool recorded() const { return g_ != nullptr; }
+
+    template <class F>
+    void run(F&& steps) {
+        if (g_) {
+            check(mpg_graph_launch(ctx_, g_), "cycle program launch", ctx_);
+            count(1);
+            return;
+        }
+        if (eager_ || cycles_++ == 0) {
+            steps();
+            return;
+        }
+        ctx_ = current_ctx();
+        check(mpg_ctx_record_begin(ctx_), "cycle program record", ctx_);
+        bool ok = true;
+        try {
+            steps();
+            flush_scalar_ops();
+        } catch (const StatusError&) {
+            discard_scalar_ops();
+            ok = false;
+        }
+        mpg_graph_t g = nullptr;
+        const int st = mpg_ctx_record_end(ctx_, &g);
+        if (!ok || st != MPG_OK || !g) {
+            if (g) mpg_graph_destroy(g);
+            eager_ = true;
+            count(2);
+            steps();
+            return;
+        }
+        g_ = g;
+        check(mpg_graph_launch(ctx_, g_), "cycle program launch", ctx_);
+        count(0);
+    }
+};
+
+}  // namespace mpg
 
 // CSR on the device: shared int32 structure (row_map, inds, analysed row
 // blocks) plus values of precision Type.

@@ -58,6 +58,25 @@ int mpg_ctx_sync(mpg_ctx_t ctx);
 /* hipStream_t of the context, as an opaque pointer. */
 void* mpg_ctx_stream(mpg_ctx_t ctx);
 int mpg_ctx_device(mpg_ctx_t ctx);
+
+/* ---- cycle programs: a run of asynchronous calls on the context's stream
+ *      recorded once (HIP stream capture) and replayed as one graph launch.
+ *      The operator-surface driver records its Arnoldi steps this way when
+ *      they contain no host read (gmres.cpp:199-243 with the per-step reads
+ *      deferred); the reference re-issues every call (no counterpart). ---- */
+typedef struct mpg_graph* mpg_graph_t;
+/* Start recording: every later call on ctx is recorded, not executed. A call
+ * that must synchronise fails while recording (the recording is then void). */
+int mpg_ctx_record_begin(mpg_ctx_t ctx);
+/* Stop recording; on success *out is an executable program. On any failure
+ * (a call inside was not recordable) *out = NULL, the status is an error and
+ * nothing recorded has run. */
+int mpg_ctx_record_end(mpg_ctx_t ctx, mpg_graph_t* out);
+/* 1 while ctx is recording, else 0 */
+int mpg_ctx_recording(mpg_ctx_t ctx);
+/* Run a recorded program on ctx's stream (asynchronous). */
+int mpg_graph_launch(mpg_ctx_t ctx, mpg_graph_t g);
+int mpg_graph_destroy(mpg_graph_t g);
 /* Zero-initialised device allocation (Kokkos views are zero-filled). */
 int mpg_malloc(mpg_ctx_t ctx, size_t bytes, void** out_dev);
 int mpg_free(mpg_ctx_t ctx, void* ptr_dev);
@@ -141,6 +160,31 @@ int mpg_rot_f32(mpg_ctx_t ctx, float* a, float* b, const float* c, const float* 
 /* apply rotations j=0..k-1 to the column a[0..k] (kernels_mkl.cpp:240-260) */
 int mpg_rot_vec_f64(mpg_ctx_t ctx, int k, double* a, const double* c, const double* s);
 int mpg_rot_vec_f32(mpg_ctx_t ctx, int k, float* a, const float* c, const float* s);
+
+/* ---- scalar programs: a short run of the scalar operators (rotg, rot,
+ *      rot_vec, scalar copy and scal) executed in call order by one lane of
+ *      ONE launch, with the arithmetic of the single-operator kernels above
+ *      (bit-identical). The operator surface batches consecutive scalar calls
+ *      into one program: on its own each is a dependent launch of ~4.6 us on
+ *      gfx950, for a few flops (the Givens step gmres.cpp:217-222 is three). */
+typedef enum {
+    MPG_SOP_ROTG = 0,      /* rotg(p0=a, p1=b, p2=c, p3=s), then b := 0 */
+    MPG_SOP_ROT = 1,       /* rot(p0=a, p1=b, p2=c, p3=s) */
+    MPG_SOP_ROT_VEC = 2,   /* rot_vec(k, p0=a, p2=c, p3=s) */
+    MPG_SOP_COPY = 3,      /* *p1 = *p0 (same precision) */
+    MPG_SOP_SCAL = 4,      /* *p1 = alpha * *p0 */
+    MPG_SOP_SCAL_DEV = 5   /* *p1 = *p2 * *p0 */
+} mpg_scalar_opcode;
+typedef struct {
+    int32_t op;       /* mpg_scalar_opcode */
+    int32_t f64;      /* 1: double operands, 0: float */
+    int32_t k;        /* MPG_SOP_ROT_VEC: number of rotations */
+    int32_t reserved;
+    double alpha;     /* MPG_SOP_SCAL (rounded to the operand precision) */
+    void* p[4];       /* device pointers */
+} mpg_scalar_op;
+#define MPG_SCALAR_PROGRAM_MAX 8
+int mpg_scalar_program(mpg_ctx_t ctx, const mpg_scalar_op* ops, int count);
 /* y[0] = alpha*x[0] (scalar scal, kernels_mkl.cpp:193-211) */
 int mpg_scal_scalar_f64(mpg_ctx_t ctx, double alpha, const double* x, double* y);
 int mpg_scal_scalar_f32(mpg_ctx_t ctx, float alpha, const float* x, float* y);

@@ -120,6 +120,12 @@ int mpg_engine_spmv_layout(mpg_engine_t e, int32_t* format, int32_t* vec_width, 
                            int64_t* stored, int32_t* window);
 int mpg_engine_destroy(mpg_engine_t e);
 
+/* process-wide counts of the operator-surface driver's cycle programs
+ * (CycleProgram<Hip>, types_hip.hpp): cycles recorded into a graph, cycles
+ * replayed from one, and recordings voided by a step that must read the
+ * device (those cycles then run eagerly). Any pointer may be NULL. */
+int mpg_cycle_program_counts(int64_t* recorded, int64_t* replayed, int64_t* voided);
+
 #ifdef __cplusplus
 }
 #endif

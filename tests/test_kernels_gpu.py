@@ -8,6 +8,8 @@ reductions are not (their error grows with n), hence fp32 comparisons are
 made against the fp64 reference with an ulp bound and against the oracle
 with a looser relative bound. Elementwise kernels are bit-exact.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -341,3 +343,56 @@ def test_jacobi_setup(hip, mpg, oracle, t):
         assert np.array_equal(dd.get(), oracle.jacobi(A, dt))
     finally:
         hip.lib.mpg_csr_destroy(csr)
+
+
+class ScalarOp(C.Structure):
+    """mpg_scalar_op (include/mpgmres/capi.h)"""
+    _fields_ = [("op", C.c_int32), ("f64", C.c_int32), ("k", C.c_int32), ("reserved", C.c_int32),
+                ("alpha", C.c_double), ("p", C.c_void_p * 4)]
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
+def test_scalar_program_matches_single_ops(hip, t):
+    """One mpg_scalar_program launch runs the Givens step of an Arnoldi step
+    (rot_vec over k earlier rotations, rotg, rot of s) plus a scalar copy and
+    both scalar scal forms, with the same bits as the single-operator calls."""
+    dt = np.float64 if t == "f64" else np.float32
+    f64 = 1 if t == "f64" else 0
+    k = 7
+    g = rng(11)
+    col0 = g.normal(size=k + 2).astype(dt)
+    th = g.uniform(0, 2 * np.pi, k)
+    c0, s0 = np.cos(th).astype(dt), np.sin(th).astype(dt)
+    sv0 = np.zeros(k + 2, dt)
+    sv0[k] = dt(g.normal())
+    out = {}
+    for how in ("program", "single"):
+        col, c, s, sv = hip.buf(np.append(col0, 0)), hip.buf(np.append(c0, [0, 0])), hip.buf(np.append(s0, [0, 0])), hip.buf(sv0)
+        rec, scal = hip.buf(np.zeros(3, dt)), hip.buf(np.array([dt(0.37)], dt))
+        if how == "program":
+            ops = (ScalarOp * 6)()
+            specs = [(2, k, 0.0, [col.p, None, c.p, s.p]),
+                     (0, 0, 0.0, [col.at(k), col.at(k + 1), c.at(k), s.at(k)]),
+                     (1, 0, 0.0, [sv.at(k), sv.at(k + 1), c.at(k), s.at(k)]),
+                     (3, 0, 0.0, [sv.at(k + 1), rec.at(0), None, None]),
+                     (4, 0, 1.7, [rec.at(0), rec.at(1), None, None]),
+                     (5, 0, 0.0, [rec.at(1), rec.at(2), scal.p, None])]
+            for i, (op, kk, alpha, ps) in enumerate(specs):
+                ops[i].op, ops[i].f64, ops[i].k, ops[i].alpha = op, f64, kk, alpha
+                for j, q in enumerate(ps):
+                    ops[i].p[j] = q.value if q is not None else None
+            hip.check(hip.lib.mpg_scalar_program(hip.ctx, ops, 6), "mpg_scalar_program")
+        else:
+            hip.call(f"mpg_rot_vec_{t}", k, col.p, c.p, s.p)
+            hip.call(f"mpg_rotg_{t}", col.at(k), col.at(k + 1), c.at(k), s.at(k))
+            hip.call(f"mpg_rot_{t}", sv.at(k), sv.at(k + 1), c.at(k), s.at(k))
+            hip.call(f"mpg_copy_{t}{t}", C.c_int64(1), sv.at(k + 1), rec.at(0))
+            alpha = C.c_double(1.7) if t == "f64" else C.c_float(1.7)
+            hip.call(f"mpg_scal_scalar_{t}", alpha, rec.at(0), rec.at(1))
+            hip.call(f"mpg_scal_scalar_dev_{t}", scal.p, rec.at(1), rec.at(2))
+        out[how] = [b.get() for b in (col, c, s, sv, rec)]
+    for a, b in zip(out["program"], out["single"]):
+        assert np.array_equal(a, b)
+    assert out["program"][4][0] != 0
+    with pytest.raises(RuntimeError):
+        hip.check(hip.lib.mpg_scalar_program(hip.ctx, (ScalarOp * 9)(), 9), "too long")

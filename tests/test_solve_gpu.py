@@ -28,9 +28,10 @@ def _case_id(c):
 # (engine, storage, environment): the fused engine on both Arnoldi SpMV
 # storages (CSR row blocks, SELL-64);: MPG_SELL_WINDOW=0 gathers v_k from memory
 # instead of the LDS window; the others are launch-count experiments
-FLAGS = ("MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS", "MPG_SELL_WINDOW", "MPG_SURFACE_SELL", "MPG_FUSE_DOTS")
+FLAGS = ("MPG_SURFACE_GRAPH", "MPG_SURFACE_BATCH", "MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS", "MPG_SELL_WINDOW", "MPG_SURFACE_SELL", "MPG_FUSE_DOTS")
 ON_BY_DEFAULT = ("MPG_SELL_WINDOW", "MPG_SURFACE_SELL")
-ENGINES = {"surface": ("surface", "auto", {}), "surface-csr": ("surface", "auto", {"MPG_SURFACE_SELL": "0"}),
+ENGINES = {"surface": ("surface", "auto", {}), "surface-eager": ("surface", "auto", {"MPG_SURFACE_GRAPH": "0", "MPG_SURFACE_BATCH": "0"}),
+           "surface-csr": ("surface", "auto", {"MPG_SURFACE_SELL": "0"}),
            "fused-csr": ("fused", "csr", {}),
            "fused-sell": ("fused", "sell", {}), "fused-gather": ("fused", "sell", {"MPG_SELL_WINDOW": "0"}),
            "fused-fold": ("fused", "auto", {"MPG_FOLD_GIVENS": "1"}),
@@ -227,3 +228,39 @@ def test_engine_sequence_in_one_process(mpg, oracle):
         for engine in ("surface", "fused"):
             got = mpg.solve(A, b, xt, engine=engine, **opts)
             compare(as_ref(ref), got, "mixed", opts["tol"], 30, f"sequence-{orth}-{engine}")
+
+
+@pytest.mark.parametrize("orth", ["cgs", "mgs", "cgsr"])
+@pytest.mark.parametrize("mode", ["mixed", "baseline", "single"])
+@pytest.mark.parametrize("prec", ["identity", "jacobi", "ilu"])
+def test_surface_cycle_program_matches_eager(mpg, orth, mode, prec, monkeypatch):
+    """The operator-surface driver records its Arnoldi steps once per solve
+    (CycleProgram<Hip>: first cycle eager, second recorded, later replayed)
+    when the strategy makes no decision inside a cycle. Replays must give the
+    same bits as issuing every call on its own (MPG_SURFACE_GRAPH=0 and
+    MPG_SURFACE_BATCH=0: no recording, no scalar-op batching); an ILU apply,
+    which reads its fault word, voids the recording and runs eagerly."""
+    A = mpg.gen_band(100_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(engine="surface", mode=mode, orth=orth, prec=prec, rlen=30, tol=1e-9, max_restarts=6)
+    got = {}
+    for g in ("1", "0"):
+        monkeypatch.setenv("MPG_SURFACE_GRAPH", g)
+        monkeypatch.setenv("MPG_SURFACE_BATCH", g)
+        before = mpg.cycle_program_counts()
+        got[g] = mpg.solve(A, b, xt, **opts)
+        after = mpg.cycle_program_counts()
+        delta = {k: after[k] - before[k] for k in after}
+        if g == "0":
+            assert delta == {"recorded": 0, "replayed": 0, "voided": 0}
+        elif got[g].total_iters // 30 >= 2:
+            if prec == "ilu":
+                assert delta == {"recorded": 0, "replayed": 0, "voided": 1}, delta
+            else:
+                assert delta["recorded"] == 1 and delta["voided"] == 0, delta
+                assert delta["replayed"] == got[g].total_iters // 30 - 2, delta
+    p, e = got["1"], got["0"]
+    assert p.status == e.status and p.total_iters == e.total_iters and p.restarts == e.restarts
+    assert np.array_equal(p.step_res, e.step_res)
+    assert p.res_norm == e.res_norm and p.err_norm == e.err_norm
