@@ -190,7 +190,8 @@ def main():
         import torch.distributed as dist
 
         # MPG_BENCH_SHARED_GPU=1 rehearses the multi-rank path with every rank on
-        # device 0 (torch side on gloo); the default is one GPU per rank over RCCL
+        # device 0 (gloo, engine collectives over the host transport); the
+        # default is one GPU per rank over RCCL
         if os.environ.get("MPG_BENCH_SHARED_GPU") == "1":
             local_rank = 0
             torch.cuda.set_device(0)
@@ -224,9 +225,16 @@ def main():
         for q in range(world):
             if q != rank:
                 plan.set_send(q, gathered[q].get(rank, []))
-        uid = [mpg.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng = mpg.Engine.distributed(A, b, xt[r0:r1], plan, uid[0], world, rank, **opts)
+        if os.environ.get("MPG_BENCH_SHARED_GPU") == "1":
+            # rehearsal on one GPU: the same engine, collectives through host
+            # memory over gloo (RCCL refuses two ranks on one device)
+            from mpgmres_amd.transport import HostTransport
+
+            eng = mpg.Engine.distributed_host(A, b, xt[r0:r1], plan, HostTransport(), world, rank, **opts)
+        else:
+            uid = [mpg.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            eng = mpg.Engine.distributed(A, b, xt[r0:r1], plan, uid[0], world, rank, **opts)
     eng.run(args.warmup)
     eng.sync()
     torch.cuda.synchronize()

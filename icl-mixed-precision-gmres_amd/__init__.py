@@ -87,6 +87,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_host_csr_free.restype = None
     lib.mpg_engine_create.argtypes = [C.POINTER(SolveArgs), C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
     lib.mpg_cycle_program_counts.argtypes = [C.POINTER(_I64)] * 3
+    lib.mpg_engine_report.argtypes = [C.c_void_p, C.POINTER(SolveResult)]
     lib.mpg_engine_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     lib.mpg_engine_sync.argtypes = [C.c_void_p]
     lib.mpg_engine_total_iters.argtypes = [C.c_void_p]
@@ -514,10 +515,15 @@ class Engine:
         if _dist is None:
             st = self._lib.mpg_engine_create(C.byref(self._args), C.byref(self._h), err, 512)
         else:
-            plan, uid, nranks, rank = _dist
+            plan, link, nranks, rank = _dist
             self._plan = plan
-            st = self._lib.mpg_engine_create_dist(C.byref(self._args), plan._h, uid, nranks, rank,
-                                                  C.byref(self._h), err, 512)
+            if isinstance(link, (bytes, bytearray)):
+                st = self._lib.mpg_engine_create_dist(C.byref(self._args), plan._h, link, nranks, rank,
+                                                      C.byref(self._h), err, 512)
+            else:
+                self._transport = link  # keeps the callbacks alive
+                st = self._lib.mpg_engine_create_dist_host(C.byref(self._args), plan._h, C.byref(link.c), nranks,
+                                                           rank, C.byref(self._h), err, 512)
         if st:
             raise RuntimeError(f"mpg_engine_create: {err.value.decode()}")
 
@@ -525,6 +531,21 @@ class Engine:
     def distributed(cls, A_local: Csr, b_local, x_true_local, plan: HaloPlan, uid: bytes, nranks: int, rank: int,
                     **opts):
         return cls(A_local, b_local, x_true_local, _dist=(plan, uid, nranks, rank), **opts)
+
+    @classmethod
+    def distributed_host(cls, A_local: Csr, b_local, x_true_local, plan: HaloPlan, transport, nranks: int,
+                         rank: int, **opts):
+        """One rank of a row-partitioned solve whose collectives go through
+        a host transport (transport.HostTransport over torch.distributed)
+        instead of RCCL: ranks may share a GPU (mpg_engine_create_dist_host)."""
+        return cls(A_local, b_local, x_true_local, _dist=(plan, transport, nranks, rank), **opts)
+
+    def report(self, cycle_cap: int = 4096, step_cap: int = 1 << 17) -> Result:
+        """The solve so far as mpg_solve reports it (mpg_engine_report): this
+        rank's rows of x; collective on a row-partitioned engine."""
+        n = self._args.n
+        lib = self._lib
+        return run_solve(lambda a, r: lib.mpg_engine_report(self._h, r), self._args, n, cycle_cap, step_cap)
 
     def run(self, cycles: int) -> tuple:
         done = C.c_int(0)

@@ -211,6 +211,89 @@ private:
     }
 };
 
+// ---------------------------------------------------------------- host transport
+// Collectives through caller-supplied host callbacks (mpg_host_transport,
+// dist.h): staging copies through host memory around each call. Lets any
+// host transport (e.g. torch.distributed over gloo) drive ranks that share a
+// GPU, which RCCL refuses, so the row-partitioned engine runs as separate
+// processes on one device. Not capturable (host waits).
+class HostComm : public Comm {
+    mpg_host_transport t_;
+    int rank_, size_, n_local_;
+    mpg_ctx_t ctx_;
+    std::vector<int32_t> recv_off_, recv_cnt_, send_cnt_;
+    std::vector<std::unique_ptr<DevMem>> send_idx_, send_dev_;
+    std::vector<std::vector<char>> send_host_, recv_host_;
+    std::vector<double> red_;
+
+    void call(int st, const char* what) {
+        if (st != 0) throw std::runtime_error(std::string("host transport: ") + what + " failed (" + std::to_string(st) + ")");
+    }
+
+public:
+    HostComm(mpg_ctx_t ctx, const mpg_halo& h, const mpg_host_transport& t, int nranks, int rank)
+        : t_(t), rank_(rank), size_(nranks), n_local_(h.n_local), ctx_(ctx), recv_off_(h.recv_off),
+          recv_cnt_(h.recv_cnt) {
+        send_cnt_.assign(nranks, 0);
+        send_idx_.resize(nranks);
+        send_dev_.resize(nranks);
+        send_host_.resize(nranks);
+        recv_host_.resize(nranks);
+        for (int q = 0; q < nranks; ++q) {
+            const auto& rows = h.send_local[q];
+            send_cnt_[q] = (int32_t)rows.size();
+            if (rows.empty()) continue;
+            send_idx_[q] = std::make_unique<DevMem>(ctx, rows.size() * 4);
+            check(mpg_memcpy_h2d(ctx, send_idx_[q]->p, rows.data(), rows.size() * 4), "h2d", ctx);
+            send_dev_[q] = std::make_unique<DevMem>(ctx, rows.size() * 8);
+        }
+    }
+    int size() const override { return size_; }
+    int rank() const override { return rank_; }
+    bool capturable() const override { return false; }
+    void allreduce_sum(double* dev, int count, hipStream_t s) override { reduce(dev, count, s, 0); }
+    void allreduce_max(double* dev, int count, hipStream_t s) override { reduce(dev, count, s, 1); }
+    void halo(void* vec, int eb, hipStream_t s) override {
+        std::vector<void*> send(size_, nullptr), recv(size_, nullptr);
+        std::vector<int64_t> sb(size_, 0), rb(size_, 0);
+        for (int q = 0; q < size_; ++q) {
+            if (send_cnt_[q]) {
+                const int st = eb == 8 ? mpg_gather_b64(ctx_, send_cnt_[q], send_idx_[q]->as<int32_t>(), vec, send_dev_[q]->p)
+                                       : mpg_gather_b32(ctx_, send_cnt_[q], send_idx_[q]->as<int32_t>(), vec, send_dev_[q]->p);
+                check(st, "halo pack", ctx_);
+                sb[q] = (int64_t)send_cnt_[q] * eb;
+                send_host_[q].resize((size_t)sb[q]);
+                send[q] = send_host_[q].data();
+            }
+            if (recv_cnt_[q]) {
+                rb[q] = (int64_t)recv_cnt_[q] * eb;
+                recv_host_[q].resize((size_t)rb[q]);
+                recv[q] = recv_host_[q].data();
+            }
+        }
+        for (int q = 0; q < size_; ++q)
+            if (sb[q]) hck(hipMemcpyAsync(send[q], send_dev_[q]->p, (size_t)sb[q], hipMemcpyDeviceToHost, s), "d2h");
+        hck(hipStreamSynchronize(s), "sync");
+        call(t_.exchange(t_.user, send.data(), sb.data(), recv.data(), rb.data()), "exchange");
+        for (int q = 0; q < size_; ++q)
+            if (rb[q]) {
+                char* dst = static_cast<char*>(vec) + ((size_t)n_local_ + recv_off_[q]) * eb;
+                hck(hipMemcpyAsync(dst, recv[q], (size_t)rb[q], hipMemcpyHostToDevice, s), "h2d");
+            }
+        hck(hipStreamSynchronize(s), "sync");
+    }
+
+private:
+    void reduce(double* dev, int count, hipStream_t s, int op) {
+        red_.resize((size_t)count);
+        hck(hipMemcpyAsync(red_.data(), dev, (size_t)count * 8, hipMemcpyDeviceToHost, s), "d2h");
+        hck(hipStreamSynchronize(s), "sync");
+        call(t_.allreduce(t_.user, red_.data(), count, op), "allreduce");
+        hck(hipMemcpyAsync(dev, red_.data(), (size_t)count * 8, hipMemcpyHostToDevice, s), "h2d");
+        hck(hipStreamSynchronize(s), "sync");
+    }
+};
+
 std::vector<int64_t> nnz_balanced_starts(int n, const int32_t* rowptr, int P) {
     std::vector<int64_t> st((size_t)P + 1, 0);
     const int64_t nnz = rowptr[n];
@@ -340,6 +423,35 @@ int mpg_engine_create_dist(const mpg_solve_args* a, mpg_halo_t plan, const char*
     return MPG_OK;
 }
 
+int mpg_engine_create_dist_host(const mpg_solve_args* a, mpg_halo_t plan, const mpg_host_transport* t,
+                                int32_t nranks, int32_t rank, mpg_engine_t* out, char* err, int errlen) {
+    if (!a || !plan || !t || !t->allreduce || !t->exchange || !out || plan->nranks != nranks || plan->rank != rank ||
+        plan->n_local != a->n)
+        return MPG_ERR_ARG;
+    for (int q = 0; q < nranks; ++q)
+        if (!plan->send_set[q]) {
+            if (err) std::snprintf(err, (size_t)errlen, "halo plan: send list of peer %d not set", q);
+            return MPG_ERR_ARG;
+        }
+    *out = nullptr;
+    auto* e = new mpg_engine();
+    try {
+        set_quiet(!a->verbose || rank != 0);
+        check(mpg_ctx_create(a->device, &e->ctx), "mpg_ctx_create");
+        ScopedContext scope(e->ctx);
+        e->comm = std::make_unique<HostComm>(e->ctx, *plan, *t, nranks, rank);
+        mpg_solve_args local = *a;
+        local.col = plan->col_local.data();
+        e->eng = std::make_unique<FusedEngine>(e->ctx, local, e->comm.get(), mpg_halo_n_ext(plan));
+    } catch (const std::exception& ex) {
+        if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", ex.what());
+        mpg_engine_destroy(e);
+        return MPG_ERR_ARG;
+    }
+    *out = e;
+    return MPG_OK;
+}
+
 int mpg_solve_loopback(const mpg_solve_args* a, int32_t P, mpg_solve_result* r) {
     if (!a || !r || P < 1 || a->n < P) return MPG_ERR_ARG;
     r->status = MPG_RESULT_ERROR;
@@ -396,25 +508,9 @@ int mpg_solve_loopback(const mpg_solve_args* a, int32_t P, mpg_solve_result* r) 
                     mine.x_out = r->x_out ? r->x_out + r0 : nullptr;
                     e.finish_report(&mine);
                     if (q == 0) {
-                        r->status = e.status;
-                        r->restarts = e.restarts;
-                        r->inner_k = e.inner_k;
-                        r->total_iters = (int64_t)e.total_iters();
-                        r->minvb_norm = e.minvb_norm;
+                        fill_history(e, r);
                         r->res_norm = mine.res_norm;
                         r->err_norm = mine.err_norm;
-                        r->setup_seconds = e.setup_seconds;
-                        r->n_cycles = (int64_t)e.cycles.size();
-                        for (size_t c = 0; c < e.cycles.size() && (int64_t)c < r->cycle_cap; ++c) {
-                            if (r->cyc_r_norm) r->cyc_r_norm[c] = e.cycles[c].r_norm;
-                            if (r->cyc_normalization) r->cyc_normalization[c] = e.cycles[c].normalization;
-                            if (r->cyc_beta) r->cyc_beta[c] = e.cycles[c].beta;
-                        }
-                        r->n_steps = (int64_t)e.step_res.size();
-                        for (size_t s = 0; s < e.step_res.size() && (int64_t)s < r->step_cap; ++s) {
-                            if (r->step_res) r->step_res[s] = e.step_res[s];
-                            if (r->step_cycle) r->step_cycle[s] = e.step_cycle[s];
-                        }
                     }
                 }
             } catch (const std::exception& ex) {

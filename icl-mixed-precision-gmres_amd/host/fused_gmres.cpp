@@ -842,22 +842,13 @@ void FusedEngine::timed(int phase, F&& launch) {
 }
 
 // ---------------------------------------------------------------- mpg_solve (fused)
-int solve_fused(const mpg_solve_args& a, mpg_solve_result* r) {
-    mpg_ctx_t ctx = current_ctx();
-    const char* banner = a.mode == MPG_MODE_MIXED || a.mode == MPG_MODE_MIXED_HALF ? "Doing Mixed Precision test"
-                                                                                     : "Doing Baseline test";
-    out() << banner << std::endl;
-    FusedEngine e(ctx, a);
-    auto t1 = clk::now();
-    bool done = false;
-    while (!done) e.run(1 << 20, done);
-    e.sync();
-    const double gmres_s = std::chrono::duration<double>(clk::now() - t1).count();
+void fill_history(const FusedEngine& e, mpg_solve_result* r) {
     r->status = e.status;
     r->restarts = e.restarts;
     r->inner_k = e.inner_k;
     r->total_iters = (int64_t)e.total_iters();
     r->minvb_norm = e.minvb_norm;
+    r->setup_seconds = e.setup_seconds;
     r->n_cycles = (int64_t)e.cycles.size();
     for (size_t c = 0; c < e.cycles.size() && (int64_t)c < r->cycle_cap; ++c) {
         if (r->cyc_r_norm) r->cyc_r_norm[c] = e.cycles[c].r_norm;
@@ -869,7 +860,20 @@ int solve_fused(const mpg_solve_args& a, mpg_solve_result* r) {
         if (r->step_res) r->step_res[s] = e.step_res[s];
         if (r->step_cycle) r->step_cycle[s] = e.step_cycle[s];
     }
-    r->setup_seconds = e.setup_seconds;
+}
+
+int solve_fused(const mpg_solve_args& a, mpg_solve_result* r) {
+    mpg_ctx_t ctx = current_ctx();
+    const char* banner = a.mode == MPG_MODE_MIXED || a.mode == MPG_MODE_MIXED_HALF ? "Doing Mixed Precision test"
+                                                                                     : "Doing Baseline test";
+    out() << banner << std::endl;
+    FusedEngine e(ctx, a);
+    auto t1 = clk::now();
+    bool done = false;
+    while (!done) e.run(1 << 20, done);
+    e.sync();
+    const double gmres_s = std::chrono::duration<double>(clk::now() - t1).count();
+    fill_history(e, r);
     r->gmres_seconds = gmres_s;
     e.finish_report(r);
     out() << "  ilu took " << (float)r->setup_seconds << "s; gmres took " << (float)gmres_s << "s" << std::endl;
@@ -943,6 +947,23 @@ int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, dou
         for (size_t i = 0; i < t.size() && (int)i < cap; ++i) per_launch_ms[i] = t[i];
         return (int)t.size();
     } catch (const std::exception&) {
+        return MPG_ERR_HIP;
+    }
+}
+
+int mpg_engine_report(mpg_engine_t e, mpg_solve_result* r) {
+    if (!e || !e->eng || !r) return MPG_ERR_ARG;
+    try {
+        mpg::ScopedContext scope(e->ctx);
+        e->eng->sync();
+        mpg::fill_history(*e->eng, r);
+        e->eng->finish_report(r);
+        return MPG_OK;
+    } catch (const mpg::StatusError& ex) {
+        std::snprintf(r->message, sizeof r->message, "%s", ex.what());
+        return ex.status;
+    } catch (const std::exception& ex) {
+        std::snprintf(r->message, sizeof r->message, "%s", ex.what());
         return MPG_ERR_HIP;
     }
 }

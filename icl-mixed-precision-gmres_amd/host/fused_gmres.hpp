@@ -114,6 +114,8 @@ private:
 };
 
 int solve_fused(const mpg_solve_args& args, mpg_solve_result* result);
+// status, counts and the per-cycle / per-step history of an engine into r
+void fill_history(const FusedEngine& e, mpg_solve_result* r);
 
 }  // namespace mpg
 

@@ -65,6 +65,26 @@ int mpg_rccl_unique_id(char* id_out, int len);
 int mpg_engine_create_dist(const mpg_solve_args* args, mpg_halo_t plan, const char* rccl_id, int32_t nranks,
                            int32_t rank, mpg_engine_t* out, char* err, int errlen);
 
+/* Collectives over a caller-supplied host transport: ranks in separate
+ * processes that may share one GPU (RCCL refuses that), e.g. driven by
+ * torch.distributed over gloo (icl-mixed-precision-gmres_amd/transport.py).
+ * Every rank calls the callbacks in the same order. Both return 0 on
+ * success. allreduce: in-place sum (op 0) or max (op 1) of `count` doubles,
+ * the same bits on every rank. exchange: for every peer q != rank, send
+ * send_bytes[q] bytes from send[q] and receive recv_bytes[q] bytes into
+ * recv[q] (zero sizes: nothing to move). */
+typedef struct {
+    void* user;
+    int (*allreduce)(void* user, double* buf, int32_t count, int32_t op);
+    int (*exchange)(void* user, void* const* send, const int64_t* send_bytes, void* const* recv,
+                    const int64_t* recv_bytes);
+} mpg_host_transport;
+
+/* mpg_engine_create_dist with the host transport instead of RCCL (the
+ * collectives stage through host memory; the cycle runs eagerly). */
+int mpg_engine_create_dist_host(const mpg_solve_args* args, mpg_halo_t plan, const mpg_host_transport* transport,
+                                int32_t nranks, int32_t rank, mpg_engine_t* out, char* err, int errlen);
+
 /* P ranks as threads on one device, rows split evenly by nnz; the result
  * (history, counts, norms, x gathered) matches mpg_solve's. */
 int mpg_solve_loopback(const mpg_solve_args* args, int32_t nranks, mpg_solve_result* result);

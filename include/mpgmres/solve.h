@@ -102,6 +102,11 @@ int mpg_engine_create(const mpg_solve_args* args, mpg_engine_t* out, char* err, 
 int mpg_engine_run(mpg_engine_t e, int max_cycles, int* done);
 int mpg_engine_sync(mpg_engine_t e);
 int64_t mpg_engine_total_iters(mpg_engine_t e);
+/* The solve so far as mpg_solve reports it: status, counts, the per-cycle
+ * and per-step history, this rank's rows of x (result->x_out) and resNorm /
+ * errNorm with the fp64 matrix (gmres_perf_test.cpp:104-117). Collective on a
+ * row-partitioned engine (the norms are all-reduced). */
+int mpg_engine_report(mpg_engine_t e, mpg_solve_result* result);
 /* device-event timing of one phase kernel replayed `reps` times on the
  * engine's stream, back to back, averaged over the steps k = 0..m-1 of a
  * cycle (which: 0 = Arnoldi SpMV k_step_spmv, 1 = residual prologue,

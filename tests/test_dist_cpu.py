@@ -7,6 +7,12 @@ needed), exchange their needs, then
   * one distributed CGS Arnoldi cycle (partial dots + all-reduce, as the
     fused engine does with RCCL) must reproduce the Hessenberg matrix of the
     serial cycle to fp64 round-off.
+
+The halo exchange and the all-reduces go through the product's host
+transport (mpgmres_amd/transport.py), called through the C function
+pointers exactly as host/dist.cpp's HostComm calls them; the GPU side of the
+same engine over this transport is tests/test_dist_gpu.py's multi-process
+test.
 """
 import os
 import socket
@@ -39,34 +45,38 @@ def _exchange(plan, rank, world):
     return sends
 
 
-def _halo(x_ext, n_loc, r0, plan, sends, rank, world):
-    reqs = []
-    for q in range(world):
-        if q == rank:
-            continue
-        if len(sends[q]):
-            reqs.append(dist.isend(torch.from_numpy(x_ext[sends[q] - r0].copy()), q))
+def _halo(x_ext, n_loc, r0, plan, sends, rank, world, transport):
+    """The halo exchange through the product's host transport
+    (mpgmres_amd/transport.py), called through its C function pointer with
+    the arguments host/dist.cpp's HostComm passes: per-peer send/recv
+    buffers and byte counts."""
+    import ctypes as C
+
+    send_arrs = {q: np.ascontiguousarray(x_ext[sends[q] - r0]) for q in range(world) if q != rank and len(sends[q])}
+    sizes = {q: 8 * len(plan.recv_rows(q)) for q in range(world) if q != rank}
+    recv_arrs = {q: np.zeros(sizes[q] // 8) for q in sizes if sizes[q]}
+    send = (C.c_void_p * world)(*[send_arrs[q].ctypes.data if q in send_arrs else None for q in range(world)])
+    sb = (C.c_int64 * world)(*[send_arrs[q].nbytes if q in send_arrs else 0 for q in range(world)])
+    recv = (C.c_void_p * world)(*[recv_arrs[q].ctypes.data if q in recv_arrs else None for q in range(world)])
+    rb = (C.c_int64 * world)(*[sizes.get(q, 0) for q in range(world)])
+    assert transport.c.exchange(None, send, sb, recv, rb) == 0, transport.error
     off = n_loc
-    bufs = []
     for q in range(world):
         if q == rank:
             continue
-        cnt = len(plan.recv_rows(q))
+        cnt = sizes[q] // 8
         if cnt:
-            buf = torch.empty(cnt, dtype=torch.float64)
-            reqs.append(dist.irecv(buf, q))
-            bufs.append((off, buf))
+            x_ext[off:off + cnt] = recv_arrs[q]
         off += cnt
-    for r in reqs:
-        r.wait()
-    for o, buf in bufs:
-        x_ext[o:o + len(buf)] = buf.numpy()
 
 
-def _allreduce(v):
-    t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64))
-    dist.all_reduce(t)
-    return t.numpy()
+def _allreduce(v, transport):
+    """fp64 sum through the host transport's C callback (rank-order sum)."""
+    import ctypes as C
+
+    buf = np.array(v, dtype=np.float64)
+    assert transport.c.allreduce(None, buf.ctypes.data_as(C.POINTER(C.c_double)), len(buf), 0) == 0, transport.error
+    return buf
 
 
 def _worker(rank, world, port, N, out_q):
@@ -76,6 +86,9 @@ def _worker(rank, world, port, N, out_q):
         from tests.conftest import load_package
 
         mpg = load_package()
+        from mpgmres_amd.transport import HostTransport
+
+        transport = HostTransport()
         A = mpg.gen_band(N, 5, 4, seed=3)
         starts = mpg.nnz_balanced_starts(A, world)
         r0, r1 = int(starts[rank]), int(starts[rank + 1])
@@ -94,7 +107,7 @@ def _worker(rank, world, port, N, out_q):
         x = mpg.rand_vect(N, 42)
         x_ext = np.zeros(n_ext)
         x_ext[:n_loc] = x[r0:r1]
-        _halo(x_ext, n_loc, r0, plan, sends, rank, world)
+        _halo(x_ext, n_loc, r0, plan, sends, rank, world, transport)
         y = np.array([np.sum(A_loc.val[A_loc.rowptr[i]:A_loc.rowptr[i + 1]]
                              * x_ext[cols[A_loc.rowptr[i]:A_loc.rowptr[i + 1]]]) for i in range(n_loc)])
         full = mpg.host_spmv(A, x)[r0:r1]
@@ -105,19 +118,25 @@ def _worker(rank, world, port, N, out_q):
         V = np.zeros((n_loc, m + 1))
         H = np.zeros((m + 1, m))
         b = mpg.host_spmv(A, x)[r0:r1]
-        beta = np.sqrt(_allreduce([b @ b])[0])
+        beta = np.sqrt(_allreduce([b @ b], transport)[0])
         V[:, 0] = b / beta
         for k in range(m):
             v_ext = np.zeros(n_ext)
             v_ext[:n_loc] = V[:, k]
-            _halo(v_ext, n_loc, r0, plan, sends, rank, world)
+            _halo(v_ext, n_loc, r0, plan, sends, rank, world, transport)
             w = S @ v_ext
-            h = _allreduce(V[:, :k + 1].T @ w)
+            h = _allreduce(V[:, :k + 1].T @ w, transport)
             w = w - V[:, :k + 1] @ h
             H[:k + 1, k] = h
-            H[k + 1, k] = np.sqrt(_allreduce([w @ w])[0])
+            H[k + 1, k] = np.sqrt(_allreduce([w @ w], transport)[0])
             V[:, k + 1] = w / H[k + 1, k]
-        out_q.put((rank, spmv_ok, H))
+        # max reduction and rank-order sums: the same bits on every rank
+        import ctypes as C
+
+        buf = np.array([float(rank), -float(rank), 1.0 / 3.0 * (rank + 1)])
+        assert transport.c.allreduce(None, buf.ctypes.data_as(C.POINTER(C.c_double)), 3, 1) == 0
+        mx = buf.copy()
+        out_q.put((rank, spmv_ok, (H, mx)))
     except Exception as e:  # surface the failure in the parent
         out_q.put((rank, repr(e), None))
     finally:
@@ -155,9 +174,10 @@ def test_partitioned_spmv_and_arnoldi_gloo(mpg, world):
         H[:k + 1, k] = h
         H[k + 1, k] = np.linalg.norm(w)
         V[:, k + 1] = w / H[k + 1, k]
-    for _, _, Hd in res:
+    for _, _, (Hd, mx) in res:
         assert np.allclose(Hd, H, rtol=1e-12, atol=1e-12)
-    assert np.array_equal(res[0][2], res[1][2])  # every rank holds the same H
+        assert np.array_equal(mx, [world - 1.0, 0.0, world / 3.0])
+    assert np.array_equal(res[0][2][0], res[1][2][0])  # every rank holds the same H
 
 
 def test_halo_plan_single_process(mpg):
