@@ -130,17 +130,22 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_ext, int 
                                                           const CI* __restrict__ col, const X* __restrict__ val,
                                                           const X* __restrict__ x, const X* __restrict__ b,
                                                           const P* __restrict__ diag, T* __restrict__ w,
-                                                          double* __restrict__ partial) {
+                                                          double* __restrict__ partial,
+                                                          const int32_t* __restrict__ sbase,
+                                                          const uint8_t* __restrict__ sexc,
+                                                          const int32_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ ccol,
+                                                          const X* __restrict__ cval, int xcd) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    const int s = blockIdx.x * (kBlock / kWave) + wid;
+    const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (kBlock / kWave) + wid;
     const bool live = s < nslices;  // a dead wave still joins the partials' barrier
     const int row0 = s * kWave;
     const int i = row0 + lane;
     const bool own = live && i < n;
     SellRow<X, CI, W, true> row;  // once per cycle: non-temporal slices
-    row.init_load(live ? s : 0, off);
+    row.init_load(live ? s : 0, off, sexc);
     __builtin_amdgcn_sched_barrier(0);
     X xr[WIN ? NQ : 1];
     if constexpr (WIN) {
@@ -154,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_ext, int 
     const X bi = b[ic], xi = x[ic];
     const P di = diag ? diag[ic] : P(0);
     __builtin_amdgcn_sched_barrier(0);
-    row.init_finish(lane, col, val);
+    row.init_finish(lane, col, val, sbase);
     row.load(0);
     __builtin_amdgcn_sched_barrier(0);
     double sum = 0.0;
@@ -174,10 +179,14 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_ext, int 
             }
         } else {
             auto xv = [&](int c) { return (double)x[c]; };
-            row.sum(0, xv, sum);
-            for (int q = row.U; q < row.steps; q += row.U) {
-                row.load(q);
-                row.sum(q, xv, sum);
+            if (SellCol<CI>::stepped && row.exc) {
+                sum = csr_row_sum(own ? i : -1, rowptr, ccol, cval, xv);
+            } else {
+                row.sum(0, xv, sum);
+                for (int q = row.U; q < row.steps; q += row.U) {
+                    row.load(q);
+                    row.sum(q, xv, sum);
+                }
             }
         }
     }
@@ -436,18 +445,23 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
                                                       const T* __restrict__ wprev, const T* __restrict__ inv_p,
                                                       T* __restrict__ V, int64_t ld, int k,
                                                       const P* __restrict__ diag, T* __restrict__ w,
-                                                      GivensFold<T> fold, SellDots dd) {
+                                                      GivensFold<T> fold, SellDots dd,
+                                                      const int32_t* __restrict__ sbase,
+                                                      const uint8_t* __restrict__ sexc,
+                                                      const int32_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ ccol,
+                                                      const typename SellStore<VI>::type* __restrict__ cval, int xcd) {
     using S = typename SellStore<VI>::type;
     constexpr int NQ = kWinLen / kWave;
     __shared__ T win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    const int s = blockIdx.x * (kBlock / kWave) + wid;
+    const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (kBlock / kWave) + wid;
     const bool live = s < nslices;  // a dead wave still joins the fold's barriers
     const int row0 = s * kWave;
     const int i = row0 + lane;
     // 0. the slice's offsets
     SellRow<S, CI, W> row;
-    row.init_load(live ? s : 0, off);
+    row.init_load(live ? s : 0, off, sexc);
     __builtin_amdgcn_sched_barrier(0);
     // 1. the fold's ||w||^2 partial (nparts <= kBlock, checked at launch: one per lane)
     double part = 0.0;
@@ -469,7 +483,7 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
     }
     __builtin_amdgcn_sched_barrier(0);
     // 3. the slice's first batch
-    row.init_finish(lane, col, val);
+    row.init_finish(lane, col, val, sbase);
     row.load(0);
     __builtin_amdgcn_sched_barrier(0);
     // the scale 1/h_{k,k-1}: the folded Givens step, or the Givens kernel's
@@ -517,10 +531,14 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
             vk = win[wid][lane + kWinLo];
         } else {
             auto xv = [&](int c) { return (double)(T)(wprev[c] * inv); };
-            row.sum(0, xv, sum);
-            for (int q = row.U; q < row.steps; q += row.U) {
-                row.load(q);
-                row.sum(q, xv, sum);
+            if (SellCol<CI>::stepped && row.exc) {
+                sum = csr_row_sum(i < n ? i : -1, rowptr, ccol, cval, xv);
+            } else {
+                row.sum(0, xv, sum);
+                for (int q = row.U; q < row.steps; q += row.U) {
+                    row.load(q);
+                    row.sum(q, xv, sum);
+                }
             }
             vk = (T)(wr[0] * inv);
         }
@@ -535,16 +553,21 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
     if constexpr (DN > 0) {
         // the earlier basis columns at this row: clamped, branch-free loads
         // issued together (one latency), then one product per column
+        // (n >= 1: spmv_impl refuses the fused dots on an empty block, so row n - 1 exists)
+        const bool own_row = live && i < n;
         const int ic = i < n ? i : n - 1;
         const int kc = k > 0 ? k - 1 : 0;
         T vc[DN];
 #pragma unroll
         for (int c = 0; c < DN; ++c) vc[c] = V[(int64_t)(c < kc ? c : kc) * ld + ic];
         __builtin_amdgcn_sched_barrier(0);
-        const double wd = (live && i < n) ? (double)wi : 0.0;
+        const double wd = (double)wi;
         double acc[DN];
+        // a lane without a row contributes an exact 0 (not a clamped row's
+        // value times 0, which is NaN when that value is Inf or NaN)
 #pragma unroll
-        for (int c = 0; c < DN; ++c) acc[c] = (c < k ? (double)vc[c] : c == k ? (double)vk : 0.0) * wd;
+        for (int c = 0; c < DN; ++c)
+            acc[c] = own_row ? (c < k ? (double)vc[c] : c == k ? (double)vk : 0.0) * wd : 0.0;
         store_partials<DN, kBlock, true>(acc, dd.nc, dd.wgpart);
         const int g = blockIdx.x / dd.gs;
         const int m0 = g * dd.gs, m1 = m0 + dd.gs < (int)gridDim.x ? m0 + dd.gs : (int)gridDim.x;
@@ -1282,13 +1305,19 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
     return MPG_OK;
 }
 
+int64_t mpg_arnoldi_sell_meta_bytes(mpg_arnoldi_t a) {
+    if (!a || a->sell.nslices == 0) return 0;
+    const int64_t steps = a->sell.padded / ((int64_t)kWave * a->sell.W);
+    return ((int64_t)a->sell.nslices + 1) * 8 + (a->sell.c16s ? steps * 4 : 0);
+}
+
 int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
                             int64_t* stored, int32_t* window) {
     if (!a) return MPG_ERR_ARG;
     const bool sell = a->sell.nslices > 0;
     if (format) *format = sell ? 2 : 1;
     if (vec_width) *vec_width = sell ? a->sell.W : 4;
-    if (col_bytes) *col_bytes = sell && a->sell.c16 ? 2 : 4;
+    if (col_bytes) *col_bytes = sell ? a->sell.col_bytes() : 4;
     if (stored) *stored = sell ? a->sell.padded : a->d.A->nnz;
     if (window) *window = sell && a->sell.win ? 1 : 0;
     return MPG_OK;
@@ -1319,14 +1348,16 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
         if (S->nslices > 0 && S->vtype == a->d.outer_type) {
             const int grid = (S->nslices + kBlock / kWave - 1) / (kBlock / kWave);
             a->last_G = grid;
-            return sell_dispatch(S->W, S->c16, [&](auto ci, auto wc) {
+            return sell_dispatch(*S, [&](auto ci, auto wc) {
                 using CI = decltype(ci);
                 return sell_dispatch_win(S->win, [&](auto wn) {
                     k_prologue_sell<T, X, P, CI, decltype(wc)::value, decltype(wn)::value>
                         <<<grid, kBlock, 0, a->ctx->stream>>>(
                             a->d.n, a->d.n_ext, S->nslices, S->off, static_cast<const CI*>(S->col),
                             static_cast<const X*>(S->val), static_cast<const X*>(a->d.x),
-                            static_cast<const X*>(a->d.b), diag, static_cast<T*>(a->w[0]), a->partial);
+                            static_cast<const X*>(a->d.b), diag, static_cast<T*>(a->w[0]), a->partial, S->sbase,
+                            S->sexc, A->rowptr, A->col, static_cast<const X*>(a->d.val_outer),
+                            sell_xcd_order(*S) ? 1 : 0);
                     return (int)MPG_OK;
                 });
             });
@@ -1388,7 +1419,7 @@ int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols) {
 // not all present -- the caller then launches the dots itself).
 static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
-    if (dots && (a->sell.nslices == 0 || !a->sell.c16 || !a->sell.win || (a->combo != 2 && a->combo != 3) ||
+    if (dots && (a->d.n <= 0 || a->sell.nslices == 0 || !a->sell.c16 || !a->sell.win || (a->combo != 2 && a->combo != 3) ||
                  k + 1 > kNC || a->d.orth == kOrthMGS))
         return MPG_ERR_UNSUPPORTED;
     if (fold && (k < 1 || a->d.m > kFoldMaxM)) return MPG_ERR_ARG;
@@ -1404,7 +1435,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
         if (a->sell.nslices > 0) {
             const auto& S = a->sell;
             if (fold == 2 && a->last_G > kBlock) return (int)MPG_ERR_ARG;  // k_step_sell folds <= kBlock partials
-            return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
+            return sell_dispatch(S, [&](auto ci, auto wc) {
                 using CI = decltype(ci);
                 constexpr int Wc = decltype(wc)::value;
                 const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
@@ -1413,7 +1444,10 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                             a->d.n, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
-                            static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd);
+                            static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd,
+                            S.sbase, S.sexc, A->rowptr, A->col,
+                            static_cast<const typename SellStore<VI>::type*>(a->d.val_inner),
+                            sell_xcd_order(S) ? 1 : 0);
                     return (int)MPG_OK;
                 };
                 if constexpr (std::is_same_v<T, float> && std::is_same_v<VI, float> &&

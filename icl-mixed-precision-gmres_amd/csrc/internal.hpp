@@ -75,6 +75,17 @@ inline void launch_timed(mpg_ctx* c, K kern, dim3 grid, dim3 block, A... args) {
     }
 }
 
+// XCD-aware workgroup order: the hardware places workgroup b on XCD b % 8
+// (round robin), so logical block xcd_block(b, G) gives each XCD one
+// contiguous range of the grid (its private L2 then caches the neighbourhood
+// of its own rows). A bijection of [0, G).
+__device__ __forceinline__ int xcd_block(int b, int G) {
+    constexpr int X = 8;
+    const int q = G / X, r = G % X;
+    const int xcd = b % X, idx = b / X;
+    return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+}
+
 inline int grid_for(int64_t n, int per_thread, int cap = 2048) {
     int64_t g = (n + (int64_t)kBlock * per_thread - 1) / ((int64_t)kBlock * per_thread);
     if (g < 1) g = 1;

@@ -47,12 +47,50 @@ __global__ void k_sell_span(int n, const int32_t* __restrict__ rowptr, const int
     }
 }
 
+// Stepped int16 columns: one wave per slice; for each step j and element e
+// the base of (slice, step, element) = the midpoint of c - (row0 + lane)
+// over that element of all 64 rows; a slice where some spread exceeds
+// +-32767 is flagged in sexc (summed from CSR by the SpMVs).
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_sell_step_base(int n, int nslices, const int32_t* __restrict__ rowptr,
+                                                           const int32_t* __restrict__ col,
+                                                           const int64_t* __restrict__ off, int32_t* __restrict__ sbase,
+                                                           uint8_t* __restrict__ sexc) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = (int)(t / kWave), lane = (int)(t % kWave);
+    if (s >= nslices) return;  // whole waves: the wave's shuffles below stay converged
+    const int r = s * kWave + lane;
+    const int64_t o = off[s];
+    const int steps = (int)((off[s + 1] - o) / (kWave * W));
+    const int b = r < n ? rowptr[r] : 0, len = r < n ? rowptr[r + 1] - b : 0;
+    bool bad = false;
+    for (int j = 0; j < steps; ++j) {
+        for (int e = 0; e < W; ++e) {
+            const int k = j * W + e;
+            int lo = INT32_MAX, hi = INT32_MIN;
+            if (k < len) {
+                const int d = col[b + k] - r;
+                lo = d;
+                hi = d;
+            }
+            for (int m = kWave / 2; m > 0; m >>= 1) {
+                lo = min(lo, __shfl_xor(lo, m, kWave));
+                hi = max(hi, __shfl_xor(hi, m, kWave));
+            }
+            const int base = lo > hi ? 0 : (int)(((int64_t)lo + (int64_t)hi) >> 1);
+            if (lo <= hi && ((int64_t)hi - base > 32767 || (int64_t)lo - base < -32767)) bad = true;
+            if (lane == 0) sbase[o / kWave + (int64_t)j * W + e] = base;
+        }
+    }
+    if (lane == 0) sexc[s] = bad ? 1 : 0;
+}
+
 // scatter the CSR (col, val) of row 64 s + lane into its slice; pads get the
 // sentinel column and a zero value (S: stored value type, half as raw bits)
 template <class S, class CI, int W>
 __global__ void k_sell_fill(int n, int nslices, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                            const S* __restrict__ val, const int64_t* __restrict__ off, CI* __restrict__ scol,
-                            S* __restrict__ sval) {
+                            const S* __restrict__ val, const int64_t* __restrict__ off, const int32_t* __restrict__ sbase,
+                            CI* __restrict__ scol, S* __restrict__ sval) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int s = (int)(t / kWave), lane = (int)(t % kWave);
     if (s >= nslices) return;
@@ -64,7 +102,8 @@ __global__ void k_sell_fill(int n, int nslices, const int32_t* __restrict__ rowp
         const int64_t pos = o + (int64_t)(j / W) * kWave * W + lane * W + (j % W);
         if (j < len) {
             const int c = col[b + j];
-            scol[pos] = sizeof(CI) == 2 ? (CI)(c - s * kWave) : (CI)c;
+            if constexpr (SellCol<CI>::stepped) scol[pos] = (CI)(uint16_t)(int16_t)(c - r - sbase[o / kWave + j]);
+            else scol[pos] = sizeof(CI) == 2 ? (CI)(c - s * kWave) : (CI)c;
             sval[pos] = val[b + j];
         } else {
             scol[pos] = SellCol<CI>::kPad;
@@ -87,17 +126,20 @@ int with_store(int vtype, F&& f) {
 template <class X, class S, class CI, int W, bool WIN>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col, const S* __restrict__ val,
-                                                      const X* __restrict__ x, X alpha, X beta,
-                                                      X* __restrict__ y) {
+                                                      const int32_t* __restrict__ sbase,
+                                                      const uint8_t* __restrict__ sexc, const int32_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ ccol, const S* __restrict__ cval,
+                                                      const X* __restrict__ x, X alpha, X beta, X* __restrict__ y,
+                                                      int xcd) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    const int s = blockIdx.x * (kBlock / kWave) + wid;
+    const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (kBlock / kWave) + wid;
     if (s >= nslices) return;  // no workgroup barrier below: a dead wave may leave
     const int row0 = s * kWave;
     const int i = row0 + lane;
     SellRow<S, CI, W> row;
-    row.init_load(s, off);
+    row.init_load(s, off, sexc);
     __builtin_amdgcn_sched_barrier(0);
     X xr[WIN ? NQ : 1];
     if constexpr (WIN) {
@@ -109,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
     }
     const X yi = beta != X(0) ? y[i < n ? i : 0] : X(0);
     __builtin_amdgcn_sched_barrier(0);
-    row.init_finish(lane, col, val);
+    row.init_finish(lane, col, val, sbase);
     row.load(0);
     __builtin_amdgcn_sched_barrier(0);
     double sum = 0.0;
@@ -128,10 +170,14 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
         }
     } else {
         auto xv = [&](int c) { return (double)x[c]; };
-        row.sum(0, xv, sum);
-        for (int q = row.U; q < row.steps; q += row.U) {
-            row.load(q);
-            row.sum(q, xv, sum);
+        if (SellCol<CI>::stepped && row.exc) {
+            sum = csr_row_sum(i < n ? i : -1, rowptr, ccol, cval, xv);
+        } else {
+            row.sum(0, xv, sum);
+            for (int q = row.U; q < row.steps; q += row.U) {
+                row.load(q);
+                row.sum(q, xv, sum);
+            }
         }
     }
     if (i < n) {
@@ -187,12 +233,12 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
     (void)hipFree(span);
     if (!ok) return MPG_ERR_HIP;
     const bool c16 = span_h[0] >= -32767 && span_h[1] <= 32767;
+    const char* senv = std::getenv("MPG_SELL_STEPPED");  // 0: never the stepped int16 form
+    const bool try_c16s = !c16 && !(senv && *senv == '0');
     const char* wenv = std::getenv("MPG_SELL_WINDOW");  // 0: always gather from global memory
     const bool win = !(wenv && *wenv == '0') && span_h[0] >= -kWinLo && span_h[1] < kWave + kWinHi;
     const size_t vsize = vtype == MPG_F64 ? 8 : vtype == MPG_F32 ? 4 : 2;
-    if (hipMalloc((void**)&S.off, off.size() * 8) != hipSuccess ||
-        hipMalloc(&S.col, (size_t)best * (c16 ? 2 : 4) + 256) != hipSuccess ||
-        hipMalloc(&S.val, (size_t)best * vsize + 256) != hipSuccess) {
+    if (hipMalloc((void**)&S.off, off.size() * 8) != hipSuccess) {
         sell_free(S);
         return MPG_ERR_ALLOC;
     }
@@ -208,12 +254,50 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
     S.win = win;
     S.padded = best;
     const int grid = (int)(((int64_t)ns * kWave + kBlock - 1) / kBlock);
+    if (try_c16s) {
+        // the (slice, step, element) bases; the stepped form when at most 1 %
+        // of the slices need the CSR fallback (sexc)
+        std::vector<uint8_t> exc((size_t)ns, 0);
+        bool okb = hipMalloc((void**)&S.sbase, (size_t)(best / kWave) * 4 + 256) == hipSuccess &&
+                   hipMalloc((void**)&S.sexc, (size_t)ns + 256) == hipSuccess;
+        if (okb) {
+            auto launch = [&](auto wc) {
+                k_sell_step_base<decltype(wc)::value><<<grid, kBlock, 0, stream>>>(n, ns, A->rowptr, A->col, S.off,
+                                                                                S.sbase, S.sexc);
+            };
+            if (best_w == 4) launch(std::integral_constant<int, 4>());
+            else if (best_w == 2) launch(std::integral_constant<int, 2>());
+            else launch(std::integral_constant<int, 1>());
+            okb = hipMemcpyAsync(exc.data(), S.sexc, (size_t)ns, hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                  hipStreamSynchronize(stream) == hipSuccess;
+        }
+        if (!okb) {
+            sell_free(S);
+            return MPG_ERR_HIP;
+        }
+        int64_t nexc = 0;
+        for (uint8_t e : exc) nexc += e;
+        if (nexc * 100 <= ns) {
+            S.c16s = true;
+            S.nexc = nexc;
+        } else {
+            (void)hipFree(S.sbase);
+            (void)hipFree(S.sexc);
+            S.sbase = nullptr;
+            S.sexc = nullptr;
+        }
+    }
+    if (hipMalloc(&S.col, (size_t)best * S.col_bytes() + 256) != hipSuccess ||
+        hipMalloc(&S.val, (size_t)best * vsize + 256) != hipSuccess) {
+        sell_free(S);
+        return MPG_ERR_ALLOC;
+    }
     int st = with_store(vtype, [&](auto sv) {
         using St = decltype(sv);
-        return sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
+        return sell_dispatch(S, [&](auto ci, auto wc) {
             using CI = decltype(ci);
             k_sell_fill<St, CI, decltype(wc)::value><<<grid, kBlock, 0, stream>>>(
-                n, ns, A->rowptr, A->col, static_cast<const St*>(val), S.off, static_cast<CI*>(S.col),
+                n, ns, A->rowptr, A->col, static_cast<const St*>(val), S.off, S.sbase, static_cast<CI*>(S.col),
                 static_cast<St*>(S.val));
             return (int)MPG_OK;
         });
@@ -224,6 +308,8 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
 }
 
 void sell_free(SellCopy& S) {
+    if (S.sbase) (void)hipFree(S.sbase);
+    if (S.sexc) (void)hipFree(S.sexc);
     if (S.off) (void)hipFree(S.off);
     if (S.col) (void)hipFree(S.col);
     if (S.val) (void)hipFree(S.val);
@@ -236,6 +322,8 @@ struct mpg_sell {
     mpg_ctx* ctx = nullptr;
     int cols = 0;
     SellCopy S;
+    const mpg_csr* A = nullptr;  // the CSR the copy was built from (flagged slices read it)
+    const void* vals = nullptr;
 };
 
 namespace {
@@ -246,12 +334,13 @@ int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y)
     const SellCopy& S = A->S;
     if (S.nslices == 0) return MPG_OK;
     const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
-    int st = sell_dispatch(S.W, S.c16, [&](auto ci, auto wc) {
+    int st = sell_dispatch(S, [&](auto ci, auto wc) {
         using CI = decltype(ci);
         return sell_dispatch_win(S.win, [&](auto wn) {
             k_sell_spmv<X, St, CI, decltype(wc)::value, decltype(wn)::value><<<grid, kBlock, 0, ctx->stream>>>(
-                S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val), x,
-                alpha, beta, y);
+                S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val), S.sbase,
+                S.sexc, A->A->rowptr, A->A->col, static_cast<const St*>(A->vals), x, alpha, beta, y,
+                sell_xcd_order(S) ? 1 : 0);
             return (int)MPG_OK;
         });
     });
@@ -272,6 +361,8 @@ int mpg_sell_create(mpg_ctx_t ctx, mpg_csr_t A, int32_t vtype, const void* vals,
     if (!h) return MPG_ERR_ALLOC;
     h->ctx = ctx;
     h->cols = A->cols;
+    h->A = A;
+    h->vals = vals;
     if (int st = sell_build(ctx, A, vtype, vals, format, h->S)) {
         delete h;
         return st;
@@ -295,9 +386,16 @@ int mpg_sell_destroy(mpg_sell_t A) {
 int mpg_sell_layout(mpg_sell_t A, int32_t* vec_width, int32_t* col_bytes, int64_t* stored, int32_t* window) {
     if (!A) return MPG_ERR_ARG;
     if (vec_width) *vec_width = A->S.W;
-    if (col_bytes) *col_bytes = A->S.c16 ? 2 : 4;
+    if (col_bytes) *col_bytes = A->S.col_bytes();
     if (stored) *stored = A->S.padded;
     if (window) *window = A->S.win ? 1 : 0;
+    return MPG_OK;
+}
+
+int mpg_sell_columns(mpg_sell_t A, int32_t* form, int64_t* csr_slices) {
+    if (!A) return MPG_ERR_ARG;
+    if (form) *form = A->S.c16 ? 1 : A->S.c16s ? 2 : 0;
+    if (csr_slices) *csr_slices = A->S.nexc;
     return MPG_OK;
 }
 

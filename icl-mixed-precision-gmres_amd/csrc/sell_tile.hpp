@@ -8,30 +8,54 @@
 //
 // so one wave-wide W-vector load per step moves 64 W contiguous entries
 // and needs no LDS, no segmented reduction and no row pointers. Columns are
-// int32, or int16 deltas against the slice's first row when every entry of
-// the matrix is within +-32767 of it (banded/stencil matrices: half the
-// index bytes). Padding carries a sentinel column and is skipped, so an
-// Inf/NaN in x never meets a padded zero. Within a row the entries keep CSR
-// order and the fp64 sum runs in that order.
+// stored in one of three forms (the first that fits):
+//   int16_t   c - row0, when every entry of the matrix is within +-32767 of
+//             its slice's first row (banded matrices, 7-point stencils);
+//   uint16_t  "stepped": the int16 bits of c - (row0 + lane) - base[s][j][e]
+//             for element e of step j, with one int32 base per (slice, step,
+//             element) (sbase, at index (off[s] / (64 W) + j) W + e): element
+//             e of step j of all 64 rows of a slice is, for a stencil in
+//             natural order, one neighbour offset +- a few, so wide stencils
+//             (the 27-point 3-dof Queen stand-in: offsets up to +-37,299)
+//             still store 2-B columns, plus 4 B per 64 entries. A slice where
+//             some (step, element) spreads wider (rows on both sides of a
+//             boundary plane) is flagged in sexc[s] and its rows are summed
+//             from the CSR arrays instead, in the same order (same bits);
+//   int32_t   c.
+// Padding carries a sentinel column and is skipped, so an Inf/NaN in x never
+// meets a padded zero. Within a row the entries keep CSR order and the fp64
+// sum runs in that order.
 #pragma once
 
 #include "internal.hpp"
 #include "csr_tile.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace mpg {
 
+// decode(c, row0, lane_base): lane_base = row0 + lane + base (stepped form only)
 template <class CI> struct SellCol;
 template <> struct SellCol<int32_t> {
     static constexpr int32_t kPad = -1;
+    static constexpr bool stepped = false;
     static __device__ __forceinline__ bool live(int32_t c) { return c >= 0; }
-    static __device__ __forceinline__ int decode(int32_t c, int /*row0*/) { return c; }
+    static __device__ __forceinline__ int decode(int32_t c, int /*row0*/, int /*lane_base*/) { return c; }
 };
 template <> struct SellCol<int16_t> {
     static constexpr int16_t kPad = INT16_MIN;
+    static constexpr bool stepped = false;
     static __device__ __forceinline__ bool live(int16_t c) { return c != INT16_MIN; }
-    static __device__ __forceinline__ int decode(int16_t c, int row0) { return row0 + (int)c; }
+    static __device__ __forceinline__ int decode(int16_t c, int row0, int /*lane_base*/) { return row0 + (int)c; }
+};
+template <> struct SellCol<uint16_t> {
+    static constexpr uint16_t kPad = 0x8000u;
+    static constexpr bool stepped = true;
+    static __device__ __forceinline__ bool live(uint16_t c) { return c != 0x8000u; }
+    static __device__ __forceinline__ int decode(uint16_t c, int /*row0*/, int lane_base) {
+        return lane_base + (int)(int16_t)c;
+    }
 };
 
 // raw storage of a value type inside the slices
@@ -96,7 +120,7 @@ __device__ __forceinline__ double sell_row_sum(int s, int lane, const int64_t* _
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int e = 0; e < W; ++e)
-                x[u][e] = SellCol<CI>::live(c[u][e]) ? xval(SellCol<CI>::decode(c[u][e], row0)) : 0.0;
+                x[u][e] = SellCol<CI>::live(c[u][e]) ? xval(SellCol<CI>::decode(c[u][e], row0, row0)) : 0.0;
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -118,35 +142,46 @@ __device__ __forceinline__ double sell_row_sum(int s, int lane, const int64_t* _
 template <class S, class CI, int W, bool NT = (MPG_SELL_NT != 0)>
 struct SellRow {
     static constexpr int U = sell_unroll<W>();
+    static constexpr bool kStepped = SellCol<CI>::stepped;
     CI c[U][W];
     S v[U][W];
-    int steps, row0;
+    int32_t bq[kStepped ? U : 1][kStepped ? W : 1];  // stepped columns: the batch's bases
+    int steps, row0, lane_row;
+    bool exc = false;  // stepped: this slice is summed from CSR (sexc)
     const CI* __restrict__ cp;
     const S* __restrict__ vp;
+    const int32_t* __restrict__ bp;
 
     int64_t o0, o1;
     // the slice's offsets: issue first (everything else needs them), use later
-    __device__ __forceinline__ void init_load(int s, const int64_t* __restrict__ off) {
+    __device__ __forceinline__ void init_load(int s, const int64_t* __restrict__ off,
+                                              const uint8_t* __restrict__ sexc = nullptr) {
         o0 = off[s];
         o1 = off[s + 1];
         row0 = s * kWave;
+        if constexpr (kStepped) exc = sexc[s] != 0;
     }
-    __device__ __forceinline__ void init_finish(int lane, const CI* __restrict__ col, const S* __restrict__ val) {
+    // sbase: the stepped form's (slice, step) bases (nullptr otherwise)
+    __device__ __forceinline__ void init_finish(int lane, const CI* __restrict__ col, const S* __restrict__ val,
+                                                const int32_t* __restrict__ sbase = nullptr) {
         steps = (int)((o1 - o0) / (kWave * W));
         const int64_t base = steps > 0 ? o0 + lane * W : 0;
         cp = col + base;
         vp = val + base;
+        lane_row = row0 + lane;
+        if constexpr (kStepped) bp = sbase + (steps > 0 ? o0 / kWave : 0);  // (o0 / (64 W)) W
     }
     __device__ __forceinline__ void init(int s, int lane, const int64_t* __restrict__ off, const CI* __restrict__ col,
-                                         const S* __restrict__ val) {
+                                         const S* __restrict__ val, const int32_t* __restrict__ sbase = nullptr) {
         init_load(s, off);
-        init_finish(lane, col, val);
+        init_finish(lane, col, val, sbase);
     }
     __device__ __forceinline__ void load(int q) {
         const int last = steps > 0 ? steps - 1 : 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int qq = q + u < last ? q + u : last;
+            if constexpr (kStepped) VecW<int32_t, W, false>::load(bp + (int64_t)qq * W, bq[u]);
             VecW<CI, W, NT>::load(cp + (int64_t)qq * kWave * W, c[u]);
             VecW<S, W, NT>::load(vp + (int64_t)qq * kWave * W, v[u]);
         }
@@ -161,7 +196,9 @@ struct SellRow {
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int e = 0; e < W; ++e)
-                x[u][e] = xval(SellCol<CI>::live(c[u][e]) ? SellCol<CI>::decode(c[u][e], row0) : row0);
+                x[u][e] = xval(SellCol<CI>::live(c[u][e])
+                                   ? SellCol<CI>::decode(c[u][e], row0, kStepped ? lane_row + bq[u][e] : 0)
+                                   : row0);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -169,6 +206,17 @@ struct SellRow {
                 if (q + u < steps && SellCol<CI>::live(c[u][e])) acc += widen(v[u][e]) * x[u][e];
     }
 };
+
+// The row sum from the CSR arrays in CSR order with SellRow::sum's
+// arithmetic (a stepped copy's flagged slices); i < 0: no row, 0.
+template <class S, class XF>
+__device__ __forceinline__ double csr_row_sum(int i, const int32_t* __restrict__ rowptr,
+                                              const int32_t* __restrict__ col, const S* __restrict__ val, XF xval) {
+    double acc = 0.0;
+    if (i < 0) return acc;
+    for (int j = rowptr[i], e = rowptr[i + 1]; j < e; ++j) acc += widen(val[j]) * xval(col[j]);
+    return acc;
+}
 
 // LDS window of x for a slice (SELL SpMVs): every column of every slice
 // within [row0 - kWinLo, row0 + 64 + kWinHi) lets the gathers read LDS
@@ -180,11 +228,16 @@ struct SellCopy {
     int n = 0, nslices = 0, W = 1;
     int vtype = 0;     // mpg_dtype_t of the stored values (MPG_F64 | MPG_F32 | MPG_F16)
     bool c16 = false;  // int16 slice-relative columns
+    bool c16s = false; // stepped int16 columns (uint16_t bits + sbase)
     bool win = false;  // every slice's columns inside the LDS window
     int64_t padded = 0;
     int64_t* off = nullptr;
     void* col = nullptr;
     void* val = nullptr;
+    int32_t* sbase = nullptr;  // c16s: one base per (slice, step, element)
+    uint8_t* sexc = nullptr;   // c16s: 1 = the slice is summed from CSR
+    int64_t nexc = 0;          // c16s: slices flagged in sexc
+    int col_bytes() const { return c16 || c16s ? 2 : 4; }
 };
 
 // Build the copy from the CSR structure and `val` (vtype; F16 = raw IEEE
@@ -195,17 +248,27 @@ void sell_free(SellCopy& S);
 
 // f(column type, integral_constant<int, W>) for the copy's layout
 template <class F>
-int sell_dispatch(int W, bool c16, F&& f) {
+int sell_dispatch(const SellCopy& S, F&& f) {
     auto with_w = [&](auto ci) {
-        switch (W) {
+        switch (S.W) {
             case 1: return f(ci, std::integral_constant<int, 1>());
             case 2: return f(ci, std::integral_constant<int, 2>());
             case 4: return f(ci, std::integral_constant<int, 4>());
             default: return (int)MPG_ERR_UNSUPPORTED;
         }
     };
-    return c16 ? with_w(int16_t()) : with_w(int32_t());
+    return S.c16 ? with_w(int16_t()) : S.c16s ? with_w(uint16_t()) : with_w(int32_t());
 }
+// XCD-ordered slices (MPG_SELL_XCD=0: off): a copy without the LDS window
+// gathers x from global memory, and with the default round-robin placement
+// of workgroups over the 8 XCDs every XCD's L2 fetches the whole of x for
+// the neighbour planes of its scattered slices; in XCD order each L2 serves
+// one contiguous run of rows (xcd_block, internal.hpp)
+inline bool sell_xcd_order(const SellCopy& S) {
+    const char* e = std::getenv("MPG_SELL_XCD");
+    return !S.win && !(e && *e == '0');
+}
+
 template <class F>
 int sell_dispatch_win(bool win, F&& f) {
     return win ? f(std::true_type()) : f(std::false_type());

@@ -767,14 +767,14 @@ double FusedEngine::phase_bytes(int which) const {
     if (which == 1) return z * (sX + 4) + (n + 1) * 4 + 3 * n * sX + n * sT + jac * n * sP;
     if (which == 4) {
         // the bytes the Arnoldi SpMV's own storage moves per launch: SELL-64
-        // slots (column offset + value) and int64 slice offsets, or CSR
+        // slots (column offset + value), slice offsets and step bases, or CSR
         // values + int32 columns + row pointers; then w_prev read once, v_k
         // stored to V(:,k), w written, the Jacobi diagonal when fused
         int32_t fmt = 0, W = 0, cb = 0, win = 0;
         int64_t stored = 0;
         check(mpg_arnoldi_spmv_layout(I.arn, &fmt, &W, &cb, &stored, &win), "layout", I.ctx);
         const double vec = 3 * n * sT + jac * n * sP;
-        if (fmt == 2) return (double)stored * (cb + sV) + std::ceil(n / 64.0) * 8 + vec;
+        if (fmt == 2) return (double)stored * (cb + sV) + (double)mpg_arnoldi_sell_meta_bytes(I.arn) + vec;
         return z * (sV + 4) + (n + 1) * 4 + vec;
     }
     if (which == 3) {

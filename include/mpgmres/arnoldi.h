@@ -78,6 +78,10 @@ int mpg_arnoldi_destroy(mpg_arnoldi_t a);
  * LDS window instead of gathering from memory. Any output may be NULL. */
 int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
                             int64_t* stored, int32_t* window);
+/* bytes of the SELL copy's per-slice metadata one SpMV reads: int64 slice
+ * offsets, plus one int32 base per (slice, step) in the stepped int16 column
+ * form (0 without a SELL copy) */
+int64_t mpg_arnoldi_sell_meta_bytes(mpg_arnoldi_t a);
 
 int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
 int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);

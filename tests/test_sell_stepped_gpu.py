@@ -1,0 +1,143 @@
+"""Stepped int16 SELL columns (sell_tile.hpp): a 7-point Laplacian on a
+190 x 190 x 6 grid has column offsets of +-36,100, beyond the int16
+slice-relative form, so its copy stores int16 offsets against one base per
+(slice, step, element). A tridiagonal matrix with two far entries in one
+slice (element 0 of one row 40,000 below its row, of the next 40,000 above)
+spreads beyond 16 bits there, so that slice alone is summed from the CSR
+arrays. Sums run in CSR
+order with the same arithmetic in every form, so the stepped copy, the
+int32 copy (MPG_SELL_STEPPED=0) and the CSR SpMV give the same bits for
+fp32/fp16 values (fp64: the CSR tile's staged products, a few ulps), and
+whole solves are bit-identical between the column forms and within the
+parity tolerances of the oracle (tests/parity.py)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests.parity import as_ref, compare
+
+pytestmark = pytest.mark.gpu
+F64_EPS = np.finfo(np.float64).eps
+
+
+def _wide(mpg):
+    return mpg.gen_laplace3d(190, 190, 6)
+
+
+def _far(mpg, n=200_000):
+    """tridiagonal, diagonally dominant; row 64000 also reads column 24000,
+    row 64001 holds only column 104001 (slice 1000: a spread of 80,000)"""
+    rows = []
+    for r in range(n):
+        if r == 64001:
+            rows.append([(104001, 0.5)])
+            continue
+        e = [(c, -1.0) for c in (r - 1, r + 1) if 0 <= c < n] + [(r, 4.0)]
+        if r == 64000:
+            e.append((24000, 0.25))
+        rows.append(sorted(e))
+    rp = np.zeros(n + 1, dtype=np.int32)
+    rp[1:] = np.cumsum([len(x) for x in rows])
+    col = np.array([c for x in rows for c, _ in x], dtype=np.int32)
+    val = np.array([v for x in rows for _, v in x], dtype=np.float64)
+    return mpg.Csr(n, n, rp, col, val)
+
+
+@pytest.mark.parametrize("stepped", ["1", "0"])
+@pytest.mark.parametrize("kind", ["wide", "far"])
+def test_sell_stepped_columns_spmv(hip, mpg, stepped, kind, monkeypatch):
+    monkeypatch.setenv("MPG_SELL_STEPPED", stepped)
+    A = _wide(mpg) if kind == "wide" else _far(mpg)
+    n = A.nrows
+    g = np.random.default_rng(3)
+    x = g.uniform(-1, 1, n)
+    y0 = g.uniform(-1, 1, n)
+    drp, dci = hip.buf(A.rowptr), hip.buf(A.col)
+    csr = C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, n, n, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    sells = []
+    try:
+        cases = [("f64", 0, A.val, np.float64, -1.0, 1.0), ("f32", 1, A.val.astype(np.float32), np.float32, 1.0, 0.0),
+                 ("f16f32", 2, A.val.astype(np.float16).view(np.uint16), np.float32, 2.0, -0.5)]
+        for name, vt, vals, xdt, alpha, beta in cases:
+            dv = hip.buf(vals)
+            sell = C.c_void_p()
+            hip.check(hip.lib.mpg_sell_create(hip.ctx, csr, vt, dv.p, 0, C.byref(sell)))
+            assert sell.value
+            sells.append(sell)
+            form, exc = C.c_int32(), C.c_int64()
+            hip.check(hip.lib.mpg_sell_columns(sell, C.byref(form), C.byref(exc)))
+            if stepped == "1":
+                assert form.value == 2 and exc.value == (0 if kind == "wide" else 1), (form.value, exc.value)
+            else:
+                assert form.value == 0
+            dx = hip.buf(x.astype(xdt))
+            dy_sell, dy_csr = hip.buf(y0.astype(xdt)), hip.buf(y0.astype(xdt))
+            hip.call(f"mpg_sell_spmv_{name}", sell, xdt(alpha), dx.p, xdt(beta), dy_sell.p)
+            hip.call(f"mpg_csr_spmv_{name}", csr, xdt(alpha), dv.p, dx.p, xdt(beta), dy_csr.p)
+            if name == "f64":
+                scale = np.abs(y0) + abs(A.to_scipy()) @ np.abs(x)
+                assert np.all(np.abs(dy_sell.get() - dy_csr.get()) <= 4 * F64_EPS * scale), name
+            else:
+                assert np.array_equal(dy_sell.get(), dy_csr.get()), name
+    finally:
+        for h in sells:
+            hip.lib.mpg_sell_destroy(h)
+        hip.lib.mpg_csr_destroy(csr)
+
+
+@pytest.mark.parametrize("mode", ["mixed", "baseline", "mixed-half"])
+def test_stepped_columns_solve(mpg, oracle, mode, monkeypatch):
+    A = _wide(mpg)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode=mode, orth="cgs", prec="jacobi", rlen=30, tol=1e-9 if mode != "mixed-half" else 1e-6,
+                max_restarts=25)
+    got = {}
+    for st in ("1", "0"):
+        monkeypatch.setenv("MPG_SELL_STEPPED", st)
+        eng = mpg.Engine(A, b, xt, spmv_format="sell", **opts)
+        assert eng.spmv_layout()["col_bytes"] == (2 if st == "1" else 4)
+        eng.close()
+        got[st] = mpg.solve(A, b, xt, engine="fused", spmv_format="sell", **opts)
+    s, i = got["1"], got["0"]
+    assert s.status == i.status and s.total_iters == i.total_iters
+    assert np.array_equal(s.step_res, i.step_res) and np.array_equal(s.x, i.x)
+    if mode != "mixed-half":
+        ref = oracle.solve(mpg, A, b, xt, **opts)
+        compare(as_ref(ref), s, mode, opts["tol"], 30, f"stepped-{mode}")
+    else:
+        assert s.status == "converged" and s.backward_error[-1] <= opts["tol"]
+
+
+@pytest.mark.parametrize("xcd", ["1", "0"])
+def test_xcd_ordered_slices_match_oracle(mpg, oracle, xcd, monkeypatch):
+    """XCD-ordered slices (MPG_SELL_XCD) only change which workgroup sums
+    which rows: every row's sum is the same; the prologue's per-workgroup
+    norm partials group differently (last-bit changes in the norms)."""
+    monkeypatch.setenv("MPG_SELL_XCD", xcd)
+    A = mpg.gen_laplace3d(60)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    for mode in ("baseline", "mixed"):
+        opts = dict(mode=mode, orth="cgs", prec="identity", rlen=30, tol=1e-10, max_restarts=60)
+        got = mpg.solve(A, b, xt, engine="fused", **opts)
+        ref = oracle.solve(mpg, A, b, xt, **opts)
+        compare(as_ref(ref), got, mode, opts["tol"], 30, f"xcd{xcd}-{mode}")
+
+
+def test_stepped_exception_slice_solve(mpg, monkeypatch):
+    """The fused engine's Arnoldi SpMV and residual prologue on a stepped copy
+    with one CSR-summed slice: the same bits as the int32 copy."""
+    A = _far(mpg)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    for mode in ("mixed", "baseline"):
+        opts = dict(mode=mode, orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3)
+        got = {}
+        for st in ("1", "0"):
+            monkeypatch.setenv("MPG_SELL_STEPPED", st)
+            got[st] = mpg.solve(A, b, xt, engine="fused", spmv_format="sell", **opts)
+        assert got["1"].total_iters == got["0"].total_iters == 90
+        assert np.array_equal(got["1"].step_res, got["0"].step_res) and np.array_equal(got["1"].x, got["0"].x)

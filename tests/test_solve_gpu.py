@@ -264,3 +264,25 @@ def test_surface_cycle_program_matches_eager(mpg, orth, mode, prec, monkeypatch)
     assert p.status == e.status and p.total_iters == e.total_iters and p.restarts == e.restarts
     assert np.array_equal(p.step_res, e.step_res)
     assert p.res_norm == e.res_norm and p.err_norm == e.err_norm
+
+
+@pytest.mark.parametrize("mode", ["mixed", "single"])
+@pytest.mark.parametrize("orth", ["cgs", "cgsr"])
+def test_fused_dots_strict(mpg, oracle, mode, orth, monkeypatch):
+    """MPG_FUSE_DOTS=2 makes an unsupported fused SpMV + dots launch an
+    error instead of a silent fallback, so this case proves k_step_sell's
+    SellDots form ran (fp32 basis and values, int16 columns, LDS window:
+    BAND) and matches the oracle. The golden-suite engines use =1, which
+    falls back wherever the form does not apply."""
+    monkeypatch.setenv("MPG_CGS_PARTIALS", "1")
+    monkeypatch.setenv("MPG_FUSE_DOTS", "2")
+    A = mpg.gen_band(150_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=1e-9, max_restarts=40)
+    eng = mpg.Engine(A, b, xt, spmv_format="sell", **opts)
+    assert eng.spmv_layout()["col_bytes"] == 2 and eng.spmv_layout()["window"]
+    eng.close()
+    got = mpg.solve(A, b, xt, engine="fused", spmv_format="sell", **opts)
+    ref = oracle.solve(mpg, A, b, xt, **opts)
+    compare(as_ref(ref), got, mode, opts["tol"], 30, f"fused-dots-strict-{mode}-{orth}")
