@@ -105,6 +105,10 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_halo_analyze.argtypes = [_I32, _I32, P64, _I32, P32, P32, C.POINTER(C.c_void_p)]
     lib.mpg_halo_n_ext.argtypes = [C.c_void_p]
     lib.mpg_halo_n_ext.restype = _I32
+    lib.mpg_halo_n_front.argtypes = [C.c_void_p]
+    lib.mpg_halo_n_front.restype = _I32
+    lib.mpg_halo_recv_pos.argtypes = [C.c_void_p, _I32]
+    lib.mpg_halo_recv_pos.restype = _I32
     lib.mpg_halo_recv_count.argtypes = [C.c_void_p, _I32]
     lib.mpg_halo_recv_count.restype = _I32
     lib.mpg_halo_recv_rows.argtypes = [C.c_void_p, _I32, P64]
@@ -436,7 +440,17 @@ class HaloPlan:
 
     @property
     def n_ext(self) -> int:
+        """end of the local numbering: own rows [0, n), higher ranks' halo [n, n_ext)"""
         return int(self._lib.mpg_halo_n_ext(self._h))
+
+    @property
+    def n_front(self) -> int:
+        """lower ranks' halo rows, local ids [-n_front, 0)"""
+        return int(self._lib.mpg_halo_n_front(self._h))
+
+    def recv_pos(self, peer: int) -> int:
+        """local id of the first row received from `peer`"""
+        return int(self._lib.mpg_halo_recv_pos(self._h, peer))
 
     def recv_rows(self, peer: int) -> np.ndarray:
         cnt = self._lib.mpg_halo_recv_count(self._h, peer)

@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__
 // k_step_sell): r = b - A x (X), w = M(T(r)), partials ||T(r)||^2,
 // ||w||^2, ||x||^2 per workgroup.
 template <class T, class X, class P, class CI, int W, bool WIN>
-__global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_ext, int nslices, const int64_t* __restrict__ off,
+__global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                           const CI* __restrict__ col, const X* __restrict__ val,
                                                           const X* __restrict__ x, const X* __restrict__ b,
                                                           const P* __restrict__ diag, T* __restrict__ w,
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_ext, int 
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const int c = row0 - kWinLo + q * kWave + lane;
-            xr[q] = x[c >= 0 && c < n_ext ? c : 0];
+            xr[q] = x[c >= n_lo && c < n_ext ? c : 0];
         }
     }
     const int ic = own ? i : 0;
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_ext, int 
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int c = row0 - kWinLo + q * kWave + lane;
-                win[wid][q * kWave + lane] = (c >= 0 && c < n_ext) ? xr[q] : X(0);
+                win[wid][q * kWave + lane] = (c >= n_lo && c < n_ext) ? xr[q] : X(0);
             }
             wave_lds_sync();
             auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
@@ -439,7 +439,7 @@ struct SellDots {
 };
 
 template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD, int DN = 0>
-__global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nslices, const int64_t* __restrict__ off,
+__global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col,
                                                       const typename SellStore<VI>::type* __restrict__ val,
                                                       const T* __restrict__ wprev, const T* __restrict__ inv_p,
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const int c = row0 - kWinLo + q * kWave + lane;
-            wr[q] = wprev[c >= 0 && c < n_ext ? c : 0];
+            wr[q] = wprev[c >= n_lo && c < n_ext ? c : 0];
         }
     } else {
         wr[0] = wprev[i < n ? i : 0];
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_ext, int nsli
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int c = row0 - kWinLo + q * kWave + lane;
-                win[wid][q * kWave + lane] = (c >= 0 && c < n_ext) ? (T)(wr[q] * inv) : T(0);
+                win[wid][q * kWave + lane] = (c >= n_lo && c < n_ext) ? (T)(wr[q] * inv) : T(0);
             }
             wave_lds_sync();
             auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
@@ -1161,7 +1161,9 @@ struct mpg_arnoldi {
     void* V = nullptr;
     void* H = nullptr;      // (m+1) x m
     void* small = nullptr;  // cs, sn, s (m+1 each), inv, corr (m+1), coef scratch
-    void* w[2] = {nullptr, nullptr};
+    void* w[2] = {nullptr, nullptr};      // row 0 of each w buffer
+    void* wbase[2] = {nullptr, nullptr};  // the allocations: `front` entries before row 0
+    int front = 0;                        // MPG_FRONT_PAD(d.n_front)
     double* partial = nullptr;  // (kNC + 4) x G
     double* dpart = nullptr;    // kNC x Gd: one-panel dots partials (read by the CGS update that writes `partial`)
     double* sums = nullptr;     // m + 4
@@ -1268,6 +1270,11 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
     a->Grb = desc->A->nblocks > 0 ? desc->A->nblocks : 1;
     a->Gd = (int)std::min<int64_t>(kCombineGroups, std::max<int64_t>(1, ((int64_t)desc->n + 4 * kCombineBlock - 1) /
                                                                           (4 * kCombineBlock)));
+    if (desc->n_front < 0) {
+        delete a;
+        return MPG_ERR_ARG;
+    }
+    a->front = MPG_FRONT_PAD(desc->n_front);
     const size_t align = 256 / a->tsize;
     a->ld = ((int64_t)desc->n + align - 1) / align * align;
     if (a->ld == 0) a->ld = align;
@@ -1278,8 +1285,8 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
     };
     bool ok = alloc(&a->V, (size_t)a->ld * (m + 1) * a->tsize) && alloc(&a->H, (size_t)(m + 1) * m * a->tsize) &&
               alloc(&a->small, (size_t)6 * (m + 1) * a->tsize) &&
-              alloc(&a->w[0], (size_t)(desc->n_ext + 64) * a->tsize) &&
-              alloc(&a->w[1], (size_t)(desc->n_ext + 64) * a->tsize) &&
+              alloc(&a->wbase[0], (size_t)(a->front + desc->n_ext + 64) * a->tsize) &&
+              alloc(&a->wbase[1], (size_t)(a->front + desc->n_ext + 64) * a->tsize) &&
               alloc((void**)&a->partial, std::max<size_t>(std::max<size_t>((size_t)(kNC + 4) * a->Grb,
                                                                            (size_t)(m + 4) * a->G),
                                                           (size_t)kNC * kCombineGroups) *  // uniform groups
@@ -1288,6 +1295,8 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
               alloc((void**)&a->report, (size_t)(m + 8) * sizeof(double)) &&
               alloc((void**)&a->dpart, (size_t)kNC * kCombineGroups * sizeof(double)) &&
               alloc((void**)&a->counters, 256);
+    for (int q = 0; q < 2; ++q)
+        a->w[q] = a->wbase[q] ? static_cast<char*>(a->wbase[q]) + (size_t)a->front * a->tsize : nullptr;
     if (!ok) {
         mpg_arnoldi_destroy(a);
         return MPG_ERR_ALLOC;
@@ -1326,7 +1335,7 @@ int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width
 int mpg_arnoldi_destroy(mpg_arnoldi_t a) {
     if (!a) return MPG_OK;
     if (a->ctx) (void)hipStreamSynchronize(a->ctx->stream);
-    void* ps[] = {a->V, a->H, a->small, a->w[0], a->w[1], a->partial, a->dpart, a->sums, a->report,
+    void* ps[] = {a->V, a->H, a->small, a->wbase[0], a->wbase[1], a->partial, a->dpart, a->sums, a->report,
                   a->counters, a->fd_part, a->fd_cnt};
     for (void* p : ps)
         if (p) (void)hipFree(p);
@@ -1353,7 +1362,7 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
                 return sell_dispatch_win(S->win, [&](auto wn) {
                     k_prologue_sell<T, X, P, CI, decltype(wc)::value, decltype(wn)::value>
                         <<<grid, kBlock, 0, a->ctx->stream>>>(
-                            a->d.n, a->d.n_ext, S->nslices, S->off, static_cast<const CI*>(S->col),
+                            a->d.n, -a->front, a->d.n_ext, S->nslices, S->off, static_cast<const CI*>(S->col),
                             static_cast<const X*>(S->val), static_cast<const X*>(a->d.x),
                             static_cast<const X*>(a->d.b), diag, static_cast<T*>(a->w[0]), a->partial, S->sbase,
                             S->sexc, A->rowptr, A->col, static_cast<const X*>(a->d.val_outer),
@@ -1441,7 +1450,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                 const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
                 auto launch = [&](auto kern, SellDots dd) {
                     launch_timed(a->ctx, kern, dim3(grid), dim3(kBlock),
-                            a->d.n, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
+                            a->d.n, -a->front, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
                             static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd,

@@ -22,13 +22,20 @@
 #include "gmres.hpp"
 #include "types_hip.hpp"
 
+// Local numbering of one rank's vector (x, w): its own rows at [0, n_local),
+// the halo rows owned by LOWER ranks in front of them at [-n_front, 0), the
+// rest after them at [n_local, n_ext). A banded matrix's first rows then
+// read columns -5..-1 rather than ~n_local, so every slice of the block stays
+// within the int16 SELL form and the LDS window.
 struct mpg_halo {
     int rank = 0, nranks = 1;
     std::vector<int64_t> row_starts;
     int n_local = 0;
+    int n_front = 0;                              // halo rows of lower ranks
     std::vector<int32_t> col_local;
     std::vector<int64_t> halo_global;             // sorted external columns
-    std::vector<int32_t> recv_off, recv_cnt;      // per peer, into the halo segment
+    std::vector<int32_t> recv_off, recv_cnt;      // per peer, into halo_global
+    std::vector<int32_t> recv_pos;                // per peer, local id of its first row
     std::vector<std::vector<int32_t>> send_local; // per peer, local rows to send
     std::vector<bool> send_set;
 };
@@ -48,14 +55,14 @@ class RcclComm : public Comm {
     ncclComm_t comm_ = nullptr;
     int rank_, size_, n_local_;
     mpg_ctx_t ctx_;
-    std::vector<int32_t> recv_off_, recv_cnt_;
+    std::vector<int32_t> recv_pos_, recv_cnt_;
     std::vector<std::unique_ptr<DevMem>> send_idx_, send_buf_;
     std::vector<int32_t> send_cnt_;
     std::vector<int32_t> send_first_;  // >= 0: the rows sent to q are [first, first + cnt) (sent in place, no pack)
 
 public:
     RcclComm(mpg_ctx_t ctx, const mpg_halo& h, const char* id, int nranks, int rank)
-        : rank_(rank), size_(nranks), n_local_(h.n_local), ctx_(ctx), recv_off_(h.recv_off), recv_cnt_(h.recv_cnt) {
+        : rank_(rank), size_(nranks), n_local_(h.n_local), ctx_(ctx), recv_pos_(h.recv_pos), recv_cnt_(h.recv_cnt) {
         ncclUniqueId uid;
         std::memcpy(&uid, id, sizeof uid);
         nck(ncclCommInitRank(&comm_, nranks, uid, rank), "ncclCommInitRank");
@@ -114,7 +121,7 @@ private:
                 nck(ncclSend(src, (size_t)send_cnt_[q] * eb, ncclUint8, q, comm_, s), "send");
             }
             if (recv_cnt_[q]) {
-                char* dst = static_cast<char*>(vec) + ((size_t)n_local_ + recv_off_[q]) * eb;
+                char* dst = static_cast<char*>(vec) + (ptrdiff_t)recv_pos_[q] * eb;
                 nck(ncclRecv(dst, (size_t)recv_cnt_[q] * eb, ncclUint8, q, comm_, s), "recv");
             }
         }
@@ -157,12 +164,13 @@ class LoopbackComm : public Comm {
     Hub& hub_;
     int rank_, n_local_;
     mpg_ctx_t ctx_;
-    std::vector<int32_t> recv_off_, recv_cnt_;
+    std::vector<int32_t> recv_off_, recv_pos_, recv_cnt_;
     std::vector<std::unique_ptr<DevMem>> src_idx_;  // per peer: indices in the peer's numbering
 
 public:
     LoopbackComm(Hub& hub, mpg_ctx_t ctx, const mpg_halo& h)
-        : hub_(hub), rank_(h.rank), n_local_(h.n_local), ctx_(ctx), recv_off_(h.recv_off), recv_cnt_(h.recv_cnt) {
+        : hub_(hub), rank_(h.rank), n_local_(h.n_local), ctx_(ctx), recv_off_(h.recv_off), recv_pos_(h.recv_pos),
+          recv_cnt_(h.recv_cnt) {
         src_idx_.resize(h.nranks);
         for (int q = 0; q < h.nranks; ++q) {
             if (!recv_cnt_[q]) continue;
@@ -184,7 +192,7 @@ public:
         hub_.barrier();
         for (int q = 0; q < hub_.P; ++q) {
             if (!recv_cnt_[q]) continue;
-            char* dst = static_cast<char*>(vec) + ((size_t)n_local_ + recv_off_[q]) * eb;
+            char* dst = static_cast<char*>(vec) + (ptrdiff_t)recv_pos_[q] * eb;
             const int st = eb == 8 ? mpg_gather_b64(ctx_, recv_cnt_[q], src_idx_[q]->as<int32_t>(), hub_.ptrs[q], dst)
                                    : mpg_gather_b32(ctx_, recv_cnt_[q], src_idx_[q]->as<int32_t>(), hub_.ptrs[q], dst);
             check(st, "loopback halo", ctx_);
@@ -221,7 +229,7 @@ class HostComm : public Comm {
     mpg_host_transport t_;
     int rank_, size_, n_local_;
     mpg_ctx_t ctx_;
-    std::vector<int32_t> recv_off_, recv_cnt_, send_cnt_;
+    std::vector<int32_t> recv_pos_, recv_cnt_, send_cnt_;
     std::vector<std::unique_ptr<DevMem>> send_idx_, send_dev_;
     std::vector<std::vector<char>> send_host_, recv_host_;
     std::vector<double> red_;
@@ -232,7 +240,7 @@ class HostComm : public Comm {
 
 public:
     HostComm(mpg_ctx_t ctx, const mpg_halo& h, const mpg_host_transport& t, int nranks, int rank)
-        : t_(t), rank_(rank), size_(nranks), n_local_(h.n_local), ctx_(ctx), recv_off_(h.recv_off),
+        : t_(t), rank_(rank), size_(nranks), n_local_(h.n_local), ctx_(ctx), recv_pos_(h.recv_pos),
           recv_cnt_(h.recv_cnt) {
         send_cnt_.assign(nranks, 0);
         send_idx_.resize(nranks);
@@ -277,7 +285,7 @@ public:
         call(t_.exchange(t_.user, send.data(), sb.data(), recv.data(), rb.data()), "exchange");
         for (int q = 0; q < size_; ++q)
             if (rb[q]) {
-                char* dst = static_cast<char*>(vec) + ((size_t)n_local_ + recv_off_[q]) * eb;
+                char* dst = static_cast<char*>(vec) + (ptrdiff_t)recv_pos_[q] * eb;
                 hck(hipMemcpyAsync(dst, recv[q], (size_t)rb[q], hipMemcpyHostToDevice, s), "h2d");
             }
         hck(hipStreamSynchronize(s), "sync");
@@ -334,6 +342,11 @@ int mpg_halo_analyze(int32_t rank, int32_t nranks, const int64_t* row_starts, in
     }
     std::sort(h->halo_global.begin(), h->halo_global.end());
     h->halo_global.erase(std::unique(h->halo_global.begin(), h->halo_global.end()), h->halo_global.end());
+    h->n_front = (int)(std::lower_bound(h->halo_global.begin(), h->halo_global.end(), r0) - h->halo_global.begin());
+    // local id of the t-th halo row: the lower ones in front of row 0
+    auto local_of = [&](int64_t t) {
+        return t < h->n_front ? (int32_t)(t - h->n_front) : (int32_t)(n_local + (t - h->n_front));
+    };
     h->col_local.resize((size_t)nnz);
     for (int64_t k = 0; k < nnz; ++k) {
         const int64_t c = col_global[k];
@@ -341,16 +354,18 @@ int mpg_halo_analyze(int32_t rank, int32_t nranks, const int64_t* row_starts, in
             h->col_local[(size_t)k] = (int32_t)(c - r0);
         } else {
             const auto it = std::lower_bound(h->halo_global.begin(), h->halo_global.end(), c);
-            h->col_local[(size_t)k] = n_local + (int32_t)(it - h->halo_global.begin());
+            h->col_local[(size_t)k] = local_of(it - h->halo_global.begin());
         }
     }
     h->recv_off.assign(nranks, 0);
     h->recv_cnt.assign(nranks, 0);
+    h->recv_pos.assign(nranks, 0);
     size_t pos = 0;
     for (int q = 0; q < nranks; ++q) {
         h->recv_off[q] = (int32_t)pos;
         while (pos < h->halo_global.size() && h->halo_global[pos] < row_starts[q + 1]) ++pos;
         h->recv_cnt[q] = (int32_t)(pos - h->recv_off[q]);
+        h->recv_pos[q] = local_of(h->recv_off[q]);
     }
     h->send_local.assign(nranks, {});
     h->send_set.assign(nranks, false);
@@ -359,7 +374,13 @@ int mpg_halo_analyze(int32_t rank, int32_t nranks, const int64_t* row_starts, in
     return MPG_OK;
 }
 
-int32_t mpg_halo_n_ext(mpg_halo_t h) { return h ? h->n_local + (int32_t)h->halo_global.size() : -1; }
+int32_t mpg_halo_n_ext(mpg_halo_t h) {
+    return h ? h->n_local + (int32_t)h->halo_global.size() - h->n_front : -1;
+}
+int32_t mpg_halo_n_front(mpg_halo_t h) { return h ? h->n_front : -1; }
+int32_t mpg_halo_recv_pos(mpg_halo_t h, int32_t q) {
+    return h && q >= 0 && q < h->nranks ? h->recv_pos[q] : INT32_MIN;
+}
 int32_t mpg_halo_recv_count(mpg_halo_t h, int32_t q) {
     return h && q >= 0 && q < h->nranks ? h->recv_cnt[q] : -1;
 }
@@ -413,7 +434,7 @@ int mpg_engine_create_dist(const mpg_solve_args* a, mpg_halo_t plan, const char*
         e->comm = std::make_unique<RcclComm>(e->ctx, *plan, id, nranks, rank);
         mpg_solve_args local = *a;
         local.col = plan->col_local.data();
-        e->eng = std::make_unique<FusedEngine>(e->ctx, local, e->comm.get(), mpg_halo_n_ext(plan));
+        e->eng = std::make_unique<FusedEngine>(e->ctx, local, e->comm.get(), mpg_halo_n_ext(plan), plan->n_front);
     } catch (const std::exception& ex) {
         if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", ex.what());
         mpg_engine_destroy(e);
@@ -442,7 +463,7 @@ int mpg_engine_create_dist_host(const mpg_solve_args* a, mpg_halo_t plan, const 
         e->comm = std::make_unique<HostComm>(e->ctx, *plan, *t, nranks, rank);
         mpg_solve_args local = *a;
         local.col = plan->col_local.data();
-        e->eng = std::make_unique<FusedEngine>(e->ctx, local, e->comm.get(), mpg_halo_n_ext(plan));
+        e->eng = std::make_unique<FusedEngine>(e->ctx, local, e->comm.get(), mpg_halo_n_ext(plan), plan->n_front);
     } catch (const std::exception& ex) {
         if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", ex.what());
         mpg_engine_destroy(e);
@@ -500,7 +521,7 @@ int mpg_solve_loopback(const mpg_solve_args* a, int32_t P, mpg_solve_result* r) 
                     la.b = a->b + r0;
                     la.x_true = a->x_true ? a->x_true + r0 : nullptr;
                     if (q != 0) la.verbose = 0;
-                    FusedEngine e(ctx, la, &comm, mpg_halo_n_ext(plans[q]));
+                    FusedEngine e(ctx, la, &comm, mpg_halo_n_ext(plans[q]), plans[q]->n_front);
                     bool done = false;
                     while (!done) e.run(1 << 20, done);
                     e.sync();

@@ -90,6 +90,8 @@ struct FusedEngine::Impl {
     Comm* comm = nullptr;
     ModeTypes ty{};
     int n = 0, n_ext = 0, m = 0, orth = 0;
+    int front = 0;       // MPG_FRONT_PAD(n_front): entries of x / x64 before row 0
+    void* xp = nullptr;  // row 0 of x (x.p + front entries)
     int64_t nnz = 0;
     DevMem rowptr, col, val64, val_outer_own, val_inner_own, diag, b, x, tmp_t, tmp_p, scal;
     const void* val_outer = nullptr;
@@ -176,7 +178,8 @@ struct FusedEngine::Impl {
     }
 };
 
-FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int n_ext) : p_(new Impl) {
+FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int n_ext, int n_front)
+    : p_(new Impl) {
     auto t0 = clk::now();
     Impl& I = *p_;
     I.ctx = ctx;
@@ -185,6 +188,8 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     I.ty = types_for(a.mode);
     I.n = a.n;
     I.n_ext = n_ext < 0 ? a.n : n_ext;
+    if (n_front < 0) throw std::invalid_argument("n_front < 0");
+    I.front = MPG_FRONT_PAD(n_front);
     I.m = a.rlen;
     I.orth = a.orth;
     I.nnz = a.nnz;
@@ -264,7 +269,8 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
         I.b = DevMem(ctx, (size_t)I.n * 4 + 8);
         I.cast(b64.p, MPG_F64, I.b.p, MPG_F32, I.n);
     }
-    I.x = DevMem(ctx, (size_t)I.n_ext * dsize(ty.X) + 64);
+    I.x = DevMem(ctx, (size_t)(I.front + I.n_ext) * dsize(ty.X) + 64);
+    I.xp = static_cast<char*>(I.x.p) + (size_t)I.front * dsize(ty.X);
 
     // one-time norms of the drivers (gmres.cpp:51-58, 162-168)
     b_norm = I.nrm2(I.b.p, ty.X, I.n);
@@ -316,8 +322,9 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     d.val_inner = I.val_inner;
     d.diag = d.jacobi ? I.diag.p : nullptr;
     d.b = I.b.p;
-    d.x = I.x.p;
+    d.x = I.xp;
     d.spmv_format = a.spmv_format;
+    d.n_front = n_front;
     check(mpg_arnoldi_create(ctx, &d, &I.arn), "mpg_arnoldi_create", ctx);
     // ranks all-reduce per-workgroup partials in place: same count on every rank
     if (comm) check(mpg_arnoldi_uniform_groups(I.arn), "uniform groups", ctx);
@@ -327,7 +334,7 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     for (hipEvent_t& e : I.report_ev) hipck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
     const char* qenv = std::getenv("MPG_PIPELINE");  // 0: read each cycle's report before the next launch
     I.pipeline = !(qenv && *qenv == '0');
-    if (I.pipeline) I.x_snap = DevMem(ctx, (size_t)I.n_ext * dsize(ty.X) + 64);
+    if (I.pipeline) I.x_snap = DevMem(ctx, I.x.bytes);
 
     // convergence strategy (gmres_perf_test.cpp:185-196)
     const size_t mm = (size_t)a.rlen, mr = (size_t)a.max_restarts;
@@ -381,7 +388,7 @@ void FusedEngine::sync() { check(mpg_ctx_sync(p_->ctx), "sync", p_->ctx); }
 
 void FusedEngine::prologue() {
     Impl& I = *p_;
-    if (I.comm) I.comm->halo(I.x.p, (int)dsize(I.ty.X), I.stream());
+    if (I.comm) I.comm->halo(I.xp, (int)dsize(I.ty.X), I.stream());
     timed(1, [&] { check(mpg_arnoldi_prologue(I.arn), "prologue", I.ctx); });
     check(mpg_arnoldi_prologue(I.arn), "prologue", I.ctx);
     if (I.ilu) {  // w = M(T(r)) outside the kernel, then ||w||^2 again
@@ -735,20 +742,20 @@ void FusedEngine::finish_report(mpg_solve_result* r) {
     Impl& I = *p_;
     const int n = I.n;
     // x and b widened to fp64 (DoBaselineProblem copies x_type / b_type to double)
-    DevMem x64(I.ctx, (size_t)I.n_ext * 8 + 8), r64(I.ctx, (size_t)n * 8 + 8), b64(I.ctx, (size_t)n * 8 + 8);
-    I.cast(I.x.p, I.ty.X, x64.p, MPG_F64, n);
+    DevMem x64m(I.ctx, (size_t)(I.front + I.n_ext) * 8 + 8), r64(I.ctx, (size_t)n * 8 + 8), b64(I.ctx, (size_t)n * 8 + 8);
+    double* x64 = x64m.as<double>() + I.front;  // row 0
+    I.cast(I.xp, I.ty.X, x64, MPG_F64, n);
     I.cast(I.b.p, I.ty.X, b64.p, MPG_F64, n);
-    if (r->x_out) check(mpg_memcpy_d2h(I.ctx, r->x_out, x64.p, (size_t)n * 8), "d2h", I.ctx);
-    if (I.comm) I.comm->halo(x64.p, 8, I.stream());
+    if (r->x_out) check(mpg_memcpy_d2h(I.ctx, r->x_out, x64, (size_t)n * 8), "d2h", I.ctx);
+    if (I.comm) I.comm->halo(x64, 8, I.stream());
     check(mpg_memcpy_d2d(I.ctx, r64.p, b64.p, (size_t)n * 8), "d2d", I.ctx);
-    check(mpg_csr_spmv_f64(I.ctx, I.csr, -1.0, I.val64.as<double>(), x64.as<double>(), 1.0, r64.as<double>()), "spmv",
-          I.ctx);
+    check(mpg_csr_spmv_f64(I.ctx, I.csr, -1.0, I.val64.as<double>(), x64, 1.0, r64.as<double>()), "spmv", I.ctx);
     r->res_norm = std::sqrt(I.dot_acc(r64.p, r64.p, MPG_F64, n));
     if (I.args.x_true) {
         DevMem xt(I.ctx, (size_t)n * 8 + 8);
         check(mpg_memcpy_h2d(I.ctx, xt.p, I.args.x_true, (size_t)n * 8), "h2d", I.ctx);
-        check(mpg_axpy_f64(I.ctx, n, -1.0, xt.as<double>(), x64.as<double>()), "axpy", I.ctx);
-        r->err_norm = std::sqrt(I.dot_acc(x64.p, x64.p, MPG_F64, n));
+        check(mpg_axpy_f64(I.ctx, n, -1.0, xt.as<double>(), x64), "axpy", I.ctx);
+        r->err_norm = std::sqrt(I.dot_acc(x64, x64, MPG_F64, n));
     }
 }
 

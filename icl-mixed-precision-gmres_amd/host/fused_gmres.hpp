@@ -35,7 +35,8 @@ public:
     // in-place sum / max of `count` doubles across ranks (bit-identical on every rank)
     virtual void allreduce_sum(double* dev, int count, hipStream_t s) = 0;
     virtual void allreduce_max(double* dev, int count, hipStream_t s) = 0;
-    // fill the halo tail [n, n_ext) of a vector of `elem_bytes` elements
+    // fill the halo entries [-n_front, 0) and [n, n_ext) of a vector of
+    // `elem_bytes` elements (passed as a pointer to its row 0)
     virtual void halo(void* dev_vec, int elem_bytes, hipStream_t s) = 0;
     // allreduce_sum and halo together (independent inputs): one RCCL group,
     // i.e. one collective launch per Arnoldi step instead of two
@@ -67,7 +68,8 @@ public:
     // `rows`/`halo` describe the local row block of a partitioned matrix
     // (global columns already remapped to [0, n_ext)); a single GPU passes the
     // whole matrix and no communicator.
-    FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& args, Comm* comm = nullptr, int n_ext = -1);
+    // n_front: halo rows of lower ranks, local ids [-n_front, 0) (dist.h)
+    FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& args, Comm* comm = nullptr, int n_ext = -1, int n_front = 0);
     ~FusedEngine();
 
     // Advance the solve by up to max_cycles outer iterations; returns the

@@ -55,14 +55,21 @@ typedef struct {
     int32_t prec_type;     /* P: preconditioner arithmetic (MPG_F64 | MPG_F32) */
     int32_t inner_val;     /* value type of the Arnoldi SpMV (MPG_F64 | MPG_F32 | MPG_F16) */
     int32_t jacobi;        /* 1: w = d∘w (gdmv), 0: identity */
-    mpg_csr_t A;           /* analysed local CSR, columns in [0, n_ext) */
+    mpg_csr_t A;           /* analysed local CSR, columns in [-n_front, n_ext) */
     const void* val_outer; /* residual values, outer_type */
     const void* val_inner; /* Arnoldi values, inner_val */
     const void* diag;      /* Jacobi inverse diagonal (prec_type) or NULL */
     const void* b;         /* outer_type, n */
-    void* x;               /* outer_type, n_ext (halo tail filled by the caller) */
+    void* x;               /* outer_type, row 0 of [-MPG_FRONT_PAD(n_front), n_ext) (halo filled by the caller) */
     int32_t spmv_format;   /* Arnoldi SpMV storage: 0 auto, 1 CSR row blocks, 2 sliced ELL (SELL-64) */
+    int32_t n_front;       /* halo rows of lower ranks, local ids [-n_front, 0) (0 on one GPU) */
 } mpg_arnoldi_desc;
+
+/* Entries allocated in front of row 0 of every vector with a halo (x, the
+ * w buffers): the lower halo rounded up to 64, plus the 64 rows the first
+ * slice's LDS window reads below row 0 (vectors are passed as a pointer to
+ * row 0; mpg_halo_n_front, dist.h). */
+#define MPG_FRONT_PAD(n_front) ((n_front) > 0 ? ((n_front) + 63) / 64 * 64 + 64 : 0)
 
 /* Allocates the basis V (n x (m+1), leading dimension padded to 256 B),
  * H, Givens state, two w buffers (n_ext), partials and the report block. */

@@ -47,7 +47,14 @@ typedef struct mpg_halo* mpg_halo_t;
  * n_local rows with global column ids (sorted per row). */
 int mpg_halo_analyze(int32_t rank, int32_t nranks, const int64_t* row_starts, int32_t n_local,
                      const int32_t* rowptr, const int32_t* col_global, mpg_halo_t* out);
+/* Local numbering (columns and vector layout): own rows [0, n_local), halo
+ * rows of lower ranks [-n_front, 0), halo rows of higher ranks
+ * [n_local, n_ext); a vector with halo spans n_front + n_ext entries, its
+ * row 0 at entry n_front. */
 int32_t mpg_halo_n_ext(mpg_halo_t h);
+int32_t mpg_halo_n_front(mpg_halo_t h);
+/* local id of the first row received from `peer` (its rows are consecutive) */
+int32_t mpg_halo_recv_pos(mpg_halo_t h, int32_t peer);
 int32_t mpg_halo_recv_count(mpg_halo_t h, int32_t peer);
 /* global ids (ascending) of the rows this rank needs from `peer` */
 int mpg_halo_recv_rows(mpg_halo_t h, int32_t peer, int64_t* rows_out);

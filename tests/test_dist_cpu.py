@@ -52,7 +52,8 @@ def _halo(x_ext, n_loc, r0, plan, sends, rank, world, transport):
     buffers and byte counts."""
     import ctypes as C
 
-    send_arrs = {q: np.ascontiguousarray(x_ext[sends[q] - r0]) for q in range(world) if q != rank and len(sends[q])}
+    f = plan.n_front
+    send_arrs = {q: np.ascontiguousarray(x_ext[f + sends[q] - r0]) for q in range(world) if q != rank and len(sends[q])}
     sizes = {q: 8 * len(plan.recv_rows(q)) for q in range(world) if q != rank}
     recv_arrs = {q: np.zeros(sizes[q] // 8) for q in sizes if sizes[q]}
     send = (C.c_void_p * world)(*[send_arrs[q].ctypes.data if q in send_arrs else None for q in range(world)])
@@ -60,14 +61,10 @@ def _halo(x_ext, n_loc, r0, plan, sends, rank, world, transport):
     recv = (C.c_void_p * world)(*[recv_arrs[q].ctypes.data if q in recv_arrs else None for q in range(world)])
     rb = (C.c_int64 * world)(*[sizes.get(q, 0) for q in range(world)])
     assert transport.c.exchange(None, send, sb, recv, rb) == 0, transport.error
-    off = n_loc
     for q in range(world):
-        if q == rank:
-            continue
-        cnt = sizes[q] // 8
-        if cnt:
-            x_ext[off:off + cnt] = recv_arrs[q]
-        off += cnt
+        if q != rank and sizes[q]:
+            o = plan.n_front + plan.recv_pos(q)  # x_ext holds the front halo first
+            x_ext[o:o + sizes[q] // 8] = recv_arrs[q]
 
 
 def _allreduce(v, transport):
@@ -98,15 +95,18 @@ def _worker(rank, world, port, N, out_q):
         assert np.array_equal(B.col, A_loc.col) and np.array_equal(B.val, A_loc.val)
         plan = mpg.HaloPlan(rank, world, starts, A_loc)
         sends = _exchange(plan, rank, world)
-        n_loc, n_ext = r1 - r0, plan.n_ext
-        cols = plan.local_cols()
+        # local numbering: lower ranks' halo at [-f, 0), own rows, higher
+        # ranks' halo at [n_loc, n_ext); x_ext stores it from -f
+        n_loc, n_ext, f = r1 - r0, plan.n_ext, plan.n_front
+        assert (f > 0) == (rank > 0)
+        cols = plan.local_cols() + f
         import scipy.sparse as sp
 
-        S = sp.csr_matrix((A_loc.val, cols, A_loc.rowptr), shape=(n_loc, n_ext))
+        S = sp.csr_matrix((A_loc.val, cols, A_loc.rowptr), shape=(n_loc, f + n_ext))
         S.has_sorted_indices = True  # keep the file's per-row order (= global order)
         x = mpg.rand_vect(N, 42)
-        x_ext = np.zeros(n_ext)
-        x_ext[:n_loc] = x[r0:r1]
+        x_ext = np.zeros(f + n_ext)
+        x_ext[f:f + n_loc] = x[r0:r1]
         _halo(x_ext, n_loc, r0, plan, sends, rank, world, transport)
         y = np.array([np.sum(A_loc.val[A_loc.rowptr[i]:A_loc.rowptr[i + 1]]
                              * x_ext[cols[A_loc.rowptr[i]:A_loc.rowptr[i + 1]]]) for i in range(n_loc)])
@@ -121,8 +121,8 @@ def _worker(rank, world, port, N, out_q):
         beta = np.sqrt(_allreduce([b @ b], transport)[0])
         V[:, 0] = b / beta
         for k in range(m):
-            v_ext = np.zeros(n_ext)
-            v_ext[:n_loc] = V[:, k]
+            v_ext = np.zeros(f + n_ext)
+            v_ext[f:f + n_loc] = V[:, k]
             _halo(v_ext, n_loc, r0, plan, sends, rank, world, transport)
             w = S @ v_ext
             h = _allreduce(V[:, :k + 1].T @ w, transport)
@@ -185,11 +185,18 @@ def test_halo_plan_single_process(mpg):
     A = mpg.gen_band(1000, 5, 4, seed=1)
     starts = np.array([0, 300, 700, 1000])
     plans = [mpg.HaloPlan(r, 3, starts, mpg.row_slice(A, starts[r], starts[r + 1])) for r in range(3)]
-    # middle rank needs 5 rows below and 4 above its block
+    # middle rank needs 5 rows below and 4 above its block: the lower ones
+    # get local ids -5..-1 (in front of its rows), the upper ones 400..403
     assert list(plans[1].recv_rows(0)) == list(range(295, 300))
     assert list(plans[1].recv_rows(2)) == list(range(700, 704))
-    assert plans[1].n_ext == 400 + 9
+    assert plans[1].n_front == 5 and plans[1].n_ext == 400 + 4
+    assert plans[1].recv_pos(0) == -5 and plans[1].recv_pos(2) == 400
+    assert plans[0].n_front == 0 and plans[0].recv_pos(1) == 300
     cols = plans[1].local_cols()
-    assert cols.min() == 0 and cols.max() == 408
+    assert cols.min() == -5 and cols.max() == 403
+    # global column c of the block's rows maps to c - 300 for every c: banded
+    # rows keep their offsets, so slices stay within int16 and the LDS window
+    A1 = mpg.row_slice(A, 300, 700)
+    assert np.array_equal(cols, A1.col - 300)
     with pytest.raises(ValueError):
         plans[1].set_send(0, [10])  # row 10 is not owned by rank 1
