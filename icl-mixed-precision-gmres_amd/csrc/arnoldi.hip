@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
                                                           const P* __restrict__ diag, T* __restrict__ w,
                                                           double* __restrict__ partial,
                                                           const int32_t* __restrict__ sbase,
-                                                          const uint8_t* __restrict__ sexc,
+                                                          const int32_t* __restrict__ spat, const CI* __restrict__ pat,
                                                           const int32_t* __restrict__ rowptr,
                                                           const int32_t* __restrict__ ccol,
                                                           const X* __restrict__ cval, int xcd) {
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
     const int i = row0 + lane;
     const bool own = live && i < n;
     SellRow<X, CI, W, true> row;  // once per cycle: non-temporal slices
-    row.init_load(live ? s : 0, off, sexc);
+    row.init_load(live ? s : 0, off, spat);
     __builtin_amdgcn_sched_barrier(0);
     X xr[WIN ? NQ : 1];
     if constexpr (WIN) {
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
     const X bi = b[ic], xi = x[ic];
     const P di = diag ? diag[ic] : P(0);
     __builtin_amdgcn_sched_barrier(0);
-    row.init_finish(lane, col, val, sbase);
+    row.init_finish(lane, col, val, sbase, pat);
     row.load(0);
     __builtin_amdgcn_sched_barrier(0);
     double sum = 0.0;
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_lo, int n_ext
                                                       const P* __restrict__ diag, T* __restrict__ w,
                                                       GivensFold<T> fold, SellDots dd,
                                                       const int32_t* __restrict__ sbase,
-                                                      const uint8_t* __restrict__ sexc,
+                                                      const int32_t* __restrict__ spat, const CI* __restrict__ pat,
                                                       const int32_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ ccol,
                                                       const typename SellStore<VI>::type* __restrict__ cval, int xcd) {
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_lo, int n_ext
     const int i = row0 + lane;
     // 0. the slice's offsets
     SellRow<S, CI, W> row;
-    row.init_load(live ? s : 0, off, sexc);
+    row.init_load(live ? s : 0, off, spat);
     __builtin_amdgcn_sched_barrier(0);
     // 1. the fold's ||w||^2 partial (nparts <= kBlock, checked at launch: one per lane)
     double part = 0.0;
@@ -483,16 +483,18 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_lo, int n_ext
     }
     __builtin_amdgcn_sched_barrier(0);
     // 3. the slice's first batch
-    row.init_finish(lane, col, val, sbase);
+    row.init_finish(lane, col, val, sbase, pat);
     row.load(0);
     __builtin_amdgcn_sched_barrier(0);
     // the scale 1/h_{k,k-1}: the folded Givens step, or the Givens kernel's
     T inv;
+    // the folded step's ||w||^2; workgroup 0 runs the rotation step with it
+    // after its own rows (nothing in this launch reads what the rotation
+    // writes, and its serial chain then holds none of the slice's loads live)
+    double nrm2sq = 0.0;
     if constexpr (FOLD) {
-        __shared__ T col_s[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
         __shared__ double scratch[kBlock / kWave];
         __shared__ T inv_s;
-        double nrm2sq;
         if (fold.nparts > 0) {
             const double v = wave_sum(part + 0.0);  // the same fixed order in every workgroup
             if (lane == 0) scratch[wid] = v;
@@ -505,13 +507,14 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_lo, int n_ext
             nrm2sq = fold.norm2[0];
         }
         if (threadIdx.x == 0) inv_s = inv_of_norm2<T>(nrm2sq);
-        if (blockIdx.x == 0) givens_block(fold.g, nrm2sq, col_s, c_s, s_s);
         lds_barrier();
         inv = inv_s;
     } else {
         inv = *inv_p;
     }
-    if (DN == 0 && !live) return;  // with dots, a dead wave joins the partials' barriers
+    // with dots, a dead wave joins the partials' barriers; with the fold,
+    // workgroup 0's waves all join the rotation step's barriers at the end
+    if (DN == 0 && !live && !(FOLD && blockIdx.x == 0)) return;
     double sum = 0.0;
     T vk = T(0);  // v_k(i) = T(w_prev(i) * inv)
     if (live) {
@@ -577,6 +580,10 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_lo, int n_ext
             for (int m = m0; m < m1; ++m) v += dd.wgpart[(size_t)c * gridDim.x + m];
             dd.out[(size_t)c * dd.ng + g] = v;
         }
+    }
+    if constexpr (FOLD) {
+        __shared__ T col_s[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
+        if (blockIdx.x == 0) givens_block(fold.g, nrm2sq, col_s, c_s, s_s);
     }
 }
 
@@ -1314,10 +1321,16 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
     return MPG_OK;
 }
 
-int64_t mpg_arnoldi_sell_meta_bytes(mpg_arnoldi_t a) {
+int64_t mpg_arnoldi_sell_matrix_bytes(mpg_arnoldi_t a) {
     if (!a || a->sell.nslices == 0) return 0;
-    const int64_t steps = a->sell.padded / ((int64_t)kWave * a->sell.W);
-    return ((int64_t)a->sell.nslices + 1) * 8 + (a->sell.c16s ? steps * 4 : 0);
+    const SellCopy& S = a->sell;
+    const int64_t vbytes = S.vtype == MPG_F64 ? 8 : S.vtype == MPG_F32 ? 4 : 2;
+    const int64_t steps = S.padded / ((int64_t)kWave * S.W);
+    // every slot's value; the columns of slots outside implicit slices (the
+    // shared patterns are a few cache lines); int64 slice offsets; the
+    // pattern indices; the stepped form's bases
+    return S.padded * vbytes + (S.padded - S.imp_slots) * S.col_bytes() + S.npat * S.col_bytes() +
+           ((int64_t)S.nslices + 1) * 8 + (S.spat ? (int64_t)S.nslices * 4 : 0) + (S.c16s ? steps * S.W * 4 : 0);
 }
 
 int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
@@ -1365,7 +1378,7 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
                             a->d.n, -a->front, a->d.n_ext, S->nslices, S->off, static_cast<const CI*>(S->col),
                             static_cast<const X*>(S->val), static_cast<const X*>(a->d.x),
                             static_cast<const X*>(a->d.b), diag, static_cast<T*>(a->w[0]), a->partial, S->sbase,
-                            S->sexc, A->rowptr, A->col, static_cast<const X*>(a->d.val_outer),
+                            S->spat, static_cast<const CI*>(S->pat), A->rowptr, A->col, static_cast<const X*>(a->d.val_outer),
                             sell_xcd_order(*S) ? 1 : 0);
                     return (int)MPG_OK;
                 });
@@ -1454,7 +1467,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
                             static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd,
-                            S.sbase, S.sexc, A->rowptr, A->col,
+                            S.sbase, S.spat, static_cast<const CI*>(S.pat), A->rowptr, A->col,
                             static_cast<const typename SellStore<VI>::type*>(a->d.val_inner),
                             sell_xcd_order(S) ? 1 : 0);
                     return (int)MPG_OK;

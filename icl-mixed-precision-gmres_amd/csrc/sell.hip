@@ -19,6 +19,8 @@
 #include "mpgmres/capi.h"
 
 #include <algorithm>
+#include <cstring>
+#include <map>
 #include <cstdlib>
 #include <new>
 #include <vector>
@@ -47,15 +49,21 @@ __global__ void k_sell_span(int n, const int32_t* __restrict__ rowptr, const int
     }
 }
 
-// Stepped int16 columns: one wave per slice; for each step j and element e
-// the base of (slice, step, element) = the midpoint of c - (row0 + lane)
-// over that element of all 64 rows; a slice where some spread exceeds
-// +-32767 is flagged in sexc (summed from CSR by the SpMVs).
+// Slice classification, one wave per slice. For each step j and element e:
+// d = c - (row0 + lane) over the rows that have that entry, its min and max
+// across the 64 rows, and how many rows have it. The base of (slice, step,
+// element) is the midpoint of [min, max] (kBasePad where no row has the
+// entry). Kind: implicit when every (step, element) is either present in all
+// 64 rows with one d, or absent from all; else, for the stepped form, CSR
+// when some spread exceeds +-32767; else stored.
+constexpr uint8_t kSliceStored = 0, kSliceCsr = 1, kSliceImplicit = 2;
+constexpr int32_t kBasePad = INT32_MIN;  // an element that is padding in every row of the slice
+
 template <int W>
-__global__ __launch_bounds__(kBlock) void k_sell_step_base(int n, int nslices, const int32_t* __restrict__ rowptr,
-                                                           const int32_t* __restrict__ col,
-                                                           const int64_t* __restrict__ off, int32_t* __restrict__ sbase,
-                                                           uint8_t* __restrict__ sexc) {
+__global__ __launch_bounds__(kBlock) void k_sell_classify(int n, int nslices, const int32_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ col,
+                                                          const int64_t* __restrict__ off, int32_t* __restrict__ sbase,
+                                                          uint8_t* __restrict__ skind, int stepped, int implicit) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int s = (int)(t / kWave), lane = (int)(t % kWave);
     if (s >= nslices) return;  // whole waves: the wave's shuffles below stay converged
@@ -63,26 +71,29 @@ __global__ __launch_bounds__(kBlock) void k_sell_step_base(int n, int nslices, c
     const int64_t o = off[s];
     const int steps = (int)((off[s + 1] - o) / (kWave * W));
     const int b = r < n ? rowptr[r] : 0, len = r < n ? rowptr[r + 1] - b : 0;
-    bool bad = false;
+    bool bad = false, imp = implicit != 0;
     for (int j = 0; j < steps; ++j) {
         for (int e = 0; e < W; ++e) {
             const int k = j * W + e;
+            const bool has = k < len;
             int lo = INT32_MAX, hi = INT32_MIN;
-            if (k < len) {
+            if (has) {
                 const int d = col[b + k] - r;
                 lo = d;
                 hi = d;
             }
+            const int cnt = __popcll(__ballot(has));
             for (int m = kWave / 2; m > 0; m >>= 1) {
                 lo = min(lo, __shfl_xor(lo, m, kWave));
                 hi = max(hi, __shfl_xor(hi, m, kWave));
             }
-            const int base = lo > hi ? 0 : (int)(((int64_t)lo + (int64_t)hi) >> 1);
-            if (lo <= hi && ((int64_t)hi - base > 32767 || (int64_t)lo - base < -32767)) bad = true;
+            const int base = cnt == 0 ? kBasePad : (int)(((int64_t)lo + (int64_t)hi) >> 1);
+            if (cnt > 0 && ((int64_t)hi - base > 32767 || (int64_t)lo - base < -32767)) bad = true;
+            if (!(cnt == 0 || (cnt == kWave && lo == hi))) imp = false;
             if (lane == 0) sbase[o / kWave + (int64_t)j * W + e] = base;
         }
     }
-    if (lane == 0) sexc[s] = bad ? 1 : 0;
+    if (lane == 0) skind[s] = imp ? kSliceImplicit : (stepped && bad) ? kSliceCsr : kSliceStored;
 }
 
 // scatter the CSR (col, val) of row 64 s + lane into its slice; pads get the
@@ -127,7 +138,8 @@ template <class X, class S, class CI, int W, bool WIN>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col, const S* __restrict__ val,
                                                       const int32_t* __restrict__ sbase,
-                                                      const uint8_t* __restrict__ sexc, const int32_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ spat, const CI* __restrict__ pat,
+                                                      const int32_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ ccol, const S* __restrict__ cval,
                                                       const X* __restrict__ x, X alpha, X beta, X* __restrict__ y,
                                                       int xcd) {
@@ -139,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
     const int row0 = s * kWave;
     const int i = row0 + lane;
     SellRow<S, CI, W> row;
-    row.init_load(s, off, sexc);
+    row.init_load(s, off, spat);
     __builtin_amdgcn_sched_barrier(0);
     X xr[WIN ? NQ : 1];
     if constexpr (WIN) {
@@ -151,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
     }
     const X yi = beta != X(0) ? y[i < n ? i : 0] : X(0);
     __builtin_amdgcn_sched_barrier(0);
-    row.init_finish(lane, col, val, sbase);
+    row.init_finish(lane, col, val, sbase, pat);
     row.load(0);
     __builtin_amdgcn_sched_barrier(0);
     double sum = 0.0;
@@ -254,37 +266,82 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
     S.win = win;
     S.padded = best;
     const int grid = (int)(((int64_t)ns * kWave + kBlock - 1) / kBlock);
-    if (try_c16s) {
-        // the (slice, step, element) bases; the stepped form when at most 1 %
-        // of the slices need the CSR fallback (sexc)
-        std::vector<uint8_t> exc((size_t)ns, 0);
-        bool okb = hipMalloc((void**)&S.sbase, (size_t)(best / kWave) * 4 + 256) == hipSuccess &&
-                   hipMalloc((void**)&S.sexc, (size_t)ns + 256) == hipSuccess;
+    const char* ienv = std::getenv("MPG_SELL_IMPLICIT");  // 0: always read the stored columns
+    const bool try_imp = !(ienv && *ienv == '0');
+    std::vector<int32_t> spat_h;   // per slice (host), when the copy has implicit or CSR slices
+    std::vector<int32_t> pat_h;    // implicit patterns: lane-relative offsets, W per step
+    if (try_c16s || try_imp) {
+        // bases and kinds (k_sell_classify); the stepped form when at most 1 %
+        // of the slices need the CSR fallback; implicit slices wherever they
+        // occur, their offset patterns deduplicated
+        std::vector<uint8_t> kind((size_t)ns, 0);
+        const size_t nb = (size_t)(best / kWave);
+        uint8_t* kind_d = nullptr;
+        bool okb = hipMalloc((void**)&S.sbase, nb * 4 + 256) == hipSuccess &&
+                   hipMalloc((void**)&kind_d, (size_t)ns + 256) == hipSuccess;
         if (okb) {
             auto launch = [&](auto wc) {
-                k_sell_step_base<decltype(wc)::value><<<grid, kBlock, 0, stream>>>(n, ns, A->rowptr, A->col, S.off,
-                                                                                S.sbase, S.sexc);
+                k_sell_classify<decltype(wc)::value><<<grid, kBlock, 0, stream>>>(
+                    n, ns, A->rowptr, A->col, S.off, S.sbase, kind_d, try_c16s ? 1 : 0, try_imp ? 1 : 0);
             };
             if (best_w == 4) launch(std::integral_constant<int, 4>());
             else if (best_w == 2) launch(std::integral_constant<int, 2>());
             else launch(std::integral_constant<int, 1>());
-            okb = hipMemcpyAsync(exc.data(), S.sexc, (size_t)ns, hipMemcpyDeviceToHost, stream) == hipSuccess &&
+            okb = hipMemcpyAsync(kind.data(), kind_d, (size_t)ns, hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                  hipStreamSynchronize(stream) == hipSuccess;
+        }
+        if (kind_d) (void)hipFree(kind_d);
+        std::vector<int32_t> bases;
+        int64_t nexc = 0, nimp = 0;
+        for (uint8_t k : kind) {
+            nexc += k == kSliceCsr;
+            nimp += k == kSliceImplicit;
+        }
+        if (okb && nimp) {
+            bases.resize(nb);
+            okb = hipMemcpyAsync(bases.data(), S.sbase, nb * 4, hipMemcpyDeviceToHost, stream) == hipSuccess &&
                   hipStreamSynchronize(stream) == hipSuccess;
         }
         if (!okb) {
             sell_free(S);
             return MPG_ERR_HIP;
         }
-        int64_t nexc = 0;
-        for (uint8_t e : exc) nexc += e;
-        if (nexc * 100 <= ns) {
-            S.c16s = true;
-            S.nexc = nexc;
-        } else {
+        S.c16s = try_c16s && nexc * 100 <= ns;
+        if (!S.c16s) nexc = 0;  // int32 columns: those slices are stored
+        if (nimp || nexc) {
+            spat_h.assign((size_t)ns, -1);
+            std::map<std::vector<int32_t>, int32_t> index;
+            for (int s2 = 0; s2 < ns; ++s2) {
+                if (kind[s2] == kSliceCsr && S.c16s) {
+                    spat_h[s2] = -2;
+                } else if (kind[s2] == kSliceImplicit) {
+                    const int64_t b0 = off[s2] / kWave, b1 = off[s2 + 1] / kWave;
+                    std::vector<int32_t> key(bases.begin() + b0, bases.begin() + b1);
+                    bool fits = true;  // int16 slice-relative form: the lane-relative offsets must fit too
+                    if (S.c16)
+                        for (int32_t d : key) fits = fits && (d == kBasePad || (d >= -32767 && d <= 32767));
+                    if (!fits) {
+                        --nimp;
+                        continue;
+                    }
+                    auto it = index.find(key);
+                    if (it == index.end()) {
+                        it = index.emplace(key, (int32_t)pat_h.size()).first;
+                        // lane-relative offsets; the stepped form stores them
+                        // against its bases, i.e. 0 (an implicit element's d
+                        // is its base)
+                        for (int32_t d : key) pat_h.push_back(d == kBasePad ? INT32_MIN : (S.c16s ? 0 : d));
+                    }
+                    spat_h[s2] = it->second;
+                    S.imp_slots += off[s2 + 1] - off[s2];
+                }
+            }
+            S.nimp = nimp;
+        }
+        S.nexc = nexc;
+        if (!S.c16s) {  // only the stepped form reads the bases
             (void)hipFree(S.sbase);
-            (void)hipFree(S.sexc);
             S.sbase = nullptr;
-            S.sexc = nullptr;
         }
     }
     if (hipMalloc(&S.col, (size_t)best * S.col_bytes() + 256) != hipSuccess ||
@@ -302,6 +359,30 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
             return (int)MPG_OK;
         });
     });
+    if (!st && !spat_h.empty()) {
+        // implicit patterns in the copy's column type (int16 forms: the
+        // offsets fit, since every slice's columns do)
+        const size_t cb = (size_t)S.col_bytes();
+        std::vector<char> pat_bytes(std::max<size_t>(pat_h.size(), 1) * cb + 64, 0);
+        for (size_t t = 0; t < pat_h.size(); ++t) {
+            const int32_t d = pat_h[t];
+            if (cb == 4) {
+                std::memcpy(pat_bytes.data() + t * 4, &d, 4);
+            } else {
+                const int16_t v = d == INT32_MIN ? (int16_t)INT16_MIN : (int16_t)d;
+                std::memcpy(pat_bytes.data() + t * 2, &v, 2);
+            }
+        }
+        S.npat = (int64_t)pat_h.size();
+        if (hipMalloc((void**)&S.spat, spat_h.size() * 4 + 256) != hipSuccess ||
+            hipMalloc(&S.pat, pat_bytes.size()) != hipSuccess)
+            st = MPG_ERR_ALLOC;
+        else if (hipMemcpyAsync(S.spat, spat_h.data(), spat_h.size() * 4, hipMemcpyHostToDevice, stream) !=
+                     hipSuccess ||
+                 hipMemcpyAsync(S.pat, pat_bytes.data(), pat_bytes.size(), hipMemcpyHostToDevice, stream) !=
+                     hipSuccess)
+            st = MPG_ERR_HIP;
+    }
     if (!st && hipStreamSynchronize(stream) != hipSuccess) st = MPG_ERR_HIP;
     if (st) sell_free(S);
     return st;
@@ -309,7 +390,8 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
 
 void sell_free(SellCopy& S) {
     if (S.sbase) (void)hipFree(S.sbase);
-    if (S.sexc) (void)hipFree(S.sexc);
+    if (S.spat) (void)hipFree(S.spat);
+    if (S.pat) (void)hipFree(S.pat);
     if (S.off) (void)hipFree(S.off);
     if (S.col) (void)hipFree(S.col);
     if (S.val) (void)hipFree(S.val);
@@ -339,7 +421,7 @@ int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y)
         return sell_dispatch_win(S.win, [&](auto wn) {
             k_sell_spmv<X, St, CI, decltype(wc)::value, decltype(wn)::value><<<grid, kBlock, 0, ctx->stream>>>(
                 S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val), S.sbase,
-                S.sexc, A->A->rowptr, A->A->col, static_cast<const St*>(A->vals), x, alpha, beta, y,
+                S.spat, static_cast<const CI*>(S.pat), A->A->rowptr, A->A->col, static_cast<const St*>(A->vals), x, alpha, beta, y,
                 sell_xcd_order(S) ? 1 : 0);
             return (int)MPG_OK;
         });
@@ -392,10 +474,11 @@ int mpg_sell_layout(mpg_sell_t A, int32_t* vec_width, int32_t* col_bytes, int64_
     return MPG_OK;
 }
 
-int mpg_sell_columns(mpg_sell_t A, int32_t* form, int64_t* csr_slices) {
+int mpg_sell_columns(mpg_sell_t A, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices) {
     if (!A) return MPG_ERR_ARG;
     if (form) *form = A->S.c16 ? 1 : A->S.c16s ? 2 : 0;
     if (csr_slices) *csr_slices = A->S.nexc;
+    if (implicit_slices) *implicit_slices = A->S.nimp;
     return MPG_OK;
 }
 

@@ -19,9 +19,17 @@
 //             (the 27-point 3-dof Queen stand-in: offsets up to +-37,299)
 //             still store 2-B columns, plus 4 B per 64 entries. A slice where
 //             some (step, element) spreads wider (rows on both sides of a
-//             boundary plane) is flagged in sexc[s] and its rows are summed
+//             boundary plane) gets spat[s] = -2 and its rows are summed
 //             from the CSR arrays instead, in the same order (same bits);
 //   int32_t   c.
+// Implicit slices: a slice whose 64 rows all have the same column offsets
+// c - row in the same order (every interior slice of a banded matrix) reads
+// its columns from a shared pattern instead: spat[s] >= 0 indexes a W-per-step
+// run of lane-relative offsets in `pat` that every lane of the wave loads
+// (the same address: one cache line), decoded against the lane's own row.
+// Identical patterns are stored once, so BAND-10M's 20 MB of int16 columns
+// become one 10-entry pattern. spat[s] = -1: stored columns; -2 (stepped
+// form): the slice is summed from the CSR arrays (below).
 // Padding carries a sentinel column and is skipped, so an Inf/NaN in x never
 // meets a padded zero. Within a row the entries keep CSR order and the fp64
 // sum runs in that order.
@@ -35,27 +43,32 @@
 
 namespace mpg {
 
-// decode(c, row0, lane_base): lane_base = row0 + lane + base (stepped form only)
+// decode(c, rbase, lane_base): rbase = the row the stored offset is relative
+// to (int16: the slice's first row; int32: 0, i.e. absolute; implicit
+// patterns: the lane's own row); lane_base = row0 + lane + base (stepped)
 template <class CI> struct SellCol;
 template <> struct SellCol<int32_t> {
-    static constexpr int32_t kPad = -1;
+    static constexpr int32_t kPad = INT32_MIN;
     static constexpr bool stepped = false;
-    static __device__ __forceinline__ bool live(int32_t c) { return c >= 0; }
-    static __device__ __forceinline__ int decode(int32_t c, int /*row0*/, int /*lane_base*/) { return c; }
+    static __device__ __forceinline__ bool live(int32_t c) { return c != INT32_MIN; }
+    static __device__ __forceinline__ int decode(int32_t c, int rbase, int /*lane_base*/) { return rbase + c; }
+    static __device__ __forceinline__ int stored_base(int /*row0*/) { return 0; }
 };
 template <> struct SellCol<int16_t> {
     static constexpr int16_t kPad = INT16_MIN;
     static constexpr bool stepped = false;
     static __device__ __forceinline__ bool live(int16_t c) { return c != INT16_MIN; }
-    static __device__ __forceinline__ int decode(int16_t c, int row0, int /*lane_base*/) { return row0 + (int)c; }
+    static __device__ __forceinline__ int decode(int16_t c, int rbase, int /*lane_base*/) { return rbase + (int)c; }
+    static __device__ __forceinline__ int stored_base(int row0) { return row0; }
 };
 template <> struct SellCol<uint16_t> {
     static constexpr uint16_t kPad = 0x8000u;
     static constexpr bool stepped = true;
     static __device__ __forceinline__ bool live(uint16_t c) { return c != 0x8000u; }
-    static __device__ __forceinline__ int decode(uint16_t c, int /*row0*/, int lane_base) {
+    static __device__ __forceinline__ int decode(uint16_t c, int /*rbase*/, int lane_base) {
         return lane_base + (int)(int16_t)c;
     }
+    static __device__ __forceinline__ int stored_base(int row0) { return row0; }
 };
 
 // raw storage of a value type inside the slices
@@ -120,7 +133,7 @@ __device__ __forceinline__ double sell_row_sum(int s, int lane, const int64_t* _
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int e = 0; e < W; ++e)
-                x[u][e] = SellCol<CI>::live(c[u][e]) ? xval(SellCol<CI>::decode(c[u][e], row0, row0)) : 0.0;
+                x[u][e] = SellCol<CI>::live(c[u][e]) ? xval(SellCol<CI>::decode(c[u][e], SellCol<CI>::stored_base(row0), row0)) : 0.0;
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -146,35 +159,48 @@ struct SellRow {
     CI c[U][W];
     S v[U][W];
     int32_t bq[kStepped ? U : 1][kStepped ? W : 1];  // stepped columns: the batch's bases
-    int steps, row0, lane_row;
-    bool exc = false;  // stepped: this slice is summed from CSR (sexc)
+    int steps, row0, lane_row, rbase;
+    int pk = -1;       // spat[s]: >= 0 implicit pattern, -1 stored, -2 summed from CSR
+    bool exc = false;  // stepped: this slice is summed from CSR
     const CI* __restrict__ cp;
+    int64_t cstride;   // column entries between steps: 64 W stored, W for a pattern
     const S* __restrict__ vp;
     const int32_t* __restrict__ bp;
 
     int64_t o0, o1;
-    // the slice's offsets: issue first (everything else needs them), use later
+    // the slice's offsets and pattern index: issue first (everything else
+    // needs them), use later
     __device__ __forceinline__ void init_load(int s, const int64_t* __restrict__ off,
-                                              const uint8_t* __restrict__ sexc = nullptr) {
+                                              const int32_t* __restrict__ spat = nullptr) {
         o0 = off[s];
         o1 = off[s + 1];
         row0 = s * kWave;
-        if constexpr (kStepped) exc = sexc[s] != 0;
+        if (spat) pk = spat[s];
     }
-    // sbase: the stepped form's (slice, step) bases (nullptr otherwise)
+    // sbase: the stepped form's (slice, step, element) bases; pat: the
+    // implicit slices' column patterns (nullptr when the copy has none).
+    // Stored and implicit slices differ only in where the same column load
+    // reads (a pointer and a stride chosen once per slice), never in a branch.
     __device__ __forceinline__ void init_finish(int lane, const CI* __restrict__ col, const S* __restrict__ val,
-                                                const int32_t* __restrict__ sbase = nullptr) {
+                                                const int32_t* __restrict__ sbase = nullptr,
+                                                const CI* __restrict__ pat = nullptr) {
         steps = (int)((o1 - o0) / (kWave * W));
         const int64_t base = steps > 0 ? o0 + lane * W : 0;
-        cp = col + base;
-        vp = val + base;
         lane_row = row0 + lane;
+        const bool imp = pk >= 0;
+        cp = imp ? pat + pk : col + base;
+        cstride = imp ? W : (int64_t)kWave * W;
+        rbase = imp ? lane_row : SellCol<CI>::stored_base(row0);
+        vp = val + base;
+        exc = pk == -2;
         if constexpr (kStepped) bp = sbase + (steps > 0 ? o0 / kWave : 0);  // (o0 / (64 W)) W
     }
     __device__ __forceinline__ void init(int s, int lane, const int64_t* __restrict__ off, const CI* __restrict__ col,
-                                         const S* __restrict__ val, const int32_t* __restrict__ sbase = nullptr) {
-        init_load(s, off);
-        init_finish(lane, col, val, sbase);
+                                         const S* __restrict__ val, const int32_t* __restrict__ sbase = nullptr,
+                                         const int32_t* __restrict__ spat = nullptr,
+                                         const CI* __restrict__ pat = nullptr) {
+        init_load(s, off, spat);
+        init_finish(lane, col, val, sbase, pat);
     }
     __device__ __forceinline__ void load(int q) {
         const int last = steps > 0 ? steps - 1 : 0;
@@ -182,7 +208,7 @@ struct SellRow {
         for (int u = 0; u < U; ++u) {
             const int qq = q + u < last ? q + u : last;
             if constexpr (kStepped) VecW<int32_t, W, false>::load(bp + (int64_t)qq * W, bq[u]);
-            VecW<CI, W, NT>::load(cp + (int64_t)qq * kWave * W, c[u]);
+            VecW<CI, W, NT>::load(cp + (int64_t)qq * cstride, c[u]);
             VecW<S, W, NT>::load(vp + (int64_t)qq * kWave * W, v[u]);
         }
     }
@@ -197,7 +223,7 @@ struct SellRow {
 #pragma unroll
             for (int e = 0; e < W; ++e)
                 x[u][e] = xval(SellCol<CI>::live(c[u][e])
-                                   ? SellCol<CI>::decode(c[u][e], row0, kStepped ? lane_row + bq[u][e] : 0)
+                                   ? SellCol<CI>::decode(c[u][e], rbase, kStepped ? lane_row + bq[u][e] : 0)
                                    : row0);
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -235,8 +261,12 @@ struct SellCopy {
     void* col = nullptr;
     void* val = nullptr;
     int32_t* sbase = nullptr;  // c16s: one base per (slice, step, element)
-    uint8_t* sexc = nullptr;   // c16s: 1 = the slice is summed from CSR
-    int64_t nexc = 0;          // c16s: slices flagged in sexc
+    int32_t* spat = nullptr;   // per slice: implicit pattern index, -1 stored, -2 CSR (nullptr: all stored)
+    void* pat = nullptr;       // the implicit slices' column patterns (CI entries, W per step)
+    int64_t nexc = 0;          // c16s: slices summed from CSR
+    int64_t nimp = 0;          // implicit slices
+    int64_t imp_slots = 0;     // their slots (their columns are not read)
+    int64_t npat = 0;          // pattern entries
     int col_bytes() const { return c16 || c16s ? 2 : 4; }
 };
 

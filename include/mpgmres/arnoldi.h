@@ -85,10 +85,11 @@ int mpg_arnoldi_destroy(mpg_arnoldi_t a);
  * LDS window instead of gathering from memory. Any output may be NULL. */
 int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
                             int64_t* stored, int32_t* window);
-/* bytes of the SELL copy's per-slice metadata one SpMV reads: int64 slice
- * offsets, plus one int32 base per (slice, step) in the stepped int16 column
- * form (0 without a SELL copy) */
-int64_t mpg_arnoldi_sell_meta_bytes(mpg_arnoldi_t a);
+/* matrix bytes one SELL SpMV reads (0 without a SELL copy): every slot's
+ * value, the columns of slots outside implicit slices (plus their shared
+ * patterns), int64 slice offsets, the per-slice pattern indices and the
+ * stepped form's (slice, step, element) bases */
+int64_t mpg_arnoldi_sell_matrix_bytes(mpg_arnoldi_t a);
 
 int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
 int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);

@@ -238,8 +238,10 @@ int mpg_sell_destroy(mpg_sell_t A);
 int mpg_sell_layout(mpg_sell_t A, int32_t* vec_width, int32_t* col_bytes, int64_t* stored, int32_t* window);
 /* column form of the copy: 0 int32, 1 int16 slice-relative, 2 stepped int16
  * (per-(slice, step, element) bases; sell_tile.hpp); *csr_slices = slices
- * of a stepped copy summed from the CSR arrays (a spread beyond int16) */
-int mpg_sell_columns(mpg_sell_t A, int32_t* form, int64_t* csr_slices);
+ * of a stepped copy summed from the CSR arrays (a spread beyond int16);
+ * *implicit_slices = slices whose rows share one column pattern (no columns
+ * read; MPG_SELL_IMPLICIT=0 disables them). Pointers may be NULL. */
+int mpg_sell_columns(mpg_sell_t A, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices);
 int mpg_sell_spmv_f64(mpg_ctx_t ctx, mpg_sell_t A, double alpha, const double* x, double beta, double* y);
 int mpg_sell_spmv_f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y);
 int mpg_sell_spmv_f16f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y);

@@ -66,8 +66,8 @@ def test_sell_stepped_columns_spmv(hip, mpg, stepped, kind, monkeypatch):
             hip.check(hip.lib.mpg_sell_create(hip.ctx, csr, vt, dv.p, 0, C.byref(sell)))
             assert sell.value
             sells.append(sell)
-            form, exc = C.c_int32(), C.c_int64()
-            hip.check(hip.lib.mpg_sell_columns(sell, C.byref(form), C.byref(exc)))
+            form, exc, imp = C.c_int32(), C.c_int64(), C.c_int64()
+            hip.check(hip.lib.mpg_sell_columns(sell, C.byref(form), C.byref(exc), C.byref(imp)))
             if stepped == "1":
                 assert form.value == 2 and exc.value == (0 if kind == "wide" else 1), (form.value, exc.value)
             else:
@@ -141,3 +141,64 @@ def test_stepped_exception_slice_solve(mpg, monkeypatch):
             got[st] = mpg.solve(A, b, xt, engine="fused", spmv_format="sell", **opts)
         assert got["1"].total_iters == got["0"].total_iters == 90
         assert np.array_equal(got["1"].step_res, got["0"].step_res) and np.array_equal(got["1"].x, got["0"].x)
+
+
+@pytest.mark.parametrize("implicit", ["1", "0"])
+def test_implicit_slices_spmv(hip, mpg, implicit, monkeypatch):
+    """Implicit slices (every row of the slice with the same column offsets:
+    all but the first and last slice of a banded matrix) read no columns;
+    their sums are the CSR sums in CSR order, so fp32/fp16 results equal the
+    CSR SpMV's bits and the copy without implicit slices gives the same bits
+    in every precision."""
+    monkeypatch.setenv("MPG_SELL_IMPLICIT", implicit)
+    A = mpg.gen_band(200_000, 5, 4, seed=11)
+    n = A.nrows
+    g = np.random.default_rng(5)
+    x = g.uniform(-1, 1, n)
+    y0 = g.uniform(-1, 1, n)
+    drp, dci = hip.buf(A.rowptr), hip.buf(A.col)
+    csr = C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, n, n, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    sells = []
+    try:
+        cases = [("f64", 0, A.val, np.float64, -1.0, 1.0), ("f32", 1, A.val.astype(np.float32), np.float32, 1.0, 0.0),
+                 ("f16f32", 2, A.val.astype(np.float16).view(np.uint16), np.float32, 2.0, -0.5)]
+        for name, vt, vals, xdt, alpha, beta in cases:
+            dv = hip.buf(vals)
+            sell = C.c_void_p()
+            hip.check(hip.lib.mpg_sell_create(hip.ctx, csr, vt, dv.p, 0, C.byref(sell)))
+            sells.append(sell)
+            form, exc, imp = C.c_int32(), C.c_int64(), C.c_int64()
+            hip.check(hip.lib.mpg_sell_columns(sell, C.byref(form), C.byref(exc), C.byref(imp)))
+            assert form.value == 1 and imp.value == (n // 64 - 2 if implicit == "1" else 0), imp.value
+            dx = hip.buf(x.astype(xdt))
+            dy_sell, dy_csr = hip.buf(y0.astype(xdt)), hip.buf(y0.astype(xdt))
+            hip.call(f"mpg_sell_spmv_{name}", sell, xdt(alpha), dx.p, xdt(beta), dy_sell.p)
+            hip.call(f"mpg_csr_spmv_{name}", csr, xdt(alpha), dv.p, dx.p, xdt(beta), dy_csr.p)
+            if name == "f64":
+                scale = np.abs(y0) + abs(A.to_scipy()) @ np.abs(x)
+                assert np.all(np.abs(dy_sell.get() - dy_csr.get()) <= 4 * F64_EPS * scale), name
+            else:
+                assert np.array_equal(dy_sell.get(), dy_csr.get()), name
+    finally:
+        for h in sells:
+            hip.lib.mpg_sell_destroy(h)
+        hip.lib.mpg_csr_destroy(csr)
+
+
+@pytest.mark.parametrize("mode", ["mixed", "baseline", "mixed-half"])
+@pytest.mark.parametrize("orth", ["cgs", "mgs"])
+def test_implicit_slices_solve(mpg, mode, orth, monkeypatch):
+    """The fused engine's Arnoldi SpMV and residual prologue with and without
+    implicit slices: the same bits."""
+    A = mpg.gen_band(120_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=0.0, max_restarts=3)
+    got = {}
+    for imp in ("1", "0"):
+        monkeypatch.setenv("MPG_SELL_IMPLICIT", imp)
+        got[imp] = mpg.solve(A, b, xt, engine="fused", spmv_format="sell", **opts)
+    assert got["1"].total_iters == got["0"].total_iters == 90
+    assert np.array_equal(got["1"].step_res, got["0"].step_res) and np.array_equal(got["1"].x, got["0"].x)
+    assert got["1"].res_norm == got["0"].res_norm
