@@ -24,10 +24,15 @@ def per_kernel(d, counter):
                 continue
             m = re.search(r"(k_\w+)(<[^(]*>)?", r["Kernel_Name"])
             name = m.group(1) if m else r["Kernel_Name"][:40]
-            # the Arnoldi SpMVs come in a plain and a Givens-folded (FOLD =
-            # last template argument true) instantiation: keep them apart
-            if m and name in ("k_step_sell", "k_step_spmv") and m.group(2) and m.group(2).endswith("true>"):
-                name += ":fold"
+            # the Arnoldi SpMVs come in a plain and a Givens-folded
+            # instantiation: keep them apart (FOLD is template argument 7 of
+            # k_step_sell<T, P, VI, CI, W, WIN, FOLD, DN> and 4 of
+            # k_step_spmv<T, P, VI, FOLD>)
+            if m and name in ("k_step_sell", "k_step_spmv") and m.group(2):
+                args = [a.strip() for a in m.group(2)[1:-1].split(",")]
+                at = 6 if name == "k_step_sell" else 3
+                if len(args) > at and args[at] == "true":
+                    name += ":fold"
             vals[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
