@@ -6,6 +6,8 @@
 // sums the partials in a fixed order and writes the result on device).
 #include "internal.hpp"
 
+#include <algorithm>
+
 using namespace mpg;
 
 namespace {
@@ -35,15 +37,66 @@ __global__ __launch_bounds__(1024) void k_reduce_stage2(int nparts, const double
     if (threadIdx.x == 0) *result = SQRT ? (T)sqrt(s) : (T)s;
 }
 
+// Stage 2 folded into the consumer of the result (the operator surface's
+// nrm2 -> scal_recip of add_vector, dot -> naxpy of the MGS kernel): every
+// 1024-thread workgroup sums the stage-1 partials with stage 2's own
+// block_sum<1024> (the same bits), workgroup 0 stores the result, and all
+// apply it. OP 0: y = (1/r) x with r = T(sqrt(s)); OP 1: y -= T(s) x.
+template <class T, int OP>
+__global__ __launch_bounds__(1024) void k_consume_partials(int nparts, const double* __restrict__ partial,
+                                                           T* __restrict__ result, int64_t n, const T* x, T* y) {
+    __shared__ double scratch[1024 / kWave];
+    __shared__ T r_s;
+    double v = threadIdx.x < nparts ? partial[threadIdx.x] : 0.0;
+    const double s = block_sum<1024>(v, scratch);
+    if (threadIdx.x == 0) {
+        const T r = OP == 0 ? (T)sqrt(s) : (T)s;
+        r_s = r;
+        if (blockIdx.x == 0) *result = r;
+    }
+    __syncthreads();
+    const T r = r_s;
+    const int64_t stride = (int64_t)gridDim.x * 1024;
+    if (OP == 0) {
+        const T a = T(1) / r;  // k_scal_copy<T, true, true>
+        for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) y[i] = a * x[i];
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) y[i] -= r * x[i];  // k_axpy NEG
+    }
+}
+
 template <class T, bool SQUARE>
-int reduce(mpg_ctx* ctx, int64_t n, const T* x, const T* y, T* result_dev) {
-    if (!ctx || n < 0) return MPG_ERR_ARG;
-    int g = grid_for(n, 4, kMaxRedBlocks);
+int reduce_partials(mpg_ctx* ctx, int64_t n, const T* x, const T* y, int32_t* nparts) {
+    if (!ctx || n < 0 || !nparts) return MPG_ERR_ARG;
+    const int g = grid_for(n, 4, kMaxRedBlocks);
     k_reduce_stage1<T, SQUARE><<<g, kBlock, 0, ctx->stream>>>(n, x, y, ctx->red_ws);
     MPG_LAUNCH_CHECK(ctx);
-    k_reduce_stage2<T, SQUARE><<<1, 1024, 0, ctx->stream>>>(g, ctx->red_ws, result_dev);
+    *nparts = g;
+    return MPG_OK;
+}
+
+template <class T, bool SQRT>
+int reduce_finish(mpg_ctx* ctx, int32_t nparts, T* result_dev) {
+    if (!ctx || nparts < 1 || nparts > kMaxRedBlocks) return MPG_ERR_ARG;
+    k_reduce_stage2<T, SQRT><<<1, 1024, 0, ctx->stream>>>(nparts, ctx->red_ws, result_dev);
     MPG_LAUNCH_CHECK(ctx);
     return MPG_OK;
+}
+
+template <class T, int OP>
+int consume_partials(mpg_ctx* ctx, int32_t nparts, T* result_dev, int64_t n, const T* x, T* y) {
+    if (!ctx || nparts < 1 || nparts > kMaxRedBlocks || n < 0) return MPG_ERR_ARG;
+    const int g = (int)std::max<int64_t>(1, std::min<int64_t>(256, (n + 4 * 1024 - 1) / (4 * 1024)));
+    k_consume_partials<T, OP><<<g, 1024, 0, ctx->stream>>>(nparts, ctx->red_ws, result_dev, n, x, y);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+template <class T, bool SQUARE>
+int reduce(mpg_ctx* ctx, int64_t n, const T* x, const T* y, T* result_dev) {
+    int32_t g = 0;
+    if (int st = reduce_partials<T, SQUARE>(ctx, n, x, y, &g)) return st;
+    return reduce_finish<T, SQUARE>(ctx, g, result_dev);
 }
 
 template <class T, bool SQUARE>
@@ -301,6 +354,18 @@ int mpg_dot_f64(mpg_ctx_t c, int64_t n, const double* x, const double* y, double
 int mpg_dot_f32(mpg_ctx_t c, int64_t n, const float* x, const float* y, float* r) { return reduce<float, false>(c, n, x, y, r); }
 int mpg_dot_f64_host(mpg_ctx_t c, int64_t n, const double* x, const double* y, double* r) { return reduce_host<double, false>(c, n, x, y, r); }
 int mpg_dot_f32_host(mpg_ctx_t c, int64_t n, const float* x, const float* y, float* r) { return reduce_host<float, false>(c, n, x, y, r); }
+int mpg_dot_partials_f64(mpg_ctx_t c, int64_t n, const double* x, const double* y, int32_t* np) { return reduce_partials<double, false>(c, n, x, y, np); }
+int mpg_dot_partials_f32(mpg_ctx_t c, int64_t n, const float* x, const float* y, int32_t* np) { return reduce_partials<float, false>(c, n, x, y, np); }
+int mpg_nrm2_partials_f64(mpg_ctx_t c, int64_t n, const double* x, int32_t* np) { return reduce_partials<double, true>(c, n, x, x, np); }
+int mpg_nrm2_partials_f32(mpg_ctx_t c, int64_t n, const float* x, int32_t* np) { return reduce_partials<float, true>(c, n, x, x, np); }
+int mpg_dot_finish_f64(mpg_ctx_t c, int32_t np, double* r) { return reduce_finish<double, false>(c, np, r); }
+int mpg_dot_finish_f32(mpg_ctx_t c, int32_t np, float* r) { return reduce_finish<float, false>(c, np, r); }
+int mpg_nrm2_finish_f64(mpg_ctx_t c, int32_t np, double* r) { return reduce_finish<double, true>(c, np, r); }
+int mpg_nrm2_finish_f32(mpg_ctx_t c, int32_t np, float* r) { return reduce_finish<float, true>(c, np, r); }
+int mpg_scal_recip_nrm2_f64(mpg_ctx_t c, int32_t np, double* h, int64_t n, const double* x, double* y) { return consume_partials<double, 0>(c, np, h, n, x, y); }
+int mpg_scal_recip_nrm2_f32(mpg_ctx_t c, int32_t np, float* h, int64_t n, const float* x, float* y) { return consume_partials<float, 0>(c, np, h, n, x, y); }
+int mpg_naxpy_dot_f64(mpg_ctx_t c, int32_t np, double* a, int64_t n, const double* x, double* y) { return consume_partials<double, 1>(c, np, a, n, x, y); }
+int mpg_naxpy_dot_f32(mpg_ctx_t c, int32_t np, float* a, int64_t n, const float* x, float* y) { return consume_partials<float, 1>(c, np, a, n, x, y); }
 int mpg_nrm2_f64(mpg_ctx_t c, int64_t n, const double* x, double* r) { return reduce<double, true>(c, n, x, x, r); }
 int mpg_nrm2_f32(mpg_ctx_t c, int64_t n, const float* x, float* r) { return reduce<float, true>(c, n, x, x, r); }
 int mpg_nrm2_f64_host(mpg_ctx_t c, int64_t n, const double* x, double* r) { return reduce_host<double, true>(c, n, x, x, r); }

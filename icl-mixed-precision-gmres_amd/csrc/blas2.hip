@@ -124,6 +124,15 @@ __global__ __launch_bounds__(kBlock) void k_gemv_n_nc(int64_t rows, T alpha, con
     }
 }
 
+// Stage 2 of gemv^T: one wave per column, lane l summing partials l, l + 64,
+// ... in order, then the wave's shuffle tree. The fused gemv (N)
+// forms its coefficients with the same function, so both give the same bits.
+__device__ __forceinline__ double column_sum(const double* __restrict__ partial, int nparts, int c, int lane) {
+    double v = 0.0;
+    for (int j = lane; j < nparts; j += kWave) v += partial[(int64_t)c * nparts + j];
+    return wave_sum(v);
+}
+
 constexpr int kQuadBlock = 1024;
 constexpr int kQuadGroups = 256;
 
@@ -161,14 +170,31 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_t_quad(int64_t rows, const 
     store_partials<NP, kQuadBlock>(acc, NC, partial);
 }
 
-// y = alpha*T(A x) + beta*y, 4 rows per lane, fp64 sums in column order
-template <class T, int NC>
+// y = alpha*T(A x) + beta*y, 4 rows per lane, fp64 sums in column order.
+// FROM_PARTS: x is the pending result of a gemv^T whose stage-1 partials are
+// in `partial` (x = alpha_t * T(sum), beta_t = 0): every workgroup forms the
+// coefficients itself with stage 2's column_sum and workgroup 0 stores them
+// to x, saving the stage-2 launch (CGS: h = V^T w, then w -= V h).
+template <class T, int NC, bool FROM_PARTS = false>
 __global__ __launch_bounds__(kQuadBlock) void k_gemv_n_quad(int64_t rows, T alpha, const T* __restrict__ A,
-                                                            int64_t lda, const T* __restrict__ x, T beta,
-                                                            T* __restrict__ y) {
+                                                            int64_t lda, T* __restrict__ x, T beta,
+                                                            T* __restrict__ y, const double* __restrict__ partial = nullptr,
+                                                            int nparts = 0, T alpha_t = T(1)) {
     constexpr int B = kColBatch<T>;
     __shared__ double xs[NC];
-    if (threadIdx.x < NC) xs[threadIdx.x] = (double)x[threadIdx.x];
+    if constexpr (FROM_PARTS) {
+        const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+        for (int c = wid; c < NC; c += kQuadBlock / kWave) {
+            const double sc = column_sum(partial, nparts, c, lane);
+            if (lane == 0) {
+                const T h = alpha_t * (T)sc;
+                xs[c] = (double)h;
+                if (blockIdx.x == 0) x[c] = h;
+            }
+        }
+    } else {
+        if (threadIdx.x < NC) xs[threadIdx.x] = (double)x[threadIdx.x];
+    }
     __syncthreads();
     const int64_t n4 = rows & ~int64_t(3);
     const int64_t step = 4 * (int64_t)gridDim.x * kQuadBlock;
@@ -221,16 +247,17 @@ int with_cols(int nc, F&& f) {
     }
 }
 
+
 template <class T>
-__global__ __launch_bounds__(1024) void k_gemv_t_stage2(int nparts, const double* __restrict__ partial,
+__global__ __launch_bounds__(1024) void k_gemv_t_stage2(int nparts, int nc, const double* __restrict__ partial,
                                                         T alpha, T beta, T* __restrict__ y) {
-    __shared__ double scratch[1024 / kWave];
-    const int c = blockIdx.x;
-    double v = threadIdx.x < nparts ? partial[(int64_t)c * nparts + threadIdx.x] : 0.0;
-    double s = block_sum<1024>(v, scratch);
-    if (threadIdx.x == 0) {
-        T t = (T)s;
-        y[c] = beta == T(0) ? alpha * t : alpha * t + beta * y[c];
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    for (int c = wid; c < nc; c += 1024 / kWave) {
+        const double s = column_sum(partial, nparts, c, lane);
+        if (lane == 0) {
+            const T t = (T)s;
+            y[c] = beta == T(0) ? alpha * t : alpha * t + beta * y[c];
+        }
     }
 }
 
@@ -256,8 +283,8 @@ int gemv_impl(mpg_ctx* ctx, int trans, int64_t rows, int64_t cols, T alpha, cons
         if (cols >= 1 && cols <= kGemvMaxCols && quad_aligned(A, lda, y)) {
             const int g = (int)std::min<int64_t>(kQuadGroups, (rows + 4 * kQuadBlock - 1) / (4 * kQuadBlock));
             const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto nc) {
-                k_gemv_n_quad<T, decltype(nc)::value><<<g, kQuadBlock, 0, ctx->stream>>>(rows, alpha, A, lda, x,
-                                                                                        beta, y);
+                k_gemv_n_quad<T, decltype(nc)::value><<<g, kQuadBlock, 0, ctx->stream>>>(
+                    rows, alpha, A, lda, const_cast<T*>(x), beta, y);
                 return (int)MPG_OK;
             });
             if (st) return st;
@@ -291,9 +318,58 @@ int gemv_impl(mpg_ctx* ctx, int trans, int64_t rows, int64_t cols, T alpha, cons
         });
         if (st) return st;
         MPG_LAUNCH_CHECK(ctx);
-        k_gemv_t_stage2<T><<<nc, 1024, 0, ctx->stream>>>(g, ctx->red_ws, alpha, beta, y + c0);
+        k_gemv_t_stage2<T><<<1, 1024, 0, ctx->stream>>>(g, nc, ctx->red_ws, alpha, beta, y + c0);
         MPG_LAUNCH_CHECK(ctx);
     }
+    return MPG_OK;
+}
+
+// gemv^T stage 1 alone (<= kGemvMaxCols columns): partials in the context
+// workspace, *nparts of them per column, until the next reduction on ctx
+template <class T>
+int gemv_t_partials(mpg_ctx* ctx, int64_t rows, int64_t cols, const T* A, int64_t lda, const T* x, int32_t* nparts) {
+    if (!ctx || !nparts || rows < 0 || cols < 1 || (rows > 0 && lda < rows)) return MPG_ERR_ARG;
+    if (cols > kGemvMaxCols) return MPG_ERR_UNSUPPORTED;
+    const bool quad = quad_aligned(A, lda, x);
+    const int g = quad ? (int)std::max<int64_t>(1, std::min<int64_t>(kQuadGroups, (rows + 4 * kQuadBlock - 1) /
+                                                                                    (4 * kQuadBlock)))
+                       : grid_for(rows, 4, kMaxRedBlocks);
+    const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto ncc) {
+        if (quad)
+            k_gemv_t_quad<T, decltype(ncc)::value><<<g, kQuadBlock, 0, ctx->stream>>>(rows, A, lda, x, ctx->red_ws);
+        else
+            k_gemv_t_nc<T, decltype(ncc)::value><<<g, kBlock, 0, ctx->stream>>>(rows, A, lda, x, ctx->red_ws);
+        return (int)MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(ctx);
+    *nparts = g;
+    return MPG_OK;
+}
+
+template <class T>
+int gemv_t_finish(mpg_ctx* ctx, int32_t nparts, int64_t cols, T alpha, T beta, T* y) {
+    if (!ctx || nparts < 1 || cols < 1 || cols > kGemvMaxCols) return MPG_ERR_ARG;
+    k_gemv_t_stage2<T><<<1, 1024, 0, ctx->stream>>>(nparts, (int)cols, ctx->red_ws, alpha, beta, y);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+// y = alpha*T(A x) + beta*y where x = alpha_t * T(pending gemv^T sums);
+// MPG_ERR_UNSUPPORTED unless A, lda and y allow the quad form
+template <class T>
+int gemv_n_from_t(mpg_ctx* ctx, int64_t rows, int64_t cols, T alpha, const T* A, int64_t lda, int32_t nparts,
+                  T alpha_t, T* x, T beta, T* y) {
+    if (!ctx || rows < 0 || cols < 1 || nparts < 1 || (rows > 0 && lda < rows)) return MPG_ERR_ARG;
+    if (cols > kGemvMaxCols || !quad_aligned(A, lda, y)) return MPG_ERR_UNSUPPORTED;
+    const int g = (int)std::max<int64_t>(1, std::min<int64_t>(kQuadGroups, (rows + 4 * kQuadBlock - 1) / (4 * kQuadBlock)));
+    const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto nc) {
+        k_gemv_n_quad<T, decltype(nc)::value, true><<<g, kQuadBlock, 0, ctx->stream>>>(
+            rows, alpha, A, lda, x, beta, y, ctx->red_ws, nparts, alpha_t);
+        return (int)MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(ctx);
     return MPG_OK;
 }
 
@@ -370,6 +446,28 @@ int mpg_gemv_f64(mpg_ctx_t c, int trans, int64_t rows, int64_t cols, double alph
 int mpg_gemv_f32(mpg_ctx_t c, int trans, int64_t rows, int64_t cols, float alpha, const float* A,
                  int64_t lda, const float* x, float beta, float* y) {
     return gemv_impl<float>(c, trans, rows, cols, alpha, A, lda, x, beta, y);
+}
+int mpg_gemv_t_partials_f64(mpg_ctx_t c, int64_t rows, int64_t cols, const double* A, int64_t lda, const double* x,
+                            int32_t* np) {
+    return gemv_t_partials<double>(c, rows, cols, A, lda, x, np);
+}
+int mpg_gemv_t_partials_f32(mpg_ctx_t c, int64_t rows, int64_t cols, const float* A, int64_t lda, const float* x,
+                            int32_t* np) {
+    return gemv_t_partials<float>(c, rows, cols, A, lda, x, np);
+}
+int mpg_gemv_t_finish_f64(mpg_ctx_t c, int32_t np, int64_t cols, double alpha, double beta, double* y) {
+    return gemv_t_finish<double>(c, np, cols, alpha, beta, y);
+}
+int mpg_gemv_t_finish_f32(mpg_ctx_t c, int32_t np, int64_t cols, float alpha, float beta, float* y) {
+    return gemv_t_finish<float>(c, np, cols, alpha, beta, y);
+}
+int mpg_gemv_n_from_t_f64(mpg_ctx_t c, int64_t rows, int64_t cols, double alpha, const double* A, int64_t lda,
+                          int32_t np, double alpha_t, double* x, double beta, double* y) {
+    return gemv_n_from_t<double>(c, rows, cols, alpha, A, lda, np, alpha_t, x, beta, y);
+}
+int mpg_gemv_n_from_t_f32(mpg_ctx_t c, int64_t rows, int64_t cols, float alpha, const float* A, int64_t lda,
+                          int32_t np, float alpha_t, float* x, float beta, float* y) {
+    return gemv_n_from_t<float>(c, rows, cols, alpha, A, lda, np, alpha_t, x, beta, y);
 }
 int mpg_trsv_f64(mpg_ctx_t c, int upper, int trans, int64_t n, const double* A, int64_t lda, double* x) {
     return trsv_impl<double>(c, upper, trans, n, A, lda, x);

@@ -103,6 +103,67 @@ mpg_ctx_t ctx_no_flush() {
 }
 }  // namespace
 
+// ---- deferred stage 2 of reductions ----
+// A reduction whose result goes to device memory (nrm2 / dot into a Scalar,
+// gemv^T into a Vect with beta = 0) runs its stage 1 and leaves stage 2
+// pending. If the very next call consumes that result (add_vector's
+// scal_recip of the nrm2, MGS's naxpy of the dot, CGS's gemv of the gemv^T
+// coefficients), it runs as one launch that sums the partials itself in
+// stage 2's order (the same bits); any other call issues stage 2 first
+// through current_ctx(). MPG_SURFACE_FUSE (bit mask below; 0: none) picks
+// the pairs: MGS's dot -> naxpy is off by default, its 1024-thread consumer
+// measured slower than stage 2 + naxpy (5.4k vs 5.7k it/s on BAND-10M).
+namespace {
+struct PendingReduction {
+    int kind = 0;  // 0 none, 1 nrm2, 2 dot, 3 gemv^T
+    bool f64 = false;
+    mpg_ctx_t ctx = nullptr;
+    int32_t nparts = 0;
+    void* result = nullptr;
+    int64_t cols = 0;    // gemv^T
+    double alpha = 1.0;  // gemv^T
+};
+thread_local PendingReduction tl_red;
+
+// MPG_SURFACE_FUSE: a bit mask of the fused pairs (1 nrm2 -> scal_recip,
+// 2 dot -> naxpy, 4 gemv^T -> gemv); unset: kFuseDefault; 0: none
+constexpr int kFuseDefault = 1 | 4;
+bool fuse_enabled(int bit) {
+    const char* env = std::getenv("MPG_SURFACE_FUSE");
+    const int mask = env && *env ? std::atoi(env) : kFuseDefault;
+    return (mask & bit) != 0;
+}
+}  // namespace
+
+void flush_pending_reduction() {
+    if (!tl_red.kind) return;
+    const PendingReduction r = tl_red;
+    tl_red.kind = 0;
+    int st = MPG_OK;
+    if (r.kind == 1)
+        st = r.f64 ? mpg_nrm2_finish_f64(r.ctx, r.nparts, (double*)r.result)
+                   : mpg_nrm2_finish_f32(r.ctx, r.nparts, (float*)r.result);
+    else if (r.kind == 2)
+        st = r.f64 ? mpg_dot_finish_f64(r.ctx, r.nparts, (double*)r.result)
+                   : mpg_dot_finish_f32(r.ctx, r.nparts, (float*)r.result);
+    else
+        st = r.f64 ? mpg_gemv_t_finish_f64(r.ctx, r.nparts, r.cols, r.alpha, 0.0, (double*)r.result)
+                   : mpg_gemv_t_finish_f32(r.ctx, r.nparts, r.cols, (float)r.alpha, 0.f, (float*)r.result);
+    check(st, "reduction stage 2", r.ctx);
+}
+
+void discard_pending_reduction() { tl_red.kind = 0; }
+
+// the pending reduction of `kind` whose result is `result`, taken (cleared)
+// when the caller will consume it; nullptr otherwise
+static const PendingReduction* take_pending(int kind, bool f64, const void* result) {
+    if (tl_red.kind != kind || tl_red.f64 != f64 || tl_red.result != result || tl_red.ctx != tl_ctx) return nullptr;
+    static thread_local PendingReduction taken;
+    taken = tl_red;
+    tl_red.kind = 0;
+    return &taken;
+}
+
 void flush_scalar_ops() {
     if (tl_nops == 0) return;
     const int n = tl_nops;
@@ -115,6 +176,7 @@ void discard_scalar_ops() { tl_nops = 0; }
 // true when queued (the caller issues the op itself otherwise)
 bool queue_scalar_op(const mpg_scalar_op& op) {
     if (!batch_enabled()) return false;
+    if (tl_red.kind) flush_pending_reduction();
     mpg_ctx_t c = ctx_no_flush();
     if (tl_nops && tl_ops_ctx != c) flush_scalar_ops();
     tl_ops_ctx = c;
@@ -125,20 +187,29 @@ bool queue_scalar_op(const mpg_scalar_op& op) {
 
 mpg_ctx_t current_ctx() {
     if (tl_nops) flush_scalar_ops();
+    if (tl_red.kind) flush_pending_reduction();
     return ctx_no_flush();
 }
 
 ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) {
     if (tl_nops) flush_scalar_ops();
+    if (tl_red.kind) flush_pending_reduction();
     tl_ctx = ctx;
 }
 ScopedContext::~ScopedContext() {
-    // the queue belongs to this scope's context; a failure here has already
-    // been reported by the call that follows it, or the scope is unwinding
+    // the queue and a pending stage 2 belong to this scope's context; a
+    // failure here has already been reported by the call that follows it,
+    // or the scope is unwinding
     if (tl_nops) {
         const int n = tl_nops;
         tl_nops = 0;
         (void)mpg_scalar_program(tl_ops_ctx, tl_ops, n);
+    }
+    if (tl_red.kind) {
+        try {
+            flush_pending_reduction();
+        } catch (...) {
+        }
     }
     tl_ctx = prev_;
 }
@@ -247,10 +318,24 @@ template <> float dot<float, Hip>(Vect<float, Hip> x, Vect<float, Hip> y) {
 }
 template <> void dot<double, Hip>(Vect<double, Hip> x, Vect<double, Hip> y, Scalar<double, Hip> r) {
     assert(x.n() == y.n());
+    if (mpg::fuse_enabled(2) && x.n() > 0) {
+        mpg_ctx_t c = C;
+        int32_t np = 0;
+        check(mpg_dot_partials_f64(c, x.n(), x.data(), y.data(), &np), "dot");
+        mpg::tl_red = mpg::PendingReduction{2, true, c, np, r.data()};
+        return;
+    }
     check(mpg_dot_f64(C, x.n(), x.data(), y.data(), r.data()), "dot");
 }
 template <> void dot<float, Hip>(Vect<float, Hip> x, Vect<float, Hip> y, Scalar<float, Hip> r) {
     assert(x.n() == y.n());
+    if (mpg::fuse_enabled(2) && x.n() > 0) {
+        mpg_ctx_t c = C;
+        int32_t np = 0;
+        check(mpg_dot_partials_f32(c, x.n(), x.data(), y.data(), &np), "dot");
+        mpg::tl_red = mpg::PendingReduction{2, false, c, np, r.data()};
+        return;
+    }
     check(mpg_dot_f32(C, x.n(), x.data(), y.data(), r.data()), "dot");
 }
 template <> double nrm2<double, Hip>(Vect<double, Hip> x) {
@@ -264,9 +349,23 @@ template <> float nrm2<float, Hip>(Vect<float, Hip> x) {
     return r;
 }
 template <> void nrm2<double, Hip>(Vect<double, Hip> x, Scalar<double, Hip> r) {
+    if (mpg::fuse_enabled(1) && x.n() > 0) {
+        mpg_ctx_t c = C;
+        int32_t np = 0;
+        check(mpg_nrm2_partials_f64(c, x.n(), x.data(), &np), "nrm2");
+        mpg::tl_red = mpg::PendingReduction{1, true, c, np, r.data()};
+        return;
+    }
     check(mpg_nrm2_f64(C, x.n(), x.data(), r.data()), "nrm2");
 }
 template <> void nrm2<float, Hip>(Vect<float, Hip> x, Scalar<float, Hip> r) {
+    if (mpg::fuse_enabled(1) && x.n() > 0) {
+        mpg_ctx_t c = C;
+        int32_t np = 0;
+        check(mpg_nrm2_partials_f32(c, x.n(), x.data(), &np), "nrm2");
+        mpg::tl_red = mpg::PendingReduction{1, false, c, np, r.data()};
+        return;
+    }
     check(mpg_nrm2_f32(C, x.n(), x.data(), r.data()), "nrm2");
 }
 
@@ -289,10 +388,18 @@ template <> void axpy<float, Hip>(Scalar<float, Hip> a, Vect<float, Hip> x, Vect
 }
 template <> void naxpy<double, Hip>(Scalar<double, Hip> a, Vect<double, Hip> x, Vect<double, Hip> y) {
     assert(x.n() == y.n());
+    if (const auto* p = mpg::take_pending(2, true, a.data())) {
+        check(mpg_naxpy_dot_f64(p->ctx, p->nparts, a.data(), x.n(), x.data(), y.data()), "naxpy (dot)", p->ctx);
+        return;
+    }
     check(mpg_naxpy_dev_f64(C, x.n(), a.data(), x.data(), y.data()), "naxpy");
 }
 template <> void naxpy<float, Hip>(Scalar<float, Hip> a, Vect<float, Hip> x, Vect<float, Hip> y) {
     assert(x.n() == y.n());
+    if (const auto* p = mpg::take_pending(2, false, a.data())) {
+        check(mpg_naxpy_dot_f32(p->ctx, p->nparts, a.data(), x.n(), x.data(), y.data()), "naxpy (dot)", p->ctx);
+        return;
+    }
     check(mpg_naxpy_dev_f32(C, x.n(), a.data(), x.data(), y.data()), "naxpy");
 }
 
@@ -338,10 +445,20 @@ template <> void scal<float, Hip>(Scalar<float, Hip> a, Scalar<float, Hip> x, Sc
 
 template <> void scal_recip<double, Hip>(Scalar<double, Hip> a, Vect<double, Hip> x, Vect<double, Hip> y) {
     assert(x.n() == y.n());
+    if (const auto* p = mpg::take_pending(1, true, a.data())) {
+        check(mpg_scal_recip_nrm2_f64(p->ctx, p->nparts, a.data(), x.n(), x.data(), y.data()), "scal_recip (nrm2)",
+              p->ctx);
+        return;
+    }
     check(mpg_scal_recip_copy_dev_f64(C, x.n(), a.data(), x.data(), y.data()), "scal_recip");
 }
 template <> void scal_recip<float, Hip>(Scalar<float, Hip> a, Vect<float, Hip> x, Vect<float, Hip> y) {
     assert(x.n() == y.n());
+    if (const auto* p = mpg::take_pending(1, false, a.data())) {
+        check(mpg_scal_recip_nrm2_f32(p->ctx, p->nparts, a.data(), x.n(), x.data(), y.data()), "scal_recip (nrm2)",
+              p->ctx);
+        return;
+    }
     check(mpg_scal_recip_copy_dev_f32(C, x.n(), a.data(), x.data(), y.data()), "scal_recip");
 }
 
@@ -389,6 +506,28 @@ template <> void rot<float, Hip>(Vect<float, Hip> a, Vect<float, Hip> c, Vect<fl
 template <> void gemv<double, Hip>(double alpha, MultiVect<double, Hip> A, Vect<double, Hip> x, double beta,
                                    Vect<double, Hip> y) {
     assert(A.ncols() == x.n() && A.nrows() == y.n());
+    if (A.transposed() && beta == double(0) && mpg::fuse_enabled(4) && y.n() > 0 && y.n() <= 32) {
+        // stage 1 now, stage 2 pending (CGS: the gemv that follows consumes it)
+        mpg_ctx_t c = C;
+        int32_t np = 0;
+        const int st = mpg_gemv_t_partials_f64(c, A.nrows_base(), A.ncols_base(), A.data(), A.stride(), x.data(), &np);
+        if (st == MPG_OK) {
+            mpg::tl_red = mpg::PendingReduction{3, true, c, np, y.data(), (int64_t)y.n(), (double)alpha};
+            return;
+        }
+        if (st != MPG_ERR_UNSUPPORTED) check(st, "gemv^T", c);
+    }
+    if (!A.transposed()) {
+        if (const auto* p = mpg::take_pending(3, true, x.data())) {
+            const int st = p->cols == (int64_t)x.n()
+                               ? mpg_gemv_n_from_t_f64(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
+                                                        A.stride(), p->nparts, (double)p->alpha, x.data(), beta, y.data())
+                               : MPG_ERR_UNSUPPORTED;
+            if (st == MPG_OK) return;
+            if (st != MPG_ERR_UNSUPPORTED) check(st, "gemv (gemv^T)", p->ctx);
+            mpg::tl_red = *p;  // not fusable here: issue its stage 2 first (below, through C)
+        }
+    }
     check(mpg_gemv_f64(C, A.transposed() ? 1 : 0, A.nrows_base(), A.ncols_base(), alpha, A.data(), A.stride(),
                        x.data(), beta, y.data()),
           "gemv");
@@ -396,6 +535,28 @@ template <> void gemv<double, Hip>(double alpha, MultiVect<double, Hip> A, Vect<
 template <> void gemv<float, Hip>(float alpha, MultiVect<float, Hip> A, Vect<float, Hip> x, float beta,
                                   Vect<float, Hip> y) {
     assert(A.ncols() == x.n() && A.nrows() == y.n());
+    if (A.transposed() && beta == float(0) && mpg::fuse_enabled(4) && y.n() > 0 && y.n() <= 32) {
+        // stage 1 now, stage 2 pending (CGS: the gemv that follows consumes it)
+        mpg_ctx_t c = C;
+        int32_t np = 0;
+        const int st = mpg_gemv_t_partials_f32(c, A.nrows_base(), A.ncols_base(), A.data(), A.stride(), x.data(), &np);
+        if (st == MPG_OK) {
+            mpg::tl_red = mpg::PendingReduction{3, false, c, np, y.data(), (int64_t)y.n(), (double)alpha};
+            return;
+        }
+        if (st != MPG_ERR_UNSUPPORTED) check(st, "gemv^T", c);
+    }
+    if (!A.transposed()) {
+        if (const auto* p = mpg::take_pending(3, false, x.data())) {
+            const int st = p->cols == (int64_t)x.n()
+                               ? mpg_gemv_n_from_t_f32(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
+                                                        A.stride(), p->nparts, (float)p->alpha, x.data(), beta, y.data())
+                               : MPG_ERR_UNSUPPORTED;
+            if (st == MPG_OK) return;
+            if (st != MPG_ERR_UNSUPPORTED) check(st, "gemv (gemv^T)", p->ctx);
+            mpg::tl_red = *p;  // not fusable here: issue its stage 2 first (below, through C)
+        }
+    }
     check(mpg_gemv_f32(C, A.transposed() ? 1 : 0, A.nrows_base(), A.ncols_base(), alpha, A.data(), A.stride(),
                        x.data(), beta, y.data()),
           "gemv");

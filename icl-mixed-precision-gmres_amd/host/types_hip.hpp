@@ -35,6 +35,9 @@ void no_recording(const char* what);
 // drop it (a voided recording re-runs its steps, which queue them again)
 void flush_scalar_ops();
 void discard_scalar_ops();
+// a reduction's pending stage 2 (kernels_hip.cpp): issue it now / drop it
+void flush_pending_reduction();
+void discard_pending_reduction();
 
 // The calling thread's current HIP context (stream + workspace). Created
 // lazily on the device named by MPG_DEVICE (default 0) unless a
@@ -142,8 +145,10 @@ public:
         try {
             steps();
             flush_scalar_ops();
+            flush_pending_reduction();
         } catch (const StatusError&) {
             discard_scalar_ops();
+            discard_pending_reduction();
             ok = false;
         }
         mpg_graph_t g = nullptr;

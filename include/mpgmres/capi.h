@@ -105,6 +105,26 @@ int mpg_nrm2_f64(mpg_ctx_t ctx, int64_t n, const double* x, double* result_dev);
 int mpg_nrm2_f32(mpg_ctx_t ctx, int64_t n, const float* x, float* result_dev);
 int mpg_nrm2_f64_host(mpg_ctx_t ctx, int64_t n, const double* x, double* result_host);
 int mpg_nrm2_f32_host(mpg_ctx_t ctx, int64_t n, const float* x, float* result_host);
+/* Split reductions (the operator surface defers stage 2 into the consumer
+ * of the result; kernels_hip.cpp). *_partials runs stage 1 only: *nparts
+ * fp64 partials in the context workspace, valid until the next reduction on
+ * ctx. *_finish is stage 2 (the same result as the one-call form). The
+ * consumers fold stage 2 in, every workgroup with stage 2's own order (same
+ * bits), workgroup 0 storing the result:
+ *   mpg_scal_recip_nrm2_*: h = ||x||, y = (1/h) x   (add_vector, Orthogonalization.hpp:51-60)
+ *   mpg_naxpy_dot_*:       a = <x', y'>, y -= a x   (MGS_Kernel, Orthogonalization.hpp:91-107) */
+int mpg_dot_partials_f64(mpg_ctx_t ctx, int64_t n, const double* x, const double* y, int32_t* nparts);
+int mpg_dot_partials_f32(mpg_ctx_t ctx, int64_t n, const float* x, const float* y, int32_t* nparts);
+int mpg_nrm2_partials_f64(mpg_ctx_t ctx, int64_t n, const double* x, int32_t* nparts);
+int mpg_nrm2_partials_f32(mpg_ctx_t ctx, int64_t n, const float* x, int32_t* nparts);
+int mpg_dot_finish_f64(mpg_ctx_t ctx, int32_t nparts, double* result_dev);
+int mpg_dot_finish_f32(mpg_ctx_t ctx, int32_t nparts, float* result_dev);
+int mpg_nrm2_finish_f64(mpg_ctx_t ctx, int32_t nparts, double* result_dev);
+int mpg_nrm2_finish_f32(mpg_ctx_t ctx, int32_t nparts, float* result_dev);
+int mpg_scal_recip_nrm2_f64(mpg_ctx_t ctx, int32_t nparts, double* h_dev, int64_t n, const double* x, double* y);
+int mpg_scal_recip_nrm2_f32(mpg_ctx_t ctx, int32_t nparts, float* h_dev, int64_t n, const float* x, float* y);
+int mpg_naxpy_dot_f64(mpg_ctx_t ctx, int32_t nparts, double* a_dev, int64_t n, const double* x, double* y);
+int mpg_naxpy_dot_f32(mpg_ctx_t ctx, int32_t nparts, float* a_dev, int64_t n, const float* x, float* y);
 /* the unrounded fp64 accumulator of <x, y> (one rank's share of a
  * distributed dot / squared norm, summed across ranks before rounding) */
 int mpg_dot_acc_f64(mpg_ctx_t ctx, int64_t n, const double* x, const double* y, double* acc_dev);
@@ -200,6 +220,20 @@ int mpg_gemv_f64(mpg_ctx_t ctx, int trans, int64_t rows, int64_t cols, double al
                  const double* A, int64_t lda, const double* x, double beta, double* y);
 int mpg_gemv_f32(mpg_ctx_t ctx, int trans, int64_t rows, int64_t cols, float alpha,
                  const float* A, int64_t lda, const float* x, float beta, float* y);
+/* gemv^T split the same way (<= 32 columns): stage 1, stage 2, and gemv (N)
+ * with x = alpha_t * (the pending sums) formed in-launch and stored by
+ * workgroup 0 (CGS_Kernel: h = V^T w, then w -= V h; MPG_ERR_UNSUPPORTED
+ * unless A, lda and y allow the 16-B quad form) */
+int mpg_gemv_t_partials_f64(mpg_ctx_t ctx, int64_t rows, int64_t cols, const double* A, int64_t lda, const double* x,
+                            int32_t* nparts);
+int mpg_gemv_t_partials_f32(mpg_ctx_t ctx, int64_t rows, int64_t cols, const float* A, int64_t lda, const float* x,
+                            int32_t* nparts);
+int mpg_gemv_t_finish_f64(mpg_ctx_t ctx, int32_t nparts, int64_t cols, double alpha, double beta, double* y);
+int mpg_gemv_t_finish_f32(mpg_ctx_t ctx, int32_t nparts, int64_t cols, float alpha, float beta, float* y);
+int mpg_gemv_n_from_t_f64(mpg_ctx_t ctx, int64_t rows, int64_t cols, double alpha, const double* A, int64_t lda,
+                          int32_t nparts, double alpha_t, double* x, double beta, double* y);
+int mpg_gemv_n_from_t_f32(mpg_ctx_t ctx, int64_t rows, int64_t cols, float alpha, const float* A, int64_t lda,
+                          int32_t nparts, float alpha_t, float* x, float beta, float* y);
 /* triangular solve, non-unit diagonal, single workgroup (n <= 4096).
  * upper = 1 'U', 0 'L'; trans = 1 solves with A^T (kernels_mkl.cpp:291-321) */
 int mpg_trsv_f64(mpg_ctx_t ctx, int upper, int trans, int64_t n, const double* A, int64_t lda, double* x);

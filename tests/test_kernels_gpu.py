@@ -396,3 +396,48 @@ def test_scalar_program_matches_single_ops(hip, t):
     assert out["program"][4][0] != 0
     with pytest.raises(RuntimeError):
         hip.check(hip.lib.mpg_scalar_program(hip.ctx, (ScalarOp * 9)(), 9), "too long")
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
+def test_split_reductions_match_one_call(hip, t):
+    """Stage 1 / stage 2 split reductions and the consumers that fold stage 2
+    in (the operator surface's deferred reductions) give the one-call forms'
+    bits: nrm2 -> 1/h scal, dot -> naxpy, gemv^T -> gemv."""
+    dt = np.float64 if t == "f64" else np.float32
+    CT = C.c_double if t == "f64" else C.c_float
+    g = rng(17)
+    n = 300_001
+    x, y = g.normal(size=n).astype(dt), g.normal(size=n).astype(dt)
+    dx, dy = hip.buf(x), hip.buf(y)
+    np_ = C.c_int32()
+    # nrm2 -> scal_recip
+    h1, h2 = hip.buf(1, dt), hip.buf(1, dt)
+    o1, o2 = hip.buf(n, dt), hip.buf(n, dt)
+    hip.call(f"mpg_nrm2_{t}", C.c_int64(n), dx.p, h1.p)
+    hip.call(f"mpg_scal_recip_copy_dev_{t}", C.c_int64(n), h1.p, dx.p, o1.p)
+    hip.call(f"mpg_nrm2_partials_{t}", C.c_int64(n), dx.p, C.byref(np_))
+    hip.call(f"mpg_scal_recip_nrm2_{t}", np_, h2.p, C.c_int64(n), dx.p, o2.p)
+    assert np.array_equal(h1.get(), h2.get()) and np.array_equal(o1.get(), o2.get())
+    # dot -> naxpy
+    a1, a2 = hip.buf(1, dt), hip.buf(1, dt)
+    z1, z2 = hip.buf(y), hip.buf(y)
+    hip.call(f"mpg_dot_{t}", C.c_int64(n), dx.p, dy.p, a1.p)
+    hip.call(f"mpg_naxpy_dev_{t}", C.c_int64(n), a1.p, dx.p, z1.p)
+    hip.call(f"mpg_dot_partials_{t}", C.c_int64(n), dx.p, dy.p, C.byref(np_))
+    hip.call(f"mpg_naxpy_dot_{t}", np_, a2.p, C.c_int64(n), dx.p, z2.p)
+    assert np.array_equal(a1.get(), a2.get()) and np.array_equal(z1.get(), z2.get())
+    # gemv^T -> gemv on a padded panel (16-B quad form), and the finish form
+    rows, cols = 200_000, 17
+    lda = (rows + 63) // 64 * 64
+    V = g.normal(size=(cols, lda)).astype(dt)
+    w = g.normal(size=rows).astype(dt)
+    dV, dw1, dw2 = hip.buf(V.ravel()), hip.buf(w), hip.buf(w)
+    c1, c2, c3 = hip.buf(cols, dt), hip.buf(cols, dt), hip.buf(cols, dt)
+    hip.call(f"mpg_gemv_{t}", 1, C.c_int64(rows), C.c_int64(cols), CT(1.0), dV.p, C.c_int64(lda), dw1.p, CT(0.0), c1.p)
+    hip.call(f"mpg_gemv_{t}", 0, C.c_int64(rows), C.c_int64(cols), CT(-1.0), dV.p, C.c_int64(lda), c1.p, CT(1.0), dw1.p)
+    hip.call(f"mpg_gemv_t_partials_{t}", C.c_int64(rows), C.c_int64(cols), dV.p, C.c_int64(lda), dw2.p, C.byref(np_))
+    hip.call(f"mpg_gemv_t_finish_{t}", np_, C.c_int64(cols), CT(1.0), CT(0.0), c3.p)
+    hip.call(f"mpg_gemv_n_from_t_{t}", C.c_int64(rows), C.c_int64(cols), CT(-1.0), dV.p, C.c_int64(lda), np_, CT(1.0),
+             c2.p, CT(1.0), dw2.p)
+    assert np.array_equal(c1.get(), c2.get()) and np.array_equal(c1.get(), c3.get())
+    assert np.array_equal(dw1.get(), dw2.get())

@@ -28,9 +28,10 @@ def _case_id(c):
 # (engine, storage, environment): the fused engine on both Arnoldi SpMV
 # storages (CSR row blocks, SELL-64);: MPG_SELL_WINDOW=0 gathers v_k from memory
 # instead of the LDS window; the others are launch-count experiments
-FLAGS = ("MPG_SURFACE_GRAPH", "MPG_SURFACE_BATCH", "MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS", "MPG_SELL_WINDOW", "MPG_SURFACE_SELL", "MPG_FUSE_DOTS")
+FLAGS = ("MPG_SURFACE_GRAPH", "MPG_SURFACE_BATCH", "MPG_SURFACE_FUSE", "MPG_COMBINE", "MPG_FOLD_GIVENS", "MPG_CGS_PARTIALS", "MPG_SELL_WINDOW", "MPG_SURFACE_SELL", "MPG_FUSE_DOTS")
 ON_BY_DEFAULT = ("MPG_SELL_WINDOW", "MPG_SURFACE_SELL")
-ENGINES = {"surface": ("surface", "auto", {}), "surface-eager": ("surface", "auto", {"MPG_SURFACE_GRAPH": "0", "MPG_SURFACE_BATCH": "0"}),
+ENGINES = {"surface": ("surface", "auto", {}), "surface-eager": ("surface", "auto", {"MPG_SURFACE_GRAPH": "0", "MPG_SURFACE_BATCH": "0",
+                                                 "MPG_SURFACE_FUSE": "0"}),
            "surface-csr": ("surface", "auto", {"MPG_SURFACE_SELL": "0"}),
            "fused-csr": ("fused", "csr", {}),
            "fused-sell": ("fused", "sell", {}), "fused-gather": ("fused", "sell", {"MPG_SELL_WINDOW": "0"}),
@@ -237,8 +238,9 @@ def test_surface_cycle_program_matches_eager(mpg, orth, mode, prec, monkeypatch)
     """The operator-surface driver records its Arnoldi steps once per solve
     (CycleProgram<Hip>: first cycle eager, second recorded, later replayed)
     when the strategy makes no decision inside a cycle. Replays must give the
-    same bits as issuing every call on its own (MPG_SURFACE_GRAPH=0 and
-    MPG_SURFACE_BATCH=0: no recording, no scalar-op batching); an ILU apply,
+    same bits as issuing every call on its own (MPG_SURFACE_GRAPH=0,
+    MPG_SURFACE_BATCH=0, MPG_SURFACE_FUSE=0: no recording, no scalar-op
+    batching, every reduction's stage 2 its own launch); an ILU apply,
     which reads its fault word, voids the recording and runs eagerly."""
     A = mpg.gen_band(100_000, 5, 4, seed=7)
     xt = mpg.rand_vect(A.nrows, 42)
@@ -248,6 +250,7 @@ def test_surface_cycle_program_matches_eager(mpg, orth, mode, prec, monkeypatch)
     for g in ("1", "0"):
         monkeypatch.setenv("MPG_SURFACE_GRAPH", g)
         monkeypatch.setenv("MPG_SURFACE_BATCH", g)
+        monkeypatch.setenv("MPG_SURFACE_FUSE", g)
         before = mpg.cycle_program_counts()
         got[g] = mpg.solve(A, b, xt, **opts)
         after = mpg.cycle_program_counts()
