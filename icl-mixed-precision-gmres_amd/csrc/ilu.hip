@@ -2,11 +2,13 @@
 // on gfx950 (include/mpgmres/ilu.h).
 //
 // Factorisation and solves hand rows out in order through an atomic ticket:
-// a wave64 takes the next row, waits (handoff.hpp) only for the rows that
-// row reads, computes it, stores it write-through and raises the row's
-// flag. A wave only ever waits for rows taken earlier by running waves, so
-// the schedule always progresses; every wait is bounded (a fault is
-// recorded instead of hanging the GPU).
+// a wave64 (factorisation) or a lane (solves) takes the next row, waits
+// only for the rows that row reads, computes it and stores it write-through;
+// the factorisation then raises the row's flag (handoff.hpp), the solves
+// let the stored value itself be the flag (k_ilu_trsv_tagged). A row only
+// ever waits for rows taken earlier by running waves, so the schedule
+// always progresses; every wait is bounded (a fault is recorded instead of
+// hanging the GPU).
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -36,9 +38,10 @@ constexpr int kPersistGroups = 2048;         // 8 workgroups per CU
 constexpr int kSolveGroups = 64;
 constexpr uint64_t kDeadline = 3000000000ull;  // 30 s of the 100 MHz clock: a wave gives up (fault 2)
 
-// sync block layout (ints): [0, n) factor / L flags, [n, 2n) U flags, then
-// tickets at 2n + 0 / 32 / 64 / 96 (separate 128-B lines), the fault word at 2n + 128
-inline size_t sync_ints(int n) { return 2 * (size_t)n + 160; }
+// sync block layout (ints): [0, n) factorisation flags, then tickets at
+// n + 0 / 32 / 64 (factorisation, L solve, U solve: separate 128-B lines),
+// the fault word at n + 128
+inline size_t sync_ints(int n) { return (size_t)n + 160; }
 
 // ---------------------------------------------------------------- set-up
 __global__ void k_find_diag(int n, const int* __restrict__ rowptr, const int* __restrict__ col, int* __restrict__ diag,
@@ -163,25 +166,77 @@ __global__ void k_dinv(int n, const int* __restrict__ diag, const T* __restrict_
 }
 
 // ---------------------------------------------------------------- triangular solves
-// x := L^-1 x (unit lower) or U^-1 x (upper), in place, level-scheduled and
+// out := L^-1 rhs (unit lower) or U^-1 rhs (upper), level-scheduled and
 // sync-free. mpg_ilu0_create sorts the rows by dependency level (a row's
 // level is one more than the highest level among the rows its off-diagonal
 // entries read) and cuts every level into chunks of <= 64 rows, so the rows
 // of a chunk never depend on each other. A wave takes the next chunk from an
 // atomic ticket (chunks in level order: a wave only waits for rows of
 // earlier chunks, taken by running waves, so the schedule always
-// progresses), and each lane solves one row: it waits for the flags of the
-// rows it reads, the wave takes one agent-scope acquire, then the lane
-// forms x_i = T((x_i - sum_j a_ij x_j) [/ u_ii]) with the sum in fp64 in CSR
-// order, stores it write-through, drains, and raises the row's flag.
-// One row per lane (the previous form took one row per wave, one ticket per
-// row, 2048 workgroups): LAP-1M's L + U solves from ~40 ms to 3.0 ms.
+// progresses), and each lane solves one row, x_i = T((b_i - sum_j a_ij x_j)
+// [/ u_ii]) with the sum in fp64 in CSR order, rounded once.
+//
+// The VALUE is its own flag: the output vector starts filled with a tag (a
+// signalling-NaN bit pattern that no arithmetic produces -- results are
+// quiet NaNs at worst, and a result equal to the tag is stored as the
+// canonical NaN), a lane polls the values of the rows it reads (relaxed
+// agent-scope loads, four dependencies in flight at once) until none is the
+// tag, and stores its own value write-through. The lane that reads rhs[row]
+// overwrites it with the tag, so after the L solve x is the tagged output
+// buffer of the U solve.
+//
+// History (LAP-1M, mixed CGS GMRES(30) with ILU(0), tools/prec_bench.py):
+// one row per wave and a ticket per row, 2048 workgroups: ~40 ms per L + U;
+// one row per lane with a done-flag per row (store, drain, flag store, flag
+// poll, agent acquire, value loads: ~5 us a level hop): 3.0 ms, 318 it/s;
+// the value as flag (store, value poll): 746 it/s, ~2.2 us a hop.
+template <class T>
+struct TrsvTag;
+template <>
+struct TrsvTag<double> {
+    typedef unsigned long long U;
+    typedef gu64 G;
+    static constexpr U kBits = 0x7FF5A5A5A5A5A5A5ull;
+    static constexpr U kQuiet = 0x7FF8000000000000ull;
+    __device__ static double val(U u) { return __longlong_as_double((long long)u); }
+    __device__ static U bits(double v) { return (U)__double_as_longlong(v); }
+};
+template <>
+struct TrsvTag<float> {
+    typedef unsigned U;
+    typedef gu32 G;
+    static constexpr U kBits = 0x7FA5A5A5u;
+    static constexpr U kQuiet = 0x7FC00000u;
+    __device__ static float val(U u) { return __uint_as_float(u); }
+    __device__ static U bits(float v) { return __float_as_uint(v); }
+};
+
+template <class T>
+__device__ __forceinline__ typename TrsvTag<T>::U poll_tagged(const T* p, int* err, uint64_t bound) {
+    typedef TrsvTag<T> Tg;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    typename Tg::U v;
+    while ((v = __hip_atomic_load((const typename Tg::G*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == Tg::kBits) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > bound) {  // give up: the tag is a NaN, the row goes on
+            __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+    }
+    return v;
+}
+
+constexpr int kTagBatch = 4;  // dependencies polled together
 template <class T, bool UPPER>
-__global__ __launch_bounds__(kBlock) void k_ilu_trsv(int nchunks, const int* __restrict__ chunk,
-                                                     const int* __restrict__ ord, const int* __restrict__ rowptr,
-                                                     const int* __restrict__ col, const int* __restrict__ diag,
-                                                     const T* __restrict__ lu, T* x, int* done, unsigned* ticket,
-                                                     int* err, uint64_t wait_bound) {
+__global__ __launch_bounds__(kBlock) void k_ilu_trsv_tagged(int nchunks, const int* __restrict__ chunk,
+                                                            const int* __restrict__ ord,
+                                                            const int* __restrict__ rowptr,
+                                                            const int* __restrict__ col,
+                                                            const int* __restrict__ diag, const T* __restrict__ lu,
+                                                            T* rhs, T* out, unsigned* ticket, int* err,
+                                                            uint64_t wait_bound) {
+    typedef TrsvTag<T> Tg;
+    typedef typename Tg::U U;
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     for (;;) {
@@ -194,26 +249,58 @@ __global__ __launch_bounds__(kBlock) void k_ilu_trsv(int nchunks, const int* __r
         t = __shfl(t, 0, kWave);
         if (t >= nchunks) break;
         const int c0 = chunk[t], cnt = chunk[t + 1] - c0;
-        const bool live = lane < cnt;
-        int row = 0, d = 0, j0 = 0, j1 = 0;
-        if (live) {
-            row = ord[c0 + lane];
-            d = diag[row];
-            j0 = UPPER ? d + 1 : rowptr[row];
-            j1 = UPPER ? rowptr[row + 1] : d;
-            for (int j = j0; j < j1; ++j) wait_flag(done + col[j], err, wait_bound);
-        }
-        acquire_agent();
-        if (live) {
+        if (lane < cnt) {
+            const int row = ord[c0 + lane], d = diag[row];
+            const int j0 = UPPER ? d + 1 : rowptr[row];
+            const int j1 = UPPER ? rowptr[row + 1] : d;
+            const T b = rhs[row];
+            const T piv = UPPER ? lu[d] : T(1);
+            rhs[row] = TrsvTag<T>::val(Tg::kBits);
             double s = 0.0;
-            for (int j = j0; j < j1; ++j) s += (double)lu[j] * (double)x[col[j]];
-            double r = (double)x[row] - s;
-            if (UPPER) r = r / (double)lu[d];
-            store_wt(x + row, (T)r);
+            for (int j = j0; j < j1; j += kTagBatch) {
+                int c[kTagBatch];
+                U v[kTagBatch];
+                T a[kTagBatch];
+#pragma unroll
+                for (int q = 0; q < kTagBatch; ++q) c[q] = j + q < j1 ? col[j + q] : -1;
+#pragma unroll
+                for (int q = 0; q < kTagBatch; ++q) {
+                    v[q] = c[q] >= 0 ? __hip_atomic_load((const typename Tg::G*)(out + c[q]), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : U(0);
+                    a[q] = c[q] >= 0 ? lu[j + q] : T(0);
+                }
+#pragma unroll
+                for (int q = 0; q < kTagBatch; ++q)
+                    if (c[q] >= 0 && v[q] == Tg::kBits) v[q] = poll_tagged(out + c[q], err, wait_bound);
+#pragma unroll
+                for (int q = 0; q < kTagBatch; ++q)
+                    if (c[q] >= 0) s += (double)a[q] * (double)Tg::val(v[q]);
+            }
+            double r = (double)b - s;
+            if (UPPER) r = r / (double)piv;
+            T res = (T)r;
+            if (Tg::bits(res) == Tg::kBits) res = Tg::val(Tg::kQuiet);
+            store_wt(out + row, res);
         }
-        drain_stores();
-        if (live) set_flag(done + row);
     }
+}
+
+// out := tag, and the two solve tickets (32 ints apart) zeroed
+template <class T>
+__global__ void k_trsv_tag_fill(int n, T* __restrict__ out, unsigned* __restrict__ tickets) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = TrsvTag<T>::val(TrsvTag<T>::kBits);
+    if (i < 2) tickets[32 * i] = 0u;
+}
+
+// dst := src, src := tag (a serial solve next to a tagged one)
+template <class T>
+__global__ void k_trsv_tag_move(int n, T* __restrict__ src, T* __restrict__ dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dst[i] = src[i];
+    src[i] = TrsvTag<T>::val(TrsvTag<T>::kBits);
 }
 
 // The same solve for matrices whose dependency levels hold few rows (banded:
@@ -370,6 +457,7 @@ struct mpg_ilu {
     int* sync = nullptr;
     uint64_t wait_bound = kWaitBound;  // per-wait bound of the level-scheduled solves (test hook)
     void* w[2] = {nullptr, nullptr};  // ILU-Jacobi: right-hand side and the second sweep buffer
+    void* tagbuf = nullptr;           // tagged solves: L^-1 b between the two directions
     unsigned long long* scratch = nullptr;
     // level schedules of the two triangular solves: rows by level, and
     // chunk starts (<= 64 rows, never across a level) into that order
@@ -386,8 +474,8 @@ struct mpg_ilu {
 
     size_t tsize() const { return type == 0 ? 8 : 4; }
     void* values() const { return type == 0 ? (void*)lu64 : (void*)lu32; }
-    unsigned* ticket(int which) { return reinterpret_cast<unsigned*>(sync + 2 * (size_t)n + 32 * which); }
-    int* err() { return sync + 2 * (size_t)n + 128; }
+    unsigned* ticket(int which) { return reinterpret_cast<unsigned*>(sync + (size_t)n + 32 * which); }
+    int* err() { return sync + (size_t)n + 128; }
 };
 
 namespace {
@@ -397,12 +485,6 @@ int by_type(int type, F&& f) {
     if (type == 0) return f(double());
     if (type == 1) return f(float());
     return MPG_ERR_UNSUPPORTED;
-}
-
-int reset_sync(mpg_ilu* L) {
-    // flags and tickets (the fault word, past them, stays sticky)
-    MPG_HIP(L->ctx, hipMemsetAsync(L->sync, 0, (2 * (size_t)L->n + 128) * sizeof(int), L->ctx->stream));
-    return MPG_OK;
 }
 
 // (the factorisation keeps 8 workgroups per CU: 64 / 256 of them took
@@ -495,6 +577,7 @@ int mpg_ilu0_create(mpg_ctx_t ctx, mpg_csr_t A, const double* val64, int type, m
     if (!ok(hipMalloc((void**)&L->lu64, zb * 8)) || !ok(hipMalloc((void**)&L->diag, nb * 4)) ||
         !ok(hipMalloc(&L->dinv, nb * L->tsize())) || !ok(hipMalloc((void**)&L->sync, sync_ints(n) * 4)) ||
         !ok(hipMalloc(&L->w[0], nb * L->tsize())) || !ok(hipMalloc(&L->w[1], nb * L->tsize())) ||
+        !ok(hipMalloc(&L->tagbuf, nb * L->tsize())) ||
         !ok(hipMalloc((void**)&L->scratch, 64)) || (type == 1 && !ok(hipMalloc((void**)&L->lu32, zb * 4))))
         return fail(MPG_ERR_ALLOC);
     if (!ok(hipMemsetAsync(L->sync, 0, sync_ints(n) * 4, s)) || !ok(hipMemsetAsync(L->scratch, 0, 64, s)))
@@ -577,7 +660,7 @@ int mpg_ilu_destroy(mpg_ilu_t L) {
     if (L->ctx) (void)hipStreamSynchronize(L->ctx->stream);
     void* ps[] = {L->lu64,    L->lu32,    L->diag,     L->dinv,     L->sync,     L->w[0],    L->w[1],
                   L->scratch, L->ord[0],  L->ord[1],   L->chunk[0], L->chunk[1], L->stage[0], L->stage[1],
-                  L->eoff[0], L->eoff[1]};
+                  L->eoff[0], L->eoff[1], L->tagbuf};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete L;
@@ -587,7 +670,6 @@ int mpg_ilu_destroy(mpg_ilu_t L) {
 int mpg_ilu_solve(mpg_ctx_t ctx, mpg_ilu_t L, void* x) {
     if (!ctx || !L || (!x && L->n)) return MPG_ERR_ARG;
     if (L->n == 0) return MPG_OK;
-    if (int st = reset_sync(L)) return st;
     const int n = L->n;
     // one wave per chunk in flight at most: a wave per 64 rows, <= 8 workgroups per CU
     static const int cap = [] {
@@ -595,26 +677,34 @@ int mpg_ilu_solve(mpg_ctx_t ctx, mpg_ilu_t L, void* x) {
         return e && std::atoi(e) > 0 ? std::atoi(e) : kSolveGroups;
     }();
     auto grid = [&](int u) { return std::max(1, std::min(cap, (L->nchunks[u] + kWaves - 1) / kWaves)); };
+    // tagged level solves: L x -> y (x left tagged), U y -> x; a serial
+    // direction solves in place in x, moved to / from y next to a tagged one
+    const int g = (n + kBlock - 1) / kBlock;
+    hipStream_t s = ctx->stream;
     int st = by_type(L->type, [&](auto t) {
         using T = decltype(t);
         const T* lu = static_cast<const T*>(L->values());
         T* xv = static_cast<T*>(x);
-        if (L->serial[0])
-            k_ilu_trsv_serial<T, false><<<1, kBlock, 0, ctx->stream>>>(n, L->nstages[0], L->stage[0], L->eoff[0],
-                                                                       L->A->rowptr, L->A->col, L->diag, lu, xv);
-        else
-            k_ilu_trsv<T, false><<<grid(0), kBlock, 0, ctx->stream>>>(L->nchunks[0], L->chunk[0], L->ord[0],
-                                                                        L->A->rowptr, L->A->col, L->diag, lu, xv,
-                                                                        L->sync, L->ticket(1), L->err(),
-                                                                        L->wait_bound);
-        if (L->serial[1])
-            k_ilu_trsv_serial<T, true><<<1, kBlock, 0, ctx->stream>>>(n, L->nstages[1], L->stage[1], L->eoff[1],
-                                                                      L->A->rowptr, L->A->col, L->diag, lu, xv);
-        else
-            k_ilu_trsv<T, true><<<grid(1), kBlock, 0, ctx->stream>>>(L->nchunks[1], L->chunk[1], L->ord[1],
-                                                                       L->A->rowptr, L->A->col, L->diag, lu, xv,
-                                                                       L->sync + n, L->ticket(2), L->err(),
-                                                                       L->wait_bound);
+        T* yv = static_cast<T*>(L->tagbuf);
+        if (!L->serial[0] || !L->serial[1]) k_trsv_tag_fill<T><<<g, kBlock, 0, s>>>(n, yv, L->ticket(1));
+        if (L->serial[0]) {
+            k_ilu_trsv_serial<T, false><<<1, kBlock, 0, s>>>(n, L->nstages[0], L->stage[0], L->eoff[0],
+                                                             L->A->rowptr, L->A->col, L->diag, lu, xv);
+            if (!L->serial[1]) k_trsv_tag_move<T><<<g, kBlock, 0, s>>>(n, xv, yv);
+        } else {
+            k_ilu_trsv_tagged<T, false><<<grid(0), kBlock, 0, s>>>(L->nchunks[0], L->chunk[0], L->ord[0],
+                                                                   L->A->rowptr, L->A->col, L->diag, lu, xv,
+                                                                   yv, L->ticket(1), L->err(), L->wait_bound);
+        }
+        if (L->serial[1]) {
+            if (!L->serial[0]) k_trsv_tag_move<T><<<g, kBlock, 0, s>>>(n, yv, xv);
+            k_ilu_trsv_serial<T, true><<<1, kBlock, 0, s>>>(n, L->nstages[1], L->stage[1], L->eoff[1],
+                                                            L->A->rowptr, L->A->col, L->diag, lu, xv);
+        } else {
+            k_ilu_trsv_tagged<T, true><<<grid(1), kBlock, 0, s>>>(L->nchunks[1], L->chunk[1], L->ord[1],
+                                                                  L->A->rowptr, L->A->col, L->diag, lu, yv,
+                                                                  xv, L->ticket(2), L->err(), L->wait_bound);
+        }
         return (int)MPG_OK;
     });
     if (st) return st;

@@ -53,7 +53,7 @@ void hck(hipError_t e, const char* what) {
 // ---------------------------------------------------------------- RCCL
 class RcclComm : public Comm {
     ncclComm_t comm_ = nullptr;
-    int rank_, size_, n_local_;
+    int rank_, size_;
     mpg_ctx_t ctx_;
     std::vector<int32_t> recv_pos_, recv_cnt_;
     std::vector<std::unique_ptr<DevMem>> send_idx_, send_buf_;
@@ -62,7 +62,7 @@ class RcclComm : public Comm {
 
 public:
     RcclComm(mpg_ctx_t ctx, const mpg_halo& h, const char* id, int nranks, int rank)
-        : rank_(rank), size_(nranks), n_local_(h.n_local), ctx_(ctx), recv_pos_(h.recv_pos), recv_cnt_(h.recv_cnt) {
+        : rank_(rank), size_(nranks), ctx_(ctx), recv_pos_(h.recv_pos), recv_cnt_(h.recv_cnt) {
         ncclUniqueId uid;
         std::memcpy(&uid, id, sizeof uid);
         nck(ncclCommInitRank(&comm_, nranks, uid, rank), "ncclCommInitRank");
@@ -162,14 +162,14 @@ struct Hub {
 
 class LoopbackComm : public Comm {
     Hub& hub_;
-    int rank_, n_local_;
+    int rank_;
     mpg_ctx_t ctx_;
     std::vector<int32_t> recv_off_, recv_pos_, recv_cnt_;
     std::vector<std::unique_ptr<DevMem>> src_idx_;  // per peer: indices in the peer's numbering
 
 public:
     LoopbackComm(Hub& hub, mpg_ctx_t ctx, const mpg_halo& h)
-        : hub_(hub), rank_(h.rank), n_local_(h.n_local), ctx_(ctx), recv_off_(h.recv_off), recv_pos_(h.recv_pos),
+        : hub_(hub), rank_(h.rank), ctx_(ctx), recv_off_(h.recv_off), recv_pos_(h.recv_pos),
           recv_cnt_(h.recv_cnt) {
         src_idx_.resize(h.nranks);
         for (int q = 0; q < h.nranks; ++q) {
@@ -227,7 +227,7 @@ private:
 // processes on one device. Not capturable (host waits).
 class HostComm : public Comm {
     mpg_host_transport t_;
-    int rank_, size_, n_local_;
+    int rank_, size_;
     mpg_ctx_t ctx_;
     std::vector<int32_t> recv_pos_, recv_cnt_, send_cnt_;
     std::vector<std::unique_ptr<DevMem>> send_idx_, send_dev_;
@@ -240,7 +240,7 @@ class HostComm : public Comm {
 
 public:
     HostComm(mpg_ctx_t ctx, const mpg_halo& h, const mpg_host_transport& t, int nranks, int rank)
-        : t_(t), rank_(rank), size_(nranks), n_local_(h.n_local), ctx_(ctx), recv_pos_(h.recv_pos),
+        : t_(t), rank_(rank), size_(nranks), ctx_(ctx), recv_pos_(h.recv_pos),
           recv_cnt_(h.recv_cnt) {
         send_cnt_.assign(nranks, 0);
         send_idx_.resize(nranks);

@@ -18,10 +18,12 @@
  * waiting only on the rows it reads (sync-free): the same data-dependency
  * schedule cuSPARSE's level policy follows, with no host round trip.
  *
- * Triangular solves: unit-lower L then upper U, in place, the same
- * sync-free row schedule (L forward, U backward), fp64 row sums rounded
- * once to T. Depth = the longest dependency chain of the matrix (natural-
- * order 3-D stencils: ~nx+ny+nz; banded matrices: n — use ILU-Jacobi).
+ * Triangular solves: unit-lower L then upper U, fp64 row sums rounded
+ * once to T; x in, x out. Rows are level-scheduled and sync-free, with each
+ * value its own ready flag (an internal buffer pre-filled with a NaN tag
+ * the arithmetic never produces). Depth = the longest dependency chain of
+ * the matrix (natural-order 3-D stencils: ~nx+ny+nz; banded matrices: n,
+ * run by one workgroup serially — or use ILU-Jacobi).
  *
  * ILU-Jacobi: `steps` Jacobi sweeps per factor, every row independent
  * (ilusv_jacobi with the generic ilu_jacobi_mv, kernels.hpp:171-248).
