@@ -1,10 +1,11 @@
 """Kernel statistics from a rocprofv3 results database (rocpd SQLite, the
-default output format of this ROCm's rocprofv3), in the layout of
+default output format of this ROCm's rocprofv3) or a `--output-format csv`
+kernel_trace.csv, in the layout of
 `rocprofv3 --stats` kernel_stats.csv, plus a per-(kernel, grid) split that
 separates the same kernel run on two problem sizes in one process (bench.py
 times BAND-10M and the BAND-100M HBM-scale figure).
 
-usage: python tools/rocpd_summary.py RESULTS.db OUT_PREFIX
+usage: python tools/rocpd_summary.py RESULTS.db|KERNEL_TRACE.csv OUT_PREFIX
   writes OUT_PREFIX_kernel_stats.csv and OUT_PREFIX_kernel_grid.csv
 """
 import csv
@@ -20,9 +21,15 @@ def short(name: str) -> str:
 
 
 def main():
-    db = sqlite3.connect(sys.argv[1])
     prefix = sys.argv[2]
-    rows = db.execute("select name, start, end, grid_x, workgroup_x from kernels order by start").fetchall()
+    if sys.argv[1].endswith(".csv"):
+        with open(sys.argv[1], newline="") as f:
+            rows = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["Grid_Size_X"]),
+                     int(r["Workgroup_Size_X"])) for r in csv.DictReader(f)]
+        rows.sort(key=lambda r: r[1])
+    else:
+        db = sqlite3.connect(sys.argv[1])
+        rows = db.execute("select name, start, end, grid_x, workgroup_x from kernels order by start").fetchall()
     by_name = defaultdict(list)
     by_grid = defaultdict(list)
     for name, s, e, g, w in rows:
