@@ -165,6 +165,42 @@ def test_ilu_serial_solve_matches_levels(hip, mpg, monkeypatch, mat, dt):
     assert np.array_equal(out["1"][0], out["0"][0])
 
 
+@pytest.mark.parametrize("dt", [np.float64, np.float32], ids=["f64", "f32"])
+def test_ilu_level_solve_tag_pattern_and_nan_inputs(hip, mpg, monkeypatch, dt):
+    """The level-scheduled solves use a signalling-NaN bit pattern as the
+    'not yet solved' tag of their output. A right-hand side holding exactly
+    that pattern, a quiet NaN and an Inf must neither hang a poll nor fault:
+    the rows they reach come out NaN/Inf, and every other row keeps the bits
+    of the serial chain (which has no tag). The matrix is two decoupled
+    1500-row bands, the special values all go into the second one, so the
+    first block's rows stay finite."""
+    B = mpg.gen_band(1500, 5, 4, seed=3)
+    A = mpg.Csr(3000, 3000, np.concatenate([B.rowptr, B.rowptr[1:] + B.nnz]).astype(np.int32),
+                np.concatenate([B.col, B.col + 1500]).astype(np.int32), np.concatenate([B.val, B.val]))
+    x = mpg.rand_vect(A.nrows, 5).astype(dt)
+    tag = np.array([0x7FF5A5A5A5A5A5A5 if dt == np.float64 else 0x7FA5A5A5],
+                   np.uint64 if dt == np.float64 else np.uint32).view(dt)[0]
+    x[1600] = tag
+    x[2000] = np.nan
+    x[2500] = np.inf
+    out = {}
+    for env in ("1", "0"):  # serial chain, then the level schedule (tagged)
+        monkeypatch.setenv("MPG_ILU_SERIAL", env)
+        L = Ilu(hip, A, dt)
+        try:
+            out[env] = (L.apply(x, "ilu"), hip.lib.mpg_ilu_solve_mode(L.h))  # apply asserts no fault
+        finally:
+            L.close()
+    assert out["1"][1] == 3 and out["0"][1] == 0
+    s, lv = out["1"][0], out["0"][0]
+    assert np.isnan(lv[1500:]).any() and np.isfinite(lv[:1500]).all()
+    assert np.array_equal(np.isnan(s), np.isnan(lv))
+    ok = ~np.isnan(s)
+    assert np.array_equal(s[ok], lv[ok])
+    bits = lv.view(np.uint64 if dt == np.float64 else np.uint32)
+    assert not (bits == np.array([tag]).view(bits.dtype)[0]).any()  # no tag left in the output
+
+
 def test_ilu_rejects_missing_diagonal(hip, mpg):
     A = mpg.Csr(3, 3, np.array([0, 1, 2, 3], np.int32), np.array([1, 1, 2], np.int32), np.ones(3))
     drp, dci, dv = hip.buf(A.rowptr), hip.buf(A.col), hip.buf(A.val)
