@@ -27,6 +27,7 @@ using namespace mpg;
 namespace {
 
 constexpr int kRowCap = 512;                 // entries of one row staged in LDS
+constexpr int kUpCap = 128;                  // pivot rows' upper entries staged per row (else read in place)
 constexpr int kWaves = kBlock / kWave;       // 4 rows in flight per workgroup
 constexpr int kPersistGroups = 2048;         // 8 workgroups per CU
 // level-scheduled solves: few spinning waves. 64 workgroups (one per CU on a
@@ -79,17 +80,27 @@ __global__ void k_abs_rowsum_max(int n, const int* __restrict__ rowptr, const do
 // entry, the r-th of its column in the row's remaining run, meets the r-th
 // entry of that column in row k (duplicates handled as the merge does).
 // Products and differences are not contracted, as in the reference loop.
+// Rows are handed out in the L solve's dependency-level order (a row reads
+// exactly the rows its L part names): in row order the rows in flight on a
+// natural-order 3-D stencil were one chain of x-line hand-offs wide.
 #pragma clang fp contract(off)
 __global__ __launch_bounds__(kBlock) void k_ilu0_factor(int n, const int* __restrict__ rowptr,
                                                         const int* __restrict__ col, const int* __restrict__ diag,
                                                         double* lu, double eps,
                                                         const unsigned long long* __restrict__ rowmax, int* done,
-                                                        unsigned* ticket, int* err) {
+                                                        unsigned* ticket, int* err, const int* __restrict__ ord) {
     __shared__ double vs[kWaves][kRowCap];
     __shared__ int cs[kWaves][kRowCap];
+    __shared__ double uvs[kWaves][kUpCap];  // staged upper parts of the pivot rows
+    __shared__ int ucs[kWaves][kUpCap];
+    __shared__ int uos[kWaves][kWave], kds[kWaves][kWave];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     double* v = vs[wid];
     int* c = cs[wid];
+    double* uv = uvs[wid];
+    int* uc = ucs[wid];
+    int* uo = uos[wid];
+    int* ukd = kds[wid];
     const double alpha = __longlong_as_double((long long)*rowmax) * eps;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     for (;;) {
@@ -97,10 +108,11 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(int n, const int* __rest
             if (lane == 0) __hip_atomic_store((gu32*)err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         }
-        int row = 0;
-        if (lane == 0) row = (int)__hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        row = __shfl(row, 0, kWave);
-        if (row >= n) break;
+        int t = 0;
+        if (lane == 0) t = (int)__hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __shfl(t, 0, kWave);
+        if (t >= n) break;
+        const int row = ord[t];  // rows in dependency-level order
         const int rs = rowptr[row], len = rowptr[row + 1] - rs, dpos = diag[row] - rs;
         for (int e = lane; e < len; e += kWave) {
             c[e] = col[rs + e];
@@ -110,25 +122,78 @@ __global__ __launch_bounds__(kBlock) void k_ilu0_factor(int n, const int* __rest
         if (row > 0) {  // the reference loop starts at row 1 (no elimination, no boost on row 0)
             for (int e = lane; e < dpos; e += kWave) wait_flag(done + c[e], err);
             acquire_agent();
+            // Stage the pivot rows' upper parts (columns, values) and pivots
+            // with all lanes at once (dpos <= 64, <= kUpCap entries): one load
+            // round trip for all of them, so the elimination steps below run
+            // from LDS and registers instead of a chain of dependent global
+            // loads per step (~8 us a row on a chain). Same values, same
+            // search, same arithmetic: identical factors.
+            int my_kd = 0, my_cnt = 0;
+            double my_piv = 1.0;
+            if (dpos <= kWave && lane < dpos) {
+                const int k = c[lane];
+                my_kd = diag[k];
+                my_cnt = rowptr[k + 1] - my_kd - 1;
+                my_piv = lu[my_kd];
+            }
+            int incl = my_cnt;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const int t = __shfl_up(incl, o, kWave);
+                if (lane >= o) incl += t;
+            }
+            const int tot = __shfl(incl, kWave - 1, kWave);
+            const int my_off = incl - my_cnt;
+            const bool staged = dpos <= kWave && tot <= kUpCap;
+            if (staged) {
+                uo[lane] = my_off;
+                ukd[lane] = my_kd;
+                wave_lds_sync();
+                for (int f = lane; f < tot; f += kWave) {
+                    int lo = 0, hi = dpos;  // the last pivot row whose entries start at or before f
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (uo[mid] <= f) lo = mid;
+                        else hi = mid;
+                    }
+                    const int src = ukd[lo] + 1 + (f - uo[lo]);
+                    uc[f] = col[src];
+                    uv[f] = lu[src];
+                }
+                wave_lds_sync();
+            }
             for (int p = 0; p < dpos; ++p) {
-                const int k = c[p];
-                const int kd = diag[k], ke = rowptr[k + 1];
-                const double factor = v[p] / lu[kd];
+                int b0, b1;  // the pivot row's upper entries: [b0, b1) of uc / uv, or of col / lu
+                double pivot;
+                if (staged) {
+                    b0 = __shfl(my_off, p, kWave);
+                    b1 = b0 + __shfl(my_cnt, p, kWave);
+                    pivot = __shfl(my_piv, p, kWave);
+                } else {
+                    const int k = c[p];
+                    const int kd = diag[k];
+                    b0 = kd + 1;
+                    b1 = rowptr[k + 1];
+                    pivot = lu[kd];
+                }
+                const int* __restrict__ bc = staged ? uc : col;
+                const double* bv = staged ? uv : lu;
+                const double factor = v[p] / pivot;
                 wave_lds_sync();
                 if (lane == 0) v[p] = factor;
                 for (int e = p + 1 + lane; e < len; e += kWave) {
                     const int cc = c[e];
                     int f = e;
                     while (f > p + 1 && c[f - 1] == cc) --f;
-                    int lo = kd + 1, hi = ke;
+                    int lo = b0, hi = b1;
                     while (lo < hi) {
                         const int mid = (lo + hi) >> 1;
-                        if (col[mid] < cc) lo = mid + 1;
+                        if (bc[mid] < cc) lo = mid + 1;
                         else hi = mid;
                     }
                     const int t = lo + (e - f);
-                    if (t < ke && col[t] == cc) {
-                        const double prod = factor * lu[t];
+                    if (t < b1 && bc[t] == cc) {
+                        const double prod = factor * bv[t];
                         v[e] = v[e] - prod;
                     }
                 }
@@ -630,7 +695,7 @@ int mpg_ilu0_create(mpg_ctx_t ctx, mpg_csr_t A, const double* val64, int type, m
     const double eps = type == 0 ? (double)std::numeric_limits<double>::epsilon()
                                  : (double)std::numeric_limits<float>::epsilon();
     k_ilu0_factor<<<persist_grid(n), kBlock, 0, s>>>(n, A->rowptr, A->col, L->diag, L->lu64, eps, L->scratch,
-                                                     L->sync, L->ticket(0), L->err());
+                                                     L->sync, L->ticket(0), L->err(), L->ord[0]);
     int st = by_type(type, [&](auto t) {
         using T = decltype(t);
         T* lu = static_cast<T*>(L->values());
