@@ -382,6 +382,9 @@ __global__ void k_trsv_tag_move(int n, T* __restrict__ src, T* __restrict__ dst)
 // are read while the current row finishes. The arithmetic is the level
 // kernel's -- fp64 sum in CSR order, rounded once; a padded term adds an
 // exact +0 (the sum never holds -0) -- so both modes give identical results.
+// P (<= kPass): entries per pass, the direction's longest row (BAND-100k:
+// 5 for L, 4 for U), so rows are padded to what the matrix needs: one lane
+// runs every padded term, and the chain is bound by its instruction count.
 constexpr int kRing = 2048, kStageRows = 256, kStageEnt = 1536, kPass = 8;
 template <class T>
 struct SerialStage {
@@ -392,7 +395,7 @@ struct SerialStage {
     T elu[kStageEnt + kPass];
 };
 
-template <class T, bool UPPER>
+template <class T, bool UPPER, int P>
 __global__ __launch_bounds__(kBlock) void k_ilu_trsv_serial(int n, int nstages, const int* __restrict__ stage,
                                                             const int* __restrict__ eoff,
                                                             const int* __restrict__ rowptr,
@@ -435,32 +438,32 @@ __global__ __launch_bounds__(kBlock) void k_ilu_trsv_serial(int n, int nstages, 
             // row p's operands, read one row ahead
             int eb = 0, ee = B.eend[0];
             T rhs = B.rhs[0], piv = UPPER ? B.piv[0] : T(1);
-            int sl[kPass];
-            T a[kPass];
+            int sl[P];
+            T a[P];
 #pragma unroll
-            for (int k = 0; k < kPass; ++k) {
+            for (int k = 0; k < P; ++k) {
                 sl[k] = B.slot[k];
                 a[k] = B.elu[k];
             }
             for (int p = p0; p < p1; ++p) {
-                T xv[kPass];
+                T xv[P];
 #pragma unroll
-                for (int k = 0; k < kPass; ++k) xv[k] = ring[sl[k]];
+                for (int k = 0; k < P; ++k) xv[k] = ring[sl[k]];
                 double s = 0.0;
 #pragma unroll
-                for (int k = 0; k < kPass; ++k) s += (double)a[k] * (double)xv[k];
-                for (int e = eb + kPass; e < ee; e += kPass) {  // rows of more than kPass entries
+                for (int k = 0; k < P; ++k) s += (double)a[k] * (double)xv[k];
+                for (int e = eb + P; e < ee; e += P) {  // rows of more than P entries
 #pragma unroll
-                    for (int k = 0; k < kPass; ++k) xv[k] = ring[B.slot[e + k]];
+                    for (int k = 0; k < P; ++k) xv[k] = ring[B.slot[e + k]];
 #pragma unroll
-                    for (int k = 0; k < kPass; ++k) s += (double)B.elu[e + k] * (double)xv[k];
+                    for (int k = 0; k < P; ++k) s += (double)B.elu[e + k] * (double)xv[k];
                 }
                 // the next row's operands (past the stage's last row: unused reads within the arrays)
                 const int q = p + 1 - p0;
                 const int nb = ee, ne = B.eend[q];
                 const T nrhs = B.rhs[q], npiv = UPPER ? B.piv[q] : T(1);
 #pragma unroll
-                for (int k = 0; k < kPass; ++k) {
+                for (int k = 0; k < P; ++k) {
                     sl[k] = B.slot[nb + k];
                     a[k] = B.elu[nb + k];
                 }
@@ -536,6 +539,7 @@ struct mpg_ilu {
     int* stage[2] = {nullptr, nullptr};
     int* eoff[2] = {nullptr, nullptr};
     int nstages[2] = {0, 0};
+    int spass[2] = {kPass, kPass};  // entries per pass of each serial solve
 
     size_t tsize() const { return type == 0 ? 8 : 4; }
     void* values() const { return type == 0 ? (void*)lu64 : (void*)lu32; }
@@ -562,13 +566,17 @@ int persist_grid(int n) { return std::max(1, std::min(kPersistGroups, (n + kWave
 // rows, or a row with more than kStageEnt off-diagonal entries. Entry
 // offsets count each row padded to a multiple of kPass (at least kPass).
 bool serial_plan(int n, int nlev, const std::vector<int>& rp, const std::vector<int>& ci, const std::vector<int>& dg,
-                 bool upper, std::vector<int>& stage, std::vector<int>& eoff) {
+                 bool upper, std::vector<int>& stage, std::vector<int>& eoff, int& P) {
     if (n == 0 || (int64_t)n >= 16 * (int64_t)nlev) return false;
+    int longest = 1;
+    for (int i = 0; i < n; ++i)
+        longest = std::max(longest, upper ? rp[(size_t)i + 1] - dg[i] - 1 : dg[i] - rp[i]);
+    P = std::min(kPass, longest);
     eoff.assign((size_t)n + 1, 0);
     for (int p = 0; p < n; ++p) {
         const int i = upper ? n - 1 - p : p;
         const int j0 = upper ? dg[i] + 1 : rp[i], j1 = upper ? rp[i + 1] : dg[i];
-        const int padded = std::max(kPass, (j1 - j0 + kPass - 1) / kPass * kPass);
+        const int padded = std::max(P, (j1 - j0 + P - 1) / P * P);
         if (padded > kStageEnt) return false;
         for (int j = j0; j < j1; ++j)
             if (std::abs(ci[j] - i) >= kRing) return false;
@@ -674,7 +682,7 @@ int mpg_ilu0_create(mpg_ctx_t ctx, mpg_csr_t A, const double* val64, int type, m
             L->nchunks[u] = (int)chunk.size() - 1;
             std::vector<int> stage, eoff;
             const char* senv = std::getenv("MPG_ILU_SERIAL");  // 0: always the level schedule
-            if (!(senv && *senv == '0') && serial_plan(n, L->levels[u], rp, ci, dg, u == 1, stage, eoff)) {
+            if (!(senv && *senv == '0') && serial_plan(n, L->levels[u], rp, ci, dg, u == 1, stage, eoff, L->spass[u])) {
                 L->serial[u] = true;
                 L->nstages[u] = (int)stage.size() - 1;
                 if (!ok(hipMalloc((void**)&L->stage[u], stage.size() * 4)) ||
@@ -751,10 +759,26 @@ int mpg_ilu_solve(mpg_ctx_t ctx, mpg_ilu_t L, void* x) {
         const T* lu = static_cast<const T*>(L->values());
         T* xv = static_cast<T*>(x);
         T* yv = static_cast<T*>(L->tagbuf);
+        auto serial = [&](int u, auto upper) {  // in place in x, P entries per pass
+            constexpr bool UP = decltype(upper)::value;
+            auto go = [&](auto pc) {
+                k_ilu_trsv_serial<T, UP, decltype(pc)::value><<<1, kBlock, 0, s>>>(
+                    n, L->nstages[u], L->stage[u], L->eoff[u], L->A->rowptr, L->A->col, L->diag, lu, xv);
+            };
+            switch (L->spass[u]) {
+                case 1: go(std::integral_constant<int, 1>()); break;
+                case 2: go(std::integral_constant<int, 2>()); break;
+                case 3: go(std::integral_constant<int, 3>()); break;
+                case 4: go(std::integral_constant<int, 4>()); break;
+                case 5: go(std::integral_constant<int, 5>()); break;
+                case 6: go(std::integral_constant<int, 6>()); break;
+                case 7: go(std::integral_constant<int, 7>()); break;
+                default: go(std::integral_constant<int, kPass>()); break;
+            }
+        };
         if (!L->serial[0] || !L->serial[1]) k_trsv_tag_fill<T><<<g, kBlock, 0, s>>>(n, yv, L->ticket(1));
         if (L->serial[0]) {
-            k_ilu_trsv_serial<T, false><<<1, kBlock, 0, s>>>(n, L->nstages[0], L->stage[0], L->eoff[0],
-                                                             L->A->rowptr, L->A->col, L->diag, lu, xv);
+            serial(0, std::false_type());
             if (!L->serial[1]) k_trsv_tag_move<T><<<g, kBlock, 0, s>>>(n, xv, yv);
         } else {
             k_ilu_trsv_tagged<T, false><<<grid(0), kBlock, 0, s>>>(L->nchunks[0], L->chunk[0], L->ord[0],
@@ -763,8 +787,7 @@ int mpg_ilu_solve(mpg_ctx_t ctx, mpg_ilu_t L, void* x) {
         }
         if (L->serial[1]) {
             if (!L->serial[0]) k_trsv_tag_move<T><<<g, kBlock, 0, s>>>(n, yv, xv);
-            k_ilu_trsv_serial<T, true><<<1, kBlock, 0, s>>>(n, L->nstages[1], L->stage[1], L->eoff[1],
-                                                            L->A->rowptr, L->A->col, L->diag, lu, xv);
+            serial(1, std::true_type());
         } else {
             k_ilu_trsv_tagged<T, true><<<grid(1), kBlock, 0, s>>>(L->nchunks[1], L->chunk[1], L->ord[1],
                                                                   L->A->rowptr, L->A->col, L->diag, lu, yv,
