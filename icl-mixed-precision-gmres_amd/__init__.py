@@ -174,6 +174,8 @@ _HIP_DECLS.update({
     "mpg_sell_spmv_f64": ([_P, _P, C.c_double, _P, C.c_double, _P], C.c_int),
     "mpg_sell_spmv_f32": ([_P, _P, C.c_float, _P, C.c_float, _P], C.c_int),
     "mpg_sell_spmv_f16f32": ([_P, _P, C.c_float, _P, C.c_float, _P], C.c_int),
+    "mpg_sell_spmv_prog_f64": ([_P, _P, C.c_double, _P, C.c_double, _P, _P, C.c_int32], C.c_int),
+    "mpg_sell_spmv_prog_f32": ([_P, _P, C.c_float, _P, C.c_float, _P, _P, C.c_int32], C.c_int),
     "mpg_copy_f64f64": ([_P, _I64, _P, _P], C.c_int),
     "mpg_copy_f32f32": ([_P, _I64, _P, _P], C.c_int),
     "mpg_copy_f64f32": ([_P, _I64, _P, _P], C.c_int),

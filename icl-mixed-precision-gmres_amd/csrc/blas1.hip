@@ -5,6 +5,7 @@
 // partial per workgroup into the context workspace, stage 2: one workgroup
 // sums the partials in a fixed order and writes the result on device).
 #include "internal.hpp"
+#include "scalar_program.hpp"
 
 #include <algorithm>
 
@@ -180,41 +181,6 @@ __global__ __launch_bounds__(kBlock) void k_gdmv(int64_t n, T alpha, const T* __
         y[i] = beta * y[i] + alpha * d[i] * x[i];   // kernels.hpp:141-144 (x may alias y)
 }
 
-// ---------------- Givens (single lane; O(1)/O(k) scalar work) ----------------
-// Exact IEEE order: products rounded separately, no FMA contraction, so the
-// results equal the reference BLAS formulas evaluated in T.
-#pragma clang fp contract(off)
-template <class T>
-__device__ void rotg_dev(T* a, T* b, T* c, T* s) {
-    // Reference BLAS xROTG (classic netlib form), then b := 0
-    // (kernels_mkl.cpp:214-226 zeroes b after cblas_?rotg).
-    T av = *a, bv = *b;
-    T roe = fabs(av) > fabs(bv) ? av : bv;
-    T scale = fabs(av) + fabs(bv);
-    T cc, ss, r;
-    if (scale == T(0)) {
-        cc = T(1); ss = T(0); r = T(0);
-    } else {
-        T as = av / scale, bs = bv / scale;
-        r = scale * sqrt(as * as + bs * bs);
-        r = roe >= T(0) ? r : -r;
-        cc = av / r;
-        ss = bv / r;
-    }
-    *a = r;
-    *b = T(0);
-    *c = cc;
-    *s = ss;
-}
-
-template <class T>
-__device__ void rot_pair(T* a, T* b, T c, T s) {
-    T a1 = *a, a2 = *b;
-    *a = c * a1 + s * a2;
-    *b = c * a2 - s * a1;
-}
-#pragma clang fp contract(on)
-
 template <class T>
 __global__ void k_rotg(T* a, T* b, T* c, T* s) { rotg_dev(a, b, c, s); }
 
@@ -226,74 +192,11 @@ __global__ void k_rot_vec(int k, T* a, const T* c, const T* s) {
     for (int j = 0; j < k; ++j) rot_pair(a + j, a + j + 1, c[j], s[j]);
 }
 
-// A scalar program (mpg_scalar_program) in call order with the
-// single-operator kernels' arithmetic, on one wave: lane 0 runs every
-// operator; a rot_vec first stages its column and rotations in LDS with all
-// 64 lanes (one memory latency instead of one per rotation: the chain
-// stores a[j+1] before it loads it back), rotates there, and writes the
-// column back with all lanes.
-struct ScalarProgram {
-    mpg_scalar_op ops[MPG_SCALAR_PROGRAM_MAX];
-    int count;
-};
-
 constexpr int kRotStage = 256;  // rotations staged in LDS per pass
-
-template <class T>
-__device__ void scalar_op(const mpg_scalar_op& o, T* lds) {
-    T* p0 = static_cast<T*>(o.p[0]);
-    T* p1 = static_cast<T*>(o.p[1]);
-    T* p2 = static_cast<T*>(o.p[2]);
-    T* p3 = static_cast<T*>(o.p[3]);
-    const int lane = threadIdx.x;
-    if (o.op == MPG_SOP_ROT_VEC) {
-        // the column a[0..k] and c, s never overlap in the drivers; if they
-        // do, run the chain from memory like k_rot_vec
-        const bool disjoint = (p0 + o.k + 1 <= p2 || p2 + o.k <= p0) && (p0 + o.k + 1 <= p3 || p3 + o.k <= p0);
-        if (!disjoint) {
-            if (lane == 0)
-                for (int j = 0; j < o.k; ++j) rot_pair(p0 + j, p0 + j + 1, p2[j], p3[j]);
-            __syncthreads();
-            return;
-        }
-        T* la = lds;
-        T* lc = lds + kRotStage + 1;
-        T* ls = lc + kRotStage;
-        for (int j0 = 0; j0 < o.k; j0 += kRotStage) {
-            const int kk = o.k - j0 < kRotStage ? o.k - j0 : kRotStage;
-            for (int j = lane; j <= kk; j += kWave) la[j] = p0[j0 + j];
-            for (int j = lane; j < kk; j += kWave) {
-                lc[j] = p2[j0 + j];
-                ls[j] = p3[j0 + j];
-            }
-            __syncthreads();
-            if (lane == 0)
-                for (int j = 0; j < kk; ++j) rot_pair(la + j, la + j + 1, lc[j], ls[j]);
-            __syncthreads();
-            for (int j = lane; j <= kk; j += kWave) p0[j0 + j] = la[j];
-            __syncthreads();
-        }
-        return;
-    }
-    if (lane == 0) {
-        switch (o.op) {
-            case MPG_SOP_ROTG: rotg_dev(p0, p1, p2, p3); break;
-            case MPG_SOP_ROT: rot_pair(p0, p1, *p2, *p3); break;
-            case MPG_SOP_COPY: *p1 = *p0; break;
-            case MPG_SOP_SCAL: *p1 = T(o.alpha) * *p0; break;
-            case MPG_SOP_SCAL_DEV: *p1 = *p2 * *p0; break;
-            default: break;
-        }
-    }
-    __syncthreads();
-}
 
 __global__ __launch_bounds__(kWave) void k_scalar_program(ScalarProgram prog) {
     __shared__ double lds[3 * kRotStage + 1];
-    for (int i = 0; i < prog.count; ++i) {
-        if (prog.ops[i].f64) scalar_op<double>(prog.ops[i], lds);
-        else scalar_op<float>(prog.ops[i], reinterpret_cast<float*>(lds));
-    }
+    run_scalar_program<kRotStage>(prog, lds);
 }
 
 template <class T, bool ALPHA_DEV>
@@ -452,14 +355,9 @@ int mpg_rot_vec_f32(mpg_ctx_t c, int k, float* a, const float* cs, const float* 
     MPG_SINGLE(c, (k_rot_vec<float><<<1, 1, 0, c->stream>>>(k, a, cs, s)));
 }
 int mpg_scalar_program(mpg_ctx_t c, const mpg_scalar_op* ops, int count) {
-    if (!c || count < 0 || count > MPG_SCALAR_PROGRAM_MAX || (count && !ops)) return MPG_ERR_ARG;
+    ScalarProgram prog;
+    if (!c || make_scalar_program(ops, count, prog) != MPG_OK) return MPG_ERR_ARG;
     if (count == 0) return MPG_OK;
-    ScalarProgram prog{};
-    for (int i = 0; i < count; ++i) {
-        if (ops[i].op < MPG_SOP_ROTG || ops[i].op > MPG_SOP_SCAL_DEV) return MPG_ERR_ARG;
-        prog.ops[i] = ops[i];
-    }
-    prog.count = count;
     MPG_SINGLE(c, (k_scalar_program<<<1, kWave, 0, c->stream>>>(prog)));
 }
 int mpg_scal_scalar_f64(mpg_ctx_t c, double a, const double* x, double* y) { MPG_SINGLE(c, (k_scal_scalar<double, false><<<1, 1, 0, c->stream>>>(a, nullptr, x, y))); }

@@ -13,6 +13,7 @@
 // before all of them are in flight. Sums are fp64 in CSR order, rounded
 // once to the vector type: y = alpha*t (+ beta*y), as spmv.hip.
 #include "sell_tile.hpp"
+#include "scalar_program.hpp"
 #include "handoff.hpp"
 #include "internal.hpp"
 #include "mpgmres/arnoldi.h"
@@ -133,7 +134,12 @@ int with_store(int vtype, F&& f) {
     }
 }
 
-// y = alpha * T(A x) (+ beta * y) on the sliced copy; one wave per slice
+constexpr int kProgStage = 64;  // rot_vec rotations staged per pass by a riding scalar program
+
+// y = alpha * T(A x) (+ beta * y) on the sliced copy; one wave per slice.
+// prog.count > 0: workgroup 0 runs that scalar program instead (the
+// operator surface's Givens step of the previous Arnoldi step, which nothing
+// in this SpMV reads or writes: kernels_hip.cpp checks the operands).
 template <class X, class S, class CI, int W, bool WIN>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col, const S* __restrict__ val,
@@ -142,11 +148,23 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
                                                       const int32_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ ccol, const S* __restrict__ cval,
                                                       const X* __restrict__ x, X alpha, X beta, X* __restrict__ y,
-                                                      int xcd) {
+                                                      int xcd, ScalarProgram prog) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (kBlock / kWave) + wid;
+    // a scalar program riding in this launch: workgroup 0 (dispatched first,
+    // so it runs under the slices instead of after them), its first wave
+    int b = (int)blockIdx.x, G = (int)gridDim.x;
+    if (prog.count > 0) {
+        if (b == 0) {
+            __shared__ double plds[3 * kProgStage + 1];
+            if (wid == 0) run_scalar_program<kProgStage>(prog, plds);
+            return;
+        }
+        --b;
+        --G;
+    }
+    const int s = (xcd ? xcd_block(b, G) : b) * (kBlock / kWave) + wid;
     if (s >= nslices) return;  // no workgroup barrier below: a dead wave may leave
     const int row0 = s * kWave;
     const int i = row0 + lane;
@@ -411,18 +429,19 @@ struct mpg_sell {
 namespace {
 
 template <class X, class St>
-int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y) {
+int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y,
+                   const ScalarProgram& prog = ScalarProgram{}) {
     if (!ctx || !A) return MPG_ERR_ARG;
     const SellCopy& S = A->S;
-    if (S.nslices == 0) return MPG_OK;
-    const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
+    if (S.nslices == 0) return prog.count > 0 ? mpg_scalar_program(ctx, prog.ops, prog.count) : MPG_OK;
+    const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave) + (prog.count > 0 ? 1 : 0);
     int st = sell_dispatch(S, [&](auto ci, auto wc) {
         using CI = decltype(ci);
         return sell_dispatch_win(S.win, [&](auto wn) {
             k_sell_spmv<X, St, CI, decltype(wc)::value, decltype(wn)::value><<<grid, kBlock, 0, ctx->stream>>>(
                 S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val), S.sbase,
                 S.spat, static_cast<const CI*>(S.pat), A->A->rowptr, A->A->col, static_cast<const St*>(A->vals), x, alpha, beta, y,
-                sell_xcd_order(S) ? 1 : 0);
+                sell_xcd_order(S) ? 1 : 0, prog);
             return (int)MPG_OK;
         });
     });
@@ -493,6 +512,18 @@ int mpg_sell_spmv_f32(mpg_ctx_t c, mpg_sell_t A, float alpha, const float* x, fl
 int mpg_sell_spmv_f16f32(mpg_ctx_t c, mpg_sell_t A, float alpha, const float* x, float beta, float* y) {
     if (A && A->S.vtype != MPG_F16) return MPG_ERR_ARG;
     return sell_spmv_impl<float, uint16_t>(c, A, alpha, x, beta, y);
+}
+int mpg_sell_spmv_prog_f64(mpg_ctx_t c, mpg_sell_t A, double alpha, const double* x, double beta, double* y,
+                           const mpg_scalar_op* ops, int32_t nops) {
+    ScalarProgram prog;
+    if ((A && A->S.vtype != MPG_F64) || make_scalar_program(ops, nops, prog) != MPG_OK) return MPG_ERR_ARG;
+    return sell_spmv_impl<double, double>(c, A, alpha, x, beta, y, prog);
+}
+int mpg_sell_spmv_prog_f32(mpg_ctx_t c, mpg_sell_t A, float alpha, const float* x, float beta, float* y,
+                           const mpg_scalar_op* ops, int32_t nops) {
+    ScalarProgram prog;
+    if ((A && A->S.vtype != MPG_F32) || make_scalar_program(ops, nops, prog) != MPG_OK) return MPG_ERR_ARG;
+    return sell_spmv_impl<float, float>(c, A, alpha, x, beta, y, prog);
 }
 
 }  // extern "C"

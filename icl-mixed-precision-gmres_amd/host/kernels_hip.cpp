@@ -185,6 +185,39 @@ bool queue_scalar_op(const mpg_scalar_op& op) {
     return true;
 }
 
+// The queued program for the SELL SpMV that comes next to carry in one
+// extra workgroup of its launch (mpg_sell_spmv_prog_*): taken, emptying the
+// queue, when it belongs to this context, no reduction stage is pending, and
+// none of its operand cells overlaps the SpMV's x or y (so running it
+// concurrently with the rows cannot change any value); otherwise the queue
+// is issued as usual. MPG_SURFACE_RIDE=0: never taken. Returns the context.
+mpg_ctx_t take_scalar_ops_for(const void* x, size_t xbytes, const void* y, size_t ybytes, mpg_scalar_op* ops,
+                              int& nops) {
+    nops = 0;
+    const char* env = std::getenv("MPG_SURFACE_RIDE");
+    bool ok = tl_nops > 0 && !tl_red.kind && tl_ops_ctx == ctx_no_flush() && !(env && *env == '0');
+    auto clash = [&](const void* p, size_t bytes) {
+        const char* a = static_cast<const char*>(p);
+        const char* xa = static_cast<const char*>(x);
+        const char* ya = static_cast<const char*>(y);
+        return (a < xa + xbytes && xa < a + bytes) || (a < ya + ybytes && ya < a + bytes);
+    };
+    for (int i = 0; i < tl_nops && ok; ++i) {
+        const mpg_scalar_op& o = tl_ops[i];
+        const size_t es = o.f64 ? 8 : 4;
+        for (int q = 0; q < 4 && ok; ++q) {
+            if (!o.p[q]) continue;
+            const size_t cells = o.op != MPG_SOP_ROT_VEC ? 1 : q == 0 ? (size_t)o.k + 1 : (size_t)o.k;
+            ok = !clash(o.p[q], cells * es);
+        }
+    }
+    if (!ok) return current_ctx();
+    for (int i = 0; i < tl_nops; ++i) ops[i] = tl_ops[i];
+    nops = tl_nops;
+    tl_nops = 0;
+    return tl_ops_ctx;
+}
+
 mpg_ctx_t current_ctx() {
     if (tl_nops) flush_scalar_ops();
     if (tl_red.kind) flush_pending_reduction();
@@ -591,15 +624,31 @@ template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Ve
                                    Vect<double, Hip> y) {
     assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
                              : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
-    if (mpg_sell_t s = A.sell()) check(mpg_sell_spmv_f64(C, s, alpha, x.data(), beta, y.data()), "spmv");
-    else check(mpg_csr_spmv_f64(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
+    if (mpg_sell_t s = A.sell()) {
+        mpg_scalar_op ops[MPG_SCALAR_PROGRAM_MAX];
+        int nops = 0;
+        mpg_ctx_t c = mpg::take_scalar_ops_for(x.data(), x.n() * 8, y.data(), y.n() * 8, ops, nops);
+        check(nops ? mpg_sell_spmv_prog_f64(c, s, alpha, x.data(), beta, y.data(), ops, nops)
+                   : mpg_sell_spmv_f64(c, s, alpha, x.data(), beta, y.data()),
+              "spmv");
+    } else {
+        check(mpg_csr_spmv_f64(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
+    }
 }
 template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<float, Hip> x, float beta,
                                   Vect<float, Hip> y) {
     assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
                              : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
-    if (mpg_sell_t s = A.sell()) check(mpg_sell_spmv_f32(C, s, alpha, x.data(), beta, y.data()), "spmv");
-    else check(mpg_csr_spmv_f32(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
+    if (mpg_sell_t s = A.sell()) {
+        mpg_scalar_op ops[MPG_SCALAR_PROGRAM_MAX];
+        int nops = 0;
+        mpg_ctx_t c = mpg::take_scalar_ops_for(x.data(), x.n() * 4, y.data(), y.n() * 4, ops, nops);
+        check(nops ? mpg_sell_spmv_prog_f32(c, s, alpha, x.data(), beta, y.data(), ops, nops)
+                   : mpg_sell_spmv_f32(c, s, alpha, x.data(), beta, y.data()),
+              "spmv");
+    } else {
+        check(mpg_csr_spmv_f32(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
+    }
 }
 template <> void jacobi_diag<double, Hip>(SparseMatrix<double, Hip> A, Vect<double, Hip> d) {
     check(mpg_jacobi_setup_f64(C, A.csr(), A.vals_data(), d.data()), "jacobi setup");

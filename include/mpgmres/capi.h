@@ -279,6 +279,15 @@ int mpg_sell_columns(mpg_sell_t A, int32_t* form, int64_t* csr_slices, int64_t* 
 int mpg_sell_spmv_f64(mpg_ctx_t ctx, mpg_sell_t A, double alpha, const double* x, double beta, double* y);
 int mpg_sell_spmv_f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y);
 int mpg_sell_spmv_f16f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y);
+/* The same SpMV with a scalar program (mpg_scalar_program) run by one extra
+ * workgroup of the launch, concurrently with the rows: for a program whose
+ * operands the SpMV neither reads nor writes (the caller checks). Replaces
+ * the program's own launch before the next step's spmv (gmres.cpp:106-110
+ * then 96-100 in the operator surface's order). nops = 0: plain SpMV. */
+int mpg_sell_spmv_prog_f64(mpg_ctx_t ctx, mpg_sell_t A, double alpha, const double* x, double beta, double* y,
+                           const mpg_scalar_op* ops, int32_t nops);
+int mpg_sell_spmv_prog_f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y,
+                           const mpg_scalar_op* ops, int32_t nops);
 
 /* A^T as its own CSR (SparseMatrix::set_transpose, types_cuda.hpp:145-151;
  * cusparse?csrmv TRANSPOSE, kernels_cuda.cpp:588-596; condest.cpp:49-50).

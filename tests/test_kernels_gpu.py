@@ -399,6 +399,55 @@ def test_scalar_program_matches_single_ops(hip, t):
 
 
 @pytest.mark.parametrize("t", ["f64", "f32"])
+def test_scalar_program_rides_sell_spmv(hip, mpg, t):
+    """mpg_sell_spmv_prog_*: the Givens program run by one extra workgroup of
+    a SELL SpMV launch gives the bits of its own launch, and the SpMV's y the
+    bits of the plain SpMV (the operator surface hands the next step's SpMV
+    the queued program when their operands do not overlap)."""
+    dt = np.float64 if t == "f64" else np.float32
+    vt = 0 if t == "f64" else 1
+    f64 = 1 if t == "f64" else 0
+    A = mpg.gen_band(20_000, 5, 4, seed=3)
+    g = rng(5)
+    x, y0 = g.uniform(-1, 1, A.ncols).astype(dt), g.uniform(-1, 1, A.nrows).astype(dt)
+    k = 11
+    col0 = g.normal(size=k + 2).astype(dt)
+    th = g.uniform(0, 2 * np.pi, k)
+    c0, s0 = np.cos(th).astype(dt), np.sin(th).astype(dt)
+    sv0 = np.zeros(k + 2, dt)
+    sv0[k] = dt(g.normal())
+    drp, dci, dv = hip.buf(A.rowptr), hip.buf(A.col), hip.buf(A.val.astype(dt))
+    csr, sell = C.c_void_p(), C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, A.nrows, A.ncols, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    hip.check(hip.lib.mpg_sell_create(hip.ctx, csr, vt, dv.p, 2, C.byref(sell)))
+    out = {}
+    try:
+        for how in ("ride", "apart"):
+            col, c, s, sv = hip.buf(np.append(col0, 0)), hip.buf(np.append(c0, [0, 0])), hip.buf(np.append(s0, [0, 0])), hip.buf(sv0)
+            rec = hip.buf(np.zeros(1, dt))
+            dx, dy = hip.buf(x), hip.buf(y0)
+            ops = (ScalarOp * 4)()
+            specs = [(2, k, [col.p, None, c.p, s.p]), (0, 0, [col.at(k), col.at(k + 1), c.at(k), s.at(k)]),
+                     (1, 0, [sv.at(k), sv.at(k + 1), c.at(k), s.at(k)]), (3, 0, [sv.at(k + 1), rec.at(0), None, None])]
+            for i, (op, kk, ps) in enumerate(specs):
+                ops[i].op, ops[i].f64, ops[i].k, ops[i].alpha = op, f64, kk, 0.0
+                for j, q in enumerate(ps):
+                    ops[i].p[j] = q.value if q is not None else None
+            if how == "ride":
+                hip.call(f"mpg_sell_spmv_prog_{t}", sell, 1.0, dx.p, 0.5, dy.p, C.cast(ops, C.c_void_p), 4)
+            else:
+                hip.check(hip.lib.mpg_scalar_program(hip.ctx, ops, 4), "mpg_scalar_program")
+                hip.call(f"mpg_sell_spmv_{t}", sell, 1.0, dx.p, 0.5, dy.p)
+            out[how] = [b.get() for b in (col, c, s, sv, rec, dy)]
+    finally:
+        hip.lib.mpg_sell_destroy(sell)
+        hip.lib.mpg_csr_destroy(csr)
+    for a, b in zip(out["ride"], out["apart"]):
+        assert np.array_equal(a, b)
+    assert out["ride"][4][0] != 0
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
 def test_split_reductions_match_one_call(hip, t):
     """Stage 1 / stage 2 split reductions and the consumers that fold stage 2
     in (the operator surface's deferred reductions) give the one-call forms'
