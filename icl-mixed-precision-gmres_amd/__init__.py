@@ -45,6 +45,8 @@ def _lib(name: str) -> C.CDLL:
     if name in _libs:
         return _libs[name]
     path = HIP_LIB if name == "hip" else HOST_LIB
+    if name == "hip" and os.environ.get("MPG_HIP_LIB"):  # A/B of two kernel builds (tools/ab_bench.sh)
+        path = Path(os.environ["MPG_HIP_LIB"])
     if not path.exists():
         raise RuntimeError(f"{path} is missing: run build() (make -C {PKG_DIR}) — there is no CPU fallback")
     if name == "host":

@@ -3,6 +3,7 @@
 # rotation, so drift hits all variants alike; prints it/s per run and the
 # median per variant.
 # usage: tools/ab_bench.sh ROUNDS "name|ENV=.. ENV2=..|bench args" ...
+# (MPG_HIP_LIB=path/to/libmpgmres_hip.so in ENV loads another kernel build)
 set -u
 mkdir -p gpurun_out
 R=$1; shift
