@@ -438,8 +438,8 @@ struct SellDots {
     double* out;       // [c * ng + g]
 };
 
-template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD, int DN = 0>
-__global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
+template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD, int DN = 0, int BS = kBlock>
+__global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col,
                                                       const typename SellStore<VI>::type* __restrict__ val,
                                                       const T* __restrict__ wprev, const T* __restrict__ inv_p,
@@ -451,11 +451,12 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_lo, int n_ext
                                                       const int32_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ ccol,
                                                       const typename SellStore<VI>::type* __restrict__ cval, int xcd) {
+    static_assert(DN == 0 || BS == kBlock, "the fused dots' partials assume kBlock-thread workgroups");
     using S = typename SellStore<VI>::type;
     constexpr int NQ = kWinLen / kWave;
-    __shared__ T win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
+    __shared__ T win[WIN ? BS / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (kBlock / kWave) + wid;
+    const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid;
     const bool live = s < nslices;  // a dead wave still joins the fold's barriers
     const int row0 = s * kWave;
     const int i = row0 + lane;
@@ -464,10 +465,20 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_lo, int n_ext
     row.init_load(live ? s : 0, off, spat);
     __builtin_amdgcn_sched_barrier(0);
     // 1. the fold's ||w||^2 partial (nparts <= kBlock, checked at launch: one per lane)
-    double part = 0.0;
+    // (a workgroup narrower than kBlock loads kBlock / BS per lane: the
+    // partials keep their kBlock-lane positions, so the sums below run in
+    // the same order whatever BS is)
+    constexpr int NPL = BS < kBlock ? kBlock / BS : 1;
+    double part[NPL];
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) part[j] = 0.0;
     if constexpr (FOLD) {
-        part = fold.norm2[threadIdx.x < fold.nparts ? threadIdx.x : 0];
-        if (threadIdx.x >= fold.nparts) part = 0.0;
+#pragma unroll
+        for (int j = 0; j < NPL; ++j) {
+            const int t = j * BS + (int)threadIdx.x;
+            part[j] = fold.norm2[t < fold.nparts ? t : 0];
+            if (t >= fold.nparts) part[j] = 0.0;
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
     // 2. w_prev window (or this row's own w_prev), raw
@@ -493,15 +504,19 @@ __global__ __launch_bounds__(kBlock) void k_step_sell(int n, int n_lo, int n_ext
     // writes, and its serial chain then holds none of the slice's loads live)
     double nrm2sq = 0.0;
     if constexpr (FOLD) {
-        __shared__ double scratch[kBlock / kWave];
+        constexpr int NG = (BS < kBlock ? kBlock : BS) / kWave;
+        __shared__ double scratch[NG];
         __shared__ T inv_s;
         if (fold.nparts > 0) {
-            const double v = wave_sum(part + 0.0);  // the same fixed order in every workgroup
-            if (lane == 0) scratch[wid] = v;
+#pragma unroll
+            for (int j = 0; j < NPL; ++j) {
+                const double v = wave_sum(part[j] + 0.0);  // the same fixed order in every workgroup
+                if (lane == 0) scratch[j * (BS / kWave) + wid] = v;
+            }
             lds_barrier();
             double r = 0.0;
 #pragma unroll
-            for (int q = 0; q < kBlock / kWave; ++q) r += scratch[q];
+            for (int q = 0; q < NG; ++q) r += scratch[q];
             nrm2sq = r;
         } else {
             nrm2sq = fold.norm2[0];
@@ -1439,6 +1454,13 @@ int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols) {
 // dots: the panel dots fused (SellDots; MPG_ERR_UNSUPPORTED where the SELL
 // copy, an fp32 basis with fp32 values, int16 columns and the window are
 // not all present -- the caller then launches the dots itself).
+// workgroup of the SELL step kernel without fused dots (4 slices per 256)
+#ifndef MPG_STEP_SELL_BLOCK
+#define MPG_STEP_SELL_BLOCK 256
+#endif
+constexpr int kStepSellBlock = MPG_STEP_SELL_BLOCK;
+using kBlockC = std::integral_constant<int, kBlock>;
+
 static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
     if (dots && (a->d.n <= 0 || a->sell.nslices == 0 || !a->sell.c16 || !a->sell.win || (a->combo != 2 && a->combo != 3) ||
@@ -1460,9 +1482,10 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
             return sell_dispatch(S, [&](auto ci, auto wc) {
                 using CI = decltype(ci);
                 constexpr int Wc = decltype(wc)::value;
-                const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave);
-                auto launch = [&](auto kern, SellDots dd) {
-                    launch_timed(a->ctx, kern, dim3(grid), dim3(kBlock),
+                auto launch = [&](auto kern, SellDots dd, auto bs) {
+                    constexpr int BS = decltype(bs)::value;
+                    const int grid = (S.nslices + BS / kWave - 1) / (BS / kWave);
+                    launch_timed(a->ctx, kern, dim3(grid), dim3(BS),
                             a->d.n, -a->front, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
@@ -1478,8 +1501,8 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                         const SellDots dd{k + 1, a->fd_gs, a->fd_ng, a->fd_part, a->fd_cnt, a->dpart};
                         auto pick = [&](auto dn) {
                             constexpr int DN = decltype(dn)::value;
-                            return fold ? launch(k_step_sell<T, P, VI, CI, Wc, true, true, DN>, dd)
-                                        : launch(k_step_sell<T, P, VI, CI, Wc, true, false, DN>, dd);
+                            return fold ? launch(k_step_sell<T, P, VI, CI, Wc, true, true, DN>, dd, kBlockC())
+                                        : launch(k_step_sell<T, P, VI, CI, Wc, true, false, DN>, dd, kBlockC());
                         };
                         if (k + 1 <= 8) return pick(std::integral_constant<int, 8>());
                         if (k + 1 <= 16) return pick(std::integral_constant<int, 16>());
@@ -1488,8 +1511,9 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                 }
                 return sell_dispatch_win(S.win, [&](auto wn) {
                     constexpr bool WN = decltype(wn)::value;
-                    return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true>, SellDots{})
-                                : launch(k_step_sell<T, P, VI, CI, Wc, WN, false>, SellDots{});
+                    using BSC = std::integral_constant<int, kStepSellBlock>;
+                    return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock>, SellDots{}, BSC())
+                                : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock>, SellDots{}, BSC());
                 });
             });
         }
