@@ -244,8 +244,11 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
             best_w = W;
             break;
         }
+    const char* fw = std::getenv("MPG_SELL_W");  // 1, 2 or 4: force the vector width (experiments)
+    const bool forced = fw && (*fw == '1' || *fw == '2' || *fw == '4') && fw[1] == 0;
+    if (forced) best_w = *fw - '0';
     const int64_t best = padded[best_w];
-    if (format == 0 && (double)best > 1.2 * (double)A->nnz) return MPG_OK;
+    if (format == 0 && !forced && (double)best > 1.2 * (double)A->nnz) return MPG_OK;
     if (best >= ((int64_t)1 << 31) * 4) return format == 2 ? MPG_ERR_UNSUPPORTED : MPG_OK;
     std::vector<int64_t> off((size_t)ns + 1, 0);
     for (int s = 0; s < ns; ++s)
