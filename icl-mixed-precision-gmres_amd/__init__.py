@@ -22,7 +22,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._abi import (ENGINES, MODES, ORTHS, PRECS, SPMV_FORMATS, STATUS, CondestResult, HostCsr, SolveArgs, SolveResult,
+from ._abi import (ENGINES, MODES, ORTHS, PRECS, SPMV_FORMATS, STATUS, CondestResult, HostCsr, RankLayout, SolveArgs, SolveResult,
                    condest_args, condest_dict)
 
 PKG_DIR = Path(__file__).resolve().parent
@@ -122,6 +122,10 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_create_dist.argtypes = [C.POINTER(SolveArgs), C.c_void_p, C.c_char_p, _I32, _I32,
                                            C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
     lib.mpg_solve_loopback.argtypes = [C.POINTER(SolveArgs), _I32, C.POINTER(SolveResult)]
+    lib.mpg_solve_loopback_ex.argtypes = [C.POINTER(SolveArgs), _I32, C.POINTER(SolveResult), C.c_void_p]
+    lib.mpg_engine_sell_columns.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
+                                            C.POINTER(C.c_int64)]
+    lib.mpg_engine_half_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
 
 
 # (name, argtypes) for the kernel-level C-ABI, used by the per-kernel tests
@@ -170,6 +174,8 @@ for _t, _ct in (("f64", C.c_double), ("f32", C.c_float)):
     })
 _HIP_DECLS.update({
     "mpg_csr_spmv_f16f32": ([_P, _P, C.c_float, _P, _P, C.c_float, _P], C.c_int),
+    "mpg_csr_spmv_f16f32_scaled": ([_P, _P, C.c_float, _P, _P, _P, C.c_float, _P], C.c_int),
+    "mpg_csr_half_values": ([_P, _P, _P, _I32, _P, _P, C.POINTER(_I64)], C.c_int),
     "mpg_sell_create": ([_P, _P, _I32, _P, _I32, C.POINTER(_P)], C.c_int),
     "mpg_sell_destroy": ([_P], C.c_int),
     "mpg_sell_layout": ([_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I64), C.POINTER(_I32)], C.c_int),
@@ -268,14 +274,25 @@ def gen_laplace3d(nx: int, ny: Optional[int] = None, nz: Optional[int] = None) -
     return _take_csr(h)
 
 
-def gen_stencil27(nx: int, dof: int = 3, seed: int = 11) -> Csr:
-    """27-point 3-D stencil, `dof` unknowns per node (the Queen_4147 stand-in
-    at nx = 111, dof = 3)."""
+def gen_stencil27(nx: int, dof: int = 3, seed: int = 11, ny: Optional[int] = None, nz: Optional[int] = None) -> Csr:
+    """27-point 3-D stencil on nx x ny x nz nodes (cubic by default), `dof`
+    unknowns per node (the Queen_4147 stand-in at nx = 111, dof = 3)."""
     h = HostCsr()
-    st = host_lib().mpg_gen_stencil27(nx, nx, nx, dof, seed, C.byref(h))
+    st = host_lib().mpg_gen_stencil27(nx, ny or nx, nz or nx, dof, seed, C.byref(h))
     if st:
         raise ValueError(f"mpg_gen_stencil27 failed ({st})")
     return _take_csr(h)
+
+
+def load_mtx_vector(path: str, n: int, col: int = 0) -> np.ndarray:
+    """Column `col` of a Matrix Market array or coordinate file as a length-n
+    vector (mpg_load_mtx_vector; the reference's LoadVector,
+    LoadMatrix.hpp:156-233, behind --bpath)."""
+    out = np.zeros(n, dtype=np.float64)
+    err = C.create_string_buffer(256)
+    if host_lib().mpg_load_mtx_vector(path.encode(), col, out.ctypes.data_as(C.POINTER(C.c_double)), n, err, 256):
+        raise ValueError(err.value.decode())
+    return out
 
 
 def gen_spec(spec: str) -> Csr:
@@ -350,7 +367,7 @@ class Result:
 def make_args(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, mode="mixed", orth="mgs",
               prec="identity", rlen=30, tol=1e-6, max_restarts=1_000_000, rtol=0.0, repeat_iter=False,
               orthloss=False, jacobi_steps=1, engine="fused", verbose=False, device=0, threads=0,
-              spmv_format="auto"):
+              spmv_format="auto", half_unscaled=False):
     """Build mpg_solve_args (shared by mpg_solve and the CPU oracle)."""
     b = np.ascontiguousarray(b, dtype=np.float64)
     keep = [A.rowptr, A.col, A.val, b]
@@ -369,6 +386,7 @@ def make_args(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, mod
     a.repeat_iter, a.orthloss, a.jacobi_steps = int(repeat_iter), int(orthloss), jacobi_steps
     a.verbose, a.device, a.threads = int(verbose), device, threads
     a.spmv_format = SPMV_FORMATS[spmv_format]
+    a.half_unscaled = int(half_unscaled)
     return a, keep
 
 
@@ -509,12 +527,23 @@ def rccl_unique_id() -> bytes:
     return buf.raw
 
 
-def solve_loopback(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, nranks: int = 2, **opts) -> Result:
-    """The row-partitioned engine with `nranks` ranks as threads on one GPU."""
+def solve_loopback(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, nranks: int = 2,
+                   layouts: Optional[list] = None, **opts) -> Result:
+    """The row-partitioned engine with `nranks` ranks as threads on one GPU.
+    `layouts`: a list that receives one dict per rank (mpg_rank_layout)."""
     opts.pop("engine", None)
     args, keep = make_args(A, b, x_true, engine="fused", **opts)
     lib = host_lib()
-    return run_solve(lambda a, r: lib.mpg_solve_loopback(a, nranks, r), args, A.nrows)
+    lay = (RankLayout * nranks)()
+    res = run_solve(lambda a, r: lib.mpg_solve_loopback_ex(a, nranks, r, C.cast(lay, C.c_void_p)), args, A.nrows)
+    if layouts is not None:
+        forms = {-1: "none", 0: "int32", 1: "int16", 2: "stepped"}
+        for L in lay:
+            d = {f: getattr(L, f) for f, _ in RankLayout._fields_ if f != "pad_"}
+            d["format"] = {1: "csr", 2: "sell"}.get(d["format"], d["format"])
+            d["col_form"] = forms[d["col_form"]]
+            layouts.append(d)
+    return res
 
 
 class Engine:
@@ -609,6 +638,22 @@ class Engine:
             raise RuntimeError("mpg_engine_spmv_layout failed")
         return {"format": {1: "csr", 2: "sell"}[f.value], "vec_width": w.value, "col_bytes": cb.value,
                 "stored": st.value, "window": bool(win.value)}
+
+    def sell_columns(self) -> dict:
+        """Column form of the Arnoldi SpMV's SELL copy (mpg_engine_sell_columns):
+        {"form": "none"|"int32"|"int16"|"stepped", "csr_slices", "implicit_slices"}."""
+        f, e, i = C.c_int32(), C.c_int64(), C.c_int64()
+        if self._lib.mpg_engine_sell_columns(self._h, C.byref(f), C.byref(e), C.byref(i)):
+            raise RuntimeError("mpg_engine_sell_columns failed")
+        return {"form": {-1: "none", 0: "int32", 1: "int16", 2: "stepped"}[f.value], "csr_slices": e.value,
+                "implicit_slices": i.value}
+
+    def half_stats(self) -> dict:
+        """mixed-half: what the fp16 cast did (mpg_engine_half_stats)."""
+        st = (C.c_int64 * 4)()
+        if self._lib.mpg_engine_half_stats(self._h, st):
+            raise RuntimeError("mpg_engine_half_stats failed")
+        return dict(zip(("rows_scaled", "flushed", "overflowed", "exp_out_of_range"), map(int, st)))
 
     def close(self) -> None:
         if self._h:

@@ -36,6 +36,7 @@ class SolveArgs(C.Structure):
         ("device", C.c_int32),
         ("threads", C.c_int32),
         ("spmv_format", C.c_int32),
+        ("half_unscaled", C.c_int32),
     ]
 
 
@@ -121,3 +122,21 @@ def condest_args(A, rand_seed: int = 42, max_iters: int = 100000, verbose: bool 
 
 def condest_dict(r: CondestResult) -> dict:
     return {k: getattr(r, k) for k, _ in CondestResult._fields_ if k != "message"}
+
+
+class RankLayout(C.Structure):
+    """mpg_rank_layout (dist.h): one rank's Arnoldi SpMV storage and numbering."""
+    _fields_ = [
+        ("format", C.c_int32),
+        ("col_form", C.c_int32),
+        ("vec_width", C.c_int32),
+        ("window", C.c_int32),
+        ("n_local", C.c_int32),
+        ("n_front", C.c_int32),
+        ("n_ext", C.c_int32),
+        ("pad_", C.c_int32),
+        ("row0", C.c_int64),
+        ("csr_slices", C.c_int64),
+        ("implicit_slices", C.c_int64),
+        ("half_rows_scaled", C.c_int64),
+    ]

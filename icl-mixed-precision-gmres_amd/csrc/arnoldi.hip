@@ -133,9 +133,9 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
                                                           double* __restrict__ partial,
                                                           const int32_t* __restrict__ sbase,
                                                           const int32_t* __restrict__ spat, const CI* __restrict__ pat,
-                                                          const int32_t* __restrict__ rowptr,
-                                                          const int32_t* __restrict__ ccol,
-                                                          const X* __restrict__ cval, int xcd) {
+                                                          const int32_t* __restrict__ xrp,
+                                                          const int32_t* __restrict__ xcol,
+                                                          const X* __restrict__ xval, int xcd) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
         } else {
             auto xv = [&](int c) { return (double)x[c]; };
             if (SellCol<CI>::stepped && row.exc) {
-                sum = csr_row_sum(own ? i : -1, rowptr, ccol, cval, xv);
+                sum = csr_row_sum(own ? row.xrow : -1, xrp, xcol, xval, xv);
             } else {
                 row.sum(0, xv, sum);
                 for (int q = row.U; q < row.steps; q += row.U) {
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
                                                       int64_t nnz, const T* __restrict__ wprev,
                                                       const T* __restrict__ inv_p, T* __restrict__ V, int64_t ld,
                                                       int k, const P* __restrict__ diag, T* __restrict__ w,
-                                                      GivensFold<T> fold) {
+                                                      GivensFold<T> fold, const int8_t* __restrict__ rexp) {
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
     const T inv = fold_givens<FOLD>(fold, inv_p);
@@ -391,12 +391,13 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
     struct Ops {
         T wp;
         P d;
+        int e;  // row exponent of a scaled fp16 copy (mpg_csr_half_values)
     };
     for_rows(
         blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)(T)(wprev[c] * inv); },
-        [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0)}; },
+        [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0), rexp ? (int)rexp[i] : 0}; },
         [&](int i, double sum, const Ops& o) {
-            const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
+            const T t = (T)ldexp(sum, -o.e);  // spmv(1, A, v, 0, w): y = 1*t (exact unscale)
             P pw = (P)t;         // = precond<T, P> with the diagonal loaded ahead
             if (diag) pw = P(0) * pw + P(1) * o.d * pw;
             w[i] = (T)pw;
@@ -448,9 +449,10 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
                                                       GivensFold<T> fold, SellDots dd,
                                                       const int32_t* __restrict__ sbase,
                                                       const int32_t* __restrict__ spat, const CI* __restrict__ pat,
-                                                      const int32_t* __restrict__ rowptr,
-                                                      const int32_t* __restrict__ ccol,
-                                                      const typename SellStore<VI>::type* __restrict__ cval, int xcd) {
+                                                      const int32_t* __restrict__ xrp,
+                                                      const int32_t* __restrict__ xcol,
+                                                      const typename SellStore<VI>::type* __restrict__ xval,
+                                                      const int8_t* __restrict__ rexp, int xcd) {
     static_assert(DN == 0 || BS == kBlock, "the fused dots' partials assume kBlock-thread workgroups");
     using S = typename SellStore<VI>::type;
     constexpr int NQ = kWinLen / kWave;
@@ -496,6 +498,11 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
     // 3. the slice's first batch
     row.init_finish(lane, col, val, sbase, pat);
     row.load(0);
+    // 4. a scaled fp16 copy's row exponent (needed last, issued last)
+    int rex = 0;
+    if constexpr (std::is_same_v<VI, half_v>) {
+        if (rexp) rex = rexp[live && i < n ? i : 0];
+    }
     __builtin_amdgcn_sched_barrier(0);
     // the scale 1/h_{k,k-1}: the folded Givens step, or the Givens kernel's
     T inv;
@@ -550,7 +557,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
         } else {
             auto xv = [&](int c) { return (double)(T)(wprev[c] * inv); };
             if (SellCol<CI>::stepped && row.exc) {
-                sum = csr_row_sum(i < n ? i : -1, rowptr, ccol, cval, xv);
+                sum = csr_row_sum(i < n ? row.xrow : -1, xrp, xcol, xval, xv);
             } else {
                 row.sum(0, xv, sum);
                 for (int q = row.U; q < row.steps; q += row.U) {
@@ -563,6 +570,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
     }
     T wi = T(0);
     if (live && i < n) {
+        if constexpr (std::is_same_v<VI, half_v>) sum = ldexp(sum, -rex);  // exact unscale (0: unchanged)
         const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
         wi = precond<T, P>(t, diag, i);
         w[i] = wi;
@@ -1282,6 +1290,7 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
     int combo = combo_of(*desc);
     if (combo < 0) return MPG_ERR_UNSUPPORTED;
     if (desc->A->rows != desc->n || desc->A->cols > desc->n_ext) return MPG_ERR_ARG;
+    if (desc->inner_row_exp && desc->inner_val != MPG_F16) return MPG_ERR_ARG;  // only fp16 copies are scaled
     mpg_arnoldi* a = new (std::nothrow) mpg_arnoldi();
     if (!a) return MPG_ERR_ALLOC;
     a->ctx = ctx;
@@ -1343,9 +1352,20 @@ int64_t mpg_arnoldi_sell_matrix_bytes(mpg_arnoldi_t a) {
     const int64_t steps = S.padded / ((int64_t)kWave * S.W);
     // every slot's value; the columns of slots outside implicit slices (the
     // shared patterns are a few cache lines); int64 slice offsets; the
-    // pattern indices; the stepped form's bases
+    // pattern indices; the stepped form's bases; a scaled fp16 copy's row
+    // exponents
     return S.padded * vbytes + (S.padded - S.imp_slots) * S.col_bytes() + S.npat * S.col_bytes() +
-           ((int64_t)S.nslices + 1) * 8 + (S.spat ? (int64_t)S.nslices * 4 : 0) + (S.c16s ? steps * S.W * 4 : 0);
+           ((int64_t)S.nslices + 1) * 8 + (S.spat ? (int64_t)S.nslices * 4 : 0) + (S.c16s ? steps * S.W * 4 : 0) +
+           (a->d.inner_row_exp ? (int64_t)a->d.n : 0);
+}
+
+int mpg_arnoldi_sell_columns(mpg_arnoldi_t a, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices) {
+    if (!a) return MPG_ERR_ARG;
+    const SellCopy& S = a->sell;
+    if (form) *form = S.nslices == 0 ? -1 : S.c16 ? 1 : S.c16s ? 2 : 0;
+    if (csr_slices) *csr_slices = S.nexc;
+    if (implicit_slices) *implicit_slices = S.nimp;
+    return MPG_OK;
 }
 
 int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
@@ -1393,7 +1413,7 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
                             a->d.n, -a->front, a->d.n_ext, S->nslices, S->off, static_cast<const CI*>(S->col),
                             static_cast<const X*>(S->val), static_cast<const X*>(a->d.x),
                             static_cast<const X*>(a->d.b), diag, static_cast<T*>(a->w[0]), a->partial, S->sbase,
-                            S->spat, static_cast<const CI*>(S->pat), A->rowptr, A->col, static_cast<const X*>(a->d.val_outer),
+                            S->spat, static_cast<const CI*>(S->pat), S->xrp, S->xcol, static_cast<const X*>(S->xval),
                             sell_xcd_order(*S) ? 1 : 0);
                     return (int)MPG_OK;
                 });
@@ -1490,8 +1510,8 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
                             static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd,
-                            S.sbase, S.spat, static_cast<const CI*>(S.pat), A->rowptr, A->col,
-                            static_cast<const typename SellStore<VI>::type*>(a->d.val_inner),
+                            S.sbase, S.spat, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
+                            static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
                             sell_xcd_order(S) ? 1 : 0);
                     return (int)MPG_OK;
                 };
@@ -1521,7 +1541,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
         launch_timed(a->ctx, kern, dim3(rb_grid(a)), dim3(kBlock),
             A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,
             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,
-            diag, static_cast<T*>(a->w[(k + 1) & 1]), gf);
+            diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp);
         return (int)MPG_OK;
     });
     if (st) return st;

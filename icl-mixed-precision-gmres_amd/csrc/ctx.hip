@@ -17,6 +17,7 @@ const char* mpg_error_string(int status) {
         case MPG_ERR_RCCL: return "RCCL error";
         case MPG_ERR_UNSUPPORTED: return "unsupported operation";
         case MPG_ERR_BREAKDOWN: return "Arnoldi breakdown / non-finite value";
+        case MPG_ERR_RANGE: return "value outside the storage precision's range";
         default: return "unknown mpgmres status";
     }
 }

@@ -145,8 +145,8 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
                                                       const CI* __restrict__ col, const S* __restrict__ val,
                                                       const int32_t* __restrict__ sbase,
                                                       const int32_t* __restrict__ spat, const CI* __restrict__ pat,
-                                                      const int32_t* __restrict__ rowptr,
-                                                      const int32_t* __restrict__ ccol, const S* __restrict__ cval,
+                                                      const int32_t* __restrict__ xrp,
+                                                      const int32_t* __restrict__ xcol, const S* __restrict__ xval,
                                                       const X* __restrict__ x, X alpha, X beta, X* __restrict__ y,
                                                       int xcd, ScalarProgram prog) {
     constexpr int NQ = kWinLen / kWave;
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
     } else {
         auto xv = [&](int c) { return (double)x[c]; };
         if (SellCol<CI>::stepped && row.exc) {
-            sum = csr_row_sum(i < n ? i : -1, rowptr, ccol, cval, xv);
+            sum = csr_row_sum(i < n ? row.xrow : -1, xrp, xcol, xval, xv);
         } else {
             row.sum(0, xv, sum);
             for (int q = row.U; q < row.steps; q += row.U) {
@@ -332,9 +332,10 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
         if (nimp || nexc) {
             spat_h.assign((size_t)ns, -1);
             std::map<std::vector<int32_t>, int32_t> index;
+            int32_t e = 0;
             for (int s2 = 0; s2 < ns; ++s2) {
                 if (kind[s2] == kSliceCsr && S.c16s) {
-                    spat_h[s2] = -2;
+                    spat_h[s2] = -2 - e++;
                 } else if (kind[s2] == kSliceImplicit) {
                     const int64_t b0 = off[s2] / kWave, b1 = off[s2 + 1] / kWave;
                     std::vector<int32_t> key(bases.begin() + b0, bases.begin() + b1);
@@ -380,6 +381,48 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
             return (int)MPG_OK;
         });
     });
+    if (!st && S.nexc > 0) {
+        // the flagged slices' rows as a CSR the copy owns (the caller's CSR
+        // and values may be freed once the copy exists): row 64 e + lane of
+        // the e-th flagged slice, entries copied in CSR order, runs of
+        // adjacent flagged slices in one copy each
+        std::vector<int32_t> xrp_h((size_t)S.nexc * kWave + 1, 0);
+        std::vector<std::pair<int64_t, int64_t>> runs;  // (first entry, entry count) per run of flagged slices
+        int64_t e = 0, at = 0;
+        for (int s2 = 0; s2 < ns; ++s2) {
+            if (spat_h[s2] > -2) continue;
+            for (int l = 0; l < kWave; ++l) {
+                const int r = s2 * kWave + l;
+                const int64_t len = r < n ? (int64_t)rp[r + 1] - rp[r] : 0;
+                at += len;
+                xrp_h[(size_t)e * kWave + l + 1] = (int32_t)at;
+            }
+            const int64_t b0 = rp[s2 * kWave], b1 = rp[std::min(n, (s2 + 1) * kWave)];
+            if (!runs.empty() && runs.back().first + runs.back().second == b0) runs.back().second += b1 - b0;
+            else runs.emplace_back(b0, b1 - b0);
+            ++e;
+        }
+        if (hipMalloc((void**)&S.xrp, xrp_h.size() * 4) != hipSuccess ||
+            hipMalloc((void**)&S.xcol, (size_t)at * 4 + 256) != hipSuccess ||
+            hipMalloc(&S.xval, (size_t)at * vsize + 256) != hipSuccess) {
+            st = MPG_ERR_ALLOC;
+        } else if (hipMemcpyAsync(S.xrp, xrp_h.data(), xrp_h.size() * 4, hipMemcpyHostToDevice, stream) != hipSuccess) {
+            st = MPG_ERR_HIP;
+        } else {
+            int64_t dst = 0;
+            for (const auto& rn : runs) {
+                if (hipMemcpyAsync(S.xcol + dst, A->col + rn.first, (size_t)rn.second * 4, hipMemcpyDeviceToDevice,
+                                   stream) != hipSuccess ||
+                    hipMemcpyAsync(static_cast<char*>(S.xval) + dst * vsize,
+                                   static_cast<const char*>(val) + rn.first * vsize, (size_t)rn.second * vsize,
+                                   hipMemcpyDeviceToDevice, stream) != hipSuccess) {
+                    st = MPG_ERR_HIP;
+                    break;
+                }
+                dst += rn.second;
+            }
+        }
+    }
     if (!st && !spat_h.empty()) {
         // implicit patterns in the copy's column type (int16 forms: the
         // offsets fit, since every slice's columns do)
@@ -416,6 +459,9 @@ void sell_free(SellCopy& S) {
     if (S.off) (void)hipFree(S.off);
     if (S.col) (void)hipFree(S.col);
     if (S.val) (void)hipFree(S.val);
+    if (S.xrp) (void)hipFree(S.xrp);
+    if (S.xcol) (void)hipFree(S.xcol);
+    if (S.xval) (void)hipFree(S.xval);
     S = SellCopy{};
 }
 
@@ -424,9 +470,7 @@ void sell_free(SellCopy& S) {
 struct mpg_sell {
     mpg_ctx* ctx = nullptr;
     int cols = 0;
-    SellCopy S;
-    const mpg_csr* A = nullptr;  // the CSR the copy was built from (flagged slices read it)
-    const void* vals = nullptr;
+    SellCopy S;  // owns all its device memory (the flagged slices' rows included)
 };
 
 namespace {
@@ -443,7 +487,7 @@ int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y,
         return sell_dispatch_win(S.win, [&](auto wn) {
             k_sell_spmv<X, St, CI, decltype(wc)::value, decltype(wn)::value><<<grid, kBlock, 0, ctx->stream>>>(
                 S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val), S.sbase,
-                S.spat, static_cast<const CI*>(S.pat), A->A->rowptr, A->A->col, static_cast<const St*>(A->vals), x, alpha, beta, y,
+                S.spat, static_cast<const CI*>(S.pat), S.xrp, S.xcol, static_cast<const St*>(S.xval), x, alpha, beta, y,
                 sell_xcd_order(S) ? 1 : 0, prog);
             return (int)MPG_OK;
         });
@@ -465,8 +509,6 @@ int mpg_sell_create(mpg_ctx_t ctx, mpg_csr_t A, int32_t vtype, const void* vals,
     if (!h) return MPG_ERR_ALLOC;
     h->ctx = ctx;
     h->cols = A->cols;
-    h->A = A;
-    h->vals = vals;
     if (int st = sell_build(ctx, A, vtype, vals, format, h->S)) {
         delete h;
         return st;

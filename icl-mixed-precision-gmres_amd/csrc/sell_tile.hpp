@@ -19,8 +19,10 @@
 //             (the 27-point 3-dof Queen stand-in: offsets up to +-37,299)
 //             still store 2-B columns, plus 4 B per 64 entries. A slice where
 //             some (step, element) spreads wider (rows on both sides of a
-//             boundary plane) gets spat[s] = -2 and its rows are summed
-//             from the CSR arrays instead, in the same order (same bits);
+//             boundary plane) gets spat[s] = -2 - e (e: its ordinal
+//             among such slices) and its rows are summed from the copy's
+//             own CSR of those rows (xrp/xcol/xval, row 64 e + lane) in the
+//             same order (same bits);
 //   int32_t   c.
 // Implicit slices: a slice whose 64 rows all have the same column offsets
 // c - row in the same order (every interior slice of a banded matrix) reads
@@ -28,8 +30,8 @@
 // run of lane-relative offsets in `pat` that every lane of the wave loads
 // (the same address: one cache line), decoded against the lane's own row.
 // Identical patterns are stored once, so BAND-10M's 20 MB of int16 columns
-// become one 10-entry pattern. spat[s] = -1: stored columns; -2 (stepped
-// form): the slice is summed from the CSR arrays (below).
+// become one 10-entry pattern. spat[s] = -1: stored columns; <= -2 (stepped
+// form): the slice is summed from the copy's sub-CSR (below).
 // Padding carries a sentinel column and is skipped, so an Inf/NaN in x never
 // meets a padded zero. Within a row the entries keep CSR order and the fp64
 // sum runs in that order.
@@ -104,45 +106,6 @@ template <class S, bool NT> struct VecW<S, 1, NT> {
 constexpr int kSellBatch = MPG_SELL_BATCH;
 template <int W> constexpr int sell_unroll() { return W >= kSellBatch ? 1 : kSellBatch / W; }
 
-// fp64 row sum of row 64 s + lane (lane valid or not: all lanes take part).
-template <class S, class CI, int W, class XF>
-__device__ __forceinline__ double sell_row_sum(int s, int lane, const int64_t* __restrict__ off,
-                                               const CI* __restrict__ col, const S* __restrict__ val, XF xval) {
-    constexpr int U = sell_unroll<W>();
-    const int64_t o = off[s];
-    const int steps = (int)((off[s + 1] - o) / (kWave * W));
-    const int row0 = s * kWave;
-    const CI* __restrict__ cp = col + o + lane * W;
-    const S* __restrict__ vp = val + o + lane * W;
-    double acc = 0.0;
-    for (int q = 0; q < steps; q += U) {
-        CI c[U][W];
-        S v[U][W];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (q + u < steps) {
-                VecW<CI, W>::load(cp + (int64_t)(q + u) * kWave * W, c[u]);
-                VecW<S, W>::load(vp + (int64_t)(q + u) * kWave * W, v[u]);
-            } else {
-#pragma unroll
-                for (int e = 0; e < W; ++e) c[u][e] = SellCol<CI>::kPad;
-            }
-        }
-        double x[U][W];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int e = 0; e < W; ++e)
-                x[u][e] = SellCol<CI>::live(c[u][e]) ? xval(SellCol<CI>::decode(c[u][e], SellCol<CI>::stored_base(row0), row0)) : 0.0;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int e = 0; e < W; ++e)
-                if (SellCol<CI>::live(c[u][e])) acc += widen(v[u][e]) * x[u][e];
-    }
-    return acc;
-}
-
 // The same row sum split into load and sum halves, so a kernel can issue a
 // batch of slice loads early (before loads it needs sooner have returned,
 // or before a barrier) and consume it later. Loads are unconditional: steps
@@ -160,8 +123,9 @@ struct SellRow {
     S v[U][W];
     int32_t bq[kStepped ? U : 1][kStepped ? W : 1];  // stepped columns: the batch's bases
     int steps, row0, lane_row, rbase;
-    int pk = -1;       // spat[s]: >= 0 implicit pattern, -1 stored, -2 summed from CSR
+    int pk = -1;       // spat[s]: >= 0 implicit pattern, -1 stored, -2 - e summed from CSR
     bool exc = false;  // stepped: this slice is summed from CSR
+    int xrow = 0;      // exc: this lane's row in the copy's sub-CSR
     const CI* __restrict__ cp;
     int64_t cstride;   // column entries between steps: 64 W stored, W for a pattern
     const S* __restrict__ vp;
@@ -192,7 +156,8 @@ struct SellRow {
         cstride = imp ? W : (int64_t)kWave * W;
         rbase = imp ? lane_row : SellCol<CI>::stored_base(row0);
         vp = val + base;
-        exc = pk == -2;
+        exc = pk <= -2;
+        xrow = exc ? (-2 - pk) * kWave + lane : 0;
         if constexpr (kStepped) bp = sbase + (steps > 0 ? o0 / kWave : 0);  // (o0 / (64 W)) W
     }
     __device__ __forceinline__ void init(int s, int lane, const int64_t* __restrict__ off, const CI* __restrict__ col,
@@ -233,8 +198,8 @@ struct SellRow {
     }
 };
 
-// The row sum from the CSR arrays in CSR order with SellRow::sum's
-// arithmetic (a stepped copy's flagged slices); i < 0: no row, 0.
+// The row sum from a CSR in CSR order with SellRow::sum's arithmetic (a
+// stepped copy's flagged slices, from the copy's sub-CSR); i < 0: no row, 0.
 template <class S, class XF>
 __device__ __forceinline__ double csr_row_sum(int i, const int32_t* __restrict__ rowptr,
                                               const int32_t* __restrict__ col, const S* __restrict__ val, XF xval) {
@@ -264,6 +229,9 @@ struct SellCopy {
     int32_t* spat = nullptr;   // per slice: implicit pattern index, -1 stored, -2 CSR (nullptr: all stored)
     void* pat = nullptr;       // the implicit slices' column patterns (CI entries, W per step)
     int64_t nexc = 0;          // c16s: slices summed from CSR
+    int32_t* xrp = nullptr;    // their rows as a CSR owned by the copy: 64 nexc + 1 row starts
+    int32_t* xcol = nullptr;   //   (row 64 e + lane of flagged slice e; rows past n are empty),
+    void* xval = nullptr;      //   columns and values (the stored value type) in CSR order
     int64_t nimp = 0;          // implicit slices
     int64_t imp_slots = 0;     // their slots (their columns are not read)
     int64_t npat = 0;          // pattern entries

@@ -19,6 +19,8 @@
 
 #include <cfloat>
 #include <new>
+#include <string>
+#include <type_traits>
 #include <vector>
 
 using namespace mpg;
@@ -47,14 +49,95 @@ __global__ __launch_bounds__(kBlock) void k_csr_adaptive(const int32_t* __restri
         prod, scratch);
 }
 
+// fp16 values scaled per row (mpg_csr_half_values): the row sum times 2^-e_i
+template <class X>
+__global__ __launch_bounds__(kBlock) void k_csr_adaptive_scaled(const int32_t* __restrict__ blocks,
+                                                                const int32_t* __restrict__ bnnz,
+                                                                const int32_t* __restrict__ rowptr,
+                                                                const int32_t* __restrict__ col,
+                                                                const uint16_t* __restrict__ val, int64_t nnz,
+                                                                const int8_t* __restrict__ rexp,
+                                                                const X* __restrict__ x, X alpha, X beta,
+                                                                X* __restrict__ y) {
+    __shared__ double prod[kNnzCap];
+    __shared__ double scratch[kBlock / kWave];
+    struct Pre {
+        X yi;
+        int e;
+    };
+    const int b = blockIdx.x;
+    csr_row_block(
+        blocks[b], blocks[b + 1], bnnz[b], bnnz[b + 1], rowptr, col, val, nnz, [&](int c) { return (double)x[c]; },
+        [&](int i) { return Pre{beta == X(0) ? X(0) : y[i], (int)rexp[i]}; },
+        [&](int i, double sum, const Pre& p) {
+            const X t = (X)ldexp(sum, -p.e);
+            y[i] = beta == X(0) ? alpha * t : alpha * t + beta * p.yi;
+        },
+        prod, scratch);
+}
+
 template <class V, class X>
-int spmv_impl(mpg_ctx* ctx, mpg_csr* A, X alpha, const V* vals, const X* x, X beta, X* y) {
+int spmv_impl(mpg_ctx* ctx, mpg_csr* A, X alpha, const V* vals, const X* x, X beta, X* y,
+              const int8_t* rexp = nullptr) {
     if (!ctx || !A) return MPG_ERR_ARG;
     if (A->rows == 0) return MPG_OK;
+    if constexpr (std::is_same_v<V, uint16_t>) {
+        if (rexp) {
+            k_csr_adaptive_scaled<X><<<A->nblocks, kBlock, 0, ctx->stream>>>(
+                A->blocks, A->bnnz, A->rowptr, A->col, vals, A->nnz, rexp, x, alpha, beta, y);
+            MPG_LAUNCH_CHECK(ctx);
+            return MPG_OK;
+        }
+    }
     k_csr_adaptive<V, X><<<A->nblocks, kBlock, 0, ctx->stream>>>(A->blocks, A->bnnz, A->rowptr, A->col, vals, A->nnz, x,
                                                                  alpha, beta, y);
     MPG_LAUNCH_CHECK(ctx);
     return MPG_OK;
+}
+
+// ---------------- fp16 values with power-of-two row scaling ----------------
+// One thread per row: the row's largest finite |a|, its exponent e (0 when
+// the row is in range), then half(float(a * 2^e)) for each entry, counting
+// what the cast loses (stats: rows scaled, flushed to 0, overflowed, e out
+// of int8). mpg_csr_half_values, capi.h.
+constexpr int kHalfRowLo = -2, kHalfRowHi = 14, kHalfRowTop = 14;
+
+__global__ __launch_bounds__(kBlock) void k_half_rows(int32_t rows, const int32_t* __restrict__ rowptr,
+                                                      const double* __restrict__ val, int scale,
+                                                      uint16_t* __restrict__ out, int8_t* __restrict__ rexp,
+                                                      unsigned long long* __restrict__ stats) {
+    unsigned long long cnt[4] = {0, 0, 0, 0};
+    const int stride = gridDim.x * kBlock;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < rows; i += stride) {
+        const int j0 = rowptr[i], j1 = rowptr[i + 1];
+        double m = 0.0;
+        for (int j = j0; j < j1; ++j) {
+            const double a = fabs(val[j]);
+            if (a <= DBL_MAX && a > m) m = a;
+        }
+        int e = 0;
+        if (scale && m > 0.0) {
+            const int E = ilogb(m);
+            if (E < kHalfRowLo || E > kHalfRowHi) e = kHalfRowTop - E;
+            if (e < -127 || e > 127) {
+                ++cnt[3];
+                e = 0;
+            }
+        }
+        cnt[0] += e != 0;
+        if (rexp) rexp[i] = (int8_t)e;
+        for (int j = j0; j < j1; ++j) {
+            const double a = val[j];
+            const uint16_t h = __half_as_ushort(__float2half_rn((float)ldexp(a, e)));
+            if (fabs(a) <= DBL_MAX) {
+                cnt[1] += a != 0.0 && (h & 0x7fffu) == 0;
+                cnt[2] += (h & 0x7fffu) == 0x7c00u;
+            }
+            out[j] = h;
+        }
+    }
+    for (int q = 0; q < 4; ++q)
+        if (cnt[q]) atomicAdd(stats + q, cnt[q]);
 }
 
 // ---------------- Jacobi setup (types.hpp:393-431) ----------------
@@ -198,6 +281,36 @@ int mpg_csr_spmv_f32(mpg_ctx_t c, mpg_csr_t A, float alpha, const float* vals, c
 }
 int mpg_csr_spmv_f16f32(mpg_ctx_t c, mpg_csr_t A, float alpha, const uint16_t* vals, const float* x, float beta, float* y) {
     return spmv_impl<uint16_t, float>(c, A, alpha, vals, x, beta, y);
+}
+int mpg_csr_spmv_f16f32_scaled(mpg_ctx_t c, mpg_csr_t A, float alpha, const uint16_t* vals, const int8_t* row_exp,
+                               const float* x, float beta, float* y) {
+    if (!row_exp) return MPG_ERR_ARG;
+    return spmv_impl<uint16_t, float>(c, A, alpha, vals, x, beta, y, row_exp);
+}
+
+int mpg_csr_half_values(mpg_ctx_t c, mpg_csr_t A, const double* vals, int32_t scale, uint16_t* out, int8_t* row_exp,
+                        int64_t* stats) {
+    if (!c || !A || (A->nnz > 0 && (!vals || !out)) || (scale && !row_exp)) return MPG_ERR_ARG;
+    int64_t h[4] = {0, 0, 0, 0};
+    if (A->rows > 0) {
+        unsigned long long* d = reinterpret_cast<unsigned long long*>(c->red_ws);
+        if (hipMemsetAsync(d, 0, 4 * sizeof(unsigned long long), c->stream) != hipSuccess) return MPG_ERR_HIP;
+        k_half_rows<<<grid_for(A->rows, 1), kBlock, 0, c->stream>>>(A->rows, A->rowptr, vals, scale ? 1 : 0, out,
+                                                                    row_exp, d);
+        MPG_LAUNCH_CHECK(c);
+        if (hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            return MPG_ERR_HIP;
+    }
+    if (stats)
+        for (int q = 0; q < 4; ++q) stats[q] = h[q];
+    if (h[2] || h[3] || (!scale && h[1])) {
+        c->last_error = "fp16 values: " + std::to_string(h[2]) + " entries overflow, " + std::to_string(h[1]) +
+                        " nonzero entries round to 0, " + std::to_string(h[3]) + " row exponents out of range" +
+                        (scale ? "" : " (row scaling off)");
+        return MPG_ERR_RANGE;
+    }
+    return MPG_OK;
 }
 
 int mpg_jacobi_rowmax_f64(mpg_ctx_t c, mpg_csr_t A, const double* vals, double* out) { return rowmax_impl<double>(c, A, vals, out); }

@@ -474,6 +474,10 @@ int mpg_engine_create_dist_host(const mpg_solve_args* a, mpg_halo_t plan, const 
 }
 
 int mpg_solve_loopback(const mpg_solve_args* a, int32_t P, mpg_solve_result* r) {
+    return mpg_solve_loopback_ex(a, P, r, nullptr);
+}
+
+int mpg_solve_loopback_ex(const mpg_solve_args* a, int32_t P, mpg_solve_result* r, mpg_rank_layout* layouts) {
     if (!a || !r || P < 1 || a->n < P) return MPG_ERR_ARG;
     r->status = MPG_RESULT_ERROR;
     r->message[0] = 0;
@@ -522,6 +526,20 @@ int mpg_solve_loopback(const mpg_solve_args* a, int32_t P, mpg_solve_result* r) 
                     la.x_true = a->x_true ? a->x_true + r0 : nullptr;
                     if (q != 0) la.verbose = 0;
                     FusedEngine e(ctx, la, &comm, mpg_halo_n_ext(plans[q]), plans[q]->n_front);
+                    if (layouts) {
+                        mpg_rank_layout& L = layouts[q];
+                        L = mpg_rank_layout{};
+                        int64_t stored = 0;
+                        check(mpg_arnoldi_spmv_layout(e.arnoldi(), &L.format, &L.vec_width, nullptr, &stored,
+                                                      &L.window), "layout", ctx);
+                        check(mpg_arnoldi_sell_columns(e.arnoldi(), &L.col_form, &L.csr_slices, &L.implicit_slices),
+                              "columns", ctx);
+                        L.n_local = la.n;
+                        L.n_front = plans[q]->n_front;
+                        L.n_ext = mpg_halo_n_ext(plans[q]);
+                        L.row0 = r0;
+                        L.half_rows_scaled = e.half_stats()[0];
+                    }
                     bool done = false;
                     while (!done) e.run(1 << 20, done);
                     e.sync();

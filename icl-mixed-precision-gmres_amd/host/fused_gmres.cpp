@@ -94,6 +94,8 @@ struct FusedEngine::Impl {
     void* xp = nullptr;  // row 0 of x (x.p + front entries)
     int64_t nnz = 0;
     DevMem rowptr, col, val64, val_outer_own, val_inner_own, diag, b, x, tmp_t, tmp_p, scal;
+    DevMem row_exp;                 // mixed-half: per-row exponents of the scaled fp16 values
+    int64_t half_stats[4] = {0, 0, 0, 0};
     const void* val_outer = nullptr;
     const void* val_inner = nullptr;
     mpg_csr_t csr = nullptr;
@@ -232,7 +234,19 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     } else {
         I.val_outer = I.val64.p;
         I.val_inner_own = DevMem(ctx, std::max<size_t>(nz, 1) * dsize(ty.VI));
-        I.cast(I.val64.p, MPG_F64, I.val_inner_own.p, ty.VI, (int64_t)nz);
+        if (ty.VI == MPG_F16) {
+            // fp16 values, scaled per row by powers of two where a row's
+            // magnitude falls outside fp16's range (mpg_csr_half_values);
+            // with a.half_unscaled such a matrix fails here (MPG_ERR_RANGE)
+            const bool scale = a.half_unscaled == 0;
+            if (scale) I.row_exp = DevMem(ctx, (size_t)I.n + 64);
+            check(mpg_csr_half_values(ctx, I.csr, I.val64.as<double>(), scale ? 1 : 0,
+                                      I.val_inner_own.as<uint16_t>(), scale ? I.row_exp.as<int8_t>() : nullptr,
+                                      I.half_stats),
+                  "fp16 Arnoldi values", ctx);
+        } else {
+            I.cast(I.val64.p, MPG_F64, I.val_inner_own.p, ty.VI, (int64_t)nz);
+        }
         I.val_inner = I.val_inner_own.p;
     }
 
@@ -325,6 +339,8 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     d.x = I.xp;
     d.spmv_format = a.spmv_format;
     d.n_front = n_front;
+    // rows all in range: the unscaled kernels (no exponent loads, same bits)
+    d.inner_row_exp = I.half_stats[0] > 0 ? I.row_exp.as<int8_t>() : nullptr;
     check(mpg_arnoldi_create(ctx, &d, &I.arn), "mpg_arnoldi_create", ctx);
     // ranks all-reduce per-workgroup partials in place: same count on every rank
     if (comm) check(mpg_arnoldi_uniform_groups(I.arn), "uniform groups", ctx);
@@ -795,6 +811,7 @@ double FusedEngine::phase_bytes(int which) const {
 }
 
 mpg_arnoldi_t FusedEngine::arnoldi() const { return p_->arn; }
+const int64_t* FusedEngine::half_stats() const { return p_->half_stats; }
 
 // Device-event time of one phase kernel in its place in the cycle: `reps`
 // restart cycles run eagerly in cycle order, and at every launch of phase
@@ -983,6 +1000,17 @@ int mpg_engine_spmv_layout(mpg_engine_t e, int32_t* format, int32_t* vec_width, 
                            int64_t* stored, int32_t* window) {
     if (!e || !e->eng) return MPG_ERR_ARG;
     return mpg_arnoldi_spmv_layout(e->eng->arnoldi(), format, vec_width, col_bytes, stored, window);
+}
+
+int mpg_engine_sell_columns(mpg_engine_t e, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices) {
+    if (!e || !e->eng) return MPG_ERR_ARG;
+    return mpg_arnoldi_sell_columns(e->eng->arnoldi(), form, csr_slices, implicit_slices);
+}
+
+int mpg_engine_half_stats(mpg_engine_t e, int64_t* stats) {
+    if (!e || !e->eng || !stats) return MPG_ERR_ARG;
+    for (int q = 0; q < 4; ++q) stats[q] = e->eng->half_stats()[q];
+    return MPG_OK;
 }
 
 int mpg_engine_destroy(mpg_engine_t e) {

@@ -81,6 +81,9 @@ public:
     double time_phase(int which, int reps, bool inplace = false, std::vector<double>* per_launch = nullptr);
     double phase_bytes(int which) const;
     mpg_arnoldi_t arnoldi() const;
+    // mixed-half: what the fp16 cast of the Arnoldi values did (stats of
+    // mpg_csr_half_values, capi.h; zeros in other modes)
+    const int64_t* half_stats() const;
     void sync();
 
     // history (per restart / per step)

@@ -7,7 +7,8 @@
 // --jacobi-steps --gpu (accepted; this build always runs on the GPU).
 // Additions: --matrix band:N[:LO:HI[:SEED]] | laplace:NX[:NY:NZ] |
 // stencil27:NX[:DOF[:SEED]] (synthetic input instead of --Apath,
-// mpg_gen_spec), --mode mixed-half, --engine {fused,surface},
+// mpg_gen_spec), --mode mixed-half, --half-unscaled (mixed-half: plain fp16
+// cast, a value outside fp16's range is an error), --engine {fused,surface},
 // --device D.
 #include <cmath>
 #include <cstdio>
@@ -68,6 +69,7 @@ int main(int argc, char* argv[]) {
         else if (f == "--jacobi-steps") a.jacobi_steps = std::stoi(next());
         else if (f == "--gpu") { /* always on the GPU */ }
         else if (f == "--device") a.device = std::stoi(next());
+        else if (f == "--half-unscaled") a.half_unscaled = 1;
         else if (f == "--mode") {
             const std::string v = next();
             if (v == "mixed") a.mode = MPG_MODE_MIXED;

@@ -147,9 +147,21 @@ public:
             flush_scalar_ops();
             flush_pending_reduction();
         } catch (const StatusError&) {
+            // a step that cannot be recorded: end the recording and run eagerly
             discard_scalar_ops();
             discard_pending_reduction();
             ok = false;
+        } catch (...) {
+            // anything else: leave the context out of capture mode (a later
+            // call on the stream would otherwise be recorded, not run), drop
+            // the partial graph and the queued work, then rethrow
+            discard_scalar_ops();
+            discard_pending_reduction();
+            mpg_graph_t partial = nullptr;
+            (void)mpg_ctx_record_end(ctx_, &partial);
+            if (partial) mpg_graph_destroy(partial);
+            eager_ = true;
+            throw;
         }
         mpg_graph_t g = nullptr;
         const int st = mpg_ctx_record_end(ctx_, &g);

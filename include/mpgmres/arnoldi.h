@@ -63,6 +63,8 @@ typedef struct {
     void* x;               /* outer_type, row 0 of [-MPG_FRONT_PAD(n_front), n_ext) (halo filled by the caller) */
     int32_t spmv_format;   /* Arnoldi SpMV storage: 0 auto, 1 CSR row blocks, 2 sliced ELL (SELL-64) */
     int32_t n_front;       /* halo rows of lower ranks, local ids [-n_front, 0) (0 on one GPU) */
+    const int8_t* inner_row_exp; /* inner_val MPG_F16: per-row exponents of the scaled fp16 copy
+                                    (mpg_csr_half_values, capi.h), or NULL (unscaled) */
 } mpg_arnoldi_desc;
 
 /* Entries allocated in front of row 0 of every vector with a halo (x, the
@@ -90,6 +92,10 @@ int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width
  * patterns), int64 slice offsets, the per-slice pattern indices and the
  * stepped form's (slice, step, element) bases */
 int64_t mpg_arnoldi_sell_matrix_bytes(mpg_arnoldi_t a);
+/* column form of the SELL copy as mpg_sell_columns (capi.h): -1 no copy,
+ * 0 int32, 1 int16 slice-relative, 2 stepped int16; CSR-summed and implicit
+ * slice counts. Any output may be NULL. */
+int mpg_arnoldi_sell_columns(mpg_arnoldi_t a, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices);
 
 int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
 int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);

@@ -38,7 +38,8 @@ typedef enum {
     MPG_ERR_ALLOC = -3,        /* device allocation failed */
     MPG_ERR_RCCL = -4,         /* an RCCL call failed */
     MPG_ERR_UNSUPPORTED = -5,  /* operation not supported for these arguments */
-    MPG_ERR_BREAKDOWN = -6     /* Arnoldi breakdown / non-finite value detected */
+    MPG_ERR_BREAKDOWN = -6,    /* Arnoldi breakdown / non-finite value detected */
+    MPG_ERR_RANGE = -7         /* a value does not fit the storage precision (fp16 values) */
 } mpg_status_t;
 
 typedef struct mpg_ctx* mpg_ctx_t;   /* one per (GPU, host thread) */
@@ -258,13 +259,36 @@ int mpg_csr_spmv_f32(mpg_ctx_t ctx, mpg_csr_t A, float alpha, const float* vals,
 int mpg_csr_spmv_f16f32(mpg_ctx_t ctx, mpg_csr_t A, float alpha, const uint16_t* vals_half,
                         const float* x, float beta, float* y);
 
+/* ---- fp16 values for the mixed-half Arnoldi SpMV (BASELINE config 5; the
+ * reference has no fp16 path). IEEE fp16 holds
+ * magnitudes in [6.0e-8, 65504] only, so the copy is scaled per row by a
+ * power of two: out[j] = half(float(vals[j] * 2^e_i)) for the entries j of
+ * row i, with e_i = 0 when the row's largest finite |a_ij| lies in
+ * [2^-2, 2^15) and otherwise e_i = 14 - floor(log2 max |a_ij|) (the row's
+ * largest entry then lands in [2^14, 2^15)). A SpMV over the copy forms
+ * the row sum in fp64 and multiplies it by 2^-e_i (exact) before rounding,
+ * so rows with e_i = 0 keep the bits of the unscaled copy, and scaled rows
+ * lose nothing to range (power-of-two scaling commutes with rounding in
+ * the normal range). row_exp: int8 per row (may be NULL with scale == 0).
+ * scale == 0: no scaling (e_i = 0). stats (host int64[4], may be NULL):
+ * [0] rows with e_i != 0, [1] nonzero finite entries that round to 0,
+ * [2] finite entries that round to +-Inf, [3] rows whose e_i does not fit
+ * int8. Returns MPG_ERR_RANGE when [2] or [3] is nonzero, or when scale == 0
+ * and [1] is nonzero (the copy is still written); synchronises. */
+int mpg_csr_half_values(mpg_ctx_t ctx, mpg_csr_t A, const double* vals, int32_t scale, uint16_t* out_half,
+                        int8_t* row_exp, int64_t* stats);
+/* y = alpha * (2^-e_i * sum_j half(a_ij) x_j) + beta * y over that copy */
+int mpg_csr_spmv_f16f32_scaled(mpg_ctx_t ctx, mpg_csr_t A, float alpha, const uint16_t* vals_half,
+                               const int8_t* row_exp, const float* x, float beta, float* y);
+
 /* ---- SELL-64 SpMV: the same y = alpha*A x + beta*y (kernels_mkl.cpp:326-352)
  * on a sliced-ELL copy (64-row slices padded to their longest row, int16
  * slice-relative columns when they fit). mpg_sell_create copies one value
  * array (vtype MPG_F64 | MPG_F32 | MPG_F16 raw half bits) of an analysed
  * CSR; format 0 = only when padding adds <= 20 % to the stored entries
- * (*out = NULL otherwise: keep mpg_csr_spmv), 2 = always. The copy owns its
- * device memory and does not borrow vals afterwards; it synchronises. The
+ * (*out = NULL otherwise: keep mpg_csr_spmv), 2 = always. The copy owns all
+ * the device memory it reads (a stepped copy's CSR-summed slices included):
+ * A and vals may be destroyed or freed once it returns; it synchronises. The
  * spmv entry must match the copy's vtype (f64 / f32 / f16f32). */
 int mpg_sell_create(mpg_ctx_t ctx, mpg_csr_t A, int32_t vtype, const void* vals, int32_t format,
                     mpg_sell_t* out);

@@ -96,6 +96,24 @@ int mpg_engine_create_dist_host(const mpg_solve_args* args, mpg_halo_t plan, con
  * (history, counts, norms, x gathered) matches mpg_solve's. */
 int mpg_solve_loopback(const mpg_solve_args* args, int32_t nranks, mpg_solve_result* result);
 
+/* What one rank's engine runs on (mpg_solve_loopback_ex): the Arnoldi SpMV
+ * storage (mpg_arnoldi_spmv_layout / mpg_arnoldi_sell_columns), the local
+ * numbering (dist.h above) and the fp16 cast's scaled rows. */
+typedef struct {
+    int32_t format;           /* 1 CSR row blocks, 2 SELL-64 */
+    int32_t col_form;         /* SELL columns: -1 none, 0 int32, 1 int16, 2 stepped int16 */
+    int32_t vec_width;
+    int32_t window;           /* 1: the SpMV reads v_k from the LDS window */
+    int32_t n_local, n_front, n_ext;
+    int32_t pad_;
+    int64_t row0;             /* first global row */
+    int64_t csr_slices, implicit_slices;
+    int64_t half_rows_scaled; /* mixed-half: rows scaled by a power of two */
+} mpg_rank_layout;
+/* mpg_solve_loopback, reporting each rank's layout (layouts: nranks entries, may be NULL) */
+int mpg_solve_loopback_ex(const mpg_solve_args* args, int32_t nranks, mpg_solve_result* result,
+                          mpg_rank_layout* layouts);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,9 @@ typedef struct {
     int32_t device;        /* HIP device (mpg_solve only) */
     int32_t threads;       /* host threads (oracle only; 0 = default) */
     int32_t spmv_format;   /* fused engine Arnoldi SpMV: 0 auto, 1 CSR row blocks, 2 SELL-64 */
+    int32_t half_unscaled; /* mode mixed-half: 0 = fp16 values scaled per row by powers of two where
+                              a row's magnitude needs it (mpg_csr_half_values, capi.h); 1 = plain
+                              cast: a value outside fp16's range fails the set-up (MPG_ERR_RANGE) */
 } mpg_solve_args;
 
 typedef struct {
@@ -123,6 +126,10 @@ double mpg_engine_phase_bytes(mpg_engine_t e, int which);
 /* storage of the engine's Arnoldi SpMV (mpg_arnoldi_spmv_layout) */
 int mpg_engine_spmv_layout(mpg_engine_t e, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
                            int64_t* stored, int32_t* window);
+/* column form of the engine's SELL copy (mpg_arnoldi_sell_columns) */
+int mpg_engine_sell_columns(mpg_engine_t e, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices);
+/* mode mixed-half: stats[4] of the fp16 cast (mpg_csr_half_values); zeros otherwise */
+int mpg_engine_half_stats(mpg_engine_t e, int64_t* stats);
 int mpg_engine_destroy(mpg_engine_t e);
 
 /* process-wide counts of the operator-surface driver's cycle programs

@@ -3,10 +3,12 @@ engine over the host transport (mpg_engine_create_dist_host + transport.py),
 launched by tests/test_dist_gpu.py as
 
   python -m torch.distributed.run --nproc-per-node P --master-addr 127.0.0.1 \
-      --master-port PORT tests/dist_host_worker.py OUT.npz N MODE ORTH PREC MAX_RESTARTS TOL
+      --master-port PORT tests/dist_host_worker.py OUT.npz MATRIX MODE ORTH PREC MAX_RESTARTS TOL
 
+MATRIX: N (BAND-N, gen_band(N, 5, 4, seed=7)) or stencil27:NX:NY:NZ (3 dof).
 Every rank uses device 0 (the ranks share the GPU; RCCL would refuse).
-Rank 0 writes the gathered solution and its history to OUT.npz.
+Rank 0 writes the gathered solution, its history and every rank's SpMV
+layout (column form, CSR-summed slices, front halo) to OUT.npz.
 """
 import os
 import sys
@@ -19,8 +21,15 @@ REPO = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(REPO))
 
 
+def matrix(mpg, spec: str):
+    if spec.startswith("stencil27:"):
+        nx, ny, nz = (int(v) for v in spec.split(":")[1:4])
+        return mpg.gen_stencil27(nx, 3, ny=ny, nz=nz)
+    return mpg.gen_band(int(spec), 5, 4, seed=7)
+
+
 def main():
-    out, n, mode, orth, prec, max_restarts, tol = sys.argv[1:8]
+    out, spec, mode, orth, prec, max_restarts, tol = sys.argv[1:8]
     from __graft_entry__ import _load
 
     mpg = _load()
@@ -28,7 +37,7 @@ def main():
 
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    A = mpg.gen_band(int(n), 5, 4, seed=7)
+    A = matrix(mpg, spec)
     xt = mpg.rand_vect(A.nrows, 42)
     b = mpg.host_spmv(A, xt)
     starts = mpg.nnz_balanced_starts(A, world)
@@ -44,6 +53,11 @@ def main():
     transport = HostTransport()
     opts = dict(mode=mode, orth=orth, prec=prec, rlen=30, tol=float(tol), max_restarts=int(max_restarts), device=0)
     eng = mpg.Engine.distributed_host(A_loc, b[r0:r1], xt[r0:r1], plan, transport, world, rank, **opts)
+    cols = eng.sell_columns()
+    mine = [{"csr": 0, "sell": 1}[eng.spmv_layout()["format"]],
+            {"none": -1, "int32": 0, "int16": 1, "stepped": 2}[cols["form"]], cols["csr_slices"], plan.n_front]
+    lays = [None] * world
+    dist.all_gather_object(lays, mine)
     done = False
     while not done:
         _, done = eng.run(1 << 20)
@@ -56,7 +70,7 @@ def main():
                  cyc_normalization=res.cyc_normalization, cyc_beta=res.cyc_beta,
                  counts=np.array([res.restarts, res.inner_k, res.total_iters]),
                  norms=np.array([res.res_norm, res.err_norm, res.minvb_norm]), status=np.array(res.status),
-                 starts=starts, transport_error=np.array(transport.error or ""))
+                 starts=starts, transport_error=np.array(transport.error or ""), layouts=np.array(lays))
     dist.destroy_process_group()
 
 

@@ -46,3 +46,29 @@ def test_cli_default_preconditioner_is_ilu(mpg):
     m = SUMMARY.search(out)
     assert m, out
     assert float(m.group(1)) <= 1e-9
+
+
+def test_cli_bpath_right_hand_side(mpg, tmp_path):
+    """--bpath: b from a Matrix Market file, x_true = 0 (gmres_perf_test.cpp
+    :412-421), so ||x|| prints 0 and errNorm is the solution's norm; the CLI
+    solve equals the library solve with that b."""
+    import numpy as np
+
+    A = mpg.gen_spec("laplace:10")
+    xt = mpg.rand_vect(A.nrows, 5)
+    b = mpg.host_spmv(A, xt)
+    p = tmp_path / "b.mtx"
+    p.write_text("%%MatrixMarket matrix array real general\n" + f"{A.nrows} 1\n" +
+                 "".join(f"{v:.17g}\n" for v in b))
+    assert np.array_equal(mpg.load_mtx_vector(str(p), A.nrows), b)
+    out = subprocess.run([str(mpg.CLI), "--matrix", "laplace:10", "--bpath", str(p), "--rlen", "30", "--mode", "mixed",
+                          "--orth", "cgs", "--prec", "jacobi", "--tol", "1e-9", "--gpu"],
+                         capture_output=True, text=True, timeout=120, check=True).stdout
+    assert out.startswith("||x|| = 0\n"), out[:80]
+    assert f"||b|| = {np.linalg.norm(b):.6g}" in out
+    m = SUMMARY.search(out)
+    assert m, out
+    got = mpg.solve(A, b, np.zeros(A.nrows), engine="fused", mode="mixed", orth="cgs", prec="jacobi", rlen=30,
+                    tol=1e-9)
+    assert int(m.group(3)) == got.restarts and int(m.group(4)) == got.total_iters
+    assert abs(float(m.group(9)) - np.linalg.norm(got.x)) <= 1e-5 * np.linalg.norm(got.x)

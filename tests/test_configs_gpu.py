@@ -6,8 +6,12 @@ does not (SURVEY §8(a) config shorthand):
   C1  bcsstk17 stand-in through the MM loader    tests/test_c1_standin.py
   C2  LAP-1M (100^3 7-point), fp64 GMRES(30)     live oracle, CGS and MGS
   C3  LAP-1M, fp32 inner + fp64 outer            live oracle, CGS / CGSR / MGS
-  C4  Queen_4147 stand-in (27-point, 3 dof)      live oracle at 40^3 x 3,
-                                                 properties at 111^3 x 3
+  C4  Queen_4147 stand-in (27-point, 3 dof)      live oracle at 40^3 x 3 and
+                                                 at 105 x 105 x 8 x 3 (the
+                                                 stepped-int16 W = 4 SELL form
+                                                 full-size C4 runs on), its
+                                                 full-size SpMV against CSR and
+                                                 MKL, properties at 111^3 x 3
   C5  BAND-100M fp16 values + fp64 IR            full size, converges to tol
 
 Reference SpMV / drivers: kernels_mkl.cpp:326-352, gmres.cpp:24-245,
@@ -69,6 +73,80 @@ def test_c4_stencil27_live_oracle(mpg, oracle, mode, orth):
     for engine in ("fused", "surface"):
         got = mpg.solve(A, b, xt, engine=engine, **opts)
         compare(as_ref(ref), got, mode, opts["tol"], 30, f"stencil27-40-{mode}-{orth}-{engine}")
+
+
+@pytest.fixture(scope="module")
+def c4_stepped(mpg):
+    """105 x 105 x 8 nodes x 3 dof = 264,600 rows, 19,397,862 nnz: a plane
+    spans 3 * 105^2 = 33,075 rows, beyond the int16 slice-relative form, so
+    the SELL copy takes the stepped int16 form at W = 4 as full-size C4 does
+    (profiles/r02g_configs.jsonl), including slices summed from the copy's
+    sub-CSR (those straddling the first and last boundary planes)."""
+    A = mpg.gen_stencil27(105, 3, ny=105, nz=8)
+    assert A.nrows == 264_600 and A.nnz == 19_397_862
+    return _problem(mpg, A)
+
+
+@pytest.mark.parametrize("mode,orth", [("mixed", "cgs"), ("mixed", "mgs"), ("baseline", "cgs"), ("mixed", "cgsr")])
+def test_c4_stepped_layout_live_oracle(mpg, oracle, c4_stepped, mode, orth):
+    """C4's full-size SpMV layout (stepped int16 columns, W = 4, CSR-summed
+    boundary slices) in whole solves against the live oracle, on the fused
+    engine and on the operator surface (whose SELL copy is built by the same
+    builder), asserting the layout the engine really ran."""
+    A, xt, b = c4_stepped
+    opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=1e-10, max_restarts=100)
+    eng = mpg.Engine(A, b, xt, **opts)
+    lay, cols = eng.spmv_layout(), eng.sell_columns()
+    eng.close()
+    assert lay["format"] == "sell" and lay["vec_width"] == 4 and lay["col_bytes"] == 2 and not lay["window"], lay
+    assert cols["form"] == "stepped" and 1 <= cols["csr_slices"] <= A.nrows // 64 // 100, cols
+    ref = oracle.solve(mpg, A, b, xt, **opts)
+    assert ref.status == "converged"
+    for engine in ("fused", "surface"):
+        got = mpg.solve(A, b, xt, engine=engine, **opts)
+        compare(as_ref(ref), got, mode, opts["tol"], 30, f"c4-stepped-{mode}-{orth}-{engine}")
+
+
+def test_c4_full_size_spmv_sell_vs_csr_vs_mkl(hip, mpg, oracle):
+    """One fp32 SpMV of full-size C4 (stencil27(111, 3): 4,102,893 rows,
+    326,382,219 nnz) through the SELL copy (stepped int16, W = 4) against the
+    CSR SpMV (the same fp64 row sums in CSR order: identical bits) and the
+    oracle's mkl_sparse_s_mv (kernels_mkl.cpp:326-352; fp32 accumulation, so
+    within 2 * row_nnz * eps32 * (|A| |x|)_i)."""
+    import ctypes as C
+
+    A = mpg.gen_stencil27(111, 3)
+    n = A.nrows
+    assert n == 4_102_893 and A.nnz == 326_382_219
+    x = mpg.rand_vect(n, 7).astype(np.float32)
+    v32 = A.val.astype(np.float32)
+    drp, dci, dv, dx = hip.buf(A.rowptr), hip.buf(A.col), hip.buf(v32), hip.buf(x)
+    dy_sell, dy_csr = hip.buf(n, np.float32), hip.buf(n, np.float32)
+    csr, sell = C.c_void_p(), C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, n, n, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    try:
+        hip.check(hip.lib.mpg_sell_create(hip.ctx, csr, 1, dv.p, 0, C.byref(sell)))
+        assert sell.value
+        form, exc, imp = C.c_int32(), C.c_int64(), C.c_int64()
+        hip.check(hip.lib.mpg_sell_columns(sell, C.byref(form), C.byref(exc), C.byref(imp)))
+        w, cb, stored, win = C.c_int32(), C.c_int32(), C.c_int64(), C.c_int32()
+        hip.check(hip.lib.mpg_sell_layout(sell, C.byref(w), C.byref(cb), C.byref(stored), C.byref(win)))
+        assert form.value == 2 and w.value == 4 and cb.value == 2 and exc.value >= 1, (form.value, w.value, exc.value)
+        hip.call("mpg_sell_spmv_f32", sell, C.c_float(1.0), dx.p, C.c_float(0.0), dy_sell.p)
+        hip.call("mpg_csr_spmv_f32", csr, C.c_float(1.0), dv.p, dx.p, C.c_float(0.0), dy_csr.p)
+        y_sell, y_csr = dy_sell.get(), dy_csr.get()
+        assert np.array_equal(y_sell, y_csr)
+        y_mkl = oracle.spmv(A, x, dtype=np.float32)
+        scale = oracle.spmv(mpg.Csr(n, n, A.rowptr, A.col, np.abs(v32).astype(np.float64)),
+                            np.abs(x).astype(np.float64))
+        row_nnz = np.diff(A.rowptr)
+        eps32 = np.finfo(np.float32).eps
+        bad = np.abs(y_sell.astype(np.float64) - y_mkl.astype(np.float64)) > 2 * row_nnz * eps32 * scale
+        assert not bad.any(), np.flatnonzero(bad)[:10]
+    finally:
+        if sell.value:
+            hip.lib.mpg_sell_destroy(sell)
+        hip.lib.mpg_csr_destroy(csr)
 
 
 def _restart_properties(got, rlen, floor_rel):

@@ -2,7 +2,14 @@
 loopback communicator (device-to-device halo copies, rank-ordered fp64
 all-reduce) must reproduce the single-GPU solve and the golden records
 within the stated parity tolerances (tests/parity.py). The RCCL transport
-differs only in how the same bytes move (exercised by bench.py at N > 1)."""
+differs only in how the same bytes move (exercised by bench.py at N > 1).
+
+The 8-GPU configs (BASELINE C4, C5) are rehearsed at P = 8: the C4
+stand-in's structure in the stepped-int16 layout against the oracle, BAND
+with fp16 values against the oracle's fp32-value solve, and a BAND split at
+1.25M rows per rank (C5's per-GPU share) through size-independent
+properties. Each asserts per rank the SpMV layout and the front-halo
+numbering it actually ran (mpg_solve_loopback_ex)."""
 import json
 import os
 from pathlib import Path
@@ -134,3 +141,112 @@ def test_loopback_matches_single_gpu_band(mpg, nranks):
     assert np.allclose(many.step_res[:30], one.step_res[:30], rtol=1e-3, atol=1e-6 * one.minvb_norm)
     assert np.allclose(many.x, one.x, rtol=1e-3, atol=1e-5)
     assert abs(many.res_norm - one.res_norm) <= 1e-2 * one.res_norm
+
+
+def _assert_rank_layouts(lays, nranks, forms):
+    assert len(lays) == nranks
+    for q, L in enumerate(lays):
+        assert L["format"] == "sell" and L["col_form"] in forms, (q, L)
+        # the lower halo numbered in front of row 0 (dist.h): rank 0 has none
+        assert (L["n_front"] == 0) == (q == 0), (q, L)
+        assert L["n_ext"] > L["n_local"] or q == nranks - 1, (q, L)
+    assert [L["row0"] for L in lays] == sorted(L["row0"] for L in lays)
+
+
+@pytest.mark.parametrize("mode,orth", [("mixed", "cgs"), ("baseline", "mgs")])
+def test_p8_stencil27_stepped_live_oracle(mpg, oracle, mode, orth):
+    """BASELINE C4's structure (27-point, 3 dof, planes of 33,075 rows) split
+    over P = 8 ranks: each rank's SELL copy keeps the stepped int16 columns,
+    against the oracle at the parity tolerances (Orthogonalization.hpp:82-88
+    is where the dots become all-reduces)."""
+    A = mpg.gen_stencil27(105, 3, ny=105, nz=8)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=1e-10, max_restarts=100)
+    lays = []
+    got = mpg.solve_loopback(A, b, xt, nranks=8, layouts=lays, **opts)
+    _assert_rank_layouts(lays, 8, ("stepped",))
+    ref = oracle.solve(mpg, A, b, xt, **opts)
+    assert ref.status == "converged"
+    compare(as_ref(ref), got, mode, opts["tol"], 30, f"p8-stencil27-{mode}-{orth}")
+
+
+def test_p8_band_half_values_vs_oracle(mpg, oracle):
+    """BASELINE C5's cast path (fp16 Arnoldi values, fp32 vectors, fp64 outer
+    refinement) row-partitioned over P = 8: converges to tol like the oracle's
+    fp32-value mixed solve (the reference has no fp16 mode), within one
+    restart of it, with the forward error the fp64 refinement reaches."""
+    n = 400_000
+    A = mpg.gen_band(n, 5, 4, seed=7)
+    xt = mpg.rand_vect(n, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(orth="cgs", prec="identity", rlen=30, tol=1e-10, max_restarts=60)
+    lays = []
+    half = mpg.solve_loopback(A, b, xt, nranks=8, layouts=lays, mode="mixed-half", **opts)
+    _assert_rank_layouts(lays, 8, ("int16",))
+    assert all(L["window"] and L["implicit_slices"] > 0 and L["half_rows_scaled"] == 0 for L in lays), lays
+    ref = oracle.solve(mpg, A, b, xt, mode="mixed", **opts)
+    assert ref.status == half.status == "converged"
+    assert half.backward_error[-1] <= opts["tol"]
+    assert abs(half.restarts - ref.restarts) <= 1, (half.restarts, ref.restarts)
+    assert half.err_norm <= 1e-6 * np.linalg.norm(xt)
+    one = mpg.solve(A, b, xt, engine="fused", mode="mixed-half", **opts)
+    assert one.status == "converged" and abs(one.restarts - half.restarts) <= 1
+
+
+def test_p8_band_c5_share_properties(mpg):
+    """P = 8 ranks of 1.25M rows each (BAND-100M split as on 8 GPUs; every
+    rank holds C5's per-GPU share): mixed CGS GMRES(30), 3 cycles at tol = 0.
+    Cycle 0 matches the single-GPU solve to fp32 rounding, the restart
+    properties hold, and the returned x's true residual recomputed on the
+    host is the reported resNorm."""
+    from tests.test_configs_gpu import _restart_properties
+
+    n = 10_000_000
+    A = mpg.gen_band(n, 5, 4, seed=7)
+    assert A.nnz == 99_999_975
+    xt = mpg.rand_vect(n, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3)
+    lays = []
+    many = mpg.solve_loopback(A, b, xt, nranks=8, layouts=lays, **opts)
+    _assert_rank_layouts(lays, 8, ("int16",))
+    assert all(abs(L["n_local"] - n // 8) <= 64 for L in lays), [L["n_local"] for L in lays]
+    assert many.status == "aborted" and many.total_iters == 90
+    one = mpg.solve(A, b, xt, engine="fused", **opts)
+    assert np.allclose(many.step_res[:30], one.step_res[:30], rtol=1e-3, atol=1e-6 * one.minvb_norm)
+    _restart_properties(many, 30, 1e-5)
+    r = b - mpg.host_spmv(A, many.x)
+    assert abs(np.linalg.norm(r) - many.res_norm) <= 1e-6 * np.linalg.norm(b)
+
+
+def test_host_transport_processes_stencil27(mpg, oracle, tmp_path):
+    """The C4 structure as 2 separate processes over the host transport: the
+    same bits as the 2-rank loopback solve, every rank on the stepped int16
+    layout with its lower halo numbered in front, and the oracle's result at
+    the parity tolerances."""
+    import subprocess
+    import sys
+
+    spec, mode, orth, prec, max_restarts, tol = "stencil27:105:105:8", "mixed", "cgs", "jacobi", 100, 1e-10
+    out = tmp_path / "rank0.npz"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).parent / "dist_host_worker.py"),
+           str(out), spec, mode, orth, prec, str(max_restarts), str(tol)]
+    run = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert run.returncode == 0, run.stdout[-3000:] + run.stderr[-3000:]
+    got = np.load(out)
+    assert str(got["transport_error"]) == ""
+    lay = got["layouts"]  # per rank: [format (1 sell), column form (2 stepped), CSR-summed slices, n_front]
+    assert list(lay[:, 0]) == [1, 1] and list(lay[:, 1]) == [2, 2], lay
+    assert lay[0, 3] == 0 and lay[1, 3] > 0, lay
+    A = mpg.gen_stencil27(105, 3, ny=105, nz=8)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode=mode, orth=orth, prec=prec, rlen=30, tol=tol, max_restarts=max_restarts)
+    loop = mpg.solve_loopback(A, b, xt, nranks=2, **opts)
+    assert list(got["counts"]) == [loop.restarts, loop.inner_k, loop.total_iters]
+    assert np.array_equal(got["step_res"], loop.step_res) and np.array_equal(got["x"], loop.x)
+    ref = oracle.solve(mpg, A, b, xt, **opts)
+    compare(as_ref(ref), loop, mode, tol, 30, "host-transport-stencil27")

@@ -146,3 +146,38 @@ def test_oracle_ilu_solve_vs_numpy_restatement(mpg, oracle, mode, prec):
     # the preconditioner does its job: fewer restarts than without it
     r0 = oracle.solve(mpg, A, b, xt, mode=mode, orth="cgs", prec="identity", rlen=12, tol=1e-10, max_restarts=300)
     assert r.restarts < r0.restarts
+
+
+@pytest.mark.parametrize("mode", ["baseline", "mixed"])
+def test_parity_rejects_a_wrong_x(mpg, oracle, mode):
+    """tests/parity.py's x checks bound the difference by the reference's own
+    errNorm, not by the run under test's: a solution moved by e_ref (plus the
+    rounding allowance) in one entry passes the history and norm checks but
+    fails the x check (the old bound, e_ref + e_got, could never fail: a
+    moved x's own errNorm grows with the move); the run unmoved passes."""
+    A = convdiff(mpg, 16)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    r = oracle.solve(mpg, A, b, xt, mode=mode, orth="cgs", prec="jacobi", rlen=12, tol=1e-10, max_restarts=300)
+    ref = as_ref(r)
+    compare(ref, r, mode, 1e-10, 12, "unmoved")
+    e_ref = float(r.err_norm)
+    assert e_ref > 0
+    # past the rounding allowance too (1e-12 / 1e-9 relative to max |x|)
+    rt = 1e-12 if mode == "baseline" else 1e-9
+    scale = float(np.max(np.abs(r.x[:16])))
+    delta = e_ref + 2 * rt * scale
+    delta_sum = e_ref + 2 * rt * max(abs(float(np.sum(r.x))), scale) / np.sqrt(A.nrows)
+    for where in (0, 16):  # one entry of the checked head; every entry past it, evenly (only the sum sees it)
+        bad = type("R", (), {})()
+        for k in ("status", "restarts", "total_iters", "step_res", "step_cycle", "cyc_r_norm", "cyc_normalization",
+                  "res_norm"):
+            setattr(bad, k, getattr(r, k))
+        bad.x = np.array(r.x)
+        if where == 0:
+            bad.x[0] += delta
+        else:  # sum moved by sqrt(n) delta_sum, ||move||_2 ~ delta_sum
+            bad.x[16:] += np.sqrt(A.nrows) * delta_sum / (A.nrows - 16)
+        bad.err_norm = float(np.linalg.norm(bad.x - xt))
+        with pytest.raises(AssertionError, match="x head|x sum"):
+            compare(ref, bad, mode, 1e-10, 12, f"moved at {where}")

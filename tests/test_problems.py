@@ -91,3 +91,25 @@ def test_stencil27_counts_symmetry_dominance(mpg):
         assert np.all(np.diff(c) > 0)
     # Queen_4147 scale: 111^3 x 3 = 4,102,893 rows
     assert 111**3 * 3 == 4_102_893
+
+
+def test_mtx_vector_loader_reference_semantics(mpg, tmp_path):
+    """--bpath's LoadVector (LoadMatrix.hpp:156-233): an array file is read
+    column-major (column `col` after skipping col * M values); a coordinate
+    file fills the picked column's entries into zeros; a column past N and a
+    missing file are errors."""
+    p = tmp_path / "b.mtx"
+    p.write_text("%%MatrixMarket matrix array real general\n% two right-hand sides\n3 2\n1.5\n-2\n3e-1\n"
+                 "10\n20\n30\n")
+    assert np.array_equal(mpg.load_mtx_vector(str(p), 3), [1.5, -2.0, 0.3])
+    assert np.array_equal(mpg.load_mtx_vector(str(p), 3, col=1), [10.0, 20.0, 30.0])
+    with pytest.raises(ValueError, match="Column 2 is too large for the 2 vectors"):
+        mpg.load_mtx_vector(str(p), 3, col=2)
+    q = tmp_path / "c.mtx"
+    q.write_text("%%MatrixMarket matrix coordinate real general\n4 2 3\n2 1 7.25\n4 2 1.0\n4 1 -1\n")
+    assert np.array_equal(mpg.load_mtx_vector(str(q), 4), [0.0, 7.25, 0.0, -1.0])
+    assert np.array_equal(mpg.load_mtx_vector(str(q), 4, col=1), [0.0, 0.0, 0.0, 1.0])
+    with pytest.raises(ValueError, match="Could not access file"):
+        mpg.load_mtx_vector(str(tmp_path / "missing.mtx"), 4)
+    with pytest.raises(ValueError, match="does not match"):
+        mpg.load_mtx_vector(str(q), 5)

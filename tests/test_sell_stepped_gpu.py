@@ -202,3 +202,60 @@ def test_implicit_slices_solve(mpg, mode, orth, monkeypatch):
     assert got["1"].total_iters == got["0"].total_iters == 90
     assert np.array_equal(got["1"].step_res, got["0"].step_res) and np.array_equal(got["1"].x, got["0"].x)
     assert got["1"].res_norm == got["0"].res_norm
+
+
+def test_sell_copy_owns_its_flagged_rows(hip, mpg):
+    """mpg_sell_create's copy owns every byte it reads (capi.h): the flagged
+    slices of a stepped copy are summed from the copy's own sub-CSR, so the
+    caller may overwrite and free the CSR arrays, the CSR handle and the value
+    array once the copy exists (the copy used to borrow them)."""
+    A = _far(mpg)
+    n = A.nrows
+    g = np.random.default_rng(9)
+    x = g.uniform(-1, 1, n)
+    drp, dci = hip.buf(A.rowptr), hip.buf(A.col)
+    csr = C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, n, n, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    cases = [("f64", 0, A.val, np.float64), ("f32", 1, A.val.astype(np.float32), np.float32),
+             ("f16f32", 2, A.val.astype(np.float16).view(np.uint16), np.float32)]
+    sells, want, dvs = [], [], []
+    try:
+        for name, vt, vals, xdt in cases:
+            dv = hip.buf(vals)
+            dvs.append(dv)
+            sell = C.c_void_p()
+            hip.check(hip.lib.mpg_sell_create(hip.ctx, csr, vt, dv.p, 0, C.byref(sell)))
+            sells.append(sell)
+            form, exc, imp = C.c_int32(), C.c_int64(), C.c_int64()
+            hip.check(hip.lib.mpg_sell_columns(sell, C.byref(form), C.byref(exc), C.byref(imp)))
+            assert form.value == 2 and exc.value == 1
+            dx, dy = hip.buf(x.astype(xdt)), hip.buf(n, xdt)
+            hip.call(f"mpg_csr_spmv_{name}", csr, xdt(1.0), dv.p, dx.p, xdt(0.0), dy.p)
+            want.append(dy.get())
+        # poison, then free, everything the copies were built from
+        hip.check(hip.lib.mpg_memcpy_h2d(hip.ctx, dci.p, np.full(A.nnz, 7, np.int32).ctypes.data, A.nnz * 4), "h2d")
+        hip.check(hip.lib.mpg_memcpy_h2d(hip.ctx, drp.p, np.zeros(n + 1, np.int32).ctypes.data, (n + 1) * 4), "h2d")
+        for dv in dvs:
+            junk = np.full(dv.nbytes, 0xFF, np.uint8)  # NaN in every precision
+            hip.check(hip.lib.mpg_memcpy_h2d(hip.ctx, dv.p, junk.ctypes.data, dv.nbytes), "h2d")
+        hip.sync()
+        hip.lib.mpg_csr_destroy(csr)
+        csr = None
+        for dv in dvs:
+            dv.free()
+        dci.free()
+        drp.free()
+        for (name, _, _, xdt), sell, y in zip(cases, sells, want):
+            dx, dy = hip.buf(x.astype(xdt)), hip.buf(n, xdt)
+            hip.call(f"mpg_sell_spmv_{name}", sell, xdt(1.0), dx.p, xdt(0.0), dy.p)
+            got = dy.get()
+            if name == "f64":
+                scale = abs(A.to_scipy()) @ np.abs(x)
+                assert np.all(np.abs(got - y) <= 4 * F64_EPS * scale), name
+            else:
+                assert np.array_equal(got, y), name
+    finally:
+        for h in sells:
+            hip.lib.mpg_sell_destroy(h)
+        if csr is not None:
+            hip.lib.mpg_csr_destroy(csr)

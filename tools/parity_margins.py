@@ -42,6 +42,11 @@ def main():
                 be_final=(float(be_g[-1]), float(be_r[-1])),
                 xhead_rel=float(np.max(np.abs(g.x[:16] - xh)) / np.max(np.abs(xh))),
                 xsum_rel=float(abs(g.x.sum() - rec["x_sum"]) / abs(rec["x_sum"])),
+                # the x differences against the reference's own errNorm
+                # (tests/parity.py bounds them by e_ref alone)
+                xhead_eref=float(np.max(np.abs(g.x[:16] - xh)) / rec["err_norm"]) if rec["err_norm"] else None,
+                xsum_eref=float(abs(g.x.sum() - rec["x_sum"]) / (np.sqrt(len(g.x)) * rec["err_norm"]))
+                if rec["err_norm"] else None,
                 res=(g.res_norm, rec["res_norm"]), err=(g.err_norm, rec["err_norm"]))), flush=True)
 
 
@@ -63,7 +68,8 @@ def summary(path):
         floor = 1e-6 if mode == "single" else 1e-14
         above = be[:len(rel)] > floor
         d = per.setdefault(mode, dict(runs=0, same_restarts=0, same_status=0, be_rel_above_floor=0.0,
-                                      xhead_rel=0.0, xsum_rel=0.0, res_factor=1.0, err_factor=1.0))
+                                      xhead_rel=0.0, xsum_rel=0.0, xhead_eref=0.0, xsum_eref=0.0,
+                                      res_factor=1.0, err_factor=1.0))
         d["runs"] += 1
         d["same_restarts"] += r["restarts"][0] == r["restarts"][1]
         d["same_status"] += r["status"][0] == r["status"][1]
@@ -71,6 +77,9 @@ def summary(path):
             d["be_rel_above_floor"] = max(d["be_rel_above_floor"], float(rel[above].max()))
         d["xhead_rel"] = max(d["xhead_rel"], r["xhead_rel"])
         d["xsum_rel"] = max(d["xsum_rel"], r["xsum_rel"])
+        if r.get("xhead_eref") is not None and r["restarts"][0] == r["restarts"][1]:
+            d["xhead_eref"] = max(d["xhead_eref"], r["xhead_eref"])
+            d["xsum_eref"] = max(d["xsum_eref"], r["xsum_eref"])
         for k, key in (("res", "res_factor"), ("err", "err_factor")):
             a, b = r[k]
             if a > 0 and b > 0:
