@@ -128,7 +128,13 @@ __global__ __launch_bounds__(kBlock) void k_half_rows(int32_t rows, const int32_
         if (rexp) rexp[i] = (int8_t)e;
         for (int j = j0; j < j1; ++j) {
             const double a = val[j];
-            const uint16_t h = __half_as_ushort(__float2half_rn((float)ldexp(a, e)));
+            // fp64 -> fp32 -> fp16, two roundings as mpg_copy_f64f16 (and
+            // numpy's astype chain); the empty asm keeps the compiler from
+            // folding the pair into one fp64 -> fp16 rounding, which it did
+            // here (66 of BAND-100k's 1M entries differed)
+            float f = (float)ldexp(a, e);
+            asm volatile("" : "+v"(f));
+            const uint16_t h = __half_as_ushort(__float2half_rn(f));
             if (fabs(a) <= DBL_MAX) {
                 cnt[1] += a != 0.0 && (h & 0x7fffu) == 0;
                 cnt[2] += (h & 0x7fffu) == 0x7c00u;

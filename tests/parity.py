@@ -10,10 +10,11 @@ fp64 Arnoldi with an fp64 preconditioner (mode baseline):
     later cycles:               |Δ| <= 1e-5 |s_ref| + 1e-10 ||M^-1 b||;
   * every cycle's backward error: |Δ| <= 1e-5 be_ref + 1e-15;
   * x, first 16 entries: |Δ| <= 1e-12 max|x_ref| + 0.25 e_ref,
-    sum: |Δ| <= 1e-12 max(|Σx_ref|, max|x_ref|) + 0.25 sqrt(n) e_ref,
+    sum: |Δ| <= 1e-12 max(|Σx_ref|, max|x_ref|) + 1.0 sqrt(n) e_ref,
     where e_ref = errNorm = ||x_ref - x_true||_2 of the reference run only:
-    the GPU's x must lie within a quarter of the reference's own error of
-    the reference's x (a bound that does not grow with the run under test;
+    each entry of the GPU's x must lie within a quarter of the reference's
+    own error of the reference's x (a bound that does not grow with the run
+    under test;
     |Δ| <= e_ref + e_got holds for any two runs, so a bound with e_got in it
     can never fail). Rounding-level differences (an ill-conditioned C1
     differs at 2e-12 relative) sit far inside it;
@@ -28,17 +29,19 @@ preconditioner every step (modes mixed, single, mixed-half, single-prec):
     the floor F = 1e-14 (fp64 residual) or 1e-6 (mode single, fp32
     residual) — the restarts of an fp32 cycle contract the error by
     amounts that differ with the fp32 rounding, never by more than that;
-  * x: the rule above with 1e-9 (fp64 outer) / 1e-5 (single) relative
-    and half the reference's error, 0.5 e_ref and 0.5 sqrt(n) e_ref (same
-    restart count only): the fp32 cycle's corrections differ in rounding,
-    so the iterates agree only to a fraction of the error they carry;
+  * x: the rule above with 1e-9 (fp64 outer) / 1e-5 (single) relative,
+    0.5 e_ref for the head and 2.5 sqrt(n) e_ref for the sum (same restart
+    count only): the fp32 cycle's corrections differ in rounding, so the
+    iterates agree only to a fraction of the error they carry;
   * final resNorm within a factor 10 (above the floor); errNorm at most
     10x the reference's (a more accurate x than the oracle's is not a
     parity failure: forward error at convergence depends on conditioning);
   * when converged, the final backward error is <= tol.
 Measured margins behind these numbers: tools/parity_margins.py over the
 168 golden records on the fused and operator-surface engines
-(profiles/r02_parity_margins.txt).
+(profiles/r02_parity_margins.txt; the x terms against e_ref alone:
+profiles/r03_parity_margins.txt, head <= 0.038 / 0.16 e_ref and sum <=
+0.41 / 1.24 sqrt(n) e_ref for fp64 / fp32 Arnoldi).
 """
 import numpy as np
 
@@ -75,7 +78,7 @@ def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
         assert np.all(d[c0] <= 1e-8 * s_ref[c0] + 1e-12 * minvb), f"{label}: cycle-0 history {d[c0].max():.3e}"
         assert np.all(d[~c0] <= 1e-5 * s_ref[~c0] + 1e-10 * minvb), f"{label}: history {d[~c0].max():.3e}"
         assert np.all(np.abs(be_got - be_ref) <= 1e-5 * be_ref + 1e-15), f"{label}: backward errors"
-        x_rtol, e_w, norm_factor = 1e-12, 0.25, (1.2, 2.0)
+        x_rtol, e_w, e_ws, norm_factor = 1e-12, 0.25, 1.0, (1.2, 2.0)
     else:
         assert abs(got.restarts - ref["restarts"]) <= 1, f"{label}: restarts {got.restarts} vs {ref['restarts']}"
         k = min(rlen, len(s_ref), len(s_got))
@@ -88,7 +91,7 @@ def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
                 f"{label}: cycle {c} backward error {be_got[c]:.3e} vs {be_ref[c]:.3e}"
         if got.status == "converged":
             assert be_got[-1] <= tol, f"{label}: final backward error {be_got[-1]:.3e} > {tol}"
-        x_rtol, e_w = (1e-5 if mode == "single" else 1e-9), 0.5
+        x_rtol, e_w, e_ws = (1e-5 if mode == "single" else 1e-9), 0.5, 2.5
         norm_factor = (10.0, 10.0)
     same_cycles = got.restarts == ref["restarts"]
     e_ref, e_got = float(ref.get("err_norm") or 0.0), float(getattr(got, "err_norm", 0.0) or 0.0)
@@ -98,7 +101,7 @@ def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
         assert dx <= bound, f"{label}: x head differs by {dx:.3e} (bound {bound:.3e}, scale {xscale:.3e})"
         xs_ref = float(ref["x_sum"])
         ds = abs(float(np.sum(got.x)) - xs_ref)
-        bound = x_rtol * max(abs(xs_ref), xscale) + e_w * np.sqrt(len(got.x)) * e_ref
+        bound = x_rtol * max(abs(xs_ref), xscale) + e_ws * np.sqrt(len(got.x)) * e_ref
         assert ds <= bound, f"{label}: x sum differs by {ds:.3e} (bound {bound:.3e})"
     if "res_norm" in ref and same_cycles and hasattr(got, "res_norm"):
         norm_last = float(_arr(ref["cyc_normalization"])[-1])

@@ -156,8 +156,8 @@ def _assert_rank_layouts(lays, nranks, forms):
 @pytest.mark.parametrize("mode,orth", [("mixed", "cgs"), ("baseline", "mgs")])
 def test_p8_stencil27_stepped_live_oracle(mpg, oracle, mode, orth):
     """BASELINE C4's structure (27-point, 3 dof, planes of 33,075 rows) split
-    over P = 8 ranks: each rank's SELL copy keeps the stepped int16 columns,
-    against the oracle at the parity tolerances (Orthogonalization.hpp:82-88
+    over P = 8 ranks: each rank's SELL copy keeps 2-byte columns (stepped
+    int16, or int16 where a rank's span fits), against the oracle at the parity tolerances (Orthogonalization.hpp:82-88
     is where the dots become all-reduces)."""
     A = mpg.gen_stencil27(105, 3, ny=105, nz=8)
     xt = mpg.rand_vect(A.nrows, 42)
@@ -165,7 +165,10 @@ def test_p8_stencil27_stepped_live_oracle(mpg, oracle, mode, orth):
     opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=1e-10, max_restarts=100)
     lays = []
     got = mpg.solve_loopback(A, b, xt, nranks=8, layouts=lays, **opts)
-    _assert_rank_layouts(lays, 8, ("stepped",))
+    # a rank whose lower halo starts inside its own plane can fit int16
+    # offsets; the rest keep the stepped form
+    _assert_rank_layouts(lays, 8, ("stepped", "int16"))
+    assert sum(L["col_form"] == "stepped" for L in lays) >= 4, lays
     ref = oracle.solve(mpg, A, b, xt, **opts)
     assert ref.status == "converged"
     compare(as_ref(ref), got, mode, opts["tol"], 30, f"p8-stencil27-{mode}-{orth}")
