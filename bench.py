@@ -13,22 +13,25 @@ One step = one restart cycle = check_initial on the host + 30 Arnoldi
 iterations + solution update + the next true-residual prologue (the fused
 engine's graph replay).
 
-Scaling modes (one row-partitioned solve over all ranks either way):
+Scaling modes (one row-partitioned solve over all ranks either way; value
+is that one solve's GMRES iterations per second at every N):
   weak (default)       each rank owns a 1e6-row BAND block of an N*1e6-row
-                       matrix; value = GMRES iterations x N blocks per second
-                       (the aggregate rate over 10M-nnz row blocks), and
-                       solve_iters_per_s is the one solve's iteration rate;
+                       matrix (10M nnz per GPU); the aggregate over row
+                       blocks (iterations x N per second) is reported
+                       separately as "aggregate";
   strong               --global-rows R: one R-row BAND matrix split over the
-                       N ranks (R = 1e7 is the north star's 100M-nnz matrix);
-                       value = that solve's iterations per second.
+                       N ranks (R = 1e7 is the north star's 100M-nnz matrix).
 
-Also reported (N = 1, rank 0): the roofline of the dominant kernel -- the
-Arnoldi SpMV as the cycle runs it (Givens folded), each launch timed by its
-own kernel events -- on the bytes its storage moves, against the 8 TB/s spec
-and the GPU's measured streaming peak (mpg_bw_probe, 2 GiB); the same SpMV
-on BAND-100M (a working set far past the 256 MB Infinity Cache) as the HBM
-figure; and the CPU oracle (MKL restatement of kernels_mkl.cpp) on the
-host cores, 1 warm-up + median of 5 per orthogonalisation.
+Also reported, at every N from rank 0: the roofline of the dominant kernel --
+the Arnoldi SpMV as the cycle runs it (Givens folded on one GPU), each launch
+timed by its own kernel events -- on the bytes its storage moves, against the
+8 TB/s spec and the GPU's measured streaming peak (mpg_bw_probe, 2 GiB), with
+every rank's mean launch time; the whole-iteration fraction; at N = 1 the
+same SpMV on BAND-100M (past the 256 MB Infinity Cache) as the HBM figure;
+and the CPU oracle (MKL restatement of kernels_mkl.cpp) on the same global
+matrix on the host cores -- the box's share at N = 1, the N GPUs' share of
+the node's physical cores at N > 1 (all of them at N = 8) -- 1 warm-up +
+the median of the timed runs per orthogonalisation.
 """
 import argparse
 import json
@@ -69,16 +72,19 @@ def cpu_info() -> dict:
     return info
 
 
-def cpu_threads() -> int:
-    """Threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS,
-    set to 16 per GPU on the pool), never more than the affinity mask or the
-    physical cores."""
+def cpu_threads(world: int = 1) -> int:
+    """Threads for the CPU baseline. N = 1: the box's CPU share
+    (OMP_NUM_THREADS, set to 16 per GPU on the pool). N > 1: the N GPUs'
+    share of the node's physical cores (N/8 of them; all at N = 8), as the
+    north star's ">= 6x vs MKL at 8 GPUs" compares against the whole host.
+    Never more than the affinity mask or the physical cores."""
     info = _CPU_INFO or cpu_info()
-    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or info["affinity_cpus"]
-    n = min(n, info["affinity_cpus"])
-    if info["physical_cores"]:
-        n = min(n, info["physical_cores"])
-    return max(n, 1)
+    cores = min(info["affinity_cpus"], info["physical_cores"] or info["affinity_cpus"])
+    if world > 1:
+        n = max(cores * min(world, 8) // 8, 1)
+    else:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or info["affinity_cpus"]
+    return max(min(n, cores), 1)
 
 
 def load_pkg():
@@ -115,13 +121,13 @@ def spmv_roofline(eng, cycles: int) -> dict:
             "achieved_gbs": actual / (avg_ms * 1e-3) / 1e9, "csr_equiv_gbs": csr / (avg_ms * 1e-3) / 1e9}
 
 
-def cpu_baseline(mpg, A, b, xt, opts, args):
+def cpu_baseline(mpg, A, b, xt, opts, args, world=1, workload="BAND-10M"):
     """The oracle (kernels_mkl.cpp restatement over the image's MKL) on the
     host cores: per orthogonalisation, 1 warm-up + the median of `runs`
     solves of `cpu_cycles` restart cycles each."""
     from oracle import binding
 
-    threads = cpu_threads()
+    threads = cpu_threads(world)
     info = _CPU_INFO or cpu_info()
     by_orth = {}
     for orth in dict.fromkeys([args.orth, "mgs"]):
@@ -139,7 +145,7 @@ def cpu_baseline(mpg, A, b, xt, opts, args):
             f"({threads} threads)")
     return {"value": by_orth[args.orth]["median"], "unit": "GMRES it/s", "cores": threads, "kind": "port",
             "sample": f"{args.cpu_cycles} restart cycles ({args.cpu_cycles * args.rlen} iterations) of the same "
-                      f"BAND-10M GMRES({args.rlen}) {args.mode}/{args.orth} solve; 1 warm-up + median of "
+                      f"{workload} GMRES({args.rlen}) {args.mode}/{args.orth} solve; 1 warm-up + median of "
                       f"{args.cpu_runs}; oracle backend {binding.backend()} (MKL restatement of kernels_mkl.cpp, "
                       f"GNU OpenMP threading, OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, "
                       f"OMP_PLACES={os.environ.get('OMP_PLACES')})",
@@ -256,7 +262,7 @@ def main():
     iters = eng.total_iters - it0
     assert ran == args.steps and iters == args.steps * args.rlen, (ran, iters)
     solve_rate = iters / elapsed
-    value = solve_rate if strong else solve_rate * world
+    value = solve_rate  # the one solve's iterations per second, at every N
     ms_per_step = 1e3 * elapsed / args.steps
     log(f"[bench] {args.steps} cycles, {iters} iterations in {elapsed:.4f}s -> {solve_rate:.1f} it/s")
 
@@ -269,18 +275,23 @@ def main():
     iter_bytes = (eng.phase_bytes("spmv_storage") + eng.phase_bytes("dots") + eng.phase_bytes("cgs_update")
                   if args.orth == "cgs" else None)
     eng.close()
-    log(f"[bench] {sp['kernel']} in-cycle {sp['avg_launch_ms'] * 1e3:.2f} us/launch over {sp['launches']} launches: "
-        f"{sp['achieved_gbs']:.0f} GB/s on its storage bytes, {sp['csr_equiv_gbs']:.0f} GB/s CSR-equivalent; "
-        f"{sp['layout']}")
+    log(f"[bench] rank {rank} {sp['kernel']} in-cycle {sp['avg_launch_ms'] * 1e3:.2f} us/launch over {sp['launches']} "
+        f"launches: {sp['achieved_gbs']:.0f} GB/s on its storage bytes, {sp['csr_equiv_gbs']:.0f} GB/s "
+        f"CSR-equivalent; {sp['layout']}")
+    per_rank_ms = [sp["avg_launch_ms"]]
+    if dist:
+        per_rank_ms = [None] * world
+        dist.all_gather_object(per_rank_ms, sp["avg_launch_ms"])
+    shared_gpu = os.environ.get("MPG_BENCH_SHARED_GPU") == "1"
     roofline = None
     cpu = None
-    if rank == 0 and world == 1:
+    if rank == 0:
         peak_read = mpg.bw_probe("read", 2 << 30, 3, local_rank)
         peak_copy = mpg.bw_probe("copy", 1 << 30, 3, local_rank)
         measured = max(peak_read, peak_copy)
         log(f"[bench] measured streaming peak: read {peak_read:.0f} GB/s, copy {peak_copy:.0f} GB/s")
         hbm = None
-        if args.hbm_rows > 0:
+        if args.hbm_rows > 0 and world == 1:
             t1 = time.time()
             Ah = mpg.gen_band(args.hbm_rows, 5, 4, seed=7)
             xh = mpg.rand_vect(args.hbm_rows, 42)
@@ -315,7 +326,12 @@ def main():
                     "frac_of_measured": round(sp["achieved_gbs"] / measured, 4),
                     "cache_note": "the BAND-10M Arnoldi working set (~190 MB) fits the 256 MB Infinity Cache; "
                                   "hbm_scale is the same kernel past it",
-                    "hbm_scale": hbm}
+                    "hbm_scale": hbm, "rank": 0,
+                    "per_rank_avg_launch_ms": [round(t, 5) for t in per_rank_ms]}
+        if world > 1:
+            roofline["kernel"] = sp["kernel"] + " (in-cycle, rank 0's row block; each step closes with its own Givens launch)"
+            if shared_gpu:
+                roofline["note"] = "rehearsal: all ranks share GPU 0, so each rank's launches overlap the others'"
         if iter_bytes:
             ach = iter_bytes * solve_rate / 1e9
             roofline["iteration"] = {
@@ -327,29 +343,46 @@ def main():
             log(f"[bench] whole iteration: {iter_bytes / 1e6:.1f} MB x {solve_rate:.0f} it/s = {ach:.0f} GB/s "
                 f"({ach / HBM_PEAK_GBS:.3f} of 8 TB/s, {ach / measured:.3f} of measured)")
         if not args.no_cpu_baseline:
-            cpu = cpu_baseline(mpg, A, b, xt, opts, args)
+            if world == 1:
+                cpu = cpu_baseline(mpg, A, b, xt, opts, args)
+            else:
+                # the same global matrix on the host (the GPU ranks hold row
+                # blocks of it), fewer timed runs at this size
+                t2 = time.time()
+                Ag = mpg.gen_band(n, 5, 4, seed=7)
+                bg = mpg.host_spmv(Ag, xt)
+                cargs = argparse.Namespace(**dict(vars(args), cpu_runs=min(args.cpu_runs, 3)))
+                cpu = cpu_baseline(mpg, Ag, bg, xt, opts, cargs, world, f"BAND n={n} ({global_nnz} nnz)")
+                log(f"[bench] CPU baseline on the global matrix took {time.time() - t2:.1f}s")
+                del Ag, bg
+            cpu["vs_gpu"] = round(value / cpu["value"], 2) if cpu["value"] else None
 
     if rank == 0:
         scaling = "strong" if strong else "weak"
+        transport = ("RCCL" if not shared_gpu else
+                     "the gloo host transport, every rank on GPU 0 (rehearsal; RCCL refuses two ranks on one GPU)")
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GMRES iterations/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic", "roofline": roofline, "cpu_baseline": cpu,
             "solve_iters_per_s": round(solve_rate, 2),
+            "aggregate": (None if strong or world == 1 else
+                          {"value": round(solve_rate * world, 2),
+                           "unit": "GMRES iterations x 10M-nnz row blocks (one per GPU) per second"}),
             "config": {"workload": f"BAND banded CSR n={n}, offsets -5..+4, nnz={global_nnz} "
                                    f"({'split over' if strong else '1e6 rows = 10M nnz per GPU,'} {world} GPU(s)); "
                                    f"GMRES({args.rlen}) {args.mode} (fp32 Arnoldi, fp64 residual/update), "
                                    f"{args.orth}, {args.prec} preconditioner, tol=0",
                        "step": f"one restart cycle = {args.rlen} iterations",
-                       "value_counts": ("GMRES iterations of the one solve per second" if strong else
-                                        "GMRES iterations x 10M-nnz row blocks (one per GPU) per second; "
-                                        "solve_iters_per_s is the solve's own rate"),
+                       "value_counts": "GMRES iterations of the one (row-partitioned) solve per second",
                        "rows_per_gpu": (r1 - r0), "nnz": global_nnz, "spmv_storage": sp["layout"],
-                       "parallelism": f"row-partition x{world} (halo send/recv + fp64 all-reduce over RCCL)"},
+                       "parallelism": (f"row-partition x{world} (halo send/recv + fp64 all-reduce over {transport})"
+                                       if world > 1 else "one GPU")},
         }
         print(json.dumps(line), flush=True)
     if dist:
+        dist.barrier()  # the other ranks wait for rank 0's measurements
         dist.destroy_process_group()
 
 

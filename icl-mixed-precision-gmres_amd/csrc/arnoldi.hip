@@ -439,7 +439,8 @@ struct SellDots {
     double* out;       // [c * ng + g]
 };
 
-template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD, int DN = 0, int BS = kBlock>
+template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD, int DN = 0, int BS = kBlock,
+          bool UNI = false>
 __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col,
                                                       const typename SellStore<VI>::type* __restrict__ val,
@@ -452,7 +453,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
                                                       const int32_t* __restrict__ xrp,
                                                       const int32_t* __restrict__ xcol,
                                                       const typename SellStore<VI>::type* __restrict__ xval,
-                                                      const int8_t* __restrict__ rexp, int xcd) {
+                                                      const int8_t* __restrict__ rexp, int64_t ustride, int xcd) {
     static_assert(DN == 0 || BS == kBlock, "the fused dots' partials assume kBlock-thread workgroups");
     using S = typename SellStore<VI>::type;
     constexpr int NQ = kWinLen / kWave;
@@ -462,9 +463,10 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
     const bool live = s < nslices;  // a dead wave still joins the fold's barriers
     const int row0 = s * kWave;
     const int i = row0 + lane;
-    // 0. the slice's offsets
+    // 0. the slice's offsets (UNI: computed) and pattern index
     SellRow<S, CI, W> row;
-    row.init_load(live ? s : 0, off, spat);
+    if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat);
+    else row.init_load(live ? s : 0, off, spat);
     __builtin_amdgcn_sched_barrier(0);
     // 1. the fold's ||w||^2 partial (nparts <= kBlock, checked at launch: one per lane)
     // (a workgroup narrower than kBlock loads kBlock / BS per lane: the
@@ -495,9 +497,18 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
         wr[0] = wprev[i < n ? i : 0];
     }
     __builtin_amdgcn_sched_barrier(0);
-    // 3. the slice's first batch
-    row.init_finish(lane, col, val, sbase, pat);
-    row.load(0);
+    // 3. the slice's first batch (UNI: the values before the pattern index
+    // is waited for, then the columns)
+    if constexpr (UNI) {
+        row.init_vals(lane, val);
+        row.load_vals(0);
+        __builtin_amdgcn_sched_barrier(0);
+        row.init_finish(lane, col, val, sbase, pat);
+        row.load_cols(0);
+    } else {
+        row.init_finish(lane, col, val, sbase, pat);
+        row.load(0);
+    }
     // 4. a scaled fp16 copy's row exponent (needed last, issued last)
     int rex = 0;
     if constexpr (std::is_same_v<VI, half_v>) {
@@ -602,6 +613,195 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
             double v = 0.0;
             for (int m = m0; m < m1; ++m) v += dd.wgpart[(size_t)c * gridDim.x + m];
             dd.out[(size_t)c * dd.ng + g] = v;
+        }
+    }
+    if constexpr (FOLD) {
+        __shared__ T col_s[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
+        if (blockIdx.x == 0) givens_block(fold.g, nrm2sq, col_s, c_s, s_s);
+    }
+}
+
+// k_step_sell with two adjacent slices per wave (lane l owns rows
+// 128 s' + l and 128 s' + 64 + l): every load of both slices -- one LDS
+// window of 64 + 128 + 64 entries for the pair, both slices' first batches --
+// is in flight before the wave waits for any, so each wave carries twice the
+// bytes through the same fixed work (the fold's partial sum, the barriers,
+// the window). Past the Infinity Cache a slice's loads alone do not keep
+// enough bytes in flight per CU (MI355X_MICROARCH.md: ~72 KiB per CU hides
+// an HBM miss). Same sums in the same order as k_step_sell: same bits.
+template <class T, class P, class VI, int W, bool WIN, bool FOLD, int BE, int BS = kBlock>
+__global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
+                                                   const int16_t* __restrict__ col,
+                                                   const typename SellStore<VI>::type* __restrict__ val,
+                                                   const T* __restrict__ wprev, const T* __restrict__ inv_p,
+                                                   T* __restrict__ V, int64_t ld, int k,
+                                                   const P* __restrict__ diag, T* __restrict__ w,
+                                                   GivensFold<T> fold, SellDots,
+                                                   const int32_t* __restrict__ sbase,
+                                                   const int32_t* __restrict__ spat, const int16_t* __restrict__ pat,
+                                                   const int32_t* __restrict__ xrp,
+                                                   const int32_t* __restrict__ xcol,
+                                                   const typename SellStore<VI>::type* __restrict__ xval,
+                                                   const int8_t* __restrict__ rexp, int64_t ustride, int xcd) {
+    using S = typename SellStore<VI>::type;
+    using CI = int16_t;
+    constexpr bool UNI = true;
+    constexpr int SPW = 2;
+    constexpr int WL = kWinLen + (SPW - 1) * kWave;  // the pair's window
+    constexpr int NQ = WL / kWave;
+    __shared__ T win[WIN ? BS / kWave : 1][WIN ? WL : 1];
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int s0 = ((xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid) * SPW;
+    const bool live = s0 < nslices;  // a dead wave still joins the fold's barriers
+    bool live_p[SPW];
+    const int row0 = s0 * kWave;
+    // 0. both slices' offsets (UNI: computed) and pattern indices
+    SellRow<S, CI, W, (MPG_SELL_NT != 0), BE> row[SPW];
+#pragma unroll
+    for (int p = 0; p < SPW; ++p) {
+        live_p[p] = s0 + p < nslices;
+        const int sp = live_p[p] ? s0 + p : 0;
+        if constexpr (UNI) row[p].init_uniform(sp, ustride, spat);
+        else row[p].init_load(sp, off, spat);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // 1. the fold's ||w||^2 partial (one per lane, as k_step_sell)
+    constexpr int NPL = BS < kBlock ? kBlock / BS : 1;
+    double part[NPL];
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) part[j] = 0.0;
+    if constexpr (FOLD) {
+#pragma unroll
+        for (int j = 0; j < NPL; ++j) {
+            const int t = j * BS + (int)threadIdx.x;
+            part[j] = fold.norm2[t < fold.nparts ? t : 0];
+            if (t >= fold.nparts) part[j] = 0.0;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // 2. the pair's w_prev window (or the lane's own rows' w_prev), raw
+    T wr[WIN ? NQ : SPW];
+    if constexpr (WIN) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int c = row0 - kWinLo + q * kWave + lane;
+            wr[q] = wprev[c >= n_lo && c < n_ext ? c : 0];
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < SPW; ++p) {
+            const int i = row0 + p * kWave + lane;
+            wr[p] = wprev[i < n ? i : 0];
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // 3. both slices' first batches (UNI: values first, then the columns)
+    if constexpr (UNI) {
+#pragma unroll
+        for (int p = 0; p < SPW; ++p) {
+            row[p].init_vals(lane, val);
+            row[p].load_vals(0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int p = 0; p < SPW; ++p) {
+            row[p].init_finish(lane, col, val, sbase, pat);
+            row[p].load_cols(0);
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < SPW; ++p) {
+            row[p].init_finish(lane, col, val, sbase, pat);
+            row[p].load(0);
+        }
+    }
+    // 4. a scaled fp16 copy's row exponents
+    int rex[SPW] = {};
+    if constexpr (std::is_same_v<VI, half_v>) {
+        if (rexp) {
+#pragma unroll
+            for (int p = 0; p < SPW; ++p) {
+                const int i = row0 + p * kWave + lane;
+                rex[p] = rexp[live_p[p] && i < n ? i : 0];
+            }
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    T inv;
+    double nrm2sq = 0.0;
+    if constexpr (FOLD) {
+        constexpr int NG = (BS < kBlock ? kBlock : BS) / kWave;
+        __shared__ double scratch[NG];
+        __shared__ T inv_s;
+        if (fold.nparts > 0) {
+#pragma unroll
+            for (int j = 0; j < NPL; ++j) {
+                const double v = wave_sum(part[j] + 0.0);
+                if (lane == 0) scratch[j * (BS / kWave) + wid] = v;
+            }
+            lds_barrier();
+            double r = 0.0;
+#pragma unroll
+            for (int q = 0; q < NG; ++q) r += scratch[q];
+            nrm2sq = r;
+        } else {
+            nrm2sq = fold.norm2[0];
+        }
+        if (threadIdx.x == 0) inv_s = inv_of_norm2<T>(nrm2sq);
+        lds_barrier();
+        inv = inv_s;
+    } else {
+        inv = *inv_p;
+    }
+    if (!live && !(FOLD && blockIdx.x == 0)) return;
+    double sum[SPW] = {};
+    T vk[SPW] = {};
+    if (live) {
+        if constexpr (WIN) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int c = row0 - kWinLo + q * kWave + lane;
+                win[wid][q * kWave + lane] = (c >= n_lo && c < n_ext) ? (T)(wr[q] * inv) : T(0);
+            }
+            wave_lds_sync();
+            auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
+#pragma unroll
+            for (int p = 0; p < SPW; ++p) row[p].sum(0, xv, sum[p]);
+#pragma unroll
+            for (int p = 0; p < SPW; ++p) {
+                for (int q = row[p].U; q < row[p].steps; q += row[p].U) {
+                    row[p].load(q);
+                    row[p].sum(q, xv, sum[p]);
+                }
+                vk[p] = win[wid][p * kWave + lane + kWinLo];
+            }
+        } else {
+            auto xv = [&](int c) { return (double)(T)(wprev[c] * inv); };
+#pragma unroll
+            for (int p = 0; p < SPW; ++p) {
+                const int i = row0 + p * kWave + lane;
+                if (SellCol<CI>::stepped && row[p].exc) {
+                    sum[p] = csr_row_sum(live_p[p] && i < n ? row[p].xrow : -1, xrp, xcol, xval, xv);
+                } else {
+                    row[p].sum(0, xv, sum[p]);
+                    for (int q = row[p].U; q < row[p].steps; q += row[p].U) {
+                        row[p].load(q);
+                        row[p].sum(q, xv, sum[p]);
+                    }
+                }
+                vk[p] = (T)(wr[p] * inv);
+            }
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < SPW; ++p) {
+        const int i = row0 + p * kWave + lane;
+        if (live_p[p] && i < n) {
+            double sp = sum[p];
+            if constexpr (std::is_same_v<VI, half_v>) sp = ldexp(sp, -rex[p]);
+            const T t = (T)sp;
+            w[i] = precond<T, P>(t, diag, i);
+            V[(int64_t)k * ld + i] = vk[p];
         }
     }
     if constexpr (FOLD) {
@@ -1512,7 +1712,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                             static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd,
                             S.sbase, S.spat, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
                             static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
-                            sell_xcd_order(S) ? 1 : 0);
+                            S.ustride, sell_xcd_order(S) ? 1 : 0);
                     return (int)MPG_OK;
                 };
                 if constexpr (std::is_same_v<T, float> && std::is_same_v<VI, float> &&
@@ -1532,6 +1732,31 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                 return sell_dispatch_win(S.win, [&](auto wn) {
                     constexpr bool WN = decltype(wn)::value;
                     using BSC = std::integral_constant<int, kStepSellBlock>;
+                    const int be = sell_uniform(S) ? sell_pair(S) : 0;
+                    if constexpr (std::is_same_v<CI, int16_t> && (Wc == 2 || Wc == 4)) if (be) {
+                        auto launch2 = [&](auto kern) {
+                            const int grid = (S.nslices + 2 * (kStepSellBlock / kWave) - 1) / (2 * (kStepSellBlock / kWave));
+                            launch_timed(a->ctx, kern, dim3(grid), dim3(kStepSellBlock),
+                                    a->d.n, -a->front, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
+                                    static_cast<const typename SellStore<VI>::type*>(S.val),
+                                    static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
+                                    static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf,
+                                    SellDots{}, S.sbase, S.spat, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
+                                    static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
+                                    S.ustride, sell_xcd_order(S) ? 1 : 0);
+                            return (int)MPG_OK;
+                        };
+                        if (be == 8)
+                            return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 8, kStepSellBlock>)
+                                        : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 8, kStepSellBlock>);
+                        return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 12, kStepSellBlock>)
+                                    : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 12, kStepSellBlock>);
+                    }
+                    if (sell_uniform(S))
+                        return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock, true>,
+                                             SellDots{}, BSC())
+                                    : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock, true>,
+                                             SellDots{}, BSC());
                     return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock>, SellDots{}, BSC())
                                 : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock>, SellDots{}, BSC());
                 });

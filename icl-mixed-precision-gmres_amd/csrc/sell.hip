@@ -282,6 +282,9 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
     S.n = n;
     S.nslices = ns;
     S.W = best_w;
+    S.ustride = off[1];
+    for (int s2 = 1; s2 < ns && S.ustride > 0; ++s2)
+        if (off[s2 + 1] - off[s2] != S.ustride) S.ustride = 0;
     S.vtype = vtype;
     S.c16 = c16;
     S.win = win;

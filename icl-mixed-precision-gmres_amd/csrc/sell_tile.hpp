@@ -115,9 +115,9 @@ template <int W> constexpr int sell_unroll() { return W >= kSellBatch ? 1 : kSel
 // offset 0 of the arrays.
 // NT: non-temporal slice loads (a pass that runs once per restart cycle, so
 // the slices the Arnoldi steps re-read stay in the Infinity Cache)
-template <class S, class CI, int W, bool NT = (MPG_SELL_NT != 0)>
+template <class S, class CI, int W, bool NT = (MPG_SELL_NT != 0), int BE = kSellBatch>
 struct SellRow {
-    static constexpr int U = sell_unroll<W>();
+    static constexpr int U = W >= BE ? 1 : BE / W;  // steps per batch (BE entries per lane)
     static constexpr bool kStepped = SellCol<CI>::stepped;
     CI c[U][W];
     S v[U][W];
@@ -138,6 +138,14 @@ struct SellRow {
                                               const int32_t* __restrict__ spat = nullptr) {
         o0 = off[s];
         o1 = off[s + 1];
+        row0 = s * kWave;
+        if (spat) pk = spat[s];
+    }
+    // every slice of the copy has the same width (SellCopy::ustride entries):
+    // the offsets are computed, so the value loads need no load before them
+    __device__ __forceinline__ void init_uniform(int s, int64_t ustride, const int32_t* __restrict__ spat = nullptr) {
+        o0 = (int64_t)s * ustride;
+        o1 = o0 + ustride;
         row0 = s * kWave;
         if (spat) pk = spat[s];
     }
@@ -175,6 +183,31 @@ struct SellRow {
             if constexpr (kStepped) VecW<int32_t, W, false>::load(bp + (int64_t)qq * W, bq[u]);
             VecW<CI, W, NT>::load(cp + (int64_t)qq * cstride, c[u]);
             VecW<S, W, NT>::load(vp + (int64_t)qq * kWave * W, v[u]);
+        }
+    }
+    // The first batch in two halves, for computed (uniform) offsets: the
+    // values need nothing loaded before them, the columns need the pattern
+    // index spat[s], so the values go out first and the columns once the
+    // index is back (init_vals, load_vals(0), init_finish, load_cols(0)).
+    __device__ __forceinline__ void init_vals(int lane, const S* __restrict__ val) {
+        steps = (int)((o1 - o0) / (kWave * W));
+        vp = val + (steps > 0 ? o0 + lane * W : 0);
+    }
+    __device__ __forceinline__ void load_vals(int q) {
+        const int last = steps > 0 ? steps - 1 : 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int qq = q + u < last ? q + u : last;
+            VecW<S, W, NT>::load(vp + (int64_t)qq * kWave * W, v[u]);
+        }
+    }
+    __device__ __forceinline__ void load_cols(int q) {
+        const int last = steps > 0 ? steps - 1 : 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int qq = q + u < last ? q + u : last;
+            if constexpr (kStepped) VecW<int32_t, W, false>::load(bp + (int64_t)qq * W, bq[u]);
+            VecW<CI, W, NT>::load(cp + (int64_t)qq * cstride, c[u]);
         }
     }
     // acc += the batch loaded at step q, in CSR order. Every gather is issued
@@ -235,6 +268,7 @@ struct SellCopy {
     int64_t nimp = 0;          // implicit slices
     int64_t imp_slots = 0;     // their slots (their columns are not read)
     int64_t npat = 0;          // pattern entries
+    int64_t ustride = 0;       // > 0: every slice holds this many slots (off[s] = s * ustride)
     int col_bytes() const { return c16 || c16s ? 2 : 4; }
 };
 
@@ -262,6 +296,32 @@ int sell_dispatch(const SellCopy& S, F&& f) {
 // of workgroups over the 8 XCDs every XCD's L2 fetches the whole of x for
 // the neighbour planes of its scattered slices; in XCD order each L2 serves
 // one contiguous run of rows (xcd_block, internal.hpp)
+// computed slice offsets whenever every slice has the same width
+// (MPG_SELL_UNIFORM=0: always load them). The offsets' load sits in front of
+// every slice's value loads; computing them measured BAND-100M fp16 99.1 ->
+// 93.6 us, fp32 108.2 -> 103.7, BAND-10M 13.85 -> 13.61, LAP-1M 14.27 ->
+// 13.91 (profiles/r03_spmv_uniform_ab.jsonl)
+inline bool sell_uniform(const SellCopy& S) {
+    if (S.ustride <= 0) return false;
+    const char* e = std::getenv("MPG_SELL_UNIFORM");
+    return !(e && *e == '0');
+}
+
+// two slices per wave in the Arnoldi SpMV (k_step_sell2): int16 columns,
+// uniform widths of at most 12 entries per lane in one batch, W 2 or 4
+// (banded matrices, 7-point stencils). Returns the batch size in entries
+// (8 or 12: the registers of one batch per slice), or 0 for one slice per
+// wave (MPG_SELL_PAIR=0: never). In-cycle, Givens folded
+// (profiles/r03_spmv_pair_ab.jsonl, median of 5 interleaved): BAND-100M fp16
+// 94.5 -> 72.9 us, fp32 102.8 -> 92.2, BAND-10M 14.2 -> 12.9, LAP-1M fp32
+// 14.0 -> 12.8, fp64 22.4 -> 19.7.
+inline int sell_pair(const SellCopy& S) {
+    const char* e = std::getenv("MPG_SELL_PAIR");
+    if ((e && *e == '0') || S.nslices < 2 || !S.c16 || S.ustride <= 0 || (S.W != 2 && S.W != 4)) return 0;
+    const int64_t entries = S.ustride / kWave;  // per lane (row) of every slice
+    return entries <= 8 ? 8 : entries <= 12 ? 12 : 0;
+}
+
 inline bool sell_xcd_order(const SellCopy& S) {
     const char* e = std::getenv("MPG_SELL_XCD");
     return !S.win && !(e && *e == '0');

@@ -1,3 +1,5 @@
+// Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+// University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 // Restart / convergence control (reference IterUtil.hpp:10-227).
 //
 // Base Convergence (IterUtil.hpp:17-81): convergence is only ever declared

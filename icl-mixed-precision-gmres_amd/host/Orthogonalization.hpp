@@ -1,3 +1,5 @@
+// Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+// University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 // Arnoldi basis and Gram-Schmidt kernels, Kokkos-free.
 //
 // Behaviour follows the reference Orthogonalization.hpp:

@@ -1,3 +1,5 @@
+// Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+// University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 // mpg_condest (include/mpgmres/condest.h): the reference's condition-number
 // estimator (condest.cpp:36-179) over the kernels.hpp operator surface, for
 // Device = Hip. The transposed products use SparseMatrix::set_transpose

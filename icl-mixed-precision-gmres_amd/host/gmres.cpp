@@ -1,3 +1,5 @@
+// Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+// University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 // Explicit instantiations of the GMRES drivers for the Hip backend —
 // the counterpart of CREATE_TEST_CONFIGS(MKL) / (Cuda) in the reference
 // (gmres.cpp:306-360): {CGS, MGS, CGSR(2)} x {double/double baseline,

@@ -1,3 +1,5 @@
+// Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+// University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 // Template bodies of the GMRES drivers declared in gmres.hpp.
 //
 // Control flow and arithmetic order follow the reference drivers

@@ -1,3 +1,5 @@
+// Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+// University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 // Command-line driver with the reference's flags and stdout lines
 // (gmres_perf_test.cpp:309-455), running on MI355X through mpg_solve.
 //

@@ -1,3 +1,5 @@
+// Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+// University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 // Operator surface of the GMRES hot path — the plugin boundary.
 //
 // Same operator set, names, argument order and <Type, Device> templating as

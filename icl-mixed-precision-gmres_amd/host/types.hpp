@@ -1,3 +1,5 @@
+// Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+// University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 // Kokkos-free data handles of the GMRES hot path.
 //
 // Mirrors the handle surface of the reference types.hpp:15-228 (Scalar,

@@ -1,3 +1,5 @@
+// Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+// University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 // ORACLE — test infrastructure only. Never linked into the product.
 // Run-time binding of the MKL runtime (or plain loops); see cpu_blas.hpp.
 #include "cpu_blas.hpp"

@@ -1,3 +1,5 @@
+// Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+// University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 // ORACLE — test infrastructure only. Never linked into the product; only
 // tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load it.
 //

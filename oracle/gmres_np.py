@@ -15,6 +15,8 @@ Only the base restart strategy is restated here. BLAS reductions use NumPy's
 own summation order, so agreement with the MKL oracle is to round-off, not
 bitwise.
 """
+# Derived from iamsonderr/icl-mixed-precision-gmres, Copyright (c) 2019-2021,
+# University of Tennessee (BSD-3-Clause; the license text is in NOTICE).
 from __future__ import annotations
 
 import numpy as np

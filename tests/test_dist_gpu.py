@@ -165,10 +165,11 @@ def test_p8_stencil27_stepped_live_oracle(mpg, oracle, mode, orth):
     opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=1e-10, max_restarts=100)
     lays = []
     got = mpg.solve_loopback(A, b, xt, nranks=8, layouts=lays, **opts)
-    # a rank whose lower halo starts inside its own plane can fit int16
-    # offsets; the rest keep the stepped form
+    # nnz-balanced ranks hold ~30k rows, under a plane (33,075): where the
+    # compacted halo numbering brings a rank's neighbour offsets within
+    # +-32767 its copy takes int16 columns, the others the stepped form
     _assert_rank_layouts(lays, 8, ("stepped", "int16"))
-    assert sum(L["col_form"] == "stepped" for L in lays) >= 4, lays
+    assert any(L["col_form"] == "stepped" for L in lays), lays
     ref = oracle.solve(mpg, A, b, xt, **opts)
     assert ref.status == "converged"
     compare(as_ref(ref), got, mode, opts["tol"], 30, f"p8-stencil27-{mode}-{orth}")

@@ -79,7 +79,8 @@ def test_scaled_values_and_spmv(hip, mpg):
         assert np.array_equal(dh.get(), want)
         h = dh.get().view(np.float16).astype(np.float64)
         rmax = np.maximum.reduceat(np.abs(h), A.rowptr[:-1])
-        assert np.all((rmax >= 2.0 ** -2) & (rmax < 2.0 ** 15)), (rmax.min(), rmax.max())
+        # (a row maximum just under 2^15 may round up to it)
+        assert np.all((rmax >= 2.0 ** -2) & (rmax <= 2.0 ** 15)), (rmax.min(), rmax.max())
         assert np.all(e[np.arange(n) % 3 == 2] < 0)  # the 1e4-scaled dof's rows were brought down
         x = np.random.default_rng(4).uniform(-1, 1, n).astype(np.float32)
         dx, dy = hip.buf(x), hip.buf(n, np.float32)
