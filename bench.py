@@ -115,7 +115,9 @@ def spmv_roofline(eng, cycles: int) -> dict:
     avg_ms, per = eng.time_spmv_incycle(cycles)
     actual = eng.phase_bytes("spmv_storage")
     csr = eng.phase_bytes("spmv")
-    return {"kernel": "k_step_sell" if layout["format"] == "sell" else "k_step_spmv", "layout": layout,
+    kernel = ("k_step_sell2" if layout.get("slices_per_wave") == 2 else "k_step_sell") if layout["format"] == "sell" \
+        else "k_step_spmv"
+    return {"kernel": kernel, "layout": layout,
             "avg_launch_ms": avg_ms, "launches": len(per), "min_launch_ms": min(per), "max_launch_ms": max(per),
             "storage_bytes": actual, "csr_bytes": csr,
             "achieved_gbs": actual / (avg_ms * 1e-3) / 1e9, "csr_equiv_gbs": csr / (avg_ms * 1e-3) / 1e9}
@@ -303,27 +305,35 @@ def main():
             del Ah, bh, xh
             hbm = {"workload": f"BAND n={args.hbm_rows}, nnz={10 * args.hbm_rows - 25} (working set > 256 MB "
                                f"Infinity Cache), same solve", "kernel": hs["kernel"],
-                   "avg_launch_ms": round(hs["avg_launch_ms"], 5), "storage_bytes_per_launch": int(hs["storage_bytes"]),
-                   "achieved": round(hs["achieved_gbs"], 1), "frac": round(hs["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                   "frac_of_measured": round(hs["achieved_gbs"] / measured, 4),
-                   "csr_equiv_gbs": round(hs["csr_equiv_gbs"], 1), "layout": hs["layout"]}
+                   "avg_launch_ms": round(hs["avg_launch_ms"], 5), "bytes_per_launch": int(hs["csr_bytes"]),
+                   "achieved": round(hs["csr_equiv_gbs"], 1), "frac": round(hs["csr_equiv_gbs"] / HBM_PEAK_GBS, 4),
+                   "storage_bytes_per_launch": int(hs["storage_bytes"]),
+                   "storage_achieved": round(hs["achieved_gbs"], 1),
+                   "storage_frac": round(hs["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                   "storage_frac_of_measured": round(hs["achieved_gbs"] / measured, 4), "layout": hs["layout"]}
             log(f"[bench] HBM scale ({time.time() - t1:.1f}s): {hs['avg_launch_ms'] * 1e3:.1f} us/launch, "
                 f"{hs['achieved_gbs']:.0f} GB/s on storage bytes")
         traffic = pmc_traffic(REPO / "profiles", sp["kernel"] + ":fold")
-        roofline = {"bound": "hbm", "achieved": round(sp["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(sp["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+        # achieved = SURVEY 8(d)'s algorithmic bytes (the reference's CSR
+        # SpMV: B_spmv) per launch / the launch's event time; the SELL copy
+        # moves fewer bytes (storage_*), traffic is what PMC counted
+        roofline = {"bound": "hbm", "achieved": round(sp["csr_equiv_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(sp["csr_equiv_gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": sp["kernel"] + " (in-cycle, Givens folded for k >= 1)",
                     "avg_launch_ms": round(sp["avg_launch_ms"], 5), "launches_timed": sp["launches"],
                     "timing": "hipExtLaunchKernel start/stop events of each in-cycle launch",
-                    "bytes_per_launch": int(sp["storage_bytes"]),
-                    "bytes_formula": "storage: SELL slots x (col + value bytes) + slice offsets + 3 n s_T "
-                                     "(w_prev read, v_k and w written)",
-                    "csr_equiv_bytes_per_launch": int(sp["csr_bytes"]),
-                    "csr_equiv_achieved": round(sp["csr_equiv_gbs"], 1),
-                    "csr_bytes_formula": "SURVEY 8(d) B_spmv = nnz*(s_v+4) + (n+1)*4 + 2*n*s_x",
+                    "bytes_per_launch": int(sp["csr_bytes"]),
+                    "bytes_formula": "SURVEY 8(d) B_spmv = nnz*(s_v+4) + (n+1)*4 + 2*n*s_x (algorithmic)",
+                    "storage_bytes_per_launch": int(sp["storage_bytes"]),
+                    "storage_achieved": round(sp["achieved_gbs"], 1),
+                    "storage_frac": round(sp["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                    "storage_formula": "what the SELL copy moves: slots x value bytes + stored columns (implicit "
+                                       "slices read none) + slice offsets/pattern indices + 3 n s_T (w_prev read, "
+                                       "v_k and w written)",
                     "measured_peak": round(measured, 1), "measured_peak_read": round(peak_read, 1),
                     "measured_peak_copy": round(peak_copy, 1),
-                    "frac_of_measured": round(sp["achieved_gbs"] / measured, 4),
+                    "frac_of_measured": round(sp["csr_equiv_gbs"] / measured, 4),
+                    "storage_frac_of_measured": round(sp["achieved_gbs"] / measured, 4),
                     "cache_note": "the BAND-10M Arnoldi working set (~190 MB) fits the 256 MB Infinity Cache; "
                                   "hbm_scale is the same kernel past it",
                     "hbm_scale": hbm, "rank": 0,

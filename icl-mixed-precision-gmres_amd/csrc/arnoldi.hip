@@ -1559,6 +1559,11 @@ int64_t mpg_arnoldi_sell_matrix_bytes(mpg_arnoldi_t a) {
            (a->d.inner_row_exp ? (int64_t)a->d.n : 0);
 }
 
+int mpg_arnoldi_slices_per_wave(mpg_arnoldi_t a) {
+    if (!a || a->sell.nslices == 0) return 0;
+    return sell_uniform(a->sell) && sell_pair(a->sell) ? 2 : 1;
+}
+
 int mpg_arnoldi_sell_columns(mpg_arnoldi_t a, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices) {
     if (!a) return MPG_ERR_ARG;
     const SellCopy& S = a->sell;

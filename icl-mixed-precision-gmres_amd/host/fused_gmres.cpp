@@ -1007,6 +1007,11 @@ int mpg_engine_sell_columns(mpg_engine_t e, int32_t* form, int64_t* csr_slices, 
     return mpg_arnoldi_sell_columns(e->eng->arnoldi(), form, csr_slices, implicit_slices);
 }
 
+int mpg_engine_slices_per_wave(mpg_engine_t e) {
+    if (!e || !e->eng) return MPG_ERR_ARG;
+    return mpg_arnoldi_slices_per_wave(e->eng->arnoldi());
+}
+
 int mpg_engine_half_stats(mpg_engine_t e, int64_t* stats) {
     if (!e || !e->eng || !stats) return MPG_ERR_ARG;
     for (int q = 0; q < 4; ++q) stats[q] = e->eng->half_stats()[q];

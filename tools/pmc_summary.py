@@ -28,9 +28,10 @@ def per_kernel(d, counter):
             # instantiation: keep them apart (FOLD is template argument 7 of
             # k_step_sell<T, P, VI, CI, W, WIN, FOLD, DN> and 4 of
             # k_step_spmv<T, P, VI, FOLD>)
-            if m and name in ("k_step_sell", "k_step_spmv") and m.group(2):
+            if m and name in ("k_step_sell", "k_step_sell2", "k_step_spmv") and m.group(2):
+                # (k_step_sell2<T, P, VI, W, WIN, FOLD, BE, BS>: FOLD is argument 6)
                 args = [a.strip() for a in m.group(2)[1:-1].split(",")]
-                at = 6 if name == "k_step_sell" else 3
+                at = {"k_step_sell": 6, "k_step_sell2": 5, "k_step_spmv": 3}[name]
                 if len(args) > at and args[at] == "true":
                     name += ":fold"
             vals[name].append(float(r["Counter_Value"]))
