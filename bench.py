@@ -72,7 +72,7 @@ def cpu_info() -> dict:
     return info
 
 
-def cpu_threads(world: int = 1) -> int:
+def cpu_threads(world: int = 1, shared_gpu: bool = False) -> int:
     """Threads for the CPU baseline. N = 1: the box's CPU share
     (OMP_NUM_THREADS, set to 16 per GPU on the pool). N > 1: the N GPUs'
     share of the node's physical cores (N/8 of them; all at N = 8), as the
@@ -80,7 +80,7 @@ def cpu_threads(world: int = 1) -> int:
     Never more than the affinity mask or the physical cores."""
     info = _CPU_INFO or cpu_info()
     cores = min(info["affinity_cpus"], info["physical_cores"] or info["affinity_cpus"])
-    if world > 1:
+    if world > 1 and not shared_gpu:
         n = max(cores * min(world, 8) // 8, 1)
     else:
         n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or info["affinity_cpus"]
@@ -129,7 +129,8 @@ def cpu_baseline(mpg, A, b, xt, opts, args, world=1, workload="BAND-10M"):
     solves of `cpu_cycles` restart cycles each."""
     from oracle import binding
 
-    threads = cpu_threads(world)
+    # (the shared-GPU rehearsal runs on one GPU's box: its share only)
+    threads = cpu_threads(world, os.environ.get("MPG_BENCH_SHARED_GPU") == "1")
     info = _CPU_INFO or cpu_info()
     by_orth = {}
     for orth in dict.fromkeys([args.orth, "mgs"]):

@@ -85,7 +85,8 @@ def test_spmv_layout_choice(mpg):
     e = mpg.Engine(A, b, xt, mode="mixed", orth="cgs", prec="identity", rlen=30, tol=0.0, max_restarts=2)
     try:  # 10 entries per row, 64-row slices, the last one half full
         assert e.spmv_layout() == {"format": "sell", "vec_width": 2, "col_bytes": 2,
-                                   "stored": -(-A.nrows // 64) * 64 * 10, "window": True}
+                                   "stored": -(-A.nrows // 64) * 64 * 10, "window": True,
+                                   "slices_per_wave": 2}  # uniform int16 slices: k_step_sell2
     finally:
         e.close()
     B = _arrow(mpg, 3000)
