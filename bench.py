@@ -314,13 +314,14 @@ def main():
                    "storage_frac_of_measured": round(hs["achieved_gbs"] / measured, 4), "layout": hs["layout"]}
             log(f"[bench] HBM scale ({time.time() - t1:.1f}s): {hs['avg_launch_ms'] * 1e3:.1f} us/launch, "
                 f"{hs['achieved_gbs']:.0f} GB/s on storage bytes")
-        traffic = pmc_traffic(REPO / "profiles", sp["kernel"] + ":fold")
+        traffic = pmc_traffic(REPO / "profiles", sp["kernel"] + (":fold" if sp["layout"]["givens_folded"] else ""))
         # achieved = SURVEY 8(d)'s algorithmic bytes (the reference's CSR
         # SpMV: B_spmv) per launch / the launch's event time; the SELL copy
         # moves fewer bytes (storage_*), traffic is what PMC counted
         roofline = {"bound": "hbm", "achieved": round(sp["csr_equiv_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(sp["csr_equiv_gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": sp["kernel"] + " (in-cycle, Givens folded for k >= 1)",
+                    "kernel": sp["kernel"] + (" (in-cycle, Givens folded for k >= 1)" if sp["layout"]["givens_folded"]
+                                              else " (in-cycle; the Givens step has its own launch)"),
                     "avg_launch_ms": round(sp["avg_launch_ms"], 5), "launches_timed": sp["launches"],
                     "timing": "hipExtLaunchKernel start/stop events of each in-cycle launch",
                     "bytes_per_launch": int(sp["csr_bytes"]),

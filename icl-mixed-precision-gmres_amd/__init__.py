@@ -127,6 +127,7 @@ def _declare_host(lib: C.CDLL) -> None:
                                             C.POINTER(C.c_int64)]
     lib.mpg_engine_half_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     lib.mpg_engine_slices_per_wave.argtypes = [C.c_void_p]
+    lib.mpg_engine_givens_folded.argtypes = [C.c_void_p]
 
 
 # (name, argtypes) for the kernel-level C-ABI, used by the per-kernel tests
@@ -639,7 +640,8 @@ class Engine:
             raise RuntimeError("mpg_engine_spmv_layout failed")
         return {"format": {1: "csr", 2: "sell"}[f.value], "vec_width": w.value, "col_bytes": cb.value,
                 "stored": st.value, "window": bool(win.value),
-                "slices_per_wave": int(self._lib.mpg_engine_slices_per_wave(self._h))}
+                "slices_per_wave": int(self._lib.mpg_engine_slices_per_wave(self._h)),
+                "givens_folded": bool(self._lib.mpg_engine_givens_folded(self._h) == 1)}
 
     def sell_columns(self) -> dict:
         """Column form of the Arnoldi SpMV's SELL copy (mpg_engine_sell_columns):

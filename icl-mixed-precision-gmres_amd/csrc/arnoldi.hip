@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__
 // wave per slice, one lane per row; loads issued in need order as in
 // k_step_sell): r = b - A x (X), w = M(T(r)), partials ||T(r)||^2,
 // ||w||^2, ||x||^2 per workgroup.
-template <class T, class X, class P, class CI, int W, bool WIN>
+template <class T, class X, class P, class CI, int W, bool WIN, bool UNI = false>
 __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                           const CI* __restrict__ col, const X* __restrict__ val,
                                                           const X* __restrict__ x, const X* __restrict__ b,
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
                                                           const int32_t* __restrict__ spat, const CI* __restrict__ pat,
                                                           const int32_t* __restrict__ xrp,
                                                           const int32_t* __restrict__ xcol,
-                                                          const X* __restrict__ xval, int xcd) {
+                                                          const X* __restrict__ xval, int64_t ustride, int xcd) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
@@ -145,7 +145,8 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
     const int i = row0 + lane;
     const bool own = live && i < n;
     SellRow<X, CI, W, true> row;  // once per cycle: non-temporal slices
-    row.init_load(live ? s : 0, off, spat);
+    if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat);
+    else row.init_load(live ? s : 0, off, spat);
     __builtin_amdgcn_sched_barrier(0);
     X xr[WIN ? NQ : 1];
     if constexpr (WIN) {
@@ -1613,14 +1614,19 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
             return sell_dispatch(*S, [&](auto ci, auto wc) {
                 using CI = decltype(ci);
                 return sell_dispatch_win(S->win, [&](auto wn) {
-                    k_prologue_sell<T, X, P, CI, decltype(wc)::value, decltype(wn)::value>
-                        <<<grid, kBlock, 0, a->ctx->stream>>>(
+                    auto go = [&](auto kern) {
+                        kern<<<grid, kBlock, 0, a->ctx->stream>>>(
                             a->d.n, -a->front, a->d.n_ext, S->nslices, S->off, static_cast<const CI*>(S->col),
                             static_cast<const X*>(S->val), static_cast<const X*>(a->d.x),
                             static_cast<const X*>(a->d.b), diag, static_cast<T*>(a->w[0]), a->partial, S->sbase,
                             S->spat, static_cast<const CI*>(S->pat), S->xrp, S->xcol, static_cast<const X*>(S->xval),
-                            sell_xcd_order(*S) ? 1 : 0);
-                    return (int)MPG_OK;
+                            S->ustride, sell_xcd_order(*S) ? 1 : 0);
+                        return (int)MPG_OK;
+                    };
+                    constexpr int Wc = decltype(wc)::value;
+                    constexpr bool WN = decltype(wn)::value;
+                    return sell_uniform(*S) ? go(k_prologue_sell<T, X, P, CI, Wc, WN, true>)
+                                            : go(k_prologue_sell<T, X, P, CI, Wc, WN, false>);
                 });
             });
         }
@@ -1791,6 +1797,21 @@ int mpg_arnoldi_spmv_dots(mpg_arnoldi_t a, int k, int fold) {
 int mpg_arnoldi_givens_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 1); }
 int mpg_arnoldi_givens_partials_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 2); }
 int mpg_arnoldi_fold_max_m(void) { return kFoldMaxM; }
+
+// The folded Givens step costs every SpMV workgroup the sum of the previous
+// launch's partials and two barriers; a separate Givens launch costs ~4.6 us.
+// Measured whole solves (tools/bench_configs.py, profiles/r03_fold_ab.jsonl):
+// fold 25.3k vs 24.3k it/s on LAP-1M (1,954 paired workgroups), but 1,756 vs
+// 1,787 on the C4 stand-in (16,029 workgroups) and 2,874 vs 3,015 on BAND-100M
+// fp16 (19,532): the fold pays up to kFoldMaxGroups SpMV workgroups.
+constexpr int kFoldMaxGroups = 4096;
+int mpg_arnoldi_fold_pays(mpg_arnoldi_t a) {
+    if (!a) return 0;
+    const SellCopy& S = a->sell;
+    if (S.nslices == 0) return a->Grb <= kFoldMaxGroups ? 1 : 0;
+    const int per_group = (kStepSellBlock / kWave) * (sell_uniform(S) && sell_pair(S) ? 2 : 1);
+    return (S.nslices + per_group - 1) / per_group <= kFoldMaxGroups ? 1 : 0;
+}
 
 static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;

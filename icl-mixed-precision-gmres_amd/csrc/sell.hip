@@ -140,7 +140,7 @@ constexpr int kProgStage = 64;  // rot_vec rotations staged per pass by a riding
 // prog.count > 0: workgroup 0 runs that scalar program instead (the
 // operator surface's Givens step of the previous Arnoldi step, which nothing
 // in this SpMV reads or writes: kernels_hip.cpp checks the operands).
-template <class X, class S, class CI, int W, bool WIN>
+template <class X, class S, class CI, int W, bool WIN, bool UNI = false>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col, const S* __restrict__ val,
                                                       const int32_t* __restrict__ sbase,
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
                                                       const int32_t* __restrict__ xrp,
                                                       const int32_t* __restrict__ xcol, const S* __restrict__ xval,
                                                       const X* __restrict__ x, X alpha, X beta, X* __restrict__ y,
-                                                      int xcd, ScalarProgram prog) {
+                                                      int64_t ustride, int xcd, ScalarProgram prog) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
@@ -169,7 +169,8 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
     const int row0 = s * kWave;
     const int i = row0 + lane;
     SellRow<S, CI, W> row;
-    row.init_load(s, off, spat);
+    if constexpr (UNI) row.init_uniform(s, ustride, spat);
+    else row.init_load(s, off, spat);
     __builtin_amdgcn_sched_barrier(0);
     X xr[WIN ? NQ : 1];
     if constexpr (WIN) {
@@ -488,11 +489,16 @@ int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y,
     int st = sell_dispatch(S, [&](auto ci, auto wc) {
         using CI = decltype(ci);
         return sell_dispatch_win(S.win, [&](auto wn) {
-            k_sell_spmv<X, St, CI, decltype(wc)::value, decltype(wn)::value><<<grid, kBlock, 0, ctx->stream>>>(
-                S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val), S.sbase,
-                S.spat, static_cast<const CI*>(S.pat), S.xrp, S.xcol, static_cast<const St*>(S.xval), x, alpha, beta, y,
-                sell_xcd_order(S) ? 1 : 0, prog);
-            return (int)MPG_OK;
+            auto go = [&](auto kern) {
+                kern<<<grid, kBlock, 0, ctx->stream>>>(
+                    S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val),
+                    S.sbase, S.spat, static_cast<const CI*>(S.pat), S.xrp, S.xcol, static_cast<const St*>(S.xval), x,
+                    alpha, beta, y, S.ustride, sell_xcd_order(S) ? 1 : 0, prog);
+                return (int)MPG_OK;
+            };
+            constexpr int Wc = decltype(wc)::value;
+            constexpr bool WN = decltype(wn)::value;
+            return sell_uniform(S) ? go(k_sell_spmv<X, St, CI, Wc, WN, true>) : go(k_sell_spmv<X, St, CI, Wc, WN, false>);
         });
     });
     if (st) return st;

@@ -389,8 +389,11 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     // (=2: required -- an error where the storage does not support it; tests)
     I.fuse_dots = I.cgs_partials && I.orth == MPG_ORTH_CGS && denv && (*denv == '1' || *denv == '2');
     I.fuse_dots_required = I.fuse_dots && *denv == '2';
+    // MPG_FOLD_GIVENS: 0 never, 1 always (m permitting), unset: where it pays
+    // (mpg_arnoldi_fold_pays: up to ~4k SpMV workgroups)
     const char* fenv = std::getenv("MPG_FOLD_GIVENS");
-    I.fold = !I.combine && !(fenv && *fenv == '0') && I.m <= mpg_arnoldi_fold_max_m();
+    const bool fold_on = fenv && *fenv ? *fenv != '0' : mpg_arnoldi_fold_pays(I.arn) != 0;
+    I.fold = !I.combine && fold_on && I.m <= mpg_arnoldi_fold_max_m();
     check(mpg_ctx_sync(ctx), "sync", ctx);
     setup_seconds = std::chrono::duration<double>(clk::now() - t0).count();
     prologue();
@@ -812,6 +815,7 @@ double FusedEngine::phase_bytes(int which) const {
 
 mpg_arnoldi_t FusedEngine::arnoldi() const { return p_->arn; }
 const int64_t* FusedEngine::half_stats() const { return p_->half_stats; }
+bool FusedEngine::givens_folded() const { return p_->fold; }
 
 // Device-event time of one phase kernel in its place in the cycle: `reps`
 // restart cycles run eagerly in cycle order, and at every launch of phase
@@ -1005,6 +1009,11 @@ int mpg_engine_spmv_layout(mpg_engine_t e, int32_t* format, int32_t* vec_width, 
 int mpg_engine_sell_columns(mpg_engine_t e, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices) {
     if (!e || !e->eng) return MPG_ERR_ARG;
     return mpg_arnoldi_sell_columns(e->eng->arnoldi(), form, csr_slices, implicit_slices);
+}
+
+int mpg_engine_givens_folded(mpg_engine_t e) {
+    if (!e || !e->eng) return MPG_ERR_ARG;
+    return e->eng->givens_folded() ? 1 : 0;
 }
 
 int mpg_engine_slices_per_wave(mpg_engine_t e) {

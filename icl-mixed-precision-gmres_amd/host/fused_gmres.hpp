@@ -84,6 +84,8 @@ public:
     // mixed-half: what the fp16 cast of the Arnoldi values did (stats of
     // mpg_csr_half_values, capi.h; zeros in other modes)
     const int64_t* half_stats() const;
+    // the Givens step rides the next SpMV (MPG_FOLD_GIVENS, mpg_arnoldi_fold_pays)
+    bool givens_folded() const;
     void sync();
 
     // history (per restart / per step)

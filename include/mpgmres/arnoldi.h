@@ -144,6 +144,10 @@ int mpg_arnoldi_givens_partials_spmv(mpg_arnoldi_t a, int k);
  * with an fp32 basis, fp32 values, 16-bit columns and the v_k window. */
 int mpg_arnoldi_spmv_dots(mpg_arnoldi_t a, int k, int fold);
 int mpg_arnoldi_fold_max_m(void);
+/* 1 when folding the Givens step into the SpMV pays at this size (the SpMV's
+ * workgroups each sum the partials; past ~4k workgroups a separate Givens
+ * launch costs less); the engine folds then unless MPG_FOLD_GIVENS says */
+int mpg_arnoldi_fold_pays(mpg_arnoldi_t a);
 int mpg_arnoldi_update(mpg_arnoldi_t a, int k);
 /* sums[c] = sum over workgroups of partial column c, c < ncols */
 int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols);

@@ -86,7 +86,8 @@ def test_spmv_layout_choice(mpg):
     try:  # 10 entries per row, 64-row slices, the last one half full
         assert e.spmv_layout() == {"format": "sell", "vec_width": 2, "col_bytes": 2,
                                    "stored": -(-A.nrows // 64) * 64 * 10, "window": True,
-                                   "slices_per_wave": 2}  # uniform int16 slices: k_step_sell2
+                                   "slices_per_wave": 2,  # uniform int16 slices: k_step_sell2
+                                   "givens_folded": True}
     finally:
         e.close()
     B = _arrow(mpg, 3000)
