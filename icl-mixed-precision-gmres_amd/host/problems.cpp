@@ -274,7 +274,29 @@ int mpg_load_mtx(const char* path, mpg_host_csr* out, char* err, int errlen) {
     if (!read_banner(f, h, why)) { std::fclose(f); set_err(err, errlen, why); return -2; }
     char line[1025];
     long M = 0, N = 0, L = 0;
-    if (!next_data_line(f, line, sizeof line) || std::sscanf(line, "%ld %ld %ld", &M, &N, &L) != 3) {
+    // mm_read_mtx_crd_size (mmio.c:189-217, which LoadMatrix.hpp:44 calls):
+    // the first non-comment line, or, when it does not hold three integers,
+    // whatever fscanf("%d %d %d") finds further on (an array file's "M N"
+    // line then reads on into its values and fails the type check below,
+    // as in the reference)
+    bool size_ok = false;
+    if (std::fgets(line, sizeof line, f)) {
+        while (line[0] == '%' && std::fgets(line, sizeof line, f)) {
+        }
+        if (line[0] != '%') {
+            if (std::sscanf(line, "%ld %ld %ld", &M, &N, &L) == 3) {
+                size_ok = true;
+            } else {
+                // (a token that is not a number matches nothing and is never
+                // consumed: mmio.c loops forever there, this stops)
+                int got;
+                do got = std::fscanf(f, "%ld %ld %ld", &M, &N, &L);
+                while (got != EOF && got != 3 && got != 0);
+                size_ok = got == 3;
+            }
+        }
+    }
+    if (!size_ok) {
         std::fclose(f);
         set_err(err, errlen, "Malformed matrix size information");
         return -2;

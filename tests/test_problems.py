@@ -113,3 +113,12 @@ def test_mtx_vector_loader_reference_semantics(mpg, tmp_path):
         mpg.load_mtx_vector(str(tmp_path / "missing.mtx"), 4)
     with pytest.raises(ValueError, match="does not match"):
         mpg.load_mtx_vector(str(q), 5)
+
+
+def test_mtx_loader_stops_on_a_text_size_line(mpg, tmp_path):
+    """A size line with text in it: mmio.c's fscanf loop would spin forever
+    (it never consumes a token that matches no %d); the loader reports it."""
+    p = tmp_path / "t.mtx"
+    p.write_text("%%MatrixMarket matrix coordinate real general\nthree by three\nno numbers here\n")
+    with pytest.raises(ValueError, match="Malformed matrix size information"):
+        mpg.load_mtx(str(p))
