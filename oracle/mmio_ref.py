@@ -98,3 +98,45 @@ def assemble(N, I, J, V, symmetric):
         order = np.argsort(col[a:b], kind="stable")
         col[a:b], val[a:b] = col[a:b][order], val[a:b][order]
     return rowptr, col, val
+
+
+def load_vector(path: str, col: int = 0) -> np.ndarray:
+    """LoadVector<double>(file, col) (LoadMatrix.hpp:156-233) with the
+    reference's mmio.c banner/size readers and its fscanf formats."""
+    lib = _lib()
+    lib.mm_read_mtx_array_size.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 2
+    f = _libc.fopen(str(path).encode(), b"r")
+    if not f:
+        raise ValueError("Could not access file")
+    try:
+        code = C.create_string_buffer(4)
+        err = lib.mm_read_banner(f, code)
+        if err:
+            raise ValueError({MM_PREMATURE_EOF: "Missing values in banner", MM_NO_HEADER: "Banner is missing",
+                              MM_UNSUPPORTED_TYPE: "Unrecognized description"}.get(
+                                  err, "Malformed banner with unknown error code"))
+        array = code.raw[1:2] == b"A"
+        M, N, nnz = C.c_int(), C.c_int(), C.c_int()
+        err = (lib.mm_read_mtx_array_size(f, C.byref(M), C.byref(N)) if array
+               else lib.mm_read_mtx_crd_size(f, C.byref(M), C.byref(N), C.byref(nnz)))
+        if err:
+            raise ValueError("Malformed matrix size information")
+        if col >= N.value:
+            raise ValueError(f"Column {col} is too large for the {N.value} vectors")
+        out = np.zeros(M.value)
+        d = C.c_double()
+        if array:  # LoadMatrix.hpp:197-209
+            for _ in range(col * M.value):
+                _libc.fscanf(C.c_void_p(f), b"%lf\n", C.byref(d))
+            for j in range(M.value):
+                _libc.fscanf(C.c_void_p(f), b"%lf\n", C.byref(d))
+                out[j] = d.value
+        else:  # LoadMatrix.hpp:210-222
+            ii, jj = C.c_int(), C.c_int()
+            for _ in range(nnz.value):
+                _libc.fscanf(C.c_void_p(f), b"%d %d %lg\n", C.byref(ii), C.byref(jj), C.byref(d))
+                if jj.value - 1 == col:
+                    out[ii.value - 1] = d.value
+    finally:
+        _libc.fclose(f)
+    return out

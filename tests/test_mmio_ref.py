@@ -75,3 +75,27 @@ def test_rejections_match_reference_parser(mpg, tmp_path, text):
     with pytest.raises(ValueError) as ours:
         mpg.load_mtx(str(p))
     assert str(ours.value) == str(ref.value), (str(ours.value), str(ref.value))
+
+
+@pytest.mark.parametrize("col", [0, 1])
+def test_vector_loader_matches_reference_parser(mpg, tmp_path, col):
+    """--bpath's LoadVector (LoadMatrix.hpp:156-233): array and coordinate
+    files against the reference's mmio.c readers and fscanf formats."""
+    g = np.random.default_rng(col)
+    n = 200
+    a = g.standard_normal((2, n)) * 10.0 ** g.integers(-6, 6, (2, n))
+    pa = tmp_path / "a.mtx"
+    pa.write_text("%%MatrixMarket matrix array real general\n% rhs\n" + f"{n} 2\n" +
+                  "".join(f"{v!r}\n" for v in a.reshape(-1)))
+    rows = g.choice(n, 50, replace=False)
+    pc = tmp_path / "c.mtx"
+    pc.write_text("%%MatrixMarket matrix coordinate real general\n" + f"{n} 2 100\n" +
+                  "".join(f"{r + 1} {c + 1} {g.standard_normal()!r}\n" for c in (0, 1) for r in rows))
+    for p in (pa, pc):
+        ref = mmio_ref.load_vector(str(p), col)
+        assert np.array_equal(mpg.load_mtx_vector(str(p), n, col), ref)
+    with pytest.raises(ValueError) as ref_err:
+        mmio_ref.load_vector(str(pa), 2)
+    with pytest.raises(ValueError) as our_err:
+        mpg.load_mtx_vector(str(pa), n, 2)
+    assert str(our_err.value) == str(ref_err.value)
