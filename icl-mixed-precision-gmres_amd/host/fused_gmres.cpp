@@ -382,7 +382,9 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     const char* penv = std::getenv("MPG_CGS_PARTIALS");
     // (CGSR's first pass also emits the next dots: its in-launch form is the
     // older runtime-count kernel, slower than reduce + update; on only with =1)
-    I.cgs_partials = !comm && !I.combine && I.orth != MPG_ORTH_MGS &&
+    // (ranks: the dots' partials are all-reduced in place first, so the
+    // update still sums them itself -- no reduce launch per step)
+    I.cgs_partials = !I.combine && I.orth != MPG_ORTH_MGS &&
                      (I.orth == MPG_ORTH_CGSR ? (penv && *penv == '1') : !(penv && *penv == '0'));
     // MPG_FUSE_DOTS=1: the panel dots inside the SELL SpMV launch (SellDots)
     const char* denv = std::getenv("MPG_FUSE_DOTS");
@@ -421,9 +423,12 @@ void FusedEngine::prologue() {
 
 // ranks: sum the last kernel's per-workgroup partials across ranks in place
 // (bit-identical on every rank), for a consumer that sums them itself
-void FusedEngine::allreduce_partials() {
+void FusedEngine::allreduce_partials(int ncols) {
     Impl& I = *p_;
-    I.comm->allreduce_sum(mpg_arnoldi_partials_dev(I.arn), mpg_arnoldi_partials_count(I.arn), I.stream());
+    // the last launch's partials, [column][workgroup] (uniform workgroup
+    // counts on every rank: mpg_arnoldi_uniform_groups), summed in place
+    I.comm->allreduce_sum(mpg_arnoldi_partials_dev(I.arn), (int64_t)ncols * mpg_arnoldi_partials_count(I.arn),
+                          I.stream());
 }
 
 void FusedEngine::reduce(int nc) {
@@ -479,7 +484,7 @@ void FusedEngine::step(int k, bool fold) {
             for (int j = 0; j <= k; ++j) check(mpg_arnoldi_mgs_partials(I.arn, k, j), "mgs", I.ctx);
         } else {  // ranks: all-reduce the 256 partials in place, then the same in-launch sums
             for (int j = 0; j <= k; ++j) {
-                allreduce_partials();
+                allreduce_partials(1);
                 check(mpg_arnoldi_mgs_partials(I.arn, k, j), "mgs", I.ctx);
             }
         }
@@ -496,6 +501,7 @@ void FusedEngine::step(int k, bool fold) {
             timed(3, [&] { check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx); });
             check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
             if (I.cgs_partials && small) {
+                if (I.comm) allreduce_partials(k + 1);
                 check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx);
                 pass0_done = true;
             } else {

@@ -105,7 +105,7 @@ private:
     void prologue();
     void step(int k, bool fold);
     void reduce(int nc);
-    void allreduce_partials();
+    void allreduce_partials(int ncols);
     void givens(int k);
     template <class F>
     void timed(int phase, F&& launch);
