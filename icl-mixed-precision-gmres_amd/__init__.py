@@ -128,6 +128,8 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_half_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     lib.mpg_engine_slices_per_wave.argtypes = [C.c_void_p]
     lib.mpg_engine_givens_folded.argtypes = [C.c_void_p]
+    lib.mpg_engine_sell_shared_slices.argtypes = [C.c_void_p]
+    lib.mpg_engine_sell_shared_slices.restype = C.c_int64
 
 
 # (name, argtypes) for the kernel-level C-ABI, used by the per-kernel tests
@@ -179,6 +181,7 @@ _HIP_DECLS.update({
     "mpg_csr_spmv_f16f32_scaled": ([_P, _P, C.c_float, _P, _P, _P, C.c_float, _P], C.c_int),
     "mpg_csr_half_values": ([_P, _P, _P, _I32, _P, _P, C.POINTER(_I64)], C.c_int),
     "mpg_sell_create": ([_P, _P, _I32, _P, _I32, C.POINTER(_P)], C.c_int),
+    "mpg_sell_shared_slices": ([_P], C.c_int64),
     "mpg_sell_destroy": ([_P], C.c_int),
     "mpg_sell_layout": ([_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I64), C.POINTER(_I32)], C.c_int),
     "mpg_sell_spmv_f64": ([_P, _P, C.c_double, _P, C.c_double, _P], C.c_int),
@@ -650,7 +653,8 @@ class Engine:
         if self._lib.mpg_engine_sell_columns(self._h, C.byref(f), C.byref(e), C.byref(i)):
             raise RuntimeError("mpg_engine_sell_columns failed")
         return {"form": {-1: "none", 0: "int32", 1: "int16", 2: "stepped"}[f.value], "csr_slices": e.value,
-                "implicit_slices": i.value}
+                "implicit_slices": i.value,
+                "shared_slices": int(self._lib.mpg_engine_sell_shared_slices(self._h))}
 
     def half_stats(self) -> dict:
         """mixed-half: what the fp16 cast did (mpg_engine_half_stats)."""

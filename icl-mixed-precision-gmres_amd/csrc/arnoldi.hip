@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
                                                           const P* __restrict__ diag, T* __restrict__ w,
                                                           double* __restrict__ partial,
                                                           const int32_t* __restrict__ sbase,
-                                                          const int32_t* __restrict__ spat, const CI* __restrict__ pat,
+                                                          const int32_t* __restrict__ spat, const int64_t* __restrict__ coff, const CI* __restrict__ pat,
                                                           const int32_t* __restrict__ xrp,
                                                           const int32_t* __restrict__ xcol,
                                                           const X* __restrict__ xval, int64_t ustride, int xcd) {
@@ -145,8 +145,8 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
     const int i = row0 + lane;
     const bool own = live && i < n;
     SellRow<X, CI, W, true> row;  // once per cycle: non-temporal slices
-    if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat);
-    else row.init_load(live ? s : 0, off, spat);
+    if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat, coff);
+    else row.init_load(live ? s : 0, off, spat, coff);
     __builtin_amdgcn_sched_barrier(0);
     X xr[WIN ? NQ : 1];
     if constexpr (WIN) {
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
                                                       const P* __restrict__ diag, T* __restrict__ w,
                                                       GivensFold<T> fold, SellDots dd,
                                                       const int32_t* __restrict__ sbase,
-                                                      const int32_t* __restrict__ spat, const CI* __restrict__ pat,
+                                                      const int32_t* __restrict__ spat, const int64_t* __restrict__ coff, const CI* __restrict__ pat,
                                                       const int32_t* __restrict__ xrp,
                                                       const int32_t* __restrict__ xcol,
                                                       const typename SellStore<VI>::type* __restrict__ xval,
@@ -466,8 +466,8 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
     const int i = row0 + lane;
     // 0. the slice's offsets (UNI: computed) and pattern index
     SellRow<S, CI, W> row;
-    if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat);
-    else row.init_load(live ? s : 0, off, spat);
+    if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat, coff);
+    else row.init_load(live ? s : 0, off, spat, coff);
     __builtin_amdgcn_sched_barrier(0);
     // 1. the fold's ||w||^2 partial (nparts <= kBlock, checked at launch: one per lane)
     // (a workgroup narrower than kBlock loads kBlock / BS per lane: the
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
                                                    const P* __restrict__ diag, T* __restrict__ w,
                                                    GivensFold<T> fold, SellDots,
                                                    const int32_t* __restrict__ sbase,
-                                                   const int32_t* __restrict__ spat, const int16_t* __restrict__ pat,
+                                                   const int32_t* __restrict__ spat, const int64_t* __restrict__ coff, const int16_t* __restrict__ pat,
                                                    const int32_t* __restrict__ xrp,
                                                    const int32_t* __restrict__ xcol,
                                                    const typename SellStore<VI>::type* __restrict__ xval,
@@ -662,8 +662,8 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
     for (int p = 0; p < SPW; ++p) {
         live_p[p] = s0 + p < nslices;
         const int sp = live_p[p] ? s0 + p : 0;
-        if constexpr (UNI) row[p].init_uniform(sp, ustride, spat);
-        else row[p].init_load(sp, off, spat);
+        if constexpr (UNI) row[p].init_uniform(sp, ustride, spat, coff);
+        else row[p].init_load(sp, off, spat, coff);
     }
     __builtin_amdgcn_sched_barrier(0);
     // 1. the fold's ||w||^2 partial (one per lane, as k_step_sell)
@@ -1555,10 +1555,14 @@ int64_t mpg_arnoldi_sell_matrix_bytes(mpg_arnoldi_t a) {
     // shared patterns are a few cache lines); int64 slice offsets; the
     // pattern indices; the stepped form's bases; a scaled fp16 copy's row
     // exponents
-    return S.padded * vbytes + (S.padded - S.imp_slots) * S.col_bytes() + S.npat * S.col_bytes() +
+    // (shared column blocks: the distinct blocks once, plus the per-slice
+    // column starts)
+    return S.padded * vbytes + S.col_slots * S.col_bytes() + S.npat * S.col_bytes() +
            ((int64_t)S.nslices + 1) * 8 + (S.spat ? (int64_t)S.nslices * 4 : 0) + (S.c16s ? steps * S.W * 4 : 0) +
-           (a->d.inner_row_exp ? (int64_t)a->d.n : 0);
+           (S.coff ? (int64_t)S.nslices * 8 : 0) + (a->d.inner_row_exp ? (int64_t)a->d.n : 0);
 }
+
+int64_t mpg_arnoldi_sell_shared_slices(mpg_arnoldi_t a) { return a ? a->sell.nshared : -1; }
 
 int mpg_arnoldi_slices_per_wave(mpg_arnoldi_t a) {
     if (!a || a->sell.nslices == 0) return 0;
@@ -1619,7 +1623,7 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
                             a->d.n, -a->front, a->d.n_ext, S->nslices, S->off, static_cast<const CI*>(S->col),
                             static_cast<const X*>(S->val), static_cast<const X*>(a->d.x),
                             static_cast<const X*>(a->d.b), diag, static_cast<T*>(a->w[0]), a->partial, S->sbase,
-                            S->spat, static_cast<const CI*>(S->pat), S->xrp, S->xcol, static_cast<const X*>(S->xval),
+                            S->spat, S->coff, static_cast<const CI*>(S->pat), S->xrp, S->xcol, static_cast<const X*>(S->xval),
                             S->ustride, sell_xcd_order(*S) ? 1 : 0);
                         return (int)MPG_OK;
                     };
@@ -1721,7 +1725,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
                             static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd,
-                            S.sbase, S.spat, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
+                            S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
                             static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
                             S.ustride, sell_xcd_order(S) ? 1 : 0);
                     return (int)MPG_OK;
@@ -1752,7 +1756,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                                     static_cast<const typename SellStore<VI>::type*>(S.val),
                                     static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
                                     static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf,
-                                    SellDots{}, S.sbase, S.spat, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
+                                    SellDots{}, S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
                                     static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
                                     S.ustride, sell_xcd_order(S) ? 1 : 0);
                             return (int)MPG_OK;

@@ -124,6 +124,64 @@ __global__ void k_sell_fill(int n, int nslices, const int32_t* __restrict__ rowp
     }
 }
 
+// Shared column blocks: slices whose stored column blocks are identical
+// (2-byte forms: offsets relative to the slice, so every interior slice of
+// a stencil with the same boundary pattern has the same block) keep one copy.
+__device__ __forceinline__ uint64_t mix_bits(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+// per slice: XOR over its block of mix(position, value), and the length
+template <class CI>
+__global__ __launch_bounds__(kBlock) void k_sell_col_hash(int nslices, const int64_t* __restrict__ off,
+                                                          const CI* __restrict__ col, uint64_t* __restrict__ out) {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = (int)(t0 / kWave), lane = (int)(t0 % kWave);
+    if (s >= nslices) return;
+    const int64_t o = off[s], len = off[s + 1] - o;
+    uint64_t h = 0;
+    for (int64_t t = lane; t < len; t += kWave)
+        h ^= mix_bits(((uint64_t)t << 20) ^ (uint64_t)(uint16_t)col[o + t] ^ ((uint64_t)(uint32_t)col[o + t] << 40));
+    for (int m = kWave / 2; m > 0; m >>= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)h, m, kWave), hi = __shfl_xor((uint32_t)(h >> 32), m, kWave);
+        h ^= ((uint64_t)hi << 32) | lo;
+    }
+    if (lane == 0) out[s] = h ^ mix_bits((uint64_t)len);
+}
+
+// bad[s] = 1 where slice s's block differs from that of rep[s] (rep[s] >= 0, != s)
+template <class CI>
+__global__ __launch_bounds__(kBlock) void k_sell_col_verify(int nslices, const int64_t* __restrict__ off,
+                                                            const CI* __restrict__ col, const int32_t* __restrict__ rep,
+                                                            int* __restrict__ bad) {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = (int)(t0 / kWave), lane = (int)(t0 % kWave);
+    if (s >= nslices) return;
+    const int r = rep[s];
+    if (r < 0 || r == s) return;
+    const int64_t o = off[s], orr = off[r], len = off[s + 1] - o;
+    bool diff = len != off[r + 1] - orr;
+    for (int64_t t = lane; t < len && !diff; t += kWave) diff = col[o + t] != col[orr + t];
+    if (diff) bad[s] = 1;
+}
+
+// the stored blocks into their compacted places (newoff[s] < 0: not stored)
+template <class CI>
+__global__ __launch_bounds__(kBlock) void k_sell_col_gather(int nslices, const int64_t* __restrict__ off,
+                                                            const CI* __restrict__ col,
+                                                            const int64_t* __restrict__ newoff, CI* __restrict__ out) {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = (int)(t0 / kWave), lane = (int)(t0 % kWave);
+    if (s >= nslices) return;
+    const int64_t d = newoff[s];
+    if (d < 0) return;
+    const int64_t o = off[s], len = off[s + 1] - o;
+    for (int64_t t = lane; t < len; t += kWave) out[d + t] = col[o + t];
+}
+
 template <class F>
 int with_store(int vtype, F&& f) {
     switch (vtype) {
@@ -144,7 +202,7 @@ template <class X, class S, class CI, int W, bool WIN, bool UNI = false>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col, const S* __restrict__ val,
                                                       const int32_t* __restrict__ sbase,
-                                                      const int32_t* __restrict__ spat, const CI* __restrict__ pat,
+                                                      const int32_t* __restrict__ spat, const int64_t* __restrict__ coff, const CI* __restrict__ pat,
                                                       const int32_t* __restrict__ xrp,
                                                       const int32_t* __restrict__ xcol, const S* __restrict__ xval,
                                                       const X* __restrict__ x, X alpha, X beta, X* __restrict__ y,
@@ -169,8 +227,8 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
     const int row0 = s * kWave;
     const int i = row0 + lane;
     SellRow<S, CI, W> row;
-    if constexpr (UNI) row.init_uniform(s, ustride, spat);
-    else row.init_load(s, off, spat);
+    if constexpr (UNI) row.init_uniform(s, ustride, spat, coff);
+    else row.init_load(s, off, spat, coff);
     __builtin_amdgcn_sched_barrier(0);
     X xr[WIN ? NQ : 1];
     if constexpr (WIN) {
@@ -220,6 +278,9 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
 }  // namespace
 
 namespace mpg {
+
+int sell_share_columns(SellCopy& S, const std::vector<int64_t>& off, const std::vector<int32_t>& spat_h, int grid,
+                       hipStream_t stream);
 
 int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int format, SellCopy& S) {
     S = SellCopy{};
@@ -451,9 +512,105 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
                      hipSuccess)
             st = MPG_ERR_HIP;
     }
+    S.col_slots = best - S.imp_slots;
+    const char* shenv = std::getenv("MPG_SELL_SHARE");  // 0: every slice keeps its own column block
+    if (!st && (S.c16 || S.c16s) && !(shenv && *shenv == '0')) st = sell_share_columns(S, off, spat_h, grid, stream);
     if (!st && hipStreamSynchronize(stream) != hipSuccess) st = MPG_ERR_HIP;
     if (st) sell_free(S);
     return st;
+}
+
+// Shared column blocks (after the fill): hash every stored slice's block,
+// group equal (length, hash) pairs, verify each member against its group's
+// first slice on the device, and keep one block per group in a compacted
+// column array; coff[s] says where slice s reads its columns. Implicit
+// slices (pattern loads) store none. A slice summed from the sub-CSR keeps
+// a block of its own (its clamped loads still read one). Nothing changes
+// unless at least 1 % of the stored slices share.
+int sell_share_columns(SellCopy& S, const std::vector<int64_t>& off, const std::vector<int32_t>& spat_h, int grid,
+                       hipStream_t stream) {
+    const int ns = S.nslices;
+    uint64_t* hash_d = nullptr;
+    int32_t* rep_d = nullptr;
+    int* bad_d = nullptr;
+    int64_t* newoff_d = nullptr;
+    void* col2 = nullptr;
+    auto cleanup = [&](int st) {
+        for (void* p : {(void*)hash_d, (void*)rep_d, (void*)bad_d, (void*)newoff_d}) (void)(p ? hipFree(p) : hipSuccess);
+        if (st && col2) (void)hipFree(col2);
+        return st;
+    };
+    std::vector<uint64_t> hash((size_t)ns);
+    if (hipMalloc((void**)&hash_d, (size_t)ns * 8) != hipSuccess) return cleanup(MPG_ERR_ALLOC);
+    int st = sell_dispatch(S, [&](auto ci, auto) {
+        using CI = decltype(ci);
+        k_sell_col_hash<CI><<<grid, kBlock, 0, stream>>>(ns, S.off, static_cast<const CI*>(S.col), hash_d);
+        return (int)MPG_OK;
+    });
+    if (st || hipMemcpyAsync(hash.data(), hash_d, (size_t)ns * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+        return cleanup(st ? st : MPG_ERR_HIP);
+    std::vector<int32_t> rep((size_t)ns, -1);
+    std::map<std::pair<int64_t, uint64_t>, int32_t> first;
+    int64_t shared = 0, stored = 0;
+    for (int s2 = 0; s2 < ns; ++s2) {
+        if (!spat_h.empty() && spat_h[s2] >= 0) continue;  // implicit: no block
+        ++stored;
+        auto it = first.emplace(std::make_pair(off[s2 + 1] - off[s2], hash[s2]), s2).first;
+        rep[s2] = it->second;
+        shared += it->second != s2;
+    }
+    if (shared * 100 < stored || shared == 0) return cleanup(MPG_OK);
+    if (hipMalloc((void**)&rep_d, (size_t)ns * 4) != hipSuccess || hipMalloc((void**)&bad_d, (size_t)ns * 4) != hipSuccess)
+        return cleanup(MPG_ERR_ALLOC);
+    std::vector<int> bad((size_t)ns, 0);
+    if (hipMemcpyAsync(rep_d, rep.data(), (size_t)ns * 4, hipMemcpyHostToDevice, stream) != hipSuccess ||
+        hipMemsetAsync(bad_d, 0, (size_t)ns * 4, stream) != hipSuccess)
+        return cleanup(MPG_ERR_HIP);
+    st = sell_dispatch(S, [&](auto ci, auto) {
+        using CI = decltype(ci);
+        k_sell_col_verify<CI><<<grid, kBlock, 0, stream>>>(ns, S.off, static_cast<const CI*>(S.col), rep_d, bad_d);
+        return (int)MPG_OK;
+    });
+    if (st || hipMemcpyAsync(bad.data(), bad_d, (size_t)ns * 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+        return cleanup(st ? st : MPG_ERR_HIP);
+    for (int s2 = 0; s2 < ns; ++s2)
+        if (bad[s2]) rep[s2] = s2;  // a hash collision: its own block
+    std::vector<int64_t> newoff((size_t)ns, -1), coff((size_t)ns, 0);
+    int64_t total = 0;
+    shared = 0;
+    for (int s2 = 0; s2 < ns; ++s2)
+        if (rep[s2] == s2) {
+            newoff[s2] = total;
+            total += off[s2 + 1] - off[s2];
+        }
+    for (int s2 = 0; s2 < ns; ++s2)
+        if (rep[s2] >= 0) {
+            coff[s2] = newoff[rep[s2]];
+            shared += rep[s2] != s2;
+        }
+    if (shared * 100 < stored) return cleanup(MPG_OK);
+    const size_t cb = (size_t)S.col_bytes();
+    if (hipMalloc((void**)&newoff_d, (size_t)ns * 8) != hipSuccess || hipMalloc(&col2, (size_t)total * cb + 256) != hipSuccess ||
+        hipMalloc((void**)&S.coff, (size_t)ns * 8 + 256) != hipSuccess)
+        return cleanup(MPG_ERR_ALLOC);
+    if (hipMemcpyAsync(newoff_d, newoff.data(), (size_t)ns * 8, hipMemcpyHostToDevice, stream) != hipSuccess ||
+        hipMemcpyAsync(S.coff, coff.data(), (size_t)ns * 8, hipMemcpyHostToDevice, stream) != hipSuccess ||
+        hipMemsetAsync(col2, 0, (size_t)total * cb + 256, stream) != hipSuccess)
+        return cleanup(MPG_ERR_HIP);
+    st = sell_dispatch(S, [&](auto ci, auto) {
+        using CI = decltype(ci);
+        k_sell_col_gather<CI><<<grid, kBlock, 0, stream>>>(ns, S.off, static_cast<const CI*>(S.col), newoff_d,
+                                                          static_cast<CI*>(col2));
+        return (int)MPG_OK;
+    });
+    if (st || hipStreamSynchronize(stream) != hipSuccess) return cleanup(st ? st : MPG_ERR_HIP);
+    (void)hipFree(S.col);
+    S.col = col2;
+    S.nshared = shared;
+    S.col_slots = total;
+    return cleanup(MPG_OK);
 }
 
 void sell_free(SellCopy& S) {
@@ -466,6 +623,7 @@ void sell_free(SellCopy& S) {
     if (S.xrp) (void)hipFree(S.xrp);
     if (S.xcol) (void)hipFree(S.xcol);
     if (S.xval) (void)hipFree(S.xval);
+    if (S.coff) (void)hipFree(S.coff);
     S = SellCopy{};
 }
 
@@ -492,7 +650,7 @@ int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y,
             auto go = [&](auto kern) {
                 kern<<<grid, kBlock, 0, ctx->stream>>>(
                     S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val),
-                    S.sbase, S.spat, static_cast<const CI*>(S.pat), S.xrp, S.xcol, static_cast<const St*>(S.xval), x,
+                    S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol, static_cast<const St*>(S.xval), x,
                     alpha, beta, y, S.ustride, sell_xcd_order(S) ? 1 : 0, prog);
                 return (int)MPG_OK;
             };
@@ -546,6 +704,8 @@ int mpg_sell_layout(mpg_sell_t A, int32_t* vec_width, int32_t* col_bytes, int64_
     if (window) *window = A->S.win ? 1 : 0;
     return MPG_OK;
 }
+
+int64_t mpg_sell_shared_slices(mpg_sell_t A) { return A ? A->S.nshared : -1; }
 
 int mpg_sell_columns(mpg_sell_t A, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices) {
     if (!A) return MPG_ERR_ARG;

@@ -132,22 +132,28 @@ struct SellRow {
     const int32_t* __restrict__ bp;
 
     int64_t o0, o1;
+    int64_t co;  // where the slice's columns start: o0, or its shared block (coff)
     // the slice's offsets and pattern index: issue first (everything else
-    // needs them), use later
+    // needs them), use later. coff: per-slice column starts when slices
+    // with identical column blocks share one (SellCopy::coff), else nullptr
     __device__ __forceinline__ void init_load(int s, const int64_t* __restrict__ off,
-                                              const int32_t* __restrict__ spat = nullptr) {
+                                              const int32_t* __restrict__ spat = nullptr,
+                                              const int64_t* __restrict__ coff = nullptr) {
         o0 = off[s];
         o1 = off[s + 1];
         row0 = s * kWave;
         if (spat) pk = spat[s];
+        co = coff ? coff[s] : o0;
     }
     // every slice of the copy has the same width (SellCopy::ustride entries):
     // the offsets are computed, so the value loads need no load before them
-    __device__ __forceinline__ void init_uniform(int s, int64_t ustride, const int32_t* __restrict__ spat = nullptr) {
+    __device__ __forceinline__ void init_uniform(int s, int64_t ustride, const int32_t* __restrict__ spat = nullptr,
+                                                 const int64_t* __restrict__ coff = nullptr) {
         o0 = (int64_t)s * ustride;
         o1 = o0 + ustride;
         row0 = s * kWave;
         if (spat) pk = spat[s];
+        co = coff ? coff[s] : o0;
     }
     // sbase: the stepped form's (slice, step, element) bases; pat: the
     // implicit slices' column patterns (nullptr when the copy has none).
@@ -160,7 +166,7 @@ struct SellRow {
         const int64_t base = steps > 0 ? o0 + lane * W : 0;
         lane_row = row0 + lane;
         const bool imp = pk >= 0;
-        cp = imp ? pat + pk : col + base;
+        cp = imp ? pat + pk : col + (steps > 0 ? co + lane * W : 0);
         cstride = imp ? W : (int64_t)kWave * W;
         rbase = imp ? lane_row : SellCol<CI>::stored_base(row0);
         vp = val + base;
@@ -171,8 +177,9 @@ struct SellRow {
     __device__ __forceinline__ void init(int s, int lane, const int64_t* __restrict__ off, const CI* __restrict__ col,
                                          const S* __restrict__ val, const int32_t* __restrict__ sbase = nullptr,
                                          const int32_t* __restrict__ spat = nullptr,
-                                         const CI* __restrict__ pat = nullptr) {
-        init_load(s, off, spat);
+                                         const CI* __restrict__ pat = nullptr,
+                                         const int64_t* __restrict__ coff = nullptr) {
+        init_load(s, off, spat, coff);
         init_finish(lane, col, val, sbase, pat);
     }
     __device__ __forceinline__ void load(int q) {
@@ -269,6 +276,10 @@ struct SellCopy {
     int64_t imp_slots = 0;     // their slots (their columns are not read)
     int64_t npat = 0;          // pattern entries
     int64_t ustride = 0;       // > 0: every slice holds this many slots (off[s] = s * ustride)
+    int64_t* coff = nullptr;   // shared column blocks: per slice, where its columns start in col
+                               // (slices with identical int16 column blocks store one; nullptr: off)
+    int64_t nshared = 0;       // slices that read another slice's column block
+    int64_t col_slots = 0;     // column entries stored (after sharing; implicit slices store none)
     int col_bytes() const { return c16 || c16s ? 2 : 4; }
 };
 

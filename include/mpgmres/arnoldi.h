@@ -99,6 +99,8 @@ int mpg_arnoldi_sell_columns(mpg_arnoldi_t a, int32_t* form, int64_t* csr_slices
 /* slices per wave of the SELL Arnoldi SpMV kernel: 0 no SELL copy, 1
  * k_step_sell, 2 k_step_sell2 (uniform int16 copies; MPG_SELL_PAIR=0: 1) */
 int mpg_arnoldi_slices_per_wave(mpg_arnoldi_t a);
+/* slices of the SELL copy that read another slice's column block (mpg_sell_shared_slices) */
+int64_t mpg_arnoldi_sell_shared_slices(mpg_arnoldi_t a);
 
 int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
 int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);

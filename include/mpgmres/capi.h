@@ -300,6 +300,10 @@ int mpg_sell_layout(mpg_sell_t A, int32_t* vec_width, int32_t* col_bytes, int64_
  * *implicit_slices = slices whose rows share one column pattern (no columns
  * read; MPG_SELL_IMPLICIT=0 disables them). Pointers may be NULL. */
 int mpg_sell_columns(mpg_sell_t A, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices);
+/* slices of the copy that read another slice's column block: 2-byte column
+ * blocks are stored once per distinct block (the interior slices of a
+ * stencil with the same boundary pattern share one); -1 for NULL */
+int64_t mpg_sell_shared_slices(mpg_sell_t A);
 int mpg_sell_spmv_f64(mpg_ctx_t ctx, mpg_sell_t A, double alpha, const double* x, double beta, double* y);
 int mpg_sell_spmv_f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y);
 int mpg_sell_spmv_f16f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y);

@@ -259,3 +259,55 @@ def test_sell_copy_owns_its_flagged_rows(hip, mpg):
             hip.lib.mpg_sell_destroy(h)
         if csr is not None:
             hip.lib.mpg_csr_destroy(csr)
+
+
+@pytest.mark.parametrize("kind", ["lap", "wide", "stencil27"])
+def test_shared_column_blocks_same_bits(mpg, kind, monkeypatch):
+    """Slices whose 2-byte column blocks are identical keep one block
+    (SellCopy::coff): most slices of a stencil share. Every slice still
+    decodes with its own first row (and bases, stepped form), so the fused
+    solve gives the same bits as with every block stored (MPG_SELL_SHARE=0)."""
+    A = {"lap": lambda: mpg.gen_laplace3d(60), "wide": lambda: _wide(mpg),
+         "stencil27": lambda: mpg.gen_stencil27(105, 3, ny=105, nz=4)}[kind]()
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    got = {}
+    for sh in ("1", "0"):
+        monkeypatch.setenv("MPG_SELL_SHARE", sh)
+        for mode in ("mixed", "baseline"):
+            opts = dict(mode=mode, orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3, spmv_format="sell")
+            eng = mpg.Engine(A, b, xt, **opts)
+            shared = eng.sell_columns()["shared_slices"]
+            eng.close()
+            nslices = -(-A.nrows // 64)
+            assert (shared > nslices // 2) if sh == "1" else shared == 0, (kind, sh, shared, nslices)
+            got[sh, mode] = mpg.solve(A, b, xt, engine="fused", **opts)
+    for mode in ("mixed", "baseline"):
+        a, c = got["1", mode], got["0", mode]
+        assert a.total_iters == c.total_iters == 90
+        assert np.array_equal(a.step_res, c.step_res) and np.array_equal(a.x, c.x), mode
+
+
+def test_shared_column_blocks_surface_spmv(hip, mpg, monkeypatch):
+    """The stand-alone SELL SpMV (operator surface) on a copy with shared
+    column blocks: the CSR SpMV's bits (fp32 values)."""
+    import ctypes as C
+
+    A = mpg.gen_laplace3d(50)
+    n = A.nrows
+    x = np.random.default_rng(2).uniform(-1, 1, n).astype(np.float32)
+    drp, dci = hip.buf(A.rowptr), hip.buf(A.col)
+    csr, sell = C.c_void_p(), C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, n, n, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    try:
+        dv = hip.buf(A.val.astype(np.float32))
+        hip.check(hip.lib.mpg_sell_create(hip.ctx, csr, 1, dv.p, 0, C.byref(sell)))
+        assert hip.lib.mpg_sell_shared_slices(sell) > (n // 64) // 2
+        dx, y1, y2 = hip.buf(x), hip.buf(n, np.float32), hip.buf(n, np.float32)
+        hip.call("mpg_sell_spmv_f32", sell, C.c_float(1.0), dx.p, C.c_float(0.0), y1.p)
+        hip.call("mpg_csr_spmv_f32", csr, C.c_float(1.0), dv.p, dx.p, C.c_float(0.0), y2.p)
+        assert np.array_equal(y1.get(), y2.get())
+    finally:
+        if sell.value:
+            hip.lib.mpg_sell_destroy(sell)
+        hip.lib.mpg_csr_destroy(csr)
