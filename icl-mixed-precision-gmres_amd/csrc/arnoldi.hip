@@ -630,7 +630,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
 // the window). Past the Infinity Cache a slice's loads alone do not keep
 // enough bytes in flight per CU (MI355X_MICROARCH.md: ~72 KiB per CU hides
 // an HBM miss). Same sums in the same order as k_step_sell: same bits.
-template <class T, class P, class VI, int W, bool WIN, bool FOLD, int BE, int BS = kBlock>
+template <class T, class P, class VI, int W, bool WIN, bool FOLD, int BE, int BS = kBlock, bool PG = true>
 __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                    const int16_t* __restrict__ col,
                                                    const typename SellStore<VI>::type* __restrict__ val,
@@ -728,6 +728,18 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
         }
     }
     __builtin_amdgcn_sched_barrier(0);
+    // 5. PG, no window: the first batch's gathers of w_prev, raw, issued
+    // before the scale is known (the fold's sums and barriers), and scaled
+    // at the sum: (T)(w_prev * inv), the same operation, the same bits.
+    // A dead wave gathers for slice 0 (valid addresses) and returns.
+    constexpr bool PRE = PG && !WIN;
+    using RowT = SellRow<S, CI, W, (MPG_SELL_NT != 0), BE>;
+    T xr[PRE ? SPW : 1][PRE ? RowT::U : 1][PRE ? W : 1];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int p = 0; p < SPW; ++p) row[p].gather([&](int c) { return wprev[c]; }, xr[p]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     T inv;
     double nrm2sq = 0.0;
     if constexpr (FOLD) {
@@ -784,7 +796,8 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
                 if (SellCol<CI>::stepped && row[p].exc) {
                     sum[p] = csr_row_sum(live_p[p] && i < n ? row[p].xrow : -1, xrp, xcol, xval, xv);
                 } else {
-                    row[p].sum(0, xv, sum[p]);
+                    if constexpr (PRE) row[p].sum_gathered(0, xr[p], [&](T r) { return (double)(T)(r * inv); }, sum[p]);
+                    else row[p].sum(0, xv, sum[p]);
                     for (int q = row[p].U; q < row[p].steps; q += row[p].U) {
                         row[p].load(q);
                         row[p].sum(q, xv, sum[p]);
@@ -1761,6 +1774,14 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                                     S.ustride, sell_xcd_order(S) ? 1 : 0);
                             return (int)MPG_OK;
                         };
+                        const char* pge = std::getenv("MPG_SELL_PREGATHER");
+                        if (!WN && pge && *pge == '0') {
+                            if (be == 8)
+                                return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 8, kStepSellBlock, false>)
+                                            : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 8, kStepSellBlock, false>);
+                            return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 12, kStepSellBlock, false>)
+                                        : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 12, kStepSellBlock, false>);
+                        }
                         if (be == 8)
                             return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 8, kStepSellBlock>)
                                         : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 8, kStepSellBlock>);

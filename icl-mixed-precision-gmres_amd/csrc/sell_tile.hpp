@@ -217,12 +217,11 @@ struct SellRow {
             VecW<CI, W, NT>::load(cp + (int64_t)qq * cstride, c[u]);
         }
     }
-    // acc += the batch loaded at step q, in CSR order. Every gather is issued
-    // (padding and steps past the width read x at row0, a valid index) and
-    // masked at the sum, so the gathers of a batch are in flight together.
-    template <class XF>
-    __device__ __forceinline__ void sum(int q, XF xval, double& acc) const {
-        double x[U][W];
+    // The gathers of the loaded batch: every one is issued (padding and
+    // steps past the width read x at row0, a valid index) and masked at the
+    // sum, so the gathers of a batch are in flight together.
+    template <class XF, class X>
+    __device__ __forceinline__ void gather(XF xval, X (&x)[U][W]) const {
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -230,11 +229,24 @@ struct SellRow {
                 x[u][e] = xval(SellCol<CI>::live(c[u][e])
                                    ? SellCol<CI>::decode(c[u][e], rbase, kStepped ? lane_row + bq[u][e] : 0)
                                    : row0);
+    }
+    // acc += the batch at step q with its gathered x, in CSR order; xs(x)
+    // is the fp64 operand (a kernel that gathers x raw, before the scale it
+    // is multiplied by is known, applies the scale here)
+    template <class X, class XS>
+    __device__ __forceinline__ void sum_gathered(int q, const X (&x)[U][W], XS xs, double& acc) const {
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int e = 0; e < W; ++e)
-                if (q + u < steps && SellCol<CI>::live(c[u][e])) acc += widen(v[u][e]) * x[u][e];
+                if (q + u < steps && SellCol<CI>::live(c[u][e])) acc += widen(v[u][e]) * xs(x[u][e]);
+    }
+    // acc += the batch loaded at step q, in CSR order
+    template <class XF>
+    __device__ __forceinline__ void sum(int q, XF xval, double& acc) const {
+        double x[U][W];
+        gather(xval, x);
+        sum_gathered(q, x, [](double a) { return a; }, acc);
     }
 };
 
