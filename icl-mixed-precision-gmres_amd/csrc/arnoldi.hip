@@ -1785,6 +1785,10 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                         if (be == 8)
                             return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 8, kStepSellBlock>)
                                         : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 8, kStepSellBlock>);
+                        if constexpr (Wc == 2) if (be == 10)
+                            return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 10, kStepSellBlock>)
+                                        : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 10, kStepSellBlock>);
+                        if (be != 12) return (int)MPG_ERR_UNSUPPORTED;
                         return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 12, kStepSellBlock>)
                                     : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 12, kStepSellBlock>);
                     }

@@ -333,7 +333,7 @@ inline bool sell_uniform(const SellCopy& S) {
 // two slices per wave in the Arnoldi SpMV (k_step_sell2): int16 columns,
 // uniform widths of at most 12 entries per lane in one batch, W 2 or 4
 // (banded matrices, 7-point stencils). Returns the batch size in entries
-// (8 or 12: the registers of one batch per slice), or 0 for one slice per
+// (8, 10 (W = 2) or 12: the registers of one batch per slice), or 0 for one slice per
 // wave (MPG_SELL_PAIR=0: never). In-cycle, Givens folded
 // (profiles/r03_spmv_pair_ab.jsonl, median of 5 interleaved): BAND-100M fp16
 // 94.5 -> 72.9 us, fp32 102.8 -> 92.2, BAND-10M 14.2 -> 12.9, LAP-1M fp32
@@ -342,7 +342,9 @@ inline int sell_pair(const SellCopy& S) {
     const char* e = std::getenv("MPG_SELL_PAIR");
     if ((e && *e == '0') || S.nslices < 2 || !S.c16 || S.ustride <= 0 || (S.W != 2 && S.W != 4)) return 0;
     const int64_t entries = S.ustride / kWave;  // per lane (row) of every slice
-    return entries <= 8 ? 8 : entries <= 12 ? 12 : 0;
+    if (entries <= 8) return 8;
+    if (entries <= 10 && S.W == 2) return 10;  // BAND's 10 entries: no wasted step, fewer registers
+    return entries <= 12 ? 12 : 0;
 }
 
 inline bool sell_xcd_order(const SellCopy& S) {
