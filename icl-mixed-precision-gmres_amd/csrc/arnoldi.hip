@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
                                                           const X* __restrict__ xval, int64_t ustride, int xcd) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
     const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (kBlock / kWave) + wid;
     const bool live = s < nslices;  // a dead wave still joins the partials' barrier
     const int row0 = s * kWave;
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
     using S = typename SellStore<VI>::type;
     constexpr int NQ = kWinLen / kWave;
     __shared__ T win[WIN ? BS / kWave : 1][WIN ? kWinLen : 1];
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
     const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid;
     const bool live = s < nslices;  // a dead wave still joins the fold's barriers
     const int row0 = s * kWave;
@@ -651,7 +651,7 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
     constexpr int WL = kWinLen + (SPW - 1) * kWave;  // the pair's window
     constexpr int NQ = WL / kWave;
     __shared__ T win[WIN ? BS / kWave : 1][WIN ? WL : 1];
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
     const int s0 = ((xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid) * SPW;
     const bool live = s0 < nslices;  // a dead wave still joins the fold's barriers
     bool live_p[SPW];

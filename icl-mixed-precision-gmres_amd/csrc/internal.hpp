@@ -93,6 +93,12 @@ inline int grid_for(int64_t n, int per_thread, int cap = 2048) {
     return (int)g;
 }
 
+// The wave's index in its workgroup, as a wave-uniform value: the compiler
+// does not know threadIdx.x / 64 is the same in every lane, and everything
+// derived from it (slice index, offsets, pattern index) would otherwise sit
+// in vector registers, one copy per lane.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave)); }
+
 // ---- wave / block reductions (wave64 shuffles, then LDS across waves) ----
 template <class T>
 __device__ __forceinline__ T wave_sum(T v) {

@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
                                                       int64_t ustride, int xcd, ScalarProgram prog) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
     // a scalar program riding in this launch: workgroup 0 (dispatched first,
     // so it runs under the slices instead of after them), its first wave
     int b = (int)blockIdx.x, G = (int)gridDim.x;
