@@ -313,3 +313,32 @@ def test_shared_column_blocks_surface_spmv(hip, mpg, monkeypatch):
         if sell.value:
             hip.lib.mpg_sell_destroy(sell)
         hip.lib.mpg_csr_destroy(csr)
+
+
+@pytest.mark.parametrize("kind,mode", [("lap", "mixed"), ("lap", "baseline"), ("band", "mixed"),
+                                       ("band", "mixed-half")])
+def test_sell_schedules_same_bits(mpg, kind, mode, monkeypatch):
+    """The SELL step kernel's schedules are the same sums in the same order:
+    two slices per wave (k_step_sell2, 8- or exact 10-entry batches) or one
+    (MPG_SELL_PAIR=0), computed or loaded slice offsets (MPG_SELL_UNIFORM),
+    the first batch gathered before or after the fold's scale is known
+    (MPG_SELL_PREGATHER). Every combination gives the fused solve's bits."""
+    # (n a multiple of 64: every slice as wide, so the pair kernel applies)
+    A = mpg.gen_laplace3d(48) if kind == "lap" else mpg.gen_band(200_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode=mode, orth="cgs", prec="identity", rlen=30, tol=0.0, max_restarts=3, spmv_format="sell")
+    runs = {}
+    for pair, uni, pg in (("1", "1", "1"), ("1", "1", "0"), ("0", "1", "1"), ("0", "0", "1")):
+        monkeypatch.setenv("MPG_SELL_PAIR", pair)
+        monkeypatch.setenv("MPG_SELL_UNIFORM", uni)
+        monkeypatch.setenv("MPG_SELL_PREGATHER", pg)
+        eng = mpg.Engine(A, b, xt, **opts)
+        lay = eng.spmv_layout()
+        eng.close()
+        assert lay["format"] == "sell" and lay["slices_per_wave"] == (2 if pair == "1" else 1), lay
+        runs[pair, uni, pg] = mpg.solve(A, b, xt, engine="fused", **opts)
+    ref = runs["1", "1", "1"]
+    assert ref.total_iters == 90
+    for key, r in runs.items():
+        assert np.array_equal(r.step_res, ref.step_res) and np.array_equal(r.x, ref.x), key
