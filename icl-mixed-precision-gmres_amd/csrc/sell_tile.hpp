@@ -174,6 +174,25 @@ struct SellRow {
         xrow = exc ? (-2 - pk) * kWave + lane : 0;
         if constexpr (kStepped) bp = sbase + (steps > 0 ? o0 / kWave : 0);  // (o0 / (64 W)) W
     }
+    // a second batch buffer over the same slice (software-pipelined loops):
+    // the slice geometry without the loaded registers (copying those would
+    // wait for their loads)
+    __device__ __forceinline__ void geom_from(const SellRow& o) {
+        steps = o.steps;
+        row0 = o.row0;
+        lane_row = o.lane_row;
+        rbase = o.rbase;
+        pk = o.pk;
+        exc = o.exc;
+        xrow = o.xrow;
+        cp = o.cp;
+        cstride = o.cstride;
+        vp = o.vp;
+        if constexpr (kStepped) bp = o.bp;
+        o0 = o.o0;
+        o1 = o.o1;
+        co = o.co;
+    }
     __device__ __forceinline__ void init(int s, int lane, const int64_t* __restrict__ off, const CI* __restrict__ col,
                                          const S* __restrict__ val, const int32_t* __restrict__ sbase = nullptr,
                                          const int32_t* __restrict__ spat = nullptr,
@@ -257,7 +276,28 @@ __device__ __forceinline__ double csr_row_sum(int i, const int32_t* __restrict__
                                               const int32_t* __restrict__ col, const S* __restrict__ val, XF xval) {
     double acc = 0.0;
     if (i < 0) return acc;
-    for (int j = rowptr[i], e = rowptr[i + 1]; j < e; ++j) acc += widen(val[j]) * xval(col[j]);
+    const int j0 = rowptr[i], e = rowptr[i + 1];
+    if (j0 >= e) return acc;
+    // batches of 8: the batch's (column, value) loads, then its gathers, are
+    // each in flight together (clamped to the row's last entry, masked at
+    // the sum), so a row costs two round trips per 8 entries, not per entry
+    constexpr int B = 8;
+    for (int j = j0; j < e; j += B) {
+        int c[B];
+        S v[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int jj = j + b < e ? j + b : e - 1;
+            c[b] = col[jj];
+            v[b] = val[jj];
+        }
+        double x[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) x[b] = xval(c[b]);
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (j + b < e) acc += widen(v[b]) * x[b];
+    }
     return acc;
 }
 
@@ -345,6 +385,26 @@ inline int sell_pair(const SellCopy& S) {
     if (entries <= 8) return 8;
     if (entries <= 10 && S.W == 2) return 10;  // BAND's 10 entries: no wasted step, fewer registers
     return entries <= 12 ? 12 : 0;
+}
+
+// software-pipelined batches in the one-slice-per-wave SpMV without the LDS
+// window (k_step_sell<..., PIPE>): stepped and int32 columns (wide stencils,
+// e.g. C4). MPG_SELL_PIPE=0/1 forces it off/on.
+inline bool sell_pipe(const SellCopy& S) {
+    const char* e = std::getenv("MPG_SELL_PIPE");
+    if (e && (*e == '0' || *e == '1')) return *e == '1';
+    return false;
+}
+
+// non-temporal slice loads in the Arnoldi SpMV (k_step_sell<..., NTV>,
+// k_step_sell2<..., NTV>) for a copy too large to stay in the 256 MB
+// Infinity Cache: its slices stream from HBM every step anyway, and
+// streaming them non-temporally leaves x, w and V resident.
+// MPG_SELL_NTS=0/1 forces it off/on.
+inline bool sell_nt_stream(const SellCopy& S) {
+    const char* e = std::getenv("MPG_SELL_NTS");
+    if (e && (*e == '0' || *e == '1')) return *e == '1';
+    return false;
 }
 
 inline bool sell_xcd_order(const SellCopy& S) {
