@@ -441,7 +441,7 @@ struct SellDots {
 };
 
 template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD, int DN = 0, int BS = kBlock,
-          bool UNI = false, bool PIPE = false, bool NTV = (MPG_SELL_NT != 0)>
+          bool UNI = false, bool PIPE = false>
 __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col,
                                                       const typename SellStore<VI>::type* __restrict__ val,
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
     const int row0 = s * kWave;
     const int i = row0 + lane;
     // 0. the slice's offsets (UNI: computed) and pattern index
-    SellRow<S, CI, W, NTV> row;
+    SellRow<S, CI, W> row;
     if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat, coff);
     else row.init_load(live ? s : 0, off, spat, coff);
     __builtin_amdgcn_sched_barrier(0);
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
                 // per batch instead of a load round trip then a gather round
                 // trip). x is gathered raw and scaled at the sum: the same
                 // (T)(w_prev * inv) operand, the same bits.
-                using Row = SellRow<S, CI, W, NTV>;
+                using Row = SellRow<S, CI, W>;
                 Row rb;
                 rb.geom_from(row);
                 auto xraw = [&](int c) { return wprev[c]; };
@@ -659,8 +659,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
 // the window). Past the Infinity Cache a slice's loads alone do not keep
 // enough bytes in flight per CU (MI355X_MICROARCH.md: ~72 KiB per CU hides
 // an HBM miss). Same sums in the same order as k_step_sell: same bits.
-template <class T, class P, class VI, int W, bool WIN, bool FOLD, int BE, int BS = kBlock, bool PG = true,
-          bool NTV = (MPG_SELL_NT != 0)>
+template <class T, class P, class VI, int W, bool WIN, bool FOLD, int BE, int BS = kBlock, bool PG = true>
 __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
                                                    const int16_t* __restrict__ col,
                                                    const typename SellStore<VI>::type* __restrict__ val,
@@ -687,7 +686,7 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
     bool live_p[SPW];
     const int row0 = s0 * kWave;
     // 0. both slices' offsets (UNI: computed) and pattern indices
-    SellRow<S, CI, W, NTV, BE> row[SPW];
+    SellRow<S, CI, W, (MPG_SELL_NT != 0), BE> row[SPW];
 #pragma unroll
     for (int p = 0; p < SPW; ++p) {
         live_p[p] = s0 + p < nslices;
@@ -763,7 +762,7 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
     // at the sum: (T)(w_prev * inv), the same operation, the same bits.
     // A dead wave gathers for slice 0 (valid addresses) and returns.
     constexpr bool PRE = PG && !WIN;
-    using RowT = SellRow<S, CI, W, NTV, BE>;
+    using RowT = SellRow<S, CI, W, (MPG_SELL_NT != 0), BE>;
     T xr[PRE ? SPW : 1][PRE ? RowT::U : 1][PRE ? W : 1];
     if constexpr (PRE) {
 #pragma unroll
@@ -1812,14 +1811,6 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                             return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 12, kStepSellBlock, false>)
                                         : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 12, kStepSellBlock, false>);
                         }
-                        if (!fold && sell_nt_stream(S)) {
-                            // past the Infinity Cache (large copies run unfolded)
-                            if (be == 8) return launch2(k_step_sell2<T, P, VI, Wc, WN, false, 8, kStepSellBlock, true, true>);
-                            if constexpr (Wc == 2) if (be == 10)
-                                return launch2(k_step_sell2<T, P, VI, Wc, WN, false, 10, kStepSellBlock, true, true>);
-                            if (be != 12) return (int)MPG_ERR_UNSUPPORTED;
-                            return launch2(k_step_sell2<T, P, VI, Wc, WN, false, 12, kStepSellBlock, true, true>);
-                        }
                         if (be == 8)
                             return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 8, kStepSellBlock>)
                                         : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 8, kStepSellBlock>);
@@ -1831,17 +1822,15 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                                     : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 12, kStepSellBlock>);
                     }
                     if constexpr (!WN && !std::is_same_v<CI, int16_t>) if (sell_pipe(S)) {
-                        auto pick = [&](auto uni, auto nt) {
-                            constexpr bool UN = decltype(uni)::value, NT = decltype(nt)::value;
-                            return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock, UN, true, NT>,
-                                                 SellDots{}, BSC())
-                                        : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock, UN, true, NT>,
-                                                 SellDots{}, BSC());
-                        };
-                        const bool nts = sell_nt_stream(S);
                         if (sell_uniform(S))
-                            return nts ? pick(std::true_type(), std::true_type()) : pick(std::true_type(), std::false_type());
-                        return nts ? pick(std::false_type(), std::true_type()) : pick(std::false_type(), std::false_type());
+                            return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock, true, true>,
+                                                 SellDots{}, BSC())
+                                        : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock, true, true>,
+                                                 SellDots{}, BSC());
+                        return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock, false, true>,
+                                             SellDots{}, BSC())
+                                    : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock, false, true>,
+                                             SellDots{}, BSC());
                     }
                     if (sell_uniform(S))
                         return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock, true>,

@@ -281,6 +281,7 @@ __device__ __forceinline__ double csr_row_sum(int i, const int32_t* __restrict__
     // batches of 8: the batch's (column, value) loads, then its gathers, are
     // each in flight together (clamped to the row's last entry, masked at
     // the sum), so a row costs two round trips per 8 entries, not per entry
+    // (16 took C4's pipelined kernel from 71 to 100 VGPRs)
     constexpr int B = 8;
     for (int j = j0; j < e; j += B) {
         int c[B];
@@ -388,23 +389,14 @@ inline int sell_pair(const SellCopy& S) {
 }
 
 // software-pipelined batches in the one-slice-per-wave SpMV without the LDS
-// window (k_step_sell<..., PIPE>): stepped and int32 columns (wide stencils,
-// e.g. C4). MPG_SELL_PIPE=0/1 forces it off/on.
+// window (k_step_sell<..., PIPE>): on by default for stepped columns (C4
+// stand-in, in-cycle SpMV, interleaved: 314.5 -> 311.5 us, one wave per SIMD
+// less for one memory round trip per batch less), off for int32 columns
+// (unmeasured). MPG_SELL_PIPE=0/1 forces it off/on.
 inline bool sell_pipe(const SellCopy& S) {
     const char* e = std::getenv("MPG_SELL_PIPE");
     if (e && (*e == '0' || *e == '1')) return *e == '1';
-    return false;
-}
-
-// non-temporal slice loads in the Arnoldi SpMV (k_step_sell<..., NTV>,
-// k_step_sell2<..., NTV>) for a copy too large to stay in the 256 MB
-// Infinity Cache: its slices stream from HBM every step anyway, and
-// streaming them non-temporally leaves x, w and V resident.
-// MPG_SELL_NTS=0/1 forces it off/on.
-inline bool sell_nt_stream(const SellCopy& S) {
-    const char* e = std::getenv("MPG_SELL_NTS");
-    if (e && (*e == '0' || *e == '1')) return *e == '1';
-    return false;
+    return S.c16s;
 }
 
 inline bool sell_xcd_order(const SellCopy& S) {

@@ -364,25 +364,3 @@ def test_pipelined_batches_same_bits(mpg, stepped, mode, monkeypatch):
         p, q = got["1"], got["0"]
         assert p.total_iters == q.total_iters == 90
         assert np.array_equal(p.step_res, q.step_res) and np.array_equal(p.x, q.x)
-
-
-@pytest.mark.parametrize("mode", ["mixed", "mixed-half", "baseline"])
-def test_nontemporal_slices_same_bits(mpg, mode, monkeypatch):
-    """Non-temporal slice loads (MPG_SELL_NTS, the policy for copies past the
-    Infinity Cache) change only the cache policy: the same solve bits on the
-    paired kernel (banded: window, W = 2; 7-point: W = 4, no window; the
-    unfolded Givens step, as large copies run) and on the pipelined
-    one-slice kernel (stepped columns)."""
-    monkeypatch.setenv("MPG_FOLD_GIVENS", "0")
-    monkeypatch.setenv("MPG_SELL_PIPE", "1")
-    for A in (mpg.gen_band(300_000, 5, 4, seed=7), mpg.gen_laplace3d(40), _wide(mpg)):
-        xt = mpg.rand_vect(A.nrows, 42)
-        b = mpg.host_spmv(A, xt)
-        opts = dict(mode=mode, orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3)
-        got = {}
-        for nts in ("1", "0"):
-            monkeypatch.setenv("MPG_SELL_NTS", nts)
-            got[nts] = mpg.solve(A, b, xt, engine="fused", spmv_format="sell", **opts)
-        p, q = got["1"], got["0"]
-        assert p.total_iters == q.total_iters == 90
-        assert np.array_equal(p.step_res, q.step_res) and np.array_equal(p.x, q.x)
