@@ -5,6 +5,7 @@
 // partial per workgroup into the context workspace, stage 2: one workgroup
 // sums the partials in a fixed order and writes the result on device).
 #include "internal.hpp"
+#include "panel.hpp"
 #include "scalar_program.hpp"
 
 #include <algorithm>
@@ -26,6 +27,32 @@ __global__ __launch_bounds__(kBlock) void k_reduce_stage1(int64_t n, const T* __
         acc += SQUARE ? a * a : a * (double)y[i];
     }
     double s = block_sum<kBlock>(acc, scratch);
+    if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+// nrm2 stage 1 on a 16-B aligned vector: 4 rows per lane of 1024-lane
+// workgroups (quad_groups), the lane's rows in order, then the tail rows,
+// then block_sum<kQuadBlock> -- the layout and order in which the quad gemv
+// (k_gemv_n_quad<..., NORM>, blas2.hip) emits the ||y||^2 partials of the y
+// it writes, so both give the same partials for the same vector
+template <class T>
+__global__ __launch_bounds__(kQuadBlock) void k_nrm2_quad(int64_t n, const T* __restrict__ x,
+                                                          double* __restrict__ partial) {
+    __shared__ double scratch[kQuadBlock / kWave];
+    double acc = 0.0;
+    const int64_t n4 = n & ~int64_t(3);
+    const int64_t step = 4 * (int64_t)gridDim.x * kQuadBlock;
+    for (int64_t i = 4 * ((int64_t)blockIdx.x * kQuadBlock + threadIdx.x); i < n4; i += step) {
+        double v[4];
+        Row4<T>::load(x + i, v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc += v[r] * v[r];
+    }
+    for (int64_t i = n4 + (int64_t)blockIdx.x * kQuadBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kQuadBlock) {
+        const double a = (double)x[i];
+        acc += a * a;
+    }
+    const double s = block_sum<kQuadBlock>(acc, scratch);
     if (threadIdx.x == 0) partial[blockIdx.x] = s;
 }
 
@@ -69,6 +96,13 @@ __global__ __launch_bounds__(1024) void k_consume_partials(int nparts, const dou
 template <class T, bool SQUARE>
 int reduce_partials(mpg_ctx* ctx, int64_t n, const T* x, const T* y, int32_t* nparts) {
     if (!ctx || n < 0 || !nparts) return MPG_ERR_ARG;
+    if (SQUARE && n > 0 && (uintptr_t)x % 16 == 0) {
+        const int gq = quad_groups(n);
+        k_nrm2_quad<T><<<gq, kQuadBlock, 0, ctx->stream>>>(n, x, ctx->red_ws);
+        MPG_LAUNCH_CHECK(ctx);
+        *nparts = gq;
+        return MPG_OK;
+    }
     const int g = grid_for(n, 4, kMaxRedBlocks);
     k_reduce_stage1<T, SQUARE><<<g, kBlock, 0, ctx->stream>>>(n, x, y, ctx->red_ws);
     MPG_LAUNCH_CHECK(ctx);

@@ -133,8 +133,6 @@ __device__ __forceinline__ double column_sum(const double* __restrict__ partial,
     return wave_sum(v);
 }
 
-constexpr int kQuadBlock = 1024;
-constexpr int kQuadGroups = 256;
 
 // partial <A(:,c), x> per workgroup, 4 rows per lane (16-B loads)
 template <class T, int NC>
@@ -175,13 +173,19 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_t_quad(int64_t rows, const 
 // in `partial` (x = alpha_t * T(sum), beta_t = 0): every workgroup forms the
 // coefficients itself with stage 2's column_sum and workgroup 0 stores them
 // to x, saving the stage-2 launch (CGS: h = V^T w, then w -= V h).
-template <class T, int NC, bool FROM_PARTS = false>
+// NORM: also the ||y||^2 stage-1 partials of the y it writes, in the quad
+// nrm2 stage 1's layout and order (k_nrm2_quad, blas1.hip: the lane's rows
+// in order, then block_sum<kQuadBlock>), so an nrm2(y) right after needs no
+// launch of its own (CGS: w -= V h, then h_{k+1,k} = ||w||)
+template <class T, int NC, bool FROM_PARTS = false, bool NORM = false>
 __global__ __launch_bounds__(kQuadBlock) void k_gemv_n_quad(int64_t rows, T alpha, const T* __restrict__ A,
                                                             int64_t lda, T* __restrict__ x, T beta,
                                                             T* __restrict__ y, const double* __restrict__ partial = nullptr,
-                                                            int nparts = 0, T alpha_t = T(1)) {
+                                                            int nparts = 0, T alpha_t = T(1),
+                                                            double* __restrict__ norm_part = nullptr) {
     constexpr int B = kColBatch<T>;
     __shared__ double xs[NC];
+    double nacc = 0.0;
     if constexpr (FROM_PARTS) {
         const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
         for (int c = wid; c < NC; c += kQuadBlock / kWave) {
@@ -221,13 +225,30 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_n_quad(int64_t rows, T alph
 #pragma unroll
         for (int r = 0; r < 4; ++r) out[r] = beta == T(0) ? alpha * (T)t[r] : alpha * (T)t[r] + beta * (T)yr[r];
         Row4<T>::store(y + i, out);
+        if constexpr (NORM) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double a = (double)out[r];
+                nacc += a * a;
+            }
+        }
     }
     for (int64_t i = n4 + (int64_t)blockIdx.x * kQuadBlock + threadIdx.x; i < rows; i += (int64_t)gridDim.x * kQuadBlock) {
         double t = 0.0;
 #pragma unroll
         for (int c = 0; c < NC; ++c) t += (double)A[(int64_t)c * lda + i] * xs[c];
         const T tt = (T)t;
-        y[i] = beta == T(0) ? alpha * tt : alpha * tt + beta * y[i];
+        const T yi = beta == T(0) ? alpha * tt : alpha * tt + beta * y[i];
+        y[i] = yi;
+        if constexpr (NORM) {
+            const double a = (double)yi;
+            nacc += a * a;
+        }
+    }
+    if constexpr (NORM) {
+        __shared__ double scratch[kQuadBlock / kWave];
+        const double s = block_sum<kQuadBlock>(nacc, scratch);
+        if (threadIdx.x == 0) norm_part[blockIdx.x] = s;
     }
 }
 
@@ -336,9 +357,11 @@ int gemv_t_partials(mpg_ctx* ctx, int64_t rows, int64_t cols, const T* A, int64_
                        : grid_for(rows, 4, kMaxRedBlocks);
     const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto ncc) {
         if (quad)
-            k_gemv_t_quad<T, decltype(ncc)::value><<<g, kQuadBlock, 0, ctx->stream>>>(rows, A, lda, x, ctx->red_ws);
+            k_gemv_t_quad<T, decltype(ncc)::value><<<g, kQuadBlock, 0, ctx->stream>>>(rows, A, lda, x,
+                                                                                    ctx->red_ws + kWsGemvSplit);
         else
-            k_gemv_t_nc<T, decltype(ncc)::value><<<g, kBlock, 0, ctx->stream>>>(rows, A, lda, x, ctx->red_ws);
+            k_gemv_t_nc<T, decltype(ncc)::value><<<g, kBlock, 0, ctx->stream>>>(rows, A, lda, x,
+                                                                               ctx->red_ws + kWsGemvSplit);
         return (int)MPG_OK;
     });
     if (st) return st;
@@ -350,7 +373,7 @@ int gemv_t_partials(mpg_ctx* ctx, int64_t rows, int64_t cols, const T* A, int64_
 template <class T>
 int gemv_t_finish(mpg_ctx* ctx, int32_t nparts, int64_t cols, T alpha, T beta, T* y) {
     if (!ctx || nparts < 1 || cols < 1 || cols > kGemvMaxCols) return MPG_ERR_ARG;
-    k_gemv_t_stage2<T><<<1, 1024, 0, ctx->stream>>>(nparts, (int)cols, ctx->red_ws, alpha, beta, y);
+    k_gemv_t_stage2<T><<<1, 1024, 0, ctx->stream>>>(nparts, (int)cols, ctx->red_ws + kWsGemvSplit, alpha, beta, y);
     MPG_LAUNCH_CHECK(ctx);
     return MPG_OK;
 }
@@ -359,17 +382,24 @@ int gemv_t_finish(mpg_ctx* ctx, int32_t nparts, int64_t cols, T alpha, T beta, T
 // MPG_ERR_UNSUPPORTED unless A, lda and y allow the quad form
 template <class T>
 int gemv_n_from_t(mpg_ctx* ctx, int64_t rows, int64_t cols, T alpha, const T* A, int64_t lda, int32_t nparts,
-                  T alpha_t, T* x, T beta, T* y) {
+                  T alpha_t, T* x, T beta, T* y, int32_t* norm_nparts = nullptr) {
     if (!ctx || rows < 0 || cols < 1 || nparts < 1 || (rows > 0 && lda < rows)) return MPG_ERR_ARG;
     if (cols > kGemvMaxCols || !quad_aligned(A, lda, y)) return MPG_ERR_UNSUPPORTED;
-    const int g = (int)std::max<int64_t>(1, std::min<int64_t>(kQuadGroups, (rows + 4 * kQuadBlock - 1) / (4 * kQuadBlock)));
+    if (norm_nparts && rows < 1) return MPG_ERR_UNSUPPORTED;
+    const int g = quad_groups(rows);
     const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto nc) {
-        k_gemv_n_quad<T, decltype(nc)::value, true><<<g, kQuadBlock, 0, ctx->stream>>>(
-            rows, alpha, A, lda, x, beta, y, ctx->red_ws, nparts, alpha_t);
+        // the coefficients' partials sit apart from the ||y||^2 partials (kWsGemvSplit)
+        if (norm_nparts)
+            k_gemv_n_quad<T, decltype(nc)::value, true, true><<<g, kQuadBlock, 0, ctx->stream>>>(
+                rows, alpha, A, lda, x, beta, y, ctx->red_ws + kWsGemvSplit, nparts, alpha_t, ctx->red_ws);
+        else
+            k_gemv_n_quad<T, decltype(nc)::value, true><<<g, kQuadBlock, 0, ctx->stream>>>(
+                rows, alpha, A, lda, x, beta, y, ctx->red_ws + kWsGemvSplit, nparts, alpha_t);
         return (int)MPG_OK;
     });
     if (st) return st;
     MPG_LAUNCH_CHECK(ctx);
+    if (norm_nparts) *norm_nparts = g;
     return MPG_OK;
 }
 
@@ -468,6 +498,16 @@ int mpg_gemv_n_from_t_f64(mpg_ctx_t c, int64_t rows, int64_t cols, double alpha,
 int mpg_gemv_n_from_t_f32(mpg_ctx_t c, int64_t rows, int64_t cols, float alpha, const float* A, int64_t lda,
                           int32_t np, float alpha_t, float* x, float beta, float* y) {
     return gemv_n_from_t<float>(c, rows, cols, alpha, A, lda, np, alpha_t, x, beta, y);
+}
+int mpg_gemv_n_from_t_nrm2_f64(mpg_ctx_t c, int64_t rows, int64_t cols, double alpha, const double* A, int64_t lda,
+                               int32_t np, double alpha_t, double* x, double beta, double* y, int32_t* norm_np) {
+    if (!norm_np) return MPG_ERR_ARG;
+    return gemv_n_from_t<double>(c, rows, cols, alpha, A, lda, np, alpha_t, x, beta, y, norm_np);
+}
+int mpg_gemv_n_from_t_nrm2_f32(mpg_ctx_t c, int64_t rows, int64_t cols, float alpha, const float* A, int64_t lda,
+                               int32_t np, float alpha_t, float* x, float beta, float* y, int32_t* norm_np) {
+    if (!norm_np) return MPG_ERR_ARG;
+    return gemv_n_from_t<float>(c, rows, cols, alpha, A, lda, np, alpha_t, x, beta, y, norm_np);
 }
 int mpg_trsv_f64(mpg_ctx_t c, int upper, int trans, int64_t n, const double* A, int64_t lda, double* x) {
     return trsv_impl<double>(c, upper, trans, n, A, lda, x);

@@ -35,7 +35,7 @@ int mpg_ctx_create(int device, mpg_ctx_t* out) {
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) {
-        ctx->red_ws_elems = (size_t)mpg::kMaxRedBlocks * mpg::kGemvMaxCols + 64;
+        ctx->red_ws_elems = mpg::kWsElems;
         e = hipMalloc(&ctx->red_ws, ctx->red_ws_elems * sizeof(double));
     }
     if (e != hipSuccess) {

@@ -42,6 +42,20 @@ constexpr int kWave = 64;            // CDNA wavefront width (never 32)
 constexpr int kBlock = 256;          // default workgroup: 4 waves
 constexpr int kMaxRedBlocks = 1024;  // stage-1 grid cap for reductions
 constexpr int kGemvMaxCols = 32;     // columns per panel pass of gemv^T
+// context workspace (red_ws, doubles): [0, kMaxRedBlocks * kGemvMaxCols)
+// stage-1 partials of the one-call reductions and of nrm2 / dot; 64 scalars
+// after them; then the split gemv^T partials (mpg_gemv_t_partials_*), kept
+// apart so their consumer can write ||y||^2 partials while it reads them
+constexpr size_t kWsGemvSplit = (size_t)kMaxRedBlocks * kGemvMaxCols + 64;
+constexpr size_t kWsElems = kWsGemvSplit + (size_t)kMaxRedBlocks * kGemvMaxCols;
+// the quad form of the nrm2 stage 1 and of the gemv that can emit its
+// partials (4 rows per lane, 1024-lane workgroups, this many at most)
+constexpr int kQuadBlock = 1024;
+constexpr int kQuadGroups = 256;
+inline int quad_groups(int64_t rows) {
+    const int64_t g = (rows + 4 * kQuadBlock - 1) / (4 * kQuadBlock);
+    return (int)(g < 1 ? 1 : g > kQuadGroups ? kQuadGroups : g);
+}
 
 inline int set_hip_error(mpg_ctx* ctx, hipError_t e, const char* what) {
     if (ctx) {

@@ -126,8 +126,24 @@ struct PendingReduction {
 thread_local PendingReduction tl_red;
 
 // MPG_SURFACE_FUSE: a bit mask of the fused pairs (1 nrm2 -> scal_recip,
-// 2 dot -> naxpy, 4 gemv^T -> gemv); unset: kFuseDefault; 0: none
-constexpr int kFuseDefault = 1 | 4;
+// 2 dot -> naxpy, 4 gemv^T -> gemv, 8 gemv -> nrm2: the CGS update emits
+// the ||w||^2 partials that the nrm2 of add_vector would compute, below);
+// unset: kFuseDefault; 0: none
+constexpr int kFuseDefault = 1 | 4 | 8;
+
+// The ||y||^2 stage-1 partials a fused CGS gemv (mpg_gemv_n_from_t_nrm2_*)
+// left in the context workspace: an nrm2 of exactly that y as the very
+// next call takes them instead of launching its stage 1 (the same partials,
+// bit for bit). Every other call reaches the device through current_ctx()
+// (or queues a scalar op), which forgets them.
+struct NormMemo {
+    mpg_ctx_t ctx = nullptr;
+    const void* y = nullptr;
+    int64_t n = 0;
+    bool f64 = false;
+    int32_t nparts = 0;
+};
+thread_local NormMemo tl_norm;
 bool fuse_enabled(int bit) {
     const char* env = std::getenv("MPG_SURFACE_FUSE");
     const int mask = env && *env ? std::atoi(env) : kFuseDefault;
@@ -152,7 +168,32 @@ void flush_pending_reduction() {
     check(st, "reduction stage 2", r.ctx);
 }
 
-void discard_pending_reduction() { tl_red.kind = 0; }
+void discard_pending_reduction() {
+    tl_red.kind = 0;
+    tl_norm.y = nullptr;
+}
+
+// An elementwise call that writes none of the memo's y and runs no
+// reduction (CGSR's axpy(1, corr, h) between its last gemv and the nrm2)
+// keeps the memo: the partials in the workspace are still y's.
+struct KeepNormMemo {
+    NormMemo m;
+    KeepNormMemo(const void* out, size_t bytes) : m(tl_norm) {
+        const char* a = static_cast<const char*>(out);
+        const char* y = static_cast<const char*>(m.y);
+        if (m.y && a < y + m.n * (m.f64 ? 8 : 4) && y < a + bytes) m.y = nullptr;
+    }
+    void done() const { tl_norm = m; }
+};
+
+// the memo of the ||y||^2 partials, taken (cleared) when it is exactly y's
+// on the current context and nothing is pending or queued; its nparts, or 0
+static int32_t take_norm_memo(const void* y, int64_t n, bool f64) {
+    const NormMemo m = tl_norm;
+    tl_norm.y = nullptr;
+    if (!m.y || m.y != y || m.n != n || m.f64 != f64 || m.ctx != tl_ctx || tl_red.kind || tl_nops) return 0;
+    return m.nparts;
+}
 
 // the pending reduction of `kind` whose result is `result`, taken (cleared)
 // when the caller will consume it; nullptr otherwise
@@ -175,6 +216,7 @@ void discard_scalar_ops() { tl_nops = 0; }
 
 // true when queued (the caller issues the op itself otherwise)
 bool queue_scalar_op(const mpg_scalar_op& op) {
+    tl_norm.y = nullptr;
     if (!batch_enabled()) return false;
     if (tl_red.kind) flush_pending_reduction();
     mpg_ctx_t c = ctx_no_flush();
@@ -219,12 +261,14 @@ mpg_ctx_t take_scalar_ops_for(const void* x, size_t xbytes, const void* y, size_
 }
 
 mpg_ctx_t current_ctx() {
+    tl_norm.y = nullptr;
     if (tl_nops) flush_scalar_ops();
     if (tl_red.kind) flush_pending_reduction();
     return ctx_no_flush();
 }
 
 ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) {
+    tl_norm.y = nullptr;
     if (tl_nops) flush_scalar_ops();
     if (tl_red.kind) flush_pending_reduction();
     tl_ctx = ctx;
@@ -383,6 +427,11 @@ template <> float nrm2<float, Hip>(Vect<float, Hip> x) {
 }
 template <> void nrm2<double, Hip>(Vect<double, Hip> x, Scalar<double, Hip> r) {
     if (mpg::fuse_enabled(1) && x.n() > 0) {
+        if (const int32_t np = mpg::take_norm_memo(x.data(), (int64_t)x.n(), true)) {
+            // the partials the CGS gemv just emitted for this x: no stage 1
+            mpg::tl_red = mpg::PendingReduction{1, true, mpg::tl_ctx, np, r.data()};
+            return;
+        }
         mpg_ctx_t c = C;
         int32_t np = 0;
         check(mpg_nrm2_partials_f64(c, x.n(), x.data(), &np), "nrm2");
@@ -393,6 +442,11 @@ template <> void nrm2<double, Hip>(Vect<double, Hip> x, Scalar<double, Hip> r) {
 }
 template <> void nrm2<float, Hip>(Vect<float, Hip> x, Scalar<float, Hip> r) {
     if (mpg::fuse_enabled(1) && x.n() > 0) {
+        if (const int32_t np = mpg::take_norm_memo(x.data(), (int64_t)x.n(), false)) {
+            // the partials the CGS gemv just emitted for this x: no stage 1
+            mpg::tl_red = mpg::PendingReduction{1, false, mpg::tl_ctx, np, r.data()};
+            return;
+        }
         mpg_ctx_t c = C;
         int32_t np = 0;
         check(mpg_nrm2_partials_f32(c, x.n(), x.data(), &np), "nrm2");
@@ -405,11 +459,15 @@ template <> void nrm2<float, Hip>(Vect<float, Hip> x, Scalar<float, Hip> r) {
 // ---------------- axpy ----------------
 template <> void axpy<double, Hip>(double a, Vect<double, Hip> x, Vect<double, Hip> y) {
     assert(x.n() == y.n());
+    const mpg::KeepNormMemo keep(y.data(), y.n() * sizeof(double));
     check(mpg_axpy_f64(C, x.n(), a, x.data(), y.data()), "axpy");
+    keep.done();
 }
 template <> void axpy<float, Hip>(float a, Vect<float, Hip> x, Vect<float, Hip> y) {
     assert(x.n() == y.n());
+    const mpg::KeepNormMemo keep(y.data(), y.n() * sizeof(float));
     check(mpg_axpy_f32(C, x.n(), a, x.data(), y.data()), "axpy");
+    keep.done();
 }
 template <> void axpy<double, Hip>(Scalar<double, Hip> a, Vect<double, Hip> x, Vect<double, Hip> y) {
     assert(x.n() == y.n());
@@ -552,11 +610,19 @@ template <> void gemv<double, Hip>(double alpha, MultiVect<double, Hip> A, Vect<
     }
     if (!A.transposed()) {
         if (const auto* p = mpg::take_pending(3, true, x.data())) {
-            const int st = p->cols == (int64_t)x.n()
-                               ? mpg_gemv_n_from_t_f64(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
-                                                        A.stride(), p->nparts, (double)p->alpha, x.data(), beta, y.data())
-                               : MPG_ERR_UNSUPPORTED;
-            if (st == MPG_OK) return;
+            const bool emit = mpg::fuse_enabled(8) && mpg::fuse_enabled(1) && y.n() > 0;
+            int32_t nnp = 0;
+            const int st = p->cols != (int64_t)x.n() ? MPG_ERR_UNSUPPORTED
+                           : emit ? mpg_gemv_n_from_t_nrm2_f64(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
+                                                                 A.stride(), p->nparts, (double)p->alpha, x.data(), beta,
+                                                                 y.data(), &nnp)
+                                  : mpg_gemv_n_from_t_f64(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
+                                                            A.stride(), p->nparts, (double)p->alpha, x.data(), beta, y.data());
+            if (st == MPG_OK) {
+                if (emit && A.nrows_base() == (int64_t)y.n())
+                    mpg::tl_norm = mpg::NormMemo{p->ctx, y.data(), (int64_t)y.n(), true, nnp};
+                return;
+            }
             if (st != MPG_ERR_UNSUPPORTED) check(st, "gemv (gemv^T)", p->ctx);
             mpg::tl_red = *p;  // not fusable here: issue its stage 2 first (below, through C)
         }
@@ -581,11 +647,19 @@ template <> void gemv<float, Hip>(float alpha, MultiVect<float, Hip> A, Vect<flo
     }
     if (!A.transposed()) {
         if (const auto* p = mpg::take_pending(3, false, x.data())) {
-            const int st = p->cols == (int64_t)x.n()
-                               ? mpg_gemv_n_from_t_f32(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
-                                                        A.stride(), p->nparts, (float)p->alpha, x.data(), beta, y.data())
-                               : MPG_ERR_UNSUPPORTED;
-            if (st == MPG_OK) return;
+            const bool emit = mpg::fuse_enabled(8) && mpg::fuse_enabled(1) && y.n() > 0;
+            int32_t nnp = 0;
+            const int st = p->cols != (int64_t)x.n() ? MPG_ERR_UNSUPPORTED
+                           : emit ? mpg_gemv_n_from_t_nrm2_f32(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
+                                                                 A.stride(), p->nparts, (float)p->alpha, x.data(), beta,
+                                                                 y.data(), &nnp)
+                                  : mpg_gemv_n_from_t_f32(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
+                                                            A.stride(), p->nparts, (float)p->alpha, x.data(), beta, y.data());
+            if (st == MPG_OK) {
+                if (emit && A.nrows_base() == (int64_t)y.n())
+                    mpg::tl_norm = mpg::NormMemo{p->ctx, y.data(), (int64_t)y.n(), false, nnp};
+                return;
+            }
             if (st != MPG_ERR_UNSUPPORTED) check(st, "gemv (gemv^T)", p->ctx);
             mpg::tl_red = *p;  // not fusable here: issue its stage 2 first (below, through C)
         }

@@ -235,6 +235,16 @@ int mpg_gemv_n_from_t_f64(mpg_ctx_t ctx, int64_t rows, int64_t cols, double alph
                           int32_t nparts, double alpha_t, double* x, double beta, double* y);
 int mpg_gemv_n_from_t_f32(mpg_ctx_t ctx, int64_t rows, int64_t cols, float alpha, const float* A, int64_t lda,
                           int32_t nparts, float alpha_t, float* x, float beta, float* y);
+/* the same, and also the ||y||^2 partials of the y it wrote, exactly as
+ * mpg_nrm2_partials_* of that y would leave them (*norm_nparts of them, in the
+ * context workspace until the next reduction on ctx): the consumer of a
+ * following nrm2(y) (mpg_nrm2_finish_*, mpg_scal_recip_nrm2_*) needs no
+ * stage-1 launch (CGS: w -= V h, then h_{k+1,k} = ||w||, Orthogonalization.hpp:
+ * 51-89). MPG_ERR_UNSUPPORTED as above, or for rows < 1. */
+int mpg_gemv_n_from_t_nrm2_f64(mpg_ctx_t ctx, int64_t rows, int64_t cols, double alpha, const double* A, int64_t lda,
+                               int32_t nparts, double alpha_t, double* x, double beta, double* y, int32_t* norm_nparts);
+int mpg_gemv_n_from_t_nrm2_f32(mpg_ctx_t ctx, int64_t rows, int64_t cols, float alpha, const float* A, int64_t lda,
+                               int32_t nparts, float alpha_t, float* x, float beta, float* y, int32_t* norm_nparts);
 /* triangular solve, non-unit diagonal, single workgroup (n <= 4096).
  * upper = 1 'U', 0 'L'; trans = 1 solves with A^T (kernels_mkl.cpp:291-321) */
 int mpg_trsv_f64(mpg_ctx_t ctx, int upper, int trans, int64_t n, const double* A, int64_t lda, double* x);

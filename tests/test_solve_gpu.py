@@ -291,3 +291,25 @@ def test_fused_dots_strict(mpg, oracle, mode, orth, monkeypatch):
     got = mpg.solve(A, b, xt, engine="fused", spmv_format="sell", **opts)
     ref = oracle.solve(mpg, A, b, xt, **opts)
     compare(as_ref(ref), got, mode, opts["tol"], 30, f"fused-dots-strict-{mode}-{orth}")
+
+
+@pytest.mark.parametrize("orth", ["cgs", "cgsr"])
+@pytest.mark.parametrize("mode", ["mixed", "baseline"])
+def test_surface_gemv_emits_nrm2_partials_same_bits(mpg, orth, mode, monkeypatch):
+    """Operator surface, MPG_SURFACE_FUSE bit 8: the CGS update's gemv emits
+    the ||w||^2 stage-1 partials in the quad nrm2 layout, and add_vector's
+    nrm2(w) takes them instead of launching its stage 1 (CGSR: across the
+    axpy into h). The partials are the ones k_nrm2_quad computes, so the
+    solve bits are those of the unfused surface (bit 8 off), on a size with
+    tail rows and on one with several row quads per lane."""
+    for A in (mpg.gen_laplace3d(23), mpg.gen_band(1_200_003, 5, 4, seed=5)):
+        xt = mpg.rand_vect(A.nrows, 42)
+        b = mpg.host_spmv(A, xt)
+        opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=0.0, max_restarts=2)
+        got = {}
+        for fuse in ("13", "5"):
+            monkeypatch.setenv("MPG_SURFACE_FUSE", fuse)
+            got[fuse] = mpg.solve(A, b, xt, engine="surface", **opts)
+        p, q = got["13"], got["5"]
+        assert p.total_iters == q.total_iters == 60
+        assert np.array_equal(p.step_res, q.step_res) and np.array_equal(p.x, q.x), A.nrows
