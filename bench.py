@@ -341,7 +341,10 @@ def main():
                     "hbm_scale": hbm, "rank": 0,
                     "per_rank_avg_launch_ms": [round(t, 5) for t in per_rank_ms]}
         if world > 1:
-            roofline["kernel"] = sp["kernel"] + " (in-cycle, rank 0's row block; each step closes with its own Givens launch)"
+            roofline["kernel"] = sp["kernel"] + (" (in-cycle, rank 0's row block; Givens folded for k >= 1, its "
+                                                 "||w||^2 partials all-reduced with the halo)"
+                                                 if sp["layout"]["givens_folded"]
+                                                 else " (in-cycle, rank 0's row block; the Givens step has its own launch)")
             if shared_gpu:
                 roofline["note"] = "rehearsal: all ranks share GPU 0, so each rank's launches overlap the others'"
         if iter_bytes:
