@@ -256,6 +256,39 @@ __global__ __launch_bounds__(BS) void k_reduce_partials(int G, const double* __r
     if (threadIdx.x == 0) sums[blockIdx.x] = s;
 }
 
+// k_reduce_partials of the prologue's 3 columns + k_prologue_finish in one
+// workgroup (one GPU: nothing to all-reduce between them): each column is
+// summed by sum_partials<BS>, as its k_reduce_partials workgroup would, so
+// the sums and everything formed from them have the same bits
+template <class T, class X, int BS>
+__global__ __launch_bounds__(BS) void k_prologue_finish_parts(int G, const double* __restrict__ partial,
+                                                              double* __restrict__ sums, int m, T* __restrict__ s,
+                                                              T* __restrict__ inv, double* __restrict__ report) {
+    __shared__ double scratch[BS / kWave];
+    __shared__ double sm[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const double v = sum_partials<BS>(partial + (size_t)c * G, G, scratch);
+        if (threadIdx.x == 0) {
+            sm[c] = v;
+            sums[c] = v;
+        }
+    }
+    __syncthreads();
+    const T r_norm = (T)sqrt(sm[0]);
+    const T beta = (T)sqrt(sm[1]);
+    const X x_norm = (X)sqrt(sm[2]);
+    const T iv = beta != T(0) ? T(1) / beta : T(0);  // first_vector: zero fill when beta == 0
+    if (threadIdx.x == 0) {
+        report[0] = (double)r_norm;
+        report[1] = (double)beta;
+        report[2] = (double)x_norm;
+        report[3] = (double)iv;
+        *inv = iv;
+    }
+    for (int i = threadIdx.x; i <= m; i += blockDim.x) s[i] = i == 0 ? beta : T(0);
+}
+
 // ---------------------------------------------------------------- step: Givens
 #pragma clang fp contract(off)
 template <class T>
@@ -1710,6 +1743,24 @@ int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a) {
         using X = decltype(x);
         k_prologue_finish<T, X><<<1, 64, 0, a->ctx->stream>>>(a->sums, a->d.m, static_cast<T*>(a->s()),
                                                                 static_cast<T*>(a->inv()), a->report);
+        return MPG_OK;
+    });
+    if (st) return st;
+    MPG_LAUNCH_CHECK(a->ctx);
+    return MPG_OK;
+}
+
+int mpg_arnoldi_prologue_finish_partials(mpg_arnoldi_t a) {
+    if (!a) return MPG_ERR_ARG;
+    int st = dispatch(a->combo, [&](auto t, auto x, auto, auto) {
+        using T = decltype(t);
+        using X = decltype(x);
+        if (a->last_G <= 2 * kBlock)
+            k_prologue_finish_parts<T, X, kBlock><<<1, kBlock, 0, a->ctx->stream>>>(
+                a->last_G, a->last_part, a->sums, a->d.m, static_cast<T*>(a->s()), static_cast<T*>(a->inv()), a->report);
+        else
+            k_prologue_finish_parts<T, X, 1024><<<1, 1024, 0, a->ctx->stream>>>(
+                a->last_G, a->last_part, a->sums, a->d.m, static_cast<T*>(a->s()), static_cast<T*>(a->inv()), a->report);
         return MPG_OK;
     });
     if (st) return st;

@@ -416,8 +416,12 @@ void FusedEngine::prologue() {
         I.apply_ilu(mpg_arnoldi_wprev_dev(I.arn, 0));
         check(mpg_arnoldi_prologue_wnorm(I.arn), "prologue wnorm", I.ctx);
     }
+    if (!I.comm) {  // the 3 column sums inside the finish launch (same bits)
+        check(mpg_arnoldi_prologue_finish_partials(I.arn), "prologue_finish", I.ctx);
+        return;
+    }
     check(mpg_arnoldi_reduce(I.arn, 3), "reduce", I.ctx);
-    if (I.comm) I.comm->allreduce_sum(mpg_arnoldi_sums_dev(I.arn), 3, I.stream());
+    I.comm->allreduce_sum(mpg_arnoldi_sums_dev(I.arn), 3, I.stream());
     check(mpg_arnoldi_prologue_finish(I.arn), "prologue_finish", I.ctx);
 }
 

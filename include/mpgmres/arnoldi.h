@@ -104,6 +104,9 @@ int64_t mpg_arnoldi_sell_shared_slices(mpg_arnoldi_t a);
 
 int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
 int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);
+/* one GPU: mpg_arnoldi_reduce(a, 3) + mpg_arnoldi_prologue_finish in one
+ * launch (the same column sums, the same bits) */
+int mpg_arnoldi_prologue_finish_partials(mpg_arnoldi_t a);
 /* recompute the ||w||^2 partials of the prologue (column 1) after the
  * caller preconditioned w (mpg_arnoldi_wprev_dev(a, 0)) itself — ILU */
 int mpg_arnoldi_prologue_wnorm(mpg_arnoldi_t a);
