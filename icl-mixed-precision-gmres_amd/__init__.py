@@ -97,6 +97,8 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_time_phase.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]
     lib.mpg_engine_time_spmv_incycle.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double),
                                                  C.POINTER(C.c_double), C.c_int]
+    lib.mpg_engine_time_spmv_graph.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double),
+                                               C.POINTER(C.c_double), C.c_int]
     lib.mpg_engine_phase_bytes.argtypes = [C.c_void_p, C.c_int]
     lib.mpg_engine_phase_bytes.restype = C.c_double
     lib.mpg_engine_destroy.argtypes = [C.c_void_p]
@@ -363,6 +365,9 @@ class Result:
     step_cycle: np.ndarray
     message: str = ""
     extra: dict = field(default_factory=dict)
+    nonfinite_steps: int = 0       # Arnoldi steps with a NaN/Inf |s(k+1)| (breakdown report)
+    nonfinite_cycles: int = 0      # restarts with a NaN/Inf true residual or beta
+    first_nonfinite_step: int = -1
 
     @property
     def backward_error(self) -> np.ndarray:
@@ -372,7 +377,7 @@ class Result:
 def make_args(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, mode="mixed", orth="mgs",
               prec="identity", rlen=30, tol=1e-6, max_restarts=1_000_000, rtol=0.0, repeat_iter=False,
               orthloss=False, jacobi_steps=1, engine="fused", verbose=False, device=0, threads=0,
-              spmv_format="auto", half_unscaled=False):
+              spmv_format="auto", half_unscaled=False, stop_on_breakdown=False):
     """Build mpg_solve_args (shared by mpg_solve and the CPU oracle)."""
     b = np.ascontiguousarray(b, dtype=np.float64)
     keep = [A.rowptr, A.col, A.val, b]
@@ -392,6 +397,7 @@ def make_args(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, mod
     a.verbose, a.device, a.threads = int(verbose), device, threads
     a.spmv_format = SPMV_FORMATS[spmv_format]
     a.half_unscaled = int(half_unscaled)
+    a.stop_on_breakdown = int(stop_on_breakdown)
     return a, keep
 
 
@@ -413,7 +419,8 @@ def run_solve(fn, args: SolveArgs, n: int, cycle_cap: int = 4096, step_cap: int 
     nc, ns = min(r.n_cycles, cycle_cap), min(r.n_steps, step_cap)
     return Result(STATUS.get(r.status, str(r.status)), r.restarts, r.inner_k, r.total_iters, r.res_norm,
                   r.err_norm, r.gmres_seconds, r.setup_seconds, r.minvb_norm, x, cr[:nc].copy(), cn[:nc].copy(),
-                  cb[:nc].copy(), sr[:ns].copy(), sc[:ns].copy(), msg)
+                  cb[:nc].copy(), sr[:ns].copy(), sc[:ns].copy(), msg, nonfinite_steps=r.nonfinite_steps,
+                  nonfinite_cycles=r.nonfinite_cycles, first_nonfinite_step=r.first_nonfinite_step)
 
 
 def solve(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, **opts) -> Result:
@@ -544,7 +551,7 @@ def solve_loopback(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, n
     if layouts is not None:
         forms = {-1: "none", 0: "int32", 1: "int16", 2: "stepped"}
         for L in lay:
-            d = {f: getattr(L, f) for f, _ in RankLayout._fields_ if f != "pad_"}
+            d = {f: getattr(L, f) for f, _ in RankLayout._fields_}
             d["format"] = {1: "csr", 2: "sell"}.get(d["format"], d["format"])
             d["col_form"] = forms[d["col_form"]]
             layouts.append(d)
@@ -630,6 +637,18 @@ class Engine:
         cnt = self._lib.mpg_engine_time_spmv_incycle(self._h, cycles, C.byref(ms), per, cap)
         if cnt < 0:
             raise RuntimeError(f"mpg_engine_time_spmv_incycle failed ({cnt})")
+        return ms.value, [per[i] for i in range(min(cnt, cap))]
+
+    def time_spmv_graph(self, reps: int = 3) -> tuple:
+        """(mean ms, per-launch ms) of the Arnoldi SpMV inside graph replays
+        of the cycle: external event nodes on each side of every SpMV launch
+        (mpg_engine_time_spmv_graph); measurement only."""
+        ms = C.c_double()
+        cap = 8192
+        per = (C.c_double * cap)()
+        cnt = self._lib.mpg_engine_time_spmv_graph(self._h, reps, C.byref(ms), per, cap)
+        if cnt < 0:
+            raise RuntimeError(f"mpg_engine_time_spmv_graph failed ({cnt})")
         return ms.value, [per[i] for i in range(min(cnt, cap))]
 
     def phase_bytes(self, phase: str) -> float:

@@ -37,6 +37,7 @@ class SolveArgs(C.Structure):
         ("threads", C.c_int32),
         ("spmv_format", C.c_int32),
         ("half_unscaled", C.c_int32),
+        ("stop_on_breakdown", C.c_int32),
     ]
 
 
@@ -62,6 +63,9 @@ class SolveResult(C.Structure):
         ("step_res", C.POINTER(C.c_double)),
         ("step_cycle", C.POINTER(C.c_int32)),
         ("message", C.c_char * 256),
+        ("nonfinite_steps", C.c_int64),
+        ("nonfinite_cycles", C.c_int64),
+        ("first_nonfinite_step", C.c_int64),
     ]
 
 
@@ -103,6 +107,9 @@ class CondestResult(C.Structure):
         ("stop_reason", C.c_int32),
         ("seconds", C.c_double),
         ("message", C.c_char * 256),
+        ("nonfinite_steps", C.c_int64),
+        ("nonfinite_cycles", C.c_int64),
+        ("first_nonfinite_step", C.c_int64),
     ]
 
 
@@ -134,7 +141,7 @@ class RankLayout(C.Structure):
         ("n_local", C.c_int32),
         ("n_front", C.c_int32),
         ("n_ext", C.c_int32),
-        ("pad_", C.c_int32),
+        ("givens_folded", C.c_int32),
         ("row0", C.c_int64),
         ("csr_slices", C.c_int64),
         ("implicit_slices", C.c_int64),

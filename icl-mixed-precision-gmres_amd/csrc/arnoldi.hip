@@ -1924,13 +1924,17 @@ int mpg_arnoldi_fold_max_m(void) { return kFoldMaxM; }
 // fold 25.3k vs 24.3k it/s on LAP-1M (1,954 paired workgroups), but 1,756 vs
 // 1,787 on the C4 stand-in (16,029 workgroups) and 2,874 vs 3,015 on BAND-100M
 // fp16 (19,532): the fold pays up to kFoldMaxGroups SpMV workgroups.
+// (MPG_FOLD_MAX_GROUPS overrides the limit: tests put it between two ranks'
+// workgroup counts to check that the ranks still decide alike)
 constexpr int kFoldMaxGroups = 4096;
 int mpg_arnoldi_fold_pays(mpg_arnoldi_t a) {
     if (!a) return 0;
+    const char* env = std::getenv("MPG_FOLD_MAX_GROUPS");
+    const int64_t limit = env && *env ? std::atoll(env) : kFoldMaxGroups;
     const SellCopy& S = a->sell;
-    if (S.nslices == 0) return a->Grb <= kFoldMaxGroups ? 1 : 0;
+    if (S.nslices == 0) return a->Grb <= limit ? 1 : 0;
     const int per_group = (kStepSellBlock / kWave) * (sell_uniform(S) && sell_pair(S) ? 2 : 1);
-    return (S.nslices + per_group - 1) / per_group <= kFoldMaxGroups ? 1 : 0;
+    return (S.nslices + per_group - 1) / per_group <= limit ? 1 : 0;
 }
 
 static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {

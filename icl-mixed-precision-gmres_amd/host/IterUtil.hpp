@@ -15,7 +15,11 @@
 #ifndef MPGMRES_ITERUTIL_HPP
 #define MPGMRES_ITERUTIL_HPP
 
+#include <cmath>
 #include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
 #include <vector>
 
 #include "Orthogonalization.hpp"
@@ -182,6 +186,38 @@ struct CycleRecord {
     double r_norm = 0, normalization = 0, beta = 0, minvb_norm = 0;
 };
 
+// Breakdown report (our addition). The reference divides by
+// h_{k+1,k} unguarded (Orthogonalization.hpp:56-59), so a zero or non-finite
+// h turns |s(k+1)| and everything after it into NaN/Inf and the restart loop
+// runs on until max_restarts. The solve keeps that behaviour; this log
+// counts what happened, and with `stop` (--stop-on-breakdown) the driver
+// ends the solve at the first non-finite value instead (BreakdownError ->
+// MPG_ERR_BREAKDOWN).
+struct BreakdownError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct BreakdownLog {
+    int64_t steps = 0, cycles = 0, first_step = -1;
+    bool stop = false;
+    // step `index` of the step history had |s(k+1)| = res
+    void step(double res, int64_t index, int64_t cycle, size_t k) {
+        if (std::isfinite(res)) return;
+        if (steps++ == 0) first_step = index;
+        if (stop)
+            throw BreakdownError("non-finite Arnoldi residual |s(k+1)| at step k = " + std::to_string(k) +
+                                 " of restart " + std::to_string(cycle) +
+                                 " (h(k+1,k) zero or non-finite: breakdown; --stop-on-breakdown)");
+    }
+    // restart `cycle`: true residual norm and preconditioned beta
+    void cycle(double r_norm, double beta, int64_t cycle) {
+        if (std::isfinite(r_norm) && std::isfinite(beta)) return;
+        ++cycles;
+        if (stop)
+            throw BreakdownError("non-finite residual norm at restart " + std::to_string(cycle) +
+                                 " (--stop-on-breakdown)");
+    }
+};
+
 // Pass-through strategy that records the residual history.
 template <class T, class Device>
 class Recorder : public Convergence<T, Device> {
@@ -191,6 +227,7 @@ public:
     std::vector<CycleRecord> cycles;
     std::vector<double> step_residual;  // |s(k+1)| per Arnoldi step
     std::vector<int> step_cycle;        // cycle index of each step
+    BreakdownLog breakdown;
 
     explicit Recorder(Convergence<T, Device>& inner)
         : Convergence<T, Device>(inner.tol, inner.restart_length, inner.max_restarts), inner_(inner) {}
@@ -198,11 +235,13 @@ public:
     void setup(Orthogonalization::Orth<T, Device>& o) override { inner_.setup(o); }
     iteration_action check_initial(double r, double nrm, double pr, double pb) override {
         cycles.push_back(CycleRecord{r, nrm, pr, pb});
+        breakdown.cycle(r, pr, (int64_t)cycles.size() - 1);
         return inner_.check_initial(r, nrm, pr, pb);
     }
     iteration_action check(size_t k, double res, double bnorm) override {
         step_residual.push_back(res);
         step_cycle.push_back((int)cycles.size() - 1);
+        breakdown.step(res, (int64_t)step_residual.size() - 1, (int64_t)cycles.size() - 1, k - 1);
         return inner_.check(k, res, bnorm);
     }
     size_t max_restart_length() const override { return inner_.max_restart_length(); }

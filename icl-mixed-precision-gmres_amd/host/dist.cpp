@@ -539,6 +539,7 @@ int mpg_solve_loopback_ex(const mpg_solve_args* a, int32_t P, mpg_solve_result* 
                         L.n_ext = mpg_halo_n_ext(plans[q]);
                         L.row0 = r0;
                         L.half_rows_scaled = e.half_stats()[0];
+                        L.givens_folded = e.givens_folded() ? 1 : 0;
                     }
                     bool done = false;
                     while (!done) e.run(1 << 20, done);

@@ -119,6 +119,7 @@ struct FusedEngine::Impl {
     bool fuse_dots_required = false;
     int timed = -1;                  // phase whose launches time_phase brackets with events
     bool timed_inplace = false;      // ... the cycle's own SpMV launch, by its kernel events
+    bool timed_graph = false;        // ... external event nodes around it in a captured cycle
     std::vector<hipEvent_t> marks;   // ... begin/end pairs
     std::vector<int32_t> rowptr_host;
     mpg_ilu_t ilu = nullptr;  // ILU(0) factors (prec ilu / ilu_jacobi), applied between phase kernels
@@ -244,6 +245,14 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
                                       I.val_inner_own.as<uint16_t>(), scale ? I.row_exp.as<int8_t>() : nullptr,
                                       I.half_stats),
                   "fp16 Arnoldi values", ctx);
+            // a row whose own range exceeds fp16's (~2^39 below its largest
+            // entry) loses its smallest entries to 0 even when scaled: not an
+            // error (the plain cast's MPG_ERR_RANGE case), but said
+            if (I.half_stats[1] > 0 && a.verbose)
+                std::fprintf(stderr,
+                             "mpgmres: mixed-half: %lld nonzero entries rounded to 0 in the fp16 Arnoldi copy "
+                             "(rows spanning more than fp16's range; %lld rows scaled)\n",
+                             (long long)I.half_stats[1], (long long)I.half_stats[0]);
         } else {
             I.cast(I.val64.p, MPG_F64, I.val_inner_own.p, ty.VI, (int64_t)nz);
         }
@@ -364,6 +373,7 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
         conv_ = std::move(lo);
     } else conv_ = std::make_unique<RelPrecRes_Convergence<double, void>>(a.tol, a.rtol, mm, mr);
     conv_->total_iters = 0;
+    breakdown.stop = a.stop_on_breakdown != 0;
 
     const char* env = std::getenv("MPG_NO_GRAPH");
     I.use_graph = !(env && *env == '1') && (!comm || comm->capturable());
@@ -394,7 +404,21 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     // MPG_FOLD_GIVENS: 0 never, 1 always (m permitting), unset: where it pays
     // (mpg_arnoldi_fold_pays: up to ~4k SpMV workgroups)
     const char* fenv = std::getenv("MPG_FOLD_GIVENS");
-    const bool fold_on = fenv && *fenv ? *fenv != '0' : mpg_arnoldi_fold_pays(I.arn) != 0;
+    bool fold_on = fenv && *fenv ? *fenv != '0' : mpg_arnoldi_fold_pays(I.arn) != 0;
+    if (comm && !(fenv && *fenv)) {
+        // ranks of one solve must run the same collective sequence (a folding
+        // rank all-reduces the ||w||^2 partials with the halo, a non-folding
+        // one reduces + all-reduces one sum after it): every rank's row block
+        // and SELL layout differ, so the fold is taken only if it pays on
+        // EVERY rank (all-reduce max of "does not pay")
+        double* flag = I.scal.as<double>() + 6;
+        const double no = fold_on ? 0.0 : 1.0;
+        check(mpg_memcpy_h2d(ctx, flag, &no, sizeof no), "h2d", ctx);
+        comm->allreduce_max(flag, 1, I.stream());
+        double any_no = 0;
+        check(mpg_memcpy_d2h(ctx, &any_no, flag, sizeof any_no), "d2h", ctx);
+        fold_on = any_no == 0.0;
+    }
     I.fold = !I.combine && fold_on && I.m <= mpg_arnoldi_fold_max_m();
     check(mpg_ctx_sync(ctx), "sync", ctx);
     setup_seconds = std::chrono::duration<double>(clk::now() - t0).count();
@@ -461,6 +485,7 @@ void FusedEngine::step(int k, bool fold) {
     if (I.fuse_dots && !I.comm && !I.ilu && I.orth == MPG_ORTH_CGS && I.cgs_partials && !I.combine && k + 1 <= 32) {
         timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
         const int st = mpg_arnoldi_spmv_dots(I.arn, k, fold && k > 0 ? 2 : 0);
+        timed_end(0);
         if (st == MPG_OK) {
             check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx);
             if (!fold) givens(k);
@@ -476,10 +501,12 @@ void FusedEngine::step(int k, bool fold) {
                                            I.stream());
         timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
         check(mpg_arnoldi_givens_partials_spmv(I.arn, k), "givens+spmv", I.ctx);
+        timed_end(0);
     } else {
         if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
         timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
         check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
+        timed_end(0);
     }
     if (I.ilu) I.apply_ilu(mpg_arnoldi_wprev_dev(I.arn, k + 1));  // w = M(A v_k)
     if (I.orth == MPG_ORTH_MGS) {
@@ -607,6 +634,7 @@ bool FusedEngine::check_start(int64_t i) {
     else normalization = b_norm + a_norm * x_norm;
     cycles.push_back(CycleRecord{r_norm, normalization, beta, minvb_norm});
     restarts = i;
+    breakdown.cycle(r_norm, beta, i);
     switch (conv_->check_initial(r_norm, normalization, beta, minvb_norm)) {
         case iteration_converged: {
             const double rel = I.ty.single_scalars ? (double)(float)((float)beta / (float)minvb_norm)
@@ -656,6 +684,7 @@ void FusedEngine::record_steps(int64_t i) {
         const double res = I.report_host[4 + k];
         step_res.push_back(res);
         step_cycle.push_back((int)i);
+        breakdown.step(res, (int64_t)step_res.size() - 1, i, (size_t)k);
         conv_->check((size_t)k + 1, res, minvb_norm);  // base strategy: counts, restarts at m
     }
 }
@@ -707,7 +736,20 @@ int FusedEngine::run_pipelined(int max_cycles, bool& done) {
     }
 }
 
+// --stop-on-breakdown: the first non-finite value ends the solve with
+// MPG_ERR_BREAKDOWN (nothing left in flight: a pipelined cycle may be)
 int FusedEngine::run(int max_cycles, bool& done) {
+    try {
+        return run_cycles(max_cycles, done);
+    } catch (const BreakdownError& e) {
+        (void)hipStreamSynchronize(p_->stream());
+        done = true;
+        status = MPG_RESULT_ERROR;
+        throw StatusError(MPG_ERR_BREAKDOWN, e.what());
+    }
+}
+
+int FusedEngine::run_cycles(int max_cycles, bool& done) {
     Impl& I = *p_;
     done = false;
     int ran = 0;
@@ -737,6 +779,7 @@ int FusedEngine::run(int max_cycles, bool& done) {
             const double res = I.report_host[4 + k];
             step_res.push_back(res);
             step_cycle.push_back((int)i);
+            breakdown.step(res, (int64_t)step_res.size() - 1, i, (size_t)k);
             const iteration_action act = conv_->check((size_t)k + 1, res, minvb_norm);
             if (act == iteration_converged) {
                 update(k + 1);
@@ -866,6 +909,15 @@ template <class F>
 void FusedEngine::timed(int phase, F&& launch) {
     Impl& I = *p_;
     if (I.timed != phase) return;
+    if (I.timed_graph) {
+        // an external event node ahead of the site's own launch (its pair
+        // follows the launch: timed_end)
+        hipEvent_t e0;
+        hipck(hipEventCreate(&e0), "event");
+        hipck(hipEventRecordWithFlags(e0, I.stream(), hipEventRecordExternal), "record (graph)");
+        I.marks.push_back(e0);
+        return;
+    }
     hipEvent_t e[2];
     for (auto& x : e) hipck(hipEventCreate(&x), "event");
     if (I.timed_inplace) {
@@ -877,6 +929,69 @@ void FusedEngine::timed(int phase, F&& launch) {
     }
     I.marks.push_back(e[0]);
     I.marks.push_back(e[1]);
+}
+
+void FusedEngine::timed_end(int phase) {
+    Impl& I = *p_;
+    if (I.timed != phase || !I.timed_graph) return;
+    hipEvent_t e1;
+    hipck(hipEventCreate(&e1), "event");
+    hipck(hipEventRecordWithFlags(e1, I.stream(), hipEventRecordExternal), "record (graph)");
+    I.marks.push_back(e1);
+}
+
+// The Arnoldi SpMV timed inside graph replays of the cycle: the cycle is
+// captured once more with an external event node on each side of every
+// SpMV launch, and that graph is replayed `reps` times (each replay
+// re-records the events; they are read after it). Measurement only, like
+// time_phase: the replays run without the host's restart checks.
+double FusedEngine::time_spmv_graph(int reps, std::vector<double>* per_launch) {
+    Impl& I = *p_;
+    if (!I.use_graph) throw StatusError(MPG_ERR_UNSUPPORTED, "the cycle is not captured (MPG_NO_GRAPH / eager ranks)");
+    I.timed = 0;
+    I.timed_graph = true;
+    I.marks.clear();
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    double total = 0;
+    size_t count = 0;
+    auto cleanup = [&] {
+        I.timed = -1;
+        I.timed_graph = false;
+        if (ge) (void)hipGraphExecDestroy(ge);
+        if (g) (void)hipGraphDestroy(g);
+        for (hipEvent_t e : I.marks) (void)hipEventDestroy(e);
+        I.marks.clear();
+    };
+    try {
+        hipck(hipStreamBeginCapture(I.stream(), hipStreamCaptureModeThreadLocal), "begin capture");
+        try {
+            cycle_program();
+        } catch (...) {
+            (void)hipStreamEndCapture(I.stream(), &g);
+            throw;
+        }
+        hipck(hipStreamEndCapture(I.stream(), &g), "end capture");
+        hipck(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0), "instantiate");
+        const size_t pairs = I.marks.size() / 2;
+        for (int r = 0; r < reps; ++r) {
+            hipck(hipGraphLaunch(ge, I.stream()), "graph launch");
+            hipck(hipStreamSynchronize(I.stream()), "sync");
+            for (size_t q = 0; q < pairs; ++q) {
+                float ms = 0;
+                hipck(hipEventElapsedTime(&ms, I.marks[2 * q], I.marks[2 * q + 1]), "elapsed");
+                total += ms;
+                ++count;
+                if (per_launch) per_launch->push_back(ms);
+            }
+        }
+    } catch (...) {
+        cleanup();
+        (void)hipGetLastError();
+        throw;
+    }
+    cleanup();
+    return count ? total / count : 0.0;
 }
 
 // ---------------------------------------------------------------- mpg_solve (fused)
@@ -893,6 +1008,9 @@ void fill_history(const FusedEngine& e, mpg_solve_result* r) {
         if (r->cyc_normalization) r->cyc_normalization[c] = e.cycles[c].normalization;
         if (r->cyc_beta) r->cyc_beta[c] = e.cycles[c].beta;
     }
+    r->nonfinite_steps = e.breakdown.steps;
+    r->nonfinite_cycles = e.breakdown.cycles;
+    r->first_nonfinite_step = e.breakdown.first_step;
     r->n_steps = (int64_t)e.step_res.size();
     for (size_t s = 0; s < e.step_res.size() && (int64_t)s < r->step_cap; ++s) {
         if (r->step_res) r->step_res[s] = e.step_res[s];
@@ -984,6 +1102,21 @@ int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, dou
         *avg_ms = e->eng->time_phase(0, cycles, true, &t);
         for (size_t i = 0; i < t.size() && (int)i < cap; ++i) per_launch_ms[i] = t[i];
         return (int)t.size();
+    } catch (const std::exception&) {
+        return MPG_ERR_HIP;
+    }
+}
+
+int mpg_engine_time_spmv_graph(mpg_engine_t e, int reps, double* avg_ms, double* per_launch_ms, int cap) {
+    if (!e || !e->eng || !avg_ms || reps < 1 || cap < 0 || (cap && !per_launch_ms)) return MPG_ERR_ARG;
+    try {
+        mpg::ScopedContext scope(e->ctx);
+        std::vector<double> t;
+        *avg_ms = e->eng->time_spmv_graph(reps, &t);
+        for (size_t i = 0; i < t.size() && (int)i < cap; ++i) per_launch_ms[i] = t[i];
+        return (int)t.size();
+    } catch (const mpg::StatusError& ex) {
+        return ex.status;
     } catch (const std::exception&) {
         return MPG_ERR_HIP;
     }

@@ -79,6 +79,7 @@ public:
 
     size_t total_iters() const { return conv_->total_iterations(); }
     double time_phase(int which, int reps, bool inplace = false, std::vector<double>* per_launch = nullptr);
+    double time_spmv_graph(int reps, std::vector<double>* per_launch = nullptr);
     double phase_bytes(int which) const;
     mpg_arnoldi_t arnoldi() const;
     // mixed-half: what the fp16 cast of the Arnoldi values did (stats of
@@ -97,6 +98,7 @@ public:
     int64_t inner_k = 0;
     double minvb_norm = 0, b_norm = 0, a_norm = 0;
     double setup_seconds = 0;
+    BreakdownLog breakdown;  // non-finite |s(k+1)| / restart residuals (IterUtil.hpp)
 
 private:
     struct Impl;
@@ -109,6 +111,7 @@ private:
     void givens(int k);
     template <class F>
     void timed(int phase, F&& launch);
+    void timed_end(int phase);
     void update(int k);
     void store_next_basis(int k);
     double orth_loss_step(size_t k);
@@ -117,6 +120,7 @@ private:
     void ensure_graph();
     void record_steps(int64_t i);
     int run_pipelined(int max_cycles, bool& done);
+    int run_cycles(int max_cycles, bool& done);
     bool check_start(int64_t i);
 };
 

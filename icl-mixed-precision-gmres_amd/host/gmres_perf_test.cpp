@@ -11,7 +11,8 @@
 // stencil27:NX[:DOF[:SEED]] (synthetic input instead of --Apath,
 // mpg_gen_spec), --mode mixed-half, --half-unscaled (mixed-half: plain fp16
 // cast, a value outside fp16's range is an error), --engine {fused,surface},
-// --device D.
+// --device D, --stop-on-breakdown (end the solve with an error at the first
+// non-finite Arnoldi residual; without it the count goes to stderr).
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -72,6 +73,7 @@ int main(int argc, char* argv[]) {
         else if (f == "--gpu") { /* always on the GPU */ }
         else if (f == "--device") a.device = std::stoi(next());
         else if (f == "--half-unscaled") a.half_unscaled = 1;
+        else if (f == "--stop-on-breakdown") a.stop_on_breakdown = 1;
         else if (f == "--mode") {
             const std::string v = next();
             if (v == "mixed") a.mode = MPG_MODE_MIXED;
@@ -158,6 +160,12 @@ int main(int argc, char* argv[]) {
     mpg_solve_result r{};
     int st = mpg_solve(&a, &r);
     mpg_host_csr_free(&A);
+    // (stderr: the stdout lines stay the reference's, automated.py:33-38)
+    if (r.nonfinite_steps > 0 || r.nonfinite_cycles > 0)
+        std::cerr << "warning: breakdown: " << r.nonfinite_steps << " Arnoldi step(s) with a non-finite |s(k+1)| "
+                  << "(first at step " << r.first_nonfinite_step << " of the history) and " << r.nonfinite_cycles
+                  << " restart(s) with a non-finite residual norm; --stop-on-breakdown ends the solve there"
+                  << std::endl;
     if (st != 0) {
         std::cerr << "mpg_solve failed: " << r.message << std::endl;
         return 1;

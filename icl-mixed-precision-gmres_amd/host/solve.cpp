@@ -70,6 +70,9 @@ void record(const Recorder<T, Hip>& rec, const Convergence<T, Hip>& conv, mpg_so
         if (r->step_res) r->step_res[s] = rec.step_residual[s];
         if (r->step_cycle) r->step_cycle[s] = rec.step_cycle[s];
     }
+    r->nonfinite_steps = rec.breakdown.steps;
+    r->nonfinite_cycles = rec.breakdown.cycles;
+    r->first_nonfinite_step = rec.breakdown.first_step;
     // status: converged iff the last check_initial said so (or a check did)
     r->restarts = rec.cycles.empty() ? 0 : (int64_t)rec.cycles.size() - 1;
 }
@@ -118,6 +121,7 @@ void do_baseline(const mpg_solve_args& a, const SparseMatrix<double, Hip>& A, Ve
     copy(b, b_type);
     auto conv = make_convergence<Type>(a);
     Recorder<Type, Hip> rec(*conv);
+    rec.breakdown.stop = a.stop_on_breakdown != 0;
 
     Hip::fence();
     auto t1 = clk::now();
@@ -147,6 +151,7 @@ void do_mixed(const mpg_solve_args& a, const SparseMatrix<double, Hip>& A, Vect<
 
     auto conv = make_convergence<float>(a);
     Recorder<float, Hip> rec(*conv);
+    rec.breakdown.stop = a.stop_on_breakdown != 0;
     Hip::fence();
     auto t1 = clk::now();
     gmres_singleUpdate<Orth, Hip>(rec, A, A_single, M.get(), b, x);
@@ -197,6 +202,8 @@ extern "C" int mpg_solve(const mpg_solve_args* args, mpg_solve_result* result) {
     result->message[0] = '\0';
     result->n_cycles = result->n_steps = 0;
     result->res_norm = result->err_norm = 0;
+    result->nonfinite_steps = result->nonfinite_cycles = 0;
+    result->first_nonfinite_step = -1;
     try {
         if (args->n <= 0 || args->rlen <= 0 || !args->rowptr || !args->col || !args->val || !args->b)
             throw std::invalid_argument("invalid solve arguments (n, rlen, CSR arrays and b are required)");
@@ -216,6 +223,10 @@ extern "C" int mpg_solve(const mpg_solve_args* args, mpg_solve_result* result) {
         result->status = MPG_RESULT_ERROR;
         std::snprintf(result->message, sizeof result->message, "%s", e.what());
         return e.status;
+    } catch (const mpg::BreakdownError& e) {
+        result->status = MPG_RESULT_ERROR;
+        std::snprintf(result->message, sizeof result->message, "%s", e.what());
+        return MPG_ERR_BREAKDOWN;
     } catch (const std::exception& e) {
         result->status = MPG_RESULT_ERROR;
         std::snprintf(result->message, sizeof result->message, "%s", e.what());

@@ -105,7 +105,8 @@ typedef struct {
     int32_t vec_width;
     int32_t window;           /* 1: the SpMV reads v_k from the LDS window */
     int32_t n_local, n_front, n_ext;
-    int32_t pad_;
+    int32_t givens_folded;    /* 1: this rank folds the Givens step into the next SpMV (the
+                                 same on every rank: decided collectively at create) */
     int64_t row0;             /* first global row */
     int64_t csr_slices, implicit_slices;
     int64_t half_rows_scaled; /* mixed-half: rows scaled by a power of two */

@@ -65,6 +65,10 @@ typedef struct {
     int32_t half_unscaled; /* mode mixed-half: 0 = fp16 values scaled per row by powers of two where
                               a row's magnitude needs it (mpg_csr_half_values, capi.h); 1 = plain
                               cast: a value outside fp16's range fails the set-up (MPG_ERR_RANGE) */
+    int32_t stop_on_breakdown; /* 1: stop at the first non-finite |s(k+1)| or restart residual and
+                                  return MPG_ERR_BREAKDOWN (--stop-on-breakdown); 0: the reference's
+                                  behaviour (Orthogonalization.hpp:56-59 divides unguarded and the
+                                  restart loop runs on), the count is only reported */
 } mpg_solve_args;
 
 typedef struct {
@@ -87,6 +91,12 @@ typedef struct {
     double* step_res;         /* |s(k+1)| per Arnoldi step */
     int32_t* step_cycle;      /* cycle index of each step */
     char message[256];        /* error text when status == MPG_RESULT_ERROR */
+    /* breakdown report (not a reference decision: the solve runs as the
+       reference's does unless args->stop_on_breakdown) */
+    int64_t nonfinite_steps;  /* Arnoldi steps whose |s(k+1)| was NaN/Inf (h_{k+1,k} = 0 or
+                                 non-finite makes the normalisation 1/h non-finite) */
+    int64_t nonfinite_cycles; /* restarts whose true residual norm or beta was NaN/Inf */
+    int64_t first_nonfinite_step; /* index of the first such step in the step history, -1: none */
 } mpg_solve_result;
 
 /* HIP path (libmpgmres_host.so). Returns 0 on success (result->status tells
@@ -121,6 +131,11 @@ int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms);
  * `cap` per-launch times in cycle order (measurement only: the cycles run
  * without the host's restart checks) */
 int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, double* per_launch_ms, int cap);
+/* the same SpMV timed inside graph replays of the cycle: the cycle captured
+ * with an external event node on each side of every SpMV launch, replayed
+ * `reps` times (returns the launch count, m per replay; MPG_ERR_UNSUPPORTED
+ * when the engine runs eagerly) */
+int mpg_engine_time_spmv_graph(mpg_engine_t e, int reps, double* avg_ms, double* per_launch_ms, int cap);
 /* algorithmic bytes of one launch of phase `which` */
 double mpg_engine_phase_bytes(mpg_engine_t e, int which);
 /* storage of the engine's Arnoldi SpMV (mpg_arnoldi_spmv_layout) */

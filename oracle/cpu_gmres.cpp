@@ -622,6 +622,14 @@ void fill_result(const Strategy& st, const Outcome& o, mpg_solve_result* r) {
         if (r->step_res) r->step_res[s] = st.step_res[s];
         if (r->step_cycle) r->step_cycle[s] = st.step_cyc[s];
     }
+    // the product's breakdown report (solve.h), counted the same way: steps
+    // with a non-finite |s(k+1)|, restarts with a non-finite r_norm or beta
+    r->nonfinite_steps = r->nonfinite_cycles = 0;
+    r->first_nonfinite_step = -1;
+    for (size_t s = 0; s < st.step_res.size(); ++s)
+        if (!std::isfinite(st.step_res[s]) && r->nonfinite_steps++ == 0) r->first_nonfinite_step = (int64_t)s;
+    for (size_t c = 0; c < st.cyc_r.size(); ++c)
+        if (!std::isfinite(st.cyc_r[c]) || !std::isfinite(st.cyc_beta[c])) ++r->nonfinite_cycles;
 }
 
 // final report with the original fp64 A (gmres_perf_test.cpp:104-115, 169-178)

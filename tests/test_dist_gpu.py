@@ -254,3 +254,52 @@ def test_host_transport_processes_stencil27(mpg, oracle, tmp_path):
     assert np.array_equal(got["step_res"], loop.step_res) and np.array_equal(got["x"], loop.x)
     ref = oracle.solve(mpg, A, b, xt, **opts)
     compare(as_ref(ref), loop, mode, tol, 30, "host-transport-stencil27")
+
+
+def _two_width_band(mpg, n):
+    """Rows [0, n/2) hold offsets -1..+1, rows [n/2, n) offsets -5..+4
+    (diagonally dominant, the BAND value rule): nnz-balanced ranks then get
+    very different row counts and SELL forms (rank 0 mixed widths, one slice
+    per wave; rank 1 uniform, two slices per wave)."""
+    rng = np.random.default_rng(5)
+    rows, cols, vals = [], [], []
+    for lo, hi, r0, r1 in ((1, 1, 0, n // 2), (5, 4, n // 2, n)):
+        r = np.arange(r0, r1)
+        for o in range(-lo, hi + 1):
+            c = r + o
+            ok = (c >= 0) & (c < n) & (o != 0)
+            rows.append(r[ok]), cols.append(c[ok]), vals.append(-rng.random(ok.sum()))
+    rr, cc, vv = np.concatenate(rows), np.concatenate(cols), np.concatenate(vals)
+    diag = 1.0 + np.bincount(rr, weights=np.abs(vv), minlength=n)
+    rr = np.concatenate([rr, np.arange(n)])
+    cc = np.concatenate([cc, np.arange(n)])
+    vv = np.concatenate([vv, diag])
+    order = np.lexsort((cc, rr))
+    rp = np.zeros(n + 1, np.int32)
+    np.cumsum(np.bincount(rr, minlength=n), out=rp[1:])
+    return mpg.Csr(n, n, rp, cc[order].astype(np.int32), vv[order].astype(np.float64))
+
+
+@pytest.mark.parametrize("limit,folded", [("600", 0), ("4096", 1)], ids=["straddle", "both-pay"])
+def test_fold_decision_is_collective(mpg, oracle, monkeypatch, limit, folded):
+    """each rank used to decide the Givens fold from its own SpMV
+    workgroup count, so ranks near the limit could run different collective
+    sequences. With the limit between the two ranks' counts (~1,055 and ~254
+    workgroups) and MPG_FOLD_GIVENS unset, every rank must take the same
+    decision (the fold only where it pays on every rank) and the solve must
+    match the oracle."""
+    monkeypatch.delenv("MPG_FOLD_GIVENS", raising=False)
+    monkeypatch.setenv("MPG_FOLD_MAX_GROUPS", limit)
+    A = _two_width_band(mpg, 400_000)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    # fp64 Arnoldi: the strict rules (same counts, history to 1e-8). In mode
+    # mixed this matrix's cycle-1 backward error is 45x smaller on the GPU than
+    # on MKL, whose fp32 sgemv rounds every term (DESIGN §2), past the 3x rule
+    opts = dict(mode="baseline", orth="cgs", prec="jacobi", rlen=30, tol=1e-12, max_restarts=60)
+    lays = []
+    got = mpg.solve_loopback(A, b, xt, nranks=2, layouts=lays, **opts)
+    assert lays[0]["n_local"] > 1.8 * lays[1]["n_local"], lays
+    assert [L["givens_folded"] for L in lays] == [folded, folded], lays
+    ref = oracle.solve(mpg, A, b, xt, **opts)
+    compare(as_ref(ref), got, "baseline", opts["tol"], 30, f"fold-collective-{limit}")

@@ -148,3 +148,42 @@ def test_in_range_matrix_solve_unchanged_by_scaling(mpg, fmt):
     c = mpg.solve(A, b, xt, half_unscaled=True, **opts)
     assert a.total_iters == c.total_iters == 90
     assert np.array_equal(a.step_res, c.step_res) and np.array_equal(a.x, c.x)
+
+
+def _row_scaled(mpg, A, lo=-6.0, hi=6.0, seed=3):
+    """D A with D = diag(10^u), u ~ U(lo, hi) per row: every row's own range
+    stays small, but most rows leave fp16's and are scaled by a power of 2."""
+    d = 10.0 ** np.random.default_rng(seed).uniform(lo, hi, A.nrows)
+    rows = np.repeat(np.arange(A.nrows), np.diff(A.rowptr))
+    return mpg.Csr(A.nrows, A.ncols, A.rowptr, A.col, A.val * d[rows])
+
+
+@pytest.mark.parametrize("which", ["band-pair", "stencil27-stepped"])
+def test_row_scaled_unscaling_on_every_sell_kernel(mpg, which):
+    """the scaled fp16 rows must also run through the paired
+    uniform SELL kernel (k_step_sell2, BAND) and the stepped copy with
+    CSR-summed slices (C4's structure), not only the single-slice int16
+    kernel. Each layout is asserted; the fp16 SELL solve is compared with the
+    CSR-tile solve of the same scaled copy (both unscale the same fp64 row
+    sums; the prologues differ in the last fp64 bits, as above)."""
+    if which == "band-pair":
+        A = _row_scaled(mpg, mpg.gen_band(200_000, 5, 4, seed=7))
+    else:
+        A = _row_scaled(mpg, mpg.gen_stencil27(105, 3, ny=105, nz=8))
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode="mixed-half", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=2)
+    eng = mpg.Engine(A, b, xt, spmv_format="sell", **opts)
+    lay, cols, hs = eng.spmv_layout(), eng.sell_columns(), eng.half_stats()
+    eng.close()
+    assert hs["rows_scaled"] > A.nrows // 2 and hs["overflowed"] == 0 and hs["exp_out_of_range"] == 0, hs
+    if which == "band-pair":
+        assert lay["format"] == "sell" and lay["slices_per_wave"] == 2 and cols["form"] == "int16", (lay, cols)
+    else:
+        assert lay["format"] == "sell" and cols["form"] == "stepped" and cols["csr_slices"] > 0, (lay, cols)
+    s = mpg.solve(A, b, xt, engine="fused", spmv_format="sell", **opts)
+    c = mpg.solve(A, b, xt, engine="fused", spmv_format="csr", **opts)
+    assert s.total_iters == c.total_iters == 60
+    assert np.all(np.isfinite(s.step_res)) and s.nonfinite_steps == 0
+    np.testing.assert_allclose(s.step_res, c.step_res, rtol=1e-4)
+    np.testing.assert_allclose(s.cyc_r_norm, c.cyc_r_norm, rtol=1e-4)

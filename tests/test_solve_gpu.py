@@ -169,6 +169,34 @@ def test_tiny_systems_match_oracle(mpg, oracle, engine, n):
     assert np.array_equal(np.isfinite(got.step_res), np.isfinite(ref.step_res))
 
 
+@pytest.mark.parametrize("engine", ["surface", "fused"])
+@pytest.mark.parametrize("mode", ["baseline", "mixed"])
+@pytest.mark.parametrize("n", [1, 3])
+def test_breakdown_report_and_stop(mpg, oracle, engine, mode, n):
+    """the solve keeps the reference's unguarded
+    normalisation (Orthogonalization.hpp:56-59), but reports what happened:
+    at n = 1 the Krylov space is exhausted after one step and every later
+    |s(k+1)| of the cycle is NaN (the oracle: 29 steps from step 1, one
+    restart with a non-finite residual); n = 3 stays finite. The counts
+    match the oracle's, and --stop-on-breakdown ends the solve with
+    MPG_ERR_BREAKDOWN at the first one instead."""
+    A = mpg.gen_band(n, 1, 1, seed=5)
+    xt = mpg.rand_vect(n, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode=mode, orth="cgs", prec="identity", rlen=30, tol=1e-12, max_restarts=5)
+    ref = oracle.solve(mpg, A, b, xt, **opts)
+    got = mpg.solve(A, b, xt, engine=engine, **opts)
+    assert (got.nonfinite_steps, got.nonfinite_cycles, got.first_nonfinite_step) == \
+        (ref.nonfinite_steps, ref.nonfinite_cycles, ref.first_nonfinite_step)
+    assert (ref.nonfinite_steps > 0) == (n == 1), ref.nonfinite_steps
+    if n == 1:
+        with pytest.raises(RuntimeError, match=r"\(-6\).*non-finite"):
+            mpg.solve(A, b, xt, engine=engine, stop_on_breakdown=True, **opts)
+    else:
+        ok = mpg.solve(A, b, xt, engine=engine, stop_on_breakdown=True, **opts)
+        assert ok.status == got.status and np.array_equal(ok.step_res, got.step_res)
+
+
 @pytest.mark.parametrize("engine", ["fused", "fused-cgspart", "surface"])
 @pytest.mark.parametrize("orth", ["cgs", "mgs", "cgsr"])
 @pytest.mark.parametrize("mode", ["mixed", "baseline"])

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""How long does the in-cycle Arnoldi SpMV take? Three clocks on one engine,
+in this order, so a rocprofv3 --kernel-trace of this script can be split
+by launch index and set beside each:
+  1. `--warm` graph-replayed restart cycles (the bench's timed region;
+     no timing of our own: rocprof alone),
+  2. `--eager` eager cycles, every SpMV launch timed by its own
+     hipExtLaunchKernel start/stop events (mpg_engine_time_spmv_incycle),
+  3. `--graph` replays of the cycle captured with an external event node on
+     each side of every SpMV (mpg_engine_time_spmv_graph).
+Prints one JSON line: the mean of 2 and 3, the launch counts of each block
+(m per cycle) and the workload.
+usage: python tools/timing_probe.py [--rows 1000000] [--rlen 30]"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--rlen", type=int, default=30)
+    ap.add_argument("--orth", default="cgs")
+    ap.add_argument("--warm", type=int, default=4)
+    ap.add_argument("--eager", type=int, default=3)
+    ap.add_argument("--graph", type=int, default=5)
+    args = ap.parse_args()
+    from __graft_entry__ import _load
+
+    mpg = _load()
+    A = mpg.gen_band(args.rows, 5, 4, seed=7)
+    xt = mpg.rand_vect(args.rows, 42)
+    b = mpg.host_spmv(A, xt)
+    eng = mpg.Engine(A, b, xt, mode="mixed", orth=args.orth, prec="identity", rlen=args.rlen, tol=0.0,
+                     max_restarts=args.warm + 10)
+    eng.run(args.warm)
+    eng.sync()
+    e_ms, e_per = eng.time_spmv_incycle(args.eager)
+    g_ms, g_per = eng.time_spmv_graph(args.graph)
+    lay = eng.spmv_layout()
+    eng.close()
+    m = args.rlen
+    print(json.dumps({
+        "workload": f"BAND n={args.rows} mixed {args.orth} GMRES({m})", "layout": lay,
+        "blocks": {"warm_graph": args.warm * m, "eager_events": len(e_per), "graph_events": len(g_per)},
+        "eager_event_us": round(1e3 * e_ms, 3), "eager_event_median_us": round(1e3 * float(np.median(e_per)), 3),
+        "graph_event_us": round(1e3 * g_ms, 3), "graph_event_median_us": round(1e3 * float(np.median(g_per)), 3),
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
