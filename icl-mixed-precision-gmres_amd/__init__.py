@@ -81,6 +81,9 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_gen_spec.argtypes = [C.c_char_p, C.POINTER(HostCsr), C.c_char_p, C.c_int]
     lib.mpg_condest.restype = C.c_int
     lib.mpg_gen_stencil27.argtypes = [_I32, _I32, _I32, _I32, C.c_uint64, C.POINTER(HostCsr)]
+    lib.mpg_gen_fem27.argtypes = [_I32, _I32, _I32, _I32, _I32, C.c_uint64, C.POINTER(HostCsr)]
+    lib.mpg_perm_node_blocks.argtypes = [C.c_int64, _I32, _I32, C.c_uint64, C.POINTER(C.c_int32)]
+    lib.mpg_csr_permute_sym.argtypes = [C.POINTER(HostCsr), C.POINTER(C.c_int32), C.POINTER(HostCsr)]
     lib.mpg_load_mtx.argtypes = [C.c_char_p, C.POINTER(HostCsr), C.c_char_p, C.c_int]
     lib.mpg_load_mtx_vector.argtypes = [C.c_char_p, _I32, C.POINTER(C.c_double), _I64, C.c_char_p, C.c_int]
     lib.mpg_rand_vect.argtypes = [_I64, C.c_uint32, C.POINTER(C.c_double)]
@@ -97,8 +100,8 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_time_phase.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double)]
     lib.mpg_engine_time_spmv_incycle.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double),
                                                  C.POINTER(C.c_double), C.c_int]
-    lib.mpg_engine_time_spmv_graph.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double),
-                                               C.POINTER(C.c_double), C.c_int]
+    lib.mpg_engine_time_phase_graph.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
+                                                C.POINTER(C.c_double), C.c_int]
     lib.mpg_engine_phase_bytes.argtypes = [C.c_void_p, C.c_int]
     lib.mpg_engine_phase_bytes.restype = C.c_double
     lib.mpg_engine_destroy.argtypes = [C.c_void_p]
@@ -300,6 +303,43 @@ def load_mtx_vector(path: str, n: int, col: int = 0) -> np.ndarray:
     if host_lib().mpg_load_mtx_vector(path.encode(), col, out.ctypes.data_as(C.POINTER(C.c_double)), n, err, 256):
         raise ValueError(err.value.decode())
     return out
+
+
+def gen_fem27(nx: int, dof: int = 3, keep_pct: int = 70, seed: int = 13, ny: Optional[int] = None,
+              nz: Optional[int] = None) -> Csr:
+    """FEM-like irregular matrix: the 27-point node coupling with each node
+    pair kept with probability keep_pct % (symmetric; rows of variable length)."""
+    h = HostCsr()
+    st = host_lib().mpg_gen_fem27(nx, ny or nx, nz or nx, dof, keep_pct, seed, C.byref(h))
+    if st:
+        raise ValueError(f"mpg_gen_fem27 failed ({st})")
+    return _take_csr(h)
+
+
+def perm_node_blocks(nodes: int, dof: int = 3, block: int = 64, seed: int = 5) -> np.ndarray:
+    """perm[old] = new: node blocks in a seeded random order, nodes shuffled
+    inside each block, dof kept together (mpg_perm_node_blocks)."""
+    perm = np.zeros(nodes * dof, dtype=np.int32)
+    if host_lib().mpg_perm_node_blocks(nodes, dof, block, seed, perm.ctypes.data_as(C.POINTER(C.c_int32))):
+        raise ValueError("mpg_perm_node_blocks failed")
+    return perm
+
+
+def permute_sym(A: Csr, perm: np.ndarray) -> Csr:
+    """P A P^T with row perm[i] = row i of A (mpg_csr_permute_sym)."""
+    perm = np.ascontiguousarray(perm, dtype=np.int32)
+    a, h = A._c(), HostCsr()
+    if host_lib().mpg_csr_permute_sym(C.byref(a), perm.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(h)):
+        raise ValueError("mpg_csr_permute_sym failed (not a permutation?)")
+    return _take_csr(h)
+
+
+def gen_stencil27p(nx: int, dof: int = 3, seed: int = 11, block: int = 64, perm_seed: int = 5,
+                   ny: Optional[int] = None, nz: Optional[int] = None) -> Csr:
+    """The Queen_4147-like irregular stand-in: gen_stencil27 under a symmetric
+    node-block permutation (same spectrum, scattered neighbours)."""
+    A = gen_stencil27(nx, dof, seed, ny=ny, nz=nz)
+    return permute_sym(A, perm_node_blocks(A.nrows // dof, dof, block, perm_seed))
 
 
 def gen_spec(spec: str) -> Csr:
@@ -639,16 +679,18 @@ class Engine:
             raise RuntimeError(f"mpg_engine_time_spmv_incycle failed ({cnt})")
         return ms.value, [per[i] for i in range(min(cnt, cap))]
 
-    def time_spmv_graph(self, reps: int = 3) -> tuple:
-        """(mean ms, per-launch ms) of the Arnoldi SpMV inside graph replays
-        of the cycle: external event nodes on each side of every SpMV launch
-        (mpg_engine_time_spmv_graph); measurement only."""
+    def time_phase_graph(self, phase: str = "spmv", reps: int = 3) -> tuple:
+        """(mean ms, per-launch ms in cycle order) of a phase kernel ("spmv",
+        "cgs_update", "dots") inside graph replays of the cycle: external
+        event nodes on each side of every launch of that phase
+        (mpg_engine_time_phase_graph); measurement only."""
         ms = C.c_double()
-        cap = 8192
+        cap = 16384
         per = (C.c_double * cap)()
-        cnt = self._lib.mpg_engine_time_spmv_graph(self._h, reps, C.byref(ms), per, cap)
+        which = {"spmv": 0, "cgs_update": 2, "dots": 3}[phase]
+        cnt = self._lib.mpg_engine_time_phase_graph(self._h, which, reps, C.byref(ms), per, cap)
         if cnt < 0:
-            raise RuntimeError(f"mpg_engine_time_spmv_graph failed ({cnt})")
+            raise RuntimeError(f"mpg_engine_time_phase_graph failed ({cnt})")
         return ms.value, [per[i] for i in range(min(cnt, cap))]
 
     def phase_bytes(self, phase: str) -> float:

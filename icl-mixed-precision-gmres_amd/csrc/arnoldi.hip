@@ -379,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void k_givens(GivensArgs<T> g, const double
 // <= kFoldMaxM): every workgroup sums the ||w||^2 partials in the same
 // fixed order and forms 1/h_{k,k-1} itself; workgroup 0 also runs the
 // rotation step. Returns the scale for v_k in every thread.
-constexpr int kFoldMaxM = 64;
+constexpr int kFoldMaxM = 128;  // GMRES(100), the reference's published restart length
 template <class T>
 struct GivensFold {
     const double* norm2;  // nullptr: not folded (use *inv_p)
@@ -937,8 +937,8 @@ __global__ __launch_bounds__(BS) void k_panel_dots(int n, const T* __restrict__ 
 // waited for it before the next (one memory latency per column: t(k) =
 // 8.6 + 0.50 k us for the dots on BAND-10M, tools/per_step.py).
 template <class T, int BS, int NC>
-__global__ __launch_bounds__(BS) void k_dots_nc(int n, const T* __restrict__ V, int64_t ld,
-                                                const T* __restrict__ w, double* __restrict__ partial) {
+__device__ __forceinline__ void dots_panel(int n, const T* __restrict__ V, int64_t ld, const T* __restrict__ w,
+                                           double* __restrict__ partial) {
     static_assert(NC >= 1 && NC <= kNC, "one panel");
     constexpr int NP = Pow2Ceil<NC>::v;
     constexpr int B = kColBatch<T>;
@@ -967,6 +967,28 @@ __global__ __launch_bounds__(BS) void k_dots_nc(int n, const T* __restrict__ V, 
         for (int c = 0; c < NC; ++c) acc[c] += (double)V[(int64_t)c * ld + i] * wi;
     }
     store_partials<NP, BS>(acc, NC, partial);
+}
+
+template <class T, int BS, int NC>
+__global__ __launch_bounds__(BS) void k_dots_nc(int n, const T* __restrict__ V, int64_t ld,
+                                                const T* __restrict__ w, double* __restrict__ partial) {
+    dots_panel<T, BS, NC>(n, V, ld, w, partial);
+}
+
+// V^T w for nc > kNC columns in ONE launch (GMRES(100): the round-3 form ran
+// one runtime-count k_panel_dots launch per 32 columns, each re-reading w and
+// waiting for every column in turn): blockIdx.y is the 32-column panel,
+// the last one holding NCL columns; blockIdx.x a row group. The grid keeps
+// about one workgroup per CU in total (gridDim.x = kCombineGroups / panels),
+// so each column gets gridDim.x <= 128 partials, [column][gridDim.x], which
+// the wide CGS update sums itself (k_cgs_update_wide).
+template <class T, int BS, int NCL>
+__global__ __launch_bounds__(BS) void k_dots_panels(int n, const T* __restrict__ V, int64_t ld,
+                                                    const T* __restrict__ w, double* __restrict__ partial) {
+    const int c0 = blockIdx.y * kNC;
+    double* __restrict__ part = partial + (size_t)c0 * gridDim.x;
+    if (blockIdx.y + 1 < gridDim.y) dots_panel<T, BS, kNC>(n, V + (int64_t)c0 * ld, ld, w, part);
+    else dots_panel<T, BS, NCL>(n, V + (int64_t)c0 * ld, ld, w, part);
 }
 
 // coef = T(sums[0..NC)); w = w - T(V coef); partial ||w'||^2 (the last
@@ -1076,6 +1098,87 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
         }
     }
     store_partials<NA, BS>(acc, NEXT_DOTS ? NC : 1, partial);
+}
+
+// The CGS update for kNC < nc <= kWideMax columns (GMRES(100)): the
+// coefficients are summed here from k_dots_panels' part_G <= 128 partials per
+// column (8 lanes per column, 16 branch-free loads each in g order, then an
+// xor tree: the same fixed order in every workgroup; no reduce launch), then
+// w = w - T(V coef) with 4 rows per lane, the columns in compile-time batches
+// of B (the last batch clamped to column nc - 1 with coefficient 0: +0 terms,
+// so t is the j-ordered sum of the real terms), and the ||w'||^2 partials.
+constexpr int kWideMax = 128;
+template <class T, int BS>
+__global__ __launch_bounds__(BS) void k_cgs_update_wide(int n, const T* __restrict__ V, int64_t ld, int nc,
+                                                        const double* __restrict__ parts, int part_G,
+                                                        T* __restrict__ coef_out, T* __restrict__ w,
+                                                        double* __restrict__ partial) {
+    constexpr int LPC = BS / kWideMax, Q = 128 / LPC, B = kColBatch<T>;
+    static_assert(LPC * kWideMax == BS && Q * LPC == 128, "8 lanes per column, <= 128 partials");
+    __shared__ double coef[kWideMax];
+    {
+        const int j = threadIdx.x / LPC, sub = threadIdx.x % LPC;
+        const int jc = j < nc ? j : nc - 1;
+        double pp[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int g = sub + LPC * q;
+            pp[q] = parts[(size_t)jc * part_G + (g < part_G ? g : 0)];
+        }
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            if (sub + LPC * q < part_G) v += pp[q];
+#pragma unroll
+        for (int o = LPC / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+        if (sub == 0) {
+            const T c = (T)v;
+            coef[j] = j < nc ? (double)c : 0.0;
+            if (blockIdx.x == 0 && j < nc) coef_out[j] = c;
+        }
+    }
+    __syncthreads();
+    double acc[1] = {0.0};
+    const int n4 = n & ~3;
+    const int nb = (nc + B - 1) / B;
+    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
+        Raw4<T> wr;
+        wr.load(w + i);
+        double t[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int bi = 0; bi < nb; ++bi) {
+            const int c0 = bi * B;
+            Raw4<T> v[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                const int c = c0 + u < nc ? c0 + u : nc - 1;
+                v[u].load(V + (int64_t)c * ld + i);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // keep the batch's loads issued back to back
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                const double cu = coef[c0 + u < kWideMax ? c0 + u : kWideMax - 1];
+                if (c0 + u < nc)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) t[r] += v[u][r] * cu;
+            }
+        }
+        T wo[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            wo[r] = T(-1) * (T)t[r] + T(1) * (T)wr[r];
+            const double wd = (double)wo[r];
+            acc[0] += wd * wd;
+        }
+        Row4<T>::store(w + i, wo);
+    }
+    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
+        double t = 0.0;
+        for (int j = 0; j < nc; ++j) t += (double)V[(int64_t)j * ld + i] * coef[j];
+        const T wi = T(-1) * (T)t + T(1) * w[i];
+        w[i] = wi;
+        acc[0] += (double)wi * (double)wi;
+    }
+    store_partials<1, BS>(acc, 1, partial);
 }
 
 // f(integral_constant<int, nc>) for 1 <= nc <= N
@@ -1345,6 +1448,64 @@ __global__ __launch_bounds__(kBlock) void k_trsv_upper(int k, int ldh, const T* 
     }
     for (int i = threadIdx.x; i < k; i += kBlock) y[i] = ys[i];
 }
+// The same solve for 64 < k <= 64 * KW by one wave64 (GMRES(100): the
+// one-lane-per-step form above took 92.6 us at k = 100, one workgroup barrier
+// pair per column). The upper triangle of H(0:k,0:k) is staged in LDS packed
+// by columns (column j at j(j+1)/2, dynamic shared memory) with one load
+// round; lane l holds y_{l + 64q} in register slot q. The column sweep is
+// the netlib order of k_trsv_upper (no contraction): y_j /= H(j,j) (when
+// y_j != 0), broadcast by a shuffle, then y_i -= y_j H(i,j) for i < j.
+// (kBlock threads stage H, 8 independent loads per lane per round; wave 0 solves)
+template <class T, int KW>
+__global__ __launch_bounds__(kBlock) void k_trsv_upper_lds(int k, int ldh, const T* __restrict__ H,
+                                                           T* __restrict__ y) {
+    extern __shared__ char trsv_smem[];
+    T* Hp = reinterpret_cast<T*>(trsv_smem);
+    const int lane = threadIdx.x;
+    const int P = k * (k + 1) / 2;
+    constexpr int U = 8;
+    for (int base = 0; base < P; base += kBlock * U) {
+        T v[U];
+        int e[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            e[u] = base + kBlock * u + (int)threadIdx.x;
+            const int ec = e[u] < P ? e[u] : P - 1;
+            // column j of packed entry ec: j(j+1)/2 <= ec < (j+1)(j+2)/2
+            int j = (int)((sqrtf(8.0f * (float)ec + 1.0f) - 1.0f) * 0.5f);
+            while (j * (j + 1) / 2 > ec) --j;
+            while ((j + 1) * (j + 2) / 2 <= ec) ++j;
+            v[u] = H[(int64_t)j * ldh + (ec - j * (j + 1) / 2)];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (e[u] < P) Hp[e[u]] = v[u];
+    }
+    __syncthreads();
+    if (threadIdx.x >= kWave) return;
+    T yr[KW];
+#pragma unroll
+    for (int q = 0; q < KW; ++q) yr[q] = lane + kWave * q < k ? y[lane + kWave * q] : T(0);
+    for (int j = k - 1; j >= 0; --j) {
+        const int jq = j / kWave, jl = j % kWave;
+        T mine = yr[0];
+#pragma unroll
+        for (int q = 1; q < KW; ++q)
+            if (q == jq) mine = yr[q];
+        T yj = __shfl(mine, jl, kWave);
+        if (yj != T(0)) yj = yj / Hp[j * (j + 1) / 2 + j];
+#pragma unroll
+        for (int q = 0; q < KW; ++q) {
+            const int i = lane + kWave * q;
+            if (q == jq && lane == jl) yr[q] = yj;
+            if (yj != T(0) && i < j) yr[q] = yr[q] - yj * Hp[j * (j + 1) / 2 + i];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < KW; ++q)
+        if (lane + kWave * q < k) y[lane + kWave * q] = yr[q];
+}
+
 // The same upper solve by one wave64 (k <= 64): lane i holds y_i, the
 // column sweep's scalar is broadcast with a shuffle, H(0:k,0:k) is in LDS
 // (column j at Hs[j * 64]). No barrier inside the sweep.
@@ -1917,6 +2078,7 @@ int mpg_arnoldi_spmv_dots(mpg_arnoldi_t a, int k, int fold) {
 int mpg_arnoldi_givens_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 1); }
 int mpg_arnoldi_givens_partials_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 2); }
 int mpg_arnoldi_fold_max_m(void) { return kFoldMaxM; }
+int mpg_arnoldi_partials_max_cols(void) { return kWideMax; }
 
 // The folded Givens step costs every SpMV workgroup the sum of the previous
 // launch's partials and two barriers; a separate Givens launch costs ~4.6 us.
@@ -1935,6 +2097,14 @@ int mpg_arnoldi_fold_pays(mpg_arnoldi_t a) {
     if (S.nslices == 0) return a->Grb <= limit ? 1 : 0;
     const int per_group = (kStepSellBlock / kWave) * (sell_uniform(S) && sell_pair(S) ? 2 : 1);
     return (S.nslices + per_group - 1) / per_group <= limit ? 1 : 0;
+}
+
+// row groups per panel of k_dots_panels: about one workgroup per CU in all
+// (the same on every rank: uniform groups set Gd = kCombineGroups), so each
+// column has <= kCombineGroups / 2 partials for k_cgs_update_wide
+static int wide_groups(const mpg_arnoldi* a, int ncols) {
+    const int np = (ncols + kNC - 1) / kNC;
+    return std::max(1, std::min(a->Gd, kCombineGroups / np));
 }
 
 static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
@@ -1956,6 +2126,16 @@ static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
                 return (int)MPG_OK;
             });
         }
+        if (ndots_all <= kWideMax) {  // every panel in one launch -> wide_groups(a, k) partials per column
+            const int np = (ndots_all + kNC - 1) / kNC;
+            return with_nc<kNC>(ndots_all - (np - 1) * kNC, [&](auto ncl) {
+                k_dots_panels<T, kCombineBlock, decltype(ncl)::value>
+                    <<<dim3(wide_groups(a, ndots_all), np), kCombineBlock, 0, a->ctx->stream>>>(
+                        a->d.n, static_cast<const T*>(a->V), a->ld, static_cast<const T*>(a->w[(k + 1) & 1]),
+                        a->dpart);
+                return (int)MPG_OK;
+            });
+        }
         for (int c0 = 0; c0 < ndots_all; c0 += kNC) {
             const int nc = ndots_all - c0 < kNC ? ndots_all - c0 : kNC;
             k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
@@ -1964,8 +2144,9 @@ static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
         }
         return (int)MPG_OK;
     });
-    a->last_G = combine || ndots_all <= kNC ? a->Gd : row_grid(a);
-    a->last_part = !combine && ndots_all <= kNC ? a->dpart : a->partial;
+    const bool wide = !combine && ndots_all > kNC && ndots_all <= kWideMax;
+    a->last_G = combine || ndots_all <= kNC ? a->Gd : wide ? wide_groups(a, ndots_all) : row_grid(a);
+    a->last_part = !combine && ndots_all <= kWideMax ? a->dpart : a->partial;
     if (st) return st;
     MPG_LAUNCH_CHECK(a->ctx);
     return MPG_OK;
@@ -1981,7 +2162,8 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
     if (givens && (next_dots || a->d.m > kFoldMaxM || from_partials)) return MPG_ERR_ARG;
     // from_partials: the coefficients are summed from the preceding one-panel
     // dots' partials inside this launch (no reduce launch)
-    if (from_partials && (pass != 0 || k + 1 > kNC || a->last_part != a->dpart)) return MPG_ERR_ARG;
+    if (from_partials && (pass != 0 || k + 1 > kWideMax || a->last_part != a->dpart)) return MPG_ERR_ARG;
+    if (from_partials && k + 1 > kNC && (next_dots || a->last_G > kWideMax)) return MPG_ERR_ARG;
     const double* src = from_partials ? a->dpart : a->sums;
     const int part_G = from_partials ? a->last_G : 0;  // Gd (k_dots_nc) or fd_ng (k_step_sell's dots)
     if (part_G > kCombineGroups) return MPG_ERR_ARG;
@@ -2013,6 +2195,9 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
         } else if (givens) {
             k_cgs_update<T, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, a->counters + 32, g, 0);
+        } else if (from_partials && k + 1 > kNC) {  // GMRES(100): sums from k_dots_panels' partials
+            k_cgs_update_wide<T, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
+                a->d.n, static_cast<const T*>(a->V), a->ld, k + 1, src, part_G, coef_out, w, a->partial);
         } else if (k + 1 <= kNC) {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
             return with_nc<kNC>(k + 1, [&](auto nc) {
                 constexpr int NC = decltype(nc)::value;
@@ -2101,8 +2286,13 @@ int mpg_arnoldi_update(mpg_arnoldi_t a, int k) {
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, static_cast<const T*>(a->s()),
                 static_cast<const T*>(a->H), a->d.m + 1, static_cast<X*>(a->d.x));
         } else {
-            k_trsv_upper<T><<<1, kBlock, 0, a->ctx->stream>>>(k, a->d.m + 1, static_cast<const T*>(a->H),
-                                                              static_cast<T*>(a->s()));
+            const size_t packed = (size_t)k * (k + 1) / 2 * sizeof(T);
+            if (k <= 2 * kWave && packed <= 65536)
+                k_trsv_upper_lds<T, 2><<<1, kBlock, packed, a->ctx->stream>>>(
+                    k, a->d.m + 1, static_cast<const T*>(a->H), static_cast<T*>(a->s()));
+            else
+                k_trsv_upper<T><<<1, kBlock, 0, a->ctx->stream>>>(k, a->d.m + 1, static_cast<const T*>(a->H),
+                                                                  static_cast<T*>(a->s()));
             k_update_x<T, X, false><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k, static_cast<const T*>(a->s()), nullptr, 0,
                 static_cast<X*>(a->d.x));

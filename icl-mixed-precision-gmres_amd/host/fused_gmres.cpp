@@ -523,17 +523,22 @@ void FusedEngine::step(int k, bool fold) {
         // MPG_CGS_PARTIALS=1 (one GPU, k+1 <= 32): the CGS update sums the dots
         // partials itself; MPG_COMBINE=1: the dots' last workgroup writes the
         // sums and the last CGS pass's last workgroup runs the Givens step
-        const bool small = k + 1 <= 32;
+        // (one GPU, plain CGS: up to 128 columns -- GMRES(100) -- the wide
+        // update sums the one-launch panel dots' partials itself)
+        const bool small = k + 1 <= 32 || (!I.comm && I.orth == MPG_ORTH_CGS && k + 1 <= mpg_arnoldi_partials_max_cols());
         const int last_pass = I.orth == MPG_ORTH_CGSR ? 1 : 0;
         bool pass0_done = false;
-        if (I.combine && small) {
+        if (I.combine && k + 1 <= 32) {
             check(mpg_arnoldi_dots_sums(I.arn, k), "dots+sums", I.ctx);
         } else {
             timed(3, [&] { check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx); });
             check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
+            timed_end(3);
             if (I.cgs_partials && small) {
                 if (I.comm) allreduce_partials(k + 1);
+                timed(2, [&] { check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx); });
                 check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx);
+                timed_end(2);
                 pass0_done = true;
             } else {
                 reduce(k + 1);
@@ -552,6 +557,7 @@ void FusedEngine::step(int k, bool fold) {
         }
         timed(2, [&] { check(mpg_arnoldi_cgs(I.arn, k, last_pass), "cgs", I.ctx); });
         check(mpg_arnoldi_cgs(I.arn, k, last_pass), "cgs", I.ctx);
+        timed_end(2);
     }
     if (!fold) givens(k);
 }
@@ -940,15 +946,17 @@ void FusedEngine::timed_end(int phase) {
     I.marks.push_back(e1);
 }
 
-// The Arnoldi SpMV timed inside graph replays of the cycle: the cycle is
-// captured once more with an external event node on each side of every
-// SpMV launch, and that graph is replayed `reps` times (each replay
+// A phase kernel timed inside graph replays of the cycle (which: 0 the
+// Arnoldi SpMV, 2 the CGS update, 3 the panel dots): the cycle is captured
+// once more with an external event node on each side of every launch of
+// that phase, and that graph is replayed `reps` times (each replay
 // re-records the events; they are read after it). Measurement only, like
 // time_phase: the replays run without the host's restart checks.
-double FusedEngine::time_spmv_graph(int reps, std::vector<double>* per_launch) {
+double FusedEngine::time_phase_graph(int which, int reps, std::vector<double>* per_launch) {
     Impl& I = *p_;
     if (!I.use_graph) throw StatusError(MPG_ERR_UNSUPPORTED, "the cycle is not captured (MPG_NO_GRAPH / eager ranks)");
-    I.timed = 0;
+    if (which != 0 && which != 2 && which != 3) throw std::invalid_argument("phase: 0 spmv, 2 cgs update, 3 dots");
+    I.timed = which;
     I.timed_graph = true;
     I.marks.clear();
     hipGraph_t g = nullptr;
@@ -1107,12 +1115,15 @@ int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, dou
     }
 }
 
-int mpg_engine_time_spmv_graph(mpg_engine_t e, int reps, double* avg_ms, double* per_launch_ms, int cap) {
-    if (!e || !e->eng || !avg_ms || reps < 1 || cap < 0 || (cap && !per_launch_ms)) return MPG_ERR_ARG;
+int mpg_engine_time_phase_graph(mpg_engine_t e, int which, int reps, double* avg_ms, double* per_launch_ms,
+                                int cap) {
+    if (!e || !e->eng || !avg_ms || reps < 1 || cap < 0 || (cap && !per_launch_ms) ||
+        (which != 0 && which != 2 && which != 3))
+        return MPG_ERR_ARG;
     try {
         mpg::ScopedContext scope(e->ctx);
         std::vector<double> t;
-        *avg_ms = e->eng->time_spmv_graph(reps, &t);
+        *avg_ms = e->eng->time_phase_graph(which, reps, &t);
         for (size_t i = 0; i < t.size() && (int)i < cap; ++i) per_launch_ms[i] = t[i];
         return (int)t.size();
     } catch (const mpg::StatusError& ex) {

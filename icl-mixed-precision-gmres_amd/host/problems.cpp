@@ -230,6 +230,119 @@ int mpg_gen_stencil27(int32_t nx, int32_t ny, int32_t nz, int32_t dof, uint64_t 
     return emit(out, (int32_t)n, (int32_t)n, rp, ci, va);
 }
 
+int mpg_gen_fem27(int32_t nx, int32_t ny, int32_t nz, int32_t dof, int32_t keep_pct, uint64_t seed,
+                  mpg_host_csr* out) {
+    if (!out || nx <= 0 || ny <= 0 || nz <= 0 || dof <= 0 || dof > 8 || keep_pct < 0 || keep_pct > 100) return -2;
+    const int64_t nodes = (int64_t)nx * ny * nz, n = nodes * dof;
+    if (n > INT32_MAX || n * 27 * dof > INT32_MAX) return -2;
+    // an undirected node pair {a, b} is coupled when its hash falls under
+    // keep_pct %: the same decision from both ends, so the pattern (and, with
+    // the values keyed on the unordered unknown pair, A) is symmetric
+    auto kept = [&](int64_t a, int64_t b) {
+        if (a == b) return true;
+        const int64_t lo = std::min(a, b), hi = std::max(a, b);
+        return mix64(seed * 0x2545f4914f6cdd1dULL ^ mix64((uint64_t)lo * 0x9e3779b97f4a7c15ULL + (uint64_t)hi)) % 100 <
+               (uint64_t)keep_pct;
+    };
+    std::vector<int32_t> rp((size_t)n + 1), ci;
+    std::vector<double> va;
+    ci.reserve((size_t)(n * 27 * dof * (keep_pct + 5) / 100));
+    va.reserve(ci.capacity());
+    for (int32_t z = 0; z < nz; ++z)
+        for (int32_t y = 0; y < ny; ++y)
+            for (int32_t x = 0; x < nx; ++x) {
+                const int64_t node = x + (int64_t)nx * (y + (int64_t)ny * z);
+                for (int32_t d = 0; d < dof; ++d) {
+                    const int64_t i = node * dof + d;
+                    rp[(size_t)i] = (int32_t)ci.size();
+                    double offsum = 0.0;
+                    size_t diag_slot = 0;
+                    for (int dz = -1; dz <= 1; ++dz)
+                        for (int dy = -1; dy <= 1; ++dy)
+                            for (int dx = -1; dx <= 1; ++dx) {
+                                const int32_t X = x + dx, Y = y + dy, Z = z + dz;
+                                if (X < 0 || X >= nx || Y < 0 || Y >= ny || Z < 0 || Z >= nz) continue;
+                                const int64_t nb = X + (int64_t)nx * (Y + (int64_t)ny * Z);
+                                if (!kept(node, nb)) continue;
+                                for (int32_t e = 0; e < dof; ++e) {
+                                    const int64_t c = nb * dof + e;
+                                    ci.push_back((int32_t)c);
+                                    if (c == i) {
+                                        diag_slot = va.size();
+                                        va.push_back(0.0);
+                                    } else {
+                                        const int64_t a = std::min(i, c), b = std::max(i, c);
+                                        const double v = -unit_double(seed ^ (uint64_t)b, a, 0);
+                                        offsum += std::fabs(v);
+                                        va.push_back(v);
+                                    }
+                                }
+                            }
+                    va[diag_slot] = 1.0 + offsum;
+                }
+            }
+    rp[(size_t)n] = (int32_t)ci.size();
+    return emit(out, (int32_t)n, (int32_t)n, rp, ci, va);
+}
+
+int mpg_perm_node_blocks(int64_t nodes, int32_t dof, int32_t block, uint64_t seed, int32_t* perm) {
+    if (nodes <= 0 || dof <= 0 || block <= 0 || !perm || nodes * dof > INT32_MAX) return -2;
+    const int64_t nb = (nodes + block - 1) / block;
+    std::mt19937_64 rng(seed);
+    std::vector<int64_t> order((size_t)nb);
+    std::iota(order.begin(), order.end(), 0);
+    std::shuffle(order.begin(), order.end(), rng);  // block q goes to position pos[q]
+    std::vector<int64_t> pos((size_t)nb);
+    for (int64_t p = 0; p < nb; ++p) pos[(size_t)order[(size_t)p]] = p;
+    // new node positions: the blocks in shuffled order, each block's nodes
+    // shuffled inside it (the last, short block keeps its size wherever it lands)
+    std::vector<int64_t> start((size_t)nb + 1, 0);
+    for (int64_t p = 0; p < nb; ++p) {
+        const int64_t q = order[(size_t)p];
+        start[(size_t)p + 1] = start[(size_t)p] + std::min<int64_t>(block, nodes - q * block);
+    }
+    std::vector<int64_t> inner((size_t)block);
+    for (int64_t q = 0; q < nb; ++q) {
+        const int64_t len = std::min<int64_t>(block, nodes - q * block);
+        std::iota(inner.begin(), inner.begin() + len, 0);
+        std::shuffle(inner.begin(), inner.begin() + len, rng);
+        for (int64_t t = 0; t < len; ++t) {
+            const int64_t old_node = q * block + t, new_node = start[(size_t)pos[(size_t)q]] + inner[(size_t)t];
+            for (int32_t d = 0; d < dof; ++d) perm[old_node * dof + d] = (int32_t)(new_node * dof + d);
+        }
+    }
+    return 0;
+}
+
+int mpg_csr_permute_sym(const mpg_host_csr* a, const int32_t* perm, mpg_host_csr* out) {
+    if (!a || !perm || !out || a->nrows != a->ncols || a->nrows < 0) return -2;
+    const int64_t n = a->nrows;
+    std::vector<int32_t> inv((size_t)n, -1);
+    for (int64_t i = 0; i < n; ++i) {
+        if (perm[i] < 0 || perm[i] >= n || inv[(size_t)perm[i]] >= 0) return -2;  // not a permutation
+        inv[(size_t)perm[i]] = (int32_t)i;
+    }
+    std::vector<int32_t> rp((size_t)n + 1, 0), ci((size_t)a->nnz);
+    std::vector<double> va((size_t)a->nnz);
+    for (int64_t r = 0; r < n; ++r) {
+        const int32_t i = inv[(size_t)r];
+        rp[(size_t)r + 1] = rp[(size_t)r] + (a->rowptr[i + 1] - a->rowptr[i]);
+    }
+    std::vector<std::pair<int32_t, double>> row;
+    for (int64_t r = 0; r < n; ++r) {
+        const int32_t i = inv[(size_t)r];
+        row.clear();
+        for (int32_t e = a->rowptr[i]; e < a->rowptr[i + 1]; ++e) row.emplace_back(perm[a->col[e]], a->val[e]);
+        // each row sorted by column (LoadMatrix.hpp:128-145 semantics; stable for duplicates)
+        std::stable_sort(row.begin(), row.end(), [](const auto& u, const auto& v) { return u.first < v.first; });
+        for (size_t t = 0; t < row.size(); ++t) {
+            ci[(size_t)rp[(size_t)r] + t] = row[t].first;
+            va[(size_t)rp[(size_t)r] + t] = row[t].second;
+        }
+    }
+    return emit(out, (int32_t)n, (int32_t)n, rp, ci, va);
+}
+
 int mpg_gen_spec(const char* spec, mpg_host_csr* out, char* err, int errlen) {
     auto fail = [&](const char* what) {
         if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", what);
@@ -262,7 +375,35 @@ int mpg_gen_spec(const char* spec, mpg_host_csr* out, char* err, int errlen) {
             return fail("bad stencil27 spec");
         return 0;
     }
-    return fail("unknown --matrix spec (band:N[:LO:HI[:SEED]], laplace:NX[:NY:NZ] or stencil27:NX[:DOF[:SEED]])");
+    // stencil27p / fem27: the irregular stand-ins (a symmetric permutation of
+    // node blocks; a randomly thinned 27-point coupling with variable rows)
+    auto permute = [&](long long block, long long pseed, int dof) {
+        if (block <= 0) return 0;
+        const int64_t n = out->nrows;
+        std::vector<int32_t> perm((size_t)n);
+        if (mpg_perm_node_blocks(n / dof, dof, (int32_t)block, (uint64_t)pseed, perm.data()) != 0) return -2;
+        mpg_host_csr b{};
+        const int st = mpg_csr_permute_sym(out, perm.data(), &b);
+        mpg_host_csr_free(out);
+        *out = b;
+        return st;
+    };
+    if (f[0] == "stencil27p" && f.size() >= 2) {
+        const int nx = (int)num(1, 0), dof = (int)num(2, 3);
+        if (mpg_gen_stencil27(nx, nx, nx, dof, (uint64_t)num(3, 11), out) != 0 ||
+            permute(num(4, 64), num(5, 5), dof) != 0)
+            return fail("bad stencil27p spec");
+        return 0;
+    }
+    if (f[0] == "fem27" && f.size() >= 2) {
+        const int nx = (int)num(1, 0), dof = (int)num(2, 3);
+        if (mpg_gen_fem27(nx, nx, nx, dof, (int)num(3, 70), (uint64_t)num(4, 13), out) != 0 ||
+            permute(num(5, 0), num(6, 5), dof) != 0)
+            return fail("bad fem27 spec");
+        return 0;
+    }
+    return fail("unknown --matrix spec (band:N[:LO:HI[:SEED]], laplace:NX[:NY:NZ], stencil27:NX[:DOF[:SEED]], "
+                "stencil27p:NX[:DOF[:SEED[:BLOCK[:PSEED]]]] or fem27:NX[:DOF[:KEEP%[:SEED[:BLOCK[:PSEED]]]]])");
 }
 
 int mpg_load_mtx(const char* path, mpg_host_csr* out, char* err, int errlen) {

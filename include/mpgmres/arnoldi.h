@@ -113,10 +113,12 @@ int mpg_arnoldi_prologue_wnorm(mpg_arnoldi_t a);
 int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k);           /* w = M(A v_k), V(:,k) */
 int mpg_arnoldi_dots(mpg_arnoldi_t a, int k);           /* partials: k+1 (CGS/CGSR) or 1 (MGS) */
 int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass);  /* pass 0: h; pass 1: CGSR correction */
-/* one GPU, k+1 <= 32: CGS pass 0 that sums the preceding mpg_arnoldi_dots
- * partials itself (every workgroup, same fixed order) — replaces
- * mpg_arnoldi_reduce + mpg_arnoldi_cgs(a, k, 0) */
+/* one GPU, k+1 <= 32 (plain CGS: k+1 <= mpg_arnoldi_partials_max_cols()):
+ * CGS pass 0 that sums the preceding mpg_arnoldi_dots partials itself
+ * (every workgroup, same fixed order) — replaces mpg_arnoldi_reduce +
+ * mpg_arnoldi_cgs(a, k, 0) */
 int mpg_arnoldi_cgs_partials(mpg_arnoldi_t a, int k);
+int mpg_arnoldi_partials_max_cols(void);
 int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j);
 /* one GPU: MGS update j taking h_jk from the partials of the previous launch
  * (mpg_arnoldi_dots for j = 0, the previous update otherwise) — replaces

@@ -46,9 +46,29 @@ int mpg_gen_laplace3d(int32_t nx, int32_t ny, int32_t nz, mpg_host_csr* out);
  * rows, ~3.2e8 nnz. */
 int mpg_gen_stencil27(int32_t nx, int32_t ny, int32_t nz, int32_t dof, uint64_t seed, mpg_host_csr* out);
 
+/* FEM-like irregular stand-in: the 27-point node coupling of
+ * mpg_gen_stencil27 with each undirected node pair kept with probability
+ * keep_pct / 100 (a hash of the pair, so the pattern is symmetric): rows of
+ * dof x (1 + kept neighbours) entries, i.e. variable lengths (24..81 at dof 3
+ * and most keep values). Values as mpg_gen_stencil27 (symmetric, diagonal
+ * 1 + sum|off|). */
+int mpg_gen_fem27(int32_t nx, int32_t ny, int32_t nz, int32_t dof, int32_t keep_pct, uint64_t seed,
+                  mpg_host_csr* out);
+/* perm[old] = new for nodes * dof unknowns: blocks of `block` consecutive
+ * nodes placed in a seeded random order (mt19937_64), nodes shuffled within
+ * each block, a node's dof kept together — a mesh-like ordering with local
+ * runs and scattered neighbours (Queen_4147-like), not a uniform scatter. */
+int mpg_perm_node_blocks(int64_t nodes, int32_t dof, int32_t block, uint64_t seed, int32_t* perm);
+/* B = P A P^T (row perm[i] of B = row i of A, columns c -> perm[c], each row
+ * sorted by column): the same spectrum under a symmetric renumbering. */
+int mpg_csr_permute_sym(const mpg_host_csr* a, const int32_t* perm, mpg_host_csr* out);
+
 /* One of the generators above from a CLI spec: "band:N[:LO:HI[:SEED]]"
  * (defaults 5, 4, 7), "laplace:NX[:NY:NZ]", "stencil27:NX[:DOF[:SEED]]"
- * (defaults 3, 11). Returns 0, or -2 with a message in err. */
+ * (defaults 3, 11), "stencil27p:NX[:DOF[:SEED[:BLOCK[:PSEED]]]]" (stencil27
+ * under mpg_perm_node_blocks; defaults block 64, pseed 5),
+ * "fem27:NX[:DOF[:KEEP%[:SEED[:BLOCK[:PSEED]]]]]" (defaults 3, 70, 13, 0 =
+ * natural order, 5). Returns 0, or -2 with a message in err. */
 int mpg_gen_spec(const char* spec, mpg_host_csr* out, char* err, int errlen);
 
 /* Matrix Market coordinate real|integer, general|symmetric, loaded as

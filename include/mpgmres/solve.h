@@ -131,11 +131,14 @@ int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms);
  * `cap` per-launch times in cycle order (measurement only: the cycles run
  * without the host's restart checks) */
 int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, double* per_launch_ms, int cap);
-/* the same SpMV timed inside graph replays of the cycle: the cycle captured
- * with an external event node on each side of every SpMV launch, replayed
- * `reps` times (returns the launch count, m per replay; MPG_ERR_UNSUPPORTED
- * when the engine runs eagerly) */
-int mpg_engine_time_spmv_graph(mpg_engine_t e, int reps, double* avg_ms, double* per_launch_ms, int cap);
+/* a phase kernel timed inside graph replays of the cycle (which: 0 the
+ * Arnoldi SpMV, 2 the CGS update, 3 the panel dots): the cycle captured with
+ * an external event node on each side of every launch of that phase,
+ * replayed `reps` times; per-launch times in cycle order (step k), the
+ * launch count returned (m per replay for 0; MPG_ERR_UNSUPPORTED when the
+ * engine runs eagerly). Measurement only, like the in-cycle timing above. */
+int mpg_engine_time_phase_graph(mpg_engine_t e, int which, int reps, double* avg_ms, double* per_launch_ms,
+                                int cap);
 /* algorithmic bytes of one launch of phase `which` */
 double mpg_engine_phase_bytes(mpg_engine_t e, int which);
 /* storage of the engine's Arnoldi SpMV (mpg_arnoldi_spmv_layout) */

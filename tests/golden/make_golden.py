@@ -16,6 +16,7 @@ normalisations, the per-step Arnoldi residuals |s(k+1)|, iteration counts,
 final resNorm/errNorm and a checksum of x.
 
 Usage: python tests/golden/make_golden.py   (writes tests/golden/gmres_golden.json)
+       python tests/golden/make_golden.py --m100   (GMRES(100) records: gmres_golden_m100.json)
 """
 import json
 import sys
@@ -83,7 +84,22 @@ for mat in ("lap10", "band2000", "convdiff32"):
                               jacobi_steps=3))
 
 
+# GMRES(100), the restart length of every published reference number
+# (automated.py:41, the notebook's timings at rlen '100'): identity / Jacobi
+# x 4 modes x 3 orthogonalisations, in their own file (gmres_golden_m100.json)
+CASES_M100 = []
+for mat in ("lap10", "band2000", "convdiff32"):
+    for mode in ("mixed", "baseline", "single-prec", "single"):
+        for orth in ("cgs", "mgs", "cgsr"):
+            for prec in ("identity", "jacobi"):
+                tol = 1e-5 if mode == "single" else 1e-10
+                CASES_M100.append(dict(matrix=mat, mode=mode, orth=orth, prec=prec, rlen=100, tol=tol,
+                                       max_restarts=200))
+
+
 def main():
+    m100 = "--m100" in sys.argv
+    cases, fname = (CASES_M100, "gmres_golden_m100.json") if m100 else (CASES, "gmres_golden.json")
     mpg = load_package()
     from oracle import binding
 
@@ -93,7 +109,7 @@ def main():
         xt = mpg.rand_vect(A.nrows, 42)
         b = mpg.host_spmv(A, xt)
         out["inputs"][name] = {"n": A.nrows, "checksum": checksum(A), "b_sum": float(b.sum())}
-    for case in CASES:
+    for case in cases:
         A = mats[case["matrix"]]
         xt = mpg.rand_vect(A.nrows, 42)
         b = mpg.host_spmv(A, xt)
@@ -105,7 +121,7 @@ def main():
             cyc_r_norm=r.cyc_r_norm.tolist(), cyc_normalization=r.cyc_normalization.tolist(),
             cyc_beta=r.cyc_beta.tolist(), step_res=r.step_res.tolist(),
             x_sum=float(r.x.sum()), x_head=r.x[:16].tolist()))
-    (HERE / "gmres_golden.json").write_text(json.dumps(out, indent=0))
+    (HERE / fname).write_text(json.dumps(out, indent=0))
     print(f"wrote {len(out['cases'])} cases, backend {out['backend']}")
 
 

@@ -1,0 +1,77 @@
+"""GMRES(100), the restart length of every published reference number
+(automated.py:41 defaults --rlen to 100; the notebook's timings are all
+rlen '100'). At m = 100 the cycle runs other kernels than at m = 30: the
+V^T w panel dots for k + 1 > 32 in one two-dimensional launch
+(k_dots_panels), the CGS update summing their partials itself
+(k_cgs_update_wide, up to 128 columns), the Givens step folded into the SpMV
+up to m = 128, the LDS-staged one-wave trsv (k > 64) before the solution
+update. Parity: the golden records at m = 100 (tests/golden/
+gmres_golden_m100.json, made by the oracle) on both engines, and the live
+oracle on a BAND matrix large enough that every panel kernel runs many
+workgroups (Orthogonalization.hpp:76-136, gmres.cpp:210-242)."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from tests.golden.make_golden import inputs
+from tests.parity import as_ref, compare
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.loads((Path(__file__).parent / "golden" / "gmres_golden_m100.json").read_text())
+
+
+@pytest.fixture(scope="module")
+def mats(mpg):
+    return inputs(mpg)
+
+
+def _case_id(c):
+    k = c["case"]
+    return f"{k['matrix']}-{k['mode']}-{k['orth']}-{k['prec']}-m{k['rlen']}"
+
+
+@pytest.mark.parametrize("engine", ["fused", "surface"])
+@pytest.mark.parametrize("rec", GOLDEN["cases"], ids=_case_id)
+def test_golden_m100(mpg, mats, rec, engine):
+    case = dict(rec["case"])
+    A = mats[case.pop("matrix")]
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    got = mpg.solve(A, b, xt, engine=engine, **case)
+    compare(rec, got, case["mode"], case["tol"], case["rlen"], _case_id(rec) + "/" + engine)
+
+
+@pytest.mark.parametrize("engine", ["fused", "surface"])
+@pytest.mark.parametrize("mode,orth", [("mixed", "cgs"), ("baseline", "cgs"), ("mixed", "cgsr"), ("mixed", "mgs")])
+def test_band_m100_live_oracle(mpg, oracle, engine, mode, orth):
+    """n = 300k (~73 one-per-CU workgroups per panel row group at k + 1 = 100:
+    the two-level partial sums run for real), 2 restart cycles at tol = 0 then
+    compared cycle by cycle with the oracle."""
+    A = mpg.gen_band(300_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=100, tol=0.0, max_restarts=2)
+    ref = oracle.solve(mpg, A, b, xt, **opts)
+    got = mpg.solve(A, b, xt, engine=engine, **opts)
+    assert got.total_iters == ref.total_iters == 200
+    compare(as_ref(ref), got, mode, 0.0, 100, f"band300k-{mode}-{orth}-m100/{engine}")
+    if mode == "mixed":  # the whole history, not only cycle 0
+        np.testing.assert_allclose(got.step_res, ref.step_res, rtol=1e-3, atol=1e-6 * ref.minvb_norm)
+
+
+def test_band_m100_engine_layout(mpg):
+    """The bench configuration at m = 100 folds the Givens step into the SpMV
+    (kFoldMaxM = 128) and takes the paired SELL kernel."""
+    A = mpg.gen_band(200_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    eng = mpg.Engine(A, b, xt, mode="mixed", orth="cgs", prec="identity", rlen=100, tol=0.0, max_restarts=3)
+    lay = eng.spmv_layout()
+    ran, done = eng.run(2)
+    res = eng.report()
+    eng.close()
+    assert lay["givens_folded"] and lay["slices_per_wave"] == 2, lay
+    assert ran == 2 and res.total_iters == 200 and np.all(np.isfinite(res.step_res))

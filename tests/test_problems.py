@@ -122,3 +122,69 @@ def test_mtx_loader_stops_on_a_text_size_line(mpg, tmp_path):
     p.write_text("%%MatrixMarket matrix coordinate real general\nthree by three\nno numbers here\n")
     with pytest.raises(ValueError, match="Malformed matrix size information"):
         mpg.load_mtx(str(p))
+
+
+def test_node_block_permutation(mpg):
+    """mpg_perm_node_blocks: a permutation; a node's dof stay together and in
+    order; each block of `block` consecutive nodes lands on one run of
+    consecutive new nodes (mesh-like locality), in a shuffled block order."""
+    nodes, dof, block = 1000, 3, 64
+    perm = mpg.perm_node_blocks(nodes, dof, block, seed=5)
+    assert np.array_equal(np.sort(perm), np.arange(nodes * dof))
+    p = perm.reshape(nodes, dof)
+    assert np.all(p[:, 0] % dof == 0) and np.all(np.diff(p, axis=1) == 1)
+    new_node = p[:, 0] // dof
+    for q in range(0, nodes, block):
+        run = np.sort(new_node[q:q + block])
+        assert np.all(np.diff(run) == 1)
+    assert not np.array_equal(new_node, np.arange(nodes))
+    assert np.array_equal(perm, mpg.perm_node_blocks(nodes, dof, block, seed=5))
+
+
+def test_permute_sym_matches_scipy(mpg):
+    A = mpg.gen_stencil27(9, 3)
+    perm = mpg.perm_node_blocks(A.nrows // 3, 3, 16, seed=7)
+    B = mpg.permute_sym(A, perm)
+    import scipy.sparse as sp
+
+    P = sp.csr_matrix((np.ones(A.nrows), (perm, np.arange(A.nrows))), shape=(A.nrows, A.nrows))
+    ref = (P @ A.to_scipy() @ P.T).tocsr()
+    ref.sort_indices()
+    Bs = B.to_scipy()
+    assert np.array_equal(Bs.indptr, ref.indptr) and np.array_equal(Bs.indices, ref.indices)
+    assert np.array_equal(Bs.data, ref.data)
+    # same spectrum: the same multiset of values and a symmetric matrix
+    assert np.array_equal(np.sort(B.val), np.sort(A.val)) and abs(Bs - Bs.T).max() == 0
+    with pytest.raises(ValueError):
+        mpg.permute_sym(A, np.zeros(A.nrows, np.int32))
+
+
+def test_fem27_irregular_rows(mpg):
+    """The FEM-like stand-in: symmetric, strictly diagonally dominant, each
+    row dof x (1 + kept neighbours) long -- variable lengths -- with the
+    explicit diagonal and sorted columns LoadMatrix.hpp guarantees."""
+    A = mpg.gen_fem27(14, 3, keep_pct=70, seed=13)
+    S = A.to_scipy()
+    assert abs(S - S.T).max() == 0
+    d = S.diagonal()
+    assert np.all(d > abs(S).sum(axis=1).A1 - abs(d))
+    rl = np.diff(A.rowptr)
+    assert np.all(rl % 3 == 0) and rl.min() >= 3 and rl.max() <= 81 and len(np.unique(rl)) > 10
+    assert 30 <= np.median(rl) <= 66
+    for i in range(0, A.nrows, 97):
+        c = A.col[A.rowptr[i]:A.rowptr[i + 1]]
+        assert np.all(np.diff(c) > 0) and i in c
+    full = mpg.gen_fem27(6, 2, keep_pct=100, seed=1)
+    st = mpg.gen_stencil27(6, 2, seed=1)
+    assert np.array_equal(full.rowptr, st.rowptr) and np.array_equal(full.col, st.col)
+
+
+def test_irregular_specs(mpg):
+    A = mpg.gen_spec("stencil27p:10:3:11:8:5")
+    ref = mpg.gen_stencil27p(10, 3, seed=11, block=8, perm_seed=5)
+    assert np.array_equal(A.col, ref.col) and np.array_equal(A.val, ref.val)
+    F = mpg.gen_spec("fem27:8")
+    G = mpg.gen_fem27(8, 3, 70, 13)
+    assert np.array_equal(F.col, G.col) and np.array_equal(F.val, G.val)
+    Fp = mpg.gen_spec("fem27:8:3:70:13:16:5")
+    assert Fp.nnz == F.nnz and not np.array_equal(Fp.col, F.col)

@@ -41,7 +41,14 @@ def main():
     eng.run(args.warm)
     eng.sync()
     e_ms, e_per = eng.time_spmv_incycle(args.eager)
-    g_ms, g_per = eng.time_spmv_graph(args.graph)
+    g_ms, g_per = eng.time_phase_graph("spmv", args.graph)
+    phases = {}
+    for ph in ("dots", "cgs_update"):
+        ms, per = eng.time_phase_graph(ph, args.graph)
+        m = args.rlen
+        byk = np.asarray(per[:len(per) // m * m]).reshape(-1, m).mean(axis=0) * 1e3
+        b, a = np.polyfit(np.arange(m), byk, 1)
+        phases[ph] = {"mean_us": round(1e3 * ms, 3), "fit_a_us": round(float(a), 3), "fit_b_us": round(float(b), 4)}
     lay = eng.spmv_layout()
     eng.close()
     m = args.rlen
@@ -50,6 +57,7 @@ def main():
         "blocks": {"warm_graph": args.warm * m, "eager_events": len(e_per), "graph_events": len(g_per)},
         "eager_event_us": round(1e3 * e_ms, 3), "eager_event_median_us": round(1e3 * float(np.median(e_per)), 3),
         "graph_event_us": round(1e3 * g_ms, 3), "graph_event_median_us": round(1e3 * float(np.median(g_per)), 3),
+        "phases_graph_events": phases,
     }), flush=True)
 
 
