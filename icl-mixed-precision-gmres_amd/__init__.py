@@ -102,6 +102,8 @@ def _declare_host(lib: C.CDLL) -> None:
                                                  C.POINTER(C.c_double), C.c_int]
     lib.mpg_engine_time_phase_graph.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
                                                 C.POINTER(C.c_double), C.c_int]
+    lib.mpg_engine_last_error.argtypes = [C.c_void_p]
+    lib.mpg_engine_last_error.restype = C.c_char_p
     lib.mpg_engine_phase_bytes.argtypes = [C.c_void_p, C.c_int]
     lib.mpg_engine_phase_bytes.restype = C.c_double
     lib.mpg_engine_destroy.argtypes = [C.c_void_p]
@@ -650,7 +652,8 @@ class Engine:
         done = C.c_int(0)
         ran = self._lib.mpg_engine_run(self._h, cycles, C.byref(done))
         if ran < 0:
-            raise RuntimeError(f"mpg_engine_run failed ({ran})")
+            msg = self._lib.mpg_engine_last_error(self._h).decode(errors="replace")
+            raise RuntimeError(f"mpg_engine_run failed ({ran}): {msg}")
         return ran, bool(done.value)
 
     def sync(self) -> None:

@@ -91,6 +91,17 @@ public:
     int size() const override { return size_; }
     int rank() const override { return rank_; }
     bool capturable() const override { return true; }
+    bool async() const override { return true; }
+    std::string async_error() override {
+        if (!comm_) return "communicator aborted";
+        ncclResult_t r = ncclSuccess;
+        if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
+        return r == ncclSuccess || r == ncclInProgress ? std::string() : std::string(ncclGetErrorString(r));
+    }
+    void abort() override {
+        if (comm_) ncclCommAbort(comm_);
+        comm_ = nullptr;
+    }
     void allreduce_sum(double* dev, int count, hipStream_t s) override {
         nck(ncclAllReduce(dev, dev, (size_t)count, ncclFloat64, ncclSum, comm_, s), "allreduce");
     }

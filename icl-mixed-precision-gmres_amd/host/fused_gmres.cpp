@@ -8,6 +8,7 @@
 #include <cstring>
 #include <functional>
 #include <stdexcept>
+#include <thread>
 
 #include "gmres.hpp"
 #include "types_hip.hpp"
@@ -352,7 +353,10 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     d.inner_row_exp = I.half_stats[0] > 0 ? I.row_exp.as<int8_t>() : nullptr;
     check(mpg_arnoldi_create(ctx, &d, &I.arn), "mpg_arnoldi_create", ctx);
     // ranks all-reduce per-workgroup partials in place: same count on every rank
-    if (comm) check(mpg_arnoldi_uniform_groups(I.arn), "uniform groups", ctx);
+    // (MPG_UNIFORM_GROUPS=1 gives one GPU the ranks' partial counts: a P = 1
+    // RCCL solve then has the single-GPU solve's bits, tests/test_dist_gpu.py)
+    const char* uenv = std::getenv("MPG_UNIFORM_GROUPS");
+    if (comm || (uenv && *uenv == '1')) check(mpg_arnoldi_uniform_groups(I.arn), "uniform groups", ctx);
     I.report_len = mpg_arnoldi_report_len(I.arn);
     for (double*& r : I.rep) hipck(hipHostMalloc((void**)&r, (size_t)I.report_len * sizeof(double), 0), "hipHostMalloc");
     I.report_host = I.rep[0];
@@ -615,7 +619,61 @@ void FusedEngine::read_report(int count) {
     hipck(hipMemcpyAsync(I.report_host, mpg_arnoldi_report_dev(I.arn), (size_t)count * sizeof(double),
                          hipMemcpyDeviceToHost, I.stream()),
           "report d2h");
+    if (I.comm && I.comm->async()) {
+        hipck(hipEventRecord(I.report_ev[0], I.stream()), "event record");
+        wait_event(I.report_ev[0], (int64_t)cycles.size(), "the step collectives (halo send/recv, all-reduces)");
+    }
     hipck(hipStreamSynchronize(I.stream()), "report sync");
+}
+
+// Host wait for the device. With an asynchronous transport (RCCL) a peer
+// that never arrives would hang the rank in hipEventSynchronize, and the
+// driver's 8-GPU run would only end at its time limit with no message: poll
+// instead, check the communicator's asynchronous error, and after
+// MPG_COMM_TIMEOUT_S seconds (default 120) without completion abort the
+// communicator and fail with the rank, the restart cycle and the collectives
+// in flight named (MPG_ERR_RCCL).
+void FusedEngine::wait_event(hipEvent_t ev, int64_t cycle, const char* what) {
+    Impl& I = *p_;
+    if (!I.comm || !I.comm->async()) {
+        hipck(hipEventSynchronize(ev), "wait");
+        return;
+    }
+    const char* env = std::getenv("MPG_COMM_TIMEOUT_S");
+    const double limit = env && *env ? std::atof(env) : 120.0;
+    const auto t0 = clk::now();
+    for (int polls = 0;; ++polls) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) hipck(q, "event query");
+        const double waited = std::chrono::duration<double>(clk::now() - t0).count();
+        std::string why = I.comm->async_error();
+        if (why.empty() && waited > limit)
+            why = "no progress for " + std::to_string(waited) + " s (MPG_COMM_TIMEOUT_S " + std::to_string(limit) + ")";
+        if (!why.empty()) {
+            // a grace period first: work that still completes was slow, not
+            // hung, and is not torn down under running kernels (the
+            // communicator stays intact); otherwise abort it
+            bool done_late = false;
+            const bool async_err = waited <= limit;
+            if (!async_err) {
+                const auto g0 = clk::now();
+                while (std::chrono::duration<double>(clk::now() - g0).count() < 5.0)
+                    if (hipEventQuery(ev) == hipSuccess) {
+                        done_late = true;
+                        break;
+                    }
+            }
+            if (!done_late) I.comm->abort();
+            throw StatusError(MPG_ERR_RCCL, "rank " + std::to_string(I.comm->rank()) + " of " +
+                                                std::to_string(I.comm->size()) + ": restart cycle " +
+                                                std::to_string(cycle) + ", waiting for " + what + ": " + why +
+                                                (done_late ? "; it completed within the 5 s grace period (not aborted)"
+                                                           : "; communicator aborted"));
+        }
+        // spin for the first ~ms (a cycle is ~1 ms), then back off
+        if (polls > 2000) std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
 }
 
 // steps 0..m-1, solution update with k = m, next residual prologue
@@ -724,7 +782,7 @@ int FusedEngine::run_pipelined(int max_cycles, bool& done) {
     for (;;) {
         const bool more = ran + 1 < max_cycles;
         if (more) launch(p ^ 1);  // speculative: decided by this cycle's report
-        hipck(hipEventSynchronize(I.report_ev[p]), "report wait");
+        wait_event(I.report_ev[p], i, "the step collectives (halo send/recv, all-reduces)");
         if (I.ilu) check_ilu_fault(I.ilu);  // every apply of this cycle is valid
         I.report_host = I.rep[p];
         record_steps(i);
@@ -1071,6 +1129,7 @@ int mpg_engine_create(const mpg_solve_args* a, mpg_engine_t* out, char* err, int
 
 int mpg_engine_run(mpg_engine_t e, int max_cycles, int* done) {
     if (!e || !e->eng) return MPG_ERR_ARG;
+    e->last_error.clear();
     try {
         mpg::ScopedContext scope(e->ctx);
         bool d = false;
@@ -1078,11 +1137,15 @@ int mpg_engine_run(mpg_engine_t e, int max_cycles, int* done) {
         if (done) *done = d ? 1 : 0;
         return ran;
     } catch (const mpg::StatusError& ex) {
+        e->last_error = ex.what();
         return ex.status;
-    } catch (const std::exception&) {
+    } catch (const std::exception& ex) {
+        e->last_error = ex.what();
         return MPG_ERR_HIP;
     }
 }
+
+const char* mpg_engine_last_error(mpg_engine_t e) { return e ? e->last_error.c_str() : ""; }
 
 int mpg_engine_sync(mpg_engine_t e) {
     if (!e) return MPG_ERR_ARG;

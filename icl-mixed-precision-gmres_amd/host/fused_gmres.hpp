@@ -46,6 +46,14 @@ public:
     }
     // whether the collectives may be captured into a hipGraph (no host waits)
     virtual bool capturable() const = 0;
+    // device-side transport (RCCL) whose collectives can hang or fail
+    // asynchronously: the engine then waits with a bounded poll
+    // (FusedEngine::wait_event) instead of a blocking synchronise
+    virtual bool async() const { return false; }
+    // "" or the transport's asynchronous error (ncclCommGetAsyncError)
+    virtual std::string async_error() { return {}; }
+    // tear the communicator down so that pending collectives return (ncclCommAbort)
+    virtual void abort() {}
 };
 
 // RAII device buffer through the C-ABI allocator
@@ -116,6 +124,7 @@ private:
     void store_next_basis(int k);
     double orth_loss_step(size_t k);
     void read_report(int count);
+    void wait_event(hipEvent_t ev, int64_t cycle, const char* what);
     void cycle_program();
     void ensure_graph();
     void record_steps(int64_t i);
@@ -135,6 +144,7 @@ struct mpg_engine {
     mpg_ctx_t ctx = nullptr;
     std::unique_ptr<mpg::Comm> comm;          // declared first: destroyed after eng
     std::unique_ptr<mpg::FusedEngine> eng;
+    std::string last_error;  // the text of the last failed mpg_engine_run
 };
 
 #endif  // MPGMRES_FUSED_GMRES_HPP

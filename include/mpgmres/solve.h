@@ -113,6 +113,8 @@ int mpg_solve(const mpg_solve_args* args, mpg_solve_result* result);
 typedef struct mpg_engine* mpg_engine_t;
 int mpg_engine_create(const mpg_solve_args* args, mpg_engine_t* out, char* err, int errlen);
 int mpg_engine_run(mpg_engine_t e, int max_cycles, int* done);
+/* the error text of the last mpg_engine_run that failed ("" otherwise) */
+const char* mpg_engine_last_error(mpg_engine_t e);
 int mpg_engine_sync(mpg_engine_t e);
 int64_t mpg_engine_total_iters(mpg_engine_t e);
 /* The solve so far as mpg_solve reports it: status, counts, the per-cycle

@@ -303,3 +303,76 @@ def test_fold_decision_is_collective(mpg, oracle, monkeypatch, limit, folded):
     assert [L["givens_folded"] for L in lays] == [folded, folded], lays
     ref = oracle.solve(mpg, A, b, xt, **opts)
     compare(as_ref(ref), got, "baseline", opts["tol"], 30, f"fold-collective-{limit}")
+
+
+def _rccl_one_rank(mpg, A, b, xt, opts, cycles=10):
+    plan = mpg.HaloPlan(0, 1, [0, A.nrows], A)
+    eng = mpg.Engine.distributed(A, b, xt, plan, mpg.rccl_unique_id(), 1, 0, **opts)
+    try:
+        eng.run(cycles)
+        return eng.report()
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("orth", ["cgs", "mgs"])
+def test_rccl_single_rank_bits(mpg, orth, monkeypatch):
+    """at P = 1 the RCCL engine runs the single-GPU
+    engine's kernels in the same order (the all-reduces and the empty halo are
+    identities); the one difference is the panel kernels' partial count (256
+    on ranks, so every rank all-reduces equal-length arrays, against
+    ceil(n / 4096) on one GPU), which regroups the fp64 partial sums. With
+    MPG_UNIFORM_GROUPS=1 the single-GPU engine takes the ranks' count, and
+    the two solves are bit-identical."""
+    A = mpg.gen_band(100_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode="mixed", orth=orth, prec="jacobi", rlen=30, tol=0.0, max_restarts=4)
+    dist_res = _rccl_one_rank(mpg, A, b, xt, opts)
+    monkeypatch.setenv("MPG_UNIFORM_GROUPS", "1")
+    one = mpg.Engine(A, b, xt, **opts)
+    one.run(10)
+    one_res = one.report()
+    one.close()
+    assert dist_res.total_iters == one_res.total_iters == 120
+    assert np.array_equal(dist_res.step_res, one_res.step_res)
+    assert np.array_equal(dist_res.cyc_r_norm, one_res.cyc_r_norm)
+    assert np.array_equal(dist_res.x, one_res.x)
+    assert dist_res.res_norm == one_res.res_norm
+
+
+def test_rccl_eager_matches_captured(mpg, monkeypatch):
+    """The uncaptured RCCL path (MPG_NO_GRAPH=1: the same collectives issued
+    eagerly, the fallback when capture is refused) gives the captured
+    cycle's bits."""
+    A = mpg.gen_band(100_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3)
+    cap = _rccl_one_rank(mpg, A, b, xt, opts)
+    monkeypatch.setenv("MPG_NO_GRAPH", "1")
+    eager = _rccl_one_rank(mpg, A, b, xt, opts)
+    assert cap.total_iters == eager.total_iters == 90
+    assert np.array_equal(cap.step_res, eager.step_res) and np.array_equal(cap.x, eager.x)
+    assert cap.res_norm == eager.res_norm
+
+
+def test_rccl_watchdog_names_rank_and_cycle(mpg, monkeypatch):
+    """A collective that never completes must end the rank with a message,
+    not hang until the driver's time limit: with MPG_COMM_TIMEOUT_S at 0 the
+    first wait for a cycle expires at once and mpg_engine_run fails
+    (MPG_ERR_RCCL, -4) naming the rank and the cycle. (Here the cycle does
+    complete within the 5 s grace period, so the communicator is not
+    aborted under running kernels; a real hang is.)"""
+    A = mpg.gen_band(100_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode="mixed", orth="cgs", prec="identity", rlen=30, tol=0.0, max_restarts=5)
+    plan = mpg.HaloPlan(0, 1, [0, A.nrows], A)
+    eng = mpg.Engine.distributed(A, b, xt, plan, mpg.rccl_unique_id(), 1, 0, **opts)
+    try:
+        monkeypatch.setenv("MPG_COMM_TIMEOUT_S", "0")
+        with pytest.raises(RuntimeError, match=r"\(-4\).*rank 0 of 1: restart cycle \d+.*no progress.*not aborted"):
+            eng.run(3)
+    finally:
+        eng.close()
