@@ -93,34 +93,86 @@ def load_pkg():
     return _load()
 
 
-def pmc_traffic(profile_dir: Path, kernel_key: str):
-    """HBM bytes per launch of the dominant kernel from a committed rocprofv3
-    PMC summary (profiles/pmc_traffic.json written by tools/pmc_summary.py:
-    FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or None."""
+def pmc_traffic(profile_dir: Path) -> dict:
+    """HBM bytes per launch of each kernel of the bench command from the
+    committed rocprofv3 PMC summary (profiles/pmc_traffic.json written by
+    tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE in separate passes,
+    gfx950 correction), {} when absent."""
     f = profile_dir / "pmc_traffic.json"
     if not f.exists():
-        return None
+        return {}
     try:
         d = json.loads(f.read_text())
-        return d.get(kernel_key, {}).get("hbm_bytes_per_launch")
+        return {k: v.get("hbm_bytes_per_launch") for k, v in d.items() if isinstance(v, dict)}
     except Exception:
-        return None
+        return {}
 
 
 def spmv_roofline(eng, cycles: int) -> dict:
-    """The Arnoldi SpMV in its place in the cycle: mean kernel time over every
-    launch of `cycles` cycles (k = 0 plain, k >= 1 with the Givens step
-    folded), the bytes its storage moves, and SURVEY 8(d)'s CSR bytes."""
+    """The Arnoldi SpMV in its place in the cycle (k = 0 plain, k >= 1 with
+    the Givens step folded): mean launch time inside graph replays of the
+    cycle -- the form the timed region runs -- bracketed by external event
+    nodes on each side of every SpMV launch (mpg_engine_time_phase_graph);
+    eager cycles with each launch's own kernel events when the engine does
+    not capture its cycle. Bytes: what the storage moves, and SURVEY 8(d)'s
+    CSR bytes."""
     layout = eng.spmv_layout()
-    avg_ms, per = eng.time_spmv_incycle(cycles)
+    try:
+        avg_ms, per = eng.time_phase_graph("spmv", cycles)
+        timing = "graph"
+    except RuntimeError:
+        avg_ms, per = eng.time_spmv_incycle(cycles)
+        timing = "eager"
     actual = eng.phase_bytes("spmv_storage")
     csr = eng.phase_bytes("spmv")
     kernel = ("k_step_sell2" if layout.get("slices_per_wave") == 2 else "k_step_sell") if layout["format"] == "sell" \
         else "k_step_spmv"
-    return {"kernel": kernel, "layout": layout,
+    return {"kernel": kernel, "layout": layout, "timing": timing,
             "avg_launch_ms": avg_ms, "launches": len(per), "min_launch_ms": min(per), "max_launch_ms": max(per),
             "storage_bytes": actual, "csr_bytes": csr,
             "achieved_gbs": actual / (avg_ms * 1e-3) / 1e9, "csr_equiv_gbs": csr / (avg_ms * 1e-3) / 1e9}
+
+
+def phase_roofline(eng, rlen: int, reps: int, traffic: dict) -> dict:
+    """The CGS step's other two kernels, timed like the SpMV (event nodes in
+    graph replays of the cycle): per kernel the mean launch time over the
+    cycle's steps, the fit t(k) = a + b k (a = the fixed cost of a launch, b
+    = one more basis column), the bytes it moves at the cycle's mean k
+    (basis columns 0..k, w read, and for the update w written) and their
+    fraction of 8 TB/s; PMC bytes from the committed profile when present."""
+    out = {}
+    for ph, kname in (("dots", "k_dots_nc"), ("cgs_update", "k_cgs_update_nc")):
+        ms, per = eng.time_phase_graph(ph, reps)
+        byk = np.asarray(per[:len(per) // rlen * rlen]).reshape(-1, rlen).mean(axis=0) * 1e3
+        b, a = np.polyfit(np.arange(rlen), byk, 1)
+        mb = eng.phase_bytes(ph)
+        ach = mb / (ms * 1e-3) / 1e9
+        pmc = traffic.get(kname) if rlen <= 32 else None
+        out[kname] = {"bytes_mean_k": int(mb), "avg_launch_ms": round(ms, 5), "achieved": round(ach, 1),
+                      "frac": round(ach / HBM_PEAK_GBS, 4), "fit_a_us": round(float(a), 3),
+                      "fit_b_us_per_column": round(float(b), 4),
+                      "traffic": pmc, "traffic_over_bytes": round(pmc / mb, 4) if pmc else None}
+    return out
+
+
+def surface_rate(mpg, A, b, xt, opts, cycles: int, fused_rate: float) -> dict:
+    """The same solve through the drop-in boundary north_star names: the
+    reference's driver (gmres_singleUpdate / gmres_baseline, restated in
+    host/gmres_impl.hpp) over the kernels.hpp operator surface of
+    kernels_hip.cpp (mpg_solve, engine surface). Two solves of 4 and 4 +
+    `cycles` restart cycles; the rate is the difference of their GMRES
+    iterations over the difference of their GMRES times, so the first
+    cycle's lazy set-up (SELL copy, cycle recording) cancels."""
+    o = {k: v for k, v in opts.items() if k not in ("spmv_format",)}
+    runs = []
+    for r in (4, 4 + cycles):
+        res = mpg.solve(A, b, xt, engine="surface", **dict(o, max_restarts=r))
+        runs.append((res.total_iters, res.gmres_seconds))
+    rate = (runs[1][0] - runs[0][0]) / (runs[1][1] - runs[0][1])
+    log(f"[bench] operator surface: {rate:.0f} it/s ({rate / fused_rate:.3f} of the fused engine)")
+    return {"iters_per_s": round(rate, 2), "vs_fused": round(rate / fused_rate, 4),
+            "how": f"mpg_solve engine=surface (gmres.cpp's driver over kernels_hip.cpp), (iters, time) of a "
+                   f"{4 + cycles}-cycle solve minus a 4-cycle solve"}
 
 
 def cpu_baseline(mpg, A, b, xt, opts, args, world=1, workload="BAND-10M"):
@@ -174,6 +226,8 @@ def main():
     ap.add_argument("--roofline-cycles", type=int, default=3)
     ap.add_argument("--hbm-rows", type=int, default=10_000_000,
                     help="rows of the BAND matrix of the HBM-scale SpMV figure (0: skip)")
+    ap.add_argument("--surface-cycles", type=int, default=20,
+                    help="N = 1: restart cycles of the same solve through the drop-in operator surface (0: skip)")
     ap.add_argument("--spmv-format", default="auto", choices=["auto", "csr", "sell"],
                     help="Arnoldi SpMV storage (auto: SELL-64 when its padding is small)")
     args = ap.parse_args()
@@ -271,6 +325,9 @@ def main():
 
     # roofline of the dominant kernel: the Arnoldi SpMV as the cycle runs it
     sp = spmv_roofline(eng, args.roofline_cycles)
+    pmc = pmc_traffic(REPO / "profiles")
+    phases = (phase_roofline(eng, args.rlen, args.roofline_cycles, pmc)
+              if args.orth == "cgs" and world == 1 and sp["timing"] == "graph" else None)
     # the whole CGS Arnoldi iteration on the same footing: the SpMV's storage
     # bytes + the panel dots and the CGS update at the cycle's mean k (the
     # once-per-cycle prologue and solution update are left out, so this
@@ -286,6 +343,9 @@ def main():
         per_rank_ms = [None] * world
         dist.all_gather_object(per_rank_ms, sp["avg_launch_ms"])
     shared_gpu = os.environ.get("MPG_BENCH_SHARED_GPU") == "1"
+    surface = None
+    if rank == 0 and world == 1 and args.surface_cycles > 0:
+        surface = surface_rate(mpg, A, b, xt, opts, args.surface_cycles, solve_rate)
     roofline = None
     cpu = None
     if rank == 0:
@@ -305,37 +365,53 @@ def main():
             eh.close()
             del Ah, bh, xh
             hbm = {"workload": f"BAND n={args.hbm_rows}, nnz={10 * args.hbm_rows - 25} (working set > 256 MB "
-                               f"Infinity Cache), same solve", "kernel": hs["kernel"],
-                   "avg_launch_ms": round(hs["avg_launch_ms"], 5), "bytes_per_launch": int(hs["csr_bytes"]),
-                   "achieved": round(hs["csr_equiv_gbs"], 1), "frac": round(hs["csr_equiv_gbs"] / HBM_PEAK_GBS, 4),
-                   "storage_bytes_per_launch": int(hs["storage_bytes"]),
-                   "storage_achieved": round(hs["achieved_gbs"], 1),
-                   "storage_frac": round(hs["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                   "storage_frac_of_measured": round(hs["achieved_gbs"] / measured, 4), "layout": hs["layout"]}
+                               f"Infinity Cache), same solve", "kernel": hs["kernel"], "timing": hs["timing"],
+                   "avg_launch_ms": round(hs["avg_launch_ms"], 5), "bytes_per_launch": int(hs["storage_bytes"]),
+                   "bytes_basis": "storage",
+                   "achieved": round(hs["achieved_gbs"], 1), "frac": round(hs["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                   "frac_of_measured": round(hs["achieved_gbs"] / measured, 4),
+                   "csr_equiv_bytes_per_launch": int(hs["csr_bytes"]),
+                   "csr_equiv_achieved": round(hs["csr_equiv_gbs"], 1),
+                   "csr_equiv_frac": round(hs["csr_equiv_gbs"] / HBM_PEAK_GBS, 4), "layout": hs["layout"]}
             log(f"[bench] HBM scale ({time.time() - t1:.1f}s): {hs['avg_launch_ms'] * 1e3:.1f} us/launch, "
                 f"{hs['achieved_gbs']:.0f} GB/s on storage bytes")
-        traffic = pmc_traffic(REPO / "profiles", sp["kernel"] + (":fold" if sp["layout"]["givens_folded"] else ""))
-        # achieved = SURVEY 8(d)'s algorithmic bytes (the reference's CSR
-        # SpMV: B_spmv) per launch / the launch's event time; the SELL copy
-        # moves fewer bytes (storage_*), traffic is what PMC counted
-        roofline = {"bound": "hbm", "achieved": round(sp["csr_equiv_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(sp["csr_equiv_gbs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+        # the PMC figure of the committed profile belongs to this workload's
+        # kernel only (BAND-10M, one GPU, m <= 32: tools/pmc_summary.py)
+        key = sp["kernel"] + (":fold" if sp["layout"]["givens_folded"] else "")
+        traffic = pmc.get(key) if world == 1 and args.rlen <= 32 and args.n_local == 1_000_000 else None
+        # achieved / frac: the bytes the kernel really moves (PMC HBM bytes of
+        # the committed profile when they belong to this run's kernel, else
+        # its storage bytes) over the in-cycle launch time -- a physical
+        # fraction of 8 TB/s. SURVEY 8(d)'s algorithmic CSR bytes,
+        # which count column indices the implicit slices never read, are
+        # reported beside it as csr_equiv_*.
+        moved = traffic if traffic else sp["storage_bytes"]
+        ach = moved / (sp["avg_launch_ms"] * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "bytes_per_launch": int(moved), "bytes_basis": "pmc" if traffic else "storage",
                     "kernel": sp["kernel"] + (" (in-cycle, Givens folded for k >= 1)" if sp["layout"]["givens_folded"]
                                               else " (in-cycle; the Givens step has its own launch)"),
                     "avg_launch_ms": round(sp["avg_launch_ms"], 5), "launches_timed": sp["launches"],
-                    "timing": "hipExtLaunchKernel start/stop events of each in-cycle launch",
-                    "bytes_per_launch": int(sp["csr_bytes"]),
-                    "bytes_formula": "SURVEY 8(d) B_spmv = nnz*(s_v+4) + (n+1)*4 + 2*n*s_x (algorithmic)",
+                    "timing": ("external event nodes on each side of every SpMV launch inside graph replays of "
+                               "the cycle (the timed region's form)" if sp["timing"] == "graph" else
+                               "hipExtLaunchKernel start/stop events of each launch of eager cycles"),
                     "storage_bytes_per_launch": int(sp["storage_bytes"]),
                     "storage_achieved": round(sp["achieved_gbs"], 1),
                     "storage_frac": round(sp["achieved_gbs"] / HBM_PEAK_GBS, 4),
                     "storage_formula": "what the SELL copy moves: slots x value bytes + stored columns (implicit "
                                        "slices read none) + slice offsets/pattern indices + 3 n s_T (w_prev read, "
                                        "v_k and w written)",
+                    "csr_equiv_bytes_per_launch": int(sp["csr_bytes"]),
+                    "csr_equiv_achieved": round(sp["csr_equiv_gbs"], 1),
+                    "csr_equiv_frac": round(sp["csr_equiv_gbs"] / HBM_PEAK_GBS, 4),
+                    "csr_equiv_formula": "SURVEY 8(d) B_spmv = nnz*(s_v+4) + (n+1)*4 + 2*n*s_x (algorithmic: "
+                                         "the reference's CSR SpMV; above the bytes the SELL copy moves)",
                     "measured_peak": round(measured, 1), "measured_peak_read": round(peak_read, 1),
                     "measured_peak_copy": round(peak_copy, 1),
-                    "frac_of_measured": round(sp["csr_equiv_gbs"] / measured, 4),
+                    "frac_of_measured": round(ach / measured, 4),
                     "storage_frac_of_measured": round(sp["achieved_gbs"] / measured, 4),
+                    "phases": phases,
                     "cache_note": "the BAND-10M Arnoldi working set (~190 MB) fits the 256 MB Infinity Cache; "
                                   "hbm_scale is the same kernel past it",
                     "hbm_scale": hbm, "rank": 0,
@@ -381,7 +457,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic", "roofline": roofline, "cpu_baseline": cpu,
-            "solve_iters_per_s": round(solve_rate, 2),
+            "solve_iters_per_s": round(solve_rate, 2), "surface": surface,
+            "surface_iters_per_s": surface["iters_per_s"] if surface else None,
             "aggregate": (None if strong or world == 1 else
                           {"value": round(solve_rate * world, 2),
                            "unit": "GMRES iterations x 10M-nnz row blocks (one per GPU) per second"}),

@@ -118,6 +118,7 @@ struct FusedEngine::Impl {
     bool cgs_partials = false;  // CGS update sums the dots partials in-launch
     bool fuse_dots = false;     // ... from dots formed in the SpMV launch
     bool fuse_dots_required = false;
+    int fuse_dots_k0 = 32;      // ... for the steps with k + 1 <= fuse_dots_k0
     int timed = -1;                  // phase whose launches time_phase brackets with events
     bool timed_inplace = false;      // ... the cycle's own SpMV launch, by its kernel events
     bool timed_graph = false;        // ... external event nodes around it in a captured cycle
@@ -405,6 +406,10 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     // (=2: required -- an error where the storage does not support it; tests)
     I.fuse_dots = I.cgs_partials && I.orth == MPG_ORTH_CGS && denv && (*denv == '1' || *denv == '2');
     I.fuse_dots_required = I.fuse_dots && *denv == '2';
+    // MPG_FUSE_DOTS_K0=K: fuse only the steps with k + 1 <= K (the first
+    // steps, whose per-row basis loads are few; VERDICT r3 item 5's policy)
+    const char* kenv = std::getenv("MPG_FUSE_DOTS_K0");
+    I.fuse_dots_k0 = kenv && *kenv ? std::max(0, std::min(32, std::atoi(kenv))) : 32;
     // MPG_FOLD_GIVENS: 0 never, 1 always (m permitting), unset: where it pays
     // (mpg_arnoldi_fold_pays: up to ~4k SpMV workgroups)
     const char* fenv = std::getenv("MPG_FOLD_GIVENS");
@@ -486,7 +491,8 @@ void FusedEngine::givens(int k) {
 void FusedEngine::step(int k, bool fold) {
     Impl& I = *p_;
     // SpMV and panel dots in one launch (one GPU, CGS with in-launch sums)
-    if (I.fuse_dots && !I.comm && !I.ilu && I.orth == MPG_ORTH_CGS && I.cgs_partials && !I.combine && k + 1 <= 32) {
+    if (I.fuse_dots && !I.comm && !I.ilu && I.orth == MPG_ORTH_CGS && I.cgs_partials && !I.combine &&
+        k + 1 <= I.fuse_dots_k0) {
         timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
         const int st = mpg_arnoldi_spmv_dots(I.arn, k, fold && k > 0 ? 2 : 0);
         timed_end(0);
