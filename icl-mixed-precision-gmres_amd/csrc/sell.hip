@@ -275,6 +275,119 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
     }
 }
 
+// k_sell_spmv with two 64-row slices per wave (the operator surface's form of
+// the fused engine's k_step_sell2): uniform int16 copies of W = 2 or 4 with
+// at most 12 entries per row (sell_pair). Lane l owns rows 128 s' + l and
+// 128 s' + 64 + l; both slices' values, columns, the window (or the first
+// batch's gathers) are issued before the wave waits for any of them, so a
+// wave carries twice the bytes through the same fixed work. The row sums are
+// k_sell_spmv's (fp64, CSR order), so y has the same bits.
+template <class X, class S, int W, bool WIN, int BE>
+__global__ __launch_bounds__(kBlock) void k_sell_spmv2(int n, int cols, int nslices, const int16_t* __restrict__ col,
+                                                       const S* __restrict__ val, const int32_t* __restrict__ sbase,
+                                                       const int32_t* __restrict__ spat, const int64_t* __restrict__ coff,
+                                                       const int16_t* __restrict__ pat, const X* __restrict__ x, X alpha,
+                                                       X beta, X* __restrict__ y, int64_t ustride, int xcd,
+                                                       ScalarProgram prog) {
+    using CI = int16_t;
+    constexpr int SPW = 2;
+    constexpr int WL = kWinLen + (SPW - 1) * kWave;
+    constexpr int NQ = WL / kWave;
+    __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? WL : 1];
+    const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
+    int b = (int)blockIdx.x, G = (int)gridDim.x;
+    if (prog.count > 0) {  // the riding scalar program: workgroup 0's first wave
+        if (b == 0) {
+            __shared__ double plds[3 * kProgStage + 1];
+            if (wid == 0) run_scalar_program<kProgStage>(prog, plds);
+            return;
+        }
+        --b;
+        --G;
+    }
+    const int s0 = ((xcd ? xcd_block(b, G) : b) * (kBlock / kWave) + wid) * SPW;
+    if (s0 >= nslices) return;  // no workgroup barrier below
+    const int row0 = s0 * kWave;
+    bool live_p[SPW];
+    SellRow<S, CI, W, false, BE> row[SPW];
+#pragma unroll
+    for (int p = 0; p < SPW; ++p) {
+        live_p[p] = s0 + p < nslices;
+        row[p].init_uniform(live_p[p] ? s0 + p : s0, ustride, spat, coff);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    X xw[WIN ? NQ : 1];
+    if constexpr (WIN) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int c = row0 - kWinLo + q * kWave + lane;
+            xw[q] = x[c >= 0 && c < cols ? c : 0];
+        }
+    }
+    X yi[SPW];
+#pragma unroll
+    for (int p = 0; p < SPW; ++p) {
+        const int i = row0 + p * kWave + lane;
+        yi[p] = beta != X(0) ? y[live_p[p] && i < n ? i : 0] : X(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int p = 0; p < SPW; ++p) {
+        row[p].init_vals(lane, val);
+        row[p].load_vals(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int p = 0; p < SPW; ++p) {
+        row[p].init_finish(lane, col, val, sbase, pat);
+        row[p].load_cols(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    using RowT = SellRow<S, CI, W, false, BE>;
+    X xg[WIN ? 1 : SPW][WIN ? 1 : RowT::U][WIN ? 1 : W];
+    if constexpr (!WIN) {
+#pragma unroll
+        for (int p = 0; p < SPW; ++p) row[p].gather([&](int c) { return x[c]; }, xg[p]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double sum[SPW] = {};
+    if constexpr (WIN) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int c = row0 - kWinLo + q * kWave + lane;
+            win[wid][q * kWave + lane] = (c >= 0 && c < cols) ? xw[q] : X(0);
+        }
+        wave_lds_sync();
+        auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
+#pragma unroll
+        for (int p = 0; p < SPW; ++p) row[p].sum(0, xv, sum[p]);
+#pragma unroll
+        for (int p = 0; p < SPW; ++p)
+            for (int q = row[p].U; q < row[p].steps; q += row[p].U) {
+                row[p].load(q);
+                row[p].sum(q, xv, sum[p]);
+            }
+    } else {
+        auto xv = [&](int c) { return (double)x[c]; };
+#pragma unroll
+        for (int p = 0; p < SPW; ++p) {
+            row[p].sum_gathered(0, xg[p], [](X r) { return (double)r; }, sum[p]);
+            for (int q = row[p].U; q < row[p].steps; q += row[p].U) {
+                row[p].load(q);
+                row[p].sum(q, xv, sum[p]);
+            }
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < SPW; ++p) {
+        const int i = row0 + p * kWave + lane;
+        if (live_p[p] && i < n) {
+            const X t = (X)sum[p];
+            y[i] = beta == X(0) ? alpha * t : alpha * t + beta * yi[p];
+        }
+    }
+}
+
 }  // namespace
 
 namespace mpg {
@@ -644,9 +757,27 @@ int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y,
     const SellCopy& S = A->S;
     if (S.nslices == 0) return prog.count > 0 ? mpg_scalar_program(ctx, prog.ops, prog.count) : MPG_OK;
     const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave) + (prog.count > 0 ? 1 : 0);
+    const int be = sell_uniform(S) ? sell_pair(S) : 0;
     int st = sell_dispatch(S, [&](auto ci, auto wc) {
         using CI = decltype(ci);
         return sell_dispatch_win(S.win, [&](auto wn) {
+            constexpr int Wc = decltype(wc)::value;
+            constexpr bool WN = decltype(wn)::value;
+            // two slices per wave (MPG_SURFACE_PAIR=0: one)
+            const char* pe = std::getenv("MPG_SURFACE_PAIR");
+            if constexpr (std::is_same_v<CI, int16_t> && (Wc == 2 || Wc == 4)) if (be && !(pe && *pe == '0')) {
+                const int grid2 = (S.nslices + 2 * (kBlock / kWave) - 1) / (2 * (kBlock / kWave)) + (prog.count > 0 ? 1 : 0);
+                auto go2 = [&](auto kern) {
+                    kern<<<grid2, kBlock, 0, ctx->stream>>>(
+                        S.n, A->cols, S.nslices, static_cast<const int16_t*>(S.col), static_cast<const St*>(S.val),
+                        S.sbase, S.spat, S.coff, static_cast<const int16_t*>(S.pat), x, alpha, beta, y, S.ustride,
+                        sell_xcd_order(S) ? 1 : 0, prog);
+                    return (int)MPG_OK;
+                };
+                if (be == 8) return go2(k_sell_spmv2<X, St, Wc, WN, 8>);
+                if constexpr (Wc == 2) if (be == 10) return go2(k_sell_spmv2<X, St, Wc, WN, 10>);
+                if (be == 12) return go2(k_sell_spmv2<X, St, Wc, WN, 12>);
+            }
             auto go = [&](auto kern) {
                 kern<<<grid, kBlock, 0, ctx->stream>>>(
                     S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val),
@@ -654,8 +785,6 @@ int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y,
                     alpha, beta, y, S.ustride, sell_xcd_order(S) ? 1 : 0, prog);
                 return (int)MPG_OK;
             };
-            constexpr int Wc = decltype(wc)::value;
-            constexpr bool WN = decltype(wn)::value;
             return sell_uniform(S) ? go(k_sell_spmv<X, St, CI, Wc, WN, true>) : go(k_sell_spmv<X, St, CI, Wc, WN, false>);
         });
     });

@@ -4,7 +4,7 @@ in-cycle SpMV (Givens folded) timed by its own kernel events
 (mpg_engine_time_spmv_incycle), median over `--reps` interleaved rounds.
 
 usage: python tools/spmv_ab.py --case band100m-half --var MPG_SELL_UNIFORM=0 --var MPG_SELL_UNIFORM=1
-cases: band10m, band100m, band100m-half, lap1m, lap1m-f64, c4"""
+cases: band10m, band100m, band100m-half, lap1m, lap1m-f64, c4, c4p, fem27, fem27p"""
 import argparse
 import json
 import os
@@ -17,12 +17,17 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 CASES = {
-    "band10m": (("band", 1_000_000), "mixed"),
-    "band100m": (("band", 10_000_000), "mixed"),
-    "band100m-half": (("band", 10_000_000), "mixed-half"),
-    "lap1m": (("laplace", 100), "mixed"),
-    "lap1m-f64": (("laplace", 100), "baseline"),
-    "c4": (("stencil27", 111), "mixed"),
+    "band10m": ("band:1000000", "mixed"),
+    "band100m": ("band:10000000", "mixed"),
+    "band100m-half": ("band:10000000", "mixed-half"),
+    "lap1m": ("laplace:100", "mixed"),
+    "lap1m-f64": ("laplace:100", "baseline"),
+    "c4": ("stencil27:111", "mixed"),
+    # irregular stand-ins (mpg_gen_spec): C4 under a node-block permutation,
+    # the thinned 27-point coupling in natural and permuted order
+    "c4p": ("stencil27p:111", "mixed"),
+    "fem27": ("fem27:111", "mixed"),
+    "fem27p": ("fem27:111:3:70:13:64", "mixed"),
 }
 
 
@@ -36,12 +41,10 @@ def main():
     from __graft_entry__ import _load
 
     mpg = _load()
-    gens = {"laplace": mpg.gen_laplace3d, "stencil27": lambda s: mpg.gen_stencil27(s, 3),
-            "band": lambda s: mpg.gen_band(s, 5, 4, seed=7)}
     variants = [dict(kv.split("=", 1) for kv in v.split(",")) for v in args.var]
     for case in args.case:
-        (kind, size), mode = CASES[case]
-        A = gens[kind](size)
+        spec, mode = CASES[case]
+        A = mpg.gen_spec(spec)
         xt = mpg.rand_vect(A.nrows, 42)
         b = mpg.host_spmv(A, xt)
         def with_env(v, fn):
@@ -60,14 +63,18 @@ def main():
         # read at engine creation, e.g. MPG_FOLD_GIVENS, and at launch)
         engs = []
         for v in variants:
+            # (a variant's spmv_format=auto|csr|sell picks the storage; the rest are environment flags)
+            fmt = v.pop("spmv_format", "auto")
             e = with_env(v, lambda: mpg.Engine(A, b, xt, mode=mode, orth="cgs", prec="identity", rlen=30, tol=0.0,
-                                              max_restarts=1000))
+                                              max_restarts=1000, spmv_format=fmt))
+            v["spmv_format"] = fmt
             with_env(v, lambda: e.run(1))
             engs.append(e)
         times = [[] for _ in variants]
         for _ in range(args.reps):
             for i, v in enumerate(variants):
-                ms, _ = with_env(v, lambda: engs[i].time_spmv_incycle(args.cycles))
+                env = {k: x for k, x in v.items() if k != "spmv_format"}
+                ms, _ = with_env(env, lambda: engs[i].time_spmv_incycle(args.cycles))
                 times[i].append(ms * 1e3)
         for v, t, e in zip(variants, times, engs):
             med = float(np.median(t))
@@ -75,7 +82,7 @@ def main():
             print(json.dumps({"case": case, "variant": v, "us_median": round(med, 2), "us": [round(x, 2) for x in t],
                               "storage_mb": round(storage / 1e6, 2),
                               "storage_tbs": round(storage / (med * 1e-6) / 1e12, 3),
-                              "layout": e.spmv_layout()}), flush=True)
+                              "layout": dict(e.spmv_layout(), **e.sell_columns())}), flush=True)
             e.close()
         del A, b, xt
 
