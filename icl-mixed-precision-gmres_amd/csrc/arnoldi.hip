@@ -1000,15 +1000,25 @@ __global__ __launch_bounds__(BS) void k_dots_panels(int n, const T* __restrict__
 // loads per lane are branch-free so they issue together: one latency.
 // NEXT_DOTS (CGSR's first pass): the partials of <v_j, w'> for j < NC
 // instead of ||w'||^2, from a second batched pass over the lane's columns.
-template <class T, int BS, int NC, bool FROM_PARTS = false, bool NEXT_DOTS = false>
+// PF (with FROM_PARTS): the lane's first row group -- w and the first batch
+// of basis columns, raw and unconditional (clamped row) -- is issued right
+// behind the partial loads, so its memory latency runs under the coefficient
+// sums; the coefficients are published with an LDS-only barrier
+// (__syncthreads would drain those loads). Same operands, same order.
+template <class T, int BS, int NC, bool FROM_PARTS = false, bool NEXT_DOTS = false, bool PF = false>
 __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict__ V, int64_t ld,
                                                       const double* __restrict__ sums, int part_G,
                                                       T* __restrict__ coef_out, T* __restrict__ w,
                                                       double* __restrict__ partial) {
     static_assert(NC >= 1 && NC <= kNC, "one panel");
     static_assert(!FROM_PARTS || BS >= 32 * NC, "32 lanes per column");
+    static_assert(!PF || (FROM_PARTS && !NEXT_DOTS), "prefetch under the partial sums");
     constexpr int B = kColBatch<T>;
+    constexpr int B0 = NC < B ? NC : B;
     __shared__ double coef[NC];
+    const int n4 = n & ~3;
+    const int i_first = 4 * (blockIdx.x * BS + threadIdx.x);
+    Raw4<T> pw, pv[PF ? B0 : 1];
     if constexpr (FROM_PARTS) {
         const int j = threadIdx.x / 32, sub = threadIdx.x % 32;
         const int jc = j < NC ? j : NC - 1;
@@ -1018,6 +1028,14 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
         for (int q = 0; q < Q; ++q) {
             const int g = sub + 32 * q;
             pp[q] = sums[(size_t)jc * part_G + (g < part_G ? g : 0)];
+        }
+        if constexpr (PF) {
+            __builtin_amdgcn_sched_barrier(0);
+            const int ip = i_first < n4 ? i_first : 0;
+            pw.load(w + ip);
+#pragma unroll
+            for (int u = 0; u < B0; ++u) pv[u].load(V + (int64_t)u * ld + ip);
+            __builtin_amdgcn_sched_barrier(0);
         }
         double v = 0.0;
 #pragma unroll
@@ -1035,22 +1053,27 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
         coef[threadIdx.x] = (double)c;
         if (blockIdx.x == 0) coef_out[threadIdx.x] = c;
     }
-    __syncthreads();
+    if constexpr (PF) lds_barrier();
+    else __syncthreads();
     constexpr int NA = NEXT_DOTS ? Pow2Ceil<NC>::v : 1;
     double acc[NA];
 #pragma unroll
     for (int c = 0; c < NA; ++c) acc[c] = 0.0;
-    const int n4 = n & ~3;
-    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
+    bool first = PF;
+    for (int i = i_first; i < n4; i += 4 * gridDim.x * BS) {
         Raw4<T> wr;
-        wr.load(w + i);
+        if (first) wr = pw;
+        else wr.load(w + i);
         double t[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int c0 = 0; c0 < NC; c0 += B) {
             Raw4<T> v[B];
 #pragma unroll
             for (int u = 0; u < B; ++u)
-                if (c0 + u < NC) v[u].load(V + (int64_t)(c0 + u) * ld + i);
+                if (c0 + u < NC) {
+                    if (c0 == 0 && first) v[u] = pv[u < B0 ? u : 0];
+                    else v[u].load(V + (int64_t)(c0 + u) * ld + i);
+                }
             __builtin_amdgcn_sched_barrier(0);  // keep the batch's loads issued back to back
 #pragma unroll
             for (int u = 0; u < B; ++u)
@@ -1069,6 +1092,7 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
             if (!NEXT_DOTS) acc[0] += wd[r] * wd[r];
         }
         Row4<T>::store(w + i, wo);
+        first = false;
         if constexpr (NEXT_DOTS) {
 #pragma unroll
             for (int c0 = 0; c0 < NC; c0 += B) {
@@ -2155,6 +2179,13 @@ static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
 int mpg_arnoldi_dots(mpg_arnoldi_t a, int k) { return dots_impl(a, k, false); }
 int mpg_arnoldi_dots_sums(mpg_arnoldi_t a, int k) { return dots_impl(a, k, true); }
 
+// MPG_CGS_PREFETCH=1: the in-launch-sum CGS update issues its first row
+// group under the coefficient sums (k_cgs_update_nc<..., PF>)
+static bool cgs_prefetch() {
+    const char* e = std::getenv("MPG_CGS_PREFETCH");
+    return e && *e == '1';
+}
+
 static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_partials = false) {
     if (!a || k < 0 || k >= a->d.m || pass < 0 || pass > 1 || k + 1 > 256) return MPG_ERR_ARG;
     const bool cgsr = a->d.orth == kOrthCGSR;
@@ -2201,6 +2232,16 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
         } else if (k + 1 <= kNC) {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
             return with_nc<kNC>(k + 1, [&](auto nc) {
                 constexpr int NC = decltype(nc)::value;
+                // (the prefetch variant for one batch of columns only: wider
+                // panels spill with the prefetched batch held across the sums)
+                if constexpr (NC <= kColBatch<T>) {
+                    if (from_partials && cgs_prefetch()) {
+                        k_cgs_update_nc<T, kCombineBlock, NC, true, false, true>
+                            <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->V), a->ld,
+                                                                           src, part_G, coef_out, w, a->partial);
+                        return (int)MPG_OK;
+                    }
+                }
                 if (from_partials)
                     k_cgs_update_nc<T, kCombineBlock, NC, true><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
                         a->d.n, static_cast<const T*>(a->V), a->ld, src, part_G, coef_out, w, a->partial);

@@ -341,3 +341,24 @@ def test_surface_gemv_emits_nrm2_partials_same_bits(mpg, orth, mode, monkeypatch
         p, q = got["13"], got["5"]
         assert p.total_iters == q.total_iters == 60
         assert np.array_equal(p.step_res, q.step_res) and np.array_equal(p.x, q.x), A.nrows
+
+
+@pytest.mark.parametrize("flag,engine", [("MPG_CGS_PREFETCH", "fused"), ("MPG_SURFACE_PAIR", "surface")])
+@pytest.mark.parametrize("mode", ["mixed", "baseline"])
+def test_round4_kernel_variants_same_bits(mpg, flag, engine, mode, monkeypatch):
+    """Round-4 kernel forms that must not change a bit: the CGS update that
+    issues its first row group under the coefficient sums (MPG_CGS_PREFETCH)
+    and the operator surface's two-slice-per-wave SELL SpMV (MPG_SURFACE_PAIR,
+    on by default) -- the same operands summed in the same order."""
+    res = {}
+    for mpg_case in ("band", "lap"):
+        A = mpg.gen_band(120_000, 5, 4, seed=7) if mpg_case == "band" else mpg.gen_laplace3d(40)
+        xt = mpg.rand_vect(A.nrows, 42)
+        b = mpg.host_spmv(A, xt)
+        opts = dict(mode=mode, orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3)
+        for v in ("0", "1"):
+            monkeypatch.setenv(flag, v)
+            res[(mpg_case, v)] = mpg.solve(A, b, xt, engine=engine, **opts)
+        a, c = res[(mpg_case, "0")], res[(mpg_case, "1")]
+        assert a.total_iters == c.total_iters == 90
+        assert np.array_equal(a.step_res, c.step_res) and np.array_equal(a.x, c.x), (flag, mpg_case)
