@@ -137,6 +137,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_givens_folded.argtypes = [C.c_void_p]
     lib.mpg_engine_sell_shared_slices.argtypes = [C.c_void_p]
     lib.mpg_engine_sell_shared_slices.restype = C.c_int64
+    lib.mpg_engine_sell_sigma.argtypes = [C.c_void_p]
 
 
 # (name, argtypes) for the kernel-level C-ABI, used by the per-kernel tests
@@ -718,7 +719,8 @@ class Engine:
             raise RuntimeError("mpg_engine_sell_columns failed")
         return {"form": {-1: "none", 0: "int32", 1: "int16", 2: "stepped"}[f.value], "csr_slices": e.value,
                 "implicit_slices": i.value,
-                "shared_slices": int(self._lib.mpg_engine_sell_shared_slices(self._h))}
+                "shared_slices": int(self._lib.mpg_engine_sell_shared_slices(self._h)),
+                "sigma": int(self._lib.mpg_engine_sell_sigma(self._h))}
 
     def half_stats(self) -> dict:
         """mixed-half: what the fp16 cast did (mpg_engine_half_stats)."""

@@ -135,14 +135,16 @@ __global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n
                                                           const int32_t* __restrict__ spat, const int64_t* __restrict__ coff, const CI* __restrict__ pat,
                                                           const int32_t* __restrict__ xrp,
                                                           const int32_t* __restrict__ xcol,
-                                                          const X* __restrict__ xval, int64_t ustride, int xcd) {
+                                                          const X* __restrict__ xval, int64_t ustride, int xcd,
+                                                          const int32_t* __restrict__ rows) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
     const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (kBlock / kWave) + wid;
     const bool live = s < nslices;  // a dead wave still joins the partials' barrier
     const int row0 = s * kWave;
-    const int i = row0 + lane;
+    // the lane's row (a sorted SELL-C-sigma copy: rows[], padding lanes n)
+    const int i = rows ? rows[live ? row0 + lane : 0] : row0 + lane;
     const bool own = live && i < n;
     SellRow<X, CI, W, true> row;  // once per cycle: non-temporal slices
     if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat, coff);
@@ -487,7 +489,8 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
                                                       const int32_t* __restrict__ xrp,
                                                       const int32_t* __restrict__ xcol,
                                                       const typename SellStore<VI>::type* __restrict__ xval,
-                                                      const int8_t* __restrict__ rexp, int64_t ustride, int xcd) {
+                                                      const int8_t* __restrict__ rexp, int64_t ustride, int xcd,
+                                                      const int32_t* __restrict__ rows) {
     static_assert(DN == 0 || BS == kBlock, "the fused dots' partials assume kBlock-thread workgroups");
     using S = typename SellStore<VI>::type;
     constexpr int NQ = kWinLen / kWave;
@@ -496,7 +499,9 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
     const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid;
     const bool live = s < nslices;  // a dead wave still joins the fold's barriers
     const int row0 = s * kWave;
-    const int i = row0 + lane;
+    // the lane's row: row0 + lane, or a sorted (SELL-C-sigma) copy's rows[],
+    // loaded behind the slice's first batch (below); nothing before needs it
+    int i = row0 + lane;
     // 0. the slice's offsets (UNI: computed) and pattern index
     SellRow<S, CI, W> row;
     if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat, coff);
@@ -527,8 +532,6 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
             const int c = row0 - kWinLo + q * kWave + lane;
             wr[q] = wprev[c >= n_lo && c < n_ext ? c : 0];
         }
-    } else {
-        wr[0] = wprev[i < n ? i : 0];
     }
     __builtin_amdgcn_sched_barrier(0);
     // 3. the slice's first batch (UNI: the values before the pattern index
@@ -542,6 +545,12 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
     } else {
         row.init_finish(lane, col, val, sbase, pat);
         row.load(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // 3b. without the window: the lane's own row's w_prev (needed last)
+    if constexpr (!WIN) {
+        if (rows) i = rows[live ? row0 + lane : 0];
+        wr[0] = wprev[i < n ? i : 0];
     }
     // 4. a scaled fp16 copy's row exponent (needed last, issued last)
     int rex = 0;
@@ -1819,8 +1828,11 @@ int64_t mpg_arnoldi_sell_matrix_bytes(mpg_arnoldi_t a) {
     // column starts)
     return S.padded * vbytes + S.col_slots * S.col_bytes() + S.npat * S.col_bytes() +
            ((int64_t)S.nslices + 1) * 8 + (S.spat ? (int64_t)S.nslices * 4 : 0) + (S.c16s ? steps * S.W * 4 : 0) +
-           (S.coff ? (int64_t)S.nslices * 8 : 0) + (a->d.inner_row_exp ? (int64_t)a->d.n : 0);
+           (S.coff ? (int64_t)S.nslices * 8 : 0) + (a->d.inner_row_exp ? (int64_t)a->d.n : 0) +
+           (S.rows ? (int64_t)S.nslices * kWave * 4 : 0);
 }
+
+int mpg_arnoldi_sell_sigma(mpg_arnoldi_t a) { return a ? a->sell.sigma : -1; }
 
 int64_t mpg_arnoldi_sell_shared_slices(mpg_arnoldi_t a) { return a ? a->sell.nshared : -1; }
 
@@ -1884,7 +1896,7 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
                             static_cast<const X*>(S->val), static_cast<const X*>(a->d.x),
                             static_cast<const X*>(a->d.b), diag, static_cast<T*>(a->w[0]), a->partial, S->sbase,
                             S->spat, S->coff, static_cast<const CI*>(S->pat), S->xrp, S->xcol, static_cast<const X*>(S->xval),
-                            S->ustride, sell_xcd_order(*S) ? 1 : 0);
+                            S->ustride, sell_xcd_order(*S) ? 1 : 0, S->rows);
                         return (int)MPG_OK;
                     };
                     constexpr int Wc = decltype(wc)::value;
@@ -2005,7 +2017,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                             static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd,
                             S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
                             static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
-                            S.ustride, sell_xcd_order(S) ? 1 : 0);
+                            S.ustride, sell_xcd_order(S) ? 1 : 0, S.rows);
                     return (int)MPG_OK;
                 };
                 if constexpr (std::is_same_v<T, float> && std::is_same_v<VI, float> &&

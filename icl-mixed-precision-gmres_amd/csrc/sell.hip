@@ -102,11 +102,11 @@ __global__ __launch_bounds__(kBlock) void k_sell_classify(int n, int nslices, co
 template <class S, class CI, int W>
 __global__ void k_sell_fill(int n, int nslices, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                             const S* __restrict__ val, const int64_t* __restrict__ off, const int32_t* __restrict__ sbase,
-                            CI* __restrict__ scol, S* __restrict__ sval) {
+                            CI* __restrict__ scol, S* __restrict__ sval, const int32_t* __restrict__ rows) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int s = (int)(t / kWave), lane = (int)(t % kWave);
     if (s >= nslices) return;
-    const int r = s * kWave + lane;
+    const int r = rows ? rows[s * kWave + lane] : s * kWave + lane;  // (sorted copies: int32 columns only)
     const int64_t o = off[s];
     const int width = (int)((off[s + 1] - o) / kWave);
     const int b = r < n ? rowptr[r] : 0, len = r < n ? rowptr[r + 1] - b : 0;
@@ -206,7 +206,8 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
                                                       const int32_t* __restrict__ xrp,
                                                       const int32_t* __restrict__ xcol, const S* __restrict__ xval,
                                                       const X* __restrict__ x, X alpha, X beta, X* __restrict__ y,
-                                                      int64_t ustride, int xcd, ScalarProgram prog) {
+                                                      int64_t ustride, int xcd, ScalarProgram prog,
+                                                      const int32_t* __restrict__ rows) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
@@ -225,11 +226,12 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
     const int s = (xcd ? xcd_block(b, G) : b) * (kBlock / kWave) + wid;
     if (s >= nslices) return;  // no workgroup barrier below: a dead wave may leave
     const int row0 = s * kWave;
-    const int i = row0 + lane;
     SellRow<S, CI, W> row;
     if constexpr (UNI) row.init_uniform(s, ustride, spat, coff);
     else row.init_load(s, off, spat, coff);
     __builtin_amdgcn_sched_barrier(0);
+    // the lane's row: row0 + lane, or a sorted (SELL-C-sigma) copy's rows[]
+    const int i = rows ? rows[row0 + lane] : row0 + lane;
     X xr[WIN ? NQ : 1];
     if constexpr (WIN) {
 #pragma unroll
@@ -405,24 +407,67 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
         hipStreamSynchronize(stream) != hipSuccess)
         return MPG_ERR_HIP;
     const int ns = (n + kWave - 1) / kWave;
+    auto len_of = [&](int r) { return r < n ? rp[r + 1] - rp[r] : 0; };
     std::vector<int> width((size_t)ns, 0);
-    for (int r = 0; r < n; ++r) width[r / kWave] = std::max(width[r / kWave], rp[r + 1] - rp[r]);
-    // the widest vector whose padding stays within 15 % of the least padded
-    // layout: narrow (2-4 B per lane) index loads cost more than the padding
-    int64_t padded[5] = {0, 0, 0, 0, 0};
-    for (int W : {4, 2, 1})
-        for (int s = 0; s < ns; ++s) padded[W] += (int64_t)kWave * ((width[s] + W - 1) / W * W);
-    const int64_t least = std::min(padded[1], std::min(padded[2], padded[4]));
-    int best_w = 1;
-    for (int W : {4, 2, 1})
-        if ((double)padded[W] <= 1.15 * (double)least) {
-            best_w = W;
-            break;
-        }
+    for (int r = 0; r < n; ++r) width[r / kWave] = std::max(width[r / kWave], len_of(r));
     const char* fw = std::getenv("MPG_SELL_W");  // 1, 2 or 4: force the vector width (experiments)
     const bool forced = fw && (*fw == '1' || *fw == '2' || *fw == '4') && fw[1] == 0;
-    if (forced) best_w = *fw - '0';
-    const int64_t best = padded[best_w];
+    // the widest vector whose padding stays within 15 % of the least padded
+    // layout: narrow (2-4 B per lane) index loads cost more than the padding
+    auto choose = [&](const std::vector<int>& wd, int& bw, int64_t& bp) {
+        int64_t padded[5] = {0, 0, 0, 0, 0};
+        for (int W : {4, 2, 1})
+            for (int s = 0; s < ns; ++s) padded[W] += (int64_t)kWave * ((wd[s] + W - 1) / W * W);
+        const int64_t least = std::min(padded[1], std::min(padded[2], padded[4]));
+        bw = 1;
+        for (int W : {4, 2, 1})
+            if ((double)padded[W] <= 1.15 * (double)least) {
+                bw = W;
+                break;
+            }
+        if (forced) bw = *fw - '0';
+        bp = padded[bw];
+    };
+    int best_w = 1;
+    int64_t best = 0;
+    choose(width, best_w, best);
+    // SELL-C-sigma (MPG_SELL_SIGMA: the window in rows, default 1024; 0 off;
+    // -1 always, for tests): rows of varying length in one slice pad it to its
+    // longest row (the FEM-like fem27 stand-in: 26 % at W = 4). Sorting the
+    // rows of each window of sigma rows by length (longest first, stable) and
+    // slicing that order brings the padding to ~5 %, at the price of the
+    // lanes' row numbers (4 B per row, S.rows) and scattered row stores
+    // within the window. Sorted copies keep int32 columns and no LDS window:
+    // the 2-byte and implicit forms and the window assume a slice holds
+    // consecutive rows.
+    std::vector<int32_t> order;
+    {
+        const char* se = std::getenv("MPG_SELL_SIGMA");
+        const int sg = se && *se ? std::atoi(se) : 1024;
+        const int sigma = sg < 0 ? 1024 : sg / kWave * kWave;
+        if (sigma >= kWave && (sg < 0 || (double)best > 1.2 * (double)A->nnz)) {
+            std::vector<int32_t> ord((size_t)ns * kWave);
+            for (int64_t w0 = 0; w0 < (int64_t)ns * kWave; w0 += sigma) {
+                const int64_t w1 = std::min<int64_t>(w0 + sigma, (int64_t)ns * kWave);
+                for (int64_t p = w0; p < w1; ++p) ord[(size_t)p] = (int32_t)std::min<int64_t>(p, n);
+                std::stable_sort(ord.begin() + w0, ord.begin() + w1,
+                                 [&](int32_t a, int32_t b) { return len_of(a) > len_of(b); });
+            }
+            std::vector<int> wd((size_t)ns, 0);
+            for (int s = 0; s < ns; ++s)
+                for (int l = 0; l < kWave; ++l) wd[s] = std::max(wd[s], len_of(ord[(size_t)s * kWave + l]));
+            int bw = 1;
+            int64_t bp = 0;
+            choose(wd, bw, bp);
+            if (sg < 0 || bp < best) {
+                order.swap(ord);
+                width.swap(wd);
+                best_w = bw;
+                best = bp;
+                S.sigma = sigma;
+            }
+        }
+    }
     if (format == 0 && !forced && (double)best > 1.2 * (double)A->nnz) return MPG_OK;
     if (best >= ((int64_t)1 << 31) * 4) return format == 2 ? MPG_ERR_UNSUPPORTED : MPG_OK;
     std::vector<int64_t> off((size_t)ns + 1, 0);
@@ -440,11 +485,19 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
     }
     (void)hipFree(span);
     if (!ok) return MPG_ERR_HIP;
-    const bool c16 = span_h[0] >= -32767 && span_h[1] <= 32767;
+    const bool sorted = !order.empty();
+    const bool c16 = !sorted && span_h[0] >= -32767 && span_h[1] <= 32767;
     const char* senv = std::getenv("MPG_SELL_STEPPED");  // 0: never the stepped int16 form
-    const bool try_c16s = !c16 && !(senv && *senv == '0');
+    const bool try_c16s = !sorted && !c16 && !(senv && *senv == '0');
     const char* wenv = std::getenv("MPG_SELL_WINDOW");  // 0: always gather from global memory
-    const bool win = !(wenv && *wenv == '0') && span_h[0] >= -kWinLo && span_h[1] < kWave + kWinHi;
+    const bool win = !sorted && !(wenv && *wenv == '0') && span_h[0] >= -kWinLo && span_h[1] < kWave + kWinHi;
+    if (sorted) {
+        if (hipMalloc((void**)&S.rows, order.size() * 4) != hipSuccess ||
+            hipMemcpyAsync(S.rows, order.data(), order.size() * 4, hipMemcpyHostToDevice, stream) != hipSuccess) {
+            sell_free(S);
+            return MPG_ERR_ALLOC;
+        }
+    }
     const size_t vsize = vtype == MPG_F64 ? 8 : vtype == MPG_F32 ? 4 : 2;
     if (hipMalloc((void**)&S.off, off.size() * 8) != hipSuccess) {
         sell_free(S);
@@ -466,7 +519,7 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
     S.padded = best;
     const int grid = (int)(((int64_t)ns * kWave + kBlock - 1) / kBlock);
     const char* ienv = std::getenv("MPG_SELL_IMPLICIT");  // 0: always read the stored columns
-    const bool try_imp = !(ienv && *ienv == '0');
+    const bool try_imp = !sorted && !(ienv && *ienv == '0');
     std::vector<int32_t> spat_h;   // per slice (host), when the copy has implicit or CSR slices
     std::vector<int32_t> pat_h;    // implicit patterns: lane-relative offsets, W per step
     if (try_c16s || try_imp) {
@@ -555,7 +608,7 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
             using CI = decltype(ci);
             k_sell_fill<St, CI, decltype(wc)::value><<<grid, kBlock, 0, stream>>>(
                 n, ns, A->rowptr, A->col, static_cast<const St*>(val), S.off, S.sbase, static_cast<CI*>(S.col),
-                static_cast<St*>(S.val));
+                static_cast<St*>(S.val), S.rows);
             return (int)MPG_OK;
         });
     });
@@ -737,6 +790,7 @@ void sell_free(SellCopy& S) {
     if (S.xcol) (void)hipFree(S.xcol);
     if (S.xval) (void)hipFree(S.xval);
     if (S.coff) (void)hipFree(S.coff);
+    if (S.rows) (void)hipFree(S.rows);
     S = SellCopy{};
 }
 
@@ -782,7 +836,7 @@ int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y,
                 kern<<<grid, kBlock, 0, ctx->stream>>>(
                     S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val),
                     S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol, static_cast<const St*>(S.xval), x,
-                    alpha, beta, y, S.ustride, sell_xcd_order(S) ? 1 : 0, prog);
+                    alpha, beta, y, S.ustride, sell_xcd_order(S) ? 1 : 0, prog, S.rows);
                 return (int)MPG_OK;
             };
             return sell_uniform(S) ? go(k_sell_spmv<X, St, CI, Wc, WN, true>) : go(k_sell_spmv<X, St, CI, Wc, WN, false>);

@@ -333,6 +333,11 @@ struct SellCopy {
                                // (slices with identical int16 column blocks store one; nullptr: off)
     int64_t nshared = 0;       // slices that read another slice's column block
     int64_t col_slots = 0;     // column entries stored (after sharing; implicit slices store none)
+    // SELL-C-sigma: the rows of every window of `sigma` rows sorted by length
+    // (longest first) before slicing; rows[64 s + l] = the row lane l of slice
+    // s holds (n for padding lanes). nullptr / 0: slice s holds rows 64 s..
+    int32_t* rows = nullptr;
+    int sigma = 0;
     int col_bytes() const { return c16 || c16s ? 2 : 4; }
 };
 

@@ -1244,6 +1244,11 @@ int64_t mpg_engine_sell_shared_slices(mpg_engine_t e) {
     return mpg_arnoldi_sell_shared_slices(e->eng->arnoldi());
 }
 
+int mpg_engine_sell_sigma(mpg_engine_t e) {
+    if (!e || !e->eng) return MPG_ERR_ARG;
+    return mpg_arnoldi_sell_sigma(e->eng->arnoldi());
+}
+
 int mpg_engine_slices_per_wave(mpg_engine_t e) {
     if (!e || !e->eng) return MPG_ERR_ARG;
     return mpg_arnoldi_slices_per_wave(e->eng->arnoldi());

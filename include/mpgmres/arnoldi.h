@@ -101,6 +101,10 @@ int mpg_arnoldi_sell_columns(mpg_arnoldi_t a, int32_t* form, int64_t* csr_slices
 int mpg_arnoldi_slices_per_wave(mpg_arnoldi_t a);
 /* slices of the SELL copy that read another slice's column block (mpg_sell_shared_slices) */
 int64_t mpg_arnoldi_sell_shared_slices(mpg_arnoldi_t a);
+/* SELL-C-sigma: the window (rows) inside which the copy's rows were sorted by
+ * length before slicing (rows of varying length, e.g. FEM-like matrices);
+ * 0: slice s holds rows 64 s .. 64 s + 63 (MPG_SELL_SIGMA, sell_tile.hpp) */
+int mpg_arnoldi_sell_sigma(mpg_arnoldi_t a);
 
 int mpg_arnoldi_prologue(mpg_arnoldi_t a);              /* partials: 3 columns */
 int mpg_arnoldi_prologue_finish(mpg_arnoldi_t a);

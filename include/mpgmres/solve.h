@@ -150,6 +150,8 @@ int mpg_engine_spmv_layout(mpg_engine_t e, int32_t* format, int32_t* vec_width, 
 int mpg_engine_sell_columns(mpg_engine_t e, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices);
 /* slices of the engine's SELL copy reading a shared column block (mpg_arnoldi_sell_shared_slices) */
 int64_t mpg_engine_sell_shared_slices(mpg_engine_t e);
+/* the engine's SELL-C-sigma window (mpg_arnoldi_sell_sigma; 0 unsorted) */
+int mpg_engine_sell_sigma(mpg_engine_t e);
 /* 1: the Givens step of step k-1 rides SpMV(k) (mpg_arnoldi_fold_pays); 0: its own launch */
 int mpg_engine_givens_folded(mpg_engine_t e);
 /* slices per wave of the engine's SELL Arnoldi SpMV (mpg_arnoldi_slices_per_wave) */
