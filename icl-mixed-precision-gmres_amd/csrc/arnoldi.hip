@@ -2198,14 +2198,18 @@ static bool cgs_prefetch() {
     return e && *e == '1';
 }
 
-static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_partials = false) {
+// no_next (CGSR at 32 < k + 1 <= kWideMax, one GPU): a pass that takes its
+// coefficients from the preceding one-launch panel dots and emits no next
+// dots (the caller launches k_dots_panels on the updated w instead)
+static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_partials = false, bool no_next = false) {
     if (!a || k < 0 || k >= a->d.m || pass < 0 || pass > 1 || k + 1 > 256) return MPG_ERR_ARG;
     const bool cgsr = a->d.orth == kOrthCGSR;
-    const bool next_dots = cgsr && pass == 0;
+    const bool next_dots = cgsr && pass == 0 && !no_next;
     if (givens && (next_dots || a->d.m > kFoldMaxM || from_partials)) return MPG_ERR_ARG;
+    if (no_next && (!cgsr || !from_partials || k + 1 <= kNC)) return MPG_ERR_ARG;
     // from_partials: the coefficients are summed from the preceding one-panel
     // dots' partials inside this launch (no reduce launch)
-    if (from_partials && (pass != 0 || k + 1 > kWideMax || a->last_part != a->dpart)) return MPG_ERR_ARG;
+    if (from_partials && ((pass != 0 && !no_next) || k + 1 > kWideMax || a->last_part != a->dpart)) return MPG_ERR_ARG;
     if (from_partials && k + 1 > kNC && (next_dots || a->last_G > kWideMax)) return MPG_ERR_ARG;
     const double* src = from_partials ? a->dpart : a->sums;
     const int part_G = from_partials ? a->last_G : 0;  // Gd (k_dots_nc) or fd_ng (k_step_sell's dots)
@@ -2278,6 +2282,7 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
 int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, false); }
 int mpg_arnoldi_cgs_partials(mpg_arnoldi_t a, int k) { return cgs_impl(a, k, 0, false, true); }
 int mpg_arnoldi_cgs_givens(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, true); }
+int mpg_arnoldi_cgsr_wide_pass(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, false, true, true); }
 
 static int mgs_impl(mpg_arnoldi_t a, int k, int j, bool from_partials) {
     if (!a || k < 0 || k >= a->d.m || j < 0 || j > k) return MPG_ERR_ARG;

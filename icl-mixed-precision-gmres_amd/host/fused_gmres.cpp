@@ -536,6 +536,16 @@ void FusedEngine::step(int k, bool fold) {
         // (one GPU, plain CGS: up to 128 columns -- GMRES(100) -- the wide
         // update sums the one-launch panel dots' partials itself)
         const bool small = k + 1 <= 32 || (!I.comm && I.orth == MPG_ORTH_CGS && k + 1 <= mpg_arnoldi_partials_max_cols());
+        if (!I.comm && !I.combine && I.orth == MPG_ORTH_CGSR && k + 1 > 32 &&
+            k + 1 <= mpg_arnoldi_partials_max_cols()) {
+            // CGSR at GMRES(100): dots, pass 0, dots again on the updated w, pass 1
+            for (int pass = 0; pass < 2; ++pass) {
+                check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
+                check(mpg_arnoldi_cgsr_wide_pass(I.arn, k, pass), "cgsr", I.ctx);
+            }
+            if (!fold) givens(k);
+            return;
+        }
         const int last_pass = I.orth == MPG_ORTH_CGSR ? 1 : 0;
         bool pass0_done = false;
         if (I.combine && k + 1 <= 32) {

@@ -123,6 +123,13 @@ int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass);  /* pass 0: h; pass 1: CG
  * mpg_arnoldi_cgs(a, k, 0) */
 int mpg_arnoldi_cgs_partials(mpg_arnoldi_t a, int k);
 int mpg_arnoldi_partials_max_cols(void);
+/* one GPU, CGSR(2) with 32 < k+1 <= mpg_arnoldi_partials_max_cols(): pass
+ * `pass` (0: h(0:k,k), 1: the correction, Orthogonalization.hpp:109-136)
+ * with its coefficients summed from the preceding mpg_arnoldi_dots partials
+ * (the one-launch panel dots) and no next dots: the step is dots, pass 0,
+ * dots, pass 1 -- four launches where the round-3 form needed one per 32
+ * columns plus two reduces */
+int mpg_arnoldi_cgsr_wide_pass(mpg_arnoldi_t a, int k, int pass);
 int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j);
 /* one GPU: MGS update j taking h_jk from the partials of the previous launch
  * (mpg_arnoldi_dots for j = 0, the previous update otherwise) — replaces
