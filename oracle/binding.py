@@ -26,6 +26,7 @@ def lib() -> C.CDLL:
         _lib.oracle_backend.restype = C.c_char_p
         _lib.oracle_max_threads.restype = C.c_int
         _lib.oracle_solve.restype = C.c_int
+        _lib.oracle_force_loops.argtypes = [C.c_int]
         d, f, i, p = C.c_double, C.c_float, C.c_int, C.c_void_p
         _lib.oracle_spmv_f64.argtypes = [i, p, p, p, d, p, d, p]
         _lib.oracle_spmv_f32.argtypes = [i, p, p, p, f, p, f, p]
@@ -60,14 +61,24 @@ def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
-def solve(mpg, A, b, x_true=None, **opts):
-    """Run the oracle on the same mpg_solve_args the HIP path takes."""
+def solve(mpg, A, b, x_true=None, backend=None, **opts):
+    """Run the oracle on the same mpg_solve_args the HIP path takes.
+    backend="loops" runs this solve on the loop kernels even where MKL loaded
+    (fp32 products summed in fp64 in index order -- the summation class of
+    the HIP kernels, and the same on every machine; MKL's fp32 sgemv sums in
+    fp32 in an order that depends on the CPU and its thread count)."""
     opts = dict(opts)
     opts.pop("engine", None)
     args, keep = mpg.make_args(A, b, x_true, **opts)
     fn = lib().oracle_solve
     fn.argtypes = [C.POINTER(type(args)), C.POINTER(mpg.SolveResult)]
-    return mpg.run_solve(fn, args, A.nrows)
+    if backend not in (None, "mkl", "loops"):
+        raise ValueError(f"oracle backend {backend!r}")
+    lib().oracle_force_loops(int(backend == "loops"))
+    try:
+        return mpg.run_solve(fn, args, A.nrows)
+    finally:
+        lib().oracle_force_loops(0)
 
 
 def spmv(A, x: np.ndarray, alpha=1.0, beta=0.0, y=None, dtype=np.float64) -> np.ndarray:

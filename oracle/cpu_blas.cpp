@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <atomic>
 #include <mutex>
 
 namespace oracle {
@@ -15,6 +16,8 @@ namespace oracle {
 namespace {
 
 MklApi g_api;
+MklApi g_off;  // loaded = false: the loop kernels
+std::atomic<bool> g_force_loops{false};
 std::once_flag g_once;
 
 template <class F>
@@ -134,8 +137,10 @@ void trsv_upper_loops(int n, const T* A, int lda, T* x) {
 
 const MklApi& mkl() {
     std::call_once(g_once, load);
-    return g_api;
+    return g_force_loops.load(std::memory_order_relaxed) ? g_off : g_api;
 }
+
+void force_loops(bool on) { g_force_loops.store(on, std::memory_order_relaxed); }
 
 const char* backend_name() { return mkl().loaded ? "mkl" : "loops"; }
 

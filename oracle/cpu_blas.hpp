@@ -56,6 +56,9 @@ struct MklApi {
 
 // Loaded once per process; `loaded` false means the loop backend.
 const MklApi& mkl();
+// Use the loop kernels (fp32 products summed in fp64, in index order) while
+// on, whether or not MKL loaded: a machine-independent summation order.
+void force_loops(bool on);
 const char* backend_name();
 void set_threads(int threads);
 int max_threads();

@@ -19,7 +19,8 @@ fp64 Arnoldi with an fp64 preconditioner (mode baseline):
     can never fail). Rounding-level differences (an ill-conditioned C1
     differs at 2e-12 relative) sit far inside it;
   * final resNorm within a factor 1.2 and errNorm within a factor 2, both
-    above a floor of 64 eps (||b|| + ||A||_F ||x||) / eps-level errors.
+    above a floor: 64 eps (||b|| + ||A||_F ||x||) for resNorm, 64 eps
+    sqrt(n) max|x| for errNorm (a 2-norm of n eps-level entry errors).
 fp32 Arnoldi, or fp64 Arnoldi whose vectors pass through an fp32
 preconditioner every step (modes mixed, single, mixed-half, single-prec):
   * same final status; restart index within ±1;
@@ -37,6 +38,14 @@ preconditioner every step (modes mixed, single, mixed-half, single-prec):
     10x the reference's (a more accurate x than the oracle's is not a
     parity failure: forward error at convergence depends on conditioning);
   * when converged, the final backward error is <= tol.
+Live-oracle comparisons of fp32 Arnoldi on large inputs run the oracle on
+its loop kernels (binding.solve(backend="loops"): fp32 products summed in
+fp64 in index order, the HIP kernels' summation class) and bound the GPU by
+the MKL oracle one-sidedly (not_worse_than): MKL's fp32 sgemv sums in fp32
+in an order that depends on the CPU and its thread count, and on n >= 80k
+its cycle-1 backward error moved 3-12x between this container and the GPU
+box (profiles/r04_oracle_backends.txt) while the loop oracle matched the GPU
+to 4 digits.
 Measured margins behind these numbers: tools/parity_margins.py over the
 168 golden records on the fused and operator-surface engines
 (profiles/r02_parity_margins.txt; the x terms against e_ref alone:
@@ -109,12 +118,27 @@ def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
         assert _ratio_ok(max(got.res_norm, rf), max(ref["res_norm"], rf), norm_factor[0]), \
             f"{label}: resNorm {got.res_norm:.3e} vs {ref['res_norm']:.3e}"
         if e_ref:
-            ef = 64 * np.finfo(np.float64).eps * xscale
+            # errNorm is a 2-norm over n entries, each carrying eps-level
+            # rounding: its floor grows with sqrt(n)
+            ef = 64 * np.finfo(np.float64).eps * np.sqrt(len(got.x)) * xscale
             if fp64:
                 assert _ratio_ok(max(e_got, ef), max(e_ref, ef), norm_factor[1]), \
                     f"{label}: errNorm {e_got:.3e} vs {e_ref:.3e}"
             else:
                 assert e_got <= norm_factor[1] * max(e_ref, ef), f"{label}: errNorm {e_got:.3e} vs {e_ref:.3e}"
+
+
+def not_worse_than(ref, got, mode: str, label: str = "", factor: float = 3.0):
+    """One-sided bound: every cycle's backward error of `got` at most
+    `factor` x the reference run's (above the compare() floor); a GPU run
+    more accurate than an fp32-summing oracle passes."""
+    floor = 1e-6 if mode == "single" else 1e-14
+    be_ref = _arr(ref.cyc_r_norm) / _arr(ref.cyc_normalization)
+    be_got = _arr(got.cyc_r_norm) / _arr(got.cyc_normalization)
+    nc = min(len(be_ref), len(be_got)) - (0 if got.restarts == ref.restarts else 1)
+    for c in range(max(nc, 0)):
+        assert be_got[c] <= factor * max(be_ref[c], floor), \
+            f"{label}: cycle {c} backward error {be_got[c]:.3e} > {factor} x {be_ref[c]:.3e}"
 
 
 def as_ref(result) -> dict:

@@ -32,6 +32,24 @@ def test_backend_reported(oracle):
     assert oracle.backend() in ("mkl", "loops")
 
 
+@pytest.mark.parametrize("mode", ["mixed", "baseline"])
+def test_oracle_loops_backend_per_solve(mpg, oracle, mode):
+    """backend="loops" (the summation class of the HIP kernels, used by the
+    large live-oracle GPU tests) passes the parity rules against the default
+    backend and leaves the default in place afterwards."""
+    A = convdiff(mpg, 16)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode=mode, orth="cgs", prec="jacobi", rlen=12, tol=1e-10, max_restarts=300)
+    d = oracle.solve(mpg, A, b, xt, **opts)
+    lp = oracle.solve(mpg, A, b, xt, backend="loops", **opts)
+    compare(as_ref(d), lp, mode, 1e-10, 12, f"loops-vs-default {mode}")
+    again = oracle.solve(mpg, A, b, xt, **opts)
+    assert np.array_equal(again.step_res, d.step_res) and np.array_equal(again.x, d.x)
+    with pytest.raises(ValueError):
+        oracle.solve(mpg, A, b, xt, backend="blas", **opts)
+
+
 @pytest.mark.parametrize("mode", ["mixed", "baseline", "single-prec", "single"])
 @pytest.mark.parametrize("orth", ["cgs", "mgs", "cgsr"])
 @pytest.mark.parametrize("prec", ["identity", "jacobi"])

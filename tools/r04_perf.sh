@@ -23,6 +23,7 @@ for s in $steps; do
     ab_k0) cmds+=("${tag}_ab_k0|600|tools/ab_bench.sh 3 'k0|MPG_FUSE_DOTS=0|--hbm-rows 0 --surface-cycles 0' 'k2|MPG_CGS_PARTIALS=1 MPG_FUSE_DOTS=1 MPG_FUSE_DOTS_K0=2|--hbm-rows 0 --surface-cycles 0' 'k4|MPG_CGS_PARTIALS=1 MPG_FUSE_DOTS=1 MPG_FUSE_DOTS_K0=4|--hbm-rows 0 --surface-cycles 0' 'k8|MPG_CGS_PARTIALS=1 MPG_FUSE_DOTS=1 MPG_FUSE_DOTS_K0=8|--hbm-rows 0 --surface-cycles 0' > gpurun_out/${tag}_ab_k0.txt") ;;
     c4pmc) for v in 0 1; do
              cmds+=("${tag}_c4f_share$v|200|timeout -s KILL 190 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${tag}_c4_share${v}_fetch -o fetch -- python3 tools/spmv_ab.py --case c4 --var MPG_SELL_SHARE=$v --reps 1 --cycles 1")
+             cmds+=("${tag}_c4h_share$v|200|timeout -s KILL 190 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/${tag}_c4_share${v}_hit -o hit -- python3 tools/spmv_ab.py --case c4 --var MPG_SELL_SHARE=$v --reps 1 --cycles 1")
            done ;;
     irr) cmds+=("${tag}_irr|700|python -u tools/spmv_ab.py --case c4p --case fem27 --case fem27p --var spmv_format=auto --var spmv_format=csr --var spmv_format=sell,MPG_SELL_SIGMA=0 --reps 3 --cycles 1 > gpurun_out/${tag}_irr.jsonl") ;;
   esac
