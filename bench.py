@@ -93,6 +93,33 @@ def load_pkg():
     return _load()
 
 
+ROCPROF_STATS = "bench_kernel_stats.csv"
+
+
+def rocprof_avg_ms(profile_dir: Path, kernel: str):
+    """Mean duration (ms) over all launches of `kernel` (every template
+    instance) in the committed rocprofv3 --kernel-trace --stats summary of
+    `bench.py --steps 10 --no-cpu-baseline --hbm-rows 0 --surface-cycles 0`
+    (profiles/bench_kernel_stats.csv, this round's copy), None when absent:
+    the CP's timestamps of each dispatch, which rocprof reports, set beside
+    the live wave-stamp time."""
+    f = profile_dir / ROCPROF_STATS
+    if not f.exists():
+        return None
+    import csv
+
+    calls, total = 0, 0.0
+    try:
+        for r in csv.DictReader(f.open()):
+            name = r["Name"]
+            if f"::{kernel}<" in name or name.startswith(f"{kernel}<") or f" {kernel}<" in name:
+                calls += int(r["Calls"])
+                total += float(r["TotalDurationNs"])
+    except (KeyError, ValueError, OSError):
+        return None
+    return round(total / calls * 1e-6, 5) if calls else None
+
+
 def pmc_traffic(profile_dir: Path) -> dict:
     """HBM bytes per launch of each kernel of the bench command from the
     committed rocprofv3 PMC summary (profiles/pmc_traffic.json written by
@@ -110,31 +137,39 @@ def pmc_traffic(profile_dir: Path) -> dict:
 
 def spmv_roofline(eng, cycles: int) -> dict:
     """The Arnoldi SpMV in its place in the cycle (k = 0 plain, k >= 1 with
-    the Givens step folded): mean launch time inside graph replays of the
-    cycle -- the form the timed region runs -- bracketed by external event
-    nodes on each side of every SpMV launch (mpg_engine_time_phase_graph);
-    eager cycles with each launch's own kernel events when the engine does
-    not capture its cycle. Bytes: what the storage moves, and SURVEY 8(d)'s
-    CSR bytes."""
+    the Givens step folded): mean launch duration inside graph replays of
+    the cycle -- the form the timed region runs -- from the device wall
+    clock each wave stores at its start and end (first start to last end,
+    mpg_engine_time_phase_stamps: the kernel alone, as rocprofv3 times it);
+    the same launches between event-record nodes (which add the queue's
+    packet latency) beside it; eager cycles with each launch's own kernel
+    events when the engine does not capture its cycle. Bytes: what the
+    storage moves, and SURVEY 8(d)'s CSR bytes."""
     layout = eng.spmv_layout()
+    event_ms = None
     try:
-        avg_ms, per = eng.time_phase_graph("spmv", cycles)
-        timing = "graph"
-    except RuntimeError:
+        avg_ms, per = eng.time_phase_stamps("spmv", cycles)
+        timing = "stamps"
+        try:  # the same launches between event-record nodes, for comparison
+            event_ms = eng.time_phase_graph("spmv", cycles)[0]
+        except RuntimeError as ex:
+            log(f"[bench] graph-event timing unavailable ({ex})")
+    except RuntimeError as ex:
+        log(f"[bench] wave-stamp timing unavailable ({ex}); timing eager cycles")
         avg_ms, per = eng.time_spmv_incycle(cycles)
         timing = "eager"
     actual = eng.phase_bytes("spmv_storage")
     csr = eng.phase_bytes("spmv")
     kernel = ("k_step_sell2" if layout.get("slices_per_wave") == 2 else "k_step_sell") if layout["format"] == "sell" \
         else "k_step_spmv"
-    return {"kernel": kernel, "layout": layout, "timing": timing,
+    return {"kernel": kernel, "layout": layout, "timing": timing, "event_graph_ms": event_ms,
             "avg_launch_ms": avg_ms, "launches": len(per), "min_launch_ms": min(per), "max_launch_ms": max(per),
             "storage_bytes": actual, "csr_bytes": csr,
             "achieved_gbs": actual / (avg_ms * 1e-3) / 1e9, "csr_equiv_gbs": csr / (avg_ms * 1e-3) / 1e9}
 
 
 def phase_roofline(eng, rlen: int, reps: int, traffic: dict) -> dict:
-    """The CGS step's other two kernels, timed like the SpMV (event nodes in
+    """The CGS step's other two kernels, timed like the SpMV (wave stamps in
     graph replays of the cycle): per kernel the mean launch time over the
     cycle's steps, the fit t(k) = a + b k (a = the fixed cost of a launch, b
     = one more basis column), the bytes it moves at the cycle's mean k
@@ -142,13 +177,20 @@ def phase_roofline(eng, rlen: int, reps: int, traffic: dict) -> dict:
     fraction of 8 TB/s; PMC bytes from the committed profile when present."""
     out = {}
     for ph, kname in (("dots", "k_dots_nc"), ("cgs_update", "k_cgs_update_nc")):
-        ms, per = eng.time_phase_graph(ph, reps)
+        try:
+            ms, per = eng.time_phase_stamps(ph, reps)
+            timing = "wave wall-clock stamps, first start to last end, in graph replays of the cycle"
+        except RuntimeError:
+            ms, per = eng.time_phase_graph(ph, reps)
+            timing = "event-record nodes on each side of every launch in graph replays of the cycle"
         byk = np.asarray(per[:len(per) // rlen * rlen]).reshape(-1, rlen).mean(axis=0) * 1e3
         b, a = np.polyfit(np.arange(rlen), byk, 1)
         mb = eng.phase_bytes(ph)
         ach = mb / (ms * 1e-3) / 1e9
         pmc = traffic.get(kname) if rlen <= 32 else None
         out[kname] = {"bytes_mean_k": int(mb), "avg_launch_ms": round(ms, 5), "achieved": round(ach, 1),
+                      "timing": timing,
+                      "rocprof_avg_launch_ms": rocprof_avg_ms(REPO / "profiles", kname),
                       "frac": round(ach / HBM_PEAK_GBS, 4), "fit_a_us": round(float(a), 3),
                       "fit_b_us_per_column": round(float(b), 4),
                       "traffic": pmc, "traffic_over_bytes": round(pmc / mb, 4) if pmc else None}
@@ -162,17 +204,24 @@ def surface_rate(mpg, A, b, xt, opts, cycles: int, fused_rate: float) -> dict:
     kernels_hip.cpp (mpg_solve, engine surface). Two solves of 4 and 4 +
     `cycles` restart cycles; the rate is the difference of their GMRES
     iterations over the difference of their GMRES times, so the first
-    cycle's lazy set-up (SELL copy, cycle recording) cancels."""
+    cycle's lazy set-up (SELL copy, cycle recording) cancels. A 2-cycle
+    warm-up solve runs first: the process's first surface solve also pays
+    one-time costs (code-object loads on each kernel's first launch) that a
+    later solve does not, which would shrink the difference of the times."""
     o = {k: v for k, v in opts.items() if k not in ("spmv_format",)}
+    mpg.solve(A, b, xt, engine="surface", **dict(o, max_restarts=2))
     runs = []
     for r in (4, 4 + cycles):
         res = mpg.solve(A, b, xt, engine="surface", **dict(o, max_restarts=r))
         runs.append((res.total_iters, res.gmres_seconds))
     rate = (runs[1][0] - runs[0][0]) / (runs[1][1] - runs[0][1])
-    log(f"[bench] operator surface: {rate:.0f} it/s ({rate / fused_rate:.3f} of the fused engine)")
+    whole = runs[1][0] / runs[1][1]
+    log(f"[bench] operator surface: {rate:.0f} it/s ({rate / fused_rate:.3f} of the fused engine); "
+        f"{whole:.0f} it/s over the whole {4 + cycles}-cycle solve")
     return {"iters_per_s": round(rate, 2), "vs_fused": round(rate / fused_rate, 4),
-            "how": f"mpg_solve engine=surface (gmres.cpp's driver over kernels_hip.cpp), (iters, time) of a "
-                   f"{4 + cycles}-cycle solve minus a 4-cycle solve"}
+            "whole_solve_iters_per_s": round(whole, 2),
+            "how": f"mpg_solve engine=surface (gmres.cpp's driver over kernels_hip.cpp), after a 2-cycle warm-up "
+                   f"solve: (iters, time) of a {4 + cycles}-cycle solve minus a 4-cycle solve"}
 
 
 def cpu_baseline(mpg, A, b, xt, opts, args, world=1, workload="BAND-10M"):
@@ -327,7 +376,7 @@ def main():
     sp = spmv_roofline(eng, args.roofline_cycles)
     pmc = pmc_traffic(REPO / "profiles")
     phases = (phase_roofline(eng, args.rlen, args.roofline_cycles, pmc)
-              if args.orth == "cgs" and world == 1 and sp["timing"] == "graph" else None)
+              if args.orth == "cgs" and world == 1 and sp["timing"] == "stamps" else None)
     # the whole CGS Arnoldi iteration on the same footing: the SpMV's storage
     # bytes + the panel dots and the CGS update at the cycle's mean k (the
     # once-per-cycle prologue and solution update are left out, so this
@@ -393,9 +442,12 @@ def main():
                     "kernel": sp["kernel"] + (" (in-cycle, Givens folded for k >= 1)" if sp["layout"]["givens_folded"]
                                               else " (in-cycle; the Givens step has its own launch)"),
                     "avg_launch_ms": round(sp["avg_launch_ms"], 5), "launches_timed": sp["launches"],
-                    "timing": ("external event nodes on each side of every SpMV launch inside graph replays of "
-                               "the cycle (the timed region's form)" if sp["timing"] == "graph" else
+                    "timing": ("device wall clock (wall_clock64, 100 MHz) stored by every wave at its start and "
+                               "end, first start to last end of each SpMV launch inside graph replays of the cycle "
+                               "(the timed region's form)" if sp["timing"] == "stamps" else
                                "hipExtLaunchKernel start/stop events of each launch of eager cycles"),
+                    "event_graph_ms": round(sp["event_graph_ms"], 5) if sp["event_graph_ms"] else None,
+                    "rocprof_avg_launch_ms": rocprof_avg_ms(REPO / "profiles", sp["kernel"]),
                     "storage_bytes_per_launch": int(sp["storage_bytes"]),
                     "storage_achieved": round(sp["achieved_gbs"], 1),
                     "storage_frac": round(sp["achieved_gbs"] / HBM_PEAK_GBS, 4),

@@ -102,6 +102,8 @@ def _declare_host(lib: C.CDLL) -> None:
                                                  C.POINTER(C.c_double), C.c_int]
     lib.mpg_engine_time_phase_graph.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
                                                 C.POINTER(C.c_double), C.c_int]
+    lib.mpg_engine_time_phase_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
+                                                 C.POINTER(C.c_double), C.c_int]
     lib.mpg_engine_last_error.argtypes = [C.c_void_p]
     lib.mpg_engine_last_error.restype = C.c_char_p
     lib.mpg_engine_phase_bytes.argtypes = [C.c_void_p, C.c_int]
@@ -694,7 +696,23 @@ class Engine:
         which = {"spmv": 0, "cgs_update": 2, "dots": 3}[phase]
         cnt = self._lib.mpg_engine_time_phase_graph(self._h, which, reps, C.byref(ms), per, cap)
         if cnt < 0:
-            raise RuntimeError(f"mpg_engine_time_phase_graph failed ({cnt})")
+            msg = self._lib.mpg_engine_last_error(self._h).decode(errors="replace")
+            raise RuntimeError(f"mpg_engine_time_phase_graph failed ({cnt}): {msg}")
+        return ms.value, [per[i] for i in range(min(cnt, cap))]
+
+    def time_phase_stamps(self, phase: str = "spmv", reps: int = 3) -> tuple:
+        """(mean ms, per-launch ms in cycle order) of a phase kernel ("spmv",
+        "cgs_update", "dots") inside graph replays of the cycle, from its
+        waves' wall-clock stamps (first wave start to last wave end;
+        mpg_engine_time_phase_stamps); measurement only."""
+        ms = C.c_double()
+        cap = 16384
+        per = (C.c_double * cap)()
+        which = {"spmv": 0, "cgs_update": 2, "dots": 3}[phase]
+        cnt = self._lib.mpg_engine_time_phase_stamps(self._h, which, reps, C.byref(ms), per, cap)
+        if cnt < 0:
+            msg = self._lib.mpg_engine_last_error(self._h).decode(errors="replace")
+            raise RuntimeError(f"mpg_engine_time_phase_stamps failed ({cnt}): {msg}")
         return ms.value, [per[i] for i in range(min(cnt, cap))]
 
     def phase_bytes(self, phase: str) -> float:

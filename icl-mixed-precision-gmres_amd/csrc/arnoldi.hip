@@ -387,7 +387,22 @@ struct GivensFold {
     const double* norm2;  // nullptr: not folded (use *inv_p)
     int nparts;
     GivensArgs<T> g;
+    // measurement only (mpg_arnoldi_stamp_next; nullptr in a solve):
+    // wave q's lane 0 stores the wall clock at its start to stamp[2q] and
+    // at its end to stamp[2q + 1]
+    unsigned long long* stamp = nullptr;
 };
+
+// measurement only: wave q's lane 0 stores the wall clock to stamp[2q + end]
+// (end 0 at the wave's start, 1 at its end); a one-dimensional grid
+__device__ __forceinline__ void stamp_at(unsigned long long* stamp, int end) {
+    if (stamp && (threadIdx.x & (kWave - 1)) == 0)
+        stamp[2 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave) + end] = wall_clock64();
+}
+template <class T>
+__device__ __forceinline__ void stamp_wave(const GivensFold<T>& f, int end) {
+    stamp_at(f.stamp, end);
+}
 
 template <bool FOLD, class T>
 __device__ __forceinline__ T fold_givens(const GivensFold<T>& f, const T* __restrict__ inv_p) {
@@ -422,6 +437,7 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
                                                       GivensFold<T> fold, const int8_t* __restrict__ rexp) {
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
+    stamp_wave(fold, 0);
     const T inv = fold_givens<FOLD>(fold, inv_p);
     T* __restrict__ Vk = V + (int64_t)k * ld;
     struct Ops {
@@ -440,6 +456,7 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
             Vk[i] = o.wp * inv;
         },
         prod, scratch);
+    stamp_wave(fold, 1);
 }
 
 // ---------------------------------------------------------------- step: SpMV (SELL-64)
@@ -496,6 +513,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
     constexpr int NQ = kWinLen / kWave;
     __shared__ T win[WIN ? BS / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
+    stamp_wave(fold, 0);
     const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid;
     const bool live = s < nslices;  // a dead wave still joins the fold's barriers
     const int row0 = s * kWave;
@@ -691,6 +709,7 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
         __shared__ T col_s[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
         if (blockIdx.x == 0) givens_block(fold.g, nrm2sq, col_s, c_s, s_s);
     }
+    stamp_wave(fold, 1);
 }
 
 // k_step_sell with two adjacent slices per wave (lane l owns rows
@@ -723,6 +742,7 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
     constexpr int NQ = WL / kWave;
     __shared__ T win[WIN ? BS / kWave : 1][WIN ? WL : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
+    stamp_wave(fold, 0);
     const int s0 = ((xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid) * SPW;
     const bool live = s0 < nslices;  // a dead wave still joins the fold's barriers
     bool live_p[SPW];
@@ -893,6 +913,7 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
         __shared__ T col_s[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
         if (blockIdx.x == 0) givens_block(fold.g, nrm2sq, col_s, c_s, s_s);
     }
+    stamp_wave(fold, 1);
 }
 
 // Tall-skinny panel reduction: partial <v_j, w> for j in [c0, c0 + nc),
@@ -980,8 +1001,11 @@ __device__ __forceinline__ void dots_panel(int n, const T* __restrict__ V, int64
 
 template <class T, int BS, int NC>
 __global__ __launch_bounds__(BS) void k_dots_nc(int n, const T* __restrict__ V, int64_t ld,
-                                                const T* __restrict__ w, double* __restrict__ partial) {
+                                                const T* __restrict__ w, double* __restrict__ partial,
+                                                unsigned long long* stamp) {
+    stamp_at(stamp, 0);
     dots_panel<T, BS, NC>(n, V, ld, w, partial);
+    stamp_at(stamp, 1);
 }
 
 // V^T w for nc > kNC columns in ONE launch (GMRES(100): the round-3 form ran
@@ -1018,8 +1042,9 @@ template <class T, int BS, int NC, bool FROM_PARTS = false, bool NEXT_DOTS = fal
 __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict__ V, int64_t ld,
                                                       const double* __restrict__ sums, int part_G,
                                                       T* __restrict__ coef_out, T* __restrict__ w,
-                                                      double* __restrict__ partial) {
+                                                      double* __restrict__ partial, unsigned long long* stamp) {
     static_assert(NC >= 1 && NC <= kNC, "one panel");
+    stamp_at(stamp, 0);
     static_assert(!FROM_PARTS || BS >= 32 * NC, "32 lanes per column");
     static_assert(!PF || (FROM_PARTS && !NEXT_DOTS), "prefetch under the partial sums");
     constexpr int B = kColBatch<T>;
@@ -1131,6 +1156,7 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
         }
     }
     store_partials<NA, BS>(acc, NEXT_DOTS ? NC : 1, partial);
+    stamp_at(stamp, 1);
 }
 
 // The CGS update for kNC < nc <= kWideMax columns (GMRES(100)): the
@@ -2001,6 +2027,16 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
         GivensFold<T> gf{nullptr, 0, {}};
         if (fold)
             gf = GivensFold<T>{fold == 2 ? a->last_part : a->sums, fold == 2 ? a->last_G : 0, givens_args<T>(a, k - 1)};
+        // measurement: this launch's wave stamps (mpg_arnoldi_stamp_next),
+        // when the slots hold all of its waves
+        unsigned long long* const stamp = a->ctx->stamp_next;
+        const int64_t stamp_cap = a->ctx->stamp_cap;
+        a->ctx->stamp_next = nullptr;
+        auto stamped = [&](int64_t waves) {
+            GivensFold<T> g = gf;
+            g.stamp = stamp && waves <= stamp_cap ? stamp : nullptr;
+            return g;
+        };
         if (a->sell.nslices > 0) {
             const auto& S = a->sell;
             if (fold == 2 && a->last_G > kBlock) return (int)MPG_ERR_ARG;  // k_step_sell folds <= kBlock partials
@@ -2014,7 +2050,8 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                             a->d.n, -a->front, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
-                            static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd,
+                            static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]),
+                            stamped((int64_t)grid * (BS / kWave)), dd,
                             S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
                             static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
                             S.ustride, sell_xcd_order(S) ? 1 : 0, S.rows);
@@ -2045,7 +2082,8 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                                     a->d.n, -a->front, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
                                     static_cast<const typename SellStore<VI>::type*>(S.val),
                                     static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
-                                    static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf,
+                                    static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]),
+                                    stamped((int64_t)grid * (kStepSellBlock / kWave)),
                                     SellDots{}, S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
                                     static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
                                     S.ustride, sell_xcd_order(S) ? 1 : 0);
@@ -2094,7 +2132,8 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
         launch_timed(a->ctx, kern, dim3(rb_grid(a)), dim3(kBlock),
             A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,
             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,
-            diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp);
+            diag, static_cast<T*>(a->w[(k + 1) & 1]), stamped((int64_t)rb_grid(a) * (kBlock / kWave)),
+            a->d.inner_row_exp);
         return (int)MPG_OK;
     });
     if (st) return st;
@@ -2143,6 +2182,14 @@ static int wide_groups(const mpg_arnoldi* a, int ncols) {
     return std::max(1, std::min(a->Gd, kCombineGroups / np));
 }
 
+// measurement: the armed stamp slots (mpg_arnoldi_stamp_next) for this launch when they hold all of its waves;
+// disarmed either way
+static unsigned long long* take_stamp(mpg_arnoldi* a, int64_t waves) {
+    unsigned long long* p = a->ctx->stamp_next;
+    a->ctx->stamp_next = nullptr;
+    return p && waves <= a->ctx->stamp_cap ? p : nullptr;
+}
+
 static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
     const int ndots_all = a->d.orth == kOrthMGS ? 1 : k + 1;
@@ -2158,7 +2205,8 @@ static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
         if (ndots_all <= kNC) {  // one panel: 1024-thread workgroups, one per CU -> Gd partials per column
             return with_nc<kNC>(ndots_all, [&](auto nc) {
                 k_dots_nc<T, kCombineBlock, decltype(nc)::value><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                    a->d.n, static_cast<const T*>(a->V), a->ld, static_cast<const T*>(a->w[(k + 1) & 1]), a->dpart);
+                    a->d.n, static_cast<const T*>(a->V), a->ld, static_cast<const T*>(a->w[(k + 1) & 1]), a->dpart,
+                    take_stamp(a, (int64_t)a->Gd * (kCombineBlock / kWave)));
                 return (int)MPG_OK;
             });
         }
@@ -2224,7 +2272,8 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
             // than the 128 VGPRs of a 1024-thread one) -> row_grid partials
             return with_nc<kNC>(k + 1, [&](auto nc) {
                 k_cgs_update_nc<T, kBlock, decltype(nc)::value, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                    a->d.n, static_cast<const T*>(a->V), a->ld, src, 0, coef_out, w, a->partial);
+                    a->d.n, static_cast<const T*>(a->V), a->ld, src, 0, coef_out, w, a->partial,
+                    take_stamp(a, (int64_t)row_grid(a) * (kBlock / kWave)));
                 return (int)MPG_OK;
             });
         } else if (next_dots) {
@@ -2246,6 +2295,7 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
             k_cgs_update_wide<T, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k + 1, src, part_G, coef_out, w, a->partial);
         } else if (k + 1 <= kNC) {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
+            const int64_t nc_waves = (int64_t)a->Gd * (kCombineBlock / kWave);
             return with_nc<kNC>(k + 1, [&](auto nc) {
                 constexpr int NC = decltype(nc)::value;
                 // (the prefetch variant for one batch of columns only: wider
@@ -2254,16 +2304,19 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
                     if (from_partials && cgs_prefetch()) {
                         k_cgs_update_nc<T, kCombineBlock, NC, true, false, true>
                             <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->V), a->ld,
-                                                                           src, part_G, coef_out, w, a->partial);
+                                                                           src, part_G, coef_out, w, a->partial,
+                                                                           take_stamp(a, nc_waves));
                         return (int)MPG_OK;
                     }
                 }
                 if (from_partials)
                     k_cgs_update_nc<T, kCombineBlock, NC, true><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                        a->d.n, static_cast<const T*>(a->V), a->ld, src, part_G, coef_out, w, a->partial);
+                        a->d.n, static_cast<const T*>(a->V), a->ld, src, part_G, coef_out, w, a->partial,
+                        take_stamp(a, nc_waves));
                 else
                     k_cgs_update_nc<T, kCombineBlock, NC, false><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                        a->d.n, static_cast<const T*>(a->V), a->ld, src, 0, coef_out, w, a->partial);
+                        a->d.n, static_cast<const T*>(a->V), a->ld, src, 0, coef_out, w, a->partial,
+                        take_stamp(a, nc_waves));
                 return (int)MPG_OK;
             });
         } else {
@@ -2379,6 +2432,24 @@ int mpg_arnoldi_time_next_spmv(mpg_arnoldi_t a, void* start_event, void* stop_ev
     a->ctx->time_start = static_cast<hipEvent_t>(start_event);
     a->ctx->time_stop = static_cast<hipEvent_t>(stop_event);
     return MPG_OK;
+}
+int mpg_arnoldi_stamp_next(mpg_arnoldi_t a, unsigned long long* slots, int64_t cap_waves) {
+    if (!a || (slots && cap_waves < 1)) return MPG_ERR_ARG;
+    a->ctx->stamp_next = slots;
+    a->ctx->stamp_cap = slots ? cap_waves : 0;
+    return MPG_OK;
+}
+int64_t mpg_arnoldi_stamp_waves(mpg_arnoldi_t a) {
+    if (!a) return MPG_ERR_ARG;
+    // the most waves a stamped launch has: the SpMV (a wave per slice, the
+    // pair kernel half of that, rounded up to whole workgroups, or the
+    // CSR-adaptive grid), the one-panel dots / CGS update (Gd 1024-thread
+    // workgroups, or row_grid 256-thread ones for CGSR's first pass)
+    int64_t w = a->sell.nslices > 0 ? a->sell.nslices + 1024 / kWave : 0;
+    w = std::max<int64_t>(w, (int64_t)rb_grid(a) * (kBlock / kWave));
+    w = std::max<int64_t>(w, (int64_t)a->Gd * (kCombineBlock / kWave));
+    w = std::max<int64_t>(w, (int64_t)row_grid(a) * (kBlock / kWave));
+    return w;
 }
 int mpg_arnoldi_num_groups(mpg_arnoldi_t a) { return a ? a->G : 0; }
 double* mpg_arnoldi_partials_dev(mpg_arnoldi_t a) { return a ? a->last_part : nullptr; }

@@ -22,6 +22,11 @@ struct mpg_ctx {
     // measurement hook (mpg_arnoldi_time_next_spmv): the next launch made
     // through launch_timed records its own start/stop on these events
     hipEvent_t time_start = nullptr, time_stop = nullptr;
+    // measurement hook (mpg_arnoldi_stamp_next): the next stamped launch
+    // (Arnoldi SpMV, k_dots_nc, k_cgs_update_nc) stores each wave's start /
+    // end wall clock into these slots
+    unsigned long long* stamp_next = nullptr;
+    int64_t stamp_cap = 0;  // waves the slots hold
 };
 
 // Analysed CSR structure (row blocks of the CSR-adaptive schedule).

@@ -123,6 +123,8 @@ struct FusedEngine::Impl {
     bool timed_inplace = false;      // ... the cycle's own SpMV launch, by its kernel events
     bool timed_graph = false;        // ... external event nodes around it in a captured cycle
     std::vector<hipEvent_t> marks;   // ... begin/end pairs
+    unsigned long long* stamps = nullptr;  // time_phase_stamps: wave stamp slots of each timed launch
+    int64_t stamp_cap = 0, stamp_q = 0, stamp_max = 0;  // waves per launch, launches armed, launch slots
     std::vector<int32_t> rowptr_host;
     mpg_ilu_t ilu = nullptr;  // ILU(0) factors (prec ilu / ilu_jacobi), applied between phase kernels
     bool orthloss = false;    // LostOrthogonality: v_{k+1} stored each step, S / u below
@@ -985,17 +987,43 @@ double FusedEngine::time_phase(int which, int reps, bool inplace, std::vector<do
 // replay mode: kTimedReplays plain launches between one event pair ahead of
 // the site's own launch; in-place mode (SpMV): arm the kernel events that
 // the site's own launch records (mpg_arnoldi_time_next_spmv)
+// An event-record node spliced into the capture in progress on `st`: the
+// node depends on the capture's current tail and becomes the new tail. Same
+// place in the graph as hipEventRecordWithFlags(hipEventRecordExternal),
+// which the HIP runtime bundled with PyTorch (ROCm 7.0) rejects inside a
+// capture ("invalid argument").
+static void capture_event_record(hipStream_t st, hipEvent_t ev) {
+    hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t graph = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t ndeps = 0;
+    hipck(hipStreamGetCaptureInfo_v2(st, &status, &id, &graph, &deps, &ndeps), "capture info");
+    if (status != hipStreamCaptureStatusActive || !graph) throw StatusError(MPG_ERR_HIP, "timing mark outside a capture");
+    hipGraphNode_t node = nullptr;
+    hipck(hipGraphAddEventRecordNode(&node, graph, deps, ndeps, ev), "event record node");
+    hipck(hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies), "capture tail");
+}
+
 template <class F>
 void FusedEngine::timed(int phase, F&& launch) {
     Impl& I = *p_;
     if (I.timed != phase) return;
+    if (I.stamps) {
+        // wave stamps of the site's own launch (disarmed again by timed_end,
+        // so a site that launches another form stores nothing)
+        if (I.stamp_q < I.stamp_max)
+            check(mpg_arnoldi_stamp_next(I.arn, I.stamps + 2 * I.stamp_cap * I.stamp_q++, I.stamp_cap), "stamp",
+                  I.ctx);
+        return;
+    }
     if (I.timed_graph) {
         // an external event node ahead of the site's own launch (its pair
         // follows the launch: timed_end)
         hipEvent_t e0;
         hipck(hipEventCreate(&e0), "event");
-        hipck(hipEventRecordWithFlags(e0, I.stream(), hipEventRecordExternal), "record (graph)");
         I.marks.push_back(e0);
+        capture_event_record(I.stream(), e0);
         return;
     }
     hipEvent_t e[2];
@@ -1013,11 +1041,16 @@ void FusedEngine::timed(int phase, F&& launch) {
 
 void FusedEngine::timed_end(int phase) {
     Impl& I = *p_;
-    if (I.timed != phase || !I.timed_graph) return;
+    if (I.timed != phase) return;
+    if (I.stamps) {
+        check(mpg_arnoldi_stamp_next(I.arn, nullptr, 0), "stamp", I.ctx);
+        return;
+    }
+    if (!I.timed_graph) return;
     hipEvent_t e1;
     hipck(hipEventCreate(&e1), "event");
-    hipck(hipEventRecordWithFlags(e1, I.stream(), hipEventRecordExternal), "record (graph)");
     I.marks.push_back(e1);
+    capture_event_record(I.stream(), e1);
 }
 
 // A phase kernel timed inside graph replays of the cycle (which: 0 the
@@ -1074,6 +1107,85 @@ double FusedEngine::time_phase_graph(int which, int reps, std::vector<double>* p
     }
     cleanup();
     return count ? total / count : 0.0;
+}
+
+// A phase kernel's own duration inside graph replays of the cycle (which: 0
+// the Arnoldi SpMV, 2 the one-panel CGS update, 3 the one-panel dots): the
+// cycle is captured once more (after a memset node clearing the slots) with
+// every launch of that phase storing its waves' wall-clock stamps
+// (mpg_arnoldi_stamp_next); a launch lasts max(end) - min(start) over its
+// waves -- the kernel alone, with no event packet in the queue around it.
+// Launches of another form at the phase's site (the panel kernels past 32
+// columns) store nothing and are skipped. Measurement only, like
+// time_phase_graph.
+double FusedEngine::time_phase_stamps(int which, int reps, std::vector<double>* per_launch) {
+    Impl& I = *p_;
+    if (!I.use_graph) throw StatusError(MPG_ERR_UNSUPPORTED, "the cycle is not captured (MPG_NO_GRAPH / eager ranks)");
+    if (which != 0 && which != 2 && which != 3) throw std::invalid_argument("phase: 0 spmv, 2 cgs update, 3 dots");
+    const int64_t cap = mpg_arnoldi_stamp_waves(I.arn);
+    if (cap < 1) throw StatusError(MPG_ERR_HIP, "no SpMV waves");
+    const int64_t slots = (int64_t)(I.m + 2);
+    const size_t bytes = (size_t)(2 * cap * slots) * sizeof(unsigned long long);
+    DevMem buf(I.ctx, bytes);
+    int dev = 0, khz = 0;
+    hipck(hipGetDevice(&dev), "device");
+    hipck(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev), "wall clock rate");
+    if (khz <= 0) throw StatusError(MPG_ERR_HIP, "no wall clock rate");
+    std::vector<unsigned long long> host(bytes / sizeof(unsigned long long));
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    double total = 0;
+    size_t count = 0;
+    I.timed = which;
+    I.stamps = buf.as<unsigned long long>();
+    I.stamp_cap = cap;
+    I.stamp_q = 0;
+    I.stamp_max = slots;
+    auto cleanup = [&] {
+        I.timed = -1;
+        I.stamps = nullptr;
+        I.stamp_q = I.stamp_max = 0;
+        if (ge) (void)hipGraphExecDestroy(ge);
+        if (g) (void)hipGraphDestroy(g);
+    };
+    try {
+        hipck(hipStreamBeginCapture(I.stream(), hipStreamCaptureModeThreadLocal), "begin capture");
+        try {
+            hipck(hipMemsetAsync(buf.p, 0, bytes, I.stream()), "clear stamps");
+            cycle_program();
+        } catch (...) {
+            (void)hipStreamEndCapture(I.stream(), &g);
+            throw;
+        }
+        hipck(hipStreamEndCapture(I.stream(), &g), "end capture");
+        hipck(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0), "instantiate");
+        const int64_t launches = I.stamp_q;
+        for (int r = 0; r < reps; ++r) {
+            hipck(hipGraphLaunch(ge, I.stream()), "graph launch");
+            hipck(hipStreamSynchronize(I.stream()), "sync");
+            hipck(hipMemcpy(host.data(), buf.p, bytes, hipMemcpyDeviceToHost), "read stamps");
+            for (int64_t q = 0; q < launches; ++q) {
+                const unsigned long long* st = host.data() + 2 * cap * q;
+                unsigned long long t0 = ~0ull, t1 = 0;
+                for (int64_t wv = 0; wv < cap; ++wv) {
+                    if (st[2 * wv] && st[2 * wv] < t0) t0 = st[2 * wv];
+                    if (st[2 * wv + 1] > t1) t1 = st[2 * wv + 1];
+                }
+                if (t0 == ~0ull || t1 <= t0) continue;  // another form ran at the site
+                const double ms = (double)(t1 - t0) / (double)khz;
+                total += ms;
+                ++count;
+                if (per_launch) per_launch->push_back(ms);
+            }
+        }
+    } catch (...) {
+        cleanup();
+        (void)hipGetLastError();
+        throw;
+    }
+    cleanup();
+    if (!count) throw StatusError(MPG_ERR_UNSUPPORTED, "no launch of the phase stored stamps");
+    return total / count;
 }
 
 // ---------------------------------------------------------------- mpg_solve (fused)
@@ -1194,11 +1306,33 @@ int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, dou
     }
 }
 
+int mpg_engine_time_phase_stamps(mpg_engine_t e, int which, int reps, double* avg_ms, double* per_launch_ms,
+                                 int cap) {
+    if (!e || !e->eng || !avg_ms || reps < 1 || cap < 0 || (cap && !per_launch_ms) ||
+        (which != 0 && which != 2 && which != 3))
+        return MPG_ERR_ARG;
+    e->last_error.clear();
+    try {
+        mpg::ScopedContext scope(e->ctx);
+        std::vector<double> t;
+        *avg_ms = e->eng->time_phase_stamps(which, reps, &t);
+        for (size_t i = 0; i < t.size() && (int)i < cap; ++i) per_launch_ms[i] = t[i];
+        return (int)t.size();
+    } catch (const mpg::StatusError& ex) {
+        e->last_error = ex.what();
+        return ex.status;
+    } catch (const std::exception& ex) {
+        e->last_error = ex.what();
+        return MPG_ERR_HIP;
+    }
+}
+
 int mpg_engine_time_phase_graph(mpg_engine_t e, int which, int reps, double* avg_ms, double* per_launch_ms,
                                 int cap) {
     if (!e || !e->eng || !avg_ms || reps < 1 || cap < 0 || (cap && !per_launch_ms) ||
         (which != 0 && which != 2 && which != 3))
         return MPG_ERR_ARG;
+    e->last_error.clear();
     try {
         mpg::ScopedContext scope(e->ctx);
         std::vector<double> t;
@@ -1206,8 +1340,10 @@ int mpg_engine_time_phase_graph(mpg_engine_t e, int which, int reps, double* avg
         for (size_t i = 0; i < t.size() && (int)i < cap; ++i) per_launch_ms[i] = t[i];
         return (int)t.size();
     } catch (const mpg::StatusError& ex) {
+        e->last_error = ex.what();
         return ex.status;
-    } catch (const std::exception&) {
+    } catch (const std::exception& ex) {
+        e->last_error = ex.what();
         return MPG_ERR_HIP;
     }
 }

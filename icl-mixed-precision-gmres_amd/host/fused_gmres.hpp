@@ -88,6 +88,7 @@ public:
     size_t total_iters() const { return conv_->total_iterations(); }
     double time_phase(int which, int reps, bool inplace = false, std::vector<double>* per_launch = nullptr);
     double time_phase_graph(int which, int reps, std::vector<double>* per_launch = nullptr);
+    double time_phase_stamps(int which, int reps, std::vector<double>* per_launch = nullptr);
     double phase_bytes(int which) const;
     mpg_arnoldi_t arnoldi() const;
     // mixed-half: what the fp16 cast of the Arnoldi values did (stats of

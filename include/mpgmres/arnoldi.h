@@ -188,6 +188,18 @@ const void* mpg_arnoldi_inv_dev(mpg_arnoldi_t a);
  * dots fused) records its own kernel start/stop on these hipEvent_t
  * (hipExtLaunchKernel events: the kernel alone, not the queue around it) */
 int mpg_arnoldi_time_next_spmv(mpg_arnoldi_t a, void* start_event, void* stop_event);
+/* measurement: the next stamped launch -- the Arnoldi SpMV (every form),
+ * the one-panel dots (k_dots_nc) or the one-panel CGS update
+ * (k_cgs_update_nc) -- stores, per wave q, the device wall clock
+ * (wall_clock64, hipDeviceAttributeWallClockRate kHz) at the wave's start
+ * to slots[2q] and at its end to slots[2q + 1] (device memory, 2 *
+ * cap_waves entries; waves that exit early store no end). Nothing is stored
+ * when the launch has more than cap_waves waves; slots = NULL disarms.
+ * Usable inside a stream capture: the kernel's duration is max(end) -
+ * min(start). */
+int mpg_arnoldi_stamp_next(mpg_arnoldi_t a, unsigned long long* slots, int64_t cap_waves);
+/* the most waves a stamped launch of this workspace has */
+int64_t mpg_arnoldi_stamp_waves(mpg_arnoldi_t a);
 
 /* Number of workgroups of the row-block phase kernels (partials per column). */
 int mpg_arnoldi_num_groups(mpg_arnoldi_t a);

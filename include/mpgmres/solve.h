@@ -133,9 +133,18 @@ int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms);
  * `cap` per-launch times in cycle order (measurement only: the cycles run
  * without the host's restart checks) */
 int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, double* per_launch_ms, int cap);
+/* a phase kernel's own duration inside graph replays of the cycle (which: 0
+ * the Arnoldi SpMV, 2 the one-panel CGS update k_cgs_update_nc, 3 the
+ * one-panel dots k_dots_nc): every launch of that phase in a captured cycle
+ * stores its waves' wall-clock stamps (mpg_arnoldi_stamp_next), duration =
+ * last wave end - first wave start; per-launch ms in cycle order, the launch
+ * count returned (MPG_ERR_UNSUPPORTED when the engine runs eagerly or no
+ * launch of the phase was a stamped form). Measurement only. */
+int mpg_engine_time_phase_stamps(mpg_engine_t e, int which, int reps, double* avg_ms, double* per_launch_ms,
+                                 int cap);
 /* a phase kernel timed inside graph replays of the cycle (which: 0 the
  * Arnoldi SpMV, 2 the CGS update, 3 the panel dots): the cycle captured with
- * an external event node on each side of every launch of that phase,
+ * an event-record node on each side of every launch of that phase,
  * replayed `reps` times; per-launch times in cycle order (step k), the
  * launch count returned (m per replay for 0; MPG_ERR_UNSUPPORTED when the
  * engine runs eagerly). Measurement only, like the in-cycle timing above. */

@@ -6,10 +6,13 @@ by launch index and set beside each:
      no timing of our own: rocprof alone),
   2. `--eager` eager cycles, every SpMV launch timed by its own
      hipExtLaunchKernel start/stop events (mpg_engine_time_spmv_incycle),
-  3. `--graph` replays of the cycle captured with an external event node on
-     each side of every SpMV (mpg_engine_time_spmv_graph).
-Prints one JSON line: the mean of 2 and 3, the launch counts of each block
-(m per cycle) and the workload.
+  3. `--graph` replays of the cycle captured with an event-record node on
+     each side of every SpMV (mpg_engine_time_phase_graph),
+  4. `--graph` replays of the cycle whose SpMV waves store their start / end
+     wall clock (mpg_engine_time_phase_stamps: no packet around the kernel).
+Prints one JSON line: the mean of 2, 3 and 4, the launch counts of each
+block (m per cycle) and the workload. With --torch, PyTorch's HIP runtime is
+loaded first, as in bench.py.
 usage: python tools/timing_probe.py [--rows 1000000] [--rlen 30]"""
 import argparse
 import json
@@ -29,7 +32,12 @@ def main():
     ap.add_argument("--warm", type=int, default=4)
     ap.add_argument("--eager", type=int, default=3)
     ap.add_argument("--graph", type=int, default=5)
+    ap.add_argument("--torch", action="store_true")
     args = ap.parse_args()
+    if args.torch:
+        import torch
+
+        torch.cuda.synchronize()
     from __graft_entry__ import _load
 
     mpg = _load()
@@ -42,22 +50,32 @@ def main():
     eng.sync()
     e_ms, e_per = eng.time_spmv_incycle(args.eager)
     g_ms, g_per = eng.time_phase_graph("spmv", args.graph)
+    s_ms, s_per = eng.time_phase_stamps("spmv", args.graph)
     phases = {}
     for ph in ("dots", "cgs_update"):
-        ms, per = eng.time_phase_graph(ph, args.graph)
-        m = args.rlen
-        byk = np.asarray(per[:len(per) // m * m]).reshape(-1, m).mean(axis=0) * 1e3
-        b, a = np.polyfit(np.arange(m), byk, 1)
-        phases[ph] = {"mean_us": round(1e3 * ms, 3), "fit_a_us": round(float(a), 3), "fit_b_us": round(float(b), 4)}
+        for clock, fn in (("graph_events", eng.time_phase_graph), ("stamps", eng.time_phase_stamps)):
+            try:
+                ms, per = fn(ph, args.graph)
+            except RuntimeError as ex:  # (stamps: only the one-panel forms, k + 1 <= 32)
+                phases[f"{ph}_{clock}"] = str(ex)
+                continue
+            m = args.rlen
+            byk = np.asarray(per[:len(per) // m * m]).reshape(-1, m).mean(axis=0) * 1e3 if len(per) % m == 0 \
+                else np.asarray(per) * 1e3
+            b, a = np.polyfit(np.arange(len(byk)), byk, 1)
+            phases[f"{ph}_{clock}"] = {"mean_us": round(1e3 * ms, 3), "launches": len(per), "fit_a_us": round(float(a), 3),
+                                       "fit_b_us": round(float(b), 4)}
     lay = eng.spmv_layout()
     eng.close()
     m = args.rlen
     print(json.dumps({
         "workload": f"BAND n={args.rows} mixed {args.orth} GMRES({m})", "layout": lay,
-        "blocks": {"warm_graph": args.warm * m, "eager_events": len(e_per), "graph_events": len(g_per)},
+        "blocks": {"warm_graph": args.warm * m, "eager_events": len(e_per), "graph_events": len(g_per),
+                   "graph_stamps": len(s_per)},
+        "stamp_us": round(1e3 * s_ms, 3), "stamp_median_us": round(1e3 * float(np.median(s_per)), 3),
         "eager_event_us": round(1e3 * e_ms, 3), "eager_event_median_us": round(1e3 * float(np.median(e_per)), 3),
         "graph_event_us": round(1e3 * g_ms, 3), "graph_event_median_us": round(1e3 * float(np.median(g_per)), 3),
-        "phases_graph_events": phases,
+        "phases": phases,
     }), flush=True)
 
 
