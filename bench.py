@@ -183,6 +183,9 @@ def phase_roofline(eng, rlen: int, reps: int, traffic: dict) -> dict:
         except RuntimeError:
             ms, per = eng.time_phase_graph(ph, reps)
             timing = "event-record nodes on each side of every launch in graph replays of the cycle"
+        if ms <= 0 or len(per) < rlen:  # the phase has no launch of its own (e.g. dots fused into the SpMV)
+            out[kname] = None
+            continue
         byk = np.asarray(per[:len(per) // rlen * rlen]).reshape(-1, rlen).mean(axis=0) * 1e3
         b, a = np.polyfit(np.arange(rlen), byk, 1)
         mb = eng.phase_bytes(ph)
