@@ -550,6 +550,8 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
             const int c = row0 - kWinLo + q * kWave + lane;
             wr[q] = wprev[c >= n_lo && c < n_ext ? c : 0];
         }
+    } else {
+        if (!rows) wr[0] = wprev[i < n ? i : 0];  // the round-3 order (unsorted copies)
     }
     __builtin_amdgcn_sched_barrier(0);
     // 3. the slice's first batch (UNI: the values before the pattern index
@@ -565,10 +567,13 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
         row.load(0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    // 3b. without the window: the lane's own row's w_prev (needed last)
+    // 3b. without the window, sorted (SELL-C-sigma) copies: the lane's row and
+    // its own w_prev, behind the first batch (needed last)
     if constexpr (!WIN) {
-        if (rows) i = rows[live ? row0 + lane : 0];
-        wr[0] = wprev[i < n ? i : 0];
+        if (rows) {
+            i = rows[live ? row0 + lane : 0];
+            wr[0] = wprev[i < n ? i : 0];
+        }
     }
     // 4. a scaled fp16 copy's row exponent (needed last, issued last)
     int rex = 0;
