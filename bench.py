@@ -93,14 +93,14 @@ def load_pkg():
     return _load()
 
 
-ROCPROF_STATS = "bench_kernel_stats.csv"
+ROCPROF_STATS = "bench_kernel_stats.rocprof"
 
 
 def rocprof_avg_ms(profile_dir: Path, kernel: str):
     """Mean duration (ms) over all launches of `kernel` (every template
     instance) in the committed rocprofv3 --kernel-trace --stats summary of
     `bench.py --steps 10 --no-cpu-baseline --hbm-rows 0 --surface-cycles 0`
-    (profiles/bench_kernel_stats.csv, this round's copy), None when absent:
+    (profiles/bench_kernel_stats.rocprof: the CSV, renamed so it travels with the tree), None when absent:
     the CP's timestamps of each dispatch, which rocprof reports, set beside
     the live wave-stamp time."""
     f = profile_dir / ROCPROF_STATS
@@ -137,25 +137,27 @@ def pmc_traffic(profile_dir: Path) -> dict:
 
 def spmv_roofline(eng, cycles: int) -> dict:
     """The Arnoldi SpMV in its place in the cycle (k = 0 plain, k >= 1 with
-    the Givens step folded): mean launch duration inside graph replays of
-    the cycle -- the form the timed region runs -- from the device wall
-    clock each wave stores at its start and end (first start to last end,
-    mpg_engine_time_phase_stamps: the kernel alone, as rocprofv3 times it);
-    the same launches between event-record nodes (which add the queue's
-    packet latency) beside it; eager cycles with each launch's own kernel
-    events when the engine does not capture its cycle. Bytes: what the
-    storage moves, and SURVEY 8(d)'s CSR bytes."""
+    the Givens step folded): what one launch adds to a graph replay of the
+    cycle -- the timed region's form -- measured with HIP events around
+    whole replays of the cycle as run and of the cycle with every SpMV
+    launched twice in a row (mpg_engine_time_phase_dup: the kernel plus its
+    dispatch and release, the figure rocprofv3's kernel trace reports); the
+    same launches between event-record nodes (which add two marker packets)
+    beside it; eager cycles with each launch's own kernel events when the
+    engine does not capture its cycle. Bytes: what the storage moves, and
+    SURVEY 8(d)'s CSR bytes."""
     layout = eng.spmv_layout()
     event_ms = None
     try:
-        avg_ms, per = eng.time_phase_stamps("spmv", cycles)
-        timing = "stamps"
+        avg_ms, n_added = eng.time_phase_dup("spmv", max(5, 2 * cycles))
+        per = [avg_ms] * n_added
+        timing = "dup"
         try:  # the same launches between event-record nodes, for comparison
             event_ms = eng.time_phase_graph("spmv", cycles)[0]
         except RuntimeError as ex:
             log(f"[bench] graph-event timing unavailable ({ex})")
     except RuntimeError as ex:
-        log(f"[bench] wave-stamp timing unavailable ({ex}); timing eager cycles")
+        log(f"[bench] duplicate-launch timing unavailable ({ex}); timing eager cycles")
         avg_ms, per = eng.time_spmv_incycle(cycles)
         timing = "eager"
     actual = eng.phase_bytes("spmv_storage")
@@ -178,12 +180,16 @@ def phase_roofline(eng, rlen: int, reps: int, traffic: dict) -> dict:
     out = {}
     for ph, kname in (("dots", "k_dots_nc"), ("cgs_update", "k_cgs_update_nc")):
         try:
-            ms, per = eng.time_phase_stamps(ph, reps)
-            timing = "wave wall-clock stamps, first start to last end, in graph replays of the cycle"
+            ms, n_added = eng.time_phase_dup(ph, max(5, 2 * reps))
+        except RuntimeError:  # the phase has no launch of its own (e.g. dots fused into the SpMV)
+            out[kname] = None
+            continue
+        timing = "HIP events around graph replays of the cycle as run and with the phase's launches doubled"
+        try:  # the kernel alone: its waves' wall-clock stamps, per k for the fit
+            k_ms, per = eng.time_phase_stamps(ph, reps)
         except RuntimeError:
-            ms, per = eng.time_phase_graph(ph, reps)
-            timing = "event-record nodes on each side of every launch in graph replays of the cycle"
-        if ms <= 0 or len(per) < rlen:  # the phase has no launch of its own (e.g. dots fused into the SpMV)
+            k_ms, per = eng.time_phase_graph(ph, reps)
+        if n_added < rlen or len(per) < rlen:
             out[kname] = None
             continue
         byk = np.asarray(per[:len(per) // rlen * rlen]).reshape(-1, rlen).mean(axis=0) * 1e3
@@ -192,7 +198,8 @@ def phase_roofline(eng, rlen: int, reps: int, traffic: dict) -> dict:
         ach = mb / (ms * 1e-3) / 1e9
         pmc = traffic.get(kname) if rlen <= 32 else None
         out[kname] = {"bytes_mean_k": int(mb), "avg_launch_ms": round(ms, 5), "achieved": round(ach, 1),
-                      "timing": timing,
+                      "timing": timing, "kernel_only_ms": round(k_ms, 5),
+                      "fit_basis": "wave wall-clock stamps per launch (first wave start to last wave end)",
                       "rocprof_avg_launch_ms": rocprof_avg_ms(REPO / "profiles", kname),
                       "frac": round(ach / HBM_PEAK_GBS, 4), "fit_a_us": round(float(a), 3),
                       "fit_b_us_per_column": round(float(b), 4),
@@ -379,7 +386,7 @@ def main():
     sp = spmv_roofline(eng, args.roofline_cycles)
     pmc = pmc_traffic(REPO / "profiles")
     phases = (phase_roofline(eng, args.rlen, args.roofline_cycles, pmc)
-              if args.orth == "cgs" and world == 1 and sp["timing"] == "stamps" else None)
+              if args.orth == "cgs" and world == 1 and sp["timing"] == "dup" else None)
     # the whole CGS Arnoldi iteration on the same footing: the SpMV's storage
     # bytes + the panel dots and the CGS update at the cycle's mean k (the
     # once-per-cycle prologue and solution update are left out, so this
@@ -445,9 +452,9 @@ def main():
                     "kernel": sp["kernel"] + (" (in-cycle, Givens folded for k >= 1)" if sp["layout"]["givens_folded"]
                                               else " (in-cycle; the Givens step has its own launch)"),
                     "avg_launch_ms": round(sp["avg_launch_ms"], 5), "launches_timed": sp["launches"],
-                    "timing": ("device wall clock (wall_clock64, 100 MHz) stored by every wave at its start and "
-                               "end, first start to last end of each SpMV launch inside graph replays of the cycle "
-                               "(the timed region's form)" if sp["timing"] == "stamps" else
+                    "timing": ("HIP events around graph replays of the cycle as run and with every SpMV launched "
+                               "twice in a row; median replay-time difference over the added launches (kernel + "
+                               "dispatch + release, the timed region's form)" if sp["timing"] == "dup" else
                                "hipExtLaunchKernel start/stop events of each launch of eager cycles"),
                     "event_graph_ms": round(sp["event_graph_ms"], 5) if sp["event_graph_ms"] else None,
                     "rocprof_avg_launch_ms": rocprof_avg_ms(REPO / "profiles", sp["kernel"]),

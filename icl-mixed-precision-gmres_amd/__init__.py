@@ -102,6 +102,8 @@ def _declare_host(lib: C.CDLL) -> None:
                                                  C.POINTER(C.c_double), C.c_int]
     lib.mpg_engine_time_phase_graph.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
                                                 C.POINTER(C.c_double), C.c_int]
+    lib.mpg_engine_time_phase_dup.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
+                                              C.POINTER(C.c_int64)]
     lib.mpg_engine_time_phase_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double),
                                                  C.POINTER(C.c_double), C.c_int]
     lib.mpg_engine_last_error.argtypes = [C.c_void_p]
@@ -699,6 +701,21 @@ class Engine:
             msg = self._lib.mpg_engine_last_error(self._h).decode(errors="replace")
             raise RuntimeError(f"mpg_engine_time_phase_graph failed ({cnt}): {msg}")
         return ms.value, [per[i] for i in range(min(cnt, cap))]
+
+    def time_phase_dup(self, phase: str = "spmv", reps: int = 5) -> tuple:
+        """(ms, added launches): what one launch of a phase kernel ("spmv",
+        "cgs_update", "dots") adds to a graph replay of the cycle -- the cycle
+        captured as run and with that phase's launches doubled, replayed
+        alternately between HIP events (mpg_engine_time_phase_dup); the
+        stream-share figure rocprofv3 reports. Measurement only."""
+        ms = C.c_double()
+        n = C.c_int64()
+        which = {"spmv": 0, "cgs_update": 2, "dots": 3}[phase]
+        st = self._lib.mpg_engine_time_phase_dup(self._h, which, reps, C.byref(ms), C.byref(n))
+        if st != 0:
+            msg = self._lib.mpg_engine_last_error(self._h).decode(errors="replace")
+            raise RuntimeError(f"mpg_engine_time_phase_dup failed ({st}): {msg}")
+        return ms.value, int(n.value)
 
     def time_phase_stamps(self, phase: str = "spmv", reps: int = 3) -> tuple:
         """(mean ms, per-launch ms in cycle order) of a phase kernel ("spmv",

@@ -387,21 +387,18 @@ struct GivensFold {
     const double* norm2;  // nullptr: not folded (use *inv_p)
     int nparts;
     GivensArgs<T> g;
-    // measurement only (mpg_arnoldi_stamp_next; nullptr in a solve):
-    // wave q's lane 0 stores the wall clock at its start to stamp[2q] and
-    // at its end to stamp[2q + 1]
-    unsigned long long* stamp = nullptr;
 };
 
-// measurement only: wave q's lane 0 stores the wall clock to stamp[2q + end]
-// (end 0 at the wave's start, 1 at its end); a one-dimensional grid
+// measurement only (mpg_arnoldi_stamp_next): wave q's lane 0 stores the
+// wall clock to stamp[2q + end] (end 0 at the wave's start, 1 at its end); a
+// one-dimensional grid. Used by the one-panel dots and CGS update only: in
+// the SpMVs, whose occupancy sits on VGPR thresholds, even this uniform
+// branch cost up to 20 VGPRs (C4's stepped kernel 71 -> 91, -11 % in time),
+// and a branch-free form with a sink word slowed the BAND SpMV; the SpMV is
+// timed by duplicate launches instead (time_phase_dup, host/fused_gmres.cpp).
 __device__ __forceinline__ void stamp_at(unsigned long long* stamp, int end) {
     if (stamp && (threadIdx.x & (kWave - 1)) == 0)
         stamp[2 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave) + end] = wall_clock64();
-}
-template <class T>
-__device__ __forceinline__ void stamp_wave(const GivensFold<T>& f, int end) {
-    stamp_at(f.stamp, end);
 }
 
 template <bool FOLD, class T>
@@ -437,7 +434,6 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
                                                       GivensFold<T> fold, const int8_t* __restrict__ rexp) {
     __shared__ double prod[kNnzCap];
     __shared__ double scratch[kBlock / kWave];
-    stamp_wave(fold, 0);
     const T inv = fold_givens<FOLD>(fold, inv_p);
     T* __restrict__ Vk = V + (int64_t)k * ld;
     struct Ops {
@@ -456,7 +452,6 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
             Vk[i] = o.wp * inv;
         },
         prod, scratch);
-    stamp_wave(fold, 1);
 }
 
 // ---------------------------------------------------------------- step: SpMV (SELL-64)
@@ -513,7 +508,6 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
     constexpr int NQ = kWinLen / kWave;
     __shared__ T win[WIN ? BS / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
-    stamp_wave(fold, 0);
     const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid;
     const bool live = s < nslices;  // a dead wave still joins the fold's barriers
     const int row0 = s * kWave;
@@ -714,7 +708,6 @@ __global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, in
         __shared__ T col_s[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
         if (blockIdx.x == 0) givens_block(fold.g, nrm2sq, col_s, c_s, s_s);
     }
-    stamp_wave(fold, 1);
 }
 
 // k_step_sell with two adjacent slices per wave (lane l owns rows
@@ -747,7 +740,6 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
     constexpr int NQ = WL / kWave;
     __shared__ T win[WIN ? BS / kWave : 1][WIN ? WL : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
-    stamp_wave(fold, 0);
     const int s0 = ((xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid) * SPW;
     const bool live = s0 < nslices;  // a dead wave still joins the fold's barriers
     bool live_p[SPW];
@@ -918,7 +910,6 @@ __global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, i
         __shared__ T col_s[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
         if (blockIdx.x == 0) givens_block(fold.g, nrm2sq, col_s, c_s, s_s);
     }
-    stamp_wave(fold, 1);
 }
 
 // Tall-skinny panel reduction: partial <v_j, w> for j in [c0, c0 + nc),
@@ -2032,16 +2023,6 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
         GivensFold<T> gf{nullptr, 0, {}};
         if (fold)
             gf = GivensFold<T>{fold == 2 ? a->last_part : a->sums, fold == 2 ? a->last_G : 0, givens_args<T>(a, k - 1)};
-        // measurement: this launch's wave stamps (mpg_arnoldi_stamp_next),
-        // when the slots hold all of its waves
-        unsigned long long* const stamp = a->ctx->stamp_next;
-        const int64_t stamp_cap = a->ctx->stamp_cap;
-        a->ctx->stamp_next = nullptr;
-        auto stamped = [&](int64_t waves) {
-            GivensFold<T> g = gf;
-            g.stamp = stamp && waves <= stamp_cap ? stamp : nullptr;
-            return g;
-        };
         if (a->sell.nslices > 0) {
             const auto& S = a->sell;
             if (fold == 2 && a->last_G > kBlock) return (int)MPG_ERR_ARG;  // k_step_sell folds <= kBlock partials
@@ -2055,8 +2036,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                             a->d.n, -a->front, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
                             static_cast<const typename SellStore<VI>::type*>(S.val),
                             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
-                            static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]),
-                            stamped((int64_t)grid * (BS / kWave)), dd,
+                            static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd,
                             S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
                             static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
                             S.ustride, sell_xcd_order(S) ? 1 : 0, S.rows);
@@ -2087,8 +2067,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                                     a->d.n, -a->front, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
                                     static_cast<const typename SellStore<VI>::type*>(S.val),
                                     static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
-                                    static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]),
-                                    stamped((int64_t)grid * (kStepSellBlock / kWave)),
+                                    static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf,
                                     SellDots{}, S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
                                     static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
                                     S.ustride, sell_xcd_order(S) ? 1 : 0);
@@ -2137,8 +2116,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
         launch_timed(a->ctx, kern, dim3(rb_grid(a)), dim3(kBlock),
             A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,
             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,
-            diag, static_cast<T*>(a->w[(k + 1) & 1]), stamped((int64_t)rb_grid(a) * (kBlock / kWave)),
-            a->d.inner_row_exp);
+            diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp);
         return (int)MPG_OK;
     });
     if (st) return st;
@@ -2446,13 +2424,10 @@ int mpg_arnoldi_stamp_next(mpg_arnoldi_t a, unsigned long long* slots, int64_t c
 }
 int64_t mpg_arnoldi_stamp_waves(mpg_arnoldi_t a) {
     if (!a) return MPG_ERR_ARG;
-    // the most waves a stamped launch has: the SpMV (a wave per slice, the
-    // pair kernel half of that, rounded up to whole workgroups, or the
-    // CSR-adaptive grid), the one-panel dots / CGS update (Gd 1024-thread
-    // workgroups, or row_grid 256-thread ones for CGSR's first pass)
-    int64_t w = a->sell.nslices > 0 ? a->sell.nslices + 1024 / kWave : 0;
-    w = std::max<int64_t>(w, (int64_t)rb_grid(a) * (kBlock / kWave));
-    w = std::max<int64_t>(w, (int64_t)a->Gd * (kCombineBlock / kWave));
+    // the most waves a stamped launch has: the one-panel dots / CGS update
+    // (Gd 1024-thread workgroups, or row_grid 256-thread ones for CGSR's
+    // first pass)
+    int64_t w = (int64_t)a->Gd * (kCombineBlock / kWave);
     w = std::max<int64_t>(w, (int64_t)row_grid(a) * (kBlock / kWave));
     return w;
 }

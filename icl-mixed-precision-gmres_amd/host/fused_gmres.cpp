@@ -2,6 +2,7 @@
 // mpg_solve with engine = MPG_ENGINE_FUSED).
 #include "fused_gmres.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -124,6 +125,8 @@ struct FusedEngine::Impl {
     bool timed_graph = false;        // ... external event nodes around it in a captured cycle
     std::vector<hipEvent_t> marks;   // ... begin/end pairs
     unsigned long long* stamps = nullptr;  // time_phase_stamps: wave stamp slots of each timed launch
+    int dup_phase = -1;   // time_phase_dup: phase whose site launches its kernel twice
+    int64_t dup_count = 0;  // ... extra launches captured
     int64_t stamp_cap = 0, stamp_q = 0, stamp_max = 0;  // waves per launch, launches armed, launch slots
     std::vector<int32_t> rowptr_host;
     mpg_ilu_t ilu = nullptr;  // ILU(0) factors (prec ilu / ilu_jacobi), applied between phase kernels
@@ -513,11 +516,13 @@ void FusedEngine::step(int k, bool fold) {
                                            I.stream());
         timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
         check(mpg_arnoldi_givens_partials_spmv(I.arn, k), "givens+spmv", I.ctx);
+        dup(0, [&] { check(mpg_arnoldi_givens_partials_spmv(I.arn, k), "givens+spmv", I.ctx); });
         timed_end(0);
     } else {
         if (I.comm) I.comm->halo(mpg_arnoldi_wprev_dev(I.arn, k), mpg_arnoldi_vec_bytes(I.arn), I.stream());
         timed(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
         check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx);
+        dup(0, [&] { check(mpg_arnoldi_spmv(I.arn, k), "spmv", I.ctx); });
         timed_end(0);
     }
     if (I.ilu) I.apply_ilu(mpg_arnoldi_wprev_dev(I.arn, k + 1));  // w = M(A v_k)
@@ -555,11 +560,13 @@ void FusedEngine::step(int k, bool fold) {
         } else {
             timed(3, [&] { check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx); });
             check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
+            dup(3, [&] { check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx); });
             timed_end(3);
             if (I.cgs_partials && small) {
                 if (I.comm) allreduce_partials(k + 1);
                 timed(2, [&] { check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx); });
                 check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx);
+                dup(2, [&] { check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx); });
                 timed_end(2);
                 pass0_done = true;
             } else {
@@ -579,6 +586,7 @@ void FusedEngine::step(int k, bool fold) {
         }
         timed(2, [&] { check(mpg_arnoldi_cgs(I.arn, k, last_pass), "cgs", I.ctx); });
         check(mpg_arnoldi_cgs(I.arn, k, last_pass), "cgs", I.ctx);
+        dup(2, [&] { check(mpg_arnoldi_cgs(I.arn, k, last_pass), "cgs", I.ctx); });
         timed_end(2);
     }
     if (!fold) givens(k);
@@ -1005,6 +1013,16 @@ static void capture_event_record(hipStream_t st, hipEvent_t ev) {
     hipck(hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies), "capture tail");
 }
 
+// time_phase_dup: the site's own launch once more, right behind it (the same
+// kernel, arguments and queue position)
+template <class F>
+void FusedEngine::dup(int phase, F&& launch) {
+    Impl& I = *p_;
+    if (I.dup_phase != phase) return;
+    launch();
+    ++I.dup_count;
+}
+
 template <class F>
 void FusedEngine::timed(int phase, F&& launch) {
     Impl& I = *p_;
@@ -1188,6 +1206,76 @@ double FusedEngine::time_phase_stamps(int which, int reps, std::vector<double>* 
     return total / count;
 }
 
+// A phase kernel's share of the stream inside graph replays of the cycle
+// (which: 0 the Arnoldi SpMV in the form each step runs, 2 the CGS update, 3
+// the panel dots), from HIP events around whole replays: the cycle is
+// captured twice, as the solve runs it and with every launch of that phase
+// issued twice in a row, and the graphs are replayed alternately; the
+// difference of the replay times over the number of added launches is what
+// one launch adds to the cycle -- the kernel plus its dispatch and release,
+// with no marker packet near it (what rocprofv3's kernel duration measures).
+// The duplicates run on the state the first launch left: the SpMV and the
+// dots rewrite the same outputs; a second CGS update subtracts V h once more
+// (the basis stays normalised). Measurement only, like time_phase_graph.
+double FusedEngine::time_phase_dup(int which, int reps, int64_t* launches) {
+    Impl& I = *p_;
+    if (!I.use_graph) throw StatusError(MPG_ERR_UNSUPPORTED, "the cycle is not captured (MPG_NO_GRAPH / eager ranks)");
+    if (which != 0 && which != 2 && which != 3) throw std::invalid_argument("phase: 0 spmv, 2 cgs update, 3 dots");
+    hipGraph_t g[2] = {nullptr, nullptr};
+    hipGraphExec_t ge[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    auto cleanup = [&] {
+        I.dup_phase = -1;
+        for (int q = 0; q < 2; ++q) {
+            if (ge[q]) (void)hipGraphExecDestroy(ge[q]);
+            if (g[q]) (void)hipGraphDestroy(g[q]);
+            if (ev[q]) (void)hipEventDestroy(ev[q]);
+        }
+    };
+    std::vector<double> diff;
+    int64_t added = 0;
+    try {
+        for (int q = 0; q < 2; ++q) {
+            I.dup_phase = q ? which : -1;
+            I.dup_count = 0;
+            hipck(hipStreamBeginCapture(I.stream(), hipStreamCaptureModeThreadLocal), "begin capture");
+            try {
+                cycle_program();
+            } catch (...) {
+                (void)hipStreamEndCapture(I.stream(), &g[q]);
+                throw;
+            }
+            hipck(hipStreamEndCapture(I.stream(), &g[q]), "end capture");
+            hipck(hipGraphInstantiate(&ge[q], g[q], nullptr, nullptr, 0), "instantiate");
+            if (q) added = I.dup_count;
+        }
+        I.dup_phase = -1;
+        if (added < 1) throw StatusError(MPG_ERR_UNSUPPORTED, "the cycle has no launch of that phase");
+        for (hipEvent_t& e : ev) hipck(hipEventCreate(&e), "event");
+        for (int q = 0; q < 2; ++q) hipck(hipGraphLaunch(ge[q], I.stream()), "graph launch");  // warm
+        hipck(hipStreamSynchronize(I.stream()), "sync");
+        for (int r = 0; r < reps; ++r) {
+            float ms[2] = {0, 0};
+            for (int q = 0; q < 2; ++q) {
+                hipck(hipEventRecord(ev[0], I.stream()), "record");
+                hipck(hipGraphLaunch(ge[q], I.stream()), "graph launch");
+                hipck(hipEventRecord(ev[1], I.stream()), "record");
+                hipck(hipEventSynchronize(ev[1]), "sync");
+                hipck(hipEventElapsedTime(&ms[q], ev[0], ev[1]), "elapsed");
+            }
+            diff.push_back((double)(ms[1] - ms[0]) / (double)added);
+        }
+    } catch (...) {
+        cleanup();
+        (void)hipGetLastError();
+        throw;
+    }
+    cleanup();
+    if (launches) *launches = added;
+    std::sort(diff.begin(), diff.end());
+    return diff[diff.size() / 2];
+}
+
 // ---------------------------------------------------------------- mpg_solve (fused)
 void fill_history(const FusedEngine& e, mpg_solve_result* r) {
     r->status = e.status;
@@ -1302,6 +1390,22 @@ int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, dou
         for (size_t i = 0; i < t.size() && (int)i < cap; ++i) per_launch_ms[i] = t[i];
         return (int)t.size();
     } catch (const std::exception&) {
+        return MPG_ERR_HIP;
+    }
+}
+
+int mpg_engine_time_phase_dup(mpg_engine_t e, int which, int reps, double* avg_ms, int64_t* launches) {
+    if (!e || !e->eng || !avg_ms || reps < 1 || (which != 0 && which != 2 && which != 3)) return MPG_ERR_ARG;
+    e->last_error.clear();
+    try {
+        mpg::ScopedContext scope(e->ctx);
+        *avg_ms = e->eng->time_phase_dup(which, reps, launches);
+        return MPG_OK;
+    } catch (const mpg::StatusError& ex) {
+        e->last_error = ex.what();
+        return ex.status;
+    } catch (const std::exception& ex) {
+        e->last_error = ex.what();
         return MPG_ERR_HIP;
     }
 }

@@ -89,6 +89,7 @@ public:
     double time_phase(int which, int reps, bool inplace = false, std::vector<double>* per_launch = nullptr);
     double time_phase_graph(int which, int reps, std::vector<double>* per_launch = nullptr);
     double time_phase_stamps(int which, int reps, std::vector<double>* per_launch = nullptr);
+    double time_phase_dup(int which, int reps, int64_t* launches = nullptr);
     double phase_bytes(int which) const;
     mpg_arnoldi_t arnoldi() const;
     // mixed-half: what the fp16 cast of the Arnoldi values did (stats of
@@ -120,6 +121,8 @@ private:
     void givens(int k);
     template <class F>
     void timed(int phase, F&& launch);
+    template <class F>
+    void dup(int phase, F&& launch);
     void timed_end(int phase);
     void update(int k);
     void store_next_basis(int k);

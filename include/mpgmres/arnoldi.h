@@ -188,9 +188,9 @@ const void* mpg_arnoldi_inv_dev(mpg_arnoldi_t a);
  * dots fused) records its own kernel start/stop on these hipEvent_t
  * (hipExtLaunchKernel events: the kernel alone, not the queue around it) */
 int mpg_arnoldi_time_next_spmv(mpg_arnoldi_t a, void* start_event, void* stop_event);
-/* measurement: the next stamped launch -- the Arnoldi SpMV (every form),
- * the one-panel dots (k_dots_nc) or the one-panel CGS update
- * (k_cgs_update_nc) -- stores, per wave q, the device wall clock
+/* measurement: the next stamped launch -- the one-panel dots (k_dots_nc) or
+ * the one-panel CGS update (k_cgs_update_nc); not the SpMVs, whose occupancy
+ * the stamp code would change -- stores, per wave q, the device wall clock
  * (wall_clock64, hipDeviceAttributeWallClockRate kHz) at the wave's start
  * to slots[2q] and at its end to slots[2q + 1] (device memory, 2 *
  * cap_waves entries; waves that exit early store no end). Nothing is stored

@@ -133,9 +133,18 @@ int mpg_engine_time_phase(mpg_engine_t e, int which, int reps, double* avg_ms);
  * `cap` per-launch times in cycle order (measurement only: the cycles run
  * without the host's restart checks) */
 int mpg_engine_time_spmv_incycle(mpg_engine_t e, int cycles, double* avg_ms, double* per_launch_ms, int cap);
-/* a phase kernel's own duration inside graph replays of the cycle (which: 0
- * the Arnoldi SpMV, 2 the one-panel CGS update k_cgs_update_nc, 3 the
- * one-panel dots k_dots_nc): every launch of that phase in a captured cycle
+/* a phase kernel's share of the stream inside graph replays of the cycle
+ * (which: 0 the Arnoldi SpMV in the form each step runs, 2 the CGS update, 3
+ * the panel dots): the cycle captured as the solve runs it and with every
+ * launch of that phase issued twice in a row, replayed alternately `reps`
+ * times between HIP events; *avg_ms = the median difference of the replay
+ * times over the added launches (*launches, may be NULL) -- kernel plus
+ * dispatch and release, as rocprofv3's kernel durations. MPG_ERR_UNSUPPORTED
+ * when the engine runs eagerly. Measurement only. */
+int mpg_engine_time_phase_dup(mpg_engine_t e, int which, int reps, double* avg_ms, int64_t* launches);
+/* a phase kernel's own duration inside graph replays of the cycle (which: 2
+ * the one-panel CGS update k_cgs_update_nc, 3 the one-panel dots k_dots_nc;
+ * the SpMV stores no stamps): every launch of that phase in a captured cycle
  * stores its waves' wall-clock stamps (mpg_arnoldi_stamp_next), duration =
  * last wave end - first wave start; per-launch ms in cycle order, the launch
  * count returned (MPG_ERR_UNSUPPORTED when the engine runs eagerly or no
