@@ -127,6 +127,7 @@ struct FusedEngine::Impl {
     unsigned long long* stamps = nullptr;  // time_phase_stamps: wave stamp slots of each timed launch
     int dup_phase = -1;   // time_phase_dup: phase whose site launches its kernel twice
     int64_t dup_count = 0;  // ... extra launches captured
+    int64_t dup_with_dots = 0;  // ... of which re-ran the dots ahead of a CGS update
     int64_t stamp_cap = 0, stamp_q = 0, stamp_max = 0;  // waves per launch, launches armed, launch slots
     std::vector<int32_t> rowptr_host;
     mpg_ilu_t ilu = nullptr;  // ILU(0) factors (prec ilu / ilu_jacobi), applied between phase kernels
@@ -566,7 +567,14 @@ void FusedEngine::step(int k, bool fold) {
                 if (I.comm) allreduce_partials(k + 1);
                 timed(2, [&] { check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx); });
                 check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx);
-                dup(2, [&] { check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx); });
+                // (the in-launch sums read the dots' partials, which the first
+                // update's own partials replaced: the duplicate re-runs the
+                // dots first, and time_phase_dup takes their share back out)
+                dup(2, [&] {
+                    check(mpg_arnoldi_dots(I.arn, k), "dots", I.ctx);
+                    check(mpg_arnoldi_cgs_partials(I.arn, k), "cgs", I.ctx);
+                    ++I.dup_with_dots;
+                });
                 timed_end(2);
                 pass0_done = true;
             } else {
@@ -1216,7 +1224,9 @@ double FusedEngine::time_phase_stamps(int which, int reps, std::vector<double>* 
 // with no marker packet near it (what rocprofv3's kernel duration measures).
 // The duplicates run on the state the first launch left: the SpMV and the
 // dots rewrite the same outputs; a second CGS update subtracts V h once more
-// (the basis stays normalised). Measurement only, like time_phase_graph.
+// (the basis stays normalised; an update that sums the dots' partials itself
+// gets the dots re-run ahead of it, whose own share is measured and taken
+// out). Measurement only, like time_phase_graph.
 double FusedEngine::time_phase_dup(int which, int reps, int64_t* launches) {
     Impl& I = *p_;
     if (!I.use_graph) throw StatusError(MPG_ERR_UNSUPPORTED, "the cycle is not captured (MPG_NO_GRAPH / eager ranks)");
@@ -1233,11 +1243,12 @@ double FusedEngine::time_phase_dup(int which, int reps, int64_t* launches) {
         }
     };
     std::vector<double> diff;
-    int64_t added = 0;
+    int64_t added = 0, with_dots = 0;
     try {
         for (int q = 0; q < 2; ++q) {
             I.dup_phase = q ? which : -1;
             I.dup_count = 0;
+            I.dup_with_dots = 0;
             hipck(hipStreamBeginCapture(I.stream(), hipStreamCaptureModeThreadLocal), "begin capture");
             try {
                 cycle_program();
@@ -1247,7 +1258,10 @@ double FusedEngine::time_phase_dup(int which, int reps, int64_t* launches) {
             }
             hipck(hipStreamEndCapture(I.stream(), &g[q]), "end capture");
             hipck(hipGraphInstantiate(&ge[q], g[q], nullptr, nullptr, 0), "instantiate");
-            if (q) added = I.dup_count;
+            if (q) {
+                added = I.dup_count;
+                with_dots = I.dup_with_dots;
+            }
         }
         I.dup_phase = -1;
         if (added < 1) throw StatusError(MPG_ERR_UNSUPPORTED, "the cycle has no launch of that phase");
@@ -1273,7 +1287,9 @@ double FusedEngine::time_phase_dup(int which, int reps, int64_t* launches) {
     cleanup();
     if (launches) *launches = added;
     std::sort(diff.begin(), diff.end());
-    return diff[diff.size() / 2];
+    double ms = diff[diff.size() / 2];
+    if (with_dots) ms -= time_phase_dup(3, reps) * (double)with_dots / (double)added;
+    return ms;
 }
 
 // ---------------------------------------------------------------- mpg_solve (fused)
