@@ -127,9 +127,23 @@ __global__ __launch_bounds__(kBlock) void k_gemv_n_nc(int64_t rows, T alpha, con
 // Stage 2 of gemv^T: one wave per column, lane l summing partials l, l + 64,
 // ... in order, then the wave's shuffle tree. The fused gemv (N)
 // forms its coefficients with the same function, so both give the same bits.
+// The loads go out four at a time (clamped addresses) before the adds, which
+// stay the same adds in the same order: a runtime-count loop otherwise waits
+// one memory latency per partial (the fused gemv's fixed cost, round 4).
 __device__ __forceinline__ double column_sum(const double* __restrict__ partial, int nparts, int c, int lane) {
+    const double* __restrict__ p = partial + (int64_t)c * nparts;
     double v = 0.0;
-    for (int j = lane; j < nparts; j += kWave) v += partial[(int64_t)c * nparts + j];
+    for (int j = lane; j < nparts; j += 4 * kWave) {
+        double q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int jj = j + u * kWave;
+            q[u] = p[jj < nparts ? jj : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (j + u * kWave < nparts) v += q[u];
+    }
     return wave_sum(v);
 }
 
