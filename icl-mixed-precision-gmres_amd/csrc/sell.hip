@@ -431,8 +431,13 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
     int best_w = 1;
     int64_t best = 0;
     choose(width, best_w, best);
-    // SELL-C-sigma (MPG_SELL_SIGMA: the window in rows, default 1024; 0 off;
-    // -1 always, for tests): rows of varying length in one slice pad it to its
+    // SELL-C-sigma (MPG_SELL_SIGMA: the window in rows when slicing pads more
+    // than 20 %; default 0 = off; -1 always, window 1024, for tests). Off by
+    // default since measured: on fem27 at 4.1M rows the sorted copy's SpMV
+    // took 486 us against 418 us unsorted and 423 us CSR (fem27 permuted:
+    // 549 / 463 / 458 us; profiles/r04y_irr.jsonl) -- the sorted lanes'
+    // scattered row stores and x gathers cost more than the padding they
+    // save. Rows of varying length in one slice pad it to its
     // longest row (the FEM-like fem27 stand-in: 26 % at W = 4). Sorting the
     // rows of each window of sigma rows by length (longest first, stable) and
     // slicing that order brings the padding to ~5 %, at the price of the
@@ -443,7 +448,7 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
     std::vector<int32_t> order;
     {
         const char* se = std::getenv("MPG_SELL_SIGMA");
-        const int sg = se && *se ? std::atoi(se) : 1024;
+        const int sg = se && *se ? std::atoi(se) : 0;
         const int sigma = sg < 0 ? 1024 : sg / kWave * kWave;
         if (sigma >= kWave && (sg < 0 || (double)best > 1.2 * (double)A->nnz)) {
             std::vector<int32_t> ord((size_t)ns * kWave);

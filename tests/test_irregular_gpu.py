@@ -37,16 +37,30 @@ def problems(mpg):
     return {w: _problem(mpg, w) for w in ("stencil27p", "fem27", "fem27p")}
 
 
-@pytest.mark.parametrize("fmt", ["auto", "sell", "csr"])
+def _fmt(fmt, monkeypatch):
+    """"sell-sigma": the SELL copy in SELL-C-sigma order (MPG_SELL_SIGMA=-1:
+    rows sorted by length in windows of 1024; off by default, sell.hip)."""
+    if fmt == "sell-sigma":
+        monkeypatch.setenv("MPG_SELL_SIGMA", "-1")
+        return "sell"
+    monkeypatch.delenv("MPG_SELL_SIGMA", raising=False)
+    return fmt
+
+
+@pytest.mark.parametrize("fmt", ["auto", "sell", "csr", "sell-sigma"])
 @pytest.mark.parametrize("which", ["stencil27p", "fem27", "fem27p"])
-def test_irregular_layout(mpg, problems, which, fmt):
+def test_irregular_layout(mpg, problems, which, fmt, monkeypatch):
     """What each storage choice runs: the permuted matrices never get 16-bit
     or implicit columns; auto keeps SELL only when padding adds <= 20 %."""
     A, xt, b = problems[which]
     eng = mpg.Engine(A, b, xt, mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=2,
-                     spmv_format=fmt)
+                     spmv_format=_fmt(fmt, monkeypatch))
     lay, cols = eng.spmv_layout(), eng.sell_columns()
     eng.close()
+    assert (cols["sigma"] > 0) == (fmt == "sell-sigma"), (fmt, cols)
+    if fmt == "sell-sigma":
+        assert lay["format"] == "sell" and cols["form"] == "int32" and cols["implicit_slices"] == 0, cols
+        return
     if fmt == "csr":
         assert lay["format"] == "csr" and cols["form"] == "none", (lay, cols)
         return
@@ -61,15 +75,16 @@ def test_irregular_layout(mpg, problems, which, fmt):
         assert fmt == "auto" and cols["form"] == "none"
 
 
-@pytest.mark.parametrize("engine,fmt", [("fused", "auto"), ("fused", "sell"), ("fused", "csr"), ("surface", "auto")])
+@pytest.mark.parametrize("engine,fmt", [("fused", "auto"), ("fused", "sell"), ("fused", "csr"), ("fused", "sell-sigma"),
+                                        ("surface", "auto"), ("surface", "sell-sigma")])
 @pytest.mark.parametrize("mode,orth", [("mixed", "cgs"), ("baseline", "mgs"), ("mixed", "cgsr")])
 @pytest.mark.parametrize("which", ["stencil27p", "fem27", "fem27p"])
-def test_irregular_live_oracle(mpg, oracle, problems, which, mode, orth, engine, fmt):
+def test_irregular_live_oracle(mpg, oracle, problems, which, mode, orth, engine, fmt, monkeypatch):
     A, xt, b = problems[which]
     opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=1e-10, max_restarts=200)
     ref = _oracle_runs(mpg, oracle, problems, which, mode, orth, opts)
     assert ref["loops"].status == "converged"
-    got = mpg.solve(A, b, xt, engine=engine, spmv_format=fmt, **opts)
+    got = mpg.solve(A, b, xt, engine=engine, spmv_format=_fmt(fmt, monkeypatch), **opts)
     label = f"{which}-{mode}-{orth}/{engine}-{fmt}"
     compare(as_ref(ref["loops"]), got, mode, opts["tol"], 30, label)
     not_worse_than(ref["mkl"], got, mode, label + " vs mkl")
