@@ -36,7 +36,11 @@ the median of the timed runs per orthogonalisation.
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -158,6 +162,10 @@ def spmv_roofline(eng, cycles: int) -> dict:
             log(f"[bench] graph-event timing unavailable ({ex})")
     except RuntimeError as ex:
         log(f"[bench] duplicate-launch timing unavailable ({ex}); timing eager cycles")
+        avg_ms, per, timing = None, None, "eager"
+    if avg_ms is None or not avg_ms > 0:  # unavailable, or a degenerate difference of replay times
+        if timing == "dup":
+            log(f"[bench] duplicate-launch difference {avg_ms} ms is not a launch time; timing eager cycles")
         avg_ms, per = eng.time_spmv_incycle(cycles)
         timing = "eager"
     actual = eng.phase_bytes("spmv_storage")
@@ -190,6 +198,9 @@ def phase_roofline(eng, rlen: int, reps: int, traffic: dict) -> dict:
         except RuntimeError:
             k_ms, per = eng.time_phase_graph(ph, reps)
         if n_added < rlen or len(per) < rlen:
+            out[kname] = None
+            continue
+        if not ms or ms <= 0 or not k_ms or k_ms <= 0:  # a degenerate clock (noise larger than the launch)
             out[kname] = None
             continue
         byk = np.asarray(per[:len(per) // rlen * rlen]).reshape(-1, rlen).mean(axis=0) * 1e3
@@ -267,71 +278,117 @@ def cpu_baseline(mpg, A, b, xt, opts, args, world=1, workload="BAND-10M"):
             "affinity_cpus": info["affinity_cpus"]}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20, help="timed restart cycles")
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n-local", type=int, default=1_000_000, help="rows per GPU (weak scaling)")
-    ap.add_argument("--global-rows", type=int, default=0,
-                    help="strong scaling: one BAND matrix of this many rows split over the ranks")
-    ap.add_argument("--rlen", type=int, default=30)
-    ap.add_argument("--mode", default="mixed")
-    ap.add_argument("--orth", default="cgs")
-    ap.add_argument("--prec", default="identity")
-    ap.add_argument("--cpu-cycles", type=int, default=2, help="restart cycles per CPU-baseline solve")
-    ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU-baseline solves (after 1 warm-up)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--roofline-cycles", type=int, default=3)
-    ap.add_argument("--hbm-rows", type=int, default=10_000_000,
-                    help="rows of the BAND matrix of the HBM-scale SpMV figure (0: skip)")
-    ap.add_argument("--surface-cycles", type=int, default=20,
-                    help="N = 1: restart cycles of the same solve through the drop-in operator surface (0: skip)")
-    ap.add_argument("--spmv-format", default="auto", choices=["auto", "csr", "sell"],
-                    help="Arnoldi SpMV storage (auto: SELL-64 when its padding is small)")
-    args = ap.parse_args()
+def visible_gpus() -> int:
+    """GPUs a child process will see, counted in a child so that this
+    process never initialises the GPU (it starts the ranks; an exec or fork
+    after a HIP call is unsafe). torch.cuda.device_count() does not create
+    a HIP context on this image."""
+    out = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                         capture_output=True, text=True, timeout=600)
+    try:
+        return int(out.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        log(f"[bench] could not count GPUs: {out.stderr.strip()[-400:]}")
+        return 0
 
-    # the CPU facts before anything binds this thread (libgomp pins the
-    # initial thread to one place under OMP_PROC_BIND)
-    global _CPU_INFO
-    _CPU_INFO = cpu_info()
-    # the CPU baseline's OpenMP placement (automated.py:13-15); libgomp reads
-    # these when it is first loaded, which importing torch does
-    os.environ.setdefault("OMP_PROC_BIND", "spread")
-    os.environ.setdefault("OMP_PLACES", "threads")
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    mpg = load_pkg()
-    import torch
 
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-        # MPG_BENCH_SHARED_GPU=1 rehearses the multi-rank path with every rank on
-        # device 0 (gloo, engine collectives over the host transport); the
-        # default is one GPU per rank over RCCL
-        if os.environ.get("MPG_BENCH_SHARED_GPU") == "1":
-            local_rank = 0
-            torch.cuda.set_device(0)
-            dist.init_process_group("gloo")
-        else:
-            torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    # one BAND matrix; this rank owns one contiguous row block of it
-    strong = args.global_rows > 0
-    n = args.global_rows if strong else args.n_local * world
+def launch_ranks(args, argv) -> int:
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N
+    rank processes of this script, one per GPU, before anything here touches
+    the GPU (this process imports neither torch nor the HIP library). Each
+    child gets RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT, as torch.distributed.run would set
+    them. Rank 0's stdout (the JSON line) is relayed; the other ranks'
+    stdout goes to stderr. A failing rank ends the others and the exit code
+    is non-zero; fewer visible GPUs than N is an error, never a silent N=1."""
+    n = args.gpus
+    shared = os.environ.get("MPG_BENCH_SHARED_GPU") == "1"
+    if not args.dry_run:
+        have = visible_gpus()
+        need = 1 if shared else n
+        if have < need:
+            log(f"bench.py: --gpus {n} needs {need} visible GPU(s), found {have}"
+                + ("" if shared else " (MPG_BENCH_SHARED_GPU=1 rehearses N ranks on one GPU over gloo)"))
+            return 2
+    port = int(os.environ.get("MASTER_PORT", "0") or 0) or free_port()
+    procs = []
+    for q in range(n):
+        env = dict(os.environ, RANK=str(q), LOCAL_RANK=str(q), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MPG_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()), *argv], env=env,
+                                      stdout=subprocess.PIPE, text=True, start_new_session=True))
+    lines = [[] for _ in procs]
+
+    def pump(q, p):
+        for ln in p.stdout:
+            lines[q].append(ln)
+            if q != 0:
+                sys.stderr.write(f"[rank {q} stdout] {ln}")
+                sys.stderr.flush()
+
+    pumps = [threading.Thread(target=pump, args=(q, p), daemon=True) for q, p in enumerate(procs)]
+    for t in pumps:
+        t.start()
+    rc = 0
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(q, c) for q, c in enumerate(codes) if c not in (None, 0)]
+        if bad and failed is None:
+            failed = bad[0]
+            log(f"bench.py: rank {failed[0]} exited with {failed[1]}; ending the other ranks")
+            for p in procs:
+                if p.poll() is None:
+                    os.killpg(p.pid, signal.SIGTERM)
+            deadline = time.time() + 20
+            while time.time() < deadline and any(p.poll() is None for p in procs):
+                time.sleep(0.2)
+            for p in procs:
+                if p.poll() is None:
+                    os.killpg(p.pid, signal.SIGKILL)
+        if all(c is not None for c in (p.poll() for p in procs)):
+            break
+        time.sleep(0.2)
+    for t in pumps:
+        t.join(timeout=5)
+    if failed is not None:
+        rc = failed[1] if failed[1] > 0 else 1
+    for ln in lines[0]:
+        sys.stdout.write(ln)
+    sys.stdout.flush()
+    return rc
+
+
+def dry_run_line(args) -> None:
+    """--dry-run: what this rank would run, without touching a GPU."""
+    print(json.dumps({"dry_run": True, "rank": int(os.environ.get("RANK", "0")),
+                      "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                      "world": int(os.environ.get("WORLD_SIZE", "1")), "gpus": args.gpus,
+                      "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}",
+                      "shared_gpu": os.environ.get("MPG_BENCH_SHARED_GPU") == "1"}), flush=True)
+    if os.environ.get("MPG_BENCH_DRY_FAIL_RANK") == os.environ.get("RANK"):  # (tests: a rank that fails)
+        sys.exit(3)
+
+
+def measure(mpg, torch, dist, args, world, rank, local_rank, n, strong, keep=False) -> dict:
+    """One row-partitioned BAND solve of n global rows (strong: split evenly
+    over the ranks; weak: args.n_local rows per rank): build this rank's row
+    block and engine, run the warm-up cycles, then time exactly args.steps
+    restart cycles between a barrier + device synchronise on both sides; the
+    time is the max over ranks. keep=True returns the engine (open) and the
+    local problem for the roofline / surface / CPU legs."""
     starts = [n * q // world for q in range(world + 1)] if strong else [q * args.n_local for q in range(world + 1)]
     r0, r1 = starts[rank], starts[rank + 1]
     t0 = time.time()
     A = mpg.gen_band(n, 5, 4, seed=7, row_begin=r0, row_end=r1)
     xt = mpg.rand_vect(n, 42)
     b = mpg.host_spmv(A, xt)
-    global_nnz = 10 * n - 25
     log(f"[bench] rank {rank}: BAND rows {r0}..{r1} of {n}, local nnz={A.nnz}, built in {time.time() - t0:.1f}s")
 
     opts = dict(mode=args.mode, orth=args.orth, prec=args.prec, rlen=args.rlen, tol=0.0,
@@ -357,6 +414,7 @@ def main():
             uid = [mpg.rccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             eng = mpg.Engine.distributed(A, b, xt[r0:r1], plan, uid[0], world, rank, **opts)
+    comm_ranks = eng.comm_ranks()
     eng.run(args.warmup)
     eng.sync()
     torch.cuda.synchronize()
@@ -377,10 +435,116 @@ def main():
         elapsed = float(tt.item())
     iters = eng.total_iters - it0
     assert ran == args.steps and iters == args.steps * args.rlen, (ran, iters)
-    solve_rate = iters / elapsed
+    rate = iters / elapsed
+    log(f"[bench] n={n} ({'strong' if strong else 'weak'}): {args.steps} cycles, {iters} iterations in "
+        f"{elapsed:.4f}s -> {rate:.1f} it/s; communicator ranks {comm_ranks}")
+    out = {"r0": r0, "r1": r1, "rate": rate, "elapsed": elapsed, "comm_ranks": comm_ranks, "opts": opts}
+    if keep:
+        out.update(engine=eng, A=A, b=b, xt=xt)
+    else:
+        out["spmv_ms"] = spmv_roofline(eng, args.roofline_cycles)["avg_launch_ms"]
+        out["layout"] = eng.spmv_layout()
+        eng.close()
+    return out
+
+
+def claim_stdout():
+    """The bench prints exactly one JSON line on stdout: everything else --
+    including native libraries writing to fd 1 (gloo's connection notes,
+    RCCL, HIP) -- goes to stderr. Returns a writer for the real stdout."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(os.dup(2), "w", buffering=1)
+    return os.fdopen(real, "w", buffering=1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20, help="timed restart cycles")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n-local", type=int, default=1_000_000, help="rows per GPU (weak scaling)")
+    ap.add_argument("--global-rows", type=int, default=0,
+                    help="strong scaling: one BAND matrix of this many rows split over the ranks")
+    ap.add_argument("--rlen", type=int, default=30)
+    ap.add_argument("--mode", default="mixed")
+    ap.add_argument("--orth", default="cgs")
+    ap.add_argument("--prec", default="identity")
+    ap.add_argument("--cpu-cycles", type=int, default=2, help="restart cycles per CPU-baseline solve")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU-baseline solves (after 1 warm-up)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--roofline-cycles", type=int, default=3)
+    ap.add_argument("--hbm-rows", type=int, default=10_000_000,
+                    help="rows of the BAND matrix of the HBM-scale SpMV figure (0: skip)")
+    ap.add_argument("--surface-cycles", type=int, default=20,
+                    help="N = 1: restart cycles of the same solve through the drop-in operator surface (0: skip)")
+    ap.add_argument("--spmv-format", default="auto", choices=["auto", "csr", "sell"],
+                    help="Arnoldi SpMV storage (auto: SELL-64 when its padding is small)")
+    ap.add_argument("--strong-rows", type=int, default=10_000_000,
+                    help="N > 1: also time one BAND matrix of this many rows split over the ranks (the north "
+                         "star's 100M-nnz strong-scaling case; 0: skip)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="start the ranks and report what each would run; no GPU work")
+    args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if args.dry_run:
+        dry_run_line(args)
+        return
+    out = claim_stdout()
+
+    # the CPU facts before anything binds this thread (libgomp pins the
+    # initial thread to one place under OMP_PROC_BIND)
+    global _CPU_INFO
+    _CPU_INFO = cpu_info()
+    # the CPU baseline's OpenMP placement (automated.py:13-15); libgomp reads
+    # these when it is first loaded, which importing torch does
+    os.environ.setdefault("OMP_PROC_BIND", "spread")
+    os.environ.setdefault("OMP_PLACES", "threads")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: the launcher and the flag disagree")
+        sys.exit(2)
+    import torch  # first: the engine then shares PyTorch's HIP runtime (DESIGN §5)
+
+    mpg = load_pkg()
+    shared_gpu = os.environ.get("MPG_BENCH_SHARED_GPU") == "1"
+    if world > 1 and not shared_gpu:
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        have = torch.cuda.device_count()
+        if have < local_world or local_rank >= have:
+            log(f"bench.py: rank {rank} (local rank {local_rank}) needs {local_world} visible GPUs, found {have}")
+            sys.exit(2)
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        # MPG_BENCH_SHARED_GPU=1 rehearses the multi-rank path with every rank on
+        # device 0 (gloo, engine collectives over the host transport); the
+        # default is one GPU per rank over RCCL
+        if os.environ.get("MPG_BENCH_SHARED_GPU") == "1":
+            local_rank = 0
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    strong = args.global_rows > 0
+    n = args.global_rows if strong else args.n_local * world
+    m = measure(mpg, torch, dist, args, world, rank, local_rank, n, strong, keep=True)
+    eng, A, b, xt, opts = m["engine"], m["A"], m["b"], m["xt"], m["opts"]
+    r0, r1, solve_rate, elapsed = m["r0"], m["r1"], m["rate"], m["elapsed"]
+    global_nnz = 10 * n - 25
     value = solve_rate  # the one solve's iterations per second, at every N
     ms_per_step = 1e3 * elapsed / args.steps
-    log(f"[bench] {args.steps} cycles, {iters} iterations in {elapsed:.4f}s -> {solve_rate:.1f} it/s")
 
     # roofline of the dominant kernel: the Arnoldi SpMV as the cycle runs it
     sp = spmv_roofline(eng, args.roofline_cycles)
@@ -401,7 +565,21 @@ def main():
     if dist:
         per_rank_ms = [None] * world
         dist.all_gather_object(per_rank_ms, sp["avg_launch_ms"])
-    shared_gpu = os.environ.get("MPG_BENCH_SHARED_GPU") == "1"
+    # N > 1: the north star's 100M-nnz strong-scaling case beside the default
+    # weak one (one 1e7-row BAND matrix split over the ranks)
+    strong100 = None
+    if world > 1 and args.strong_rows > 0 and not (strong and n == args.strong_rows):
+        sm = measure(mpg, torch, dist, args, world, rank, local_rank, args.strong_rows, True)
+        sp_ms = [None] * world
+        dist.all_gather_object(sp_ms, sm["spmv_ms"])
+        strong100 = {"value": round(sm["rate"], 2), "unit": "GMRES iterations/s", "scaling": "strong",
+                     "ms_per_step": round(1e3 * sm["elapsed"] / args.steps, 4), "steps": args.steps,
+                     "rccl_ranks": sm["comm_ranks"] if not shared_gpu else None, "comm_ranks": sm["comm_ranks"],
+                     "workload": f"BAND banded CSR n={args.strong_rows}, offsets -5..+4, "
+                                 f"nnz={10 * args.strong_rows - 25}, split over {world} GPUs; GMRES({args.rlen}) "
+                                 f"{args.mode}, {args.orth}, {args.prec}, tol=0",
+                     "rows_per_gpu": sm["r1"] - sm["r0"],
+                     "spmv_per_rank_avg_launch_ms": [round(t, 5) for t in sp_ms], "spmv_layout_rank0": sm["layout"]}
     surface = None
     if rank == 0 and world == 1 and args.surface_cycles > 0:
         surface = surface_rate(mpg, A, b, xt, opts, args.surface_cycles, solve_rate)
@@ -509,9 +687,24 @@ def main():
                 log(f"[bench] CPU baseline on the global matrix took {time.time() - t2:.1f}s")
                 del Ag, bg
             cpu["vs_gpu"] = round(value / cpu["value"], 2) if cpu["value"] else None
+            if strong100 is not None:
+                t3 = time.time()
+                As = mpg.gen_band(args.strong_rows, 5, 4, seed=7)
+                xs = mpg.rand_vect(args.strong_rows, 42)
+                bs = mpg.host_spmv(As, xs)
+                cargs = argparse.Namespace(**dict(vars(args), cpu_runs=min(args.cpu_runs, 3)))
+                sc = cpu_baseline(mpg, As, bs, xs, opts, cargs, world,
+                                  f"BAND n={args.strong_rows} ({10 * args.strong_rows - 25} nnz)")
+                sc["vs_gpu"] = round(strong100["value"] / sc["value"], 2) if sc["value"] else None
+                strong100["cpu_baseline"] = sc
+                log(f"[bench] strong case: {strong100['value']:.0f} it/s on {world} GPUs vs {sc['value']} it/s "
+                    f"on {sc['cores']} host cores ({sc['vs_gpu']}x); CPU leg took {time.time() - t3:.1f}s")
+                del As, bs, xs
 
     if rank == 0:
         scaling = "strong" if strong else "weak"
+        if strong100 is not None and "cpu_baseline" not in strong100:
+            strong100["cpu_baseline"] = None
         transport = ("RCCL" if not shared_gpu else
                      "the gloo host transport, every rank on GPU 0 (rehearsal; RCCL refuses two ranks on one GPU)")
         line = {
@@ -520,6 +713,8 @@ def main():
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic", "roofline": roofline, "cpu_baseline": cpu,
             "solve_iters_per_s": round(solve_rate, 2), "surface": surface,
+            "rccl_ranks": m["comm_ranks"] if world > 1 and not shared_gpu else None,
+            "comm_ranks": m["comm_ranks"], "strong_100m": strong100,
             "surface_iters_per_s": surface["iters_per_s"] if surface else None,
             "aggregate": (None if strong or world == 1 else
                           {"value": round(solve_rate * world, 2),
@@ -534,7 +729,8 @@ def main():
                        "parallelism": (f"row-partition x{world} (halo send/recv + fp64 all-reduce over {transport})"
                                        if world > 1 else "one GPU")},
         }
-        print(json.dumps(line), flush=True)
+        out.write(json.dumps(line) + "\n")
+        out.flush()
     if dist:
         dist.barrier()  # the other ranks wait for rank 0's measurements
         dist.destroy_process_group()

@@ -47,6 +47,8 @@ def _lib(name: str) -> C.CDLL:
     path = HIP_LIB if name == "hip" else HOST_LIB
     if name == "hip" and os.environ.get("MPG_HIP_LIB"):  # A/B of two kernel builds (tools/ab_bench.sh)
         path = Path(os.environ["MPG_HIP_LIB"])
+    if name == "host" and os.environ.get("MPG_HOST_LIB"):  # the ASan/UBSan build (make sanitize)
+        path = Path(os.environ["MPG_HOST_LIB"])
     if not path.exists():
         raise RuntimeError(f"{path} is missing: run build() (make -C {PKG_DIR}) — there is no CPU fallback")
     if name == "host":
@@ -134,6 +136,8 @@ def _declare_host(lib: C.CDLL) -> None:
                                            C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
     lib.mpg_solve_loopback.argtypes = [C.POINTER(SolveArgs), _I32, C.POINTER(SolveResult)]
     lib.mpg_solve_loopback_ex.argtypes = [C.POINTER(SolveArgs), _I32, C.POINTER(SolveResult), C.c_void_p]
+    lib.mpg_solve_multi_gpu.argtypes = [C.POINTER(SolveArgs), _I32, C.c_void_p, C.POINTER(SolveResult), C.c_void_p]
+    lib.mpg_engine_comm_ranks.argtypes = [C.c_void_p]
     lib.mpg_engine_sell_columns.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
                                             C.POINTER(C.c_int64)]
     lib.mpg_engine_half_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
@@ -579,6 +583,15 @@ def bw_probe(kind: str = "read", nbytes: int = 2 << 30, reps: int = 3, device: i
         lib.mpg_ctx_destroy(ctx)
 
 
+def device_count() -> int:
+    """HIP devices visible to this process (mpg_device_count), through the
+    package's own HIP runtime (importing torch after the package would load
+    a second one)."""
+    lib = hip_lib()
+    lib.mpg_device_count.argtypes = []
+    return int(lib.mpg_device_count())
+
+
 def rccl_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     if host_lib().mpg_rccl_unique_id(buf, 128):
@@ -595,13 +608,40 @@ def solve_loopback(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, n
     lib = host_lib()
     lay = (RankLayout * nranks)()
     res = run_solve(lambda a, r: lib.mpg_solve_loopback_ex(a, nranks, r, C.cast(lay, C.c_void_p)), args, A.nrows)
-    if layouts is not None:
-        forms = {-1: "none", 0: "int32", 1: "int16", 2: "stepped"}
-        for L in lay:
-            d = {f: getattr(L, f) for f, _ in RankLayout._fields_}
-            d["format"] = {1: "csr", 2: "sell"}.get(d["format"], d["format"])
-            d["col_form"] = forms[d["col_form"]]
-            layouts.append(d)
+    _layout_dicts(lay, layouts)
+    return res
+
+
+def _layout_dicts(lay, layouts: Optional[list]):
+    if layouts is None:
+        return
+    forms = {-1: "none", 0: "int32", 1: "int16", 2: "stepped"}
+    for L in lay:
+        d = {f: getattr(L, f) for f, _ in RankLayout._fields_}
+        d["format"] = {1: "csr", 2: "sell"}.get(d["format"], d["format"])
+        d["col_form"] = forms[d["col_form"]]
+        layouts.append(d)
+
+
+def solve_multi_gpu(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, ngpus: int = 1,
+                    devices: Optional[list] = None, layouts: Optional[list] = None, **opts) -> Result:
+    """The row-partitioned engine in this process with `ngpus` ranks, rank q
+    a host thread on devices[q] (default 0..ngpus-1), collectives over one
+    RCCL clique (ncclCommInitAll; mpg_solve_multi_gpu, dist.h). Raises when
+    fewer GPUs are visible than requested or a device is named twice."""
+    opts.pop("engine", None)
+    opts.pop("device", None)
+    args, keep = make_args(A, b, x_true, engine="fused", **opts)
+    lib = host_lib()
+    lay = (RankLayout * ngpus)()
+    devs = None
+    if devices is not None:
+        if len(devices) != ngpus:
+            raise ValueError(f"{len(devices)} devices for {ngpus} ranks")
+        devs = (C.c_int32 * ngpus)(*devices)
+    res = run_solve(lambda a, r: lib.mpg_solve_multi_gpu(a, ngpus, C.cast(devs, C.c_void_p) if devs else None, r,
+                                                         C.cast(lay, C.c_void_p)), args, A.nrows)
+    _layout_dicts(lay, layouts)
     return res
 
 
@@ -756,6 +796,11 @@ class Engine:
                 "implicit_slices": i.value,
                 "shared_slices": int(self._lib.mpg_engine_sell_shared_slices(self._h)),
                 "sigma": int(self._lib.mpg_engine_sell_sigma(self._h))}
+
+    def comm_ranks(self) -> int:
+        """Ranks of the engine's communicator as its transport reports them
+        (1 on one GPU; RCCL: ncclCommCount; mpg_engine_comm_ranks)."""
+        return int(self._lib.mpg_engine_comm_ranks(self._h))
 
     def half_stats(self) -> dict:
         """mixed-half: what the fp16 cast did (mpg_engine_half_stats)."""

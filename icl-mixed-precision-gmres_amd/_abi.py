@@ -107,9 +107,6 @@ class CondestResult(C.Structure):
         ("stop_reason", C.c_int32),
         ("seconds", C.c_double),
         ("message", C.c_char * 256),
-        ("nonfinite_steps", C.c_int64),
-        ("nonfinite_cycles", C.c_int64),
-        ("first_nonfinite_step", C.c_int64),
     ]
 
 
@@ -146,4 +143,6 @@ class RankLayout(C.Structure):
         ("csr_slices", C.c_int64),
         ("implicit_slices", C.c_int64),
         ("half_rows_scaled", C.c_int64),
+        ("device", C.c_int32),
+        ("transport_ranks", C.c_int32),
     ]

@@ -396,9 +396,15 @@ struct GivensFold {
 // branch cost up to 20 VGPRs (C4's stepped kernel 71 -> 91, -11 % in time),
 // and a branch-free form with a sink word slowed the BAND SpMV; the SpMV is
 // timed by duplicate launches instead (time_phase_dup, host/fused_gmres.cpp).
+// Round 5: a compile-time choice. The product instantiations
+// (STAMP = false) hold no stamp code at all; the launch sites pick the STAMP
+// = true instantiation only for a launch that mpg_arnoldi_stamp_next armed.
+template <bool STAMP>
 __device__ __forceinline__ void stamp_at(unsigned long long* stamp, int end) {
-    if (stamp && (threadIdx.x & (kWave - 1)) == 0)
-        stamp[2 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave) + end] = wall_clock64();
+    if constexpr (STAMP) {
+        if ((threadIdx.x & (kWave - 1)) == 0)
+            stamp[2 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave) + end] = wall_clock64();
+    }
 }
 
 template <bool FOLD, class T>
@@ -995,13 +1001,13 @@ __device__ __forceinline__ void dots_panel(int n, const T* __restrict__ V, int64
     store_partials<NP, BS>(acc, NC, partial);
 }
 
-template <class T, int BS, int NC>
+template <class T, int BS, int NC, bool STAMP = false>
 __global__ __launch_bounds__(BS) void k_dots_nc(int n, const T* __restrict__ V, int64_t ld,
                                                 const T* __restrict__ w, double* __restrict__ partial,
                                                 unsigned long long* stamp) {
-    stamp_at(stamp, 0);
+    stamp_at<STAMP>(stamp, 0);
     dots_panel<T, BS, NC>(n, V, ld, w, partial);
-    stamp_at(stamp, 1);
+    stamp_at<STAMP>(stamp, 1);
 }
 
 // V^T w for nc > kNC columns in ONE launch (GMRES(100): the round-3 form ran
@@ -1034,13 +1040,14 @@ __global__ __launch_bounds__(BS) void k_dots_panels(int n, const T* __restrict__
 // behind the partial loads, so its memory latency runs under the coefficient
 // sums; the coefficients are published with an LDS-only barrier
 // (__syncthreads would drain those loads). Same operands, same order.
-template <class T, int BS, int NC, bool FROM_PARTS = false, bool NEXT_DOTS = false, bool PF = false>
+template <class T, int BS, int NC, bool FROM_PARTS = false, bool NEXT_DOTS = false, bool PF = false,
+          bool STAMP = false>
 __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict__ V, int64_t ld,
                                                       const double* __restrict__ sums, int part_G,
                                                       T* __restrict__ coef_out, T* __restrict__ w,
                                                       double* __restrict__ partial, unsigned long long* stamp) {
     static_assert(NC >= 1 && NC <= kNC, "one panel");
-    stamp_at(stamp, 0);
+    stamp_at<STAMP>(stamp, 0);
     static_assert(!FROM_PARTS || BS >= 32 * NC, "32 lanes per column");
     static_assert(!PF || (FROM_PARTS && !NEXT_DOTS), "prefetch under the partial sums");
     constexpr int B = kColBatch<T>;
@@ -1152,7 +1159,7 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
         }
     }
     store_partials<NA, BS>(acc, NEXT_DOTS ? NC : 1, partial);
-    stamp_at(stamp, 1);
+    stamp_at<STAMP>(stamp, 1);
 }
 
 // The CGS update for kNC < nc <= kWideMax columns (GMRES(100)): the
@@ -2177,6 +2184,9 @@ static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
     if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
     const int ndots_all = a->d.orth == kOrthMGS ? 1 : k + 1;
     if (combine && ndots_all > kNC) return MPG_ERR_ARG;
+    // an armed stamp belongs to this launch whatever its form (disarmed
+    // here); only the one-panel k_dots_nc stores stamps
+    unsigned long long* sp = take_stamp(a, (int64_t)a->Gd * (kCombineBlock / kWave));
     int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
         using T = decltype(t);
         if (combine) {
@@ -2187,9 +2197,15 @@ static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
         }
         if (ndots_all <= kNC) {  // one panel: 1024-thread workgroups, one per CU -> Gd partials per column
             return with_nc<kNC>(ndots_all, [&](auto nc) {
-                k_dots_nc<T, kCombineBlock, decltype(nc)::value><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                    a->d.n, static_cast<const T*>(a->V), a->ld, static_cast<const T*>(a->w[(k + 1) & 1]), a->dpart,
-                    take_stamp(a, (int64_t)a->Gd * (kCombineBlock / kWave)));
+                constexpr int NC = decltype(nc)::value;
+                const T* Vp = static_cast<const T*>(a->V);
+                const T* wp = static_cast<const T*>(a->w[(k + 1) & 1]);
+                if (sp)
+                    k_dots_nc<T, kCombineBlock, NC, true>
+                        <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, Vp, a->ld, wp, a->dpart, sp);
+                else
+                    k_dots_nc<T, kCombineBlock, NC>
+                        <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, Vp, a->ld, wp, a->dpart, nullptr);
                 return (int)MPG_OK;
             });
         }
@@ -2245,6 +2261,9 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
     const double* src = from_partials ? a->dpart : a->sums;
     const int part_G = from_partials ? a->last_G : 0;  // Gd (k_dots_nc) or fd_ng (k_step_sell's dots)
     if (part_G > kCombineGroups) return MPG_ERR_ARG;
+    // an armed stamp belongs to this launch whatever its form (disarmed here);
+    // only the one-panel product form below stores stamps
+    unsigned long long* sp = take_stamp(a, (int64_t)a->Gd * (kCombineBlock / kWave));
     int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
         using T = decltype(t);
         T* coef_out = pass == 0 ? static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) : static_cast<T*>(a->corr());
@@ -2255,8 +2274,7 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
             // than the 128 VGPRs of a 1024-thread one) -> row_grid partials
             return with_nc<kNC>(k + 1, [&](auto nc) {
                 k_cgs_update_nc<T, kBlock, decltype(nc)::value, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                    a->d.n, static_cast<const T*>(a->V), a->ld, src, 0, coef_out, w, a->partial,
-                    take_stamp(a, (int64_t)row_grid(a) * (kBlock / kWave)));
+                    a->d.n, static_cast<const T*>(a->V), a->ld, src, 0, coef_out, w, a->partial, nullptr);
                 return (int)MPG_OK;
             });
         } else if (next_dots) {
@@ -2278,28 +2296,32 @@ static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_par
             k_cgs_update_wide<T, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
                 a->d.n, static_cast<const T*>(a->V), a->ld, k + 1, src, part_G, coef_out, w, a->partial);
         } else if (k + 1 <= kNC) {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
-            const int64_t nc_waves = (int64_t)a->Gd * (kCombineBlock / kWave);
+            // the wave stamps of the product form only (in-launch sums, no
+            // prefetch): the one bench.py's phases time
+            if (!from_partials || cgs_prefetch()) sp = nullptr;
             return with_nc<kNC>(k + 1, [&](auto nc) {
                 constexpr int NC = decltype(nc)::value;
+                const T* Vp = static_cast<const T*>(a->V);
                 // (the prefetch variant for one batch of columns only: wider
                 // panels spill with the prefetched batch held across the sums)
                 if constexpr (NC <= kColBatch<T>) {
                     if (from_partials && cgs_prefetch()) {
                         k_cgs_update_nc<T, kCombineBlock, NC, true, false, true>
-                            <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, static_cast<const T*>(a->V), a->ld,
-                                                                           src, part_G, coef_out, w, a->partial,
-                                                                           take_stamp(a, nc_waves));
+                            <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, Vp, a->ld, src, part_G, coef_out,
+                                                                           w, a->partial, nullptr);
                         return (int)MPG_OK;
                     }
                 }
-                if (from_partials)
+                if (from_partials && sp)
+                    k_cgs_update_nc<T, kCombineBlock, NC, true, false, false, true>
+                        <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, Vp, a->ld, src, part_G, coef_out, w,
+                                                                       a->partial, sp);
+                else if (from_partials)
                     k_cgs_update_nc<T, kCombineBlock, NC, true><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                        a->d.n, static_cast<const T*>(a->V), a->ld, src, part_G, coef_out, w, a->partial,
-                        take_stamp(a, nc_waves));
+                        a->d.n, Vp, a->ld, src, part_G, coef_out, w, a->partial, nullptr);
                 else
                     k_cgs_update_nc<T, kCombineBlock, NC, false><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                        a->d.n, static_cast<const T*>(a->V), a->ld, src, 0, coef_out, w, a->partial,
-                        take_stamp(a, nc_waves));
+                        a->d.n, Vp, a->ld, src, 0, coef_out, w, a->partial, nullptr);
                 return (int)MPG_OK;
             });
         } else {

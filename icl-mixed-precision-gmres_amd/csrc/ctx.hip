@@ -26,6 +26,11 @@ const char* mpg_ctx_last_error(mpg_ctx_t ctx) {
     return ctx ? ctx->last_error.c_str() : "null context";
 }
 
+int mpg_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 int mpg_ctx_create(int device, mpg_ctx_t* out) {
     if (!out) return MPG_ERR_ARG;
     *out = nullptr;

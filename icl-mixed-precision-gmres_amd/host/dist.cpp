@@ -8,7 +8,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -52,6 +54,7 @@ void hck(hipError_t e, const char* what) {
 
 // ---------------------------------------------------------------- RCCL
 class RcclComm : public Comm {
+    std::mutex mu_;  // guards comm_ against an abort from another thread
     ncclComm_t comm_ = nullptr;
     int rank_, size_;
     mpg_ctx_t ctx_;
@@ -61,11 +64,28 @@ class RcclComm : public Comm {
     std::vector<int32_t> send_first_;  // >= 0: the rows sent to q are [first, first + cnt) (sent in place, no pack)
 
 public:
+    // one rank per process: the communicator from a broadcast unique id
     RcclComm(mpg_ctx_t ctx, const mpg_halo& h, const char* id, int nranks, int rank)
         : rank_(rank), size_(nranks), ctx_(ctx), recv_pos_(h.recv_pos), recv_cnt_(h.recv_cnt) {
         ncclUniqueId uid;
         std::memcpy(&uid, id, sizeof uid);
         nck(ncclCommInitRank(&comm_, nranks, uid, rank), "ncclCommInitRank");
+        plan(h, nranks);
+    }
+    // one rank per host thread of one process: a communicator of an
+    // ncclCommInitAll clique, owned from here on
+    RcclComm(mpg_ctx_t ctx, const mpg_halo& h, ncclComm_t comm, int nranks, int rank)
+        : comm_(comm), rank_(rank), size_(nranks), ctx_(ctx), recv_pos_(h.recv_pos), recv_cnt_(h.recv_cnt) {
+        try {
+            plan(h, nranks);
+        } catch (...) {
+            ncclCommDestroy(comm_);
+            throw;
+        }
+    }
+
+private:
+    void plan(const mpg_halo& h, int nranks) {
         send_cnt_.assign(nranks, 0);
         send_first_.assign(nranks, -1);
         send_idx_.resize(nranks);
@@ -80,11 +100,13 @@ public:
                 send_first_[q] = rows[0];
                 continue;
             }
-            send_idx_[q] = std::make_unique<DevMem>(ctx, rows.size() * 4);
-            check(mpg_memcpy_h2d(ctx, send_idx_[q]->p, rows.data(), rows.size() * 4), "h2d", ctx);
-            send_buf_[q] = std::make_unique<DevMem>(ctx, rows.size() * 8);
+            send_idx_[q] = std::make_unique<DevMem>(ctx_, rows.size() * 4);
+            check(mpg_memcpy_h2d(ctx_, send_idx_[q]->p, rows.data(), rows.size() * 4), "h2d", ctx_);
+            send_buf_[q] = std::make_unique<DevMem>(ctx_, rows.size() * 8);
         }
     }
+
+public:
     ~RcclComm() override {
         if (comm_) ncclCommDestroy(comm_);
     }
@@ -93,14 +115,23 @@ public:
     bool capturable() const override { return true; }
     bool async() const override { return true; }
     std::string async_error() override {
+        std::lock_guard<std::mutex> lk(mu_);
         if (!comm_) return "communicator aborted";
         ncclResult_t r = ncclSuccess;
         if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
         return r == ncclSuccess || r == ncclInProgress ? std::string() : std::string(ncclGetErrorString(r));
     }
+    // idempotent, and callable from another rank's thread (mpg_solve_multi_gpu)
     void abort() override {
+        std::lock_guard<std::mutex> lk(mu_);
         if (comm_) ncclCommAbort(comm_);
         comm_ = nullptr;
+    }
+    int transport_ranks() override {
+        std::lock_guard<std::mutex> lk(mu_);
+        int n = -1;
+        if (!comm_ || ncclCommCount(comm_, &n) != ncclSuccess) return -1;
+        return n;
     }
     void allreduce_sum(double* dev, int count, hipStream_t s) override {
         nck(ncclAllReduce(dev, dev, (size_t)count, ncclFloat64, ncclSum, comm_, s), "allreduce");
@@ -488,23 +519,47 @@ int mpg_solve_loopback(const mpg_solve_args* a, int32_t P, mpg_solve_result* r) 
     return mpg_solve_loopback_ex(a, P, r, nullptr);
 }
 
-int mpg_solve_loopback_ex(const mpg_solve_args* a, int32_t P, mpg_solve_result* r, mpg_rank_layout* layouts) {
-    if (!a || !r || P < 1 || a->n < P) return MPG_ERR_ARG;
-    r->status = MPG_RESULT_ERROR;
-    r->message[0] = 0;
+}  // extern "C"
+
+namespace mpg {
+namespace {
+
+using CommFactory = std::function<std::unique_ptr<Comm>(int q, mpg_ctx_t ctx, const mpg_halo& plan)>;
+
+// calls `done` when it leaves scope (before the communicator it follows is destroyed)
+struct OnExit {
+    std::function<void()> done;
+    ~OnExit() {
+        if (done) done();
+    }
+};
+
+// P ranks as host threads of this process, rank q on devices[q], rows split
+// evenly by nnz; `make_comm` gives each rank its communicator (loopback hub
+// or an RCCL clique). The result gathers x from every rank and the history
+// from rank 0, as mpg_solve reports them.
+int solve_rank_threads(const mpg_solve_args* a, int32_t P, mpg_solve_result* r, mpg_rank_layout* layouts,
+                       const std::vector<int>& devices, const CommFactory& make_comm,
+                       const std::function<void()>& on_error,
+                       const std::function<void(int)>& on_comm_gone = nullptr) {
     const int n = a->n;
     const auto starts = nnz_balanced_starts(n, a->rowptr, P);
     // per-rank row slices and halo plans
     std::vector<std::vector<int32_t>> rp(P), cg(P);
     std::vector<mpg_halo_t> plans(P, nullptr);
+    auto free_plans = [&] {
+        for (auto p : plans) mpg_halo_free(p);
+    };
     for (int q = 0; q < P; ++q) {
         const int64_t r0 = starts[q], r1 = starts[q + 1];
         const int32_t base = a->rowptr[r0];
         rp[q].resize((size_t)(r1 - r0) + 1);
         for (int64_t i = r0; i <= r1; ++i) rp[q][(size_t)(i - r0)] = a->rowptr[i] - base;
         cg[q].assign(a->col + base, a->col + a->rowptr[r1]);
-        if (mpg_halo_analyze(q, P, starts.data(), (int32_t)(r1 - r0), rp[q].data(), cg[q].data(), &plans[q]))
+        if (mpg_halo_analyze(q, P, starts.data(), (int32_t)(r1 - r0), rp[q].data(), cg[q].data(), &plans[q])) {
+            free_plans();
             return MPG_ERR_ARG;
+        }
     }
     for (int q = 0; q < P; ++q)
         for (int p = 0; p < P; ++p) {
@@ -514,17 +569,18 @@ int mpg_solve_loopback_ex(const mpg_solve_args* a, int32_t P, mpg_solve_result* 
             mpg_halo_recv_rows(plans[p], q, rows.data());
             mpg_halo_set_send(plans[q], p, c, rows.data());
         }
-    Hub hub(P);
     std::vector<std::string> errors(P);
+    std::vector<double> seconds((size_t)P, 0.0);
     std::vector<std::thread> th;
     for (int q = 0; q < P; ++q) {
         th.emplace_back([&, q] {
             mpg_ctx_t ctx = nullptr;
             try {
-                check(mpg_ctx_create(a->device, &ctx), "mpg_ctx_create");
+                check(mpg_ctx_create(devices[(size_t)q], &ctx), "mpg_ctx_create");
                 ScopedContext scope(ctx);
                 {
-                    LoopbackComm comm(hub, ctx, *plans[q]);
+                    std::unique_ptr<Comm> comm = make_comm(q, ctx, *plans[q]);
+                    OnExit gone{on_comm_gone ? std::function<void()>([&, q] { on_comm_gone(q); }) : nullptr};
                     const int64_t r0 = starts[q], r1 = starts[q + 1];
                     const int32_t base = a->rowptr[r0];
                     mpg_solve_args la = *a;
@@ -535,8 +591,9 @@ int mpg_solve_loopback_ex(const mpg_solve_args* a, int32_t P, mpg_solve_result* 
                     la.val = a->val + base;
                     la.b = a->b + r0;
                     la.x_true = a->x_true ? a->x_true + r0 : nullptr;
+                    la.device = devices[(size_t)q];
                     if (q != 0) la.verbose = 0;
-                    FusedEngine e(ctx, la, &comm, mpg_halo_n_ext(plans[q]), plans[q]->n_front);
+                    FusedEngine e(ctx, la, comm.get(), mpg_halo_n_ext(plans[q]), plans[q]->n_front);
                     if (layouts) {
                         mpg_rank_layout& L = layouts[q];
                         L = mpg_rank_layout{};
@@ -551,10 +608,14 @@ int mpg_solve_loopback_ex(const mpg_solve_args* a, int32_t P, mpg_solve_result* 
                         L.row0 = r0;
                         L.half_rows_scaled = e.half_stats()[0];
                         L.givens_folded = e.givens_folded() ? 1 : 0;
+                        L.device = devices[(size_t)q];
+                        L.transport_ranks = comm->transport_ranks();
                     }
+                    const auto t1 = std::chrono::steady_clock::now();
                     bool done = false;
                     while (!done) e.run(1 << 20, done);
                     e.sync();
+                    seconds[(size_t)q] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
                     mpg_solve_result mine{};
                     mine.x_out = r->x_out ? r->x_out + r0 : nullptr;
                     e.finish_report(&mine);
@@ -566,13 +627,14 @@ int mpg_solve_loopback_ex(const mpg_solve_args* a, int32_t P, mpg_solve_result* 
                 }
             } catch (const std::exception& ex) {
                 errors[q] = ex.what();
-                hub.abort();
+                on_error();
             }
             if (ctx) mpg_ctx_destroy(ctx);
         });
     }
     for (auto& t : th) t.join();
-    for (auto p : plans) mpg_halo_free(p);
+    free_plans();
+    r->gmres_seconds = *std::max_element(seconds.begin(), seconds.end());  // the slowest rank's solve
     for (int q = 0; q < P; ++q)
         if (!errors[q].empty()) {
             r->status = MPG_RESULT_ERROR;
@@ -580,6 +642,84 @@ int mpg_solve_loopback_ex(const mpg_solve_args* a, int32_t P, mpg_solve_result* 
             return MPG_ERR_ARG;
         }
     return MPG_OK;
+}
+
+}  // namespace
+}  // namespace mpg
+
+extern "C" {
+
+int mpg_solve_loopback_ex(const mpg_solve_args* a, int32_t P, mpg_solve_result* r, mpg_rank_layout* layouts) {
+    if (!a || !r || P < 1 || a->n < P) return MPG_ERR_ARG;
+    r->status = MPG_RESULT_ERROR;
+    r->message[0] = 0;
+    Hub hub(P);
+    const std::vector<int> devices((size_t)P, a->device);
+    return solve_rank_threads(
+        a, P, r, layouts, devices,
+        [&](int, mpg_ctx_t ctx, const mpg_halo& h) -> std::unique_ptr<Comm> {
+            return std::make_unique<LoopbackComm>(hub, ctx, h);
+        },
+        [&] { hub.abort(); });
+}
+
+int mpg_solve_multi_gpu(const mpg_solve_args* a, int32_t ngpus, const int32_t* devices_in, mpg_solve_result* r,
+                        mpg_rank_layout* layouts) {
+    if (!a || !r || ngpus < 1 || a->n < ngpus) return MPG_ERR_ARG;
+    r->status = MPG_RESULT_ERROR;
+    r->message[0] = 0;
+    int visible = 0;
+    if (hipGetDeviceCount(&visible) != hipSuccess) visible = 0;
+    std::vector<int> devices((size_t)ngpus);
+    for (int q = 0; q < ngpus; ++q) devices[(size_t)q] = devices_in ? devices_in[q] : q;
+    for (int q = 0; q < ngpus; ++q) {
+        const int d = devices[(size_t)q];
+        if (d < 0 || d >= visible) {
+            std::snprintf(r->message, sizeof r->message,
+                          "%d GPU(s) requested but %d visible: rank %d would run on device %d", ngpus, visible, q, d);
+            return MPG_ERR_ARG;
+        }
+        for (int p = 0; p < q; ++p)
+            if (devices[(size_t)p] == d) {
+                std::snprintf(r->message, sizeof r->message,
+                              "device %d named twice (ranks %d and %d): RCCL runs one rank per GPU", d, p, q);
+                return MPG_ERR_ARG;
+            }
+    }
+    std::vector<ncclComm_t> comms((size_t)ngpus, nullptr);
+    const ncclResult_t nr = ncclCommInitAll(comms.data(), ngpus, devices.data());
+    if (nr != ncclSuccess) {
+        std::snprintf(r->message, sizeof r->message, "ncclCommInitAll over %d GPU(s): %s", ngpus,
+                      ncclGetErrorString(nr));
+        return MPG_ERR_RCCL;
+    }
+    std::vector<std::atomic<bool>> taken((size_t)ngpus);
+    for (auto& t : taken) t = false;
+    std::mutex mu;
+    std::vector<RcclComm*> live((size_t)ngpus, nullptr);
+    const int st = solve_rank_threads(
+        a, ngpus, r, layouts, devices,
+        [&](int q, mpg_ctx_t ctx, const mpg_halo& h) -> std::unique_ptr<Comm> {
+            taken[(size_t)q] = true;  // the RcclComm owns (or on failure destroyed) comms[q]
+            auto c = std::make_unique<RcclComm>(ctx, h, comms[(size_t)q], ngpus, q);
+            std::lock_guard<std::mutex> lk(mu);
+            live[(size_t)q] = c.get();
+            return c;
+        },
+        [&] {
+            // a failed rank: abort every communicator so that peers waiting
+            // on a collective return (their bounded waits then fail too)
+            std::lock_guard<std::mutex> lk(mu);
+            for (auto* c : live)
+                if (c) c->abort();
+        },
+        [&](int q) {
+            std::lock_guard<std::mutex> lk(mu);
+            live[(size_t)q] = nullptr;
+        });
+    for (int q = 0; q < ngpus; ++q)
+        if (!taken[(size_t)q] && comms[(size_t)q]) ncclCommDestroy(comms[(size_t)q]);
+    return st == MPG_OK ? MPG_OK : (std::strstr(r->message, "RCCL") ? MPG_ERR_RCCL : st);
 }
 
 }  // extern "C"

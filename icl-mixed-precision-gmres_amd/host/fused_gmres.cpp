@@ -698,12 +698,19 @@ void FusedEngine::wait_event(hipEvent_t ev, int64_t cycle, const char* what) {
                         break;
                     }
             }
-            if (!done_late) I.comm->abort();
-            throw StatusError(MPG_ERR_RCCL, "rank " + std::to_string(I.comm->rank()) + " of " +
-                                                std::to_string(I.comm->size()) + ": restart cycle " +
-                                                std::to_string(cycle) + ", waiting for " + what + ": " + why +
-                                                (done_late ? "; it completed within the 5 s grace period (not aborted)"
-                                                           : "; communicator aborted"));
+            const std::string where = "rank " + std::to_string(I.comm->rank()) + " of " +
+                                      std::to_string(I.comm->size()) + ": restart cycle " + std::to_string(cycle) +
+                                      ", waiting for " + what + ": " + why;
+            if (done_late) {
+                // slow but healthy (e.g. a huge or time-shared solve): say so
+                // and go on; only an async error or a real hang ends the solve
+                // 
+                std::fprintf(stderr, "mpgmres: warning: %s; it completed within the 5 s grace period, continuing\n",
+                             where.c_str());
+                return;
+            }
+            I.comm->abort();
+            throw StatusError(MPG_ERR_RCCL, where + "; communicator aborted");
         }
         // spin for the first ~ms (a cycle is ~1 ms), then back off
         if (polls > 2000) std::this_thread::sleep_for(std::chrono::microseconds(100));
@@ -837,6 +844,10 @@ int FusedEngine::run_pipelined(int max_cycles, bool& done) {
 // --stop-on-breakdown: the first non-finite value ends the solve with
 // MPG_ERR_BREAKDOWN (nothing left in flight: a pipelined cycle may be)
 int FusedEngine::run(int max_cycles, bool& done) {
+    if (measured)
+        throw StatusError(MPG_ERR_UNSUPPORTED,
+                          "the engine ran measurement launches (mpg_engine_time_*), which change its Krylov basis, "
+                          "Hessenberg column and iterate; create a new engine to continue a solve");
     try {
         return run_cycles(max_cycles, done);
     } catch (const BreakdownError& e) {
@@ -978,6 +989,7 @@ bool FusedEngine::givens_folded() const { return p_->fold; }
 constexpr int kTimedReplays = 10;
 
 double FusedEngine::time_phase(int which, int reps, bool inplace, std::vector<double>* per_launch) {
+    measured = true;
     Impl& I = *p_;
     if (inplace && which != 0) throw std::invalid_argument("in-place timing covers the Arnoldi SpMV only");
     I.timed = which;
@@ -1086,6 +1098,7 @@ void FusedEngine::timed_end(int phase) {
 // re-records the events; they are read after it). Measurement only, like
 // time_phase: the replays run without the host's restart checks.
 double FusedEngine::time_phase_graph(int which, int reps, std::vector<double>* per_launch) {
+    measured = true;
     Impl& I = *p_;
     if (!I.use_graph) throw StatusError(MPG_ERR_UNSUPPORTED, "the cycle is not captured (MPG_NO_GRAPH / eager ranks)");
     if (which != 0 && which != 2 && which != 3) throw std::invalid_argument("phase: 0 spmv, 2 cgs update, 3 dots");
@@ -1145,6 +1158,7 @@ double FusedEngine::time_phase_graph(int which, int reps, std::vector<double>* p
 // columns) store nothing and are skipped. Measurement only, like
 // time_phase_graph.
 double FusedEngine::time_phase_stamps(int which, int reps, std::vector<double>* per_launch) {
+    measured = true;
     Impl& I = *p_;
     if (!I.use_graph) throw StatusError(MPG_ERR_UNSUPPORTED, "the cycle is not captured (MPG_NO_GRAPH / eager ranks)");
     if (which != 0 && which != 2 && which != 3) throw std::invalid_argument("phase: 0 spmv, 2 cgs update, 3 dots");
@@ -1228,6 +1242,7 @@ double FusedEngine::time_phase_stamps(int which, int reps, std::vector<double>* 
 // gets the dots re-run ahead of it, whose own share is measured and taken
 // out). Measurement only, like time_phase_graph.
 double FusedEngine::time_phase_dup(int which, int reps, int64_t* launches) {
+    measured = true;
     Impl& I = *p_;
     if (!I.use_graph) throw StatusError(MPG_ERR_UNSUPPORTED, "the cycle is not captured (MPG_NO_GRAPH / eager ranks)");
     if (which != 0 && which != 2 && which != 3) throw std::invalid_argument("phase: 0 spmv, 2 cgs update, 3 dots");
@@ -1503,6 +1518,11 @@ int mpg_engine_sell_columns(mpg_engine_t e, int32_t* form, int64_t* csr_slices, 
 int mpg_engine_givens_folded(mpg_engine_t e) {
     if (!e || !e->eng) return MPG_ERR_ARG;
     return e->eng->givens_folded() ? 1 : 0;
+}
+
+int mpg_engine_comm_ranks(mpg_engine_t e) {
+    if (!e || !e->eng) return MPG_ERR_ARG;
+    return e->comm ? e->comm->transport_ranks() : 1;
 }
 
 int64_t mpg_engine_sell_shared_slices(mpg_engine_t e) {

@@ -54,6 +54,9 @@ public:
     virtual std::string async_error() { return {}; }
     // tear the communicator down so that pending collectives return (ncclCommAbort)
     virtual void abort() {}
+    // ranks the transport itself reports (RCCL: ncclCommCount), -1 when it
+    // cannot say; the caller's size() otherwise
+    virtual int transport_ranks() { return size(); }
 };
 
 // RAII device buffer through the C-ABI allocator
@@ -109,6 +112,10 @@ public:
     double minvb_norm = 0, b_norm = 0, a_norm = 0;
     double setup_seconds = 0;
     BreakdownLog breakdown;  // non-finite |s(k+1)| / restart residuals (IterUtil.hpp)
+    // set by every time_phase*: the measurement launches (duplicated kernels,
+    // cycles run without the host's checks) change V, H, w and x, so run()
+    // refuses to continue the solve afterwards
+    bool measured = false;
 
 private:
     struct Impl;

@@ -12,7 +12,10 @@
 // mpg_gen_spec), --mode mixed-half, --half-unscaled (mixed-half: plain fp16
 // cast, a value outside fp16's range is an error), --engine {fused,surface},
 // --device D, --stop-on-breakdown (end the solve with an error at the first
-// non-finite Arnoldi residual; without it the count goes to stderr).
+// non-finite Arnoldi residual; without it the count goes to stderr),
+// --ngpus N (row-partition the fused solve over N GPUs of this process, one
+// host thread per GPU, RCCL clique by ncclCommInitAll: mpg_solve_multi_gpu;
+// devices --device .. --device+N-1; fails when fewer GPUs are visible).
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -21,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "mpgmres/dist.h"
 #include "mpgmres/problems.h"
 #include "mpgmres/solve.h"
 
@@ -49,6 +53,7 @@ int main(int argc, char* argv[]) {
     a.engine = MPG_ENGINE_FUSED;
     a.verbose = 1;
     unsigned rand_seed = 42;
+    int ngpus = 0;  // 0: mpg_solve on one device
 
     for (int i = 1; i < argc; ++i) {
         const std::string f = argv[i];
@@ -72,6 +77,7 @@ int main(int argc, char* argv[]) {
         else if (f == "--jacobi-steps") a.jacobi_steps = std::stoi(next());
         else if (f == "--gpu") { /* always on the GPU */ }
         else if (f == "--device") a.device = std::stoi(next());
+        else if (f == "--ngpus") ngpus = std::stoi(next());
         else if (f == "--half-unscaled") a.half_unscaled = 1;
         else if (f == "--stop-on-breakdown") a.stop_on_breakdown = 1;
         else if (f == "--mode") {
@@ -112,6 +118,10 @@ int main(int argc, char* argv[]) {
     if (a.rlen <= 0) {
         // the reference indexes an empty H when --rlen is missing
         std::cout << "A positive --rlen is required" << std::endl;
+        return 1;
+    }
+    if (ngpus < 0 || (ngpus > 1 && a.engine != MPG_ENGINE_FUSED)) {
+        std::cout << "--ngpus runs the fused engine on a positive number of GPUs" << std::endl;
         return 1;
     }
     if (!a_path && synthetic.empty()) {
@@ -158,7 +168,22 @@ int main(int argc, char* argv[]) {
     a.b = b.data();
     a.x_true = x_true.data();
     mpg_solve_result r{};
-    int st = mpg_solve(&a, &r);
+    int st;
+    if (ngpus >= 1 && !(ngpus == 1 && a.engine != MPG_ENGINE_FUSED)) {
+        std::vector<int32_t> devices((size_t)ngpus);
+        for (int q = 0; q < ngpus; ++q) devices[(size_t)q] = a.device + q;
+        std::cout << (a.mode == MPG_MODE_MIXED || a.mode == MPG_MODE_MIXED_HALF ? "Doing Mixed Precision test"
+                                                                                : "Doing Baseline test")
+                  << std::endl;
+        st = mpg_solve_multi_gpu(&a, ngpus, devices.data(), &r, nullptr);
+        if (st == 0) {
+            std::cout << "  ilu took " << (float)r.setup_seconds << "s; gmres took " << (float)r.gmres_seconds << "s"
+                      << std::endl;
+            std::cout << "  resNorm = " << r.res_norm << "; errNorm = " << r.err_norm << std::endl;
+        }
+    } else {
+        st = mpg_solve(&a, &r);
+    }
     mpg_host_csr_free(&A);
     // (stderr: the stdout lines stay the reference's, automated.py:33-38)
     if (r.nonfinite_steps > 0 || r.nonfinite_cycles > 0)

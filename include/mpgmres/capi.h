@@ -53,6 +53,8 @@ const char* mpg_ctx_last_error(mpg_ctx_t ctx);
 /* ---- context / memory (replaces Kokkos::View allocation + deep_copy,
  *      types.hpp:15-228, and CudaLibSingleton, types_cuda.hpp:9-36) ---- */
 int mpg_ctx_create(int device, mpg_ctx_t* out);
+/* HIP devices visible to this process (hipGetDeviceCount; 0 when none) */
+int mpg_device_count(void);
 int mpg_ctx_destroy(mpg_ctx_t ctx);
 /* Device::execution_space().fence() (gmres.cpp:113, 225) */
 int mpg_ctx_sync(mpg_ctx_t ctx);

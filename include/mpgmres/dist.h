@@ -110,10 +110,23 @@ typedef struct {
     int64_t row0;             /* first global row */
     int64_t csr_slices, implicit_slices;
     int64_t half_rows_scaled; /* mixed-half: rows scaled by a power of two */
+    int32_t device;           /* the HIP device the rank ran on */
+    int32_t transport_ranks;  /* ranks its communicator reports (RCCL: ncclCommCount) */
 } mpg_rank_layout;
 /* mpg_solve_loopback, reporting each rank's layout (layouts: nranks entries, may be NULL) */
 int mpg_solve_loopback_ex(const mpg_solve_args* args, int32_t nranks, mpg_solve_result* result,
                           mpg_rank_layout* layouts);
+
+/* One process, `ngpus` ranks: rank q is a host thread on device devices[q]
+ * (devices NULL: 0..ngpus-1), rows split evenly by nnz as in
+ * mpg_solve_loopback, collectives over one RCCL clique made by
+ * ncclCommInitAll (the CLI's --ngpus). The result matches
+ * mpg_solve's (x gathered from every rank, history from rank 0). Fails with
+ * MPG_ERR_ARG and a message when fewer devices are visible than requested or
+ * a device is named twice (RCCL runs one rank per GPU), MPG_ERR_RCCL when the
+ * clique cannot be made. layouts: ngpus entries, may be NULL. */
+int mpg_solve_multi_gpu(const mpg_solve_args* args, int32_t ngpus, const int32_t* devices, mpg_solve_result* result,
+                        mpg_rank_layout* layouts);
 
 #ifdef __cplusplus
 }

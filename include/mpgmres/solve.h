@@ -172,6 +172,10 @@ int64_t mpg_engine_sell_shared_slices(mpg_engine_t e);
 int mpg_engine_sell_sigma(mpg_engine_t e);
 /* 1: the Givens step of step k-1 rides SpMV(k) (mpg_arnoldi_fold_pays); 0: its own launch */
 int mpg_engine_givens_folded(mpg_engine_t e);
+/* ranks of the engine's communicator as its transport reports them: 1 for a
+ * single-GPU engine, ncclCommCount for an RCCL rank, the world size for the
+ * host transport; < 0 on error */
+int mpg_engine_comm_ranks(mpg_engine_t e);
 /* slices per wave of the engine's SELL Arnoldi SpMV (mpg_arnoldi_slices_per_wave) */
 int mpg_engine_slices_per_wave(mpg_engine_t e);
 /* mode mixed-half: stats[4] of the fp16 cast (mpg_csr_half_values); zeros otherwise */

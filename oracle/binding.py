@@ -2,13 +2,22 @@
 from __future__ import annotations
 
 import ctypes as C
+import os
 import subprocess
 from pathlib import Path
 
 import numpy as np
 
 ORACLE_DIR = Path(__file__).resolve().parent
-LIB = ORACLE_DIR / "_build" / "liboracle.so"
+# MKL's conditional numerical reproducibility: one code branch on every host
+# (read by MKL at its first call, so set before the library is used). Without
+# it MKL picks its branch by CPU -- AVX-512 on the build container's Xeon, a
+# generic branch on the GPU box's EPYC -- and the fp32 sums of a large solve
+# differ between the two (tests/parity.py, tools/oracle_cnr.py). AVX2 runs on
+# both. The CPU baseline in bench.py runs on the same branch.
+os.environ.setdefault("MKL_CBWR", "AVX2")
+# MPG_ORACLE_LIB: the ASan/UBSan build of the same sources (make -C oracle sanitize)
+LIB = Path(os.environ["MPG_ORACLE_LIB"]) if os.environ.get("MPG_ORACLE_LIB") else ORACLE_DIR / "_build" / "liboracle.so"
 
 _lib = None
 
@@ -27,6 +36,7 @@ def lib() -> C.CDLL:
         _lib.oracle_max_threads.restype = C.c_int
         _lib.oracle_solve.restype = C.c_int
         _lib.oracle_force_loops.argtypes = [C.c_int]
+        _lib.oracle_cbwr_branch.restype = C.c_int
         d, f, i, p = C.c_double, C.c_float, C.c_int, C.c_void_p
         _lib.oracle_spmv_f64.argtypes = [i, p, p, p, d, p, d, p]
         _lib.oracle_spmv_f32.argtypes = [i, p, p, p, f, p, f, p]
@@ -51,6 +61,15 @@ def lib() -> C.CDLL:
             getattr(_lib, f"oracle_ilu0_{t}").argtypes = [i, p, p, p, p, p]
             getattr(_lib, f"oracle_ilu_apply_{t}").argtypes = [i, p, p, p, i, i, p]
     return _lib
+
+
+def cbwr() -> str:
+    """The MKL code branch the oracle runs ("AVX2" when pinned; "auto" when
+    MKL picks by CPU; "" without MKL)."""
+    names = {1: "auto", 3: "COMPATIBLE", 4: "SSE2", 6: "SSSE3", 7: "SSE4_1", 8: "SSE4_2", 9: "AVX", 10: "AVX2",
+             12: "AVX512", 14: "AVX512_E1"}
+    b = lib().oracle_cbwr_branch()
+    return "" if b < 0 else names.get(b, str(b))
 
 
 def backend() -> str:

@@ -72,6 +72,9 @@ void load() {
     bind(h, a.destroy, "mkl_sparse_destroy", ok);
     bind(h, a.set_num_threads, "MKL_Set_Num_Threads", ok);
     bind(h, a.get_max_threads, "MKL_Get_Max_Threads", ok);
+    // conditional numerical reproducibility (MKL_CBWR in the environment,
+    // read by MKL at its first call): the branch it runs, for the record
+    a.cbwr_get = reinterpret_cast<int (*)(int)>(dlsym(h, "MKL_CBWR_Get"));  // (mkl_cbwr_get is the by-reference Fortran entry)
     a.loaded = ok;
     a.path = used;
 }
@@ -150,6 +153,7 @@ void set_threads(int threads) {
 }
 
 int max_threads() { return mkl().loaded ? mkl().get_max_threads() : 1; }
+int cbwr_branch() { return mkl().loaded && mkl().cbwr_get ? mkl().cbwr_get(1) : -1; }
 
 double dot(int n, const double* x, const double* y) {
     if (mkl().loaded) return mkl().ddot(n, x, 1, y, 1);

@@ -52,6 +52,7 @@ struct MklApi {
     int (*destroy)(void*) = nullptr;
     void (*set_num_threads)(int) = nullptr;
     int (*get_max_threads)() = nullptr;
+    int (*cbwr_get)(int) = nullptr;  // mkl_cbwr_get (optional)
 };
 
 // Loaded once per process; `loaded` false means the loop backend.
@@ -62,6 +63,8 @@ void force_loops(bool on);
 const char* backend_name();
 void set_threads(int threads);
 int max_threads();
+// MKL's conditional-numerical-reproducibility branch (mkl_cbwr_get(MKL_CBWR_BRANCH)); -1 without MKL
+int cbwr_branch();
 
 // ---- typed BLAS used by the restated algorithm ----
 double dot(int n, const double* x, const double* y);

@@ -700,6 +700,7 @@ extern "C" {
 
 const char* oracle_backend() { return oracle::backend_name(); }
 int oracle_max_threads() { return oracle::max_threads(); }
+int oracle_cbwr_branch() { return oracle::cbwr_branch(); }
 void oracle_force_loops(int on) { oracle::force_loops(on != 0); }
 
 int oracle_solve(const mpg_solve_args* a, mpg_solve_result* r) {

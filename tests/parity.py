@@ -38,14 +38,23 @@ preconditioner every step (modes mixed, single, mixed-half, single-prec):
     10x the reference's (a more accurate x than the oracle's is not a
     parity failure: forward error at convergence depends on conditioning);
   * when converged, the final backward error is <= tol.
-Live-oracle comparisons of fp32 Arnoldi on large inputs run the oracle on
-its loop kernels (binding.solve(backend="loops"): fp32 products summed in
-fp64 in index order, the HIP kernels' summation class) and bound the GPU by
-the MKL oracle one-sidedly (not_worse_than): MKL's fp32 sgemv sums in fp32
-in an order that depends on the CPU and its thread count, and on n >= 80k
-its cycle-1 backward error moved 3-12x between this container and the GPU
-box (profiles/r04_oracle_backends.txt) while the loop oracle matched the GPU
-to 4 digits.
+Live-oracle comparisons of fp32 Arnoldi on large inputs (compare_mkl, round
+5) compare with the MKL oracle two-sidedly. The oracle's MKL is pinned to one
+code branch (MKL_CBWR=AVX2, set by oracle/binding.py: conditional numerical
+reproducibility) and run at fixed thread counts (MKL_THREADS), so its bits
+no longer depend on the host CPU: round 4 had seen its cycle-1 backward
+error move 3-12x between this container (AVX-512 branch) and the GPU box
+(EPYC: MKL's generic branch) -- profiles/r04_oracle_backends.txt,
+profiles/r05_oracle_cnr/. MKL's fp32 sgemv/sparse mv still sum in fp32 in
+an order that depends on the thread count, which moves the cycle >= 1
+backward error of a large fp32 solve by up to ~3.5x between thread counts
+on one host, while the HIP kernels sum in fp64 (more accurately than any
+of them). So each cycle's backward error must lie inside the envelope of
+the MKL runs at those thread counts widened by the factor 3 of the rule
+above ([min/3, 3 max]); everything else follows compare() against the
+1-thread run (the reference's serial arithmetic). The oracle's loop kernels
+(fp32 products summed in fp64 in index order, the HIP kernels' summation
+class) stay a diagnostic (tools/oracle_cnr.py).
 Measured margins behind these numbers: tools/parity_margins.py over the
 168 golden records on the fused and operator-surface engines
 (profiles/r02_parity_margins.txt; the x terms against e_ref alone:
@@ -68,7 +77,11 @@ def _ratio_ok(a, b, factor):
     return max(a / b, b / a) <= factor
 
 
-def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
+def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = "", envelope=None):
+    """envelope: None, or a list of oracle Results of the same solve (MKL at
+    MKL_THREADS) whose per-cycle backward errors bound got's (fp32 Arnoldi
+    rule, see the module docstring) and whose restart counts widen the +-1
+    rule; ref stays the reference for every other check."""
     fp64 = mode == "baseline"
     assert got.status == ref["status"], f"{label}: status {got.status} vs {ref['status']}"
     minvb = float(ref["minvb_norm"])
@@ -89,15 +102,20 @@ def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
         assert np.all(np.abs(be_got - be_ref) <= 1e-5 * be_ref + 1e-15), f"{label}: backward errors"
         x_rtol, e_w, e_ws, norm_factor = 1e-12, 0.25, 1.0, (1.2, 2.0)
     else:
-        assert abs(got.restarts - ref["restarts"]) <= 1, f"{label}: restarts {got.restarts} vs {ref['restarts']}"
+        restarts = [ref["restarts"]] + ([int(r.restarts) for r in envelope] if envelope else [])
+        assert min(abs(got.restarts - r) for r in restarts) <= 1, f"{label}: restarts {got.restarts} vs {restarts}"
         k = min(rlen, len(s_ref), len(s_got))
         d = np.abs(s_got[:k] - s_ref[:k])
         assert np.all(d <= 1e-3 * s_ref[:k] + 1e-5 * minvb), f"{label}: cycle-0 history {d.max():.3e}"
         floor = 1e-6 if mode == "single" else 1e-14
-        nc = min(len(be_ref), len(be_got)) - (0 if got.restarts == ref["restarts"] else 1)
-        for c in range(max(nc, 0)):
-            assert _ratio_ok(max(be_got[c], floor), max(be_ref[c], floor), 3.0), \
-                f"{label}: cycle {c} backward error {be_got[c]:.3e} vs {be_ref[c]:.3e}"
+        if envelope:
+            ok, msg = mkl_envelope_ok(envelope, got, mode)
+            assert ok, f"{label}: {msg}"
+        else:
+            nc = min(len(be_ref), len(be_got)) - (0 if got.restarts == ref["restarts"] else 1)
+            for c in range(max(nc, 0)):
+                assert _ratio_ok(max(be_got[c], floor), max(be_ref[c], floor), 3.0), \
+                    f"{label}: cycle {c} backward error {be_got[c]:.3e} vs {be_ref[c]:.3e}"
         if got.status == "converged":
             assert be_got[-1] <= tol, f"{label}: final backward error {be_got[-1]:.3e} > {tol}"
         x_rtol, e_w, e_ws = (1e-5 if mode == "single" else 1e-9), 0.5, 2.5
@@ -126,6 +144,43 @@ def compare(ref: dict, got, mode: str, tol: float, rlen: int, label: str = ""):
                     f"{label}: errNorm {e_got:.3e} vs {e_ref:.3e}"
             else:
                 assert e_got <= norm_factor[1] * max(e_ref, ef), f"{label}: errNorm {e_got:.3e} vs {e_ref:.3e}"
+
+
+# the oracle's MKL thread counts of compare_mkl (fixed, so the envelope is
+# the same on every host: the MKL branch is pinned by MKL_CBWR)
+MKL_THREADS = (1, 4, 8)
+
+
+def mkl_envelope_ok(refs, got, mode: str, factor: float = 3.0):
+    """(ok, message): every cycle's backward error of got (above the floor)
+    within [min_T be_T / factor, factor max_T be_T] over the runs refs, for
+    the cycles every run reached (all but the last when restart counts
+    differ)."""
+    floor = 1e-6 if mode == "single" else 1e-14
+    be_got = _arr(got.cyc_r_norm) / _arr(got.cyc_normalization)
+    bes = [_arr(r.cyc_r_norm) / _arr(r.cyc_normalization) for r in refs]
+    same = all(r.restarts == got.restarts for r in refs)
+    nc = min([len(be_got)] + [len(b) for b in bes]) - (0 if same else 1)
+    for c in range(max(nc, 0)):
+        lo = min(max(b[c], floor) for b in bes)
+        hi = max(max(b[c], floor) for b in bes)
+        g = max(be_got[c], floor)
+        if not (np.isfinite(g) and lo / factor <= g <= factor * hi):
+            return False, f"cycle {c} backward error {be_got[c]:.3e} outside [{lo / factor:.3e}, {factor * hi:.3e}]"
+    return True, ""
+
+
+def compare_mkl(oracle, mpg, A, b, xt, got, opts: dict, label: str = "", runs: dict = None):
+    """Two-sided parity with the MKL oracle (module docstring): the oracle at
+    each of MKL_THREADS (pinned MKL branch), got compared with the 1-thread
+    run inside the runs' envelope. runs: a cache {threads: Result}."""
+    runs = {} if runs is None else runs
+    for t in MKL_THREADS:
+        if t not in runs:
+            runs[t] = oracle.solve(mpg, A, b, xt, backend="mkl", threads=t, **opts)
+    refs = [runs[t] for t in MKL_THREADS]
+    compare(as_ref(refs[0]), got, opts["mode"], opts["tol"], opts["rlen"], label, envelope=refs)
+    return runs
 
 
 def not_worse_than(ref, got, mode: str, label: str = "", factor: float = 3.0):

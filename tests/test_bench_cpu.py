@@ -32,3 +32,102 @@ def test_pmc_traffic_has_the_bench_kernels():
     # the FETCH_SIZE x2 correction is recorded with the numbers
     d = json.loads((REPO / "profiles" / "pmc_traffic.json").read_text())
     assert "x2" in d["_fetch_correction"]
+
+
+# ---- the N-rank launcher: no GPU work in --dry-run
+
+
+def _bench(args, env_extra=None, timeout=300):
+    import os
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, str(REPO / "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=env)
+
+
+def test_launcher_starts_n_ranks():
+    """`bench.py --gpus 2` with no launcher starts two rank processes with
+    the torch.distributed.run environment; rank 0's line is relayed on
+    stdout, rank 1's goes to stderr."""
+    p = _bench(["--gpus", "2", "--dry-run"])
+    assert p.returncode == 0, p.stderr
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and lines[0]["rank"] == 0 and lines[0]["world"] == 2, p.stdout
+    assert lines[0]["master"].startswith("127.0.0.1:")
+    other = [json.loads(ln.split("] ", 1)[1]) for ln in p.stderr.splitlines() if ln.startswith("[rank 1 stdout]")]
+    assert len(other) == 1 and other[0]["world"] == 2 and other[0]["local_rank"] == 1, p.stderr
+    assert other[0]["master"] == lines[0]["master"]
+
+
+def test_launcher_fails_when_a_rank_fails():
+    p = _bench(["--gpus", "3", "--dry-run"], {"MPG_BENCH_DRY_FAIL_RANK": "1"})
+    assert p.returncode != 0
+    assert "rank 1 exited" in p.stderr
+
+
+def test_launcher_refuses_missing_gpus():
+    """Fewer visible GPUs than --gpus is an error, never a silent N = 1
+    (this container has none)."""
+    p = _bench(["--gpus", "2"])
+    assert p.returncode == 2 and "needs 2 visible GPU(s), found 0" in p.stderr, (p.returncode, p.stderr[-500:])
+    assert not p.stdout.strip()
+
+
+def test_launcher_flag_and_world_must_agree():
+    p = _bench(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "4", "RANK": "0"})
+    assert p.returncode == 0  # dry-run reports before any check
+    p = _bench(["--gpus", "2"], {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode == 2 and "disagree" in p.stderr
+
+
+# ---- degenerate timings (VERDICT r4 next #6): bench never divides by a non-positive time
+
+
+class _FakeEngine:
+    def __init__(self, dup_ms, stamps_ms):
+        self.dup_ms, self.stamps_ms = dup_ms, stamps_ms
+
+    def spmv_layout(self):
+        return {"format": "sell", "slices_per_wave": 2, "givens_folded": True}
+
+    def time_phase_dup(self, phase, reps):
+        return self.dup_ms, 30 * reps
+
+    def time_phase_graph(self, phase, reps):
+        return 0.012, [0.012] * (30 * reps)
+
+    def time_phase_stamps(self, phase, reps):
+        return self.stamps_ms, [self.stamps_ms or 0.0] * (30 * reps)
+
+    def time_spmv_incycle(self, cycles):
+        return 0.0125, [0.0125] * (30 * cycles)
+
+    def phase_bytes(self, phase):
+        return 5.2e7
+
+
+def test_phase_roofline_degenerate_clock_is_null():
+    for dup, st in ((0.0, 0.011), (-0.002, 0.011), (0.011, 0.0)):
+        out = bench.phase_roofline(_FakeEngine(dup, st), 30, 3, {})
+        assert out == {"k_dots_nc": None, "k_cgs_update_nc": None}, (dup, st, out)
+    out = bench.phase_roofline(_FakeEngine(0.012, 0.011), 30, 3, {})
+    assert out["k_dots_nc"]["avg_launch_ms"] == 0.012
+
+
+def test_phase_roofline_empty_timings_are_null():
+    class Empty(_FakeEngine):
+        def time_phase_stamps(self, phase, reps):
+            return 0.011, []
+
+    out = bench.phase_roofline(Empty(0.012, 0.011), 30, 3, {})
+    assert out == {"k_dots_nc": None, "k_cgs_update_nc": None}
+
+
+def test_spmv_roofline_falls_back_on_a_degenerate_difference():
+    for dup in (0.0, -0.001):
+        sp = bench.spmv_roofline(_FakeEngine(dup, 0.011), 3)
+        assert sp["timing"] == "eager" and sp["avg_launch_ms"] == 0.0125
+    sp = bench.spmv_roofline(_FakeEngine(0.011, 0.011), 3)
+    assert sp["timing"] == "dup" and sp["avg_launch_ms"] == 0.011

@@ -72,3 +72,19 @@ def test_cli_bpath_right_hand_side(mpg, tmp_path):
                     tol=1e-9)
     assert int(m.group(3)) == got.restarts and int(m.group(4)) == got.total_iters
     assert abs(float(m.group(8)) - np.linalg.norm(got.x)) <= 1e-5 * np.linalg.norm(got.x)  # errNorm, x_true = 0
+
+
+def test_cli_ngpus(mpg):
+    """--ngpus N row-partitions the fused solve over N GPUs of the process
+    (mpg_solve_multi_gpu): the reference's stdout lines at N = 1, and a clear
+    failure when more GPUs are asked for than are visible."""
+    args = [str(mpg.CLI), "--matrix", "laplace:12", "--rlen", "30", "--mode", "mixed", "--orth", "cgs",
+            "--prec", "jacobi", "--tol", "1e-9", "--gpu"]
+    out = subprocess.run(args + ["--ngpus", "1"], capture_output=True, text=True, timeout=120, check=True).stdout
+    m = SUMMARY.search(out)
+    assert m and "Doing Mixed Precision test" in out, out
+    ref = SUMMARY.search(subprocess.run(args, capture_output=True, text=True, timeout=120, check=True).stdout)
+    assert m.group(4) == ref.group(4)  # the same iteration count as the one-GPU solve
+    n = mpg.device_count() + 1
+    r = subprocess.run(args + ["--ngpus", str(n)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1 and "visible" in r.stderr, (r.stdout, r.stderr)

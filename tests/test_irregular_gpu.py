@@ -10,13 +10,14 @@ apply. Two stand-ins take the general path:
     probability 70 %): rows of variable length, in natural and in permuted
     order.
 Each solve is compared with the live oracle (kernels_mkl.cpp's path,
-kernels_mkl.cpp:326-352 for the SpMV; on its loop kernels, and bounded by
-its MKL run, tests/parity.py) on both engines, and each asserts
-which Arnoldi SpMV form it ran (int32 SELL or CSR-adaptive row blocks)."""
+kernels_mkl.cpp:326-352 for the SpMV: MKL pinned to one code branch at fixed
+thread counts, two-sided, tests/parity.py compare_mkl) on both engines, and
+each asserts which Arnoldi SpMV form it ran (int32 SELL or CSR-adaptive row
+blocks)."""
 import numpy as np
 import pytest
 
-from tests.parity import as_ref, compare, not_worse_than
+from tests.parity import compare_mkl
 
 pytestmark = pytest.mark.gpu
 
@@ -82,25 +83,14 @@ def test_irregular_layout(mpg, problems, which, fmt, monkeypatch):
 def test_irregular_live_oracle(mpg, oracle, problems, which, mode, orth, engine, fmt, monkeypatch):
     A, xt, b = problems[which]
     opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=1e-10, max_restarts=200)
-    ref = _oracle_runs(mpg, oracle, problems, which, mode, orth, opts)
-    assert ref["loops"].status == "converged"
     got = mpg.solve(A, b, xt, engine=engine, spmv_format=_fmt(fmt, monkeypatch), **opts)
     label = f"{which}-{mode}-{orth}/{engine}-{fmt}"
-    compare(as_ref(ref["loops"]), got, mode, opts["tol"], 30, label)
-    not_worse_than(ref["mkl"], got, mode, label + " vs mkl")
+    # the oracle runs once per (matrix, mode, orth), shared by every engine and storage
+    runs = compare_mkl(oracle, mpg, A, b, xt, got, opts, label, runs=_ORACLE.setdefault((which, mode, orth), {}))
+    assert runs[1].status == "converged"
 
 
 _ORACLE = {}
-
-
-def _oracle_runs(mpg, oracle, problems, which, mode, orth, opts):
-    """Both oracle backends once per (matrix, mode, orth): the loop kernels
-    for compare(), MKL for the one-sided bound (tests/parity.py)."""
-    key = (which, mode, orth)
-    if key not in _ORACLE:
-        A, xt, b = problems[which]
-        _ORACLE[key] = {be: oracle.solve(mpg, A, b, xt, backend=be, **opts) for be in ("loops", "mkl")}
-    return _ORACLE[key]
 
 
 @pytest.mark.parametrize("which", ["stencil27p", "fem27p"])

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from tests.golden.make_golden import inputs
-from tests.parity import as_ref, compare, not_worse_than
+from tests.parity import compare, compare_mkl
 
 pytestmark = pytest.mark.gpu
 
@@ -49,20 +49,23 @@ def test_golden_m100(mpg, mats, rec, engine):
 def test_band_m100_live_oracle(mpg, oracle, engine, mode, orth):
     """n = 300k (~73 one-per-CU workgroups per panel row group at k + 1 = 100:
     the two-level partial sums run for real), 2 restart cycles at tol = 0 then
-    compared cycle by cycle with the oracle on its loop kernels, and bounded
-    one-sidedly by the MKL oracle (tests/parity.py)."""
+    compared cycle by cycle with the MKL oracle, two-sided (round 5: its MKL
+    pinned to one code branch and run at fixed thread counts, tests/parity.py
+    compare_mkl)."""
     A = mpg.gen_band(300_000, 5, 4, seed=7)
     xt = mpg.rand_vect(A.nrows, 42)
     b = mpg.host_spmv(A, xt)
     opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=100, tol=0.0, max_restarts=2)
-    ref = oracle.solve(mpg, A, b, xt, backend="loops", **opts)
     got = mpg.solve(A, b, xt, engine=engine, **opts)
-    assert got.total_iters == ref.total_iters == 200
     label = f"band300k-{mode}-{orth}-m100/{engine}"
-    compare(as_ref(ref), got, mode, 0.0, 100, label)
-    not_worse_than(oracle.solve(mpg, A, b, xt, backend="mkl", **opts), got, mode, label + " vs mkl")
+    runs = compare_mkl(oracle, mpg, A, b, xt, got, opts, label, runs=_MKL.setdefault((mode, orth), {}))
+    ref = runs[1]
+    assert got.total_iters == ref.total_iters == 200
     if mode == "mixed":  # the whole history, not only cycle 0 (VERDICT r3 weak #1)
         np.testing.assert_allclose(got.step_res, ref.step_res, rtol=1e-3, atol=1e-6 * ref.minvb_norm)
+
+
+_MKL = {}  # (mode, orth) -> {threads: oracle Result}: one set of oracle runs for both engines
 
 
 def test_band_m100_engine_layout(mpg):

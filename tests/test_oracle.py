@@ -84,6 +84,23 @@ def test_oracle_reproduces_golden(mpg, oracle):
         compare(rec, r, case["mode"], case["tol"], case["rlen"], str(rec["case"]))
 
 
+def test_oracle_reproduces_golden_bits(mpg, oracle):
+    """Round 5: the records were made on MKL's pinned AVX2 branch (MKL_CBWR,
+    oracle/binding.py) at one thread, so the oracle reproduces them bit for
+    bit -- here and on any AVX2 host (tools/oracle_cnr.py --golden on the GPU
+    box: profiles/r05_oracle_cnr/)."""
+    assert oracle.cbwr() == GOLDEN["mkl_cbwr"] == "AVX2"
+    mats = inputs(mpg)
+    for rec in GOLDEN["cases"][::7]:
+        case = dict(rec["case"])
+        A = mats[case.pop("matrix")]
+        xt = mpg.rand_vect(A.nrows, 42)
+        b = mpg.host_spmv(A, xt)
+        r = oracle.solve(mpg, A, b, xt, threads=1, **case)
+        assert r.step_res.tolist() == rec["step_res"] and r.x[:16].tolist() == rec["x_head"], rec["case"]
+        assert r.cyc_r_norm.tolist() == rec["cyc_r_norm"] and r.total_iters == rec["total_iters"], rec["case"]
+
+
 def test_oracle_abort_semantics(mpg, oracle):
     A = mpg.gen_laplace3d(8)
     xt = mpg.rand_vect(A.nrows, 42)
