@@ -94,6 +94,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_host_csr_free.restype = None
     lib.mpg_engine_create.argtypes = [C.POINTER(SolveArgs), C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
     lib.mpg_cycle_program_counts.argtypes = [C.POINTER(_I64)] * 3
+    lib.mpg_surface_ride_counts.argtypes = [C.POINTER(_I64)] * 3
     lib.mpg_engine_report.argtypes = [C.c_void_p, C.POINTER(SolveResult)]
     lib.mpg_engine_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     lib.mpg_engine_sync.argtypes = [C.c_void_p]
@@ -486,6 +487,15 @@ def cycle_program_counts() -> dict:
     v = [_I64() for _ in range(3)]
     host_lib().mpg_cycle_program_counts(*[C.byref(x) for x in v])
     return {"recorded": v[0].value, "replayed": v[1].value, "voided": v[2].value}
+
+
+def surface_ride_counts() -> dict:
+    """The calling thread's operator-surface normalisation rides so far
+    (mpg_surface_ride_counts): CGS updates that redirected w, normalisations
+    that rode the next SpMV, and those issued separately instead."""
+    v = [_I64() for _ in range(3)]
+    host_lib().mpg_surface_ride_counts(*[C.byref(x) for x in v])
+    return {"redirects": v[0].value, "rides": v[1].value, "flushed": v[2].value}
 
 
 def row_slice(A: Csr, r0: int, r1: int) -> Csr:

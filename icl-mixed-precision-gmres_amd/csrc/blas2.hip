@@ -191,12 +191,15 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_t_quad(int64_t rows, const 
 // nrm2 stage 1's layout and order (k_nrm2_quad, blas1.hip: the lane's rows
 // in order, then block_sum<kQuadBlock>), so an nrm2(y) right after needs no
 // launch of its own (CGS: w -= V h, then h_{k+1,k} = ||w||)
+// y_out (round 5): the result goes there instead of y (a distinct buffer)
 template <class T, int NC, bool FROM_PARTS = false, bool NORM = false>
 __global__ __launch_bounds__(kQuadBlock) void k_gemv_n_quad(int64_t rows, T alpha, const T* __restrict__ A,
                                                             int64_t lda, T* __restrict__ x, T beta,
                                                             T* __restrict__ y, const double* __restrict__ partial = nullptr,
                                                             int nparts = 0, T alpha_t = T(1),
-                                                            double* __restrict__ norm_part = nullptr) {
+                                                            double* __restrict__ norm_part = nullptr,
+                                                            T* __restrict__ y_out = nullptr) {
+    T* __restrict__ yo = y_out ? y_out : y;
     constexpr int B = kColBatch<T>;
     __shared__ double xs[NC];
     double nacc = 0.0;
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_n_quad(int64_t rows, T alph
         T out[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) out[r] = beta == T(0) ? alpha * (T)t[r] : alpha * (T)t[r] + beta * (T)yr[r];
-        Row4<T>::store(y + i, out);
+        Row4<T>::store(yo + i, out);
         if constexpr (NORM) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_n_quad(int64_t rows, T alph
         for (int c = 0; c < NC; ++c) t += (double)A[(int64_t)c * lda + i] * xs[c];
         const T tt = (T)t;
         const T yi = beta == T(0) ? alpha * tt : alpha * tt + beta * y[i];
-        y[i] = yi;
+        yo[i] = yi;
         if constexpr (NORM) {
             const double a = (double)yi;
             nacc += a * a;
@@ -396,16 +399,17 @@ int gemv_t_finish(mpg_ctx* ctx, int32_t nparts, int64_t cols, T alpha, T beta, T
 // MPG_ERR_UNSUPPORTED unless A, lda and y allow the quad form
 template <class T>
 int gemv_n_from_t(mpg_ctx* ctx, int64_t rows, int64_t cols, T alpha, const T* A, int64_t lda, int32_t nparts,
-                  T alpha_t, T* x, T beta, T* y, int32_t* norm_nparts = nullptr) {
+                  T alpha_t, T* x, T beta, T* y, int32_t* norm_nparts = nullptr, T* y_out = nullptr) {
     if (!ctx || rows < 0 || cols < 1 || nparts < 1 || (rows > 0 && lda < rows)) return MPG_ERR_ARG;
-    if (cols > kGemvMaxCols || !quad_aligned(A, lda, y)) return MPG_ERR_UNSUPPORTED;
+    if (y_out && (!norm_nparts || (y_out < y + rows && y < y_out + rows))) return MPG_ERR_ARG;
+    if (cols > kGemvMaxCols || !quad_aligned(A, lda, y) || (y_out && (uintptr_t)y_out % 16)) return MPG_ERR_UNSUPPORTED;
     if (norm_nparts && rows < 1) return MPG_ERR_UNSUPPORTED;
     const int g = quad_groups(rows);
     const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto nc) {
         // the coefficients' partials sit apart from the ||y||^2 partials (kWsGemvSplit)
         if (norm_nparts)
             k_gemv_n_quad<T, decltype(nc)::value, true, true><<<g, kQuadBlock, 0, ctx->stream>>>(
-                rows, alpha, A, lda, x, beta, y, ctx->red_ws + kWsGemvSplit, nparts, alpha_t, ctx->red_ws);
+                rows, alpha, A, lda, x, beta, y, ctx->red_ws + kWsGemvSplit, nparts, alpha_t, ctx->red_ws, y_out);
         else
             k_gemv_n_quad<T, decltype(nc)::value, true><<<g, kQuadBlock, 0, ctx->stream>>>(
                 rows, alpha, A, lda, x, beta, y, ctx->red_ws + kWsGemvSplit, nparts, alpha_t);
@@ -522,6 +526,20 @@ int mpg_gemv_n_from_t_nrm2_f32(mpg_ctx_t c, int64_t rows, int64_t cols, float al
                                int32_t np, float alpha_t, float* x, float beta, float* y, int32_t* norm_np) {
     if (!norm_np) return MPG_ERR_ARG;
     return gemv_n_from_t<float>(c, rows, cols, alpha, A, lda, np, alpha_t, x, beta, y, norm_np);
+}
+int mpg_gemv_n_from_t_nrm2_out_f64(mpg_ctx_t c, int64_t rows, int64_t cols, double alpha, const double* A,
+                                   int64_t lda, int32_t np, double alpha_t, double* x, double beta, const double* y,
+                                   double* y_out, int32_t* norm_np) {
+    if (!norm_np || !y_out) return MPG_ERR_ARG;
+    return gemv_n_from_t<double>(c, rows, cols, alpha, A, lda, np, alpha_t, x, beta, const_cast<double*>(y), norm_np,
+                                 y_out);
+}
+int mpg_gemv_n_from_t_nrm2_out_f32(mpg_ctx_t c, int64_t rows, int64_t cols, float alpha, const float* A,
+                                   int64_t lda, int32_t np, float alpha_t, float* x, float beta, const float* y,
+                                   float* y_out, int32_t* norm_np) {
+    if (!norm_np || !y_out) return MPG_ERR_ARG;
+    return gemv_n_from_t<float>(c, rows, cols, alpha, A, lda, np, alpha_t, x, beta, const_cast<float*>(y), norm_np,
+                                y_out);
 }
 int mpg_trsv_f64(mpg_ctx_t c, int upper, int trans, int64_t n, const double* A, int64_t lda, double* x) {
     return trsv_impl<double>(c, upper, trans, n, A, lda, x);

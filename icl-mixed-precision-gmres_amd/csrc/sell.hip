@@ -194,11 +194,47 @@ int with_store(int vtype, F&& f) {
 
 constexpr int kProgStage = 64;  // rot_vec rotations staged per pass by a riding scalar program
 
+// NORM (round 5): the operator surface's add_vector normalisation riding the
+// next Arnoldi SpMV (kernels_hip.cpp). x is w (in a scratch copy: the SpMV
+// writes its own w); every workgroup sums the <= 256 ||w||^2 partials the
+// fused CGS gemv left in the workspace with block_sum<kBlock> (the bits of
+// k_consume_partials' block_sum<1024>: the extra lanes add exact zeros, in
+// the same sequential wave order), forms r = T(sqrt(s)) and a = T(1) / r
+// (k_consume_partials, blas1.hip), gathers T(a x_c) -- scal_recip's
+// product -- stores v = T(a x_i) for its own rows, and workgroup 0 stores
+// h = r before any riding scalar program (which reads it) runs.
+template <class X>
+struct NormArgs {
+    const double* part = nullptr;
+    int nparts = 0;
+    X* h = nullptr;
+    X* v = nullptr;
+};
+
+// a = T(1) / T(sqrt(sum of the partials)), the same in every lane; workgroup
+// 0's thread 0 stores r to *h first. Every thread of the workgroup calls it.
+template <class X>
+__device__ __forceinline__ X norm_scale(const NormArgs<X>& nm, double pv) {
+    __shared__ double scratch[kBlock / kWave];
+    __shared__ X a_s;
+    const double s = block_sum<kBlock>(pv, scratch);
+    if (threadIdx.x == 0) {
+        const X r = (X)sqrt(s);
+        if (blockIdx.x == 0) {
+            *nm.h = r;
+            __threadfence();  // the riding program reads h(k+1,k)
+        }
+        a_s = X(1) / r;
+    }
+    __syncthreads();
+    return a_s;
+}
+
 // y = alpha * T(A x) (+ beta * y) on the sliced copy; one wave per slice.
 // prog.count > 0: workgroup 0 runs that scalar program instead (the
 // operator surface's Givens step of the previous Arnoldi step, which nothing
 // in this SpMV reads or writes: kernels_hip.cpp checks the operands).
-template <class X, class S, class CI, int W, bool WIN, bool UNI = false>
+template <class X, class S, class CI, int W, bool WIN, bool UNI = false, bool NORM = false>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslices, const int64_t* __restrict__ off,
                                                       const CI* __restrict__ col, const S* __restrict__ val,
                                                       const int32_t* __restrict__ sbase,
@@ -207,24 +243,32 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
                                                       const int32_t* __restrict__ xcol, const S* __restrict__ xval,
                                                       const X* __restrict__ x, X alpha, X beta, X* __restrict__ y,
                                                       int64_t ustride, int xcd, ScalarProgram prog,
-                                                      const int32_t* __restrict__ rows) {
+                                                      const int32_t* __restrict__ rows, NormArgs<X> nm) {
     constexpr int NQ = kWinLen / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
+    // NORM: the ||w||^2 partial of this lane, issued before anything else
+    double pv = 0.0;
+    if constexpr (NORM) pv = (int)threadIdx.x < nm.nparts ? nm.part[threadIdx.x] : 0.0;
     // a scalar program riding in this launch: workgroup 0 (dispatched first,
     // so it runs under the slices instead of after them), its first wave
     int b = (int)blockIdx.x, G = (int)gridDim.x;
     if (prog.count > 0) {
         if (b == 0) {
             __shared__ double plds[3 * kProgStage + 1];
+            if constexpr (NORM) (void)norm_scale(nm, pv);  // h(k+1,k) stored before the program reads it
             if (wid == 0) run_scalar_program<kProgStage>(prog, plds);
             return;
         }
         --b;
         --G;
     }
-    const int s = (xcd ? xcd_block(b, G) : b) * (kBlock / kWave) + wid;
-    if (s >= nslices) return;  // no workgroup barrier below: a dead wave may leave
+    const int s_raw = (xcd ? xcd_block(b, G) : b) * (kBlock / kWave) + wid;
+    const bool dead = s_raw >= nslices;
+    // without NORM a dead wave may leave (no workgroup barrier below); with it
+    // every wave takes part in the partial sum first (on slice 0's loads)
+    if (!NORM && dead) return;
+    const int s = dead ? 0 : s_raw;
     const int row0 = s * kWave;
     SellRow<S, CI, W> row;
     if constexpr (UNI) row.init_uniform(s, ustride, spat, coff);
@@ -241,26 +285,36 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
         }
     }
     const X yi = beta != X(0) ? y[i < n ? i : 0] : X(0);
+    X xo = X(0);  // NORM, no window: the lane's own entry of w
+    if constexpr (NORM && !WIN) xo = x[i < n ? i : 0];
     __builtin_amdgcn_sched_barrier(0);
     row.init_finish(lane, col, val, sbase, pat);
     row.load(0);
     __builtin_amdgcn_sched_barrier(0);
+    X a = X(1);
+    if constexpr (NORM) {
+        a = norm_scale(nm, pv);
+        if (dead) return;
+    }
+    auto sc = [&](X v) { return NORM ? (X)(a * v) : v; };
     double sum = 0.0;
     if constexpr (WIN) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const int c = row0 - kWinLo + q * kWave + lane;
-            win[wid][q * kWave + lane] = (c >= 0 && c < cols) ? xr[q] : X(0);
+            win[wid][q * kWave + lane] = (c >= 0 && c < cols) ? sc(xr[q]) : X(0);
         }
         wave_lds_sync();
         auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
+        if constexpr (NORM) if (i < n) nm.v[i] = win[wid][i - row0 + kWinLo];
         row.sum(0, xv, sum);
         for (int q = row.U; q < row.steps; q += row.U) {
             row.load(q);
             row.sum(q, xv, sum);
         }
     } else {
-        auto xv = [&](int c) { return (double)x[c]; };
+        if constexpr (NORM) if (i < n) nm.v[i] = sc(xo);
+        auto xv = [&](int c) { return (double)sc(x[c]); };
         if (SellCol<CI>::stepped && row.exc) {
             sum = csr_row_sum(i < n ? row.xrow : -1, xrp, xcol, xval, xv);
         } else {
@@ -284,38 +338,43 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
 // batch's gathers) are issued before the wave waits for any of them, so a
 // wave carries twice the bytes through the same fixed work. The row sums are
 // k_sell_spmv's (fp64, CSR order), so y has the same bits.
-template <class X, class S, int W, bool WIN, int BE>
+template <class X, class S, int W, bool WIN, int BE, bool NORM = false>
 __global__ __launch_bounds__(kBlock) void k_sell_spmv2(int n, int cols, int nslices, const int16_t* __restrict__ col,
                                                        const S* __restrict__ val, const int32_t* __restrict__ sbase,
                                                        const int32_t* __restrict__ spat, const int64_t* __restrict__ coff,
                                                        const int16_t* __restrict__ pat, const X* __restrict__ x, X alpha,
                                                        X beta, X* __restrict__ y, int64_t ustride, int xcd,
-                                                       ScalarProgram prog) {
+                                                       ScalarProgram prog, NormArgs<X> nm) {
     using CI = int16_t;
     constexpr int SPW = 2;
     constexpr int WL = kWinLen + (SPW - 1) * kWave;
     constexpr int NQ = WL / kWave;
     __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? WL : 1];
     const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
+    double pv = 0.0;  // NORM: the lane's ||w||^2 partial, issued first
+    if constexpr (NORM) pv = (int)threadIdx.x < nm.nparts ? nm.part[threadIdx.x] : 0.0;
     int b = (int)blockIdx.x, G = (int)gridDim.x;
     if (prog.count > 0) {  // the riding scalar program: workgroup 0's first wave
         if (b == 0) {
             __shared__ double plds[3 * kProgStage + 1];
+            if constexpr (NORM) (void)norm_scale(nm, pv);  // h(k+1,k) stored before the program reads it
             if (wid == 0) run_scalar_program<kProgStage>(prog, plds);
             return;
         }
         --b;
         --G;
     }
-    const int s0 = ((xcd ? xcd_block(b, G) : b) * (kBlock / kWave) + wid) * SPW;
-    if (s0 >= nslices) return;  // no workgroup barrier below
+    const int s0_raw = ((xcd ? xcd_block(b, G) : b) * (kBlock / kWave) + wid) * SPW;
+    const bool dead = s0_raw >= nslices;
+    if (!NORM && dead) return;  // no workgroup barrier below (NORM: after the partial sum)
+    const int s0 = dead ? 0 : s0_raw;
     const int row0 = s0 * kWave;
     bool live_p[SPW];
     SellRow<S, CI, W, false, BE> row[SPW];
 #pragma unroll
     for (int p = 0; p < SPW; ++p) {
-        live_p[p] = s0 + p < nslices;
-        row[p].init_uniform(live_p[p] ? s0 + p : s0, ustride, spat, coff);
+        live_p[p] = !dead && s0 + p < nslices;
+        row[p].init_uniform(s0 + p < nslices ? s0 + p : s0, ustride, spat, coff);
     }
     __builtin_amdgcn_sched_barrier(0);
     X xw[WIN ? NQ : 1];
@@ -327,10 +386,12 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv2(int n, int cols, int nsli
         }
     }
     X yi[SPW];
+    X xo[NORM && !WIN ? SPW : 1];  // NORM, no window: the lanes' own entries of w
 #pragma unroll
     for (int p = 0; p < SPW; ++p) {
         const int i = row0 + p * kWave + lane;
         yi[p] = beta != X(0) ? y[live_p[p] && i < n ? i : 0] : X(0);
+        if constexpr (NORM && !WIN) xo[p] = x[live_p[p] && i < n ? i : 0];
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -352,15 +413,28 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv2(int n, int cols, int nsli
         for (int p = 0; p < SPW; ++p) row[p].gather([&](int c) { return x[c]; }, xg[p]);
     }
     __builtin_amdgcn_sched_barrier(0);
+    X a = X(1);
+    if constexpr (NORM) {
+        a = norm_scale(nm, pv);  // (its barrier also waits for the loads above)
+        if (dead) return;
+    }
+    auto sc = [&](X v) { return NORM ? (X)(a * v) : v; };
     double sum[SPW] = {};
     if constexpr (WIN) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const int c = row0 - kWinLo + q * kWave + lane;
-            win[wid][q * kWave + lane] = (c >= 0 && c < cols) ? xw[q] : X(0);
+            win[wid][q * kWave + lane] = (c >= 0 && c < cols) ? sc(xw[q]) : X(0);
         }
         wave_lds_sync();
         auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
+        if constexpr (NORM) {
+#pragma unroll
+            for (int p = 0; p < SPW; ++p) {
+                const int i = row0 + p * kWave + lane;
+                if (live_p[p] && i < n) nm.v[i] = win[wid][i - row0 + kWinLo];
+            }
+        }
 #pragma unroll
         for (int p = 0; p < SPW; ++p) row[p].sum(0, xv, sum[p]);
 #pragma unroll
@@ -370,10 +444,17 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv2(int n, int cols, int nsli
                 row[p].sum(q, xv, sum[p]);
             }
     } else {
-        auto xv = [&](int c) { return (double)x[c]; };
+        if constexpr (NORM) {
+#pragma unroll
+            for (int p = 0; p < SPW; ++p) {
+                const int i = row0 + p * kWave + lane;
+                if (live_p[p] && i < n) nm.v[i] = sc(xo[p]);
+            }
+        }
+        auto xv = [&](int c) { return (double)sc(x[c]); };
 #pragma unroll
         for (int p = 0; p < SPW; ++p) {
-            row[p].sum_gathered(0, xg[p], [](X r) { return (double)r; }, sum[p]);
+            row[p].sum_gathered(0, xg[p], [&](X r) { return (double)sc(r); }, sum[p]);
             for (int q = row[p].U; q < row[p].steps; q += row[p].U) {
                 row[p].load(q);
                 row[p].sum(q, xv, sum[p]);
@@ -809,12 +890,15 @@ struct mpg_sell {
 
 namespace {
 
-template <class X, class St>
+template <class X, class St, bool NORM = false>
 int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y,
-                   const ScalarProgram& prog = ScalarProgram{}) {
+                   const ScalarProgram& prog = ScalarProgram{}, const NormArgs<X>& nm = NormArgs<X>{}) {
     if (!ctx || !A) return MPG_ERR_ARG;
     const SellCopy& S = A->S;
-    if (S.nslices == 0) return prog.count > 0 ? mpg_scalar_program(ctx, prog.ops, prog.count) : MPG_OK;
+    if (S.nslices == 0) {
+        if (NORM) return MPG_ERR_ARG;
+        return prog.count > 0 ? mpg_scalar_program(ctx, prog.ops, prog.count) : MPG_OK;
+    }
     const int grid = (S.nslices + kBlock / kWave - 1) / (kBlock / kWave) + (prog.count > 0 ? 1 : 0);
     const int be = sell_uniform(S) ? sell_pair(S) : 0;
     int st = sell_dispatch(S, [&](auto ci, auto wc) {
@@ -830,21 +914,22 @@ int sell_spmv_impl(mpg_ctx* ctx, mpg_sell* A, X alpha, const X* x, X beta, X* y,
                     kern<<<grid2, kBlock, 0, ctx->stream>>>(
                         S.n, A->cols, S.nslices, static_cast<const int16_t*>(S.col), static_cast<const St*>(S.val),
                         S.sbase, S.spat, S.coff, static_cast<const int16_t*>(S.pat), x, alpha, beta, y, S.ustride,
-                        sell_xcd_order(S) ? 1 : 0, prog);
+                        sell_xcd_order(S) ? 1 : 0, prog, nm);
                     return (int)MPG_OK;
                 };
-                if (be == 8) return go2(k_sell_spmv2<X, St, Wc, WN, 8>);
-                if constexpr (Wc == 2) if (be == 10) return go2(k_sell_spmv2<X, St, Wc, WN, 10>);
-                if (be == 12) return go2(k_sell_spmv2<X, St, Wc, WN, 12>);
+                if (be == 8) return go2(k_sell_spmv2<X, St, Wc, WN, 8, NORM>);
+                if constexpr (Wc == 2) if (be == 10) return go2(k_sell_spmv2<X, St, Wc, WN, 10, NORM>);
+                if (be == 12) return go2(k_sell_spmv2<X, St, Wc, WN, 12, NORM>);
             }
             auto go = [&](auto kern) {
                 kern<<<grid, kBlock, 0, ctx->stream>>>(
                     S.n, A->cols, S.nslices, S.off, static_cast<const CI*>(S.col), static_cast<const St*>(S.val),
                     S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol, static_cast<const St*>(S.xval), x,
-                    alpha, beta, y, S.ustride, sell_xcd_order(S) ? 1 : 0, prog, S.rows);
+                    alpha, beta, y, S.ustride, sell_xcd_order(S) ? 1 : 0, prog, S.rows, nm);
                 return (int)MPG_OK;
             };
-            return sell_uniform(S) ? go(k_sell_spmv<X, St, CI, Wc, WN, true>) : go(k_sell_spmv<X, St, CI, Wc, WN, false>);
+            return sell_uniform(S) ? go(k_sell_spmv<X, St, CI, Wc, WN, true, NORM>)
+                                   : go(k_sell_spmv<X, St, CI, Wc, WN, false, NORM>);
         });
     });
     if (st) return st;
@@ -926,6 +1011,36 @@ int mpg_sell_spmv_prog_f32(mpg_ctx_t c, mpg_sell_t A, float alpha, const float* 
     ScalarProgram prog;
     if ((A && A->S.vtype != MPG_F32) || make_scalar_program(ops, nops, prog) != MPG_OK) return MPG_ERR_ARG;
     return sell_spmv_impl<float, float>(c, A, alpha, x, beta, y, prog);
+}
+
+}  // extern "C"
+
+namespace {
+template <class X, int VT>
+int sell_spmv_norm(mpg_ctx* c, mpg_sell* A, int32_t nparts, X* h, const X* w, X* v, X alpha, X* y,
+                   const mpg_scalar_op* ops, int32_t nops) {
+    ScalarProgram prog;
+    if (!c || !A || A->S.vtype != VT || !h || !w || !v || !y || nparts < 1 || nparts > kBlock || A->cols != A->S.n ||
+        make_scalar_program(ops, nops, prog) != MPG_OK)
+        return MPG_ERR_ARG;
+    NormArgs<X> nm;
+    nm.part = c->red_ws;
+    nm.nparts = nparts;
+    nm.h = h;
+    nm.v = v;
+    return sell_spmv_impl<X, X, true>(c, A, alpha, w, X(0), y, prog, nm);
+}
+}  // namespace
+
+extern "C" {
+
+int mpg_sell_spmv_norm_f64(mpg_ctx_t c, mpg_sell_t A, int32_t nparts, double* h, const double* w, double* v,
+                           double alpha, double* y, const mpg_scalar_op* ops, int32_t nops) {
+    return sell_spmv_norm<double, MPG_F64>(c, A, nparts, h, w, v, alpha, y, ops, nops);
+}
+int mpg_sell_spmv_norm_f32(mpg_ctx_t c, mpg_sell_t A, int32_t nparts, float* h, const float* w, float* v,
+                           float alpha, float* y, const mpg_scalar_op* ops, int32_t nops) {
+    return sell_spmv_norm<float, MPG_F32>(c, A, nparts, h, w, v, alpha, y, ops, nops);
 }
 
 }  // extern "C"

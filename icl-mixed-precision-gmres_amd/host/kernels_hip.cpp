@@ -8,6 +8,8 @@
 // the device (device pointer mode, kernels_cuda.cpp:142-150).
 #include "types_hip.hpp"
 
+#include <hip/hip_runtime_api.h>
+
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -127,9 +129,10 @@ thread_local PendingReduction tl_red;
 
 // MPG_SURFACE_FUSE: a bit mask of the fused pairs (1 nrm2 -> scal_recip,
 // 2 dot -> naxpy, 4 gemv^T -> gemv, 8 gemv -> nrm2: the CGS update emits
-// the ||w||^2 partials that the nrm2 of add_vector would compute, below);
-// unset: kFuseDefault; 0: none
-constexpr int kFuseDefault = 1 | 4 | 8;
+// the ||w||^2 partials that the nrm2 of add_vector would compute, below;
+// 16 scal_recip -> spmv: add_vector's normalisation rides the next SELL
+// SpMV, below); unset: kFuseDefault; 0: none
+constexpr int kFuseDefault = 1 | 4 | 8 | 16;
 
 // The ||y||^2 stage-1 partials a fused CGS gemv (mpg_gemv_n_from_t_nrm2_*)
 // left in the context workspace: an nrm2 of exactly that y as the very
@@ -149,6 +152,93 @@ bool fuse_enabled(int bit) {
     const int mask = env && *env ? std::atoi(env) : kFuseDefault;
     return (mask & bit) != 0;
 }
+}  // namespace
+
+// ---- add_vector's normalisation riding the next SpMV (round 5, bit 16) ----
+// The CGS step of the reference (Orthogonalization.hpp:51-89, then
+// gmres.cpp:213) is: gemv^T, gemv (w -= V h), nrm2(w) -> h(k+1,k),
+// scal_recip -> V(:,k+1), Givens (scalar ops), spmv(A, V(:,k+1), w). The
+// normalisation cannot ride that SpMV in place: the SpMV overwrites w while
+// its other workgroups still gather w's neighbours. So the fused gemv writes
+// w's new value to a scratch copy (the "redirect": w's value lives there),
+// the nrm2 keeps its partials (NormMemo), the scal_recip is deferred, and the
+// SpMV forms h, V(:,k+1) = T(1/h) w and A V(:,k+1) -> w in one launch
+// (mpg_sell_spmv_norm_*, the same bits as the separate launches). Any other
+// call through current_ctx() first issues what is deferred as the separate
+// launches would have (scal_recip from the copy, then the copy back into
+// w), so the semantics never change. tl_ride_score turns the redirect off on
+// a context where the pattern keeps failing (CGSR's second pass reads w
+// before the SpMV: two failures in a row switch it off; CGS fails only at the
+// last step of a cycle).
+namespace {
+struct Redirect {
+    mpg_ctx_t ctx = nullptr;
+    void* w = nullptr;  // the caller's w (nullptr: no redirect)
+    void* s = nullptr;  // the scratch copy holding w's value
+    int64_t n = 0;
+    bool f64 = false;
+};
+thread_local Redirect tl_redir;
+struct DeferredNorm {
+    bool on = false;
+    mpg_ctx_t ctx = nullptr;
+    bool f64 = false;
+    int32_t nparts = 0;
+    void* h = nullptr;    // h(k+1,k)
+    void* dst = nullptr;  // V(:,k+1)
+    int64_t n = 0;
+};
+thread_local DeferredNorm tl_dnorm;
+thread_local int tl_ride_score = 2;
+struct Scratch {
+    mpg_ctx_t ctx = nullptr;
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+thread_local Scratch tl_scratch;
+thread_local int64_t tl_ride_counts[3] = {0, 0, 0};  // redirects, rides, flushed
+
+// the scratch copy for w (kept per thread and context; never (re)allocated
+// while the context's stream records a cycle program)
+void* ride_scratch(mpg_ctx_t c, size_t bytes) {
+    if (tl_scratch.p && tl_scratch.ctx == c && tl_scratch.bytes >= bytes) return tl_scratch.p;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(static_cast<hipStream_t>(mpg_ctx_stream(c)), &cs) != hipSuccess ||
+        cs != hipStreamCaptureStatusNone)
+        return nullptr;
+    if (tl_scratch.p) (void)mpg_free(tl_scratch.ctx == c ? c : nullptr, tl_scratch.p);
+    tl_scratch = Scratch{};
+    void* p = nullptr;
+    if (mpg_malloc(c, bytes, &p) != MPG_OK) return nullptr;
+    tl_scratch = Scratch{c, p, bytes};
+    return p;
+}
+}  // namespace
+
+// issue what the ride deferred, as the separate calls would have
+void flush_ride() {
+    if (tl_dnorm.on) {
+        const DeferredNorm d = tl_dnorm;
+        tl_dnorm.on = false;
+        const int st = d.f64 ? mpg_scal_recip_nrm2_f64(d.ctx, d.nparts, (double*)d.h, d.n, (const double*)tl_redir.s,
+                                                       (double*)d.dst)
+                             : mpg_scal_recip_nrm2_f32(d.ctx, d.nparts, (float*)d.h, d.n, (const float*)tl_redir.s,
+                                                       (float*)d.dst);
+        check(st, "scal_recip (deferred)", d.ctx);
+    }
+    if (tl_redir.w) {
+        const Redirect r = tl_redir;
+        tl_redir.w = nullptr;
+        const int st = r.f64 ? mpg_copy_f64f64(r.ctx, r.n, (const double*)r.s, (double*)r.w)
+                             : mpg_copy_f32f32(r.ctx, r.n, (const float*)r.s, (float*)r.w);
+        check(st, "copy (redirected w)", r.ctx);
+        --tl_ride_score;
+        ++tl_ride_counts[2];
+    }
+}
+
+namespace {
+bool ride_enabled() { return fuse_enabled(16) && tl_ride_score > 0; }
 }  // namespace
 
 void flush_pending_reduction() {
@@ -171,6 +261,8 @@ void flush_pending_reduction() {
 void discard_pending_reduction() {
     tl_red.kind = 0;
     tl_norm.y = nullptr;
+    tl_dnorm.on = false;
+    tl_redir.w = nullptr;
 }
 
 // An elementwise call that writes none of the memo's y and runs no
@@ -206,6 +298,7 @@ static const PendingReduction* take_pending(int kind, bool f64, const void* resu
 }
 
 void flush_scalar_ops() {
+    flush_ride();  // a queued program may read the h a deferred normalisation forms
     if (tl_nops == 0) return;
     const int n = tl_nops;
     tl_nops = 0;
@@ -260,8 +353,37 @@ mpg_ctx_t take_scalar_ops_for(const void* x, size_t xbytes, const void* y, size_
     return tl_ops_ctx;
 }
 
+// add_vector's deferred normalisation and the next SpMV, on the SELL copy:
+// when the SpMV is exactly spmv(A, V(:,k+1), w) for the deferred
+// scal_recip's V(:,k+1) and the redirected w, take it (with the queued
+// Givens program to ride workgroup 0 when none of its cells overlaps x or y;
+// a program that would not ride makes everything issue separately). Returns
+// true with the ride's context, nparts, h and the scratch copy.
+bool take_ride(const void* x, const void* y, int64_t n, bool f64, mpg_scalar_op* ops, int& nops, mpg_ctx_t& c,
+               int32_t& nparts, void*& h, const void*& w) {
+    nops = 0;
+    if (!tl_dnorm.on || !tl_redir.w || tl_dnorm.dst != x || tl_redir.w != y || tl_dnorm.n != n ||
+        tl_redir.n != n || tl_dnorm.f64 != f64 || tl_redir.f64 != f64 || tl_dnorm.ctx != ctx_no_flush() ||
+        tl_redir.ctx != tl_dnorm.ctx || tl_red.kind)
+        return false;
+    if (tl_nops) {
+        mpg_ctx_t oc = take_scalar_ops_for(x, (size_t)n * (f64 ? 8 : 4), y, (size_t)n * (f64 ? 8 : 4), ops, nops);
+        if (!nops || oc != tl_dnorm.ctx) return false;  // (current_ctx() issued everything: no ride)
+    }
+    c = tl_dnorm.ctx;
+    nparts = tl_dnorm.nparts;
+    h = tl_dnorm.h;
+    w = tl_redir.s;
+    tl_dnorm.on = false;
+    tl_redir.w = nullptr;
+    tl_ride_score = std::min(tl_ride_score + 1, 8);
+    ++tl_ride_counts[1];
+    return true;
+}
+
 mpg_ctx_t current_ctx() {
     tl_norm.y = nullptr;
+    flush_ride();
     if (tl_nops) flush_scalar_ops();
     if (tl_red.kind) flush_pending_reduction();
     return ctx_no_flush();
@@ -269,6 +391,7 @@ mpg_ctx_t current_ctx() {
 
 ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) {
     tl_norm.y = nullptr;
+    flush_ride();
     if (tl_nops) flush_scalar_ops();
     if (tl_red.kind) flush_pending_reduction();
     tl_ctx = ctx;
@@ -277,6 +400,10 @@ ScopedContext::~ScopedContext() {
     // the queue and a pending stage 2 belong to this scope's context; a
     // failure here has already been reported by the call that follows it,
     // or the scope is unwinding
+    try {
+        flush_ride();
+    } catch (...) {
+    }
     if (tl_nops) {
         const int n = tl_nops;
         tl_nops = 0;
@@ -537,6 +664,8 @@ template <> void scal<float, Hip>(Scalar<float, Hip> a, Scalar<float, Hip> x, Sc
 template <> void scal_recip<double, Hip>(Scalar<double, Hip> a, Vect<double, Hip> x, Vect<double, Hip> y) {
     assert(x.n() == y.n());
     if (const auto* p = mpg::take_pending(1, true, a.data())) {
+        // x's value in the redirect's copy: deferred to ride the next SpMV
+        if (mpg::defer_norm(p->ctx, p->nparts, a.data(), x.data(), y.data(), (int64_t)x.n(), true)) return;
         check(mpg_scal_recip_nrm2_f64(p->ctx, p->nparts, a.data(), x.n(), x.data(), y.data()), "scal_recip (nrm2)",
               p->ctx);
         return;
@@ -546,11 +675,43 @@ template <> void scal_recip<double, Hip>(Scalar<double, Hip> a, Vect<double, Hip
 template <> void scal_recip<float, Hip>(Scalar<float, Hip> a, Vect<float, Hip> x, Vect<float, Hip> y) {
     assert(x.n() == y.n());
     if (const auto* p = mpg::take_pending(1, false, a.data())) {
+        // x's value in the redirect's copy: deferred to ride the next SpMV
+        if (mpg::defer_norm(p->ctx, p->nparts, a.data(), x.data(), y.data(), (int64_t)x.n(), false)) return;
         check(mpg_scal_recip_nrm2_f32(p->ctx, p->nparts, a.data(), x.n(), x.data(), y.data()), "scal_recip (nrm2)",
               p->ctx);
         return;
     }
     check(mpg_scal_recip_copy_dev_f32(C, x.n(), a.data(), x.data(), y.data()), "scal_recip");
+}
+
+namespace mpg {
+// add_vector's scal_recip(h, w, V(:,k+1)) when w is redirected and its
+// nrm2 partials are pending: recorded, to ride the next SpMV
+bool defer_norm(mpg_ctx_t c, int32_t nparts, void* h, const void* x, void* y, int64_t n, bool f64) {
+    if (!tl_redir.w || tl_redir.w != x || tl_redir.n != n || tl_redir.f64 != f64 || tl_redir.ctx != c ||
+        tl_dnorm.on)
+        return false;
+    tl_dnorm = DeferredNorm{true, c, f64, nparts, h, y, n};
+    return true;
+}
+// the fused CGS gemv's output buffer: the scratch copy (and the redirect
+// recorded) when the ride is on, else y itself
+void* redirect_target(mpg_ctx_t c, void* y, int64_t n, bool f64) {
+    if (!ride_enabled() || tl_redir.w || tl_dnorm.on || n < 1) return y;
+    void* sp = ride_scratch(c, (size_t)n * (f64 ? 8 : 4));
+    return sp ? sp : y;
+}
+void set_redirect(mpg_ctx_t c, void* w, void* sp, int64_t n, bool f64) {
+    tl_redir = Redirect{c, w, sp, n, f64};
+    ++tl_ride_counts[0];
+}
+}  // namespace mpg
+
+extern "C" int mpg_surface_ride_counts(int64_t* redirects, int64_t* rides, int64_t* flushed) {
+    if (redirects) *redirects = mpg::tl_ride_counts[0];
+    if (rides) *rides = mpg::tl_ride_counts[1];
+    if (flushed) *flushed = mpg::tl_ride_counts[2];
+    return MPG_OK;
 }
 
 // ---------------- fill ----------------
@@ -612,7 +773,15 @@ template <> void gemv<double, Hip>(double alpha, MultiVect<double, Hip> A, Vect<
         if (const auto* p = mpg::take_pending(3, true, x.data())) {
             const bool emit = mpg::fuse_enabled(8) && mpg::fuse_enabled(1) && y.n() > 0;
             int32_t nnp = 0;
+            // the ride (bit 16): w's new value into the scratch copy
+            double* out = emit && A.nrows_base() == (int64_t)y.n()
+                           ? static_cast<double*>(mpg::redirect_target(p->ctx, y.data(), (int64_t)y.n(), true))
+                           : y.data();
             const int st = p->cols != (int64_t)x.n() ? MPG_ERR_UNSUPPORTED
+                           : out != y.data()
+                               ? mpg_gemv_n_from_t_nrm2_out_f64(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
+                                                                  A.stride(), p->nparts, (double)p->alpha, x.data(), beta,
+                                                                  y.data(), out, &nnp)
                            : emit ? mpg_gemv_n_from_t_nrm2_f64(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
                                                                  A.stride(), p->nparts, (double)p->alpha, x.data(), beta,
                                                                  y.data(), &nnp)
@@ -621,6 +790,7 @@ template <> void gemv<double, Hip>(double alpha, MultiVect<double, Hip> A, Vect<
             if (st == MPG_OK) {
                 if (emit && A.nrows_base() == (int64_t)y.n())
                     mpg::tl_norm = mpg::NormMemo{p->ctx, y.data(), (int64_t)y.n(), true, nnp};
+                if (out != y.data()) mpg::set_redirect(p->ctx, y.data(), out, (int64_t)y.n(), true);
                 return;
             }
             if (st != MPG_ERR_UNSUPPORTED) check(st, "gemv (gemv^T)", p->ctx);
@@ -649,7 +819,15 @@ template <> void gemv<float, Hip>(float alpha, MultiVect<float, Hip> A, Vect<flo
         if (const auto* p = mpg::take_pending(3, false, x.data())) {
             const bool emit = mpg::fuse_enabled(8) && mpg::fuse_enabled(1) && y.n() > 0;
             int32_t nnp = 0;
+            // the ride (bit 16): w's new value into the scratch copy
+            float* out = emit && A.nrows_base() == (int64_t)y.n()
+                           ? static_cast<float*>(mpg::redirect_target(p->ctx, y.data(), (int64_t)y.n(), false))
+                           : y.data();
             const int st = p->cols != (int64_t)x.n() ? MPG_ERR_UNSUPPORTED
+                           : out != y.data()
+                               ? mpg_gemv_n_from_t_nrm2_out_f32(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
+                                                                  A.stride(), p->nparts, (float)p->alpha, x.data(), beta,
+                                                                  y.data(), out, &nnp)
                            : emit ? mpg_gemv_n_from_t_nrm2_f32(p->ctx, A.nrows_base(), A.ncols_base(), alpha, A.data(),
                                                                  A.stride(), p->nparts, (float)p->alpha, x.data(), beta,
                                                                  y.data(), &nnp)
@@ -658,6 +836,7 @@ template <> void gemv<float, Hip>(float alpha, MultiVect<float, Hip> A, Vect<flo
             if (st == MPG_OK) {
                 if (emit && A.nrows_base() == (int64_t)y.n())
                     mpg::tl_norm = mpg::NormMemo{p->ctx, y.data(), (int64_t)y.n(), false, nnp};
+                if (out != y.data()) mpg::set_redirect(p->ctx, y.data(), out, (int64_t)y.n(), false);
                 return;
             }
             if (st != MPG_ERR_UNSUPPORTED) check(st, "gemv (gemv^T)", p->ctx);
@@ -701,7 +880,19 @@ template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Ve
     if (mpg_sell_t s = A.sell()) {
         mpg_scalar_op ops[MPG_SCALAR_PROGRAM_MAX];
         int nops = 0;
-        mpg_ctx_t c = mpg::take_scalar_ops_for(x.data(), x.n() * 8, y.data(), y.n() * 8, ops, nops);
+        mpg_ctx_t c = nullptr;
+        int32_t np = 0;
+        void* h = nullptr;
+        const void* w = nullptr;
+        if (beta == double(0) && x.n() == y.n() &&
+            mpg::take_ride(x.data(), y.data(), (int64_t)x.n(), true, ops, nops, c, np, h, w)) {
+            // add_vector's normalisation and the Givens program ride this SpMV
+            check(mpg_sell_spmv_norm_f64(c, s, np, static_cast<double*>(h), static_cast<const double*>(w), x.data(), alpha,
+                                         y.data(), ops, nops),
+                  "spmv (normalising)", c);
+            return;
+        }
+        c = mpg::take_scalar_ops_for(x.data(), x.n() * 8, y.data(), y.n() * 8, ops, nops);
         check(nops ? mpg_sell_spmv_prog_f64(c, s, alpha, x.data(), beta, y.data(), ops, nops)
                    : mpg_sell_spmv_f64(c, s, alpha, x.data(), beta, y.data()),
               "spmv");
@@ -716,7 +907,19 @@ template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<
     if (mpg_sell_t s = A.sell()) {
         mpg_scalar_op ops[MPG_SCALAR_PROGRAM_MAX];
         int nops = 0;
-        mpg_ctx_t c = mpg::take_scalar_ops_for(x.data(), x.n() * 4, y.data(), y.n() * 4, ops, nops);
+        mpg_ctx_t c = nullptr;
+        int32_t np = 0;
+        void* h = nullptr;
+        const void* w = nullptr;
+        if (beta == float(0) && x.n() == y.n() &&
+            mpg::take_ride(x.data(), y.data(), (int64_t)x.n(), false, ops, nops, c, np, h, w)) {
+            // add_vector's normalisation and the Givens program ride this SpMV
+            check(mpg_sell_spmv_norm_f32(c, s, np, static_cast<float*>(h), static_cast<const float*>(w), x.data(), alpha,
+                                         y.data(), ops, nops),
+                  "spmv (normalising)", c);
+            return;
+        }
+        c = mpg::take_scalar_ops_for(x.data(), x.n() * 4, y.data(), y.n() * 4, ops, nops);
         check(nops ? mpg_sell_spmv_prog_f32(c, s, alpha, x.data(), beta, y.data(), ops, nops)
                    : mpg_sell_spmv_f32(c, s, alpha, x.data(), beta, y.data()),
               "spmv");

@@ -36,8 +36,17 @@ void no_recording(const char* what);
 void flush_scalar_ops();
 void discard_scalar_ops();
 // a reduction's pending stage 2 (kernels_hip.cpp): issue it now / drop it
+// (dropping also drops a deferred normalisation and w's redirect)
 void flush_pending_reduction();
 void discard_pending_reduction();
+// add_vector's normalisation deferred to ride the next SpMV (kernels_hip.cpp,
+// MPG_SURFACE_FUSE bit 16): issue it now as the separate calls would have
+void flush_ride();
+bool defer_norm(mpg_ctx_t c, int32_t nparts, void* h, const void* x, void* y, int64_t n, bool f64);
+void* redirect_target(mpg_ctx_t c, void* y, int64_t n, bool f64);
+void set_redirect(mpg_ctx_t c, void* w, void* sp, int64_t n, bool f64);
+bool take_ride(const void* x, const void* y, int64_t n, bool f64, mpg_scalar_op* ops, int& nops, mpg_ctx_t& c,
+               int32_t& nparts, void*& h, const void*& w);
 
 // The calling thread's current HIP context (stream + workspace). Created
 // lazily on the device named by MPG_DEVICE (default 0) unless a
@@ -144,7 +153,7 @@ public:
         bool ok = true;
         try {
             steps();
-            flush_scalar_ops();
+            flush_scalar_ops();  // (issues a deferred normalisation first)
             flush_pending_reduction();
         } catch (const StatusError&) {
             // a step that cannot be recorded: end the recording and run eagerly

@@ -247,6 +247,16 @@ int mpg_gemv_n_from_t_nrm2_f64(mpg_ctx_t ctx, int64_t rows, int64_t cols, double
                                int32_t nparts, double alpha_t, double* x, double beta, double* y, int32_t* norm_nparts);
 int mpg_gemv_n_from_t_nrm2_f32(mpg_ctx_t ctx, int64_t rows, int64_t cols, float alpha, const float* A, int64_t lda,
                                int32_t nparts, float alpha_t, float* x, float beta, float* y, int32_t* norm_nparts);
+/* the same with the result written to y_out (16-B aligned, not overlapping y)
+ * instead of y: y_out = alpha*T(A x) + beta*y (round 5: the operator surface
+ * keeps w's new value apart until the normalisation that rides the next
+ * SpMV has read it, mpg_sell_spmv_norm_*) */
+int mpg_gemv_n_from_t_nrm2_out_f64(mpg_ctx_t ctx, int64_t rows, int64_t cols, double alpha, const double* A,
+                                   int64_t lda, int32_t nparts, double alpha_t, double* x, double beta,
+                                   const double* y, double* y_out, int32_t* norm_nparts);
+int mpg_gemv_n_from_t_nrm2_out_f32(mpg_ctx_t ctx, int64_t rows, int64_t cols, float alpha, const float* A,
+                                   int64_t lda, int32_t nparts, float alpha_t, float* x, float beta, const float* y,
+                                   float* y_out, int32_t* norm_nparts);
 /* triangular solve, non-unit diagonal, single workgroup (n <= 4096).
  * upper = 1 'U', 0 'L'; trans = 1 solves with A^T (kernels_mkl.cpp:291-321) */
 int mpg_trsv_f64(mpg_ctx_t ctx, int upper, int trans, int64_t n, const double* A, int64_t lda, double* x);
@@ -328,6 +338,19 @@ int mpg_sell_spmv_prog_f64(mpg_ctx_t ctx, mpg_sell_t A, double alpha, const doub
                            const mpg_scalar_op* ops, int32_t nops);
 int mpg_sell_spmv_prog_f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y,
                            const mpg_scalar_op* ops, int32_t nops);
+/* add_vector's normalisation riding the next Arnoldi SpMV (round 5; the
+ * operator surface's CGS step, Orthogonalization.hpp:51-60 then the next
+ * spmv(A, V(:,k+1), w), gmres.cpp:213). The context workspace holds the
+ * nparts (<= 256) ||w||^2 stage-1 partials of w (mpg_gemv_n_from_t_nrm2_*'s);
+ * in one launch: h = T(sqrt(sum)) (stored to *h, before the riding scalar
+ * program runs), v = T(T(1)/h * w) for every row (scal_recip's two
+ * roundings), y = alpha * T(A v). w and y must not overlap (y is the
+ * caller's w, w a copy of it: mpg_gemv_n_from_t_nrm2_out_*); A square. The
+ * same bits as mpg_scal_recip_nrm2_* followed by mpg_sell_spmv_prog_*. */
+int mpg_sell_spmv_norm_f64(mpg_ctx_t ctx, mpg_sell_t A, int32_t nparts, double* h, const double* w, double* v,
+                           double alpha, double* y, const mpg_scalar_op* ops, int32_t nops);
+int mpg_sell_spmv_norm_f32(mpg_ctx_t ctx, mpg_sell_t A, int32_t nparts, float* h, const float* w, float* v,
+                           float alpha, float* y, const mpg_scalar_op* ops, int32_t nops);
 
 /* A^T as its own CSR (SparseMatrix::set_transpose, types_cuda.hpp:145-151;
  * cusparse?csrmv TRANSPOSE, kernels_cuda.cpp:588-596; condest.cpp:49-50).

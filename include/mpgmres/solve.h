@@ -187,6 +187,12 @@ int mpg_engine_destroy(mpg_engine_t e);
  * replayed from one, and recordings voided by a step that must read the
  * device (those cycles then run eagerly). Any pointer may be NULL. */
 int mpg_cycle_program_counts(int64_t* recorded, int64_t* replayed, int64_t* voided);
+/* the calling thread's counts of the operator surface's normalisation ride
+ * (kernels_hip.cpp, MPG_SURFACE_FUSE bit 16): CGS updates that kept w's new
+ * value apart, normalisations that rode the next SpMV, and those issued
+ * separately instead (a call other than the SpMV came next). Any pointer
+ * may be NULL. */
+int mpg_surface_ride_counts(int64_t* redirects, int64_t* rides, int64_t* flushed);
 
 #ifdef __cplusplus
 }

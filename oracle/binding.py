@@ -11,11 +11,15 @@ import numpy as np
 ORACLE_DIR = Path(__file__).resolve().parent
 # MKL's conditional numerical reproducibility: one code branch on every host
 # (read by MKL at its first call, so set before the library is used). Without
-# it MKL picks its branch by CPU -- AVX-512 on the build container's Xeon, a
+# it MKL picks its branch by CPU -- AVX-512 on the build container's Xeon, its
 # generic branch on the GPU box's EPYC -- and the fp32 sums of a large solve
-# differ between the two (tests/parity.py, tools/oracle_cnr.py). AVX2 runs on
-# both. The CPU baseline in bench.py runs on the same branch.
-os.environ.setdefault("MKL_CBWR", "AVX2")
+# differ between the two. COMPATIBLE is the branch MKL 2021.4 runs on the
+# EPYC whatever is asked (a request for AVX2 there reports branch AUTO and
+# gives COMPATIBLE's bits), so it is the one branch both hosts run: the
+# oracle's results are bit-identical on the Xeon and the EPYC at 1, 4 and 8
+# threads (tools/oracle_cnr.py, profiles/r05_oracle_cnr/). The CPU baseline in
+# bench.py runs on it too -- the branch MKL already ran on the box.
+os.environ.setdefault("MKL_CBWR", "COMPATIBLE")
 # MPG_ORACLE_LIB: the ASan/UBSan build of the same sources (make -C oracle sanitize)
 LIB = Path(os.environ["MPG_ORACLE_LIB"]) if os.environ.get("MPG_ORACLE_LIB") else ORACLE_DIR / "_build" / "liboracle.so"
 
@@ -63,6 +67,18 @@ def lib() -> C.CDLL:
     return _lib
 
 
+_DEFAULT_THREADS = None
+
+
+def default_threads() -> int:
+    """MKL's thread count when the oracle was first loaded (OMP_NUM_THREADS,
+    else the host's), the count of every solve that names none."""
+    global _DEFAULT_THREADS
+    if _DEFAULT_THREADS is None:
+        _DEFAULT_THREADS = max(1, int(lib().oracle_max_threads()))
+    return _DEFAULT_THREADS
+
+
 def cbwr() -> str:
     """The MKL code branch the oracle runs ("AVX2" when pinned; "auto" when
     MKL picks by CPU; "" without MKL)."""
@@ -88,6 +104,10 @@ def solve(mpg, A, b, x_true=None, backend=None, **opts):
     fp32 in an order that depends on the CPU and its thread count)."""
     opts = dict(opts)
     opts.pop("engine", None)
+    # MKL keeps the last thread count it was given: a solve without one runs
+    # on the process's initial count, whatever ran before (tests' order)
+    if not opts.get("threads"):
+        opts["threads"] = default_threads()
     args, keep = mpg.make_args(A, b, x_true, **opts)
     fn = lib().oracle_solve
     fn.argtypes = [C.POINTER(type(args)), C.POINTER(mpg.SolveResult)]

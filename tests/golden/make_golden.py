@@ -5,11 +5,11 @@ this path and cannot be built here (Kokkos 3.1 and MKL headers are absent),
 so the fixtures are produced by the oracle (oracle/cpu_gmres.cpp: the
 reference's algorithm restated over the MKL 2021.4 runtime the image ships)
 after it has been cross-checked against the independent NumPy restatement
-(oracle/gmres_np.py; tests/test_oracle.py). Single MKL thread on MKL's AVX2
-code branch (MKL_CBWR=AVX2, which oracle/binding.py pins: conditional
-numerical reproducibility), so the values are reproducible on any AVX2 host,
-not only this machine (round 5; the round-1..4 records came from MKL's
-default branch, AVX-512 on the build container).
+(oracle/gmres_np.py; tests/test_oracle.py). Single MKL thread on MKL's
+COMPATIBLE code branch (MKL_CBWR, which oracle/binding.py pins: conditional
+numerical reproducibility), so the values are reproducible on the GPU box's
+EPYC as on this Xeon, not only on this machine (round 5; the round-1..4
+records came from MKL's default branch, AVX-512 on the build container).
 
 Inputs are deterministic: lap10 (7-point Laplacian 10^3), band2000 (the
 BAND generator, n=2000, offsets -5..+4, seed 7), convdiff32 (2-D upwind

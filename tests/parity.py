@@ -40,21 +40,23 @@ preconditioner every step (modes mixed, single, mixed-half, single-prec):
   * when converged, the final backward error is <= tol.
 Live-oracle comparisons of fp32 Arnoldi on large inputs (compare_mkl, round
 5) compare with the MKL oracle two-sidedly. The oracle's MKL is pinned to one
-code branch (MKL_CBWR=AVX2, set by oracle/binding.py: conditional numerical
-reproducibility) and run at fixed thread counts (MKL_THREADS), so its bits
-no longer depend on the host CPU: round 4 had seen its cycle-1 backward
-error move 3-12x between this container (AVX-512 branch) and the GPU box
-(EPYC: MKL's generic branch) -- profiles/r04_oracle_backends.txt,
-profiles/r05_oracle_cnr/. MKL's fp32 sgemv/sparse mv still sum in fp32 in
-an order that depends on the thread count, which moves the cycle >= 1
-backward error of a large fp32 solve by up to ~3.5x between thread counts
-on one host, while the HIP kernels sum in fp64 (more accurately than any
-of them). So each cycle's backward error must lie inside the envelope of
-the MKL runs at those thread counts widened by the factor 3 of the rule
-above ([min/3, 3 max]); everything else follows compare() against the
-1-thread run (the reference's serial arithmetic). The oracle's loop kernels
-(fp32 products summed in fp64 in index order, the HIP kernels' summation
-class) stay a diagnostic (tools/oracle_cnr.py).
+code branch (MKL_CBWR=COMPATIBLE, set by oracle/binding.py: conditional
+numerical reproducibility) and run at fixed thread counts (MKL_THREADS), so
+its bits no longer depend on the host: the same digests on the build
+container's Xeon and the GPU box's EPYC at 1, 4 and 8 threads
+(profiles/r05_oracle_cnr/; round 4 had seen its cycle-1 backward error move
+3-12x between the two, profiles/r04_oracle_backends.txt). What CNR does not
+remove is the accuracy class: MKL's fp32 sgemv sums in fp32, so with plain
+CGS (one orthogonalisation pass) a large fp32 solve loses orthogonality
+faster than the HIP kernels, which sum in fp64 -- BAND-300k at m = 100:
+cycle-1 backward error 6.0e-9 (MKL, any thread count) vs 2.4e-10 (GPU);
+with CGSR the two agree to 10 %. So each cycle's backward error must lie in
+the envelope of the kernels_mkl.cpp arithmetic evaluated by the oracle --
+MKL at each of MKL_THREADS and the oracle's loop kernels (the same
+operations with fp32 products summed in fp64 in index order) -- widened by
+the factor 3 of the rule above ([min/3, 3 max]); everything else follows
+compare() against the 1-thread MKL run (the reference's serial
+arithmetic).
 Measured margins behind these numbers: tools/parity_margins.py over the
 168 golden records on the fused and operator-surface engines
 (profiles/r02_parity_margins.txt; the x terms against e_ref alone:
@@ -172,13 +174,16 @@ def mkl_envelope_ok(refs, got, mode: str, factor: float = 3.0):
 
 def compare_mkl(oracle, mpg, A, b, xt, got, opts: dict, label: str = "", runs: dict = None):
     """Two-sided parity with the MKL oracle (module docstring): the oracle at
-    each of MKL_THREADS (pinned MKL branch), got compared with the 1-thread
-    run inside the runs' envelope. runs: a cache {threads: Result}."""
+    each of MKL_THREADS (pinned MKL branch) and on its loop kernels; got
+    compared with the 1-thread MKL run, its per-cycle backward errors inside
+    the runs' envelope. runs: a cache {threads or "loops": Result}."""
     runs = {} if runs is None else runs
     for t in MKL_THREADS:
         if t not in runs:
             runs[t] = oracle.solve(mpg, A, b, xt, backend="mkl", threads=t, **opts)
-    refs = [runs[t] for t in MKL_THREADS]
+    if "loops" not in runs:
+        runs["loops"] = oracle.solve(mpg, A, b, xt, backend="loops", threads=1, **opts)
+    refs = [runs[t] for t in MKL_THREADS] + [runs["loops"]]
     compare(as_ref(refs[0]), got, opts["mode"], opts["tol"], opts["rlen"], label, envelope=refs)
     return runs
 

@@ -448,6 +448,72 @@ def test_scalar_program_rides_sell_spmv(hip, mpg, t):
 
 
 @pytest.mark.parametrize("t", ["f64", "f32"])
+@pytest.mark.parametrize("which", ["band", "lap", "stencil27", "fem27"])
+def test_sell_spmv_norm_matches_separate_launches(hip, mpg, t, which):
+    """Round 5 (the operator surface's add_vector riding the next SpMV):
+    mpg_sell_spmv_norm_* -- h = T(sqrt(sum of the ||w||^2 partials)),
+    v = T(T(1)/h w), y = T(A v), workgroup 0 storing h before the riding
+    Givens program that reads it -- gives the bits of mpg_scal_recip_nrm2_*
+    followed by mpg_sell_spmv_prog_*, on every SELL kernel form: the
+    two-slice window kernel (BAND), the two-slice gather kernel (7-point
+    Laplacian), the stepped-int16 kernel with CSR-summed slices (27-point
+    stencil) and int32 columns (fem27 forced to SELL)."""
+    dt = np.float64 if t == "f64" else np.float32
+    CT = C.c_double if t == "f64" else C.c_float
+    vt = 0 if t == "f64" else 1
+    f64 = 1 if t == "f64" else 0
+    A = {"band": lambda: mpg.gen_band(20_000, 5, 4, seed=3), "lap": lambda: mpg.gen_laplace3d(30),
+         "stencil27": lambda: mpg.gen_stencil27(105, 3, ny=105, nz=4), "fem27": lambda: mpg.gen_spec("fem27:16:3:70:13")}[which]()
+    g = rng(23)
+    n = A.nrows
+    w = g.uniform(-1, 1, n).astype(dt)
+    k = 7
+    col0 = g.normal(size=k + 2).astype(dt)  # H(:,k); h = H(k+1,k) is written by the normalisation
+    th = g.uniform(0, 2 * np.pi, k)
+    c0, s0 = np.cos(th).astype(dt), np.sin(th).astype(dt)
+    sv0 = np.zeros(k + 2, dt)
+    sv0[k] = dt(g.normal())
+    drp, dci, dv = hip.buf(A.rowptr), hip.buf(A.col), hip.buf(A.val.astype(dt))
+    csr, sell = C.c_void_p(), C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, A.nrows, A.ncols, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    hip.check(hip.lib.mpg_sell_create(hip.ctx, csr, vt, dv.p, 2, C.byref(sell)))
+    out = {}
+    try:
+        assert sell.value
+        for how in ("ride", "apart", "ride-noprog", "apart-noprog"):
+            col, c, s, sv = hip.buf(np.append(col0, 0)), hip.buf(np.append(c0, [0, 0])), hip.buf(np.append(s0, [0, 0])), hip.buf(sv0)
+            rec = hip.buf(np.zeros(1, dt))
+            dw, dvk, dy = hip.buf(w), hip.buf(n, dt), hip.buf(np.full(n, 7.0, dt))
+            ops = (ScalarOp * 4)()
+            specs = [(2, k, [col.p, None, c.p, s.p]), (0, 0, [col.at(k), col.at(k + 1), c.at(k), s.at(k)]),
+                     (1, 0, [sv.at(k), sv.at(k + 1), c.at(k), s.at(k)]), (3, 0, [sv.at(k + 1), rec.at(0), None, None])]
+            for i, (op, kk, ps) in enumerate(specs):
+                ops[i].op, ops[i].f64, ops[i].k, ops[i].alpha = op, f64, kk, 0.0
+                for j, q in enumerate(ps):
+                    ops[i].p[j] = q.value if q is not None else None
+            nops = 0 if how.endswith("noprog") else 4
+            np_ = C.c_int32()
+            hip.call(f"mpg_nrm2_partials_{t}", C.c_int64(n), dw.p, C.byref(np_))
+            if how.startswith("ride"):
+                hip.call(f"mpg_sell_spmv_norm_{t}", sell, np_, col.at(k + 1), dw.p, dvk.p, CT(1.0), dy.p,
+                         C.cast(ops, C.c_void_p), nops)
+            else:
+                hip.call(f"mpg_scal_recip_nrm2_{t}", np_, col.at(k + 1), C.c_int64(n), dw.p, dvk.p)
+                hip.call(f"mpg_sell_spmv_prog_{t}", sell, CT(1.0), dvk.p, CT(0.0), dy.p, C.cast(ops, C.c_void_p), nops)
+            out[how] = [b.get() for b in (col, c, s, sv, rec, dvk, dy)]
+    finally:
+        hip.lib.mpg_sell_destroy(sell)
+        hip.lib.mpg_csr_destroy(csr)
+    for a, b in zip(out["ride"], out["apart"]):
+        assert np.array_equal(a, b)
+    for a, b in zip(out["ride-noprog"], out["apart-noprog"]):
+        assert np.array_equal(a, b)
+    h = np.sqrt(np.sum(w.astype(np.float64) ** 2))
+    assert abs(out["ride-noprog"][0][k + 1] - h) <= 1e-6 * h
+    assert out["ride"][4][0] != 0 and np.all(np.isfinite(out["ride"][6]))
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
 def test_split_reductions_match_one_call(hip, t):
     """Stage 1 / stage 2 split reductions and the consumers that fold stage 2
     in (the operator surface's deferred reductions) give the one-call forms'

@@ -85,11 +85,11 @@ def test_oracle_reproduces_golden(mpg, oracle):
 
 
 def test_oracle_reproduces_golden_bits(mpg, oracle):
-    """Round 5: the records were made on MKL's pinned AVX2 branch (MKL_CBWR,
-    oracle/binding.py) at one thread, so the oracle reproduces them bit for
-    bit -- here and on any AVX2 host (tools/oracle_cnr.py --golden on the GPU
-    box: profiles/r05_oracle_cnr/)."""
-    assert oracle.cbwr() == GOLDEN["mkl_cbwr"] == "AVX2"
+    """Round 5: the records were made on MKL's pinned COMPATIBLE branch
+    (MKL_CBWR, oracle/binding.py) at one thread, so the oracle reproduces
+    them bit for bit -- here and on the GPU box's EPYC (tools/oracle_cnr.py
+    --golden there: profiles/r05_oracle_cnr/)."""
+    assert oracle.cbwr() == GOLDEN["mkl_cbwr"] == "COMPATIBLE"
     mats = inputs(mpg)
     for rec in GOLDEN["cases"][::7]:
         case = dict(rec["case"])

@@ -299,6 +299,51 @@ def test_surface_cycle_program_matches_eager(mpg, orth, mode, prec, monkeypatch)
     assert p.res_norm == e.res_norm and p.err_norm == e.err_norm
 
 
+@pytest.mark.parametrize("matrix", ["band", "lap", "stencil27"])
+@pytest.mark.parametrize("orth", ["cgs", "mgs", "cgsr"])
+@pytest.mark.parametrize("mode", ["mixed", "baseline", "single"])
+@pytest.mark.parametrize("prec", ["identity", "jacobi"])
+def test_surface_normalisation_ride_same_bits(mpg, matrix, orth, mode, prec, monkeypatch):
+    """Round 5: add_vector's scal_recip rides the next SELL
+    SpMV on the operator surface (MPG_SURFACE_FUSE bit 16, default on): the
+    CGS gemv writes w's new value to a scratch copy, the SpMV forms h(k+1,k),
+    V(:,k+1) and A V(:,k+1) -> w in one launch. The solve must give the bits
+    of the same surface without the ride (bits 1|4|8) and of every call on
+    its own (0), on the two-slice window kernel (BAND), the two-slice gather
+    kernel (7-point Laplacian) and the stepped kernel with CSR-summed slices
+    (27-point, 3 dof, planes past 32767 rows); CGS must actually ride, and
+    the cycles still record and replay."""
+    A = {"band": lambda: mpg.gen_band(100_000, 5, 4, seed=7), "lap": lambda: mpg.gen_laplace3d(40),
+         "stencil27": lambda: mpg.gen_stencil27(105, 3, ny=105, nz=3)}[matrix]()
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(engine="surface", mode=mode, orth=orth, prec=prec, rlen=30, tol=0.0, max_restarts=3)
+    got = {}
+    for fuse in ("", "13", "0"):
+        if fuse:
+            monkeypatch.setenv("MPG_SURFACE_FUSE", fuse)
+        else:
+            monkeypatch.delenv("MPG_SURFACE_FUSE", raising=False)
+        before = mpg.surface_ride_counts()
+        got[fuse] = mpg.solve(A, b, xt, **opts)
+        after = mpg.surface_ride_counts()
+        delta = {k: after[k] - before[k] for k in after}
+        if fuse:
+            assert delta["redirects"] == 0 and delta["rides"] == 0, delta
+        elif orth == "cgs":
+            # every step but the last of a cycle (and the first eager cycle's
+            # first step, before the SELL copy exists) rides
+            assert delta["rides"] >= 3 * 27, delta
+        elif orth == "mgs":
+            assert delta == {"redirects": 0, "rides": 0, "flushed": 0}, delta
+    ref = got["0"]
+    for fuse in ("", "13"):
+        g = got[fuse]
+        assert g.total_iters == ref.total_iters == 90, (fuse, g.total_iters)
+        assert np.array_equal(g.step_res, ref.step_res), fuse
+        assert np.array_equal(g.x, ref.x) and g.res_norm == ref.res_norm, fuse
+
+
 @pytest.mark.parametrize("mode", ["mixed", "single"])
 @pytest.mark.parametrize("orth", ["cgs", "cgsr"])
 def test_fused_dots_strict(mpg, oracle, mode, orth, monkeypatch):
