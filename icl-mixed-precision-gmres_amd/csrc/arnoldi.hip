@@ -48,25 +48,29 @@ __device__ __forceinline__ T precond(T w, const P* __restrict__ d, int64_t i) {
 
 // This workgroup's contiguous run of row blocks [rb0, rb1) — contiguous so
 // that its rows form one range [blocks[rb0], blocks[rb1]) for the dot pass.
-__device__ __forceinline__ void my_blocks(int nblocks, int& rb0, int& rb1) {
-    rb0 = (int)((int64_t)blockIdx.x * nblocks / gridDim.x);
-    rb1 = (int)((int64_t)(blockIdx.x + 1) * nblocks / gridDim.x);
+__device__ __forceinline__ void my_blocks(int nblocks, int& rb0, int& rb1, bool xcd = false) {
+    const int b = xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    rb0 = (int)((int64_t)b * nblocks / gridDim.x);
+    rb1 = (int)((int64_t)(b + 1) * nblocks / gridDim.x);
 }
 
 // For every row of this workgroup's row blocks: fp64 sum of val * xval(col)
 // (csr_tile.hpp), then epi(row, sum) on one lane. NT: non-temporal matrix
 // loads (a pass that runs once per restart cycle).
-template <bool NT = false, class V, class XF, class PF, class EPI>
+// XCD (round 5): workgroups take their runs of row blocks in XCD order
+// (xcd_block), so each XCD's L2 holds the neighbourhood of x that its own
+// contiguous eighth of the rows gathers (the SELL kernels' placement).
+template <bool NT = false, bool XCD = false, class V, class XF, class PF, class EPI>
 __device__ __forceinline__ void for_rows(const int32_t* __restrict__ blocks, int nblocks,
                                          const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                          const V* __restrict__ val, int64_t nnz, XF xval, PF pre, EPI epi,
                                          double* prod, double* scratch) {
     const int32_t* __restrict__ bnnz = blocks + nblocks + 1;  // mpg_csr's nnz starts follow the row starts
     int rb0, rb1;
-    my_blocks(nblocks, rb0, rb1);
+    my_blocks(nblocks, rb0, rb1, XCD);
     for (int b = rb0; b < rb1; ++b)
-        csr_row_block<NT>(blocks[b], blocks[b + 1], bnnz[b], bnnz[b + 1], rowptr, col, val, nnz, xval, pre, epi, prod,
-                          scratch);
+        csr_row_block<NT>(blocks[b], blocks[b + 1], bnnz[b], bnnz[b + 1], rowptr, col, val, nnz, xval, pre, epi,
+                          prod, scratch);
 }
 
 // Combine in the last arriver: sums[c] = sum over g of partial[c*G + g] for
@@ -430,7 +434,7 @@ __device__ __forceinline__ T fold_givens(const GivensFold<T>& f, const T* __rest
 // that Givens step folded in (fold.norm2 != nullptr). The Gram-Schmidt dots
 // follow in k_panel_dots (measured: dots inside this gather-bound launch
 // cost more than the separate pass, 71 us vs 30 + 20 us on BAND-10M).
-template <class T, class P, class VI, bool FOLD>
+template <class T, class P, class VI, bool FOLD, int MODE = 0>
 __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict__ blocks, int nblocks,
                                                       const int32_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ col, const VI* __restrict__ val,
@@ -447,7 +451,8 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
         P d;
         int e;  // row exponent of a scaled fp16 copy (mpg_csr_half_values)
     };
-    for_rows(
+    // MODE bit 0: non-temporal matrix streams; bit 1: XCD-ordered row blocks
+    for_rows<(MODE & 1) != 0, (MODE & 2) != 0>(
         blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)(T)(wprev[c] * inv); },
         [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0), rexp ? (int)rexp[i] : 0}; },
         [&](int i, double sum, const Ops& o) {
@@ -1743,6 +1748,13 @@ int dispatch(int combo, F&& f) {
     }
 }
 
+// MPG_CSR_MODE (the Arnoldi CSR SpMV, k_step_spmv<..., MODE>): bit 0
+// non-temporal matrix streams, bit 1 XCD-ordered row blocks
+int csr_mode() {
+    const char* e = std::getenv("MPG_CSR_MODE");
+    return e && *e >= '0' && *e <= '3' ? *e - '0' : 0;
+}
+
 int row_grid(const mpg_arnoldi* a) { return a->G; }
 int rb_grid(const mpg_arnoldi* a) { return a->Grb; }
 
@@ -2119,7 +2131,11 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                 });
             });
         }
-        auto kern = fold ? k_step_spmv<T, P, VI, true> : k_step_spmv<T, P, VI, false>;
+        const int mode = csr_mode();
+        auto kern = mode == 1   ? (fold ? k_step_spmv<T, P, VI, true, 1> : k_step_spmv<T, P, VI, false, 1>)
+                    : mode == 2 ? (fold ? k_step_spmv<T, P, VI, true, 2> : k_step_spmv<T, P, VI, false, 2>)
+                    : mode == 3 ? (fold ? k_step_spmv<T, P, VI, true, 3> : k_step_spmv<T, P, VI, false, 3>)
+                                : (fold ? k_step_spmv<T, P, VI, true> : k_step_spmv<T, P, VI, false>);
         launch_timed(a->ctx, kern, dim3(rb_grid(a)), dim3(kBlock),
             A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,
             static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,

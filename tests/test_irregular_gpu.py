@@ -103,3 +103,22 @@ def test_irregular_spmv_forms_same_bits(mpg, problems, which):
     s = mpg.solve(A, b, xt, engine="fused", spmv_format="sell", **opts)
     c = mpg.solve(A, b, xt, engine="fused", spmv_format="csr", **opts)
     np.testing.assert_allclose(s.step_res, c.step_res, rtol=1e-4)
+
+
+@pytest.mark.parametrize("mode", ["1", "2", "3"])
+@pytest.mark.parametrize("which", ["fem27", "fem27p"])
+def test_csr_stream_modes_same_bits(mpg, which, mode, monkeypatch):
+    """The Arnoldi CSR SpMV's stream options (MPG_CSR_MODE: bit 0
+    non-temporal matrix loads, bit 1 row blocks in XCD order) load the same
+    data into the same workgroup tiles: the same bits as the default."""
+    A = mpg.gen_spec("fem27:44:3:70:13" if which == "fem27" else "fem27:44:3:70:13:64:5")
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(engine="fused", mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=2,
+                spmv_format="csr")
+    monkeypatch.setenv("MPG_CSR_MODE", "0")
+    ref = mpg.solve(A, b, xt, **opts)
+    monkeypatch.setenv("MPG_CSR_MODE", mode)
+    got = mpg.solve(A, b, xt, **opts)
+    assert np.array_equal(got.step_res, ref.step_res) and np.array_equal(got.x, ref.x)
+    assert got.res_norm == ref.res_norm
