@@ -509,7 +509,8 @@ def test_sell_spmv_norm_matches_separate_launches(hip, mpg, t, which):
     for a, b in zip(out["ride-noprog"], out["apart-noprog"]):
         assert np.array_equal(a, b)
     h = np.sqrt(np.sum(w.astype(np.float64) ** 2))
-    assert abs(out["ride-noprog"][0][k + 1] - h) <= 1e-6 * h
+    got_h = out["ride-noprog"][0][k + 1]
+    assert abs(got_h - h) <= 1e-6 * h, (got_h, h, col0, out["ride-noprog"][0], out["apart-noprog"][0])
     assert out["ride"][4][0] != 0 and np.all(np.isfinite(out["ride"][6]))
 
 
