@@ -451,9 +451,11 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
         P d;
         int e;  // row exponent of a scaled fp16 copy (mpg_csr_half_values)
     };
-    // MODE bit 0: non-temporal matrix streams; bit 1: XCD-ordered row blocks
+    // MODE bit 0: non-temporal matrix streams; bit 1: XCD-ordered row blocks;
+    // bit 2 (measurement only, wrong results): no gathers, x = 1
     for_rows<(MODE & 1) != 0, (MODE & 2) != 0>(
-        blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)(T)(wprev[c] * inv); },
+        blocks, nblocks, rowptr, col, val, nnz,
+        [&](int c) { return (MODE & 4) ? 1.0 + 0.0 * c : (double)(T)(wprev[c] * inv); },
         [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0), rexp ? (int)rexp[i] : 0}; },
         [&](int i, double sum, const Ops& o) {
             const T t = (T)ldexp(sum, -o.e);  // spmv(1, A, v, 0, w): y = 1*t (exact unscale)
@@ -1752,7 +1754,7 @@ int dispatch(int combo, F&& f) {
 // non-temporal matrix streams, bit 1 XCD-ordered row blocks
 int csr_mode() {
     const char* e = std::getenv("MPG_CSR_MODE");
-    return e && *e >= '0' && *e <= '3' ? *e - '0' : 0;
+    return e && *e >= '0' && *e <= '4' ? *e - '0' : 0;
 }
 
 int row_grid(const mpg_arnoldi* a) { return a->G; }
@@ -2135,6 +2137,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
         auto kern = mode == 1   ? (fold ? k_step_spmv<T, P, VI, true, 1> : k_step_spmv<T, P, VI, false, 1>)
                     : mode == 2 ? (fold ? k_step_spmv<T, P, VI, true, 2> : k_step_spmv<T, P, VI, false, 2>)
                     : mode == 3 ? (fold ? k_step_spmv<T, P, VI, true, 3> : k_step_spmv<T, P, VI, false, 3>)
+                    : mode == 4 ? (fold ? k_step_spmv<T, P, VI, true, 4> : k_step_spmv<T, P, VI, false, 4>)
                                 : (fold ? k_step_spmv<T, P, VI, true> : k_step_spmv<T, P, VI, false>);
         launch_timed(a->ctx, kern, dim3(rb_grid(a)), dim3(kBlock),
             A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,

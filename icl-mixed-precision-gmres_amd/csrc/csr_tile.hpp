@@ -209,32 +209,6 @@ __device__ __forceinline__ void stage_products_interior(int s, int e, const int3
     }
 }
 
-// sum of prod[a..z) in index order. Round 5: eight LDS reads in flight, then
-// their eight adds in order (the same operands and order, the same bits);
-// the one-at-a-time loop waited a full LDS round trip per entry (the ISA:
-// ds_read_b64, s_waitcnt lgkmcnt(0), v_add_f64 per iteration), ~2 us of a
-// 57-entry row's workgroup on the FEM stand-ins.
-__device__ __forceinline__ double lds_row_sum(const double* __restrict__ prod, int a, int z) {
-    double acc = 0.0;
-    int j = a;
-    for (; j + 8 <= z; j += 8) {
-        double t[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) t[q] = prod[j + q];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc += t[q];
-    }
-    if (j < z) {  // the tail: up to 7 reads, clamped to the row, masked at the add
-        double t[7];
-#pragma unroll
-        for (int q = 0; q < 7; ++q) t[q] = prod[j + q < z ? j + q : z - 1];
-#pragma unroll
-        for (int q = 0; q < 7; ++q)
-            if (j + q < z) acc += t[q];
-    }
-    return acc;
-}
-
 // Row sums of one row block: epi(row, fp64 sum, pre(row)) is called once per
 // row. pre(row) loads the row's epilogue operands; for this lane's first row
 // it is issued ahead of the tile, so its latency hides under the tile's.
@@ -264,7 +238,9 @@ __device__ __forceinline__ void csr_row_block(int r0, int r1, int s, int e, cons
         const bool first = r == threadIdx.x;
         const int a = (first ? ra : rowptr[r0 + r]) - s;
         const int z = (first ? rz : rowptr[r0 + r + 1]) - s;
-        epi(r0 + r, lds_row_sum(prod, a, z), first ? pf : pre(r0 + r));
+        double acc = 0.0;
+        for (int j = a; j < z; ++j) acc += prod[j];
+        epi(r0 + r, acc, first ? pf : pre(r0 + r));
     }
     __syncthreads();
 }

@@ -367,7 +367,10 @@ def test_scalar_program_matches_single_ops(hip, t):
     sv0[k] = dt(g.normal())
     out = {}
     for how in ("program", "single"):
-        col, c, s, sv = hip.buf(np.append(col0, 0)), hip.buf(np.append(c0, [0, 0])), hip.buf(np.append(s0, [0, 0])), hip.buf(sv0)
+        # (dt zeros: np.append with Python ints promotes float32 to float64)
+        col = hip.buf(np.concatenate([col0, np.zeros(1, dt)]))
+        c, s = hip.buf(np.concatenate([c0, np.zeros(2, dt)])), hip.buf(np.concatenate([s0, np.zeros(2, dt)]))
+        sv = hip.buf(sv0)
         rec, scal = hip.buf(np.zeros(3, dt)), hip.buf(np.array([dt(0.37)], dt))
         if how == "program":
             ops = (ScalarOp * 6)()
@@ -423,7 +426,10 @@ def test_scalar_program_rides_sell_spmv(hip, mpg, t):
     out = {}
     try:
         for how in ("ride", "apart"):
-            col, c, s, sv = hip.buf(np.append(col0, 0)), hip.buf(np.append(c0, [0, 0])), hip.buf(np.append(s0, [0, 0])), hip.buf(sv0)
+            # (dt zeros: np.append with Python ints promotes float32 to float64)
+            col = hip.buf(np.concatenate([col0, np.zeros(1, dt)]))
+            c, s = hip.buf(np.concatenate([c0, np.zeros(2, dt)])), hip.buf(np.concatenate([s0, np.zeros(2, dt)]))
+            sv = hip.buf(sv0)
             rec = hip.buf(np.zeros(1, dt))
             dx, dy = hip.buf(x), hip.buf(y0)
             ops = (ScalarOp * 4)()
@@ -481,7 +487,10 @@ def test_sell_spmv_norm_matches_separate_launches(hip, mpg, t, which):
     try:
         assert sell.value
         for how in ("ride", "apart", "ride-noprog", "apart-noprog"):
-            col, c, s, sv = hip.buf(np.append(col0, 0)), hip.buf(np.append(c0, [0, 0])), hip.buf(np.append(s0, [0, 0])), hip.buf(sv0)
+            # (dt zeros: np.append with Python ints promotes float32 to float64)
+            col = hip.buf(np.concatenate([col0, np.zeros(1, dt)]))
+            c, s = hip.buf(np.concatenate([c0, np.zeros(2, dt)])), hip.buf(np.concatenate([s0, np.zeros(2, dt)]))
+            sv = hip.buf(sv0)
             rec = hip.buf(np.zeros(1, dt))
             dw, dvk, dy = hip.buf(w), hip.buf(n, dt), hip.buf(np.full(n, 7.0, dt))
             ops = (ScalarOp * 4)()
