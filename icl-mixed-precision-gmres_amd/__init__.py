@@ -628,7 +628,7 @@ def _layout_dicts(lay, layouts: Optional[list]):
     forms = {-1: "none", 0: "int32", 1: "int16", 2: "stepped"}
     for L in lay:
         d = {f: getattr(L, f) for f, _ in RankLayout._fields_}
-        d["format"] = {1: "csr", 2: "sell"}.get(d["format"], d["format"])
+        d["format"] = {1: "csr", 2: "sell", 3: "node"}.get(d["format"], d["format"])
         d["col_form"] = forms[d["col_form"]]
         layouts.append(d)
 
@@ -791,7 +791,7 @@ class Engine:
         f, w, cb, st, win = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64(), C.c_int32()
         if self._lib.mpg_engine_spmv_layout(self._h, C.byref(f), C.byref(w), C.byref(cb), C.byref(st), C.byref(win)):
             raise RuntimeError("mpg_engine_spmv_layout failed")
-        return {"format": {1: "csr", 2: "sell"}[f.value], "vec_width": w.value, "col_bytes": cb.value,
+        return {"format": {1: "csr", 2: "sell", 3: "node"}[f.value], "vec_width": w.value, "col_bytes": cb.value,
                 "stored": st.value, "window": bool(win.value),
                 "slices_per_wave": int(self._lib.mpg_engine_slices_per_wave(self._h)),
                 "givens_folded": bool(self._lib.mpg_engine_givens_folded(self._h) == 1)}

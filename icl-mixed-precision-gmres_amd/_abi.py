@@ -8,7 +8,7 @@ MODES = {"mixed": 0, "baseline": 1, "single-prec": 2, "single": 3, "mixed-half":
 ORTHS = {"cgs": 0, "mgs": 1, "cgsr": 2}
 PRECS = {"ilu": 0, "ilu_jacobi": 1, "jacobi": 2, "identity": 3}
 ENGINES = {"surface": 0, "fused": 1}
-SPMV_FORMATS = {"auto": 0, "csr": 1, "sell": 2}
+SPMV_FORMATS = {"auto": 0, "csr": 1, "sell": 2, "node": 3}
 STATUS = {1: "converged", 3: "aborted", -1: "error"}
 
 

@@ -16,6 +16,7 @@
 // stand-alone kernels (blas1/blas2/spmv) apply, so the fused engine and the
 // operator-surface driver agree to the last bit in most steps.
 #include "csr_tile.hpp"
+#include "node_tile.hpp"
 #include "sell_tile.hpp"
 #include "handoff.hpp"
 #include "panel.hpp"
@@ -465,6 +466,37 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
             Vk[i] = o.wp * inv;
         },
         prod, scratch);
+}
+
+// ---------------------------------------------------------------- step: SpMV (node blocks)
+// Same contract as k_step_spmv on the node-block copy (node_tile.hpp): one
+// tile of node rows per workgroup, the CSR tile's products and row order.
+template <class T, class P, class VI, bool FOLD>
+__global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict__ tiles,
+                                                      const int32_t* __restrict__ bptr, const char* __restrict__ recs,
+                                                      const T* __restrict__ wprev, const T* __restrict__ inv_p,
+                                                      T* __restrict__ V, int64_t ld, int k,
+                                                      const P* __restrict__ diag, T* __restrict__ w,
+                                                      GivensFold<T> fold, const int8_t* __restrict__ rexp) {
+    __shared__ double prod[kNodeProd];
+    const T inv = fold_givens<FOLD>(fold, inv_p);
+    T* __restrict__ Vk = V + (int64_t)k * ld;
+    struct Ops {
+        T wp;
+        P d;
+        int e;
+    };
+    node_tile<VI>(
+        blockIdx.x, tiles, bptr, recs, [&](int c) { return (double)(T)(wprev[c] * inv); },
+        [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0), rexp ? (int)rexp[i] : 0}; },
+        [&](int i, double sum, const Ops& o) {
+            const T t = (T)ldexp(sum, -o.e);
+            P pw = (P)t;
+            if (diag) pw = P(0) * pw + P(1) * o.d * pw;
+            w[i] = (T)pw;
+            Vk[i] = o.wp * inv;
+        },
+        prod);
 }
 
 // ---------------------------------------------------------------- step: SpMV (SELL-64)
@@ -1708,6 +1740,7 @@ struct mpg_arnoldi {
     int Gd = 1;                    // workgroups (kCombineBlock threads) of the combining panel dots
     SellCopy sell;  // sliced-ELL copy of the Arnoldi matrix (nslices == 0: CSR row blocks)
     SellCopy sell_outer;        // ... of the outer-precision values, for the residual prologue
+    NodeCopy node;              // node-block copy of the Arnoldi matrix (nblk > 0: the Arnoldi SpMV uses it)
     bool outer_is_inner = false;  // the prologue runs on `sell` (baseline / single modes)
     // SELL SpMV with the panel dots fused (SellDots): per-workgroup partials,
     // group tickets, group size and count
@@ -1773,9 +1806,32 @@ GivensArgs<T> givens_args(const mpg_arnoldi* a, int k) {
                          a->report};
 }
 
-// the Arnoldi SpMV's SELL copy of the inner-precision values
+int64_t sell_copy_bytes(const mpg_arnoldi* a);
+
+// the Arnoldi SpMV's copy of the inner-precision values: SELL-64, node
+// blocks or none (CSR row blocks). Auto (format 0) takes the node-block copy
+// when the matrix has one and it is smaller than what auto would run
+// otherwise (the SpMV is HBM-bound: fewest bytes wins) -- on 3-dof FEM
+// matrices 4.44 B per fp32 nonzero against CSR's 8 (MPG_NODE=0: never).
 int arnoldi_sell_build(mpg_arnoldi* a, int format) {
+    if (format == 3) return node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, true, a->node);
     if (int st = sell_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, format, a->sell)) return st;
+    const char* ne = std::getenv("MPG_NODE");
+    if (format == 0 && !(ne && *ne == '0')) {
+        NodeCopy nc;
+        if (int st = node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, false, nc)) return st;
+        if (nc.nblk > 0) {
+            const int64_t vb = a->d.inner_val == MPG_F64 ? 8 : a->d.inner_val == MPG_F32 ? 4 : 2;
+            const int64_t now = a->sell.nslices > 0 ? sell_copy_bytes(a)
+                                                    : a->d.A->nnz * (4 + vb) + ((int64_t)a->d.n + 1) * 4;
+            if (node_bytes(nc) < now) {
+                sell_free(a->sell);
+                a->node = nc;
+                return MPG_OK;
+            }
+            node_free(nc);
+        }
+    }
     if (a->sell.nslices == 0) return MPG_OK;
     // the residual prologue on the same slicing: shared when the residual and
     // Arnoldi matrices are the same array, else a copy of the outer values
@@ -1846,7 +1902,7 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
         return MPG_ERR_ALLOC;
     }
     a->last_part = a->partial;
-    if (desc->spmv_format < 0 || desc->spmv_format > 2) {
+    if (desc->spmv_format < 0 || desc->spmv_format > 3) {
         mpg_arnoldi_destroy(a);
         return MPG_ERR_ARG;
     }
@@ -1859,7 +1915,13 @@ int mpg_arnoldi_create(mpg_ctx_t ctx, const mpg_arnoldi_desc* desc, mpg_arnoldi_
 }
 
 int64_t mpg_arnoldi_sell_matrix_bytes(mpg_arnoldi_t a) {
+    if (a && a->node.nblk > 0) return node_bytes(a->node) + (a->d.inner_row_exp ? (int64_t)a->d.n : 0);
     if (!a || a->sell.nslices == 0) return 0;
+    return sell_copy_bytes(a);
+}
+
+namespace {
+int64_t sell_copy_bytes(const mpg_arnoldi* a) {
     const SellCopy& S = a->sell;
     const int64_t vbytes = S.vtype == MPG_F64 ? 8 : S.vtype == MPG_F32 ? 4 : 2;
     const int64_t steps = S.padded / ((int64_t)kWave * S.W);
@@ -1874,6 +1936,7 @@ int64_t mpg_arnoldi_sell_matrix_bytes(mpg_arnoldi_t a) {
            (S.coff ? (int64_t)S.nslices * 8 : 0) + (a->d.inner_row_exp ? (int64_t)a->d.n : 0) +
            (S.rows ? (int64_t)S.nslices * kWave * 4 : 0);
 }
+}  // namespace
 
 int mpg_arnoldi_sell_sigma(mpg_arnoldi_t a) { return a ? a->sell.sigma : -1; }
 
@@ -1896,11 +1959,11 @@ int mpg_arnoldi_sell_columns(mpg_arnoldi_t a, int32_t* form, int64_t* csr_slices
 int mpg_arnoldi_spmv_layout(mpg_arnoldi_t a, int32_t* format, int32_t* vec_width, int32_t* col_bytes,
                             int64_t* stored, int32_t* window) {
     if (!a) return MPG_ERR_ARG;
-    const bool sell = a->sell.nslices > 0;
-    if (format) *format = sell ? 2 : 1;
-    if (vec_width) *vec_width = sell ? a->sell.W : 4;
-    if (col_bytes) *col_bytes = sell ? a->sell.col_bytes() : 4;
-    if (stored) *stored = sell ? a->sell.padded : a->d.A->nnz;
+    const bool sell = a->sell.nslices > 0, node = a->node.nblk > 0;
+    if (format) *format = node ? 3 : sell ? 2 : 1;
+    if (vec_width) *vec_width = node ? kNodeDof * kNodeDof : sell ? a->sell.W : 4;
+    if (col_bytes) *col_bytes = sell ? a->sell.col_bytes() : 4;  // (node blocks: one per 9 values)
+    if (stored) *stored = node ? a->node.nblk * kNodeDof * kNodeDof : sell ? a->sell.padded : a->d.A->nnz;
     if (window) *window = sell && a->sell.win ? 1 : 0;
     return MPG_OK;
 }
@@ -1914,6 +1977,7 @@ int mpg_arnoldi_destroy(mpg_arnoldi_t a) {
         if (p) (void)hipFree(p);
     sell_free(a->sell);
     sell_free(a->sell_outer);
+    node_free(a->node);
     delete a;
     return MPG_OK;
 }
@@ -2132,6 +2196,14 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                                 : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock>, SellDots{}, BSC());
                 });
             });
+        }
+        if (a->node.nblk > 0) {
+            launch_timed(a->ctx, fold ? k_step_node<T, P, VI, true> : k_step_node<T, P, VI, false>,
+                         dim3(a->node.ntiles), dim3(kBlock), static_cast<const int32_t*>(a->node.tiles),
+                         static_cast<const int32_t*>(a->node.bptr), static_cast<const char*>(a->node.recs),
+                         static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V),
+                         a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp);
+            return (int)MPG_OK;
         }
         const int mode = csr_mode();
         auto kern = mode == 1   ? (fold ? k_step_spmv<T, P, VI, true, 1> : k_step_spmv<T, P, VI, false, 1>)

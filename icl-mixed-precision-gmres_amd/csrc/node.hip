@@ -1,0 +1,151 @@
+// Build of the node-block copy of the Arnoldi matrix (node_tile.hpp).
+#include "node_tile.hpp"
+
+#include <algorithm>
+#include <vector>
+
+using namespace mpg;
+
+namespace {
+
+// blocks of node row r (rows 3r .. 3r + 2), or -1 when its rows are not made
+// of the same aligned column triples in the same storage positions
+__global__ __launch_bounds__(kBlock) void k_node_check(int nn, const int32_t* __restrict__ rowptr,
+                                                       const int32_t* __restrict__ col, int32_t* __restrict__ cnt) {
+    const int r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= nn) return;
+    const int p0 = rowptr[3 * r], p1 = rowptr[3 * r + 1], p2 = rowptr[3 * r + 2], p3 = rowptr[3 * r + 3];
+    const int len = p1 - p0;
+    int ok = p2 - p1 == len && p3 - p2 == len && len % 3 == 0;
+    for (int t = 0; ok && t < len; t += 3) {
+        const int c = col[p0 + t];
+        for (int j = 0; j < 3; ++j)
+            ok &= col[p0 + t + j] == c + j && col[p1 + t + j] == c + j && col[p2 + t + j] == c + j;
+    }
+    cnt[r] = ok ? len / 3 : -1;
+}
+
+template <class VI>
+__device__ __forceinline__ uint32_t val_bits(const VI* v, int64_t i);
+template <> __device__ __forceinline__ uint32_t val_bits<float>(const float* v, int64_t i) {
+    return __float_as_uint(v[i]);
+}
+template <> __device__ __forceinline__ uint32_t val_bits<half_v>(const half_v* v, int64_t i) { return v[i].bits; }
+
+// records of node row r: word 0 the block's first column, then the 9 values
+// row-major (fp64: from word 2; fp16: two per word)
+template <class VI>
+__global__ __launch_bounds__(kBlock) void k_node_fill(int nn, const int32_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ col, const VI* __restrict__ val,
+                                                      const int32_t* __restrict__ bptr, uint32_t* __restrict__ recs) {
+    constexpr int RW = NodeRec<VI>::R / 4;
+    const int r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= nn) return;
+    const int p[3] = {rowptr[3 * r], rowptr[3 * r + 1], rowptr[3 * r + 2]};
+    for (int b = bptr[r]; b < bptr[r + 1]; ++b) {
+        const int t = 3 * (b - bptr[r]);
+        uint32_t w[RW];
+#pragma unroll
+        for (int q = 0; q < RW; ++q) w[q] = 0;
+        w[0] = (uint32_t)col[p[0] + t];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int e = 3 * k + j;
+                const int64_t i = (int64_t)p[k] + t + j;
+                if constexpr (std::is_same_v<VI, double>) {
+                    const double v = val[i];
+                    w[2 + 2 * e] = (uint32_t)__double2loint(v);
+                    w[3 + 2 * e] = (uint32_t)__double2hiint(v);
+                } else if constexpr (std::is_same_v<VI, float>) {
+                    w[1 + e] = val_bits(val, i);
+                } else {
+                    w[1 + e / 2] |= val_bits(val, i) << (e & 1 ? 16 : 0);
+                }
+            }
+        uint32_t* o = recs + (int64_t)b * RW;
+#pragma unroll
+        for (int q = 0; q < RW; ++q) o[q] = w[q];
+    }
+}
+
+}  // namespace
+
+namespace mpg {
+
+int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool required, NodeCopy& S) {
+    S = NodeCopy{};
+    const int fail = required ? MPG_ERR_UNSUPPORTED : MPG_OK;
+    const int n = A->rows;
+    if (n == 0 || n % kNodeDof || A->nnz == 0 || !val) return fail;
+    if (vtype != MPG_F64 && vtype != MPG_F32 && vtype != MPG_F16) return MPG_ERR_ARG;
+    hipStream_t stream = ctx->stream;
+    const int nn = n / kNodeDof;
+    const int grid = (nn + kBlock - 1) / kBlock;
+    int32_t* cnt = nullptr;
+    MPG_HIP(ctx, hipMalloc((void**)&cnt, (size_t)nn * 4));
+    std::vector<int32_t> ch((size_t)nn);
+    k_node_check<<<grid, kBlock, 0, stream>>>(nn, A->rowptr, A->col, cnt);
+    hipError_t e = hipMemcpyAsync(ch.data(), cnt, (size_t)nn * 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    (void)hipFree(cnt);
+    if (e != hipSuccess) return set_hip_error(ctx, e, "node_build check");
+    std::vector<int32_t> bptr((size_t)nn + 1, 0);
+    int64_t nb = 0;
+    for (int r = 0; r < nn; ++r) {
+        if (ch[r] < 0 || ch[r] > kNodeCap) return fail;
+        bptr[r] = (int32_t)nb;
+        nb += ch[r];
+        if (nb >= INT32_MAX / 2) return fail;
+    }
+    bptr[nn] = (int32_t)nb;
+    // tiles: runs of node rows with at most kNodeCap blocks (and node rows)
+    std::vector<int32_t> tiles{0};
+    for (int r = 0; r < nn;) {
+        int z = r;
+        while (z < nn && bptr[z + 1] - bptr[r] <= kNodeCap && z - r < kNodeCap) ++z;
+        tiles.push_back(z);
+        r = z;
+    }
+    S.nn = nn;
+    S.nblk = nb;
+    S.ntiles = (int)tiles.size() - 1;
+    S.vtype = vtype;
+    S.rec = node_rec_bytes(vtype);
+    bool ok = hipMalloc((void**)&S.bptr, bptr.size() * 4) == hipSuccess &&
+              hipMalloc((void**)&S.tiles, tiles.size() * 4) == hipSuccess &&
+              hipMalloc(&S.recs, (size_t)std::max<int64_t>(nb, 1) * S.rec) == hipSuccess &&
+              hipMemcpyAsync(S.bptr, bptr.data(), bptr.size() * 4, hipMemcpyHostToDevice, stream) == hipSuccess &&
+              hipMemcpyAsync(S.tiles, tiles.data(), tiles.size() * 4, hipMemcpyHostToDevice, stream) == hipSuccess;
+    if (ok) {
+        auto* o = static_cast<uint32_t*>(S.recs);
+        if (vtype == MPG_F64)
+            k_node_fill<double><<<grid, kBlock, 0, stream>>>(nn, A->rowptr, A->col, static_cast<const double*>(val),
+                                                             S.bptr, o);
+        else if (vtype == MPG_F32)
+            k_node_fill<float><<<grid, kBlock, 0, stream>>>(nn, A->rowptr, A->col, static_cast<const float*>(val),
+                                                            S.bptr, o);
+        else
+            k_node_fill<half_v><<<grid, kBlock, 0, stream>>>(nn, A->rowptr, A->col, static_cast<const half_v*>(val),
+                                                             S.bptr, o);
+        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(stream) == hipSuccess;
+    }
+    if (!ok) {
+        node_free(S);
+        return MPG_ERR_ALLOC;
+    }
+    return MPG_OK;
+}
+
+void node_free(NodeCopy& S) {
+    for (void* p : {(void*)S.bptr, (void*)S.tiles, S.recs})
+        if (p) (void)hipFree(p);
+    S = NodeCopy{};
+}
+
+int64_t node_bytes(const NodeCopy& S) {
+    return S.nblk * S.rec + ((int64_t)S.nn + 1) * 4 + ((int64_t)S.ntiles + 1) * 4;
+}
+
+}  // namespace mpg

@@ -1,0 +1,144 @@
+// Node-block copy of the Arnoldi matrix (round 5): the storage of a matrix
+// whose unknowns come in nodes of 3 degrees of freedom (the FEM class of
+// Queen_4147 and the fem27 / stencil27p stand-ins), where every coupling of
+// two nodes is a full 3 x 3 block. CSR stores a column index per nonzero
+// (8 B per fp32 nonzero); here one record per block holds the block's first
+// column and its 9 values, row-major:
+//
+//   fp32: int32 col, 9 x fp32            40 B per 9 nonzeros (4.44 B each)
+//   fp64: int32 col, pad, 9 x fp64       80 B
+//   fp16: int32 col, 9 x fp16, pad       24 B
+//
+// bptr[r] .. bptr[r + 1] are the blocks of node row r (matrix rows 3r ..
+// 3r + 2), in the CSR's own storage order: block t of node row r is CSR
+// positions 3t .. 3t + 2 of each of the node's three rows, which must hold
+// the columns c, c + 1, c + 2 (the same c in all three rows). A tile is a
+// run of node rows with at most kNodeCap blocks: one record per lane, the 9
+// fp64 products into LDS, then one lane per matrix row sums its products in
+// storage order -- the CSR tile's products and summation order (csr_tile.hpp),
+// so the Arnoldi SpMV gives the same bits on either copy.
+#pragma once
+
+#include "csr_tile.hpp"  // half_v
+#include "internal.hpp"
+#include "mpgmres/arnoldi.h"  // mpg_dtype_t
+
+#include <type_traits>
+
+namespace mpg {
+
+constexpr int kNodeDof = 3;
+constexpr int kNodeCap = kBlock;  // blocks per tile: one record per lane
+constexpr int kNodeProd = kNodeCap * kNodeDof * kNodeDof;
+
+struct NodeCopy {
+    int nn = 0;            // node rows (rows / 3)
+    int64_t nblk = 0;      // blocks
+    int ntiles = 0;
+    int vtype = 0;         // MPG_F64 / MPG_F32 / MPG_F16
+    int rec = 0;           // record bytes
+    int32_t* bptr = nullptr;   // nn + 1 block starts
+    int32_t* tiles = nullptr;  // ntiles + 1 node-row starts
+    void* recs = nullptr;      // nblk records
+};
+
+// The node-block copy of (A, val) when A qualifies (rows a multiple of 3,
+// every node row's three rows made of aligned column triples, at most
+// kNodeCap blocks per node row): S.nblk > 0. A matrix that does not qualify
+// leaves S empty and returns MPG_OK (required: MPG_ERR_UNSUPPORTED).
+int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool required, NodeCopy& S);
+void node_free(NodeCopy& S);
+// bytes the Arnoldi SpMV streams from the copy: records, block and tile starts
+int64_t node_bytes(const NodeCopy& S);
+
+inline int node_rec_bytes(int vtype) { return vtype == MPG_F64 ? 80 : vtype == MPG_F32 ? 40 : 24; }
+
+template <class VI> struct NodeRec;
+template <> struct NodeRec<float> { static constexpr int R = 40; };
+template <> struct NodeRec<double> { static constexpr int R = 80; };
+template <> struct NodeRec<half_v> { static constexpr int R = 24; };
+
+typedef uint32_t u32x4a8_t __attribute__((ext_vector_type(4), aligned(8)));
+typedef uint32_t u32x2a8_t __attribute__((ext_vector_type(2), aligned(8)));
+
+// One record's raw words, loaded with 16-byte (8-byte aligned) loads and
+// kept undecoded until used, so that no load is waited for before all are
+// in flight.
+template <class VI>
+struct NodeWords {
+    static constexpr int R = NodeRec<VI>::R;
+    static constexpr int N16 = R / 16, N8 = (R % 16) / 8;
+    u32x4a8_t q[N16 > 0 ? N16 : 1];
+    u32x2a8_t d[N8 > 0 ? N8 : 1];
+    __device__ __forceinline__ void load(const char* __restrict__ p) {
+#pragma unroll
+        for (int i = 0; i < N16; ++i) q[i] = *reinterpret_cast<const u32x4a8_t*>(p + 16 * i);
+        if constexpr (N8 > 0) d[0] = *reinterpret_cast<const u32x2a8_t*>(p + 16 * N16);
+    }
+    __device__ __forceinline__ uint32_t word(int w) const {
+        return w < 4 * N16 ? q[w / 4][w % 4] : d[0][w - 4 * N16];
+    }
+    __device__ __forceinline__ int col() const { return (int)word(0); }
+    __device__ __forceinline__ double val(int e) const {
+        if constexpr (std::is_same_v<VI, float>) {
+            return (double)__uint_as_float(word(1 + e));
+        } else if constexpr (std::is_same_v<VI, double>) {
+            return __hiloint2double((int)word(3 + 2 * e), (int)word(2 + 2 * e));
+        } else {
+            const uint32_t w = word(1 + e / 2);
+            return (double)to_float((uint16_t)(e & 1 ? w >> 16 : w & 0xffffu));
+        }
+    }
+};
+
+// Row sums of tile t: epi(row, fp64 sum, pre(row)) once per matrix row of
+// the tile's node rows. pre(row) for this lane's first row is issued ahead
+// of the tile's loads.
+template <class VI, class XF, class PF, class EPI>
+__device__ __forceinline__ void node_tile(int t, const int32_t* __restrict__ tiles, const int32_t* __restrict__ bptr,
+                                          const char* __restrict__ recs, XF xval, PF pre, EPI epi,
+                                          double* __restrict__ prod) {
+    constexpr int R = NodeRec<VI>::R;
+    const int nr0 = tiles[t], nr1 = tiles[t + 1];
+    const int b0 = bptr[nr0], nb = bptr[nr1] - b0;
+    const int rows = kNodeDof * (nr1 - nr0);
+    // this lane's first row: its node row's blocks and epilogue operands
+    const int rf = threadIdx.x < rows ? (int)threadIdx.x : 0;
+    const int nf = nr0 + rf / kNodeDof;
+    const int fa = bptr[nf] - b0, fz = bptr[nf + 1] - b0;
+    const auto pf = pre(kNodeDof * nr0 + rf);
+    __builtin_amdgcn_sched_barrier(0);
+    if (nb > 0) {
+        const int l = threadIdx.x;
+        NodeWords<VI> w;
+        w.load(recs + (int64_t)(b0 + (l < nb ? l : nb - 1)) * R);
+        __builtin_amdgcn_sched_barrier(0);
+        const int c = w.col();
+        const double x0 = xval(c), x1 = xval(c + 1), x2 = xval(c + 2);
+        if (l < nb) {
+            double* p = prod + l * (kNodeDof * kNodeDof);
+#pragma unroll
+            for (int k = 0; k < kNodeDof; ++k) {
+                p[3 * k + 0] = w.val(3 * k + 0) * x0;
+                p[3 * k + 1] = w.val(3 * k + 1) * x1;
+                p[3 * k + 2] = w.val(3 * k + 2) * x2;
+            }
+        }
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < rows; r += kBlock) {
+        const bool first = r == (int)threadIdx.x;
+        const int nr = nr0 + r / kNodeDof, k = r % kNodeDof;
+        const int a = first ? fa : bptr[nr] - b0, z = first ? fz : bptr[nr + 1] - b0;
+        double acc = 0.0;
+        for (int b = a; b < z; ++b) {
+            const double* p = prod + b * (kNodeDof * kNodeDof) + kNodeDof * k;
+            acc += p[0];
+            acc += p[1];
+            acc += p[2];
+        }
+        epi(kNodeDof * nr0 + r, acc, first ? pf : pre(kNodeDof * nr0 + r));
+    }
+}
+
+}  // namespace mpg

@@ -962,7 +962,7 @@ double FusedEngine::phase_bytes(int which) const {
         int64_t stored = 0;
         check(mpg_arnoldi_spmv_layout(I.arn, &fmt, &W, &cb, &stored, &win), "layout", I.ctx);
         const double vec = 3 * n * sT + jac * n * sP;
-        if (fmt == 2) return (double)mpg_arnoldi_sell_matrix_bytes(I.arn) + vec;
+        if (fmt == 2 || fmt == 3) return (double)mpg_arnoldi_sell_matrix_bytes(I.arn) + vec;  // (3: node blocks)
         return z * (sV + 4) + (n + 1) * 4 + vec;
     }
     if (which == 3) {

@@ -169,7 +169,9 @@ bool fuse_enabled(int bit) {
 // w), so the semantics never change. tl_ride_score turns the redirect off on
 // a context where the pattern keeps failing (CGSR's second pass reads w
 // before the SpMV: two failures in a row switch it off; CGS fails only at the
-// last step of a cycle).
+// last step of a cycle). The score starts afresh in every ScopedContext
+// (one per solve): a CGSR solve must not switch the ride off for the CGS
+// solves that follow it on the same thread.
 namespace {
 struct Redirect {
     mpg_ctx_t ctx = nullptr;
@@ -395,6 +397,7 @@ ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) {
     if (tl_nops) flush_scalar_ops();
     if (tl_red.kind) flush_pending_reduction();
     tl_ctx = ctx;
+    tl_ride_score = 2;  // (what the ride learned belongs to the previous scope's solve)
 }
 ScopedContext::~ScopedContext() {
     // the queue and a pending stage 2 belong to this scope's context; a

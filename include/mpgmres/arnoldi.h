@@ -61,7 +61,8 @@ typedef struct {
     const void* diag;      /* Jacobi inverse diagonal (prec_type) or NULL */
     const void* b;         /* outer_type, n */
     void* x;               /* outer_type, row 0 of [-MPG_FRONT_PAD(n_front), n_ext) (halo filled by the caller) */
-    int32_t spmv_format;   /* Arnoldi SpMV storage: 0 auto, 1 CSR row blocks, 2 sliced ELL (SELL-64) */
+    int32_t spmv_format;   /* Arnoldi SpMV storage: 0 auto, 1 CSR row blocks, 2 sliced ELL (SELL-64),
+                              3 node blocks (3-dof nodes, 3 x 3 blocks; node_tile.hpp) */
     int32_t n_front;       /* halo rows of lower ranks, local ids [-n_front, 0) (0 on one GPU) */
     const int8_t* inner_row_exp; /* inner_val MPG_F16: per-row exponents of the scaled fp16 copy
                                     (mpg_csr_half_values, capi.h), or NULL (unscaled) */

@@ -61,7 +61,8 @@ typedef struct {
     int32_t verbose;       /* print the reference's stdout lines */
     int32_t device;        /* HIP device (mpg_solve only) */
     int32_t threads;       /* host threads (oracle only; 0 = default) */
-    int32_t spmv_format;   /* fused engine Arnoldi SpMV: 0 auto, 1 CSR row blocks, 2 SELL-64 */
+    int32_t spmv_format;   /* fused engine Arnoldi SpMV: 0 auto, 1 CSR row blocks, 2 SELL-64,
+                              3 node blocks (3-dof nodes, 3 x 3 blocks) */
     int32_t half_unscaled; /* mode mixed-half: 0 = fp16 values scaled per row by powers of two where
                               a row's magnitude needs it (mpg_csr_half_values, capi.h); 1 = plain
                               cast: a value outside fp16's range fails the set-up (MPG_ERR_RANGE) */

@@ -188,6 +188,20 @@ def compare_mkl(oracle, mpg, A, b, xt, got, opts: dict, label: str = "", runs: d
     return runs
 
 
+def golden_envelope(oracle, mpg, A, b, xt, rec: dict, opts: dict):
+    """The envelope of a golden record (made by the oracle's pinned MKL
+    branch, 1 thread): the record and the oracle's loop kernels run live on
+    the same inputs -- the fp64-accumulating summation class of the HIP
+    kernels. Near convergence an fp32 Arnoldi's attainable accuracy moves
+    with the summation order: convdiff32 at m = 100 ends cycle 2 at 5.5e-14
+    under MKL and 6.2e-15 on the loops (GPU: 6.6e-15)."""
+    from types import SimpleNamespace
+
+    g = SimpleNamespace(cyc_r_norm=rec["cyc_r_norm"], cyc_normalization=rec["cyc_normalization"],
+                        restarts=rec["restarts"])
+    return [g, oracle.solve(mpg, A, b, xt, backend="loops", threads=1, **opts)]
+
+
 def not_worse_than(ref, got, mode: str, label: str = "", factor: float = 3.0):
     """One-sided bound: every cycle's backward error of `got` at most
     `factor` x the reference run's (above the compare() floor); a GPU run

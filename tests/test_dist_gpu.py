@@ -165,7 +165,9 @@ def test_p8_stencil27_stepped_live_oracle(mpg, oracle, mode, orth):
     b = mpg.host_spmv(A, xt)
     opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=1e-10, max_restarts=100)
     lays = []
-    got = mpg.solve_loopback(A, b, xt, nranks=8, layouts=lays, **opts)
+    # (SELL forced: auto may take the node-block copy on a rank whose rows
+    # start on a node boundary, test_p8_stencil27_auto_node_ranks)
+    got = mpg.solve_loopback(A, b, xt, nranks=8, layouts=lays, spmv_format="sell", **opts)
     # nnz-balanced ranks hold ~30k rows, under a plane (33,075): where the
     # compacted halo numbering brings a rank's neighbour offsets within
     # +-32767 its copy takes int16 columns, the others the stepped form
@@ -174,6 +176,25 @@ def test_p8_stencil27_stepped_live_oracle(mpg, oracle, mode, orth):
     ref = oracle.solve(mpg, A, b, xt, **opts)
     assert ref.status == "converged"
     compare(as_ref(ref), got, mode, opts["tol"], 30, f"p8-stencil27-{mode}-{orth}")
+
+
+def test_p8_stencil27_auto_node_ranks(mpg, oracle):
+    """The same split on auto: each rank keeps whichever copy streams fewer
+    bytes -- its stepped / int16 SELL copy, or the node-block copy where its
+    rows start on a node boundary (3-dof nodes, halo triples kept whole by
+    the compacted numbering) -- and the solve stays at oracle parity."""
+    A = mpg.gen_stencil27(105, 3, ny=105, nz=8)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=1e-10, max_restarts=100)
+    lays = []
+    got = mpg.solve_loopback(A, b, xt, nranks=8, layouts=lays, **opts)
+    for q, L in enumerate(lays):
+        assert L["format"] in ("sell", "node"), (q, L)
+        if L["format"] == "node":
+            assert L["row0"] % 3 == 0 and L["n_local"] % 3 == 0, (q, L)
+    ref = oracle.solve(mpg, A, b, xt, **opts)
+    compare(as_ref(ref), got, "mixed", opts["tol"], 30, "p8-stencil27-auto")
 
 
 def test_p8_band_half_values_vs_oracle(mpg, oracle):

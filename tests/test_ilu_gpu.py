@@ -218,16 +218,21 @@ def test_ilu_rejects_missing_diagonal(hip, mpg):
 def test_ilu_solve_live_oracle(mpg, oracle, engine, mode, prec):
     """Whole GMRES(30) solves with ILU / ILU-Jacobi(3) on the 24^3 Laplacian
     against the oracle run on the same inputs (tests/parity.py classes)."""
-    from tests.parity import as_ref, compare
+    from tests.parity import compare_mkl
 
     A = mpg.gen_laplace3d(24)
     xt = mpg.rand_vect(A.nrows, 42)
     b = mpg.host_spmv(A, xt)
     opts = dict(mode=mode, orth="cgs", prec=prec, rlen=30, tol=1e-10, max_restarts=60, jacobi_steps=3)
-    ref = oracle.solve(mpg, A, b, xt, **opts)
     got = mpg.solve(A, b, xt, engine=engine, **opts)
-    assert ref.status == "converged"
-    compare(as_ref(ref), got, mode, opts["tol"], 30, f"lap24-{mode}-{prec}-{engine}")
+    # two-sided: MKL (pinned branch) at 1/4/8 threads and the loop kernels; ILU-Jacobi's
+    # last cycle ends at 6.5e-14 under MKL, 2.8e-13 on the loops (GPU 2.7e-13)
+    runs = compare_mkl(oracle, mpg, A, b, xt, got, opts, f"lap24-{mode}-{prec}-{engine}",
+                       runs=_ILU_ORACLE.setdefault((mode, prec), {}))
+    assert runs[1].status == "converged"
+
+
+_ILU_ORACLE = {}
 
 
 @pytest.mark.parametrize("engine", ["surface", "fused"])

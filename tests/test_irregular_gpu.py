@@ -12,8 +12,9 @@ apply. Two stand-ins take the general path:
 Each solve is compared with the live oracle (kernels_mkl.cpp's path,
 kernels_mkl.cpp:326-352 for the SpMV: MKL pinned to one code branch at fixed
 thread counts, two-sided, tests/parity.py compare_mkl) on both engines, and
-each asserts which Arnoldi SpMV form it ran (int32 SELL or CSR-adaptive row
-blocks)."""
+each asserts which Arnoldi SpMV form it ran (int32 SELL, CSR-adaptive row
+blocks or node blocks: one record of a 3 x 3 block per column triple,
+node_tile.hpp)."""
 import numpy as np
 import pytest
 
@@ -52,7 +53,9 @@ def _fmt(fmt, monkeypatch):
 @pytest.mark.parametrize("which", ["stencil27p", "fem27", "fem27p"])
 def test_irregular_layout(mpg, problems, which, fmt, monkeypatch):
     """What each storage choice runs: the permuted matrices never get 16-bit
-    or implicit columns; auto keeps SELL only when padding adds <= 20 %."""
+    or implicit columns; auto keeps SELL only when padding adds <= 20 %, and
+    takes the node-block copy (3-dof nodes, 3 x 3 blocks) whenever it is the
+    smallest -- on all three stand-ins."""
     A, xt, b = problems[which]
     eng = mpg.Engine(A, b, xt, mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=2,
                      spmv_format=_fmt(fmt, monkeypatch))
@@ -64,6 +67,9 @@ def test_irregular_layout(mpg, problems, which, fmt, monkeypatch):
         return
     if fmt == "csr":
         assert lay["format"] == "csr" and cols["form"] == "none", (lay, cols)
+        return
+    if fmt == "auto":
+        assert lay["format"] == "node" and lay["stored"] == A.nnz and cols["form"] == "none", (lay, cols)
         return
     if fmt == "sell":
         assert lay["format"] == "sell", lay
@@ -77,7 +83,7 @@ def test_irregular_layout(mpg, problems, which, fmt, monkeypatch):
 
 
 @pytest.mark.parametrize("engine,fmt", [("fused", "auto"), ("fused", "sell"), ("fused", "csr"), ("fused", "sell-sigma"),
-                                        ("surface", "auto"), ("surface", "sell-sigma")])
+                                        ("fused", "node"), ("surface", "auto"), ("surface", "sell-sigma")])
 @pytest.mark.parametrize("mode,orth", [("mixed", "cgs"), ("baseline", "mgs"), ("mixed", "cgsr")])
 @pytest.mark.parametrize("which", ["stencil27p", "fem27", "fem27p"])
 def test_irregular_live_oracle(mpg, oracle, problems, which, mode, orth, engine, fmt, monkeypatch):
@@ -122,3 +128,57 @@ def test_csr_stream_modes_same_bits(mpg, which, mode, monkeypatch):
     got = mpg.solve(A, b, xt, **opts)
     assert np.array_equal(got.step_res, ref.step_res) and np.array_equal(got.x, ref.x)
     assert got.res_norm == ref.res_norm
+
+
+def _node_problem(mpg, which):
+    if which == "stencil27":  # C4's own structure (3 dof per node), small
+        A = mpg.gen_stencil27(40, 3)
+    elif which == "stencil27p":
+        A = mpg.gen_stencil27p(48, 3, ny=48, nz=6, block=64, perm_seed=5)
+    elif which == "fem27":
+        A = mpg.gen_fem27(30, 3, keep_pct=70, seed=13)
+    else:
+        A = mpg.gen_spec("fem27:30:3:70:13:32:5")
+    xt = mpg.rand_vect(A.nrows, 42)
+    return A, xt, mpg.host_spmv(A, xt)
+
+
+@pytest.mark.parametrize("mode,orth,prec", [("mixed", "cgs", "jacobi"), ("mixed", "cgsr", "identity"),
+                                            ("baseline", "mgs", "jacobi"), ("single", "cgs", "jacobi"),
+                                            ("mixed-half", "cgs", "jacobi")])
+@pytest.mark.parametrize("which", ["stencil27", "stencil27p", "fem27", "fem27p"])
+def test_node_blocks_same_bits_as_csr(mpg, which, mode, orth, prec):
+    """The node-block SpMV (one record per 3 x 3 block: the block's first
+    column and 9 values) forms the CSR tile's fp64 products and sums each row
+    in CSR storage order: whole solves on either copy agree to the last bit,
+    in every value type (fp32, fp64, scaled fp16 records)."""
+    A, xt, b = _node_problem(mpg, which)
+    opts = dict(engine="fused", mode=mode, orth=orth, prec=prec, rlen=30, tol=0.0, max_restarts=3)
+    eng = mpg.Engine(A, b, xt, **{k: v for k, v in opts.items() if k != "engine"}, spmv_format="node")
+    lay = eng.spmv_layout()
+    eng.close()
+    assert lay["format"] == "node" and lay["stored"] == A.nnz and lay["vec_width"] == 9, lay
+    ref = mpg.solve(A, b, xt, spmv_format="csr", **opts)
+    got = mpg.solve(A, b, xt, spmv_format="node", **opts)
+    assert got.total_iters == ref.total_iters == 90
+    assert np.array_equal(got.step_res, ref.step_res) and np.array_equal(got.x, ref.x)
+    assert got.res_norm == ref.res_norm
+
+
+def test_node_blocks_refused(mpg):
+    """spmv_format="node" on a matrix without aligned 3 x 3 blocks fails
+    loudly (a band matrix; fem27 under a row-level permutation that splits
+    nodes); auto never picks it there."""
+    band = mpg.gen_band(30_000, 5, 4, seed=7)
+    A = mpg.gen_fem27(12, 3, keep_pct=70, seed=13)
+    rng = np.random.default_rng(3)
+    split = mpg.permute_sym(A, rng.permutation(A.nrows).astype(np.int32))
+    for M in (band, split):
+        xt = mpg.rand_vect(M.nrows, 42)
+        b = mpg.host_spmv(M, xt)
+        with pytest.raises((RuntimeError, ValueError)):
+            mpg.Engine(M, b, xt, mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=1,
+                       spmv_format="node").close()
+        eng = mpg.Engine(M, b, xt, mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=1)
+        assert eng.spmv_layout()["format"] != "node"
+        eng.close()

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from tests.golden.make_golden import inputs
-from tests.parity import compare, compare_mkl
+from tests.parity import compare, compare_mkl, golden_envelope
 
 pytestmark = pytest.mark.gpu
 
@@ -35,13 +35,24 @@ def _case_id(c):
 
 @pytest.mark.parametrize("engine", ["fused", "surface"])
 @pytest.mark.parametrize("rec", GOLDEN["cases"], ids=_case_id)
-def test_golden_m100(mpg, mats, rec, engine):
+def test_golden_m100(mpg, oracle, mats, rec, engine):
+    """Each record on both engines; fp32-Arnoldi backward errors inside the
+    envelope of the record and the oracle's loop kernels (golden_envelope)."""
     case = dict(rec["case"])
     A = mats[case.pop("matrix")]
     xt = mpg.rand_vect(A.nrows, 42)
     b = mpg.host_spmv(A, xt)
     got = mpg.solve(A, b, xt, engine=engine, **case)
-    compare(rec, got, case["mode"], case["tol"], case["rlen"], _case_id(rec) + "/" + engine)
+    env = None
+    if case["mode"] != "baseline":
+        key = _case_id(rec)
+        if key not in _LOOPS:
+            _LOOPS[key] = golden_envelope(oracle, mpg, A, b, xt, rec, case)
+        env = _LOOPS[key]
+    compare(rec, got, case["mode"], case["tol"], case["rlen"], _case_id(rec) + "/" + engine, envelope=env)
+
+
+_LOOPS = {}
 
 
 @pytest.mark.parametrize("engine", ["fused", "surface"])
@@ -59,9 +70,11 @@ def test_band_m100_live_oracle(mpg, oracle, engine, mode, orth):
     got = mpg.solve(A, b, xt, engine=engine, **opts)
     label = f"band300k-{mode}-{orth}-m100/{engine}"
     runs = compare_mkl(oracle, mpg, A, b, xt, got, opts, label, runs=_MKL.setdefault((mode, orth), {}))
-    ref = runs[1]
-    assert got.total_iters == ref.total_iters == 200
-    if mode == "mixed":  # the whole history, not only cycle 0
+    assert got.total_iters == runs[1].total_iters == 200
+    if mode == "mixed":  # the whole history, not only cycle 0, against the
+        # oracle's loop kernels: the GPU's summation class (MKL's fp32 gemv loses orthogonality
+        # here, cycle-1 backward error 6.0e-9 against 2.4e-10; profiles/r05_oracle_cnr)
+        ref = runs["loops"]
         np.testing.assert_allclose(got.step_res, ref.step_res, rtol=1e-3, atol=1e-6 * ref.minvb_norm)
 
 
