@@ -331,9 +331,10 @@ def test_surface_normalisation_ride_same_bits(mpg, matrix, orth, mode, prec, mon
         if fuse:
             assert delta["redirects"] == 0 and delta["rides"] == 0, delta
         elif orth == "cgs":
-            # every step but the last of a cycle (and the first eager cycle's
-            # first step, before the SELL copy exists) rides
-            assert delta["rides"] >= 3 * 27, delta
+            # every step but the last of a cycle rides, counted on the host in
+            # the eager cycle and the recording one (the third cycle replays
+            # the recorded graph, rides included, with no host calls)
+            assert delta["rides"] >= 2 * 27 and delta["flushed"] <= 2, delta
         elif orth == "mgs":
             assert delta == {"redirects": 0, "rides": 0, "flushed": 0}, delta
     ref = got["0"]
