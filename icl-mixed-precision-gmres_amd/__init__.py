@@ -119,6 +119,8 @@ def _declare_host(lib: C.CDLL) -> None:
     P64 = C.POINTER(C.c_int64)
     P32 = C.POINTER(C.c_int32)
     lib.mpg_halo_analyze.argtypes = [_I32, _I32, P64, _I32, P32, P32, C.POINTER(C.c_void_p)]
+    lib.mpg_csr_node_dof.argtypes = [_I32, P32, P32]
+    lib.mpg_csr_node_dof.restype = _I32
     lib.mpg_halo_n_ext.argtypes = [C.c_void_p]
     lib.mpg_halo_n_ext.restype = _I32
     lib.mpg_halo_n_front.argtypes = [C.c_void_p]
@@ -506,12 +508,24 @@ def row_slice(A: Csr, r0: int, r1: int) -> Csr:
     return Csr(r1 - r0, A.ncols, rp, A.col[base:end].copy(), A.val[base:end].copy())
 
 
+def node_dof(A: Csr) -> int:
+    """3 when A is made of whole 3 x 3 node blocks (mpg_csr_node_dof), else 1."""
+    rp = np.ascontiguousarray(A.rowptr, dtype=np.int32)
+    col = np.ascontiguousarray(A.col, dtype=np.int32)
+    return int(host_lib().mpg_csr_node_dof(A.nrows, rp.ctypes.data_as(C.POINTER(C.c_int32)),
+                                           col.ctypes.data_as(C.POINTER(C.c_int32))))
+
+
 def nnz_balanced_starts(A: Csr, nranks: int) -> np.ndarray:
-    """Row offsets splitting A into nranks blocks of about equal nnz."""
+    """Row offsets splitting A into nranks blocks of about equal nnz, rounded
+    down to node boundaries when A has 3-dof node blocks (node_dof; as
+    mpg_solve_loopback / mpg_solve_multi_gpu split)."""
     nnz = A.nnz
+    al = node_dof(A)
     starts = [0]
     for q in range(1, nranks):
-        starts.append(max(int(np.searchsorted(A.rowptr, nnz * q // nranks, side="left")), starts[-1]))
+        r = int(np.searchsorted(A.rowptr, nnz * q // nranks, side="left"))
+        starts.append(max(r // al * al, starts[-1]))
     starts.append(A.nrows)
     return np.array(starts, dtype=np.int64)
 

@@ -471,13 +471,16 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
 // ---------------------------------------------------------------- step: SpMV (node blocks)
 // Same contract as k_step_spmv on the node-block copy (node_tile.hpp): one
 // tile of node rows per workgroup, the CSR tile's products and row order.
-template <class T, class P, class VI, bool FOLD>
+// TPW > 1: each workgroup walks TPW consecutive tiles, the next tile's
+// records in flight during this one's gathers and row sums (node_tiles).
+template <class T, class P, class VI, bool FOLD, int TPW = 1, int DEPTH = 1>
 __global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict__ tiles,
                                                       const int32_t* __restrict__ bptr, const char* __restrict__ recs,
                                                       const T* __restrict__ wprev, const T* __restrict__ inv_p,
                                                       T* __restrict__ V, int64_t ld, int k,
                                                       const P* __restrict__ diag, T* __restrict__ w,
-                                                      GivensFold<T> fold, const int8_t* __restrict__ rexp) {
+                                                      GivensFold<T> fold, const int8_t* __restrict__ rexp,
+                                                      int ntiles, int64_t nblk) {
     __shared__ double prod[kNodeProd];
     const T inv = fold_givens<FOLD>(fold, inv_p);
     T* __restrict__ Vk = V + (int64_t)k * ld;
@@ -486,17 +489,21 @@ __global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict_
         P d;
         int e;
     };
-    node_tile<VI>(
-        blockIdx.x, tiles, bptr, recs, [&](int c) { return (double)(T)(wprev[c] * inv); },
-        [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0), rexp ? (int)rexp[i] : 0}; },
-        [&](int i, double sum, const Ops& o) {
-            const T t = (T)ldexp(sum, -o.e);
-            P pw = (P)t;
-            if (diag) pw = P(0) * pw + P(1) * o.d * pw;
-            w[i] = (T)pw;
-            Vk[i] = o.wp * inv;
-        },
-        prod);
+    auto xval = [&](int c) { return (double)(T)(wprev[c] * inv); };
+    auto pre = [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0), rexp ? (int)rexp[i] : 0}; };
+    auto epi = [&](int i, double sum, const Ops& o) {
+        const T t = (T)ldexp(sum, -o.e);
+        P pw = (P)t;
+        if (diag) pw = P(0) * pw + P(1) * o.d * pw;
+        w[i] = (T)pw;
+        Vk[i] = o.wp * inv;
+    };
+    if constexpr (TPW == 1) {
+        node_tile<VI>(blockIdx.x, tiles, bptr, recs, xval, pre, epi, prod);
+    } else {
+        const int t0 = blockIdx.x * TPW, t1 = t0 + TPW < ntiles ? t0 + TPW : ntiles;
+        node_tiles<VI, DEPTH>(t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, xval, pre, epi, prod);
+    }
 }
 
 // ---------------------------------------------------------------- step: SpMV (SELL-64)
@@ -1790,6 +1797,14 @@ int csr_mode() {
     return e && *e >= '0' && *e <= '4' ? *e - '0' : 0;
 }
 
+// MPG_NODE_TPW (the node-block SpMV, k_step_node<..., TPW>): tiles per
+// workgroup, 1 (one tile each) or 2 / 4 / 8 (pipelined walk)
+int node_tpw() {
+    const char* e = std::getenv("MPG_NODE_TPW");
+    const int v = e && *e ? std::atoi(e) : 1;
+    return v == 2 || v == 4 || v == 8 || v == 41 || v == 81 ? v : 1;  // (41, 81: two tiles ahead)
+}
+
 int row_grid(const mpg_arnoldi* a) { return a->G; }
 int rb_grid(const mpg_arnoldi* a) { return a->Grb; }
 
@@ -2198,12 +2213,22 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
             });
         }
         if (a->node.nblk > 0) {
-            launch_timed(a->ctx, fold ? k_step_node<T, P, VI, true> : k_step_node<T, P, VI, false>,
-                         dim3(a->node.ntiles), dim3(kBlock), static_cast<const int32_t*>(a->node.tiles),
-                         static_cast<const int32_t*>(a->node.bptr), static_cast<const char*>(a->node.recs),
-                         static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V),
-                         a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp);
-            return (int)MPG_OK;
+            const NodeCopy& S = a->node;
+            auto go = [&](auto kern, int tpw) {
+                launch_timed(a->ctx, kern, dim3((S.ntiles + tpw - 1) / tpw), dim3(kBlock),
+                             static_cast<const int32_t*>(S.tiles), static_cast<const int32_t*>(S.bptr),
+                             static_cast<const char*>(S.recs), static_cast<const T*>(a->w[k & 1]),
+                             static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k, diag,
+                             static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp, S.ntiles, S.nblk);
+                return (int)MPG_OK;
+            };
+            const int tpw = node_tpw();
+            if (tpw == 2) return fold ? go(k_step_node<T, P, VI, true, 2>, 2) : go(k_step_node<T, P, VI, false, 2>, 2);
+            if (tpw == 4) return fold ? go(k_step_node<T, P, VI, true, 4>, 4) : go(k_step_node<T, P, VI, false, 4>, 4);
+            if (tpw == 8) return fold ? go(k_step_node<T, P, VI, true, 8>, 8) : go(k_step_node<T, P, VI, false, 8>, 8);
+            if (tpw == 41) return fold ? go(k_step_node<T, P, VI, true, 4, 2>, 4) : go(k_step_node<T, P, VI, false, 4, 2>, 4);
+            if (tpw == 81) return fold ? go(k_step_node<T, P, VI, true, 8, 2>, 8) : go(k_step_node<T, P, VI, false, 8, 2>, 8);
+            return fold ? go(k_step_node<T, P, VI, true>, 1) : go(k_step_node<T, P, VI, false>, 1);
         }
         const int mode = csr_mode();
         auto kern = mode == 1   ? (fold ? k_step_spmv<T, P, VI, true, 1> : k_step_spmv<T, P, VI, false, 1>)

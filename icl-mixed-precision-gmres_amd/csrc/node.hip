@@ -108,9 +108,12 @@ int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool 
         tiles.push_back(z);
         r = z;
     }
+    const size_t nt1 = tiles.size();
+    tiles.resize(2 * nt1);
+    for (size_t t = 0; t < nt1; ++t) tiles[nt1 + t] = bptr[tiles[t]];
     S.nn = nn;
     S.nblk = nb;
-    S.ntiles = (int)tiles.size() - 1;
+    S.ntiles = (int)nt1 - 1;
     S.vtype = vtype;
     S.rec = node_rec_bytes(vtype);
     bool ok = hipMalloc((void**)&S.bptr, bptr.size() * 4) == hipSuccess &&
@@ -145,7 +148,7 @@ void node_free(NodeCopy& S) {
 }
 
 int64_t node_bytes(const NodeCopy& S) {
-    return S.nblk * S.rec + ((int64_t)S.nn + 1) * 4 + ((int64_t)S.ntiles + 1) * 4;
+    return S.nblk * S.rec + ((int64_t)S.nn + 1) * 4 + 2 * ((int64_t)S.ntiles + 1) * 4;
 }
 
 }  // namespace mpg

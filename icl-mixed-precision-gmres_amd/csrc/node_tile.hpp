@@ -38,7 +38,7 @@ struct NodeCopy {
     int vtype = 0;         // MPG_F64 / MPG_F32 / MPG_F16
     int rec = 0;           // record bytes
     int32_t* bptr = nullptr;   // nn + 1 block starts
-    int32_t* tiles = nullptr;  // ntiles + 1 node-row starts
+    int32_t* tiles = nullptr;  // ntiles + 1 node-row starts, then ntiles + 1 block starts (tb0)
     void* recs = nullptr;      // nblk records
 };
 
@@ -138,6 +138,73 @@ __device__ __forceinline__ void node_tile(int t, const int32_t* __restrict__ til
             acc += p[2];
         }
         epi(kNodeDof * nr0 + r, acc, first ? pf : pre(kNodeDof * nr0 + r));
+    }
+}
+
+// Tiles [t0, t1) in turn on one workgroup, software-pipelined: the next
+// tile's records are loaded while this tile's gathers, products and row sums
+// run, so each workgroup keeps twice the bytes in flight. tb0[t] = bptr of
+// tiles[t] (the record addresses without the dependent bptr load). Barriers
+// wait for LDS only (lds_barrier): __syncthreads would also drain the
+// prefetched records.
+template <class VI, int DEPTH = 1, class XF, class PF, class EPI>
+__device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __restrict__ tiles,
+                                           const int32_t* __restrict__ tb0, const int32_t* __restrict__ bptr,
+                                           const char* __restrict__ recs, int64_t nblk, XF xval, PF pre, EPI epi,
+                                           double* __restrict__ prod) {
+    constexpr int R = NodeRec<VI>::R;
+    const int l = threadIdx.x;
+    auto rec = [&](int t) {
+        const int b0 = tb0[t], nb = tb0[t + 1] - b0;
+        int64_t b = (int64_t)b0 + (l < nb ? l : nb - 1);
+        b = b < 0 ? 0 : b >= nblk ? nblk - 1 : b;
+        return recs + b * R;
+    };
+    NodeWords<VI> cur, nxt, nx2;
+    cur.load(rec(t0));
+    if constexpr (DEPTH == 2)
+        if (t0 + 1 < t1) nxt.load(rec(t0 + 1));
+    for (int t = t0; t < t1; ++t) {
+        const int nr0 = tiles[t], nr1 = tiles[t + 1];
+        const int b0 = tb0[t], nb = tb0[t + 1] - b0;
+        const int rows = kNodeDof * (nr1 - nr0);
+        const int rf = l < rows ? l : 0;
+        const int nf = nr0 + rf / kNodeDof;
+        const int fa = bptr[nf] - b0, fz = bptr[nf + 1] - b0;
+        const auto pf = pre(kNodeDof * nr0 + rf);
+        const int c = cur.col();
+        const double x0 = xval(c), x1 = xval(c + 1), x2 = xval(c + 2);
+        if constexpr (DEPTH == 2) {
+            if (t + 2 < t1) nx2.load(rec(t + 2));
+        } else {
+            if (t + 1 < t1) nxt.load(rec(t + 1));
+        }
+        if (l < nb) {
+            double* p = prod + l * (kNodeDof * kNodeDof);
+#pragma unroll
+            for (int k = 0; k < kNodeDof; ++k) {
+                p[3 * k + 0] = cur.val(3 * k + 0) * x0;
+                p[3 * k + 1] = cur.val(3 * k + 1) * x1;
+                p[3 * k + 2] = cur.val(3 * k + 2) * x2;
+            }
+        }
+        lds_barrier();
+        for (int r = l; r < rows; r += kBlock) {
+            const bool first = r == l;
+            const int nr = nr0 + r / kNodeDof, k = r % kNodeDof;
+            const int a = first ? fa : bptr[nr] - b0, z = first ? fz : bptr[nr + 1] - b0;
+            double acc = 0.0;
+            for (int b = a; b < z; ++b) {
+                const double* p = prod + b * (kNodeDof * kNodeDof) + kNodeDof * k;
+                acc += p[0];
+                acc += p[1];
+                acc += p[2];
+            }
+            epi(kNodeDof * nr0 + r, acc, first ? pf : pre(kNodeDof * nr0 + r));
+        }
+        lds_barrier();
+        cur = nxt;
+        if constexpr (DEPTH == 2) nxt = nx2;
     }
 }
 

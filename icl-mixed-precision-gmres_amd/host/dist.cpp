@@ -344,14 +344,16 @@ private:
     }
 };
 
-std::vector<int64_t> nnz_balanced_starts(int n, const int32_t* rowptr, int P) {
+// rank starts at about equal nnz, rounded down to multiples of `align`
+// (the node size, mpg_csr_node_dof)
+std::vector<int64_t> nnz_balanced_starts(int n, const int32_t* rowptr, int P, int align = 1) {
     std::vector<int64_t> st((size_t)P + 1, 0);
     const int64_t nnz = rowptr[n];
     int r = 0;
     for (int q = 1; q < P; ++q) {
         const int64_t target = nnz * q / P;
         while (r < n && rowptr[r] < target) ++r;
-        st[(size_t)q] = std::max<int64_t>(r, st[(size_t)q - 1]);
+        st[(size_t)q] = std::max<int64_t>(r / align * align, st[(size_t)q - 1]);
     }
     st[(size_t)P] = n;
     return st;
@@ -363,6 +365,21 @@ std::vector<int64_t> nnz_balanced_starts(int n, const int32_t* rowptr, int P) {
 using namespace mpg;
 
 extern "C" {
+
+int32_t mpg_csr_node_dof(int32_t n, const int32_t* rowptr, const int32_t* col) {
+    if (n <= 0 || n % 3 || !rowptr || !col) return 1;
+    for (int32_t r = 0; r < n; r += 3) {
+        const int32_t p0 = rowptr[r], p1 = rowptr[r + 1], p2 = rowptr[r + 2], p3 = rowptr[r + 3];
+        const int32_t len = p1 - p0;
+        if (p2 - p1 != len || p3 - p2 != len || len % 3) return 1;
+        for (int32_t t = 0; t < len; t += 3) {
+            const int32_t c = col[p0 + t];
+            for (int32_t j = 0; j < 3; ++j)
+                if (col[p0 + t + j] != c + j || col[p1 + t + j] != c + j || col[p2 + t + j] != c + j) return 1;
+        }
+    }
+    return 3;
+}
 
 int mpg_halo_analyze(int32_t rank, int32_t nranks, const int64_t* row_starts, int32_t n_local, const int32_t* rowptr,
                      const int32_t* col_global, mpg_halo_t* out) {
@@ -543,7 +560,7 @@ int solve_rank_threads(const mpg_solve_args* a, int32_t P, mpg_solve_result* r, 
                        const std::function<void()>& on_error,
                        const std::function<void(int)>& on_comm_gone = nullptr) {
     const int n = a->n;
-    const auto starts = nnz_balanced_starts(n, a->rowptr, P);
+    const auto starts = nnz_balanced_starts(n, a->rowptr, P, mpg_csr_node_dof(n, a->rowptr, a->col));
     // per-rank row slices and halo plans
     std::vector<std::vector<int32_t>> rp(P), cg(P);
     std::vector<mpg_halo_t> plans(P, nullptr);

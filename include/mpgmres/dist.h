@@ -92,7 +92,16 @@ typedef struct {
 int mpg_engine_create_dist_host(const mpg_solve_args* args, mpg_halo_t plan, const mpg_host_transport* transport,
                                 int32_t nranks, int32_t rank, mpg_engine_t* out, char* err, int errlen);
 
-/* P ranks as threads on one device, rows split evenly by nnz; the result
+/* Degrees of freedom per node of a CSR matrix: 3 when every node row (rows
+ * 3r .. 3r + 2) is made of the same column triples c, c + 1, c + 2 in the
+ * same storage positions (the node-block copy's condition, node_tile.hpp),
+ * else 1. The nnz-balanced row split rounds its rank starts down to node
+ * boundaries when it is 3, so every rank keeps whole nodes (and can take the
+ * node-block copy). */
+int32_t mpg_csr_node_dof(int32_t n, const int32_t* rowptr, const int32_t* col);
+
+/* P ranks as threads on one device, rows split evenly by nnz (at node
+ * boundaries, mpg_csr_node_dof); the result
  * (history, counts, norms, x gathered) matches mpg_solve's. */
 int mpg_solve_loopback(const mpg_solve_args* args, int32_t nranks, mpg_solve_result* result);
 
@@ -100,7 +109,7 @@ int mpg_solve_loopback(const mpg_solve_args* args, int32_t nranks, mpg_solve_res
  * storage (mpg_arnoldi_spmv_layout / mpg_arnoldi_sell_columns), the local
  * numbering (dist.h above) and the fp16 cast's scaled rows. */
 typedef struct {
-    int32_t format;           /* 1 CSR row blocks, 2 SELL-64 */
+    int32_t format;           /* 1 CSR row blocks, 2 SELL-64, 3 node blocks */
     int32_t col_form;         /* SELL columns: -1 none, 0 int32, 1 int16, 2 stepped int16 */
     int32_t vec_width;
     int32_t window;           /* 1: the SpMV reads v_k from the LDS window */

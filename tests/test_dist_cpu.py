@@ -200,3 +200,27 @@ def test_halo_plan_single_process(mpg):
     assert np.array_equal(cols, A1.col - 300)
     with pytest.raises(ValueError):
         plans[1].set_send(0, [10])  # row 10 is not owned by rank 1
+
+
+def test_node_dof_and_node_aligned_starts(mpg):
+    """mpg_csr_node_dof: 3 on the 3-dof generators (27-point stencil, thinned
+    FEM coupling, node-block permutation), 1 on a band, a 7-point Laplacian
+    and fem27 under a row permutation that splits nodes; the nnz-balanced
+    split then starts every rank on a node boundary."""
+    A = mpg.gen_stencil27(20, 3)
+    F = mpg.gen_fem27(10, 3, keep_pct=70, seed=13)
+    Fp = mpg.gen_spec("fem27:10:3:70:13:32:5")
+    split = mpg.permute_sym(F, np.random.default_rng(3).permutation(F.nrows).astype(np.int32))
+    assert [mpg.node_dof(M) for M in (A, F, Fp)] == [3, 3, 3]
+    assert [mpg.node_dof(M) for M in (mpg.gen_band(3000, 5, 4, seed=7), mpg.gen_laplace3d(9), split)] == [1, 1, 1]
+    for M in (A, F, Fp):
+        for P in (2, 3, 5, 8):
+            st = mpg.nnz_balanced_starts(M, P)
+            assert st[0] == 0 and st[-1] == M.nrows and np.all(np.diff(st) >= 0) and np.all(st % 3 == 0), (P, st)
+            # still about nnz-balanced (within one node's rows of the target)
+            for q in range(1, P):
+                assert abs(int(M.rowptr[st[q]]) - M.nnz * q // P) <= 6 * 81, (q, st)
+    B = mpg.gen_band(4000, 5, 4, seed=7)  # no nodes: the plain nnz split
+    st = mpg.nnz_balanced_starts(B, 3)
+    want = [0] + [int(np.searchsorted(B.rowptr, B.nnz * q // 3, side="left")) for q in (1, 2)] + [4000]
+    assert np.array_equal(st, want) and any(v % 3 for v in want), (st, want)

@@ -182,3 +182,19 @@ def test_node_blocks_refused(mpg):
         eng = mpg.Engine(M, b, xt, mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=1)
         assert eng.spmv_layout()["format"] != "node"
         eng.close()
+
+
+@pytest.mark.parametrize("tpw", ["2", "4", "8", "41"])
+@pytest.mark.parametrize("which", ["stencil27", "fem27p"])
+def test_node_tile_walk_same_bits(mpg, which, tpw, monkeypatch):
+    """MPG_NODE_TPW: each workgroup walks 2 / 4 / 8 consecutive tiles with the
+    next tile's records in flight (node_tiles) -- the same tiles, products
+    and row order as one tile per workgroup: the same bits."""
+    A, xt, b = _node_problem(mpg, which)
+    opts = dict(engine="fused", mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3,
+                spmv_format="node")
+    monkeypatch.setenv("MPG_NODE_TPW", "1")
+    ref = mpg.solve(A, b, xt, **opts)
+    monkeypatch.setenv("MPG_NODE_TPW", tpw)
+    got = mpg.solve(A, b, xt, **opts)
+    assert np.array_equal(got.step_res, ref.step_res) and np.array_equal(got.x, ref.x)
