@@ -473,7 +473,7 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
 // tile of node rows per workgroup, the CSR tile's products and row order.
 // TPW > 1: each workgroup walks TPW consecutive tiles, the next tile's
 // records in flight during this one's gathers and row sums (node_tiles).
-template <class T, class P, class VI, bool FOLD, int TPW = 1, int DEPTH = 1>
+template <class T, class P, class VI, bool FOLD, int TPW = 1>
 __global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict__ tiles,
                                                       const int32_t* __restrict__ bptr, const char* __restrict__ recs,
                                                       const T* __restrict__ wprev, const T* __restrict__ inv_p,
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict_
         node_tile<VI>(blockIdx.x, tiles, bptr, recs, xval, pre, epi, prod);
     } else {
         const int t0 = blockIdx.x * TPW, t1 = t0 + TPW < ntiles ? t0 + TPW : ntiles;
-        node_tiles<VI, DEPTH>(t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, xval, pre, epi, prod);
+        node_tiles<VI>(t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, xval, pre, epi, prod);
     }
 }
 
@@ -1798,11 +1798,13 @@ int csr_mode() {
 }
 
 // MPG_NODE_TPW (the node-block SpMV, k_step_node<..., TPW>): tiles per
-// workgroup, 1 (one tile each) or 2 / 4 / 8 (pipelined walk)
+// workgroup, 1 (one tile each) or 2 (default) / 4 / 8 (pipelined walk).
+// Measured (profiles/r05_node_ab.jsonl): fem27 248 / 218 / 215-228 / 223 us,
+// C4's stencil 341 / 295 / 300 / 306 us.
 int node_tpw() {
     const char* e = std::getenv("MPG_NODE_TPW");
-    const int v = e && *e ? std::atoi(e) : 1;
-    return v == 2 || v == 4 || v == 8 || v == 41 || v == 81 ? v : 1;  // (41, 81: two tiles ahead)
+    const int v = e && *e ? std::atoi(e) : 2;
+    return v == 2 || v == 4 || v == 8 ? v : 1;
 }
 
 int row_grid(const mpg_arnoldi* a) { return a->G; }
@@ -1825,9 +1827,11 @@ int64_t sell_copy_bytes(const mpg_arnoldi* a);
 
 // the Arnoldi SpMV's copy of the inner-precision values: SELL-64, node
 // blocks or none (CSR row blocks). Auto (format 0) takes the node-block copy
-// when the matrix has one and it is smaller than what auto would run
-// otherwise (the SpMV is HBM-bound: fewest bytes wins) -- on 3-dof FEM
-// matrices 4.44 B per fp32 nonzero against CSR's 8 (MPG_NODE=0: never).
+// when the matrix has one and it streams at most 10 % more bytes than what
+// auto would run otherwise: the SpMV is HBM-bound, and the node records
+// stream faster than the SELL copies (C4's stencil: 1506 MB in 295 us against
+// the stepped SELL copy's 1438 MB in 324 us; 3-dof FEM: 4.44 B per fp32
+// nonzero against CSR's 8). MPG_NODE=0: never.
 int arnoldi_sell_build(mpg_arnoldi* a, int format) {
     if (format == 3) return node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, true, a->node);
     if (int st = sell_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, format, a->sell)) return st;
@@ -1839,7 +1843,7 @@ int arnoldi_sell_build(mpg_arnoldi* a, int format) {
             const int64_t vb = a->d.inner_val == MPG_F64 ? 8 : a->d.inner_val == MPG_F32 ? 4 : 2;
             const int64_t now = a->sell.nslices > 0 ? sell_copy_bytes(a)
                                                     : a->d.A->nnz * (4 + vb) + ((int64_t)a->d.n + 1) * 4;
-            if (node_bytes(nc) < now) {
+            if (node_bytes(nc) * 10 < now * 11) {
                 sell_free(a->sell);
                 a->node = nc;
                 return MPG_OK;
@@ -2226,8 +2230,6 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
             if (tpw == 2) return fold ? go(k_step_node<T, P, VI, true, 2>, 2) : go(k_step_node<T, P, VI, false, 2>, 2);
             if (tpw == 4) return fold ? go(k_step_node<T, P, VI, true, 4>, 4) : go(k_step_node<T, P, VI, false, 4>, 4);
             if (tpw == 8) return fold ? go(k_step_node<T, P, VI, true, 8>, 8) : go(k_step_node<T, P, VI, false, 8>, 8);
-            if (tpw == 41) return fold ? go(k_step_node<T, P, VI, true, 4, 2>, 4) : go(k_step_node<T, P, VI, false, 4, 2>, 4);
-            if (tpw == 81) return fold ? go(k_step_node<T, P, VI, true, 8, 2>, 8) : go(k_step_node<T, P, VI, false, 8, 2>, 8);
             return fold ? go(k_step_node<T, P, VI, true>, 1) : go(k_step_node<T, P, VI, false>, 1);
         }
         const int mode = csr_mode();

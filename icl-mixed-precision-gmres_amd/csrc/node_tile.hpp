@@ -146,8 +146,9 @@ __device__ __forceinline__ void node_tile(int t, const int32_t* __restrict__ til
 // run, so each workgroup keeps twice the bytes in flight. tb0[t] = bptr of
 // tiles[t] (the record addresses without the dependent bptr load). Barriers
 // wait for LDS only (lds_barrier): __syncthreads would also drain the
-// prefetched records.
-template <class VI, int DEPTH = 1, class XF, class PF, class EPI>
+// prefetched records. (Two tiles ahead measured no better: fem27 227 vs
+// 218 us, C4 298 vs 295 us, profiles/r05_node_ab.jsonl.)
+template <class VI, class XF, class PF, class EPI>
 __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __restrict__ tiles,
                                            const int32_t* __restrict__ tb0, const int32_t* __restrict__ bptr,
                                            const char* __restrict__ recs, int64_t nblk, XF xval, PF pre, EPI epi,
@@ -160,10 +161,8 @@ __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __rest
         b = b < 0 ? 0 : b >= nblk ? nblk - 1 : b;
         return recs + b * R;
     };
-    NodeWords<VI> cur, nxt, nx2;
+    NodeWords<VI> cur, nxt;
     cur.load(rec(t0));
-    if constexpr (DEPTH == 2)
-        if (t0 + 1 < t1) nxt.load(rec(t0 + 1));
     for (int t = t0; t < t1; ++t) {
         const int nr0 = tiles[t], nr1 = tiles[t + 1];
         const int b0 = tb0[t], nb = tb0[t + 1] - b0;
@@ -174,11 +173,7 @@ __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __rest
         const auto pf = pre(kNodeDof * nr0 + rf);
         const int c = cur.col();
         const double x0 = xval(c), x1 = xval(c + 1), x2 = xval(c + 2);
-        if constexpr (DEPTH == 2) {
-            if (t + 2 < t1) nx2.load(rec(t + 2));
-        } else {
-            if (t + 1 < t1) nxt.load(rec(t + 1));
-        }
+        if (t + 1 < t1) nxt.load(rec(t + 1));
         if (l < nb) {
             double* p = prod + l * (kNodeDof * kNodeDof);
 #pragma unroll
@@ -204,7 +199,6 @@ __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __rest
         }
         lds_barrier();
         cur = nxt;
-        if constexpr (DEPTH == 2) nxt = nx2;
     }
 }
 

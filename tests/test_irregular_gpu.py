@@ -184,7 +184,7 @@ def test_node_blocks_refused(mpg):
         eng.close()
 
 
-@pytest.mark.parametrize("tpw", ["2", "4", "8", "41"])
+@pytest.mark.parametrize("tpw", ["2", "4", "8"])
 @pytest.mark.parametrize("which", ["stencil27", "fem27p"])
 def test_node_tile_walk_same_bits(mpg, which, tpw, monkeypatch):
     """MPG_NODE_TPW: each workgroup walks 2 / 4 / 8 consecutive tiles with the
