@@ -3,9 +3,10 @@ engine over the host transport (mpg_engine_create_dist_host + transport.py),
 launched by tests/test_dist_gpu.py as
 
   python -m torch.distributed.run --nproc-per-node P --master-addr 127.0.0.1 \
-      --master-port PORT tests/dist_host_worker.py OUT.npz MATRIX MODE ORTH PREC MAX_RESTARTS TOL
+      --master-port PORT tests/dist_host_worker.py OUT.npz MATRIX MODE ORTH PREC MAX_RESTARTS TOL [FORMAT]
 
 MATRIX: N (BAND-N, gen_band(N, 5, 4, seed=7)) or stencil27:NX:NY:NZ (3 dof).
+FORMAT: the Arnoldi SpMV storage (spmv_format; default auto).
 Every rank uses device 0 (the ranks share the GPU; RCCL would refuse).
 Rank 0 writes the gathered solution, its history and every rank's SpMV
 layout (column form, CSR-summed slices, front halo) to OUT.npz.
@@ -30,6 +31,7 @@ def matrix(mpg, spec: str):
 
 def main():
     out, spec, mode, orth, prec, max_restarts, tol = sys.argv[1:8]
+    fmt = sys.argv[8] if len(sys.argv) > 8 else "auto"
     from __graft_entry__ import _load
 
     mpg = _load()
@@ -51,10 +53,11 @@ def main():
         if q != rank:
             plan.set_send(q, got[q].get(rank, []))
     transport = HostTransport()
-    opts = dict(mode=mode, orth=orth, prec=prec, rlen=30, tol=float(tol), max_restarts=int(max_restarts), device=0)
+    opts = dict(mode=mode, orth=orth, prec=prec, rlen=30, tol=float(tol), max_restarts=int(max_restarts), device=0,
+                spmv_format=fmt)
     eng = mpg.Engine.distributed_host(A_loc, b[r0:r1], xt[r0:r1], plan, transport, world, rank, **opts)
     cols = eng.sell_columns()
-    mine = [{"csr": 0, "sell": 1}[eng.spmv_layout()["format"]],
+    mine = [{"csr": 0, "sell": 1, "node": 2}[eng.spmv_layout()["format"]],
             {"none": -1, "int32": 0, "int16": 1, "stepped": 2}[cols["form"]], cols["csr_slices"], plan.n_front]
     lays = [None] * world
     dist.all_gather_object(lays, mine)

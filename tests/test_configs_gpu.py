@@ -89,22 +89,26 @@ def c4_stepped(mpg):
 
 @pytest.mark.parametrize("mode,orth", [("mixed", "cgs"), ("mixed", "mgs"), ("baseline", "cgs"), ("mixed", "cgsr")])
 def test_c4_stepped_layout_live_oracle(mpg, oracle, c4_stepped, mode, orth):
-    """C4's full-size SpMV layout (stepped int16 columns, W = 4, CSR-summed
-    boundary slices) in whole solves against the live oracle, on the fused
-    engine and on the operator surface (whose SELL copy is built by the same
-    builder), asserting the layout the engine really ran."""
+    """C4's full-size SpMV layouts in whole solves against the live oracle:
+    the stepped SELL copy (int16 columns, W = 4, CSR-summed boundary slices)
+    and auto's node-block copy on the fused engine, and the operator surface
+    (whose SELL copy is built by the same builder), asserting the layout the
+    engine really ran."""
     A, xt, b = c4_stepped
     opts = dict(mode=mode, orth=orth, prec="jacobi", rlen=30, tol=1e-10, max_restarts=100)
-    eng = mpg.Engine(A, b, xt, **opts)
+    eng = mpg.Engine(A, b, xt, spmv_format="sell", **opts)
     lay, cols = eng.spmv_layout(), eng.sell_columns()
     eng.close()
     assert lay["format"] == "sell" and lay["vec_width"] == 4 and lay["col_bytes"] == 2 and not lay["window"], lay
     assert cols["form"] == "stepped" and 1 <= cols["csr_slices"] <= A.nrows // 64 // 100, cols
+    eng = mpg.Engine(A, b, xt, **opts)  # auto: the node-block copy (streams faster at ~5 % more bytes)
+    assert eng.spmv_layout()["format"] == "node"
+    eng.close()
     ref = oracle.solve(mpg, A, b, xt, **opts)
     assert ref.status == "converged"
-    for engine in ("fused", "surface"):
-        got = mpg.solve(A, b, xt, engine=engine, **opts)
-        compare(as_ref(ref), got, mode, opts["tol"], 30, f"c4-stepped-{mode}-{orth}-{engine}")
+    for engine, fmt in (("fused", "sell"), ("fused", "auto"), ("surface", "auto")):
+        got = mpg.solve(A, b, xt, engine=engine, spmv_format=fmt, **opts)
+        compare(as_ref(ref), got, mode, opts["tol"], 30, f"c4-stepped-{mode}-{orth}-{engine}-{fmt}")
 
 
 def test_c4_full_size_spmv_sell_vs_csr_vs_mkl(hip, mpg, oracle):

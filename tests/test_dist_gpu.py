@@ -246,11 +246,13 @@ def test_p8_band_c5_share_properties(mpg):
     assert abs(np.linalg.norm(r) - many.res_norm) <= 1e-6 * np.linalg.norm(b)
 
 
-def test_host_transport_processes_stencil27(mpg, oracle, tmp_path):
+@pytest.mark.parametrize("fmt", ["sell", "auto"])
+def test_host_transport_processes_stencil27(mpg, oracle, tmp_path, fmt):
     """The C4 structure as 2 separate processes over the host transport: the
     same bits as the 2-rank loopback solve, every rank on the stepped int16
-    layout with its lower halo numbered in front, and the oracle's result at
-    the parity tolerances."""
+    layout (sell) or the node-block copy (auto: the ranks start on node
+    boundaries) with its lower halo numbered in front, and the oracle's
+    result at the parity tolerances."""
     import subprocess
     import sys
 
@@ -259,19 +261,22 @@ def test_host_transport_processes_stencil27(mpg, oracle, tmp_path):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).parent / "dist_host_worker.py"),
-           str(out), spec, mode, orth, prec, str(max_restarts), str(tol)]
+           str(out), spec, mode, orth, prec, str(max_restarts), str(tol), fmt]
     run = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert run.returncode == 0, run.stdout[-3000:] + run.stderr[-3000:]
     got = np.load(out)
     assert str(got["transport_error"]) == ""
-    lay = got["layouts"]  # per rank: [format (1 sell), column form (2 stepped), CSR-summed slices, n_front]
-    assert list(lay[:, 0]) == [1, 1] and list(lay[:, 1]) == [2, 2], lay
+    lay = got["layouts"]  # per rank: [format (1 sell, 2 node), column form (2 stepped), CSR-summed slices, n_front]
+    if fmt == "sell":
+        assert list(lay[:, 0]) == [1, 1] and list(lay[:, 1]) == [2, 2], lay
+    else:
+        assert list(lay[:, 0]) == [2, 2] and list(lay[:, 1]) == [-1, -1], lay
     assert lay[0, 3] == 0 and lay[1, 3] > 0, lay
     A = mpg.gen_stencil27(105, 3, ny=105, nz=8)
     xt = mpg.rand_vect(A.nrows, 42)
     b = mpg.host_spmv(A, xt)
     opts = dict(mode=mode, orth=orth, prec=prec, rlen=30, tol=tol, max_restarts=max_restarts)
-    loop = mpg.solve_loopback(A, b, xt, nranks=2, **opts)
+    loop = mpg.solve_loopback(A, b, xt, nranks=2, spmv_format=fmt, **opts)
     assert list(got["counts"]) == [loop.restarts, loop.inner_k, loop.total_iters]
     assert np.array_equal(got["step_res"], loop.step_res) and np.array_equal(got["x"], loop.x)
     ref = oracle.solve(mpg, A, b, xt, **opts)
