@@ -471,16 +471,17 @@ __global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict_
 // ---------------------------------------------------------------- step: SpMV (node blocks)
 // Same contract as k_step_spmv on the node-block copy (node_tile.hpp): one
 // tile of node rows per workgroup, the CSR tile's products and row order.
-// TPW > 1: each workgroup walks TPW consecutive tiles, the next tile's
-// records in flight during this one's gathers and row sums (node_tiles).
-template <class T, class P, class VI, bool FOLD, int TPW = 1>
+// WALK: each workgroup walks tpw consecutive tiles, the next tile's records
+// in flight during this one's gathers and row sums (node_tiles); else one
+// tile per workgroup (node_tile).
+template <class T, class P, class VI, bool FOLD, bool WALK = true>
 __global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict__ tiles,
                                                       const int32_t* __restrict__ bptr, const char* __restrict__ recs,
                                                       const T* __restrict__ wprev, const T* __restrict__ inv_p,
                                                       T* __restrict__ V, int64_t ld, int k,
                                                       const P* __restrict__ diag, T* __restrict__ w,
                                                       GivensFold<T> fold, const int8_t* __restrict__ rexp,
-                                                      int ntiles, int64_t nblk) {
+                                                      int ntiles, int64_t nblk, int tpw) {
     __shared__ double prod[kNodeProd];
     const T inv = fold_givens<FOLD>(fold, inv_p);
     T* __restrict__ Vk = V + (int64_t)k * ld;
@@ -498,10 +499,10 @@ __global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict_
         w[i] = (T)pw;
         Vk[i] = o.wp * inv;
     };
-    if constexpr (TPW == 1) {
+    if constexpr (!WALK) {
         node_tile<VI>(blockIdx.x, tiles, bptr, recs, xval, pre, epi, prod);
     } else {
-        const int t0 = blockIdx.x * TPW, t1 = t0 + TPW < ntiles ? t0 + TPW : ntiles;
+        const int t0 = blockIdx.x * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
         node_tiles<VI>(t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, xval, pre, epi, prod);
     }
 }
@@ -1797,14 +1798,19 @@ int csr_mode() {
     return e && *e >= '0' && *e <= '4' ? *e - '0' : 0;
 }
 
-// MPG_NODE_TPW (the node-block SpMV, k_step_node<..., TPW>): tiles per
-// workgroup, 1 (one tile each) or 2 (default) / 4 / 8 (pipelined walk).
-// Measured (profiles/r05_node_ab.jsonl): fem27 248 / 218 / 215-228 / 223 us,
-// C4's stencil 341 / 295 / 300 / 306 us.
-int node_tpw() {
+// Tiles per workgroup of the node-block SpMV (MPG_NODE_TPW: 1 one tile
+// each, N > 1 a pipelined walk of N tiles; default 2; 0: as many as keep
+// the grid at kNodeGroups workgroups, so the Givens step folds in).
+// Measured (profiles/r05_node_ab.jsonl): fem27 248 / 218 / 215-228 / 223-238
+// / 255 us at 1 / 2 / 4 / 8 / 16 (auto, folded: 247), C4's stencil 341 /
+// 295-312 / 300 / 306-334 / 345 (auto 355): longer walks leave the grid's
+// tail to fewer workgroups, two tiles in flight is the gain.
+constexpr int kNodeGroups = 2048;
+int node_tpw(const NodeCopy& S) {
     const char* e = std::getenv("MPG_NODE_TPW");
     const int v = e && *e ? std::atoi(e) : 2;
-    return v == 2 || v == 4 || v == 8 ? v : 1;
+    if (v >= 1) return v;
+    return std::max(2, (S.ntiles + kNodeGroups - 1) / kNodeGroups);
 }
 
 int row_grid(const mpg_arnoldi* a) { return a->G; }
@@ -1827,11 +1833,13 @@ int64_t sell_copy_bytes(const mpg_arnoldi* a);
 
 // the Arnoldi SpMV's copy of the inner-precision values: SELL-64, node
 // blocks or none (CSR row blocks). Auto (format 0) takes the node-block copy
-// when the matrix has one and it streams at most 10 % more bytes than what
-// auto would run otherwise: the SpMV is HBM-bound, and the node records
-// stream faster than the SELL copies (C4's stencil: 1506 MB in 295 us against
-// the stepped SELL copy's 1438 MB in 324 us; 3-dof FEM: 4.44 B per fp32
-// nonzero against CSR's 8). MPG_NODE=0: never.
+// when the matrix has one and it streams fewer bytes than what auto would
+// run otherwise (the SpMV is HBM-bound; 3-dof FEM: 4.44 B per fp32 nonzero
+// against CSR's 8), or at most 10 % more when x outgrows an XCD's 4 MB L2:
+// there the SELL copies' per-entry gathers cost more than the node records'
+// one per block (C4's stencil, x 16 MB: 1506 MB in 295-312 us against the
+// stepped SELL copy's 1438 MB in 324 us; one eighth of it, x 2.2 MB: SELL
+// 36 us, node 41 us). MPG_NODE=0: never.
 int arnoldi_sell_build(mpg_arnoldi* a, int format) {
     if (format == 3) return node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, true, a->node);
     if (int st = sell_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, format, a->sell)) return st;
@@ -1843,7 +1851,9 @@ int arnoldi_sell_build(mpg_arnoldi* a, int format) {
             const int64_t vb = a->d.inner_val == MPG_F64 ? 8 : a->d.inner_val == MPG_F32 ? 4 : 2;
             const int64_t now = a->sell.nslices > 0 ? sell_copy_bytes(a)
                                                     : a->d.A->nnz * (4 + vb) + ((int64_t)a->d.n + 1) * 4;
-            if (node_bytes(nc) * 10 < now * 11) {
+            // (x past one XCD's 4 MB L2: the gathers dominate, 10 % slack)
+            const bool big_x = (int64_t)a->d.n_ext * a->tsize > ((int64_t)4 << 20);
+            if (node_bytes(nc) * 10 < now * (big_x ? 11 : 10)) {
                 sell_free(a->sell);
                 a->node = nc;
                 return MPG_OK;
@@ -2218,19 +2228,17 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
         }
         if (a->node.nblk > 0) {
             const NodeCopy& S = a->node;
-            auto go = [&](auto kern, int tpw) {
+            const int tpw = node_tpw(S);
+            auto go = [&](auto kern) {
                 launch_timed(a->ctx, kern, dim3((S.ntiles + tpw - 1) / tpw), dim3(kBlock),
                              static_cast<const int32_t*>(S.tiles), static_cast<const int32_t*>(S.bptr),
                              static_cast<const char*>(S.recs), static_cast<const T*>(a->w[k & 1]),
                              static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k, diag,
-                             static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp, S.ntiles, S.nblk);
+                             static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp, S.ntiles, S.nblk, tpw);
                 return (int)MPG_OK;
             };
-            const int tpw = node_tpw();
-            if (tpw == 2) return fold ? go(k_step_node<T, P, VI, true, 2>, 2) : go(k_step_node<T, P, VI, false, 2>, 2);
-            if (tpw == 4) return fold ? go(k_step_node<T, P, VI, true, 4>, 4) : go(k_step_node<T, P, VI, false, 4>, 4);
-            if (tpw == 8) return fold ? go(k_step_node<T, P, VI, true, 8>, 8) : go(k_step_node<T, P, VI, false, 8>, 8);
-            return fold ? go(k_step_node<T, P, VI, true>, 1) : go(k_step_node<T, P, VI, false>, 1);
+            if (tpw > 1) return fold ? go(k_step_node<T, P, VI, true>) : go(k_step_node<T, P, VI, false>);
+            return fold ? go(k_step_node<T, P, VI, true, false>) : go(k_step_node<T, P, VI, false, false>);
         }
         const int mode = csr_mode();
         auto kern = mode == 1   ? (fold ? k_step_spmv<T, P, VI, true, 1> : k_step_spmv<T, P, VI, false, 1>)
@@ -2276,6 +2284,10 @@ int mpg_arnoldi_fold_pays(mpg_arnoldi_t a) {
     if (!a) return 0;
     const char* env = std::getenv("MPG_FOLD_MAX_GROUPS");
     const int64_t limit = env && *env ? std::atoll(env) : kFoldMaxGroups;
+    if (a->node.nblk > 0) {
+        const int tpw = node_tpw(a->node);
+        return (a->node.ntiles + tpw - 1) / tpw <= limit ? 1 : 0;
+    }
     const SellCopy& S = a->sell;
     if (S.nslices == 0) return a->Grb <= limit ? 1 : 0;
     const int per_group = (kStepSellBlock / kWave) * (sell_uniform(S) && sell_pair(S) ? 2 : 1);

@@ -91,7 +91,7 @@ def c4_stepped(mpg):
 def test_c4_stepped_layout_live_oracle(mpg, oracle, c4_stepped, mode, orth):
     """C4's full-size SpMV layouts in whole solves against the live oracle:
     the stepped SELL copy (int16 columns, W = 4, CSR-summed boundary slices)
-    and auto's node-block copy on the fused engine, and the operator surface
+    and the node-block copy on the fused engine, and the operator surface
     (whose SELL copy is built by the same builder), asserting the layout the
     engine really ran."""
     A, xt, b = c4_stepped
@@ -101,12 +101,12 @@ def test_c4_stepped_layout_live_oracle(mpg, oracle, c4_stepped, mode, orth):
     eng.close()
     assert lay["format"] == "sell" and lay["vec_width"] == 4 and lay["col_bytes"] == 2 and not lay["window"], lay
     assert cols["form"] == "stepped" and 1 <= cols["csr_slices"] <= A.nrows // 64 // 100, cols
-    eng = mpg.Engine(A, b, xt, **opts)  # auto: the node-block copy (streams faster at ~5 % more bytes)
-    assert eng.spmv_layout()["format"] == "node"
+    eng = mpg.Engine(A, b, xt, spmv_format="node", **opts)
+    assert eng.spmv_layout()["format"] == "node" and eng.spmv_layout()["stored"] == A.nnz
     eng.close()
     ref = oracle.solve(mpg, A, b, xt, **opts)
     assert ref.status == "converged"
-    for engine, fmt in (("fused", "sell"), ("fused", "auto"), ("surface", "auto")):
+    for engine, fmt in (("fused", "sell"), ("fused", "node"), ("surface", "auto")):
         got = mpg.solve(A, b, xt, engine=engine, spmv_format=fmt, **opts)
         compare(as_ref(ref), got, mode, opts["tol"], 30, f"c4-stepped-{mode}-{orth}-{engine}-{fmt}")
 

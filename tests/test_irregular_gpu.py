@@ -184,10 +184,10 @@ def test_node_blocks_refused(mpg):
         eng.close()
 
 
-@pytest.mark.parametrize("tpw", ["2", "4", "8"])
+@pytest.mark.parametrize("tpw", ["2", "4", "8", "0"])
 @pytest.mark.parametrize("which", ["stencil27", "fem27p"])
 def test_node_tile_walk_same_bits(mpg, which, tpw, monkeypatch):
-    """MPG_NODE_TPW: each workgroup walks 2 / 4 / 8 consecutive tiles with the
+    """MPG_NODE_TPW: each workgroup walks 2 / 4 / 8 (0: auto) consecutive tiles with the
     next tile's records in flight (node_tiles) -- the same tiles, products
     and row order as one tile per workgroup: the same bits."""
     A, xt, b = _node_problem(mpg, which)
