@@ -95,6 +95,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_create.argtypes = [C.POINTER(SolveArgs), C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
     lib.mpg_cycle_program_counts.argtypes = [C.POINTER(_I64)] * 3
     lib.mpg_surface_ride_counts.argtypes = [C.POINTER(_I64)] * 3
+    lib.mpg_surface_spmv_counts.argtypes = [C.POINTER(_I64)] * 3
     lib.mpg_engine_report.argtypes = [C.c_void_p, C.POINTER(SolveResult)]
     lib.mpg_engine_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     lib.mpg_engine_sync.argtypes = [C.c_void_p]
@@ -498,6 +499,14 @@ def surface_ride_counts() -> dict:
     v = [_I64() for _ in range(3)]
     host_lib().mpg_surface_ride_counts(*[C.byref(x) for x in v])
     return {"redirects": v[0].value, "rides": v[1].value, "flushed": v[2].value}
+
+
+def surface_spmv_counts() -> dict:
+    """The operator surface's spmv calls on this thread so far by storage
+    (mpg_surface_spmv_counts): node blocks, SELL-64, CSR."""
+    v = [_I64() for _ in range(3)]
+    host_lib().mpg_surface_spmv_counts(*[C.byref(x) for x in v])
+    return {"node": v[0].value, "sell": v[1].value, "csr": v[2].value}
 
 
 def row_slice(A: Csr, r0: int, r1: int) -> Csr:

@@ -1807,8 +1807,7 @@ int csr_mode() {
 // tail to fewer workgroups, two tiles in flight is the gain.
 constexpr int kNodeGroups = 2048;
 int node_tpw(const NodeCopy& S) {
-    const char* e = std::getenv("MPG_NODE_TPW");
-    const int v = e && *e ? std::atoi(e) : 2;
+    const int v = node_tpw_default();
     if (v >= 1) return v;
     return std::max(2, (S.ntiles + kNodeGroups - 1) / kNodeGroups);
 }
@@ -1833,13 +1832,9 @@ int64_t sell_copy_bytes(const mpg_arnoldi* a);
 
 // the Arnoldi SpMV's copy of the inner-precision values: SELL-64, node
 // blocks or none (CSR row blocks). Auto (format 0) takes the node-block copy
-// when the matrix has one and it streams fewer bytes than what auto would
-// run otherwise (the SpMV is HBM-bound; 3-dof FEM: 4.44 B per fp32 nonzero
-// against CSR's 8), or at most 10 % more when x outgrows an XCD's 4 MB L2:
-// there the SELL copies' per-entry gathers cost more than the node records'
-// one per block (C4's stencil, x 16 MB: 1506 MB in 295-312 us against the
-// stepped SELL copy's 1438 MB in 324 us; one eighth of it, x 2.2 MB: SELL
-// 36 us, node 41 us). MPG_NODE=0: never.
+// when the matrix has one and node_wins over what auto would run otherwise
+// (the SpMV is HBM-bound; 3-dof FEM: 4.44 B per fp32 nonzero against CSR's
+// 8). MPG_NODE=0: never.
 int arnoldi_sell_build(mpg_arnoldi* a, int format) {
     if (format == 3) return node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, true, a->node);
     if (int st = sell_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, format, a->sell)) return st;
@@ -1851,9 +1846,7 @@ int arnoldi_sell_build(mpg_arnoldi* a, int format) {
             const int64_t vb = a->d.inner_val == MPG_F64 ? 8 : a->d.inner_val == MPG_F32 ? 4 : 2;
             const int64_t now = a->sell.nslices > 0 ? sell_copy_bytes(a)
                                                     : a->d.A->nnz * (4 + vb) + ((int64_t)a->d.n + 1) * 4;
-            // (x past one XCD's 4 MB L2: the gathers dominate, 10 % slack)
-            const bool big_x = (int64_t)a->d.n_ext * a->tsize > ((int64_t)4 << 20);
-            if (node_bytes(nc) * 10 < now * (big_x ? 11 : 10)) {
+            if (node_wins(node_bytes(nc), now, (int64_t)a->d.n_ext * a->tsize)) {
                 sell_free(a->sell);
                 a->node = nc;
                 return MPG_OK;
@@ -1951,19 +1944,7 @@ int64_t mpg_arnoldi_sell_matrix_bytes(mpg_arnoldi_t a) {
 
 namespace {
 int64_t sell_copy_bytes(const mpg_arnoldi* a) {
-    const SellCopy& S = a->sell;
-    const int64_t vbytes = S.vtype == MPG_F64 ? 8 : S.vtype == MPG_F32 ? 4 : 2;
-    const int64_t steps = S.padded / ((int64_t)kWave * S.W);
-    // every slot's value; the columns of slots outside implicit slices (the
-    // shared patterns are a few cache lines); int64 slice offsets; the
-    // pattern indices; the stepped form's bases; a scaled fp16 copy's row
-    // exponents
-    // (shared column blocks: the distinct blocks once, plus the per-slice
-    // column starts)
-    return S.padded * vbytes + S.col_slots * S.col_bytes() + S.npat * S.col_bytes() +
-           ((int64_t)S.nslices + 1) * 8 + (S.spat ? (int64_t)S.nslices * 4 : 0) + (S.c16s ? steps * S.W * 4 : 0) +
-           (S.coff ? (int64_t)S.nslices * 8 : 0) + (a->d.inner_row_exp ? (int64_t)a->d.n : 0) +
-           (S.rows ? (int64_t)S.nslices * kWave * 4 : 0);
+    return sell_matrix_bytes(a->sell) + (a->d.inner_row_exp ? (int64_t)a->d.n : 0);
 }
 }  // namespace
 

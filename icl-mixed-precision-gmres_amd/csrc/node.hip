@@ -2,6 +2,8 @@
 #include "node_tile.hpp"
 
 #include <algorithm>
+#include <cstdlib>
+#include <new>
 #include <vector>
 
 using namespace mpg;
@@ -70,9 +72,38 @@ __global__ __launch_bounds__(kBlock) void k_node_fill(int nn, const int32_t* __r
     }
 }
 
+// y = alpha * A x + beta * y over the node copy: the CSR tile's epilogue
+// (spmv.hip k_csr_adaptive) on node_tiles' row sums
+template <class VI, class X>
+__global__ __launch_bounds__(kBlock) void k_node_spmv(const int32_t* __restrict__ tiles,
+                                                      const int32_t* __restrict__ bptr, const char* __restrict__ recs,
+                                                      int ntiles, int64_t nblk, int tpw, const X* __restrict__ x,
+                                                      X alpha, X beta, X* __restrict__ y) {
+    __shared__ double prod[kNodeProd];
+    const int t0 = blockIdx.x * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
+    node_tiles<VI>(
+        t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, [&](int c) { return (double)x[c]; },
+        [&](int i) { return beta == X(0) ? X(0) : y[i]; },
+        [&](int i, double sum, X yi) {
+            const X t = (X)sum;
+            y[i] = beta == X(0) ? alpha * t : alpha * t + beta * yi;
+        },
+        prod);
+}
+
 }  // namespace
 
+struct mpg_node {
+    mpg_ctx* ctx = nullptr;
+    mpg::NodeCopy S;
+};
+
 namespace mpg {
+
+int node_tpw_default() {
+    const char* e = std::getenv("MPG_NODE_TPW");
+    return e && *e ? std::atoi(e) : 2;
+}
 
 int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool required, NodeCopy& S) {
     S = NodeCopy{};
@@ -152,3 +183,67 @@ int64_t node_bytes(const NodeCopy& S) {
 }
 
 }  // namespace mpg
+
+template <class X>
+static int node_spmv_impl(mpg_ctx_t ctx, mpg_node_t A, X alpha, const X* x, X beta, X* y) {
+    if (!ctx || !A) return MPG_ERR_ARG;
+    if (A->S.vtype != (sizeof(X) == 8 ? MPG_F64 : MPG_F32)) return MPG_ERR_ARG;
+    if (A->S.ntiles == 0) return MPG_OK;
+    int tpw = node_tpw_default();
+    if (tpw < 1) tpw = 2;
+    using VI = std::conditional_t<sizeof(X) == 8, double, float>;
+    k_node_spmv<VI, X><<<(A->S.ntiles + tpw - 1) / tpw, kBlock, 0, ctx->stream>>>(
+        A->S.tiles, A->S.bptr, static_cast<const char*>(A->S.recs), A->S.ntiles, A->S.nblk, tpw, x, alpha, beta, y);
+    MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+
+extern "C" {
+
+int mpg_node_create(mpg_ctx_t ctx, mpg_csr_t A, int32_t vtype, const void* vals, int64_t alt_bytes,
+                    mpg_node_t* out) {
+    if (!ctx || !A || !out || (A->nnz > 0 && !vals)) return MPG_ERR_ARG;
+    if (vtype != MPG_F64 && vtype != MPG_F32) return MPG_ERR_UNSUPPORTED;
+    *out = nullptr;
+    mpg_node* h = new (std::nothrow) mpg_node();
+    if (!h) return MPG_ERR_ALLOC;
+    h->ctx = ctx;
+    if (int st = node_build(ctx, A, vtype, vals, false, h->S)) {
+        delete h;
+        return st;
+    }
+    const int64_t xb = (int64_t)A->cols * (vtype == MPG_F64 ? 8 : 4);
+    if (h->S.nblk == 0 || (alt_bytes >= 0 && !node_wins(node_bytes(h->S), alt_bytes, xb))) {
+        node_free(h->S);
+        delete h;
+        return MPG_OK;
+    }
+    *out = h;
+    return MPG_OK;
+}
+
+int mpg_node_destroy(mpg_node_t A) {
+    if (!A) return MPG_OK;
+    if (A->ctx) (void)hipStreamSynchronize(A->ctx->stream);
+    node_free(A->S);
+    delete A;
+    return MPG_OK;
+}
+
+int mpg_node_layout(mpg_node_t A, int64_t* blocks, int32_t* tiles, int64_t* bytes) {
+    if (!A) return MPG_ERR_ARG;
+    if (blocks) *blocks = A->S.nblk;
+    if (tiles) *tiles = A->S.ntiles;
+    if (bytes) *bytes = node_bytes(A->S);
+    return MPG_OK;
+}
+
+int mpg_node_spmv_f64(mpg_ctx_t ctx, mpg_node_t A, double alpha, const double* x, double beta, double* y) {
+    return node_spmv_impl(ctx, A, alpha, x, beta, y);
+}
+int mpg_node_spmv_f32(mpg_ctx_t ctx, mpg_node_t A, float alpha, const float* x, float beta, float* y) {
+    return node_spmv_impl(ctx, A, alpha, x, beta, y);
+}
+
+}  // extern "C"

@@ -51,6 +51,18 @@ void node_free(NodeCopy& S);
 // bytes the Arnoldi SpMV streams from the copy: records, block and tile starts
 int64_t node_bytes(const NodeCopy& S);
 
+// The node copy over an alternative streaming alt bytes: fewer bytes, or
+// at most 10 % more when x (x_bytes) outgrows an XCD's 4 MB L2, where the
+// alternative's per-entry gathers cost more than the node records' one per
+// block (C4's stencil, x 16 MB: node 1506 MB in 295-312 us against the
+// stepped SELL copy's 1438 MB in 324 us; one eighth of it, x 2.2 MB: SELL
+// 36 us, node 41 us; profiles/r05_node_ab.jsonl).
+inline bool node_wins(int64_t node, int64_t alt, int64_t x_bytes) {
+    return node * 10 < alt * (x_bytes > ((int64_t)4 << 20) ? 11 : 10);
+}
+// tiles per workgroup of the pipelined walk (node_tiles): MPG_NODE_TPW, default 2
+int node_tpw_default();
+
 inline int node_rec_bytes(int vtype) { return vtype == MPG_F64 ? 80 : vtype == MPG_F32 ? 40 : 24; }
 
 template <class VI> struct NodeRec;

@@ -865,6 +865,20 @@ int sell_share_columns(SellCopy& S, const std::vector<int64_t>& off, const std::
     return cleanup(MPG_OK);
 }
 
+int64_t sell_matrix_bytes(const SellCopy& S) {
+    if (S.nslices == 0) return 0;
+    const int64_t vbytes = S.vtype == MPG_F64 ? 8 : S.vtype == MPG_F32 ? 4 : 2;
+    const int64_t steps = S.padded / ((int64_t)kWave * S.W);
+    // every slot's value; the columns of slots outside implicit slices (the
+    // shared patterns are a few cache lines); int64 slice offsets; the
+    // pattern indices; the stepped form's bases; a sorted copy's row numbers
+    // (shared column blocks: the distinct blocks once, plus the per-slice
+    // column starts)
+    return S.padded * vbytes + S.col_slots * S.col_bytes() + S.npat * S.col_bytes() +
+           ((int64_t)S.nslices + 1) * 8 + (S.spat ? (int64_t)S.nslices * 4 : 0) + (S.c16s ? steps * S.W * 4 : 0) +
+           (S.coff ? (int64_t)S.nslices * 8 : 0) + (S.rows ? (int64_t)S.nslices * kWave * 4 : 0);
+}
+
 void sell_free(SellCopy& S) {
     if (S.sbase) (void)hipFree(S.sbase);
     if (S.spat) (void)hipFree(S.spat);
@@ -979,6 +993,8 @@ int mpg_sell_layout(mpg_sell_t A, int32_t* vec_width, int32_t* col_bytes, int64_
 }
 
 int64_t mpg_sell_shared_slices(mpg_sell_t A) { return A ? A->S.nshared : -1; }
+
+int64_t mpg_sell_bytes(mpg_sell_t A) { return A ? sell_matrix_bytes(A->S) : -1; }
 
 int mpg_sell_columns(mpg_sell_t A, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices) {
     if (!A) return MPG_ERR_ARG;

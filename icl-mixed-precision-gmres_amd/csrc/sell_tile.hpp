@@ -346,6 +346,8 @@ struct SellCopy {
 // entries), 1 never, 2 always. Synchronises the context's stream.
 int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int format, SellCopy& S);
 void sell_free(SellCopy& S);
+// matrix bytes one SpMV over the copy reads (mpg_sell_bytes)
+int64_t sell_matrix_bytes(const SellCopy& S);
 
 // f(column type, integral_constant<int, W>) for the copy's layout
 template <class F>

@@ -76,6 +76,11 @@ bool surface_sell_enabled() {
     const char* env = std::getenv("MPG_SURFACE_SELL");
     return !(env && *env == '0');
 }
+// MPG_SURFACE_NODE=0: never the node-block copy (SELL or CSR as before)
+bool surface_node_enabled() {
+    const char* env = std::getenv("MPG_SURFACE_NODE");
+    return !(env && *env == '0');
+}
 
 // ---- scalar-op batching ----
 // Consecutive scalar operators (rotg, rot, rot_vec, scalar copy/scal: the
@@ -199,6 +204,7 @@ struct Scratch {
 };
 thread_local Scratch tl_scratch;
 thread_local int64_t tl_ride_counts[3] = {0, 0, 0};  // redirects, rides, flushed
+thread_local int64_t tl_spmv_counts[3] = {0, 0, 0};  // spmv calls on node blocks, SELL, CSR
 
 // the scratch copy for w (kept per thread and context; never (re)allocated
 // while the context's stream records a cycle program)
@@ -710,6 +716,13 @@ void set_redirect(mpg_ctx_t c, void* w, void* sp, int64_t n, bool f64) {
 }
 }  // namespace mpg
 
+extern "C" int mpg_surface_spmv_counts(int64_t* node, int64_t* sell, int64_t* csr) {
+    if (node) *node = mpg::tl_spmv_counts[0];
+    if (sell) *sell = mpg::tl_spmv_counts[1];
+    if (csr) *csr = mpg::tl_spmv_counts[2];
+    return MPG_OK;
+}
+
 extern "C" int mpg_surface_ride_counts(int64_t* redirects, int64_t* rides, int64_t* flushed) {
     if (redirects) *redirects = mpg::tl_ride_counts[0];
     if (rides) *rides = mpg::tl_ride_counts[1];
@@ -880,7 +893,11 @@ template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Ve
                                    Vect<double, Hip> y) {
     assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
                              : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
-    if (mpg_sell_t s = A.sell()) {
+    if (mpg_node_t nd = A.node()) {
+        check(mpg_node_spmv_f64(C, nd, alpha, x.data(), beta, y.data()), "spmv (node blocks)");
+        ++mpg::tl_spmv_counts[0];
+    } else if (mpg_sell_t s = A.sell()) {
+        ++mpg::tl_spmv_counts[1];
         mpg_scalar_op ops[MPG_SCALAR_PROGRAM_MAX];
         int nops = 0;
         mpg_ctx_t c = nullptr;
@@ -901,13 +918,18 @@ template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Ve
               "spmv");
     } else {
         check(mpg_csr_spmv_f64(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
+        ++mpg::tl_spmv_counts[2];
     }
 }
 template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<float, Hip> x, float beta,
                                   Vect<float, Hip> y) {
     assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
                              : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
-    if (mpg_sell_t s = A.sell()) {
+    if (mpg_node_t nd = A.node()) {
+        check(mpg_node_spmv_f32(C, nd, alpha, x.data(), beta, y.data()), "spmv (node blocks)");
+        ++mpg::tl_spmv_counts[0];
+    } else if (mpg_sell_t s = A.sell()) {
+        ++mpg::tl_spmv_counts[1];
         mpg_scalar_op ops[MPG_SCALAR_PROGRAM_MAX];
         int nops = 0;
         mpg_ctx_t c = nullptr;
@@ -928,6 +950,7 @@ template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<
               "spmv");
     } else {
         check(mpg_csr_spmv_f32(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
+        ++mpg::tl_spmv_counts[2];
     }
 }
 template <> void jacobi_diag<double, Hip>(SparseMatrix<double, Hip> A, Vect<double, Hip> d) {

@@ -66,17 +66,23 @@ public:
 // the copies of that matrix (spmv takes A by value) and built on its first
 // non-transposed spmv, when the values are final. Absent (h == nullptr) when
 // slicing would not pay (format 0: padding > 20 %) or MPG_SURFACE_SELL=0.
+// Round 5: the node-block copy (mpg_node_create) is built beside it on
+// matrices of 3-dof nodes and replaces it when it streams fewer bytes
+// (node_tile.hpp node_wins; MPG_SURFACE_NODE=0: never).
 struct SellHolder {
     bool tried = false;
     mpg_sell_t h = nullptr;
+    mpg_node_t node = nullptr;
     SellHolder() = default;
     SellHolder(const SellHolder&) = delete;
     SellHolder& operator=(const SellHolder&) = delete;
     ~SellHolder() {
         if (h) mpg_sell_destroy(h);
+        if (node) mpg_node_destroy(node);
     }
 };
 bool surface_sell_enabled();
+bool surface_node_enabled();
 
 // Device CSR structure shared by every precision of one matrix.
 struct CsrStructure {
@@ -260,20 +266,36 @@ public:
     mpg_csr_t csr() const { return s_->csr.get(); }
     Vect<Type, Hip> vals_vect() const { return vals_; }
 
-    // the sliced copy spmv runs on, or nullptr (CSR): A only, not A^T
+    // the sliced copy spmv runs on, or nullptr (node blocks or CSR): A only, not A^T
     mpg_sell_t sell() const {
-        if (trans_ || !sell_) return nullptr;
-        if (!sell_->tried) {
-            sell_->tried = true;
-            if (mpg::surface_sell_enabled() && s_->nnz > 0)
-                mpg::check(mpg_sell_create(mpg::current_ctx(), csr(), sizeof(Type) == 8 ? 0 : 1, vals_.data(), 0,
-                                           &sell_->h),
-                           "mpg_sell_create");
-        }
-        return sell_->h;
+        build_copies();
+        return trans_ || !sell_ ? nullptr : sell_->h;
+    }
+    // the node-block copy spmv runs on, or nullptr: A only, not A^T
+    mpg_node_t node() const {
+        build_copies();
+        return trans_ || !sell_ ? nullptr : sell_->node;
     }
 
 private:
+    // SELL (format 0), then the node copy against the SELL copy's bytes or
+    // the CSR arrays' (the one of the two that streams less is kept)
+    void build_copies() const {
+        if (trans_ || !sell_ || sell_->tried) return;
+        sell_->tried = true;
+        if (s_->nnz == 0) return;
+        const int32_t vt = sizeof(Type) == 8 ? 0 : 1;
+        if (mpg::surface_sell_enabled())
+            mpg::check(mpg_sell_create(mpg::current_ctx(), csr(), vt, vals_.data(), 0, &sell_->h), "mpg_sell_create");
+        if (!mpg::surface_node_enabled()) return;
+        const int64_t alt = sell_->h ? mpg_sell_bytes(sell_->h)
+                                     : s_->nnz * (int64_t)(sizeof(Type) + 4) + ((int64_t)s_->m + 1) * 4;
+        mpg::check(mpg_node_create(mpg::current_ctx(), csr(), vt, vals_.data(), alt, &sell_->node), "mpg_node_create");
+        if (sell_->node && sell_->h) {
+            mpg_sell_destroy(sell_->h);
+            sell_->h = nullptr;
+        }
+    }
     std::shared_ptr<mpg::SellHolder> sell_ = std::make_shared<mpg::SellHolder>();
     bool trans_ = false;
     Vect<Type, Hip> tvals_;  // values in A^T's CSR order (set_transpose)

@@ -45,6 +45,7 @@ typedef enum {
 typedef struct mpg_ctx* mpg_ctx_t;   /* one per (GPU, host thread) */
 typedef struct mpg_csr* mpg_csr_t;   /* analysed CSR structure (row blocks) */
 typedef struct mpg_sell* mpg_sell_t; /* SELL-64 copy of one CSR value array */
+typedef struct mpg_node* mpg_node_t; /* node-block copy (3 x 3 blocks) of one CSR value array */
 
 const char* mpg_error_string(int status);
 /* Last HIP error text recorded in this context (for diagnostics). */
@@ -326,9 +327,33 @@ int mpg_sell_columns(mpg_sell_t A, int32_t* form, int64_t* csr_slices, int64_t* 
  * blocks are stored once per distinct block (the interior slices of a
  * stencil with the same boundary pattern share one); -1 for NULL */
 int64_t mpg_sell_shared_slices(mpg_sell_t A);
+/* matrix bytes one SpMV over the copy reads (values, columns outside
+ * implicit slices, slice offsets, pattern indices, stepped bases, a sorted
+ * copy's row numbers); -1 for NULL */
+int64_t mpg_sell_bytes(mpg_sell_t A);
 int mpg_sell_spmv_f64(mpg_ctx_t ctx, mpg_sell_t A, double alpha, const double* x, double beta, double* y);
 int mpg_sell_spmv_f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y);
 int mpg_sell_spmv_f16f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* x, float beta, float* y);
+
+/* ---- node-block SpMV: the same y = alpha*A x + beta*y (kernels_mkl.cpp:
+ * 326-352) on a copy for matrices of 3-dof nodes (rows 3r .. 3r + 2 made of
+ * the same column triples c, c + 1, c + 2 in the same storage positions:
+ * mpg_csr_node_dof, dist.h): one record per 3 x 3 block, the block's first
+ * column and its 9 values (4.44 B per fp32 nonzero against CSR's 8), the
+ * CSR tile's fp64 products and row order -- the bits of mpg_csr_spmv.
+ * mpg_node_create copies one value array (vtype MPG_F64 | MPG_F32) of an
+ * analysed CSR. alt_bytes < 0: build whenever A has the structure; else only
+ * when the copy streams fewer bytes than alt_bytes (the copy the caller
+ * would otherwise run: mpg_sell_bytes, or the CSR arrays), or at most 10 %
+ * more when x is larger than one XCD's 4 MB L2 (node_tile.hpp). *out = NULL
+ * when it is not built. Owns its device memory; synchronises. */
+int mpg_node_create(mpg_ctx_t ctx, mpg_csr_t A, int32_t vtype, const void* vals, int64_t alt_bytes,
+                    mpg_node_t* out);
+int mpg_node_destroy(mpg_node_t A);
+/* blocks, tiles (runs of node rows of <= 256 blocks) and the bytes one SpMV reads */
+int mpg_node_layout(mpg_node_t A, int64_t* blocks, int32_t* tiles, int64_t* bytes);
+int mpg_node_spmv_f64(mpg_ctx_t ctx, mpg_node_t A, double alpha, const double* x, double beta, double* y);
+int mpg_node_spmv_f32(mpg_ctx_t ctx, mpg_node_t A, float alpha, const float* x, float beta, float* y);
 /* The same SpMV with a scalar program (mpg_scalar_program) run by one extra
  * workgroup of the launch, concurrently with the rows: for a program whose
  * operands the SpMV neither reads nor writes (the caller checks). Replaces

@@ -194,6 +194,10 @@ int mpg_cycle_program_counts(int64_t* recorded, int64_t* replayed, int64_t* void
  * separately instead (a call other than the SpMV came next). Any pointer
  * may be NULL. */
 int mpg_surface_ride_counts(int64_t* redirects, int64_t* rides, int64_t* flushed);
+/* The operator surface's spmv calls on this thread so far, by the storage
+ * they ran on: node blocks (mpg_node_spmv_*), SELL-64, CSR. Pointers may be
+ * NULL. */
+int mpg_surface_spmv_counts(int64_t* node, int64_t* sell, int64_t* csr);
 
 #ifdef __cplusplus
 }

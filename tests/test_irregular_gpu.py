@@ -198,3 +198,33 @@ def test_node_tile_walk_same_bits(mpg, which, tpw, monkeypatch):
     monkeypatch.setenv("MPG_NODE_TPW", tpw)
     got = mpg.solve(A, b, xt, **opts)
     assert np.array_equal(got.step_res, ref.step_res) and np.array_equal(got.x, ref.x)
+
+
+@pytest.mark.parametrize("mode,orth", [("mixed", "cgs"), ("baseline", "mgs"), ("single", "cgsr")])
+@pytest.mark.parametrize("which", ["stencil27", "fem27", "fem27p"])
+def test_surface_node_blocks_same_bits(mpg, which, mode, orth, monkeypatch):
+    """The operator surface (kernels_hip.cpp spmv, the reference's
+    kernels.hpp boundary) runs A's SpMV on the node-block copy when it
+    streams fewer bytes than the SELL copy or the CSR arrays: whole solves
+    give the bits of the same surface with the copy off (MPG_SURFACE_NODE=0:
+    SELL or CSR, which sum every row in CSR order too), and the counts show
+    which storage each ran on."""
+    A, xt, b = _node_problem(mpg, which)
+    opts = dict(engine="surface", mode=mode, orth=orth, prec="jacobi", rlen=30, tol=0.0, max_restarts=3)
+    got = {}
+    for env in ("", "0"):
+        if env:
+            monkeypatch.setenv("MPG_SURFACE_NODE", env)
+        else:
+            monkeypatch.delenv("MPG_SURFACE_NODE", raising=False)
+        before = mpg.surface_spmv_counts()
+        got[env] = mpg.solve(A, b, xt, **opts)
+        after = mpg.surface_spmv_counts()
+        d = {k: after[k] - before[k] for k in after}
+        if env:
+            assert d["node"] == 0 and d["sell"] + d["csr"] > 0, d
+        else:
+            assert d["node"] > 0 and d["sell"] == 0, d
+    ref, g = got["0"], got[""]
+    assert g.total_iters == ref.total_iters == 90
+    assert np.array_equal(g.step_res, ref.step_res) and np.array_equal(g.x, ref.x) and g.res_norm == ref.res_norm

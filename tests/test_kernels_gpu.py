@@ -9,6 +9,7 @@ made against the fp64 reference with an ulp bound and against the oracle
 with a looser relative bound. Elementwise kernels are bit-exact.
 """
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -566,3 +567,61 @@ def test_split_reductions_match_one_call(hip, t):
              c2.p, CT(1.0), dw2.p)
     assert np.array_equal(c1.get(), c2.get()) and np.array_equal(c1.get(), c3.get())
     assert np.array_equal(dw1.get(), dw2.get())
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
+@pytest.mark.parametrize("which", ["stencil27", "fem27", "fem27p"])
+def test_node_spmv_matches_csr(hip, mpg, t, which):
+    """mpg_node_spmv_* (one record per 3 x 3 block, node_tile.hpp) forms the
+    CSR tile's fp64 products and sums each row in CSR storage order: the bits
+    of mpg_csr_spmv_* for beta = 0 and beta != 0, at the default two tiles per
+    workgroup and at one; a band matrix gets no copy, and alt_bytes decides
+    when it is built."""
+    dt = np.float64 if t == "f64" else np.float32
+    CT = C.c_double if t == "f64" else C.c_float
+    vt = 0 if t == "f64" else 1
+    A = {"stencil27": lambda: mpg.gen_stencil27(30, 3), "fem27": lambda: mpg.gen_spec("fem27:24:3:70:13"),
+         "fem27p": lambda: mpg.gen_spec("fem27:24:3:70:13:32:5")}[which]()
+    g = rng(5)
+    n = A.nrows
+    x = g.uniform(-1, 1, n).astype(dt)
+    y0 = g.uniform(-1, 1, n).astype(dt)
+    drp, dci, dv, dx = hip.buf(A.rowptr), hip.buf(A.col), hip.buf(A.val.astype(dt)), hip.buf(x)
+    csr, node = C.c_void_p(), C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, A.nrows, A.ncols, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    try:
+        hip.check(hip.lib.mpg_node_create(hip.ctx, csr, vt, dv.p, C.c_int64(-1), C.byref(node)))
+        assert node.value
+        nb, nt, by = C.c_int64(), C.c_int32(), C.c_int64()
+        hip.check(hip.lib.mpg_node_layout(node, C.byref(nb), C.byref(nt), C.byref(by)))
+        assert nb.value * 9 == A.nnz and nt.value >= nb.value // 256
+        assert by.value == nb.value * (80 if t == "f64" else 40) + 4 * (n // 3 + 1) + 8 * (nt.value + 1)
+        for tpw in ("2", "1"):
+            os.environ["MPG_NODE_TPW"] = tpw
+            try:
+                for alpha, beta in ((1.0, 0.0), (-1.5, 0.75)):
+                    dyn, dyc = hip.buf(y0), hip.buf(y0)
+                    hip.call(f"mpg_node_spmv_{t}", node, CT(alpha), dx.p, CT(beta), dyn.p)
+                    hip.call(f"mpg_csr_spmv_{t}", csr, CT(alpha), dv.p, dx.p, CT(beta), dyc.p)
+                    assert np.array_equal(dyn.get(), dyc.get()), (tpw, alpha, beta)
+            finally:
+                os.environ.pop("MPG_NODE_TPW", None)
+        # alt_bytes: built only against a copy that streams more
+        hip.lib.mpg_node_destroy(node)
+        node = C.c_void_p()
+        hip.check(hip.lib.mpg_node_create(hip.ctx, csr, vt, dv.p, C.c_int64(by.value // 2), C.byref(node)))
+        assert not node.value
+        hip.check(hip.lib.mpg_node_create(hip.ctx, csr, vt, dv.p, C.c_int64(by.value + 1), C.byref(node)))
+        assert node.value
+    finally:
+        hip.lib.mpg_node_destroy(node)
+        hip.lib.mpg_csr_destroy(csr)
+    B = mpg.gen_band(3000, 5, 4, seed=7)
+    drp, dci, dv = hip.buf(B.rowptr), hip.buf(B.col), hip.buf(B.val.astype(dt))
+    csr, node = C.c_void_p(), C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, B.nrows, B.ncols, B.nnz, B.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    try:
+        hip.check(hip.lib.mpg_node_create(hip.ctx, csr, vt, dv.p, C.c_int64(-1), C.byref(node)))
+        assert not node.value
+    finally:
+        hip.lib.mpg_csr_destroy(csr)

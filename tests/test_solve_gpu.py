@@ -313,6 +313,7 @@ def test_surface_normalisation_ride_same_bits(mpg, matrix, orth, mode, prec, mon
     kernel (7-point Laplacian) and the stepped kernel with CSR-summed slices
     (27-point, 3 dof, planes past 32767 rows); CGS must actually ride, and
     the cycles still record and replay."""
+    monkeypatch.setenv("MPG_SURFACE_NODE", "0")  # (the rides are the SELL kernels'; node blocks: no ride)
     A = {"band": lambda: mpg.gen_band(100_000, 5, 4, seed=7), "lap": lambda: mpg.gen_laplace3d(40),
          "stencil27": lambda: mpg.gen_stencil27(105, 3, ny=105, nz=3)}[matrix]()
     xt = mpg.rand_vect(A.nrows, 42)
