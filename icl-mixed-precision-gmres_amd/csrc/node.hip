@@ -11,20 +11,24 @@ using namespace mpg;
 namespace {
 
 // blocks of node row r (rows 3r .. 3r + 2), or -1 when its rows are not made
-// of the same aligned column triples in the same storage positions
+// of the same aligned column triples in the same storage positions. One wave
+// per node row, a lane per triple (coalesced column reads).
 __global__ __launch_bounds__(kBlock) void k_node_check(int nn, const int32_t* __restrict__ rowptr,
                                                        const int32_t* __restrict__ col, int32_t* __restrict__ cnt) {
-    const int r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= nn) return;
+    const int r = (int)(((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave);
+    const int lane = threadIdx.x & (kWave - 1);
+    if (r >= nn) return;  // (wave-uniform)
     const int p0 = rowptr[3 * r], p1 = rowptr[3 * r + 1], p2 = rowptr[3 * r + 2], p3 = rowptr[3 * r + 3];
     const int len = p1 - p0;
     int ok = p2 - p1 == len && p3 - p2 == len && len % 3 == 0;
-    for (int t = 0; ok && t < len; t += 3) {
-        const int c = col[p0 + t];
-        for (int j = 0; j < 3; ++j)
-            ok &= col[p0 + t + j] == c + j && col[p1 + t + j] == c + j && col[p2 + t + j] == c + j;
-    }
-    cnt[r] = ok ? len / 3 : -1;
+    if (ok)
+        for (int t = 3 * lane; t < len; t += 3 * kWave) {
+            const int c = col[p0 + t];
+            for (int j = 0; j < 3; ++j)
+                ok &= col[p0 + t + j] == c + j && col[p1 + t + j] == c + j && col[p2 + t + j] == c + j;
+        }
+    ok = __all(ok);
+    if (lane == 0) cnt[r] = ok ? len / 3 : -1;
 }
 
 template <class VI>
@@ -35,16 +39,18 @@ template <> __device__ __forceinline__ uint32_t val_bits<float>(const float* v, 
 template <> __device__ __forceinline__ uint32_t val_bits<half_v>(const half_v* v, int64_t i) { return v[i].bits; }
 
 // records of node row r: word 0 the block's first column, then the 9 values
-// row-major (fp64: from word 2; fp16: two per word)
+// row-major (fp64: from word 2; fp16: two per word). One wave per node row,
+// a lane per block: consecutive lanes write consecutive records.
 template <class VI>
 __global__ __launch_bounds__(kBlock) void k_node_fill(int nn, const int32_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ col, const VI* __restrict__ val,
                                                       const int32_t* __restrict__ bptr, uint32_t* __restrict__ recs) {
     constexpr int RW = NodeRec<VI>::R / 4;
-    const int r = blockIdx.x * kBlock + threadIdx.x;
+    const int r = (int)(((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave);
+    const int lane = threadIdx.x & (kWave - 1);
     if (r >= nn) return;
     const int p[3] = {rowptr[3 * r], rowptr[3 * r + 1], rowptr[3 * r + 2]};
-    for (int b = bptr[r]; b < bptr[r + 1]; ++b) {
+    for (int b = bptr[r] + lane; b < bptr[r + 1]; b += kWave) {
         const int t = 3 * (b - bptr[r]);
         uint32_t w[RW];
 #pragma unroll
@@ -113,7 +119,7 @@ int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool 
     if (vtype != MPG_F64 && vtype != MPG_F32 && vtype != MPG_F16) return MPG_ERR_ARG;
     hipStream_t stream = ctx->stream;
     const int nn = n / kNodeDof;
-    const int grid = (nn + kBlock - 1) / kBlock;
+    const int grid = (int)(((int64_t)nn * kWave + kBlock - 1) / kBlock);  // one wave per node row
     int32_t* cnt = nullptr;
     MPG_HIP(ctx, hipMalloc((void**)&cnt, (size_t)nn * 4));
     std::vector<int32_t> ch((size_t)nn);

@@ -1,10 +1,10 @@
 """GMRES it/s of the operator-surface driver (the reference gmres.cpp control
-flow over kernels_hip.cpp) against the fused engine on BAND-10M, mixed
-GMRES(30), --cycles restart cycles per solve (default 20) after a 1-cycle
-warm-up solve; gmres_seconds times the whole solve (set-up of the cycle
-program included).
+flow over kernels_hip.cpp) against the fused engine on BAND-1M (or --spec, a
+generator spec as the CLI's, e.g. fem27:111), mixed GMRES(30), --cycles
+restart cycles per solve (default 20) after a 1-cycle warm-up solve;
+gmres_seconds times the whole solve (set-up of the cycle program included).
 
-usage: python tools/surface_vs_fused.py [orth ...] [--engines=surface,fused] [--cycles=N]"""
+usage: python tools/surface_vs_fused.py [orth ...] [--engines=surface,fused] [--cycles=N] [--spec=SPEC]"""
 import sys
 from pathlib import Path
 
@@ -16,14 +16,17 @@ def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     engines = ["surface", "fused"]
     cycles = 20
+    spec = None
     for a in sys.argv[1:]:
+        if a.startswith("--spec="):
+            spec = a.split("=", 1)[1]
         if a.startswith("--engines="):
             engines = a.split("=", 1)[1].split(",")
         if a.startswith("--cycles="):
             cycles = int(a.split("=", 1)[1])
     orths = args or ["cgs", "mgs"]
     mpg = _load()
-    A = mpg.gen_band(1_000_000, 5, 4, seed=7)
+    A = mpg.gen_spec(spec) if spec else mpg.gen_band(1_000_000, 5, 4, seed=7)
     xt = mpg.rand_vect(A.nrows, 42)
     b = mpg.host_spmv(A, xt)
     import os
@@ -35,7 +38,7 @@ def main():
             opts = dict(engine=eng, mode="mixed", orth=orth, prec="identity", rlen=30, tol=0.0)
             mpg.solve(A, b, xt, max_restarts=1, **opts)
             r = mpg.solve(A, b, xt, max_restarts=cycles, **opts)
-            print(orth, eng, r.total_iters, "iters", round(r.gmres_seconds, 4), "s",
+            print(spec or "band1m", orth, eng, r.total_iters, "iters", round(r.gmres_seconds, 4), "s",
                   round(r.total_iters / r.gmres_seconds, 1), "it/s", flush=True)
 
 
