@@ -481,7 +481,7 @@ __global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict_
                                                       T* __restrict__ V, int64_t ld, int k,
                                                       const P* __restrict__ diag, T* __restrict__ w,
                                                       GivensFold<T> fold, const int8_t* __restrict__ rexp,
-                                                      int ntiles, int64_t nblk, int tpw) {
+                                                      int ntiles, int64_t nblk, int tpw, int xcd) {
     __shared__ double prod[kNodeProd];
     const T inv = fold_givens<FOLD>(fold, inv_p);
     T* __restrict__ Vk = V + (int64_t)k * ld;
@@ -499,10 +499,13 @@ __global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict_
         w[i] = (T)pw;
         Vk[i] = o.wp * inv;
     };
+    // xcd: workgroups take their tiles in XCD order (xcd_block), so each
+    // XCD's L2 serves one contiguous eighth of the rows' gathers
+    const int g = xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     if constexpr (!WALK) {
-        node_tile<VI>(blockIdx.x, tiles, bptr, recs, xval, pre, epi, prod);
+        node_tile<VI>(g, tiles, bptr, recs, xval, pre, epi, prod);
     } else {
-        const int t0 = blockIdx.x * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
+        const int t0 = g * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
         node_tiles<VI>(t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, xval, pre, epi, prod);
     }
 }
@@ -1805,6 +1808,12 @@ int csr_mode() {
 // / 255 us at 1 / 2 / 4 / 8 / 16 (auto, folded: 247), C4's stencil 341 /
 // 295-312 / 300 / 306-334 / 345 (auto 355): longer walks leave the grid's
 // tail to fewer workgroups, two tiles in flight is the gain.
+// MPG_NODE_XCD=1: tiles in XCD order (A/B; default off)
+int node_xcd() {
+    const char* e = std::getenv("MPG_NODE_XCD");
+    return e && *e == '1' ? 1 : 0;
+}
+
 constexpr int kNodeGroups = 2048;
 int node_tpw(const NodeCopy& S) {
     const int v = node_tpw_default();
@@ -2215,7 +2224,8 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                              static_cast<const int32_t*>(S.tiles), static_cast<const int32_t*>(S.bptr),
                              static_cast<const char*>(S.recs), static_cast<const T*>(a->w[k & 1]),
                              static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k, diag,
-                             static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp, S.ntiles, S.nblk, tpw);
+                             static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp, S.ntiles, S.nblk, tpw,
+                             node_xcd());
                 return (int)MPG_OK;
             };
             if (tpw > 1) return fold ? go(k_step_node<T, P, VI, true>) : go(k_step_node<T, P, VI, false>);
