@@ -1808,12 +1808,6 @@ int csr_mode() {
 // / 255 us at 1 / 2 / 4 / 8 / 16 (auto, folded: 247), C4's stencil 341 /
 // 295-312 / 300 / 306-334 / 345 (auto 355): longer walks leave the grid's
 // tail to fewer workgroups, two tiles in flight is the gain.
-// MPG_NODE_XCD=1: tiles in XCD order (A/B; default off)
-int node_xcd() {
-    const char* e = std::getenv("MPG_NODE_XCD");
-    return e && *e == '1' ? 1 : 0;
-}
-
 constexpr int kNodeGroups = 2048;
 int node_tpw(const NodeCopy& S) {
     const int v = node_tpw_default();
@@ -2225,7 +2219,7 @@ static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
                              static_cast<const char*>(S.recs), static_cast<const T*>(a->w[k & 1]),
                              static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k, diag,
                              static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp, S.ntiles, S.nblk, tpw,
-                             node_xcd());
+                             node_xcd(S));
                 return (int)MPG_OK;
             };
             if (tpw > 1) return fold ? go(k_step_node<T, P, VI, true>) : go(k_step_node<T, P, VI, false>);

@@ -13,22 +13,32 @@ namespace {
 // blocks of node row r (rows 3r .. 3r + 2), or -1 when its rows are not made
 // of the same aligned column triples in the same storage positions. One wave
 // per node row, a lane per triple (coalesced column reads).
+// far[r]: the node row's blocks whose column lies more than kNodeFar rows
+// from the row (scattered gathers: node_build's XCD-order choice).
+constexpr int kNodeFar = 1 << 18;
 __global__ __launch_bounds__(kBlock) void k_node_check(int nn, const int32_t* __restrict__ rowptr,
-                                                       const int32_t* __restrict__ col, int32_t* __restrict__ cnt) {
+                                                       const int32_t* __restrict__ col, int32_t* __restrict__ cnt,
+                                                       int32_t* __restrict__ far) {
     const int r = (int)(((int64_t)blockIdx.x * kBlock + threadIdx.x) / kWave);
     const int lane = threadIdx.x & (kWave - 1);
     if (r >= nn) return;  // (wave-uniform)
     const int p0 = rowptr[3 * r], p1 = rowptr[3 * r + 1], p2 = rowptr[3 * r + 2], p3 = rowptr[3 * r + 3];
     const int len = p1 - p0;
     int ok = p2 - p1 == len && p3 - p2 == len && len % 3 == 0;
+    int nfar = 0;
     if (ok)
         for (int t = 3 * lane; t < len; t += 3 * kWave) {
             const int c = col[p0 + t];
             for (int j = 0; j < 3; ++j)
                 ok &= col[p0 + t + j] == c + j && col[p1 + t + j] == c + j && col[p2 + t + j] == c + j;
+            nfar += abs(c - 3 * r) > kNodeFar;
         }
     ok = __all(ok);
-    if (lane == 0) cnt[r] = ok ? len / 3 : -1;
+    nfar = wave_sum(nfar);
+    if (lane == 0) {
+        cnt[r] = ok ? len / 3 : -1;
+        far[r] = nfar;
+    }
 }
 
 template <class VI>
@@ -83,10 +93,11 @@ __global__ __launch_bounds__(kBlock) void k_node_fill(int nn, const int32_t* __r
 template <class VI, class X>
 __global__ __launch_bounds__(kBlock) void k_node_spmv(const int32_t* __restrict__ tiles,
                                                       const int32_t* __restrict__ bptr, const char* __restrict__ recs,
-                                                      int ntiles, int64_t nblk, int tpw, const X* __restrict__ x,
-                                                      X alpha, X beta, X* __restrict__ y) {
+                                                      int ntiles, int64_t nblk, int tpw, int xcd,
+                                                      const X* __restrict__ x, X alpha, X beta, X* __restrict__ y) {
     __shared__ double prod[kNodeProd];
-    const int t0 = blockIdx.x * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
+    const int g = xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int t0 = g * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
     node_tiles<VI>(
         t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, [&](int c) { return (double)x[c]; },
         [&](int i) { return beta == X(0) ? X(0) : y[i]; },
@@ -106,6 +117,11 @@ struct mpg_node {
 
 namespace mpg {
 
+int node_xcd(const NodeCopy& S) {
+    const char* e = std::getenv("MPG_NODE_XCD");  // 0 / 1 force the order (A/B)
+    return e && (*e == '0' || *e == '1') ? *e - '0' : S.xcd ? 1 : 0;
+}
+
 int node_tpw_default() {
     const char* e = std::getenv("MPG_NODE_TPW");
     return e && *e ? std::atoi(e) : 2;
@@ -121,13 +137,15 @@ int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool 
     const int nn = n / kNodeDof;
     const int grid = (int)(((int64_t)nn * kWave + kBlock - 1) / kBlock);  // one wave per node row
     int32_t* cnt = nullptr;
-    MPG_HIP(ctx, hipMalloc((void**)&cnt, (size_t)nn * 4));
-    std::vector<int32_t> ch((size_t)nn);
-    k_node_check<<<grid, kBlock, 0, stream>>>(nn, A->rowptr, A->col, cnt);
-    hipError_t e = hipMemcpyAsync(ch.data(), cnt, (size_t)nn * 4, hipMemcpyDeviceToHost, stream);
+    MPG_HIP(ctx, hipMalloc((void**)&cnt, (size_t)nn * 8));
+    std::vector<int32_t> ch((size_t)nn * 2);
+    k_node_check<<<grid, kBlock, 0, stream>>>(nn, A->rowptr, A->col, cnt, cnt + nn);
+    hipError_t e = hipMemcpyAsync(ch.data(), cnt, (size_t)nn * 8, hipMemcpyDeviceToHost, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     (void)hipFree(cnt);
     if (e != hipSuccess) return set_hip_error(ctx, e, "node_build check");
+    int64_t nfar = 0;
+    for (int r = 0; r < nn; ++r) nfar += ch[(size_t)nn + r];
     std::vector<int32_t> bptr((size_t)nn + 1, 0);
     int64_t nb = 0;
     for (int r = 0; r < nn; ++r) {
@@ -150,6 +168,12 @@ int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool 
     for (size_t t = 0; t < nt1; ++t) tiles[nt1 + t] = bptr[tiles[t]];
     S.nn = nn;
     S.nblk = nb;
+    // scattered columns (over a quarter of the blocks far from their rows,
+    // e.g. a node-block permutation): tiles in XCD order, so the tiles of a
+    // node block share one L2 for the neighbour blocks they all gather
+    // (fem27p 282 -> 253 us, stencil27p 392 -> 355; natural order loses 3 %:
+    // fem27 219 -> 226, C4 313 -> 320; profiles/r05_node_ab.jsonl)
+    S.xcd = 4 * nfar > nb;
     S.ntiles = (int)nt1 - 1;
     S.vtype = vtype;
     S.rec = node_rec_bytes(vtype);
@@ -199,7 +223,8 @@ static int node_spmv_impl(mpg_ctx_t ctx, mpg_node_t A, X alpha, const X* x, X be
     if (tpw < 1) tpw = 2;
     using VI = std::conditional_t<sizeof(X) == 8, double, float>;
     k_node_spmv<VI, X><<<(A->S.ntiles + tpw - 1) / tpw, kBlock, 0, ctx->stream>>>(
-        A->S.tiles, A->S.bptr, static_cast<const char*>(A->S.recs), A->S.ntiles, A->S.nblk, tpw, x, alpha, beta, y);
+        A->S.tiles, A->S.bptr, static_cast<const char*>(A->S.recs), A->S.ntiles, A->S.nblk, tpw, node_xcd(A->S), x,
+        alpha, beta, y);
     MPG_LAUNCH_CHECK(ctx);
     return MPG_OK;
 }

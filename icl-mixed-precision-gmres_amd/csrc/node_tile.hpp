@@ -37,6 +37,7 @@ struct NodeCopy {
     int ntiles = 0;
     int vtype = 0;         // MPG_F64 / MPG_F32 / MPG_F16
     int rec = 0;           // record bytes
+    bool xcd = false;      // scattered columns: tiles in XCD order (node_xcd)
     int32_t* bptr = nullptr;   // nn + 1 block starts
     int32_t* tiles = nullptr;  // ntiles + 1 node-row starts, then ntiles + 1 block starts (tb0)
     void* recs = nullptr;      // nblk records
@@ -62,6 +63,8 @@ inline bool node_wins(int64_t node, int64_t alt, int64_t x_bytes) {
 }
 // tiles per workgroup of the pipelined walk (node_tiles): MPG_NODE_TPW, default 2
 int node_tpw_default();
+// 1: workgroups take their tiles in XCD order (S.xcd, MPG_NODE_XCD overrides)
+int node_xcd(const NodeCopy& S);
 
 inline int node_rec_bytes(int vtype) { return vtype == MPG_F64 ? 80 : vtype == MPG_F32 ? 40 : 24; }
 

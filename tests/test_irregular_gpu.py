@@ -232,3 +232,18 @@ def test_surface_node_blocks_same_bits(mpg, which, mode, orth, monkeypatch):
     ref, g = got["0"], got[""]
     assert g.total_iters == ref.total_iters == 90
     assert np.array_equal(g.step_res, ref.step_res) and np.array_equal(g.x, ref.x) and g.res_norm == ref.res_norm
+
+
+@pytest.mark.parametrize("which", ["stencil27", "fem27p"])
+def test_node_xcd_order_same_bits(mpg, which, monkeypatch):
+    """MPG_NODE_XCD: the node SpMV's workgroups take their tiles in XCD order
+    (auto on for scattered columns: fem27p) or in launch order -- the same
+    tiles and sums, the same bits."""
+    A, xt, b = _node_problem(mpg, which)
+    opts = dict(engine="fused", mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3,
+                spmv_format="node")
+    got = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("MPG_NODE_XCD", v)
+        got[v] = mpg.solve(A, b, xt, **opts)
+    assert np.array_equal(got["0"].step_res, got["1"].step_res) and np.array_equal(got["0"].x, got["1"].x)
