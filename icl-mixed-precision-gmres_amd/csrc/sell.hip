@@ -554,8 +554,15 @@ int sell_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, int f
             }
         }
     }
-    if (format == 0 && !forced && (double)best > 1.2 * (double)A->nnz) return MPG_OK;
-    if (best >= ((int64_t)1 << 31) * 4) return format == 2 ? MPG_ERR_UNSUPPORTED : MPG_OK;
+    // (no copy on these two paths: S.sigma reports a window only for a built copy)
+    if (format == 0 && !forced && (double)best > 1.2 * (double)A->nnz) {
+        S.sigma = 0;
+        return MPG_OK;
+    }
+    if (best >= ((int64_t)1 << 31) * 4) {
+        S.sigma = 0;
+        return format == 2 ? MPG_ERR_UNSUPPORTED : MPG_OK;
+    }
     std::vector<int64_t> off((size_t)ns + 1, 0);
     for (int s = 0; s < ns; ++s)
         off[s + 1] = off[s] + (int64_t)kWave * ((width[s] + best_w - 1) / best_w * best_w);
