@@ -1843,18 +1843,14 @@ int arnoldi_sell_build(mpg_arnoldi* a, int format) {
     if (int st = sell_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, format, a->sell)) return st;
     const char* ne = std::getenv("MPG_NODE");
     if (format == 0 && !(ne && *ne == '0')) {
+        const int64_t vb = a->d.inner_val == MPG_F64 ? 8 : a->d.inner_val == MPG_F32 ? 4 : 2;
+        const int64_t now = a->sell.nslices > 0 ? sell_copy_bytes(a) : a->d.A->nnz * (4 + vb) + ((int64_t)a->d.n + 1) * 4;
         NodeCopy nc;
-        if (int st = node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, false, nc)) return st;
-        if (nc.nblk > 0) {
-            const int64_t vb = a->d.inner_val == MPG_F64 ? 8 : a->d.inner_val == MPG_F32 ? 4 : 2;
-            const int64_t now = a->sell.nslices > 0 ? sell_copy_bytes(a)
-                                                    : a->d.A->nnz * (4 + vb) + ((int64_t)a->d.n + 1) * 4;
-            if (node_wins(node_bytes(nc), now, (int64_t)a->d.n_ext * a->tsize)) {
-                sell_free(a->sell);
-                a->node = nc;
-                return MPG_OK;
-            }
-            node_free(nc);
+        if (int st = node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, false, nc, now)) return st;
+        if (nc.nblk > 0) {  // (built only when it wins)
+            sell_free(a->sell);
+            a->node = nc;
+            return MPG_OK;
         }
     }
     if (a->sell.nslices == 0) return MPG_OK;

@@ -88,6 +88,82 @@ __global__ __launch_bounds__(kBlock) void k_node_fill(int nn, const int32_t* __r
     }
 }
 
+// Padded node blocks, for node rows whose three rows do not share one
+// pattern (a constrained dof's identity row, a dropped entry): the blocks of
+// node row r are the sorted union of the node columns q = c / 3 of its rows
+// (each row strictly increasing, columns in [0, cols)), a block's missing
+// entries stored as zeros. A row's sum then meets its CSR entries in CSR
+// (ascending) order with +-0 products in between, which leave an fp64 sum
+// that starts at +0 unchanged: the bits of the CSR sum for finite x.
+// One thread per node row (a three-way merge); cnt[r] = blocks or -1.
+__global__ __launch_bounds__(kBlock) void k_node_count_padded(int nn, int cols, const int32_t* __restrict__ rowptr,
+                                                              const int32_t* __restrict__ col,
+                                                              int32_t* __restrict__ cnt, int32_t* __restrict__ far) {
+    const int r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= nn) return;
+    int p[3], e[3];
+    bool ok = true;
+    for (int k = 0; k < 3; ++k) {
+        p[k] = rowptr[3 * r + k];
+        e[k] = rowptr[3 * r + k + 1];
+        for (int i = p[k]; i < e[k] && ok; ++i)
+            ok = col[i] >= 0 && col[i] < cols && (i == p[k] || col[i] > col[i - 1]);
+    }
+    int count = 0, nfar = 0;
+    while (ok) {
+        int q = INT32_MAX;
+        for (int k = 0; k < 3; ++k)
+            if (p[k] < e[k]) q = min(q, col[p[k]] / 3);
+        if (q == INT32_MAX) break;
+        ++count;
+        nfar += abs(3 * q - 3 * r) > kNodeFar;
+        for (int k = 0; k < 3; ++k)
+            while (p[k] < e[k] && col[p[k]] / 3 == q) ++p[k];
+    }
+    cnt[r] = ok ? count : -1;
+    far[r] = nfar;
+}
+
+template <class VI>
+__global__ __launch_bounds__(kBlock) void k_node_fill_padded(int nn, const int32_t* __restrict__ rowptr,
+                                                             const int32_t* __restrict__ col,
+                                                             const VI* __restrict__ val,
+                                                             const int32_t* __restrict__ bptr,
+                                                             uint32_t* __restrict__ recs) {
+    constexpr int RW = NodeRec<VI>::R / 4;
+    const int r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= nn) return;
+    int p[3], e[3];
+    for (int k = 0; k < 3; ++k) {
+        p[k] = rowptr[3 * r + k];
+        e[k] = rowptr[3 * r + k + 1];
+    }
+    for (int b = bptr[r]; b < bptr[r + 1]; ++b) {
+        int q = INT32_MAX;
+        for (int k = 0; k < 3; ++k)
+            if (p[k] < e[k]) q = min(q, col[p[k]] / 3);
+        uint32_t w[RW];
+#pragma unroll
+        for (int i = 0; i < RW; ++i) w[i] = 0;
+        w[0] = (uint32_t)(3 * q);
+        for (int k = 0; k < 3; ++k)
+            for (; p[k] < e[k] && col[p[k]] / 3 == q; ++p[k]) {
+                const int el = 3 * k + col[p[k]] - 3 * q;
+                if constexpr (std::is_same_v<VI, double>) {
+                    const double v = val[p[k]];
+                    w[2 + 2 * el] = (uint32_t)__double2loint(v);
+                    w[3 + 2 * el] = (uint32_t)__double2hiint(v);
+                } else if constexpr (std::is_same_v<VI, float>) {
+                    w[1 + el] = val_bits(val, p[k]);
+                } else {
+                    w[1 + el / 2] |= val_bits(val, p[k]) << (el & 1 ? 16 : 0);
+                }
+            }
+        uint32_t* o = recs + (int64_t)b * RW;
+        for (int i = 0; i < RW; ++i) o[i] = w[i];
+    }
+}
+
 // y = alpha * A x + beta * y over the node copy: the CSR tile's epilogue
 // (spmv.hip k_csr_adaptive) on node_tiles' row sums
 template <class VI, class X>
@@ -127,7 +203,8 @@ int node_tpw_default() {
     return e && *e ? std::atoi(e) : 2;
 }
 
-int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool required, NodeCopy& S) {
+int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool required, NodeCopy& S,
+               int64_t alt_bytes) {
     S = NodeCopy{};
     const int fail = required ? MPG_ERR_UNSUPPORTED : MPG_OK;
     const int n = A->rows;
@@ -144,6 +221,21 @@ int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool 
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     (void)hipFree(cnt);
     if (e != hipSuccess) return set_hip_error(ctx, e, "node_build check");
+    // exact node blocks, or else padded ones (columns in [0, cols), cols a
+    // multiple of 3, rows sorted; MPG_NODE_PAD=0: exact only)
+    bool padded = false;
+    if (std::any_of(ch.begin(), ch.begin() + nn, [](int32_t v) { return v < 0; })) {
+        const char* pe = std::getenv("MPG_NODE_PAD");
+        if ((pe && *pe == '0') || A->cols % kNodeDof) return fail;
+        MPG_HIP(ctx, hipMalloc((void**)&cnt, (size_t)nn * 8));
+        k_node_count_padded<<<(nn + kBlock - 1) / kBlock, kBlock, 0, stream>>>(nn, A->cols, A->rowptr, A->col, cnt,
+                                                                               cnt + nn);
+        e = hipMemcpyAsync(ch.data(), cnt, (size_t)nn * 8, hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        (void)hipFree(cnt);
+        if (e != hipSuccess) return set_hip_error(ctx, e, "node_build padded count");
+        padded = true;
+    }
     int64_t nfar = 0;
     for (int r = 0; r < nn; ++r) nfar += ch[(size_t)nn + r];
     std::vector<int32_t> bptr((size_t)nn + 1, 0);
@@ -166,6 +258,9 @@ int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool 
     const size_t nt1 = tiles.size();
     tiles.resize(2 * nt1);
     for (size_t t = 0; t < nt1; ++t) tiles[nt1 + t] = bptr[tiles[t]];
+    // the copy's bytes before it is built: none when it would lose to alt_bytes
+    const int64_t est = nb * node_rec_bytes(vtype) + ((int64_t)nn + 1) * 4 + 2 * (int64_t)nt1 * 4;
+    if (alt_bytes >= 0 && !node_wins(est, alt_bytes, (int64_t)A->cols * (vtype == MPG_F64 ? 8 : 4))) return fail;
     S.nn = nn;
     S.nblk = nb;
     // scattered columns (over a quarter of the blocks far from their rows,
@@ -182,7 +277,21 @@ int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool 
               hipMalloc(&S.recs, (size_t)std::max<int64_t>(nb, 1) * S.rec) == hipSuccess &&
               hipMemcpyAsync(S.bptr, bptr.data(), bptr.size() * 4, hipMemcpyHostToDevice, stream) == hipSuccess &&
               hipMemcpyAsync(S.tiles, tiles.data(), tiles.size() * 4, hipMemcpyHostToDevice, stream) == hipSuccess;
-    if (ok) {
+    S.padded = padded ? nb * kNodeDof * kNodeDof - A->nnz : 0;
+    if (ok && padded) {
+        auto* o = static_cast<uint32_t*>(S.recs);
+        const int g = (nn + kBlock - 1) / kBlock;
+        if (vtype == MPG_F64)
+            k_node_fill_padded<double><<<g, kBlock, 0, stream>>>(nn, A->rowptr, A->col,
+                                                                 static_cast<const double*>(val), S.bptr, o);
+        else if (vtype == MPG_F32)
+            k_node_fill_padded<float><<<g, kBlock, 0, stream>>>(nn, A->rowptr, A->col,
+                                                                static_cast<const float*>(val), S.bptr, o);
+        else
+            k_node_fill_padded<half_v><<<g, kBlock, 0, stream>>>(nn, A->rowptr, A->col,
+                                                                 static_cast<const half_v*>(val), S.bptr, o);
+        ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(stream) == hipSuccess;
+    } else if (ok) {
         auto* o = static_cast<uint32_t*>(S.recs);
         if (vtype == MPG_F64)
             k_node_fill<double><<<grid, kBlock, 0, stream>>>(nn, A->rowptr, A->col, static_cast<const double*>(val),
@@ -240,12 +349,11 @@ int mpg_node_create(mpg_ctx_t ctx, mpg_csr_t A, int32_t vtype, const void* vals,
     mpg_node* h = new (std::nothrow) mpg_node();
     if (!h) return MPG_ERR_ALLOC;
     h->ctx = ctx;
-    if (int st = node_build(ctx, A, vtype, vals, false, h->S)) {
+    if (int st = node_build(ctx, A, vtype, vals, false, h->S, alt_bytes)) {
         delete h;
         return st;
     }
-    const int64_t xb = (int64_t)A->cols * (vtype == MPG_F64 ? 8 : 4);
-    if (h->S.nblk == 0 || (alt_bytes >= 0 && !node_wins(node_bytes(h->S), alt_bytes, xb))) {
+    if (h->S.nblk == 0) {
         node_free(h->S);
         delete h;
         return MPG_OK;
@@ -262,8 +370,9 @@ int mpg_node_destroy(mpg_node_t A) {
     return MPG_OK;
 }
 
-int mpg_node_layout(mpg_node_t A, int64_t* blocks, int32_t* tiles, int64_t* bytes) {
+int mpg_node_layout(mpg_node_t A, int64_t* blocks, int32_t* tiles, int64_t* bytes, int64_t* padded) {
     if (!A) return MPG_ERR_ARG;
+    if (padded) *padded = A->S.padded;
     if (blocks) *blocks = A->S.nblk;
     if (tiles) *tiles = A->S.ntiles;
     if (bytes) *bytes = node_bytes(A->S);

@@ -38,6 +38,7 @@ struct NodeCopy {
     int vtype = 0;         // MPG_F64 / MPG_F32 / MPG_F16
     int rec = 0;           // record bytes
     bool xcd = false;      // scattered columns: tiles in XCD order (node_xcd)
+    int64_t padded = 0;    // zero slots of padded node blocks (0: exact blocks)
     int32_t* bptr = nullptr;   // nn + 1 block starts
     int32_t* tiles = nullptr;  // ntiles + 1 node-row starts, then ntiles + 1 block starts (tb0)
     void* recs = nullptr;      // nblk records
@@ -47,7 +48,9 @@ struct NodeCopy {
 // every node row's three rows made of aligned column triples, at most
 // kNodeCap blocks per node row): S.nblk > 0. A matrix that does not qualify
 // leaves S empty and returns MPG_OK (required: MPG_ERR_UNSUPPORTED).
-int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool required, NodeCopy& S);
+// alt_bytes >= 0: build only when node_wins over a copy streaming alt_bytes.
+int node_build(mpg_ctx* ctx, const mpg_csr* A, int vtype, const void* val, bool required, NodeCopy& S,
+               int64_t alt_bytes = -1);
 void node_free(NodeCopy& S);
 // bytes the Arnoldi SpMV streams from the copy: records, block and tile starts
 int64_t node_bytes(const NodeCopy& S);

@@ -338,7 +338,8 @@ int mpg_sell_spmv_f16f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* 
 /* ---- node-block SpMV: the same y = alpha*A x + beta*y (kernels_mkl.cpp:
  * 326-352) on a copy for matrices of 3-dof nodes (rows 3r .. 3r + 2 made of
  * the same column triples c, c + 1, c + 2 in the same storage positions:
- * mpg_csr_node_dof, dist.h): one record per 3 x 3 block, the block's first
+ * mpg_csr_node_dof, dist.h; or padded blocks, mpg_node_layout): one record
+ * per 3 x 3 block, the block's first
  * column and its 9 values (4.44 B per fp32 nonzero against CSR's 8), the
  * CSR tile's fp64 products and row order -- the bits of mpg_csr_spmv.
  * mpg_node_create copies one value array (vtype MPG_F64 | MPG_F32) of an
@@ -350,8 +351,15 @@ int mpg_sell_spmv_f16f32(mpg_ctx_t ctx, mpg_sell_t A, float alpha, const float* 
 int mpg_node_create(mpg_ctx_t ctx, mpg_csr_t A, int32_t vtype, const void* vals, int64_t alt_bytes,
                     mpg_node_t* out);
 int mpg_node_destroy(mpg_node_t A);
-/* blocks, tiles (runs of node rows of <= 256 blocks) and the bytes one SpMV reads */
-int mpg_node_layout(mpg_node_t A, int64_t* blocks, int32_t* tiles, int64_t* bytes);
+/* blocks, tiles (runs of node rows of <= 256 blocks), the bytes one SpMV
+ * reads and the zero slots of padded blocks (0: every block full). Padded
+ * blocks: when some node row's three rows do not share one pattern (a
+ * constrained dof's identity row, a dropped entry), the blocks are the
+ * union of the rows' node columns c / 3 (rows sorted ascending, columns in
+ * [0, cols), cols a multiple of 3) with zeros for the missing entries -- the
+ * CSR sum's bits for finite x (+-0 products leave an fp64 sum started at +0
+ * unchanged). Pointers may be NULL. */
+int mpg_node_layout(mpg_node_t A, int64_t* blocks, int32_t* tiles, int64_t* bytes, int64_t* padded);
 int mpg_node_spmv_f64(mpg_ctx_t ctx, mpg_node_t A, double alpha, const double* x, double beta, double* y);
 int mpg_node_spmv_f32(mpg_ctx_t ctx, mpg_node_t A, float alpha, const float* x, float beta, float* y);
 /* The same SpMV with a scalar program (mpg_scalar_program) run by one extra

@@ -15,6 +15,8 @@ thread counts, two-sided, tests/parity.py compare_mkl) on both engines, and
 each asserts which Arnoldi SpMV form it ran (int32 SELL, CSR-adaptive row
 blocks or node blocks: one record of a 3 x 3 block per column triple,
 node_tile.hpp)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -247,3 +249,52 @@ def test_node_xcd_order_same_bits(mpg, which, monkeypatch):
         monkeypatch.setenv("MPG_NODE_XCD", v)
         got[v] = mpg.solve(A, b, xt, **opts)
     assert np.array_equal(got["0"].step_res, got["1"].step_res) and np.array_equal(got["0"].x, got["1"].x)
+
+
+def _constrained(mpg, A, every=7, drop=0.01, seed=3):
+    """A with a constrained dof on every `every`-th node (row 3r + 1 replaced
+    by its diagonal entry alone, as a Dirichlet condition leaves it) and a
+    fraction `drop` of the other off-diagonal entries removed: node rows whose
+    three rows no longer share one pattern."""
+    g = np.random.default_rng(seed)
+    rows, cols, vals = [], [], []
+    for i in range(A.nrows):
+        a, z = int(A.rowptr[i]), int(A.rowptr[i + 1])
+        c, v = A.col[a:z], A.val[a:z]
+        if (i // 3) % every == 0 and i % 3 == 1:
+            keep = c == i
+        else:
+            keep = (c == i) | (g.random(z - a) >= drop)
+        rows.append(np.full(int(keep.sum()), i)), cols.append(c[keep]), vals.append(v[keep])
+    r, c, v = np.concatenate(rows), np.concatenate(cols), np.concatenate(vals)
+    rp = np.zeros(A.nrows + 1, dtype=np.int32)
+    np.add.at(rp, r + 1, 1)
+    return mpg.Csr(A.nrows, A.ncols, np.cumsum(rp).astype(np.int32), c.astype(np.int32), v.astype(np.float64))
+
+
+@pytest.mark.parametrize("mode,orth", [("mixed", "cgs"), ("baseline", "mgs"), ("mixed-half", "cgs")])
+def test_node_padded_blocks_same_bits(mpg, mode, orth):
+    """Padded node blocks (mpg_node_layout): node rows whose three rows do not
+    share a pattern store the union of their node columns with zeros for the
+    missing entries; each row still meets its entries in CSR order and the
+    zero products leave its fp64 sum unchanged, so solves give the CSR bits.
+    The exact-pattern check refuses this matrix (MPG_NODE_PAD=0)."""
+    A = _constrained(mpg, mpg.gen_fem27(24, 3, keep_pct=70, seed=13))
+    assert mpg.node_dof(A) == 1
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(engine="fused", mode=mode, orth=orth, prec="jacobi", rlen=30, tol=0.0, max_restarts=3)
+    eng = mpg.Engine(A, b, xt, **{k: v for k, v in opts.items() if k != "engine"}, spmv_format="node")
+    lay = eng.spmv_layout()
+    eng.close()
+    assert lay["format"] == "node" and A.nnz < lay["stored"] < 1.1 * A.nnz, lay
+    ref = mpg.solve(A, b, xt, spmv_format="csr", **opts)
+    got = mpg.solve(A, b, xt, spmv_format="node", **opts)
+    assert got.total_iters == ref.total_iters == 90
+    assert np.array_equal(got.step_res, ref.step_res) and np.array_equal(got.x, ref.x)
+    os.environ["MPG_NODE_PAD"] = "0"
+    try:
+        with pytest.raises((RuntimeError, ValueError)):
+            mpg.Engine(A, b, xt, **{k: v for k, v in opts.items() if k != "engine"}, spmv_format="node").close()
+    finally:
+        os.environ.pop("MPG_NODE_PAD", None)

@@ -592,9 +592,9 @@ def test_node_spmv_matches_csr(hip, mpg, t, which):
     try:
         hip.check(hip.lib.mpg_node_create(hip.ctx, csr, vt, dv.p, C.c_int64(-1), C.byref(node)))
         assert node.value
-        nb, nt, by = C.c_int64(), C.c_int32(), C.c_int64()
-        hip.check(hip.lib.mpg_node_layout(node, C.byref(nb), C.byref(nt), C.byref(by)))
-        assert nb.value * 9 == A.nnz and nt.value >= nb.value // 256
+        nb, nt, by, pad = C.c_int64(), C.c_int32(), C.c_int64(), C.c_int64()
+        hip.check(hip.lib.mpg_node_layout(node, C.byref(nb), C.byref(nt), C.byref(by), C.byref(pad)))
+        assert nb.value * 9 == A.nnz and nt.value >= nb.value // 256 and pad.value == 0
         assert by.value == nb.value * (80 if t == "f64" else 40) + 4 * (n // 3 + 1) + 8 * (nt.value + 1)
         for tpw in ("2", "1"):
             os.environ["MPG_NODE_TPW"] = tpw
