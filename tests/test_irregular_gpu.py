@@ -167,21 +167,31 @@ def test_node_blocks_same_bits_as_csr(mpg, which, mode, orth, prec):
     assert got.res_norm == ref.res_norm
 
 
-def test_node_blocks_refused(mpg):
-    """spmv_format="node" on a matrix without aligned 3 x 3 blocks fails
-    loudly (a band matrix; fem27 under a row-level permutation that splits
-    nodes); auto never picks it there."""
+def test_node_blocks_refused(mpg, monkeypatch):
+    """spmv_format="node" fails loudly where no node copy can be built (rows
+    not a multiple of 3; exact blocks only, MPG_NODE_PAD=0, on a band and on
+    fem27 under a row permutation that splits nodes), and auto never picks it
+    on those two (the padded copy would stream more bytes)."""
     band = mpg.gen_band(30_000, 5, 4, seed=7)
     A = mpg.gen_fem27(12, 3, keep_pct=70, seed=13)
     rng = np.random.default_rng(3)
     split = mpg.permute_sym(A, rng.permutation(A.nrows).astype(np.int32))
-    for M in (band, split):
+    odd = mpg.gen_band(30_001, 5, 4, seed=7)
+    opts = dict(mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=1)
+    for M, pad in ((odd, None), (band, "0"), (split, "0")):
+        if pad:
+            monkeypatch.setenv("MPG_NODE_PAD", pad)
+        else:
+            monkeypatch.delenv("MPG_NODE_PAD", raising=False)
         xt = mpg.rand_vect(M.nrows, 42)
         b = mpg.host_spmv(M, xt)
         with pytest.raises((RuntimeError, ValueError)):
-            mpg.Engine(M, b, xt, mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=1,
-                       spmv_format="node").close()
-        eng = mpg.Engine(M, b, xt, mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=1)
+            mpg.Engine(M, b, xt, spmv_format="node", **opts).close()
+    monkeypatch.delenv("MPG_NODE_PAD", raising=False)
+    for M in (band, split):
+        xt = mpg.rand_vect(M.nrows, 42)
+        b = mpg.host_spmv(M, xt)
+        eng = mpg.Engine(M, b, xt, **opts)
         assert eng.spmv_layout()["format"] != "node"
         eng.close()
 

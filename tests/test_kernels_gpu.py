@@ -575,8 +575,8 @@ def test_node_spmv_matches_csr(hip, mpg, t, which):
     """mpg_node_spmv_* (one record per 3 x 3 block, node_tile.hpp) forms the
     CSR tile's fp64 products and sums each row in CSR storage order: the bits
     of mpg_csr_spmv_* for beta = 0 and beta != 0, at the default two tiles per
-    workgroup and at one; a band matrix gets no copy, and alt_bytes decides
-    when it is built."""
+    workgroup and at one; a band matrix gets padded blocks only (the same
+    bits), and alt_bytes decides when a copy is built (node_wins)."""
     dt = np.float64 if t == "f64" else np.float32
     CT = C.c_double if t == "f64" else C.c_float
     vt = 0 if t == "f64" else 1
@@ -616,12 +616,29 @@ def test_node_spmv_matches_csr(hip, mpg, t, which):
     finally:
         hip.lib.mpg_node_destroy(node)
         hip.lib.mpg_csr_destroy(csr)
+    # a band (no node structure): only padded blocks, the CSR bits all the same, and never
+    # built against the CSR arrays' bytes
     B = mpg.gen_band(3000, 5, 4, seed=7)
     drp, dci, dv = hip.buf(B.rowptr), hip.buf(B.col), hip.buf(B.val.astype(dt))
+    dxb = hip.buf(g.uniform(-1, 1, B.nrows).astype(dt))
     csr, node = C.c_void_p(), C.c_void_p()
     hip.check(hip.lib.mpg_csr_create(hip.ctx, B.nrows, B.ncols, B.nnz, B.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
     try:
         hip.check(hip.lib.mpg_node_create(hip.ctx, csr, vt, dv.p, C.c_int64(-1), C.byref(node)))
+        assert node.value
+        nb, bb, pad = C.c_int64(), C.c_int64(), C.c_int64()
+        hip.check(hip.lib.mpg_node_layout(node, C.byref(nb), None, C.byref(bb), C.byref(pad)))
+        assert pad.value == 9 * nb.value - B.nnz > 0
+        dyn, dyc = hip.buf(np.zeros(B.nrows, dt)), hip.buf(np.zeros(B.nrows, dt))
+        hip.call(f"mpg_node_spmv_{t}", node, CT(1.0), dxb.p, CT(0.0), dyn.p)
+        hip.call(f"mpg_csr_spmv_{t}", csr, CT(1.0), dv.p, dxb.p, CT(0.0), dyc.p)
+        assert np.array_equal(dyn.get(), dyc.get())
+        hip.lib.mpg_node_destroy(node)
+        node = C.c_void_p()
+        # (a 9-wide band pads 5 blocks per node row to 27 entries: 40 % zeros, yet in fp32 fewer
+        # bytes than CSR -- auto weighs it against the SELL copy's implicit slices instead)
+        hip.check(hip.lib.mpg_node_create(hip.ctx, csr, vt, dv.p, C.c_int64(bb.value * 9 // 10), C.byref(node)))
         assert not node.value
     finally:
+        hip.lib.mpg_node_destroy(node)
         hip.lib.mpg_csr_destroy(csr)
