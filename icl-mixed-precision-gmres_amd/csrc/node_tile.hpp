@@ -30,6 +30,12 @@ namespace mpg {
 constexpr int kNodeDof = 3;
 constexpr int kNodeCap = kBlock;  // blocks per tile: one record per lane
 constexpr int kNodeProd = kNodeCap * kNodeDof * kNodeDof;
+// Row sums read this many blocks' products ahead (node_tiles). Measured
+// in-cycle (profiles/r05_node_ab.jsonl, interleaved builds): fem27 220 ->
+// 212 us, C4 315 -> 300, fem27p 253 -> 250 at 4 (54 VGPRs); 8 ahead was
+// slower (241 / 335 / 264), and one lane summing a node's three rows 26 %
+// slower: the sums' LDS latency is on the tile's critical path.
+constexpr int kNodeSumAhead = 4;
 
 struct NodeCopy {
     int nn = 0;            // node rows (rows / 3)
@@ -202,42 +208,34 @@ __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __rest
             }
         }
         lds_barrier();
-#if defined(MPG_NODE_ROW3)
-        (void)pf; (void)fa; (void)fz;
-        for (int q = l; q < nr1 - nr0; q += kBlock) {
-            const int nr = nr0 + q, i0 = kNodeDof * nr;
-            const auto p0 = pre(i0), p1 = pre(i0 + 1), p2 = pre(i0 + 2);
-            const int a = bptr[nr] - b0, z = bptr[nr + 1] - b0;
-            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-            for (int b = a; b < z; ++b) {
-                const double* p = prod + b * (kNodeDof * kNodeDof);
-                s0 += p[0]; s0 += p[1]; s0 += p[2];
-                s1 += p[3]; s1 += p[4]; s1 += p[5];
-                s2 += p[6]; s2 += p[7]; s2 += p[8];
-            }
-            epi(i0, s0, p0);
-            epi(i0 + 1, s1, p1);
-            epi(i0 + 2, s2, p2);
-        }
-#else
         for (int r = l; r < rows; r += kBlock) {
             const bool first = r == l;
             const int nr = nr0 + r / kNodeDof, k = r % kNodeDof;
             const int a = first ? fa : bptr[nr] - b0, z = first ? fz : bptr[nr + 1] - b0;
             double acc = 0.0;
-#if defined(MPG_NODE_NOSUM)
-            (void)a; (void)z;
-#else
-            for (int b = a; b < z; ++b) {
+            int b = a;
+            // kNodeSumAhead blocks' products read before any is added (the
+            // same order): one LDS round trip per four blocks, not per block
+            for (; b + kNodeSumAhead <= z; b += kNodeSumAhead) {
+                double v[3 * kNodeSumAhead];
+#pragma unroll
+                for (int u = 0; u < kNodeSumAhead; ++u) {
+                    const double* p = prod + (b + u) * (kNodeDof * kNodeDof) + kNodeDof * k;
+                    v[3 * u] = p[0];
+                    v[3 * u + 1] = p[1];
+                    v[3 * u + 2] = p[2];
+                }
+#pragma unroll
+                for (int u = 0; u < 3 * kNodeSumAhead; ++u) acc += v[u];
+            }
+            for (; b < z; ++b) {
                 const double* p = prod + b * (kNodeDof * kNodeDof) + kNodeDof * k;
                 acc += p[0];
                 acc += p[1];
                 acc += p[2];
             }
-#endif
             epi(kNodeDof * nr0 + r, acc, first ? pf : pre(kNodeDof * nr0 + r));
         }
-#endif
         lds_barrier();
         cur = nxt;
     }
