@@ -490,7 +490,9 @@ __global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict_
         P d;
         int e;
     };
-    auto xval = [&](int c) { return (double)(T)(wprev[c] * inv); };
+    auto xraw = [&](int c) { return wprev[c]; };
+    auto xfin = [&](T v) { return (double)(T)(v * inv); };
+    auto xval = [&](int c) { return xfin(xraw(c)); };
     auto pre = [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0), rexp ? (int)rexp[i] : 0}; };
     auto epi = [&](int i, double sum, const Ops& o) {
         const T t = (T)ldexp(sum, -o.e);
@@ -506,7 +508,7 @@ __global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict_
         node_tile<VI>(g, tiles, bptr, recs, xval, pre, epi, prod);
     } else {
         const int t0 = g * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
-        node_tiles<VI>(t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, xval, pre, epi, prod);
+        node_tiles<VI>(t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, xraw, xfin, pre, epi, prod);
     }
 }
 

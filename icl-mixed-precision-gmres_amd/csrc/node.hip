@@ -175,7 +175,8 @@ __global__ __launch_bounds__(kBlock) void k_node_spmv(const int32_t* __restrict_
     const int g = xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
     const int t0 = g * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
     node_tiles<VI>(
-        t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, [&](int c) { return (double)x[c]; },
+        t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, [&](int c) { return x[c]; },
+        [&](X v) { return (double)v; },
         [&](int i) { return beta == X(0) ? X(0) : y[i]; },
         [&](int i, double sum, X yi) {
             const X t = (X)sum;

@@ -172,11 +172,15 @@ __device__ __forceinline__ void node_tile(int t, const int32_t* __restrict__ til
 // wait for LDS only (lds_barrier): __syncthreads would also drain the
 // prefetched records. (Two tiles ahead measured no better: fem27 227 vs
 // 218 us, C4 298 vs 295 us, profiles/r05_node_ab.jsonl.)
-template <class VI, class XF, class PF, class EPI>
+// xraw(c) loads x's raw entry c, xfin(raw) turns it into the fp64 factor.
+// (Issuing the next tile's gathers before this tile's row sums and
+// converting them after was slower: fem27 211 -> 231 us, C4 301 -> 327,
+// stencil27p 347 -> 357; profiles/r05_node_ab.jsonl.)
+template <class VI, class XR, class XF, class PF, class EPI>
 __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __restrict__ tiles,
                                            const int32_t* __restrict__ tb0, const int32_t* __restrict__ bptr,
-                                           const char* __restrict__ recs, int64_t nblk, XF xval, PF pre, EPI epi,
-                                           double* __restrict__ prod) {
+                                           const char* __restrict__ recs, int64_t nblk, XR xraw, XF xfin, PF pre,
+                                           EPI epi, double* __restrict__ prod) {
     constexpr int R = NodeRec<VI>::R;
     const int l = threadIdx.x;
     auto rec = [&](int t) {
@@ -196,7 +200,7 @@ __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __rest
         const int fa = bptr[nf] - b0, fz = bptr[nf + 1] - b0;
         const auto pf = pre(kNodeDof * nr0 + rf);
         const int c = cur.col();
-        const double x0 = xval(c), x1 = xval(c + 1), x2 = xval(c + 2);
+        const double x0 = xfin(xraw(c)), x1 = xfin(xraw(c + 1)), x2 = xfin(xraw(c + 2));
         if (t + 1 < t1) nxt.load(rec(t + 1));
         if (l < nb) {
             double* p = prod + l * (kNodeDof * kNodeDof);
