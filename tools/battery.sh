@@ -13,6 +13,8 @@
 #   irrpmc   FETCH_SIZE, WRITE_SIZE and TCC hit/miss passes of the irregular SpMVs
 #   c4pmc    FETCH_SIZE and TCC hit/miss passes of C4's stepped SpMV
 #   n2       bench --gpus 2 rehearsal with both ranks on GPU 0 (gloo host transport)
+#   node     node-block SpMV A/B (tiles per workgroup, XCD order) on the 3-dof stand-ins
+#   ranks    C4 / C5 rank blocks at P = 8 (tools/rank_blocks.py), and C4's under PMC
 set -u
 tag=${1:?usage: tools/battery.sh TAG step...}
 shift
@@ -30,6 +32,10 @@ for s in "$@"; do
     probe) cmds+=("${tag}_probe|200|python3 tools/timing_probe.py --torch > gpurun_out/${tag}_probe.json") ;;
     configs) cmds+=("${tag}_configs|900|python -u tools/bench_configs.py --cycles 6 --cpu-cycles 1 --out gpurun_out/${tag}_configs.jsonl") ;;
     irr) cmds+=("${tag}_irr|700|python -u tools/spmv_ab.py --case c4p --case fem27 --case fem27p --var spmv_format=auto --var spmv_format=csr --var spmv_format=sell,MPG_SELL_SIGMA=0 --reps 3 --cycles 1 > gpurun_out/${tag}_irr.jsonl") ;;
+    node) cmds+=("${tag}_node|600|python -u tools/spmv_ab.py --case fem27 --case fem27p --case c4p --case c4 --var spmv_format=node --var spmv_format=node,MPG_NODE_TPW=1 --var spmv_format=node,MPG_NODE_TPW=4 --var spmv_format=node,MPG_NODE_XCD=0 --var spmv_format=node,MPG_NODE_XCD=1 --reps 3 --cycles 1 > gpurun_out/${tag}_node.jsonl") ;;
+    ranks) cmds+=("${tag}_ranks|300|python -u tools/rank_blocks.py --ranks 8 --config c4 c5 --which 0,big,last > gpurun_out/${tag}_ranks.jsonl")
+           cmds+=("${tag}_rkf|200|timeout -s KILL 190 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${tag}_rank_pmc/fetch -o fetch -- python3 tools/rank_blocks.py --ranks 8 --config c4 --which 0,big")
+           cmds+=("${tag}_rkw|200|timeout -s KILL 190 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${tag}_rank_pmc/write -o write -- python3 tools/rank_blocks.py --ranks 8 --config c4 --which 0,big") ;;
     irrpmc) for c in c4p fem27 fem27p; do
               cmds+=("${tag}_${c}_f|200|timeout -s KILL 190 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${tag}_irrpmc/${c}_fetch -o fetch -- python3 tools/spmv_ab.py --case $c --var spmv_format=auto --reps 1 --cycles 1")
               cmds+=("${tag}_${c}_w|200|timeout -s KILL 190 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${tag}_irrpmc/${c}_write -o write -- python3 tools/spmv_ab.py --case $c --var spmv_format=auto --reps 1 --cycles 1")
