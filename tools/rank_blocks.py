@@ -11,7 +11,7 @@ solve, on a numerically different problem (halo entries stay 0), so the
 per-kernel times are the rank's. Prints one JSON line per (config, rank):
 the Arnoldi SpMV's layout, its in-cycle time (each launch's own events),
 its storage bytes and fraction of 8 TB/s, and the dots / CGS update times.
-  python tools/rank_blocks.py [--ranks 8] [--config c4 c5] [--which 0,big]
+  python tools/rank_blocks.py [--ranks 8] [--config c4 c5] [--which 0,big] [--format auto]
 Run it under rocprofv3 --kernel-trace --stats for the kernel trace, or with
 --pmc FETCH_SIZE / WRITE_SIZE (separate runs) for the traffic."""
 import argparse
@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--config", nargs="+", default=["c4", "c5"])
     ap.add_argument("--which", default="0,big", help="ranks to time: numbers, 'big' (most nnz), 'last'")
     ap.add_argument("--cycles", type=int, default=2)
+    ap.add_argument("--format", default="auto", help="the Arnoldi SpMV storage (spmv_format: auto, csr, sell, node)")
     a = ap.parse_args()
     P = a.ranks
     for cfg in a.config:
@@ -96,7 +97,8 @@ def main():
                 pp.close()
             r0, r1 = int(starts[q]), int(starts[q + 1])
             bq = mpg.host_spmv(Aq, xt)  # (global columns: the rank's own b rows)
-            opts = dict(mode=mode, orth="cgs", prec="identity", rlen=30, tol=0.0, max_restarts=100)
+            opts = dict(mode=mode, orth="cgs", prec="identity", rlen=30, tol=0.0, max_restarts=100,
+                        spmv_format=a.format)
             eng = mpg.Engine.distributed_host(Aq, bq, xt[r0:r1], plan, NullTransport(), P, q, **opts)
             try:
                 eng.run(1)
