@@ -7,7 +7,11 @@ rows per GPU, column offsets -5..+4, 9,999,975 nnz at one GPU; values from
 the counter-based generator of include/mpgmres/problems.h), x_true =
 rand_vect(n, 42), b = A x_true, restarted GMRES(30), mixed precision
 (fp32 Arnoldi + fp64 residual/update: gmres_singleUpdate), CGS, identity
-preconditioner, tol = 0 so the solve never stops early.
+preconditioner, tol = 0 so the solve never stops early. The fp32 Arnoldi runs
+in the reference's fp32 accumulation class by default (--accum f32: every
+dot / norm / gemv / SpMV partial sum in fp32, as cblas_s* / mkl_sparse_s_mv
+sum); --accum f64 sums the fp32 products in fp64 instead. The line's
+"accum" names the one it timed.
 
 One step = one restart cycle = check_initial on the host + 30 Arnoldi
 iterations + solution update + the next true-residual prologue (the fused
@@ -229,7 +233,8 @@ def surface_rate(mpg, A, b, xt, opts, cycles: int, fused_rate: float) -> dict:
     warm-up solve runs first: the process's first surface solve also pays
     one-time costs (code-object loads on each kernel's first launch) that a
     later solve does not, which would shrink the difference of the times."""
-    o = {k: v for k, v in opts.items() if k not in ("spmv_format",)}
+    # (the operator surface's kernels sum in fp64: its accumulation class is f64)
+    o = {k: v for k, v in opts.items() if k not in ("spmv_format", "accum")}
     mpg.solve(A, b, xt, engine="surface", **dict(o, max_restarts=2))
     runs = []
     for r in (4, 4 + cycles):
@@ -245,37 +250,68 @@ def surface_rate(mpg, A, b, xt, opts, cycles: int, fused_rate: float) -> dict:
                    f"solve: (iters, time) of a {4 + cycles}-cycle solve minus a 4-cycle solve"}
 
 
-def cpu_baseline(mpg, A, b, xt, opts, args, world=1, workload="BAND-10M"):
+def cpu_baseline(mpg, A, b, xt, opts, args, world=1, workload="BAND-10M", solve=None):
     """The oracle (kernels_mkl.cpp restatement over the image's MKL) on the
-    host cores: per orthogonalisation, 1 warm-up + the median of `runs`
-    solves of `cpu_cycles` restart cycles each."""
-    from oracle import binding
+    host cores: per orthogonalisation, a 1-cycle warm-up, then up to
+    `cpu_runs` timed solves of `cpu_cycles` restart cycles each, as many as
+    fit the leg's wall-time budget (`cpu_budget_s`, split over the
+    orthogonalisations; at least one timed solve each), and their median.
+    `value` is the bench's own orthogonalisation (CGS by default, like the
+    GPU line); `best` is the faster of it and MGS (the reference CLI's
+    default, gmres_perf_test.cpp:320), so the GPU is also compared with the
+    strongest host figure. `solve` replaces the oracle call (CPU tests)."""
+    if solve is None:
+        from oracle import binding
 
+        solve, backend = binding.solve, binding.backend()
+    else:
+        backend = "test stub"
+    t_leg = time.perf_counter()
     # (the shared-GPU rehearsal runs on one GPU's box: its share only)
     threads = cpu_threads(world, os.environ.get("MPG_BENCH_SHARED_GPU") == "1")
     info = _CPU_INFO or cpu_info()
+    orths = list(dict.fromkeys([args.orth, "mgs"]))
+    budget = float(getattr(args, "cpu_budget_s", 0) or 0)
     by_orth = {}
-    for orth in dict.fromkeys([args.orth, "mgs"]):
+    for i, orth in enumerate(orths):
+        t_orth = time.perf_counter()
         o = dict(opts, orth=orth, max_restarts=args.cpu_cycles, threads=threads)
         o.pop("device")
         o.pop("spmv_format", None)
+        o.pop("accum", None)  # (MKL's fp32 BLAS: the f32 class by construction)
+        solve(mpg, A, b, xt, **dict(o, max_restarts=1))  # warm-up: one cycle
         rates = []
-        for r in range(args.cpu_runs + 1):
-            res = binding.solve(mpg, A, b, xt, **o)
-            if r:  # run 0 is the warm-up
-                rates.append(res.total_iters / res.gmres_seconds)
+        for r in range(args.cpu_runs):
+            t_run = time.perf_counter()
+            res = solve(mpg, A, b, xt, **o)
+            rates.append(res.total_iters / res.gmres_seconds)
+            if budget:  # stop when another solve would overrun this orthogonalisation's share
+                share = budget * (i + 1) / len(orths) - (time.perf_counter() - t_leg)
+                if time.perf_counter() - t_run > share:
+                    break
         by_orth[orth] = {"median": round(float(np.median(rates)), 2), "runs": [round(x, 2) for x in rates],
-                         "iterations_per_run": int(res.total_iters)}
-        log(f"[bench] CPU oracle {orth}: median {by_orth[orth]['median']} it/s over {args.cpu_runs} runs "
-            f"({threads} threads)")
+                         "iterations_per_run": int(res.total_iters),
+                         "wall_s": round(time.perf_counter() - t_orth, 2)}
+        log(f"[bench] CPU oracle {orth}: median {by_orth[orth]['median']} it/s over {len(rates)} runs "
+            f"({threads} threads, {by_orth[orth]['wall_s']} s)")
+    best = max(by_orth, key=lambda k: by_orth[k]["median"])
     return {"value": by_orth[args.orth]["median"], "unit": "GMRES it/s", "cores": threads, "kind": "port",
+            "best": by_orth[best]["median"], "best_orth": best,
             "sample": f"{args.cpu_cycles} restart cycles ({args.cpu_cycles * args.rlen} iterations) of the same "
-                      f"{workload} GMRES({args.rlen}) {args.mode}/{args.orth} solve; 1 warm-up + median of "
-                      f"{args.cpu_runs}; oracle backend {binding.backend()} (MKL restatement of kernels_mkl.cpp, "
+                      f"{workload} GMRES({args.rlen}) {args.mode}/{args.orth} solve; a 1-cycle warm-up + median of "
+                      f"up to {args.cpu_runs} (within a {budget or 'unlimited'} s leg budget); `best` is the faster "
+                      f"of {' and '.join(orths)}; oracle backend {backend} (MKL restatement of kernels_mkl.cpp, "
                       f"GNU OpenMP threading, OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')}, "
                       f"OMP_PLACES={os.environ.get('OMP_PLACES')})",
             "by_orth": by_orth, "cpu_model": info["model"], "physical_cores": info["physical_cores"],
-            "affinity_cpus": info["affinity_cpus"]}
+            "affinity_cpus": info["affinity_cpus"], "wall_s": round(time.perf_counter() - t_leg, 2)}
+
+
+def vs_gpu(cpu: dict, gpu_rate: float) -> None:
+    """GPU / CPU ratios: against the bench's own orthogonalisation and
+    against the faster host configuration."""
+    cpu["vs_gpu"] = round(gpu_rate / cpu["value"], 2) if cpu["value"] else None
+    cpu["vs_gpu_best"] = round(gpu_rate / cpu["best"], 2) if cpu.get("best") else None
 
 
 def visible_gpus() -> int:
@@ -365,15 +401,63 @@ def launch_ranks(args, argv) -> int:
     return rc
 
 
+# The collectives one CGS step of the row-partitioned engine issues on each
+# rank (host/dist.cpp), all on the engine's own RCCL
+# communicator, none on the torch process group (gloo: set-up and timing only).
+STEP_COLLECTIVES = [
+    "k >= 1: ncclGroupStart; ncclAllReduce(sum, fp64, the previous CGS update's 256 ||w||^2 partials, in place); "
+    "ncclSend/ncclRecv of w_prev's halo rows (fp32, unnormalised) to/from each neighbour rank; ncclGroupEnd "
+    "(FusedEngine::step, fold; k = 0: the halo send/recv group alone)",
+    "ncclAllReduce(sum, fp64, the panel dots' (k+1) x 256 partials, in place) -- the CGS update sums them itself "
+    "(k+1 <= 32; wider panels: a reduce launch + ncclAllReduce of the k+1 sums)",
+]
+CYCLE_COLLECTIVES = [
+    "x halo send/recv (fp64) before the residual SpMV (FusedEngine::prologue)",
+    "ncclAllReduce(sum, fp64, 3 sums: ||r||^2, ||x||^2, ||M r||^2) after the prologue's reduce",
+    "the last step's Givens: reduce + ncclAllReduce(sum, fp64, 1) of ||w||^2",
+]
+
+
 def dry_run_line(args) -> None:
-    """--dry-run: what this rank would run, without touching a GPU."""
-    print(json.dumps({"dry_run": True, "rank": int(os.environ.get("RANK", "0")),
-                      "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
-                      "world": int(os.environ.get("WORLD_SIZE", "1")), "gpus": args.gpus,
-                      "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}",
-                      "shared_gpu": os.environ.get("MPG_BENCH_SHARED_GPU") == "1"}), flush=True)
+    """--dry-run: what this rank would run, without touching a GPU. At N > 1
+    it also rehearses the CPU side of the set-up over the gloo group the real
+    run uses: each rank builds its BAND row block (--n-local rows), analyses
+    its halo and swaps the "rows I need from you" lists, and rank 0
+    broadcasts a 128-byte stand-in for the RCCL unique id."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    line = {"dry_run": True, "rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+            "world": world, "gpus": args.gpus,
+            "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}",
+            "shared_gpu": os.environ.get("MPG_BENCH_SHARED_GPU") == "1"}
     if os.environ.get("MPG_BENCH_DRY_FAIL_RANK") == os.environ.get("RANK"):  # (tests: a rank that fails)
+        print(json.dumps(line), flush=True)
         sys.exit(3)
+    if world > 1 and args.n_local <= 100_000:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+        mpg = load_pkg()
+        starts = [q * args.n_local for q in range(world + 1)]
+        A = mpg.gen_band(args.n_local * world, 5, 4, seed=7, row_begin=starts[rank], row_end=starts[rank + 1])
+        plan = mpg.HaloPlan(rank, world, starts, A)
+        needs = {q: plan.recv_rows(q).tolist() for q in range(world) if q != rank}
+        gathered = [None] * world
+        dist.all_gather_object(gathered, needs)
+        sends = {q: gathered[q].get(rank, []) for q in range(world) if q != rank}
+        for q, rows in sends.items():
+            plan.set_send(q, rows)
+        uid = [bytes(range(128)) if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        line.update(process_group=dist.get_backend(), uid_bytes=len(uid[0]) if uid[0] == bytes(range(128)) else -1,
+                    halo_recv={q: len(v) for q, v in needs.items() if v},
+                    halo_send={q: len(v) for q, v in sends.items() if v},
+                    n_front=plan.n_front, n_ext=plan.n_ext,
+                    step_collectives=STEP_COLLECTIVES, cycle_collectives=CYCLE_COLLECTIVES)
+        plan.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    print(json.dumps(line), flush=True)
 
 
 def measure(mpg, torch, dist, args, world, rank, local_rank, n, strong, keep=False) -> dict:
@@ -392,7 +476,8 @@ def measure(mpg, torch, dist, args, world, rank, local_rank, n, strong, keep=Fal
     log(f"[bench] rank {rank}: BAND rows {r0}..{r1} of {n}, local nnz={A.nnz}, built in {time.time() - t0:.1f}s")
 
     opts = dict(mode=args.mode, orth=args.orth, prec=args.prec, rlen=args.rlen, tol=0.0,
-                max_restarts=args.warmup + args.steps + 10, device=local_rank, spmv_format=args.spmv_format)
+                max_restarts=args.warmup + args.steps + 10, device=local_rank, spmv_format=args.spmv_format,
+                accum=args.accum)
     if world == 1:
         eng = mpg.Engine(A, b, xt, **opts)
     else:
@@ -473,14 +558,21 @@ def main():
     ap.add_argument("--prec", default="identity")
     ap.add_argument("--cpu-cycles", type=int, default=2, help="restart cycles per CPU-baseline solve")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU-baseline solves (after 1 warm-up)")
+    ap.add_argument("--cpu-budget-s", type=float, default=45.0,
+                    help="wall-time budget of each CPU-baseline leg (timed solves stop when the next would overrun)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-cycles", type=int, default=3)
     ap.add_argument("--hbm-rows", type=int, default=10_000_000,
                     help="rows of the BAND matrix of the HBM-scale SpMV figure (0: skip)")
     ap.add_argument("--surface-cycles", type=int, default=20,
                     help="N = 1: restart cycles of the same solve through the drop-in operator surface (0: skip)")
-    ap.add_argument("--spmv-format", default="auto", choices=["auto", "csr", "sell"],
-                    help="Arnoldi SpMV storage (auto: SELL-64 when its padding is small)")
+    ap.add_argument("--spmv-format", default="auto", choices=["auto", "csr", "sell", "node"],
+                    help="Arnoldi SpMV storage (auto: by the bytes each copy moves; node: 3x3 node blocks, "
+                         "for 3-dof matrices only)")
+    ap.add_argument("--accum", default="f32", choices=["f64", "f32"],
+                    help="fp32 Arnoldi's accumulation class: f32 (default: every partial sum in fp32, the "
+                         "reference's cblas_sdot / sgemv / mkl_sparse_s_mv class) or f64 (fp32 products summed in "
+                         "fp64, rounded once)")
     ap.add_argument("--strong-rows", type=int, default=10_000_000,
                     help="N > 1: also time one BAND matrix of this many rows split over the ranks (the north "
                          "star's 100M-nnz strong-scaling case; 0: skip)")
@@ -526,16 +618,18 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        # MPG_BENCH_SHARED_GPU=1 rehearses the multi-rank path with every rank on
-        # device 0 (gloo, engine collectives over the host transport); the
-        # default is one GPU per rank over RCCL
+        # The torch process group is gloo (host sockets) in both modes: it only
+        # carries the set-up exchanges (halo "rows I need" lists, the RCCL
+        # unique id), the barriers around the timed region and the max of the
+        # elapsed times. The data path's collectives are the engine's own
+        # RCCL communicator, the only NCCL/RCCL communicator a rank creates
+        # (VERDICT r5 #6). MPG_BENCH_SHARED_GPU=1 rehearses the multi-rank path
+        # with every rank on device 0 (engine collectives over the host
+        # transport); the default is one GPU per rank over RCCL.
         if os.environ.get("MPG_BENCH_SHARED_GPU") == "1":
             local_rank = 0
-            torch.cuda.set_device(0)
-            dist.init_process_group("gloo")
-        else:
-            torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("gloo")
 
     strong = args.global_rows > 0
     n = args.global_rows if strong else args.n_local * world
@@ -686,7 +780,7 @@ def main():
                 cpu = cpu_baseline(mpg, Ag, bg, xt, opts, cargs, world, f"BAND n={n} ({global_nnz} nnz)")
                 log(f"[bench] CPU baseline on the global matrix took {time.time() - t2:.1f}s")
                 del Ag, bg
-            cpu["vs_gpu"] = round(value / cpu["value"], 2) if cpu["value"] else None
+            vs_gpu(cpu, value)
             if strong100 is not None:
                 t3 = time.time()
                 As = mpg.gen_band(args.strong_rows, 5, 4, seed=7)
@@ -695,10 +789,11 @@ def main():
                 cargs = argparse.Namespace(**dict(vars(args), cpu_runs=min(args.cpu_runs, 3)))
                 sc = cpu_baseline(mpg, As, bs, xs, opts, cargs, world,
                                   f"BAND n={args.strong_rows} ({10 * args.strong_rows - 25} nnz)")
-                sc["vs_gpu"] = round(strong100["value"] / sc["value"], 2) if sc["value"] else None
+                vs_gpu(sc, strong100["value"])
                 strong100["cpu_baseline"] = sc
                 log(f"[bench] strong case: {strong100['value']:.0f} it/s on {world} GPUs vs {sc['value']} it/s "
-                    f"on {sc['cores']} host cores ({sc['vs_gpu']}x); CPU leg took {time.time() - t3:.1f}s")
+                    f"on {sc['cores']} host cores ({sc['vs_gpu']}x; best host {sc['best']} it/s, "
+                    f"{sc['vs_gpu_best']}x); CPU leg took {time.time() - t3:.1f}s")
                 del As, bs, xs
 
     if rank == 0:
@@ -711,6 +806,9 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "GMRES iterations/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
+            "accum": {"f32": "f32: every dot / norm / gemv / SpMV partial sum of the fp32 Arnoldi in fp32 (the "
+                             "reference's cblas_s* / mkl_sparse_s_mv class)",
+                      "f64": "f64: the fp32 Arnoldi's products summed in fp64, rounded once"}[args.accum],
             "data": "synthetic", "roofline": roofline, "cpu_baseline": cpu,
             "solve_iters_per_s": round(solve_rate, 2), "surface": surface,
             "rccl_ranks": m["comm_ranks"] if world > 1 and not shared_gpu else None,
@@ -721,7 +819,8 @@ def main():
                            "unit": "GMRES iterations x 10M-nnz row blocks (one per GPU) per second"}),
             "config": {"workload": f"BAND banded CSR n={n}, offsets -5..+4, nnz={global_nnz} "
                                    f"({'split over' if strong else '1e6 rows = 10M nnz per GPU,'} {world} GPU(s)); "
-                                   f"GMRES({args.rlen}) {args.mode} (fp32 Arnoldi, fp64 residual/update), "
+                                   f"GMRES({args.rlen}) {args.mode} (fp32 Arnoldi, {args.accum} accumulation, "
+                                   f"fp64 residual/update), "
                                    f"{args.orth}, {args.prec} preconditioner, tol=0",
                        "step": f"one restart cycle = {args.rlen} iterations",
                        "value_counts": "GMRES iterations of the one (row-partitioned) solve per second",

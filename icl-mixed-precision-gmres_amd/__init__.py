@@ -22,7 +22,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._abi import (ENGINES, MODES, ORTHS, PRECS, SPMV_FORMATS, STATUS, CondestResult, HostCsr, RankLayout, SolveArgs, SolveResult,
+from ._abi import (ACCUMS, ENGINES, MODES, ORTHS, PRECS, SPMV_FORMATS, STATUS, CondestResult, HostCsr, RankLayout, SolveArgs, SolveResult,
                    condest_args, condest_dict)
 
 PKG_DIR = Path(__file__).resolve().parent
@@ -39,11 +39,66 @@ def build(jobs: int = 8) -> None:
 
 
 _libs: dict = {}
+_runtime: dict = {}
+
+
+def _torch_lib_dir() -> Optional[Path]:
+    """torch/lib of an installed PyTorch, found without importing torch."""
+    import importlib.util
+
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return None
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    d = Path(list(spec.submodule_search_locations)[0]) / "lib"
+    return d if (d / "libamdhip64.so").exists() else None
+
+
+def _bind_hip_runtime() -> None:
+    """Fix the process's HIP runtime, and PyTorch's place in it, before the
+    package's libraries load and before anything initialises the GPU.
+
+    The libraries need libamdhip64.so.7 and librccl.so.1 by soname; PyTorch
+    bundles its own HIP runtime and RCCL and needs them by the file names
+    libamdhip64.so / librccl.so. A process that loaded this package first,
+    ran on the GPU, and imported torch afterwards aborted at exit with
+    "double free or corruption" (SIGABRT; tools/exit_probe.py
+    package_then_torch, profiles/r06_exit/) -- both with
+    /opt/rocm's runtime bound (two HIP and HSA runtimes in one process) and
+    with PyTorch's bound by file before the package: what the abort needs is
+    PyTorch's libraries loaded after the HIP runtime initialised. Importing
+    torch first never aborted (every bench and test process). So when
+    PyTorch is installed the package imports it here, first: one runtime
+    (PyTorch's), PyTorch's teardown in the order its own processes use.
+    MPG_HIP_RUNTIME=system skips it and binds /opt/rocm's runtime (a
+    process that will never import torch; the CLI's configuration)."""
+    if _runtime:
+        return
+    choice = os.environ.get("MPG_HIP_RUNTIME", "auto")
+    d = _torch_lib_dir() if choice in ("auto", "torch") else None
+    if choice == "torch" and d is None:
+        raise RuntimeError("MPG_HIP_RUNTIME=torch but no PyTorch installation with a HIP runtime was found")
+    if d is not None:
+        import torch  # noqa: F401  (first: see above)
+
+        _runtime["hip"] = str(d / "libamdhip64.so")
+    else:
+        _runtime["hip"] = "system"
+
+
+def hip_runtime() -> str:
+    """The HIP runtime the package's libraries are bound to: the path of
+    PyTorch's bundled libamdhip64.so, or "system" (/opt/rocm, by soname)."""
+    _bind_hip_runtime()
+    return _runtime["hip"]
 
 
 def _lib(name: str) -> C.CDLL:
     if name in _libs:
         return _libs[name]
+    _bind_hip_runtime()
     path = HIP_LIB if name == "hip" else HOST_LIB
     if name == "hip" and os.environ.get("MPG_HIP_LIB"):  # A/B of two kernel builds (tools/ab_bench.sh)
         path = Path(os.environ["MPG_HIP_LIB"])
@@ -147,6 +202,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_half_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     lib.mpg_engine_slices_per_wave.argtypes = [C.c_void_p]
     lib.mpg_engine_givens_folded.argtypes = [C.c_void_p]
+    lib.mpg_engine_accum.argtypes = [C.c_void_p]
     lib.mpg_engine_sell_shared_slices.argtypes = [C.c_void_p]
     lib.mpg_engine_sell_shared_slices.restype = C.c_int64
     lib.mpg_engine_sell_sigma.argtypes = [C.c_void_p]
@@ -209,6 +265,10 @@ _HIP_DECLS.update({
     "mpg_sell_spmv_f16f32": ([_P, _P, C.c_float, _P, C.c_float, _P], C.c_int),
     "mpg_sell_spmv_prog_f64": ([_P, _P, C.c_double, _P, C.c_double, _P, _P, C.c_int32], C.c_int),
     "mpg_sell_spmv_prog_f32": ([_P, _P, C.c_float, _P, C.c_float, _P, _P, C.c_int32], C.c_int),
+    "mpg_node_spmv_prog_f64": ([_P, _P, C.c_double, _P, C.c_double, _P, _P, C.c_int32], C.c_int),
+    "mpg_node_spmv_prog_f32": ([_P, _P, C.c_float, _P, C.c_float, _P, _P, C.c_int32], C.c_int),
+    "mpg_node_spmv_norm_f64": ([_P, _P, C.c_int32, _P, _P, _P, C.c_double, _P, _P, C.c_int32], C.c_int),
+    "mpg_node_spmv_norm_f32": ([_P, _P, C.c_int32, _P, _P, _P, C.c_float, _P, _P, C.c_int32], C.c_int),
     "mpg_copy_f64f64": ([_P, _I64, _P, _P], C.c_int),
     "mpg_copy_f32f32": ([_P, _I64, _P, _P], C.c_int),
     "mpg_copy_f64f32": ([_P, _I64, _P, _P], C.c_int),
@@ -432,8 +492,11 @@ class Result:
 def make_args(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, mode="mixed", orth="mgs",
               prec="identity", rlen=30, tol=1e-6, max_restarts=1_000_000, rtol=0.0, repeat_iter=False,
               orthloss=False, jacobi_steps=1, engine="fused", verbose=False, device=0, threads=0,
-              spmv_format="auto", half_unscaled=False, stop_on_breakdown=False):
-    """Build mpg_solve_args (shared by mpg_solve and the CPU oracle)."""
+              spmv_format="auto", half_unscaled=False, stop_on_breakdown=False, accum="f64"):
+    """Build mpg_solve_args (shared by mpg_solve and the CPU oracle).
+    accum: the fp32 Arnoldi's accumulation class, "f64" (fp32 products
+    summed in fp64, rounded once) or "f32" (every partial sum in fp32: the
+    reference's cblas_s* / mkl_sparse_s_mv class; fused engine only)."""
     b = np.ascontiguousarray(b, dtype=np.float64)
     keep = [A.rowptr, A.col, A.val, b]
     a = SolveArgs()
@@ -453,6 +516,7 @@ def make_args(A: Csr, b: np.ndarray, x_true: Optional[np.ndarray] = None, *, mod
     a.spmv_format = SPMV_FORMATS[spmv_format]
     a.half_unscaled = int(half_unscaled)
     a.stop_on_breakdown = int(stop_on_breakdown)
+    a.accum = ACCUMS[accum]
     return a, keep
 
 
@@ -817,7 +881,8 @@ class Engine:
         return {"format": {1: "csr", 2: "sell", 3: "node"}[f.value], "vec_width": w.value, "col_bytes": cb.value,
                 "stored": st.value, "window": bool(win.value),
                 "slices_per_wave": int(self._lib.mpg_engine_slices_per_wave(self._h)),
-                "givens_folded": bool(self._lib.mpg_engine_givens_folded(self._h) == 1)}
+                "givens_folded": bool(self._lib.mpg_engine_givens_folded(self._h) == 1),
+                "accum": {0: "f64", 1: "f32"}[int(self._lib.mpg_engine_accum(self._h))]}
 
     def sell_columns(self) -> dict:
         """Column form of the Arnoldi SpMV's SELL copy (mpg_engine_sell_columns):

@@ -9,6 +9,7 @@ ORTHS = {"cgs": 0, "mgs": 1, "cgsr": 2}
 PRECS = {"ilu": 0, "ilu_jacobi": 1, "jacobi": 2, "identity": 3}
 ENGINES = {"surface": 0, "fused": 1}
 SPMV_FORMATS = {"auto": 0, "csr": 1, "sell": 2, "node": 3}
+ACCUMS = {"f64": 0, "f32": 1}  # mpg_solve_args.accum (MPG_ACCUM_F64 / MPG_ACCUM_F32, arnoldi.h)
 STATUS = {1: "converged", 3: "aborted", -1: "error"}
 
 
@@ -38,6 +39,7 @@ class SolveArgs(C.Structure):
         ("spmv_format", C.c_int32),
         ("half_unscaled", C.c_int32),
         ("stop_on_breakdown", C.c_int32),
+        ("accum", C.c_int32),
     ]
 
 

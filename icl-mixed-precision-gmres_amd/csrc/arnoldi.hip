@@ -9,19 +9,11 @@
 // then k_reduce_partials in a fixed order), which is also the seam where a
 // multi-GPU caller all-reduces across ranks.
 //
-// Numerics follow the operator surface exactly where the reference fixes
-// an order (reciprocal-then-multiply normalisation, y = alpha*t + beta*y
-// forms, Givens on rounded products); every dot/norm/gemv/SpMV accumulates in
-// fp64 and is rounded once to the working precision — the same rounding the
-// stand-alone kernels (blas1/blas2/spmv) apply, so the fused engine and the
-// operator-surface driver agree to the last bit in most steps.
-#include "csr_tile.hpp"
-#include "node_tile.hpp"
-#include "sell_tile.hpp"
-#include "handoff.hpp"
-#include "panel.hpp"
-#include "internal.hpp"
-#include "mpgmres/arnoldi.h"
+// The kernels live in arnoldi_kernels.hpp, the launch code (templated on the
+// accumulation class) in arnoldi_launch.hpp; this file is the C-ABI and the
+// fp64-accumulation build, arnoldi_acc32.hip the fp32-accumulation one.
+#include "arnoldi_kernels.hpp"
+#include "arnoldi_launch.hpp"
 
 #include <cstdlib>
 #include <new>
@@ -31,1807 +23,6 @@
 using namespace mpg;
 
 namespace {
-
-constexpr int kNC = 32;        // dot columns carried in registers per pass
-constexpr int kGroups = 1024;  // max workgroups of the row-block phase kernels
-constexpr int kCombineBlock = 1024;  // threads per workgroup of the combining panel dots
-constexpr int kCombineGroups = 256;  // its workgroups: one per CU
-constexpr int kOrthMGS = 1, kOrthCGSR = 2;  // mpg_orth_t (include/mpgmres/solve.h)
-
-// Jacobi / identity preconditioner in precision P applied to a T value:
-// typesafe_apply (gmres.cpp:12-22) + gdmv(1, d, w, 0, w) (kernels.hpp:141-144).
-template <class T, class P>
-__device__ __forceinline__ T precond(T w, const P* __restrict__ d, int64_t i) {
-    P p = (P)w;
-    if (d) p = P(0) * p + P(1) * d[i] * p;
-    return (T)p;
-}
-
-// This workgroup's contiguous run of row blocks [rb0, rb1) — contiguous so
-// that its rows form one range [blocks[rb0], blocks[rb1]) for the dot pass.
-__device__ __forceinline__ void my_blocks(int nblocks, int& rb0, int& rb1, bool xcd = false) {
-    const int b = xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-    rb0 = (int)((int64_t)b * nblocks / gridDim.x);
-    rb1 = (int)((int64_t)(b + 1) * nblocks / gridDim.x);
-}
-
-// For every row of this workgroup's row blocks: fp64 sum of val * xval(col)
-// (csr_tile.hpp), then epi(row, sum) on one lane. NT: non-temporal matrix
-// loads (a pass that runs once per restart cycle).
-// XCD (round 5): workgroups take their runs of row blocks in XCD order
-// (xcd_block), so each XCD's L2 holds the neighbourhood of x that its own
-// contiguous eighth of the rows gathers (the SELL kernels' placement).
-template <bool NT = false, bool XCD = false, class V, class XF, class PF, class EPI>
-__device__ __forceinline__ void for_rows(const int32_t* __restrict__ blocks, int nblocks,
-                                         const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                                         const V* __restrict__ val, int64_t nnz, XF xval, PF pre, EPI epi,
-                                         double* prod, double* scratch) {
-    const int32_t* __restrict__ bnnz = blocks + nblocks + 1;  // mpg_csr's nnz starts follow the row starts
-    int rb0, rb1;
-    my_blocks(nblocks, rb0, rb1, XCD);
-    for (int b = rb0; b < rb1; ++b)
-        csr_row_block<NT>(blocks[b], blocks[b + 1], bnnz[b], bnnz[b + 1], rowptr, col, val, nnz, xval, pre, epi,
-                          prod, scratch);
-}
-
-// Combine in the last arriver: sums[c] = sum over g of partial[c*G + g] for
-// c < ncols <= BS/32; 32 lanes per column, each a strided run in g order,
-// then a 32-lane xor tree (fixed order).
-template <int BS>
-__device__ __forceinline__ void combine_columns(const double* __restrict__ partial, int G, int ncols,
-                                                double* __restrict__ sums) {
-    const int c = threadIdx.x / 32, sub = threadIdx.x % 32;
-    double v = 0.0;
-    if (c < ncols)
-        for (int g = sub; g < G; g += 32) v += partial[(size_t)c * G + g];
-#pragma unroll
-    for (int mask = 16; mask >= 1; mask >>= 1) v += __shfl_xor(v, mask, kWave);
-    if (c < ncols && sub == 0) sums[c] = v;
-}
-
-// ---------------------------------------------------------------- prologue
-// r = b - A x (X), w = M(T(r)); partials: ||T(r)||^2, ||w||^2, ||x||^2
-template <class T, class X, class P>
-__global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__ blocks, int nblocks,
-                                                     const int32_t* __restrict__ rowptr,
-                                                     const int32_t* __restrict__ col, const X* __restrict__ val,
-                                                     int64_t nnz, const X* __restrict__ x, const X* __restrict__ b,
-                                                     const P* __restrict__ diag, T* __restrict__ w,
-                                                     double* __restrict__ partial) {
-    __shared__ double prod[kNnzCap];
-    __shared__ double scratch[kBlock / kWave];
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    struct Ops {
-        X b, x;
-        P d;
-    };
-    for_rows<true>(  // once per cycle: keep V and the Arnoldi matrix cached
-        blocks, nblocks, rowptr, col, val, nnz, [&](int c) { return (double)x[c]; },
-        [&](int i) { return Ops{b[i], x[i], diag ? diag[i] : P(0)}; },
-        [&](int i, double sum, const Ops& o) {
-            const X bi = o.b, xi = o.x;
-            const P di = o.d;
-            const X t = (X)sum;
-            const X r = bi - t;  // copy(b, w); spmv(-1, A, x, 1, w)
-            T wi = (T)r;
-            acc[0] += (double)wi * (double)wi;
-            P pw = (P)wi;  // = precond<T, P> (typesafe_apply's rounding to P included)
-            if (diag) pw = P(0) * pw + P(1) * di * pw;
-            wi = (T)pw;
-            acc[1] += (double)wi * (double)wi;
-            acc[2] += (double)xi * (double)xi;
-            w[i] = wi;
-        },
-        prod, scratch);
-    store_partials<4>(acc, 3, partial);
-}
-
-// The same prologue on a SELL-64 copy of the outer-precision values (one
-// wave per slice, one lane per row; loads issued in need order as in
-// k_step_sell): r = b - A x (X), w = M(T(r)), partials ||T(r)||^2,
-// ||w||^2, ||x||^2 per workgroup.
-template <class T, class X, class P, class CI, int W, bool WIN, bool UNI = false>
-__global__ __launch_bounds__(kBlock) void k_prologue_sell(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
-                                                          const CI* __restrict__ col, const X* __restrict__ val,
-                                                          const X* __restrict__ x, const X* __restrict__ b,
-                                                          const P* __restrict__ diag, T* __restrict__ w,
-                                                          double* __restrict__ partial,
-                                                          const int32_t* __restrict__ sbase,
-                                                          const int32_t* __restrict__ spat, const int64_t* __restrict__ coff, const CI* __restrict__ pat,
-                                                          const int32_t* __restrict__ xrp,
-                                                          const int32_t* __restrict__ xcol,
-                                                          const X* __restrict__ xval, int64_t ustride, int xcd,
-                                                          const int32_t* __restrict__ rows) {
-    constexpr int NQ = kWinLen / kWave;
-    __shared__ X win[WIN ? kBlock / kWave : 1][WIN ? kWinLen : 1];
-    const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
-    const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (kBlock / kWave) + wid;
-    const bool live = s < nslices;  // a dead wave still joins the partials' barrier
-    const int row0 = s * kWave;
-    // the lane's row (a sorted SELL-C-sigma copy: rows[], padding lanes n)
-    const int i = rows ? rows[live ? row0 + lane : 0] : row0 + lane;
-    const bool own = live && i < n;
-    SellRow<X, CI, W, true> row;  // once per cycle: non-temporal slices
-    if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat, coff);
-    else row.init_load(live ? s : 0, off, spat, coff);
-    __builtin_amdgcn_sched_barrier(0);
-    X xr[WIN ? NQ : 1];
-    if constexpr (WIN) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int c = row0 - kWinLo + q * kWave + lane;
-            xr[q] = x[c >= n_lo && c < n_ext ? c : 0];
-        }
-    }
-    const int ic = own ? i : 0;
-    const X bi = b[ic], xi = x[ic];
-    const P di = diag ? diag[ic] : P(0);
-    __builtin_amdgcn_sched_barrier(0);
-    row.init_finish(lane, col, val, sbase, pat);
-    row.load(0);
-    __builtin_amdgcn_sched_barrier(0);
-    double sum = 0.0;
-    if (live) {
-        if constexpr (WIN) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int c = row0 - kWinLo + q * kWave + lane;
-                win[wid][q * kWave + lane] = (c >= n_lo && c < n_ext) ? xr[q] : X(0);
-            }
-            wave_lds_sync();
-            auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
-            row.sum(0, xv, sum);
-            for (int q = row.U; q < row.steps; q += row.U) {
-                row.load(q);
-                row.sum(q, xv, sum);
-            }
-        } else {
-            auto xv = [&](int c) { return (double)x[c]; };
-            if (SellCol<CI>::stepped && row.exc) {
-                sum = csr_row_sum(own ? row.xrow : -1, xrp, xcol, xval, xv);
-            } else {
-                row.sum(0, xv, sum);
-                for (int q = row.U; q < row.steps; q += row.U) {
-                    row.load(q);
-                    row.sum(q, xv, sum);
-                }
-            }
-        }
-    }
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    if (own) {
-        const X t = (X)sum;
-        const X r = bi - t;  // copy(b, w); spmv(-1, A, x, 1, w)
-        T wi = (T)r;
-        acc[0] = (double)wi * (double)wi;
-        P pw = (P)wi;  // = precond<T, P>
-        if (diag) pw = P(0) * pw + P(1) * di * pw;
-        wi = (T)pw;
-        acc[1] = (double)wi * (double)wi;
-        acc[2] = (double)xi * (double)xi;
-        w[i] = wi;
-    }
-    store_partials<4>(acc, 3, partial);
-}
-
-template <class T, class X>
-__global__ void k_prologue_finish(const double* __restrict__ sums, int m, T* __restrict__ s, T* __restrict__ inv,
-                                  double* __restrict__ report) {
-    const T r_norm = (T)sqrt(sums[0]);
-    const T beta = (T)sqrt(sums[1]);
-    const X x_norm = (X)sqrt(sums[2]);
-    const T iv = beta != T(0) ? T(1) / beta : T(0);  // first_vector: zero fill when beta == 0
-    if (threadIdx.x == 0) {
-        report[0] = (double)r_norm;
-        report[1] = (double)beta;
-        report[2] = (double)x_norm;
-        report[3] = (double)iv;
-        *inv = iv;
-    }
-    for (int i = threadIdx.x; i <= m; i += blockDim.x) s[i] = i == 0 ? beta : T(0);
-}
-
-// ||w||^2 partials again (column 1 of the prologue's partials, same grid)
-// after a preconditioner applied outside the prologue kernel (ILU)
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_wnorm_partials(int n, const T* __restrict__ w, double* __restrict__ partial) {
-    double acc[1] = {0.0};
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) acc[0] += (double)w[i] * (double)w[i];
-    store_partials<1>(acc, 1, partial + gridDim.x);
-}
-
-// ---------------------------------------------------------------- reductions
-// sum of G partials in a fixed order (identical in every workgroup that
-// calls it with the same G); result valid in thread 0
-template <int BS>
-__device__ __forceinline__ double sum_partials(const double* __restrict__ p, int G, double* scratch) {
-    double v0 = 0.0, v1 = 0.0;
-    int g = threadIdx.x;
-    for (; g + BS < G; g += 2 * BS) {
-        v0 += p[g];
-        v1 += p[g + BS];
-    }
-    if (g < G) v0 += p[g];
-    return block_sum<BS>(v0 + v1, scratch);
-}
-
-template <int BS>
-__global__ __launch_bounds__(BS) void k_reduce_partials(int G, const double* __restrict__ partial,
-                                                        double* __restrict__ sums) {
-    __shared__ double scratch[BS / kWave];
-    const double s = sum_partials<BS>(partial + (size_t)blockIdx.x * G, G, scratch);
-    if (threadIdx.x == 0) sums[blockIdx.x] = s;
-}
-
-// k_reduce_partials of the prologue's 3 columns + k_prologue_finish in one
-// workgroup (one GPU: nothing to all-reduce between them): each column is
-// summed by sum_partials<BS>, as its k_reduce_partials workgroup would, so
-// the sums and everything formed from them have the same bits
-template <class T, class X, int BS>
-__global__ __launch_bounds__(BS) void k_prologue_finish_parts(int G, const double* __restrict__ partial,
-                                                              double* __restrict__ sums, int m, T* __restrict__ s,
-                                                              T* __restrict__ inv, double* __restrict__ report) {
-    __shared__ double scratch[BS / kWave];
-    __shared__ double sm[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const double v = sum_partials<BS>(partial + (size_t)c * G, G, scratch);
-        if (threadIdx.x == 0) {
-            sm[c] = v;
-            sums[c] = v;
-        }
-    }
-    __syncthreads();
-    const T r_norm = (T)sqrt(sm[0]);
-    const T beta = (T)sqrt(sm[1]);
-    const X x_norm = (X)sqrt(sm[2]);
-    const T iv = beta != T(0) ? T(1) / beta : T(0);  // first_vector: zero fill when beta == 0
-    if (threadIdx.x == 0) {
-        report[0] = (double)r_norm;
-        report[1] = (double)beta;
-        report[2] = (double)x_norm;
-        report[3] = (double)iv;
-        *inv = iv;
-    }
-    for (int i = threadIdx.x; i <= m; i += blockDim.x) s[i] = i == 0 ? beta : T(0);
-}
-
-// ---------------------------------------------------------------- step: Givens
-#pragma clang fp contract(off)
-template <class T>
-__device__ void rot_pair(T& a, T& b, T c, T s) {
-    const T a1 = a, a2 = b;
-    a = c * a1 + s * a2;
-    b = c * a2 - s * a1;
-}
-template <class T>
-__device__ void rotg_ref(T& a, T& b, T& c, T& s) {
-    const T av = a, bv = b;
-    const T roe = fabs(av) > fabs(bv) ? av : bv;
-    const T scale = fabs(av) + fabs(bv);
-    T r;
-    if (scale == T(0)) {
-        c = T(1); s = T(0); r = T(0);
-    } else {
-        const T as = av / scale, bs = bv / scale;
-        r = scale * sqrt(as * as + bs * bs);
-        r = roe >= T(0) ? r : -r;
-        c = av / r;
-        s = bv / r;
-    }
-    a = r;
-    b = T(0);
-}
-
-// h_{k+1,k} = ||w||; (CGSR: h(0:k,k) += correction); rotations; |s(k+1)|.
-// norm2 = the squared norm: sums[0] (nparts == 0) or, on one GPU, the sum
-// of `nparts` workgroup partials reduced here (saves a launch per step).
-// Givens step k on one workgroup (gmres.cpp:217-226): col/c_s/s_s are LDS
-// arrays of at least k + 2 entries; nrm2sq (= ||w||^2) is read in thread 0.
-template <class T>
-struct GivensArgs {
-    int k, m;
-    const T* corr;  // CGSR correction (h += corr) or nullptr
-    T *H, *cs, *sn, *s, *inv;
-    double* report;
-};
-
-template <class T>
-__device__ void givens_block(const GivensArgs<T>& g, double nrm2sq, T* col, T* c_s, T* s_s) {
-    // stage the column and the previous rotations in LDS with all lanes, so
-    // the serial rotation chain runs on LDS instead of global latency
-    const int k = g.k;
-    T* gcol = g.H + (int64_t)k * (g.m + 1);
-    for (int j = threadIdx.x; j <= k; j += blockDim.x) {
-        col[j] = g.corr ? gcol[j] + T(1) * g.corr[j] : gcol[j];  // axpy(1.0, weights, h_col)
-        c_s[j] = g.cs[j];
-        s_s[j] = g.sn[j];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const T hn = (T)sqrt(nrm2sq);
-        col[k + 1] = hn;
-        *g.inv = T(1) / hn;  // scal(1/h_final, w, v_{k+1}) — no breakdown guard, as in the reference
-        for (int j = 0; j < k; ++j) rot_pair(col[j], col[j + 1], c_s[j], s_s[j]);
-        rotg_ref(col[k], col[k + 1], c_s[k], s_s[k]);
-        T sk = g.s[k], sk1 = g.s[k + 1];
-        rot_pair(sk, sk1, c_s[k], s_s[k]);
-        g.s[k] = sk;
-        g.s[k + 1] = sk1;
-        g.cs[k] = c_s[k];
-        g.sn[k] = s_s[k];
-        g.report[4 + k] = (double)fabs(sk1);
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j <= k + 1; j += blockDim.x) gcol[j] = col[j];
-}
-
-// the scale 1/h_{k+1,k} exactly as givens_block forms it
-template <class T>
-__device__ __forceinline__ T inv_of_norm2(double nrm2sq) {
-    return T(1) / (T)sqrt(nrm2sq);
-}
-
-// norm2 = the squared norm: sums[0] (nparts == 0) or, on one GPU, the sum
-// of `nparts` workgroup partials reduced here (saves a launch per step).
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_givens(GivensArgs<T> g, const double* __restrict__ norm2, int nparts) {
-    __shared__ T col[1026], c_s[1026], s_s[1026];
-    __shared__ double scratch[kBlock / kWave];
-    const double nrm2sq = nparts > 0 ? sum_partials<kBlock>(norm2, nparts, scratch) : norm2[0];
-    givens_block(g, nrm2sq, col, c_s, s_s);
-}
-
-// Givens step k-1 folded into the SpMV launch of step k (restart length
-// <= kFoldMaxM): every workgroup sums the ||w||^2 partials in the same
-// fixed order and forms 1/h_{k,k-1} itself; workgroup 0 also runs the
-// rotation step. Returns the scale for v_k in every thread.
-constexpr int kFoldMaxM = 128;  // GMRES(100), the reference's published restart length
-template <class T>
-struct GivensFold {
-    const double* norm2;  // nullptr: not folded (use *inv_p)
-    int nparts;
-    GivensArgs<T> g;
-};
-
-// measurement only (mpg_arnoldi_stamp_next): wave q's lane 0 stores the
-// wall clock to stamp[2q + end] (end 0 at the wave's start, 1 at its end); a
-// one-dimensional grid. Used by the one-panel dots and CGS update only: in
-// the SpMVs, whose occupancy sits on VGPR thresholds, even this uniform
-// branch cost up to 20 VGPRs (C4's stepped kernel 71 -> 91, -11 % in time),
-// and a branch-free form with a sink word slowed the BAND SpMV; the SpMV is
-// timed by duplicate launches instead (time_phase_dup, host/fused_gmres.cpp).
-// Round 5: a compile-time choice. The product instantiations
-// (STAMP = false) hold no stamp code at all; the launch sites pick the STAMP
-// = true instantiation only for a launch that mpg_arnoldi_stamp_next armed.
-template <bool STAMP>
-__device__ __forceinline__ void stamp_at(unsigned long long* stamp, int end) {
-    if constexpr (STAMP) {
-        if ((threadIdx.x & (kWave - 1)) == 0)
-            stamp[2 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave) + end] = wall_clock64();
-    }
-}
-
-template <bool FOLD, class T>
-__device__ __forceinline__ T fold_givens(const GivensFold<T>& f, const T* __restrict__ inv_p) {
-    if constexpr (!FOLD) {
-        return *inv_p;
-    } else {
-        __shared__ T col[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
-        __shared__ double scratch[kBlock / kWave];
-        __shared__ T inv_s;
-        const double nrm2sq = f.nparts > 0 ? sum_partials<kBlock>(f.norm2, f.nparts, scratch) : f.norm2[0];
-        if (threadIdx.x == 0) inv_s = inv_of_norm2<T>(nrm2sq);
-        if (blockIdx.x == 0) givens_block(f.g, nrm2sq, col, c_s, s_s);
-        __syncthreads();
-        return inv_s;
-    }
-}
-#pragma clang fp contract(on)
-
-// ---------------------------------------------------------------- step: SpMV
-// v_k = T(w_prev * inv) (local rows stored to V[:,k]); w = M(A v_k).
-// inv = 1/h_{k,k-1} from the previous Givens kernel, or formed here with
-// that Givens step folded in (fold.norm2 != nullptr). The Gram-Schmidt dots
-// follow in k_panel_dots (measured: dots inside this gather-bound launch
-// cost more than the separate pass, 71 us vs 30 + 20 us on BAND-10M).
-template <class T, class P, class VI, bool FOLD, int MODE = 0>
-__global__ __launch_bounds__(kBlock) void k_step_spmv(const int32_t* __restrict__ blocks, int nblocks,
-                                                      const int32_t* __restrict__ rowptr,
-                                                      const int32_t* __restrict__ col, const VI* __restrict__ val,
-                                                      int64_t nnz, const T* __restrict__ wprev,
-                                                      const T* __restrict__ inv_p, T* __restrict__ V, int64_t ld,
-                                                      int k, const P* __restrict__ diag, T* __restrict__ w,
-                                                      GivensFold<T> fold, const int8_t* __restrict__ rexp) {
-    __shared__ double prod[kNnzCap];
-    __shared__ double scratch[kBlock / kWave];
-    const T inv = fold_givens<FOLD>(fold, inv_p);
-    T* __restrict__ Vk = V + (int64_t)k * ld;
-    struct Ops {
-        T wp;
-        P d;
-        int e;  // row exponent of a scaled fp16 copy (mpg_csr_half_values)
-    };
-    // MODE bit 0: non-temporal matrix streams; bit 1: XCD-ordered row blocks;
-    // bit 2 (measurement only, wrong results): no gathers, x = 1
-    for_rows<(MODE & 1) != 0, (MODE & 2) != 0>(
-        blocks, nblocks, rowptr, col, val, nnz,
-        [&](int c) { return (MODE & 4) ? 1.0 + 0.0 * c : (double)(T)(wprev[c] * inv); },
-        [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0), rexp ? (int)rexp[i] : 0}; },
-        [&](int i, double sum, const Ops& o) {
-            const T t = (T)ldexp(sum, -o.e);  // spmv(1, A, v, 0, w): y = 1*t (exact unscale)
-            P pw = (P)t;         // = precond<T, P> with the diagonal loaded ahead
-            if (diag) pw = P(0) * pw + P(1) * o.d * pw;
-            w[i] = (T)pw;
-            Vk[i] = o.wp * inv;
-        },
-        prod, scratch);
-}
-
-// ---------------------------------------------------------------- step: SpMV (node blocks)
-// Same contract as k_step_spmv on the node-block copy (node_tile.hpp): one
-// tile of node rows per workgroup, the CSR tile's products and row order.
-// WALK: each workgroup walks tpw consecutive tiles, the next tile's records
-// in flight during this one's gathers and row sums (node_tiles); else one
-// tile per workgroup (node_tile).
-template <class T, class P, class VI, bool FOLD, bool WALK = true>
-__global__ __launch_bounds__(kBlock) void k_step_node(const int32_t* __restrict__ tiles,
-                                                      const int32_t* __restrict__ bptr, const char* __restrict__ recs,
-                                                      const T* __restrict__ wprev, const T* __restrict__ inv_p,
-                                                      T* __restrict__ V, int64_t ld, int k,
-                                                      const P* __restrict__ diag, T* __restrict__ w,
-                                                      GivensFold<T> fold, const int8_t* __restrict__ rexp,
-                                                      int ntiles, int64_t nblk, int tpw, int xcd) {
-    __shared__ double prod[kNodeProd];
-    const T inv = fold_givens<FOLD>(fold, inv_p);
-    T* __restrict__ Vk = V + (int64_t)k * ld;
-    struct Ops {
-        T wp;
-        P d;
-        int e;
-    };
-    auto xraw = [&](int c) { return wprev[c]; };
-    auto xfin = [&](T v) { return (double)(T)(v * inv); };
-    auto xval = [&](int c) { return xfin(xraw(c)); };
-    auto pre = [&](int i) { return Ops{wprev[i], diag ? diag[i] : P(0), rexp ? (int)rexp[i] : 0}; };
-    auto epi = [&](int i, double sum, const Ops& o) {
-        const T t = (T)ldexp(sum, -o.e);
-        P pw = (P)t;
-        if (diag) pw = P(0) * pw + P(1) * o.d * pw;
-        w[i] = (T)pw;
-        Vk[i] = o.wp * inv;
-    };
-    // xcd: workgroups take their tiles in XCD order (xcd_block), so each
-    // XCD's L2 serves one contiguous eighth of the rows' gathers
-    const int g = xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-    if constexpr (!WALK) {
-        node_tile<VI>(g, tiles, bptr, recs, xval, pre, epi, prod);
-    } else {
-        const int t0 = g * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
-        node_tiles<VI>(t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, xraw, xfin, pre, epi, prod);
-    }
-}
-
-// ---------------------------------------------------------------- step: SpMV (SELL-64)
-// Same contract as k_step_spmv on the sliced-ELL copy (sell_tile.hpp): one
-// wave per slice, one lane per row; v_k and w are written coalesced.
-// WIN (every column of a slice within [row0 - kWinLo, row0 + 64 + kWinHi),
-// checked when the copy is built): the slice's window of v_k is formed once
-// in LDS with three coalesced loads per lane and the gathers read LDS —
-// 10 scattered global loads per row become LDS reads (-20 % on BAND-10M,
-// tools/sell_bench.hip). Values are the same T(w_prev * inv) either way.
-
-//
-// Load order (vmcnt retires in order, so what is needed first is issued
-// first, and nothing is waited for before everything is in flight): the
-// slice's offsets, the folded Givens step's partial (one per lane), the
-// window of w_prev (raw,
-// clamped addresses), the slice's first batch of (col, val); then the
-// partial sum behind LDS-only barriers, the scaled window into LDS, the
-// gathers. A guarded load would be widened inside its branch and waited
-// for right there — the previous form waited for each window load and each
-// step's loads in turn.
-// DN > 0 (one GPU, CGS, k + 1 <= DN): the panel dots <v_j, w> for j <= k
-// are formed here too, from the lane's own w(i) (no re-read of w and no dots
-// launch). Each workgroup block-reduces its products (store_partials); the
-// last arriver of each group of `gs` workgroups sums the group's partials
-// in workgroup order, so the CGS update (FROM_PARTS) sees <= 256 partials
-// per column, as from k_dots_nc. Deterministic: fixed order throughout.
-struct SellDots {
-    int nc;            // columns: k + 1
-    int gs, ng;        // workgroups per group, groups (<= kCombineGroups)
-    double* wgpart;    // [c * gridDim.x + blockIdx.x]
-    unsigned* cnt;     // one ticket per group (zero between launches)
-    double* out;       // [c * ng + g]
-};
-
-template <class T, class P, class VI, class CI, int W, bool WIN, bool FOLD, int DN = 0, int BS = kBlock,
-          bool UNI = false, bool PIPE = false>
-__global__ __launch_bounds__(BS) void k_step_sell(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
-                                                      const CI* __restrict__ col,
-                                                      const typename SellStore<VI>::type* __restrict__ val,
-                                                      const T* __restrict__ wprev, const T* __restrict__ inv_p,
-                                                      T* __restrict__ V, int64_t ld, int k,
-                                                      const P* __restrict__ diag, T* __restrict__ w,
-                                                      GivensFold<T> fold, SellDots dd,
-                                                      const int32_t* __restrict__ sbase,
-                                                      const int32_t* __restrict__ spat, const int64_t* __restrict__ coff, const CI* __restrict__ pat,
-                                                      const int32_t* __restrict__ xrp,
-                                                      const int32_t* __restrict__ xcol,
-                                                      const typename SellStore<VI>::type* __restrict__ xval,
-                                                      const int8_t* __restrict__ rexp, int64_t ustride, int xcd,
-                                                      const int32_t* __restrict__ rows) {
-    static_assert(DN == 0 || BS == kBlock, "the fused dots' partials assume kBlock-thread workgroups");
-    using S = typename SellStore<VI>::type;
-    constexpr int NQ = kWinLen / kWave;
-    __shared__ T win[WIN ? BS / kWave : 1][WIN ? kWinLen : 1];
-    const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
-    const int s = (xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid;
-    const bool live = s < nslices;  // a dead wave still joins the fold's barriers
-    const int row0 = s * kWave;
-    // the lane's row: row0 + lane, or a sorted (SELL-C-sigma) copy's rows[],
-    // loaded behind the slice's first batch (below); nothing before needs it
-    int i = row0 + lane;
-    // 0. the slice's offsets (UNI: computed) and pattern index
-    SellRow<S, CI, W> row;
-    if constexpr (UNI) row.init_uniform(live ? s : 0, ustride, spat, coff);
-    else row.init_load(live ? s : 0, off, spat, coff);
-    __builtin_amdgcn_sched_barrier(0);
-    // 1. the fold's ||w||^2 partial (nparts <= kBlock, checked at launch: one per lane)
-    // (a workgroup narrower than kBlock loads kBlock / BS per lane: the
-    // partials keep their kBlock-lane positions, so the sums below run in
-    // the same order whatever BS is)
-    constexpr int NPL = BS < kBlock ? kBlock / BS : 1;
-    double part[NPL];
-#pragma unroll
-    for (int j = 0; j < NPL; ++j) part[j] = 0.0;
-    if constexpr (FOLD) {
-#pragma unroll
-        for (int j = 0; j < NPL; ++j) {
-            const int t = j * BS + (int)threadIdx.x;
-            part[j] = fold.norm2[t < fold.nparts ? t : 0];
-            if (t >= fold.nparts) part[j] = 0.0;
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // 2. w_prev window (or this row's own w_prev), raw
-    T wr[WIN ? NQ : 1];
-    if constexpr (WIN) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int c = row0 - kWinLo + q * kWave + lane;
-            wr[q] = wprev[c >= n_lo && c < n_ext ? c : 0];
-        }
-    } else {
-        if (!rows) wr[0] = wprev[i < n ? i : 0];  // the round-3 order (unsorted copies)
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // 3. the slice's first batch (UNI: the values before the pattern index
-    // is waited for, then the columns)
-    if constexpr (UNI) {
-        row.init_vals(lane, val);
-        row.load_vals(0);
-        __builtin_amdgcn_sched_barrier(0);
-        row.init_finish(lane, col, val, sbase, pat);
-        row.load_cols(0);
-    } else {
-        row.init_finish(lane, col, val, sbase, pat);
-        row.load(0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // 3b. without the window, sorted (SELL-C-sigma) copies: the lane's row and
-    // its own w_prev, behind the first batch (needed last)
-    if constexpr (!WIN) {
-        if (rows) {
-            i = rows[live ? row0 + lane : 0];
-            wr[0] = wprev[i < n ? i : 0];
-        }
-    }
-    // 4. a scaled fp16 copy's row exponent (needed last, issued last)
-    int rex = 0;
-    if constexpr (std::is_same_v<VI, half_v>) {
-        if (rexp) rex = rexp[live && i < n ? i : 0];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // the scale 1/h_{k,k-1}: the folded Givens step, or the Givens kernel's
-    T inv;
-    // the folded step's ||w||^2; workgroup 0 runs the rotation step with it
-    // after its own rows (nothing in this launch reads what the rotation
-    // writes, and its serial chain then holds none of the slice's loads live)
-    double nrm2sq = 0.0;
-    if constexpr (FOLD) {
-        constexpr int NG = (BS < kBlock ? kBlock : BS) / kWave;
-        __shared__ double scratch[NG];
-        __shared__ T inv_s;
-        if (fold.nparts > 0) {
-#pragma unroll
-            for (int j = 0; j < NPL; ++j) {
-                const double v = wave_sum(part[j] + 0.0);  // the same fixed order in every workgroup
-                if (lane == 0) scratch[j * (BS / kWave) + wid] = v;
-            }
-            lds_barrier();
-            double r = 0.0;
-#pragma unroll
-            for (int q = 0; q < NG; ++q) r += scratch[q];
-            nrm2sq = r;
-        } else {
-            nrm2sq = fold.norm2[0];
-        }
-        if (threadIdx.x == 0) inv_s = inv_of_norm2<T>(nrm2sq);
-        lds_barrier();
-        inv = inv_s;
-    } else {
-        inv = *inv_p;
-    }
-    // with dots, a dead wave joins the partials' barriers; with the fold,
-    // workgroup 0's waves all join the rotation step's barriers at the end
-    if (DN == 0 && !live && !(FOLD && blockIdx.x == 0)) return;
-    double sum = 0.0;
-    T vk = T(0);  // v_k(i) = T(w_prev(i) * inv)
-    if (live) {
-        if constexpr (WIN) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int c = row0 - kWinLo + q * kWave + lane;
-                win[wid][q * kWave + lane] = (c >= n_lo && c < n_ext) ? (T)(wr[q] * inv) : T(0);
-            }
-            wave_lds_sync();
-            auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
-            row.sum(0, xv, sum);
-            for (int q = row.U; q < row.steps; q += row.U) {
-                row.load(q);
-                row.sum(q, xv, sum);
-            }
-            vk = win[wid][lane + kWinLo];
-        } else {
-            auto xv = [&](int c) { return (double)(T)(wprev[c] * inv); };
-            if (SellCol<CI>::stepped && row.exc) {
-                sum = csr_row_sum(i < n ? row.xrow : -1, xrp, xcol, xval, xv);
-            } else if constexpr (PIPE) {
-                // two batch buffers: batch q's gathers are issued, then batch
-                // q + U's loads, so the wait for the gathers leaves the next
-                // batch's loads in flight under the sums (one HBM round trip
-                // per batch instead of a load round trip then a gather round
-                // trip). x is gathered raw and scaled at the sum: the same
-                // (T)(w_prev * inv) operand, the same bits.
-                using Row = SellRow<S, CI, W>;
-                Row rb;
-                rb.geom_from(row);
-                auto xraw = [&](int c) { return wprev[c]; };
-                auto xs = [&](T r) { return (double)(T)(r * inv); };
-                T x[Row::U][W];
-                for (int q = 0;;) {
-                    row.gather(xraw, x);
-                    __builtin_amdgcn_sched_barrier(0);
-                    rb.load(q + Row::U);
-                    __builtin_amdgcn_sched_barrier(0);
-                    row.sum_gathered(q, x, xs, sum);
-                    q += Row::U;
-                    if (q >= row.steps) break;
-                    rb.gather(xraw, x);
-                    __builtin_amdgcn_sched_barrier(0);
-                    row.load(q + Row::U);
-                    __builtin_amdgcn_sched_barrier(0);
-                    rb.sum_gathered(q, x, xs, sum);
-                    q += Row::U;
-                    if (q >= row.steps) break;
-                }
-            } else {
-                row.sum(0, xv, sum);
-                for (int q = row.U; q < row.steps; q += row.U) {
-                    row.load(q);
-                    row.sum(q, xv, sum);
-                }
-            }
-            vk = (T)(wr[0] * inv);
-        }
-    }
-    T wi = T(0);
-    if (live && i < n) {
-        if constexpr (std::is_same_v<VI, half_v>) sum = ldexp(sum, -rex);  // exact unscale (0: unchanged)
-        const T t = (T)sum;  // spmv(1, A, v, 0, w): y = 1*t
-        wi = precond<T, P>(t, diag, i);
-        w[i] = wi;
-        V[(int64_t)k * ld + i] = vk;
-    }
-    if constexpr (DN > 0) {
-        // the earlier basis columns at this row: clamped, branch-free loads
-        // issued together (one latency), then one product per column
-        // (n >= 1: spmv_impl refuses the fused dots on an empty block, so row n - 1 exists)
-        const bool own_row = live && i < n;
-        const int ic = i < n ? i : n - 1;
-        const int kc = k > 0 ? k - 1 : 0;
-        T vc[DN];
-#pragma unroll
-        for (int c = 0; c < DN; ++c) vc[c] = V[(int64_t)(c < kc ? c : kc) * ld + ic];
-        __builtin_amdgcn_sched_barrier(0);
-        const double wd = (double)wi;
-        double acc[DN];
-        // a lane without a row contributes an exact 0 (not a clamped row's
-        // value times 0, which is NaN when that value is Inf or NaN)
-#pragma unroll
-        for (int c = 0; c < DN; ++c)
-            acc[c] = own_row ? (c < k ? (double)vc[c] : c == k ? (double)vk : 0.0) * wd : 0.0;
-        store_partials<DN, kBlock, true>(acc, dd.nc, dd.wgpart);
-        const int g = blockIdx.x / dd.gs;
-        const int m0 = g * dd.gs, m1 = m0 + dd.gs < (int)gridDim.x ? m0 + dd.gs : (int)gridDim.x;
-        if (last_arriver_of(dd.cnt + g, (unsigned)(m1 - m0)) && (int)threadIdx.x < dd.nc) {
-            const int c = threadIdx.x;
-            double v = 0.0;
-            for (int m = m0; m < m1; ++m) v += dd.wgpart[(size_t)c * gridDim.x + m];
-            dd.out[(size_t)c * dd.ng + g] = v;
-        }
-    }
-    if constexpr (FOLD) {
-        __shared__ T col_s[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
-        if (blockIdx.x == 0) givens_block(fold.g, nrm2sq, col_s, c_s, s_s);
-    }
-}
-
-// k_step_sell with two adjacent slices per wave (lane l owns rows
-// 128 s' + l and 128 s' + 64 + l): every load of both slices -- one LDS
-// window of 64 + 128 + 64 entries for the pair, both slices' first batches --
-// is in flight before the wave waits for any, so each wave carries twice the
-// bytes through the same fixed work (the fold's partial sum, the barriers,
-// the window). Past the Infinity Cache a slice's loads alone do not keep
-// enough bytes in flight per CU (MI355X_MICROARCH.md: ~72 KiB per CU hides
-// an HBM miss). Same sums in the same order as k_step_sell: same bits.
-template <class T, class P, class VI, int W, bool WIN, bool FOLD, int BE, int BS = kBlock, bool PG = true>
-__global__ __launch_bounds__(BS) void k_step_sell2(int n, int n_lo, int n_ext, int nslices, const int64_t* __restrict__ off,
-                                                   const int16_t* __restrict__ col,
-                                                   const typename SellStore<VI>::type* __restrict__ val,
-                                                   const T* __restrict__ wprev, const T* __restrict__ inv_p,
-                                                   T* __restrict__ V, int64_t ld, int k,
-                                                   const P* __restrict__ diag, T* __restrict__ w,
-                                                   GivensFold<T> fold, SellDots,
-                                                   const int32_t* __restrict__ sbase,
-                                                   const int32_t* __restrict__ spat, const int64_t* __restrict__ coff, const int16_t* __restrict__ pat,
-                                                   const int32_t* __restrict__ xrp,
-                                                   const int32_t* __restrict__ xcol,
-                                                   const typename SellStore<VI>::type* __restrict__ xval,
-                                                   const int8_t* __restrict__ rexp, int64_t ustride, int xcd) {
-    using S = typename SellStore<VI>::type;
-    using CI = int16_t;
-    constexpr bool UNI = true;
-    constexpr int SPW = 2;
-    constexpr int WL = kWinLen + (SPW - 1) * kWave;  // the pair's window
-    constexpr int NQ = WL / kWave;
-    __shared__ T win[WIN ? BS / kWave : 1][WIN ? WL : 1];
-    const int lane = threadIdx.x & (kWave - 1), wid = wave_id();
-    const int s0 = ((xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * (BS / kWave) + wid) * SPW;
-    const bool live = s0 < nslices;  // a dead wave still joins the fold's barriers
-    bool live_p[SPW];
-    const int row0 = s0 * kWave;
-    // 0. both slices' offsets (UNI: computed) and pattern indices
-    SellRow<S, CI, W, (MPG_SELL_NT != 0), BE> row[SPW];
-#pragma unroll
-    for (int p = 0; p < SPW; ++p) {
-        live_p[p] = s0 + p < nslices;
-        const int sp = live_p[p] ? s0 + p : 0;
-        if constexpr (UNI) row[p].init_uniform(sp, ustride, spat, coff);
-        else row[p].init_load(sp, off, spat, coff);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // 1. the fold's ||w||^2 partial (one per lane, as k_step_sell)
-    constexpr int NPL = BS < kBlock ? kBlock / BS : 1;
-    double part[NPL];
-#pragma unroll
-    for (int j = 0; j < NPL; ++j) part[j] = 0.0;
-    if constexpr (FOLD) {
-#pragma unroll
-        for (int j = 0; j < NPL; ++j) {
-            const int t = j * BS + (int)threadIdx.x;
-            part[j] = fold.norm2[t < fold.nparts ? t : 0];
-            if (t >= fold.nparts) part[j] = 0.0;
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // 2. the pair's w_prev window (or the lane's own rows' w_prev), raw
-    T wr[WIN ? NQ : SPW];
-    if constexpr (WIN) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int c = row0 - kWinLo + q * kWave + lane;
-            wr[q] = wprev[c >= n_lo && c < n_ext ? c : 0];
-        }
-    } else {
-#pragma unroll
-        for (int p = 0; p < SPW; ++p) {
-            const int i = row0 + p * kWave + lane;
-            wr[p] = wprev[i < n ? i : 0];
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // 3. both slices' first batches (UNI: values first, then the columns)
-    if constexpr (UNI) {
-#pragma unroll
-        for (int p = 0; p < SPW; ++p) {
-            row[p].init_vals(lane, val);
-            row[p].load_vals(0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int p = 0; p < SPW; ++p) {
-            row[p].init_finish(lane, col, val, sbase, pat);
-            row[p].load_cols(0);
-        }
-    } else {
-#pragma unroll
-        for (int p = 0; p < SPW; ++p) {
-            row[p].init_finish(lane, col, val, sbase, pat);
-            row[p].load(0);
-        }
-    }
-    // 4. a scaled fp16 copy's row exponents
-    int rex[SPW] = {};
-    if constexpr (std::is_same_v<VI, half_v>) {
-        if (rexp) {
-#pragma unroll
-            for (int p = 0; p < SPW; ++p) {
-                const int i = row0 + p * kWave + lane;
-                rex[p] = rexp[live_p[p] && i < n ? i : 0];
-            }
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // 5. PG, no window: the first batch's gathers of w_prev, raw, issued
-    // before the scale is known (the fold's sums and barriers), and scaled
-    // at the sum: (T)(w_prev * inv), the same operation, the same bits.
-    // A dead wave gathers for slice 0 (valid addresses) and returns.
-    constexpr bool PRE = PG && !WIN;
-    using RowT = SellRow<S, CI, W, (MPG_SELL_NT != 0), BE>;
-    T xr[PRE ? SPW : 1][PRE ? RowT::U : 1][PRE ? W : 1];
-    if constexpr (PRE) {
-#pragma unroll
-        for (int p = 0; p < SPW; ++p) row[p].gather([&](int c) { return wprev[c]; }, xr[p]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    T inv;
-    double nrm2sq = 0.0;
-    if constexpr (FOLD) {
-        constexpr int NG = (BS < kBlock ? kBlock : BS) / kWave;
-        __shared__ double scratch[NG];
-        __shared__ T inv_s;
-        if (fold.nparts > 0) {
-#pragma unroll
-            for (int j = 0; j < NPL; ++j) {
-                const double v = wave_sum(part[j] + 0.0);
-                if (lane == 0) scratch[j * (BS / kWave) + wid] = v;
-            }
-            lds_barrier();
-            double r = 0.0;
-#pragma unroll
-            for (int q = 0; q < NG; ++q) r += scratch[q];
-            nrm2sq = r;
-        } else {
-            nrm2sq = fold.norm2[0];
-        }
-        if (threadIdx.x == 0) inv_s = inv_of_norm2<T>(nrm2sq);
-        lds_barrier();
-        inv = inv_s;
-    } else {
-        inv = *inv_p;
-    }
-    if (!live && !(FOLD && blockIdx.x == 0)) return;
-    double sum[SPW] = {};
-    T vk[SPW] = {};
-    if (live) {
-        if constexpr (WIN) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int c = row0 - kWinLo + q * kWave + lane;
-                win[wid][q * kWave + lane] = (c >= n_lo && c < n_ext) ? (T)(wr[q] * inv) : T(0);
-            }
-            wave_lds_sync();
-            auto xv = [&](int c) { return (double)win[wid][c - row0 + kWinLo]; };
-#pragma unroll
-            for (int p = 0; p < SPW; ++p) row[p].sum(0, xv, sum[p]);
-#pragma unroll
-            for (int p = 0; p < SPW; ++p) {
-                for (int q = row[p].U; q < row[p].steps; q += row[p].U) {
-                    row[p].load(q);
-                    row[p].sum(q, xv, sum[p]);
-                }
-                vk[p] = win[wid][p * kWave + lane + kWinLo];
-            }
-        } else {
-            auto xv = [&](int c) { return (double)(T)(wprev[c] * inv); };
-#pragma unroll
-            for (int p = 0; p < SPW; ++p) {
-                const int i = row0 + p * kWave + lane;
-                if (SellCol<CI>::stepped && row[p].exc) {
-                    sum[p] = csr_row_sum(live_p[p] && i < n ? row[p].xrow : -1, xrp, xcol, xval, xv);
-                } else {
-                    if constexpr (PRE) row[p].sum_gathered(0, xr[p], [&](T r) { return (double)(T)(r * inv); }, sum[p]);
-                    else row[p].sum(0, xv, sum[p]);
-                    for (int q = row[p].U; q < row[p].steps; q += row[p].U) {
-                        row[p].load(q);
-                        row[p].sum(q, xv, sum[p]);
-                    }
-                }
-                vk[p] = (T)(wr[p] * inv);
-            }
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < SPW; ++p) {
-        const int i = row0 + p * kWave + lane;
-        if (live_p[p] && i < n) {
-            double sp = sum[p];
-            if constexpr (std::is_same_v<VI, half_v>) sp = ldexp(sp, -rex[p]);
-            const T t = (T)sp;
-            w[i] = precond<T, P>(t, diag, i);
-            V[(int64_t)k * ld + i] = vk[p];
-        }
-    }
-    if constexpr (FOLD) {
-        __shared__ T col_s[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
-        if (blockIdx.x == 0) givens_block(fold.g, nrm2sq, col_s, c_s, s_s);
-    }
-}
-
-// Tall-skinny panel reduction: partial <v_j, w> for j in [c0, c0 + nc),
-// nc <= kNC, over all local rows. Each lane owns 4 consecutive rows per
-// iteration (16-B loads of every column: V's leading dimension is padded to
-// 256 B), issues all column loads before its FMAs, and keeps one fp64
-// accumulator per column; store_partials does the wave64/LDS combine.
-// BS threads per workgroup. COMBINE (one GPU, nc <= kNC, c0 == 0): the
-// partials go write-through and the last-arriving workgroup sums them into
-// sums[0..nc) itself — no separate reduce launch (BS = 1024, so one
-// workgroup per CU keeps the partial count at 256 per column).
-template <class T, int BS = kBlock, bool COMBINE = false>
-__global__ __launch_bounds__(BS) void k_panel_dots(int n, const T* __restrict__ V, int64_t ld, int c0, int nc,
-                                                   const T* __restrict__ w, double* __restrict__ partial,
-                                                   unsigned* __restrict__ cnt, double* __restrict__ sums) {
-    double acc[kNC];
-#pragma unroll
-    for (int c = 0; c < kNC; ++c) acc[c] = 0.0;
-    const int n4 = n & ~3;
-    const T* __restrict__ Vb = V + (int64_t)c0 * ld;
-    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
-        double wv[4];
-        Row4<T>::load(w + i, wv);
-#pragma unroll
-        for (int c = 0; c < kNC; ++c) {
-            if (c < nc) {
-                double v[4];
-                Row4<T>::load(Vb + (int64_t)c * ld + i, v);
-                acc[c] += v[0] * wv[0] + v[1] * wv[1] + v[2] * wv[2] + v[3] * wv[3];
-            }
-        }
-    }
-    // tail rows (n not a multiple of 4)
-    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
-        const double wi = (double)w[i];
-#pragma unroll
-        for (int c = 0; c < kNC; ++c)
-            if (c < nc) acc[c] += (double)Vb[(int64_t)c * ld + i] * wi;
-    }
-    store_partials<kNC, BS, COMBINE>(acc, nc, partial + (size_t)c0 * gridDim.x);
-    if constexpr (COMBINE) {
-        if (last_arriver(cnt)) combine_columns<BS>(partial, gridDim.x, nc, sums);
-    }
-}
-
-// The one-panel forms of the dots and the CGS update with the column count
-// NC a compile-time constant (the captured cycle knows k at every step):
-// every column index is static, so the loads of a batch of columns issue
-// back to back and the accumulators stay in registers. With a runtime
-// count the compiler guarded each column's load with its own branch and
-// waited for it before the next (one memory latency per column: t(k) =
-// 8.6 + 0.50 k us for the dots on BAND-10M, tools/per_step.py).
-template <class T, int BS, int NC>
-__device__ __forceinline__ void dots_panel(int n, const T* __restrict__ V, int64_t ld, const T* __restrict__ w,
-                                           double* __restrict__ partial) {
-    static_assert(NC >= 1 && NC <= kNC, "one panel");
-    constexpr int NP = Pow2Ceil<NC>::v;
-    constexpr int B = kColBatch<T>;
-    double acc[NP];
-#pragma unroll
-    for (int c = 0; c < NP; ++c) acc[c] = 0.0;
-    const int n4 = n & ~3;
-    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
-        double wv[4];
-        Row4<T>::load(w + i, wv);
-#pragma unroll
-        for (int c0 = 0; c0 < NC; c0 += B) {
-            Raw4<T> v[B];
-#pragma unroll
-            for (int u = 0; u < B; ++u)
-                if (c0 + u < NC) v[u].load(V + (int64_t)(c0 + u) * ld + i);
-            __builtin_amdgcn_sched_barrier(0);  // keep the batch's loads issued back to back
-#pragma unroll
-            for (int u = 0; u < B; ++u)
-                if (c0 + u < NC) acc[c0 + u] += v[u][0] * wv[0] + v[u][1] * wv[1] + v[u][2] * wv[2] + v[u][3] * wv[3];
-        }
-    }
-    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
-        const double wi = (double)w[i];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) acc[c] += (double)V[(int64_t)c * ld + i] * wi;
-    }
-    store_partials<NP, BS>(acc, NC, partial);
-}
-
-template <class T, int BS, int NC, bool STAMP = false>
-__global__ __launch_bounds__(BS) void k_dots_nc(int n, const T* __restrict__ V, int64_t ld,
-                                                const T* __restrict__ w, double* __restrict__ partial,
-                                                unsigned long long* stamp) {
-    stamp_at<STAMP>(stamp, 0);
-    dots_panel<T, BS, NC>(n, V, ld, w, partial);
-    stamp_at<STAMP>(stamp, 1);
-}
-
-// V^T w for nc > kNC columns in ONE launch (GMRES(100): the round-3 form ran
-// one runtime-count k_panel_dots launch per 32 columns, each re-reading w and
-// waiting for every column in turn): blockIdx.y is the 32-column panel,
-// the last one holding NCL columns; blockIdx.x a row group. The grid keeps
-// about one workgroup per CU in total (gridDim.x = kCombineGroups / panels),
-// so each column gets gridDim.x <= 128 partials, [column][gridDim.x], which
-// the wide CGS update sums itself (k_cgs_update_wide).
-template <class T, int BS, int NCL>
-__global__ __launch_bounds__(BS) void k_dots_panels(int n, const T* __restrict__ V, int64_t ld,
-                                                    const T* __restrict__ w, double* __restrict__ partial) {
-    const int c0 = blockIdx.y * kNC;
-    double* __restrict__ part = partial + (size_t)c0 * gridDim.x;
-    if (blockIdx.y + 1 < gridDim.y) dots_panel<T, BS, kNC>(n, V + (int64_t)c0 * ld, ld, w, part);
-    else dots_panel<T, BS, NCL>(n, V + (int64_t)c0 * ld, ld, w, part);
-}
-
-// coef = T(sums[0..NC)); w = w - T(V coef); partial ||w'||^2 (the last
-// CGS pass; same arithmetic and order as k_cgs_update).
-// FROM_PARTS (one GPU): the coefficients are summed here from the one-panel
-// dots' part_G <= kCombineGroups partials per column (32 lanes per column,
-// each summing its 8 strided partials in g order, then a 32-lane xor tree:
-// the same fixed order in every workgroup) instead of a reduce launch. The 8
-// loads per lane are branch-free so they issue together: one latency.
-// NEXT_DOTS (CGSR's first pass): the partials of <v_j, w'> for j < NC
-// instead of ||w'||^2, from a second batched pass over the lane's columns.
-// PF (with FROM_PARTS): the lane's first row group -- w and the first batch
-// of basis columns, raw and unconditional (clamped row) -- is issued right
-// behind the partial loads, so its memory latency runs under the coefficient
-// sums; the coefficients are published with an LDS-only barrier
-// (__syncthreads would drain those loads). Same operands, same order.
-template <class T, int BS, int NC, bool FROM_PARTS = false, bool NEXT_DOTS = false, bool PF = false,
-          bool STAMP = false>
-__global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict__ V, int64_t ld,
-                                                      const double* __restrict__ sums, int part_G,
-                                                      T* __restrict__ coef_out, T* __restrict__ w,
-                                                      double* __restrict__ partial, unsigned long long* stamp) {
-    static_assert(NC >= 1 && NC <= kNC, "one panel");
-    stamp_at<STAMP>(stamp, 0);
-    static_assert(!FROM_PARTS || BS >= 32 * NC, "32 lanes per column");
-    static_assert(!PF || (FROM_PARTS && !NEXT_DOTS), "prefetch under the partial sums");
-    constexpr int B = kColBatch<T>;
-    constexpr int B0 = NC < B ? NC : B;
-    __shared__ double coef[NC];
-    const int n4 = n & ~3;
-    const int i_first = 4 * (blockIdx.x * BS + threadIdx.x);
-    Raw4<T> pw, pv[PF ? B0 : 1];
-    if constexpr (FROM_PARTS) {
-        const int j = threadIdx.x / 32, sub = threadIdx.x % 32;
-        const int jc = j < NC ? j : NC - 1;
-        constexpr int Q = kCombineGroups / 32;
-        double pp[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int g = sub + 32 * q;
-            pp[q] = sums[(size_t)jc * part_G + (g < part_G ? g : 0)];
-        }
-        if constexpr (PF) {
-            __builtin_amdgcn_sched_barrier(0);
-            const int ip = i_first < n4 ? i_first : 0;
-            pw.load(w + ip);
-#pragma unroll
-            for (int u = 0; u < B0; ++u) pv[u].load(V + (int64_t)u * ld + ip);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        double v = 0.0;
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-            if (sub + 32 * q < part_G) v += pp[q];
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-        if (j < NC && sub == 0) {
-            const T c = (T)v;
-            coef[j] = (double)c;
-            if (blockIdx.x == 0) coef_out[j] = c;
-        }
-    } else if (threadIdx.x < NC) {
-        const T c = (T)sums[threadIdx.x];
-        coef[threadIdx.x] = (double)c;
-        if (blockIdx.x == 0) coef_out[threadIdx.x] = c;
-    }
-    if constexpr (PF) lds_barrier();
-    else __syncthreads();
-    constexpr int NA = NEXT_DOTS ? Pow2Ceil<NC>::v : 1;
-    double acc[NA];
-#pragma unroll
-    for (int c = 0; c < NA; ++c) acc[c] = 0.0;
-    bool first = PF;
-    for (int i = i_first; i < n4; i += 4 * gridDim.x * BS) {
-        Raw4<T> wr;
-        if (first) wr = pw;
-        else wr.load(w + i);
-        double t[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int c0 = 0; c0 < NC; c0 += B) {
-            Raw4<T> v[B];
-#pragma unroll
-            for (int u = 0; u < B; ++u)
-                if (c0 + u < NC) {
-                    if (c0 == 0 && first) v[u] = pv[u < B0 ? u : 0];
-                    else v[u].load(V + (int64_t)(c0 + u) * ld + i);
-                }
-            __builtin_amdgcn_sched_barrier(0);  // keep the batch's loads issued back to back
-#pragma unroll
-            for (int u = 0; u < B; ++u)
-                if (c0 + u < NC) {
-                    const double cu = coef[c0 + u];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) t[r] += v[u][r] * cu;
-                }
-        }
-        T wo[4];
-        double wd[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            wo[r] = T(-1) * (T)t[r] + T(1) * (T)wr[r];
-            wd[r] = (double)wo[r];
-            if (!NEXT_DOTS) acc[0] += wd[r] * wd[r];
-        }
-        Row4<T>::store(w + i, wo);
-        first = false;
-        if constexpr (NEXT_DOTS) {
-#pragma unroll
-            for (int c0 = 0; c0 < NC; c0 += B) {
-                Raw4<T> v[B];
-#pragma unroll
-                for (int u = 0; u < B; ++u)
-                    if (c0 + u < NC) v[u].load(V + (int64_t)(c0 + u) * ld + i);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int u = 0; u < B; ++u)
-                    if (c0 + u < NC)
-                        acc[c0 + u] += v[u][0] * wd[0] + v[u][1] * wd[1] + v[u][2] * wd[2] + v[u][3] * wd[3];
-            }
-        }
-    }
-    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
-        double t = 0.0;
-#pragma unroll
-        for (int j = 0; j < NC; ++j) t += (double)V[(int64_t)j * ld + i] * coef[j];
-        const T wi = T(-1) * (T)t + T(1) * w[i];
-        w[i] = wi;
-        if constexpr (NEXT_DOTS) {
-#pragma unroll
-            for (int c = 0; c < NC; ++c) acc[c] += (double)V[(int64_t)c * ld + i] * (double)wi;
-        } else {
-            acc[0] += (double)wi * (double)wi;
-        }
-    }
-    store_partials<NA, BS>(acc, NEXT_DOTS ? NC : 1, partial);
-    stamp_at<STAMP>(stamp, 1);
-}
-
-// The CGS update for kNC < nc <= kWideMax columns (GMRES(100)): the
-// coefficients are summed here from k_dots_panels' part_G <= 128 partials per
-// column (8 lanes per column, 16 branch-free loads each in g order, then an
-// xor tree: the same fixed order in every workgroup; no reduce launch), then
-// w = w - T(V coef) with 4 rows per lane, the columns in compile-time batches
-// of B (the last batch clamped to column nc - 1 with coefficient 0: +0 terms,
-// so t is the j-ordered sum of the real terms), and the ||w'||^2 partials.
-constexpr int kWideMax = 128;
-template <class T, int BS>
-__global__ __launch_bounds__(BS) void k_cgs_update_wide(int n, const T* __restrict__ V, int64_t ld, int nc,
-                                                        const double* __restrict__ parts, int part_G,
-                                                        T* __restrict__ coef_out, T* __restrict__ w,
-                                                        double* __restrict__ partial) {
-    constexpr int LPC = BS / kWideMax, Q = 128 / LPC, B = kColBatch<T>;
-    static_assert(LPC * kWideMax == BS && Q * LPC == 128, "8 lanes per column, <= 128 partials");
-    __shared__ double coef[kWideMax];
-    {
-        const int j = threadIdx.x / LPC, sub = threadIdx.x % LPC;
-        const int jc = j < nc ? j : nc - 1;
-        double pp[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int g = sub + LPC * q;
-            pp[q] = parts[(size_t)jc * part_G + (g < part_G ? g : 0)];
-        }
-        double v = 0.0;
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-            if (sub + LPC * q < part_G) v += pp[q];
-#pragma unroll
-        for (int o = LPC / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-        if (sub == 0) {
-            const T c = (T)v;
-            coef[j] = j < nc ? (double)c : 0.0;
-            if (blockIdx.x == 0 && j < nc) coef_out[j] = c;
-        }
-    }
-    __syncthreads();
-    double acc[1] = {0.0};
-    const int n4 = n & ~3;
-    const int nb = (nc + B - 1) / B;
-    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
-        Raw4<T> wr;
-        wr.load(w + i);
-        double t[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int bi = 0; bi < nb; ++bi) {
-            const int c0 = bi * B;
-            Raw4<T> v[B];
-#pragma unroll
-            for (int u = 0; u < B; ++u) {
-                const int c = c0 + u < nc ? c0 + u : nc - 1;
-                v[u].load(V + (int64_t)c * ld + i);
-            }
-            __builtin_amdgcn_sched_barrier(0);  // keep the batch's loads issued back to back
-#pragma unroll
-            for (int u = 0; u < B; ++u) {
-                const double cu = coef[c0 + u < kWideMax ? c0 + u : kWideMax - 1];
-                if (c0 + u < nc)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) t[r] += v[u][r] * cu;
-            }
-        }
-        T wo[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            wo[r] = T(-1) * (T)t[r] + T(1) * (T)wr[r];
-            const double wd = (double)wo[r];
-            acc[0] += wd * wd;
-        }
-        Row4<T>::store(w + i, wo);
-    }
-    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
-        double t = 0.0;
-        for (int j = 0; j < nc; ++j) t += (double)V[(int64_t)j * ld + i] * coef[j];
-        const T wi = T(-1) * (T)t + T(1) * w[i];
-        w[i] = wi;
-        acc[0] += (double)wi * (double)wi;
-    }
-    store_partials<1, BS>(acc, 1, partial);
-}
-
-// f(integral_constant<int, nc>) for 1 <= nc <= N
-template <int N, class F>
-int with_nc(int nc, F&& f) {
-    if constexpr (N == 0) {
-        return MPG_ERR_ARG;
-    } else {
-        if (nc == N) return f(std::integral_constant<int, N>());
-        return with_nc<N - 1>(nc, f);
-    }
-}
-
-// ---------------------------------------------------------------- step: CGS
-// coef = T(sums[0..k]); w = w - T(V coef) (gemv(-1, V, h, 1, w));
-// NEXT_DOTS: partials <v_j, w'> (j <= k) else partial ||w'||^2.
-// Each lane owns 4 consecutive rows (16-B loads of every basis column), and
-// issues the loads of 8 columns before their FMAs; the row sum t runs over
-// j = 0..k in order in fp64, as the scalar form did.
-// GIVENS (one GPU, last pass, m <= kFoldMaxM): the ||w'||^2 partials go
-// write-through and the last-arriving workgroup sums them and runs the
-// Givens step k (givens_block) — no separate Givens launch.
-template <class T, bool NEXT_DOTS, bool GIVENS = false, int BS = kBlock, bool FROM_PARTS = false>
-__global__ __launch_bounds__(BS) void k_cgs_update(int n, const T* __restrict__ V, int64_t ld, int k,
-                                                       const double* __restrict__ sums, T* __restrict__ coef_out,
-                                                       T* __restrict__ w, double* __restrict__ partial,
-                                                       unsigned* __restrict__ cnt, GivensArgs<T> g, int part_G) {
-    static_assert(!(NEXT_DOTS && GIVENS), "the Givens step follows the last pass");
-    __shared__ double coef[256];
-    const int nc = k + 1;
-    const int n4 = n & ~3;
-    const int i_first = 4 * (blockIdx.x * BS + threadIdx.x);
-    // part_G > 0: this lane's first row group (the first kPre columns and w)
-    // is loaded BEFORE the coefficient sums, so the partial loads below
-    // travel with it and their latency hides behind the basis stream
-    constexpr int kPre = 8;
-    const int npre = nc < kPre ? nc : kPre;
-    const bool pre = FROM_PARTS && i_first < n4;
-    double pv[kPre][4], pw[4];
-    if (pre) {
-#pragma unroll
-        for (int u = 0; u < kPre; ++u)
-            if (u < npre) Row4<T>::load(V + (int64_t)u * ld + i_first, pv[u]);
-        Row4<T>::load(w + i_first, pw);
-    }
-    if (FROM_PARTS) {
-        // sums straight from the panel-dots partials (nc <= kNC, part_G per
-        // column): LPC lanes per column, each summing part_G / LPC partials
-        // (all loads issued first) in g order, then an xor tree — the same
-        // fixed order in every workgroup
-        constexpr int LPC = BS / kNC;
-        const int j = threadIdx.x / LPC, sub = threadIdx.x % LPC;
-        const int per = (part_G + LPC - 1) / LPC;
-        double v = 0.0;
-        if (j < nc) {
-            const double* src = sums + (size_t)j * part_G + sub;
-#pragma unroll 8
-            for (int q = 0; q < per; ++q)
-                if (q * LPC + sub < part_G) v += src[q * LPC];
-        }
-#pragma unroll
-        for (int o = LPC / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-        if (j < nc && sub == 0) {
-            const T c = (T)v;
-            coef[j] = (double)c;
-            if (blockIdx.x == 0) coef_out[j] = c;
-        }
-    } else {
-        for (int j = threadIdx.x; j < nc; j += BS) {
-            const T c = (T)sums[j];
-            coef[j] = (double)c;
-            if (blockIdx.x == 0) coef_out[j] = c;
-        }
-    }
-    __syncthreads();
-    constexpr int NA = NEXT_DOTS ? kNC : 1;
-    double acc[NA];
-#pragma unroll
-    for (int c = 0; c < NA; ++c) acc[c] = 0.0;
-    for (int i = i_first; i < n4; i += 4 * gridDim.x * BS) {
-        double t[4] = {0.0, 0.0, 0.0, 0.0};
-        int j = 0;
-        const bool use_pre = pre && i == i_first;
-        if (use_pre) {
-#pragma unroll
-            for (int u = 0; u < kPre; ++u)
-                if (u < npre)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) t[r] += pv[u][r] * coef[u];
-            j = npre;
-        }
-        for (; j + 8 <= nc; j += 8) {
-            double v[8][4];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) Row4<T>::load(V + (int64_t)(j + u) * ld + i, v[u]);
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) t[r] += v[u][r] * coef[j + u];
-        }
-        for (; j < nc; ++j) {
-            double v[4];
-            Row4<T>::load(V + (int64_t)j * ld + i, v);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) t[r] += v[r] * coef[j];
-        }
-        double wv[4];
-        if (use_pre) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) wv[r] = pw[r];
-        } else {
-            Row4<T>::load(w + i, wv);
-        }
-        T wo[4];
-        double wd[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            wo[r] = T(-1) * (T)t[r] + T(1) * (T)wv[r];
-            wd[r] = (double)wo[r];
-        }
-        Row4<T>::store(w + i, wo);
-        if (NEXT_DOTS) {
-#pragma unroll
-            for (int c = 0; c < NA; ++c) {
-                if (c < nc) {
-                    double v[4];
-                    Row4<T>::load(V + (int64_t)c * ld + i, v);
-                    acc[c] += v[0] * wd[0] + v[1] * wd[1] + v[2] * wd[2] + v[3] * wd[3];
-                }
-            }
-        } else {
-            acc[0] += wd[0] * wd[0] + wd[1] * wd[1] + wd[2] * wd[2] + wd[3] * wd[3];
-        }
-    }
-    // tail rows (n not a multiple of 4)
-    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
-        double t = 0.0;
-        for (int j = 0; j < nc; ++j) t += (double)V[(int64_t)j * ld + i] * coef[j];
-        const T wi = T(-1) * (T)t + T(1) * w[i];
-        w[i] = wi;
-        if (NEXT_DOTS) {
-#pragma unroll
-            for (int c = 0; c < NA; ++c)
-                if (c < nc) acc[c] += (double)V[(int64_t)c * ld + i] * (double)wi;
-        } else {
-            acc[0] += (double)wi * (double)wi;
-        }
-    }
-    store_partials<NA, BS, GIVENS>(acc, NEXT_DOTS ? (nc < kNC ? nc : kNC) : 1, partial);
-    if constexpr (GIVENS) {
-        if (last_arriver(cnt)) {
-            __shared__ T col[kFoldMaxM + 2], c_s[kFoldMaxM + 2], s_s[kFoldMaxM + 2];
-            __shared__ double scratch[BS / kWave];
-            const double nrm2sq = sum_partials<BS>(partial, gridDim.x, scratch);
-            givens_block(g, nrm2sq, col, c_s, s_s);
-        }
-    }
-}
-
-// ---------------------------------------------------------------- step: MGS
-// h_jk = T(sums[0]); w -= h_jk v_j (naxpy); partial <v_{j+1}, w> or ||w||^2.
-// src_G > 0: h_jk is summed here from the src_G partials of the previous
-// launch (the dots or the previous MGS update, one GPU), in the same fixed
-// order in every workgroup — one launch per j instead of reduce + update.
-// Each lane owns 4 consecutive rows (16-B loads).
-template <class T, int BS>
-__global__ __launch_bounds__(BS) void k_mgs_update(int n, const T* __restrict__ V, int64_t ld, int j, int k,
-                                                   const double* __restrict__ src, int src_G, T* __restrict__ hjk,
-                                                   T* __restrict__ w, double* __restrict__ partial) {
-    __shared__ double scratch[BS / kWave];
-    __shared__ T h_s;
-    const T* __restrict__ vj = V + (int64_t)j * ld;
-    const T* __restrict__ vn = V + (int64_t)(j + 1) * ld;
-    const bool last = j == k;
-    const int n4 = n & ~3;
-    // this lane's first row group is loaded before h_jk is known, so its
-    // latency overlaps the partial sum's instead of following it
-    const int i_first = 4 * (blockIdx.x * BS + threadIdx.x);
-    const bool pre = i_first < n4;
-    // raw and unconditional (a clamped address when this lane has no row
-    // group): a guarded load would be widened to fp64 inside its branch,
-    // i.e. waited for right here. Column j + 1 <= m exists; unused when last.
-    // The partial (src_G <= BS: one per lane) is loaded FIRST: vmcnt retires
-    // in order, so waiting for it must not wait for the row group behind it.
-    static_assert(BS >= kCombineGroups * 4, "one partial per lane");
-    double part = src[threadIdx.x < src_G ? threadIdx.x : 0];
-    if (threadIdx.x >= src_G) part = 0.0;
-    __builtin_amdgcn_sched_barrier(0);
-    const int ip = pre ? i_first : 0;
-    Raw4<T> pw, pv, pn;
-    pw.load(w + ip);
-    pv.load(vj + ip);
-    pn.load(vn + ip);
-    __builtin_amdgcn_sched_barrier(0);
-    // LDS-only barriers: the first row group's loads stay in flight. The
-    // block sum runs unconditionally so the partial load is not sunk below
-    // the row group's loads.
-    {
-        const double v = wave_sum(part + 0.0);  // = sum_partials' order for src_G <= BS
-        if ((threadIdx.x & (kWave - 1)) == 0) scratch[threadIdx.x / kWave] = v;
-        lds_barrier();
-        if (threadIdx.x == 0) {
-            double r = 0.0;
-#pragma unroll
-            for (int q = 0; q < BS / kWave; ++q) r += scratch[q];
-            h_s = src_G > 0 ? (T)r : (T)src[0];
-        }
-    }
-    lds_barrier();
-    const T h = h_s;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *hjk = h;
-    double acc[1] = {0.0};
-    for (int i = i_first; i < n4; i += 4 * gridDim.x * BS) {
-        double wv[4], vv[4], nv[4] = {0.0, 0.0, 0.0, 0.0};
-        if (i == i_first) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                wv[r] = pw[r];
-                vv[r] = pv[r];
-                nv[r] = last ? 0.0 : pn[r];
-            }
-        } else {
-            Row4<T>::load(w + i, wv);
-            Row4<T>::load(vj + i, vv);
-            if (!last) Row4<T>::load(vn + i, nv);
-        }
-        T wo[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            T wi = (T)wv[r];
-            wi -= h * (T)vv[r];
-            wo[r] = wi;
-            acc[0] += last ? (double)wi * (double)wi : nv[r] * (double)wi;
-        }
-        Row4<T>::store(w + i, wo);
-    }
-    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
-        T wi = w[i];
-        wi -= h * vj[i];
-        w[i] = wi;
-        acc[0] += last ? (double)wi * (double)wi : (double)vn[i] * (double)wi;
-    }
-    store_partials<1, BS>(acc, 1, partial);
-}
-
-#pragma clang fp contract(off)
-// upper-triangular solve y = H(0:k,0:k)^-1 s(0:k), in place on s (one lane per
-// row of the axpy sweep; k <= m is small)
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_trsv_upper(int k, int ldh, const T* __restrict__ H, T* __restrict__ y) {
-    __shared__ T ys[1024];
-    __shared__ T temp_s;
-    for (int i = threadIdx.x; i < k; i += kBlock) ys[i] = y[i];
-    __syncthreads();
-    for (int j = k - 1; j >= 0; --j) {
-        if (threadIdx.x == 0) {
-            T yj = ys[j];
-            if (yj != T(0)) yj = yj / H[(int64_t)j * ldh + j];
-            ys[j] = yj;
-            temp_s = yj;
-        }
-        __syncthreads();
-        const T t = temp_s;
-        if (t != T(0))
-            for (int i = threadIdx.x; i < j; i += kBlock) ys[i] = ys[i] - t * H[(int64_t)j * ldh + i];
-        __syncthreads();
-    }
-    for (int i = threadIdx.x; i < k; i += kBlock) y[i] = ys[i];
-}
-// The same solve for 64 < k <= 64 * KW by one wave64 (GMRES(100): the
-// one-lane-per-step form above took 92.6 us at k = 100, one workgroup barrier
-// pair per column). The upper triangle of H(0:k,0:k) is staged in LDS packed
-// by columns (column j at j(j+1)/2, dynamic shared memory) with one load
-// round; lane l holds y_{l + 64q} in register slot q. The column sweep is
-// the netlib order of k_trsv_upper (no contraction): y_j /= H(j,j) (when
-// y_j != 0), broadcast by a shuffle, then y_i -= y_j H(i,j) for i < j.
-// (kBlock threads stage H, 8 independent loads per lane per round; wave 0 solves)
-template <class T, int KW>
-__global__ __launch_bounds__(kBlock) void k_trsv_upper_lds(int k, int ldh, const T* __restrict__ H,
-                                                           T* __restrict__ y) {
-    extern __shared__ char trsv_smem[];
-    T* Hp = reinterpret_cast<T*>(trsv_smem);
-    const int lane = threadIdx.x;
-    const int P = k * (k + 1) / 2;
-    constexpr int U = 8;
-    for (int base = 0; base < P; base += kBlock * U) {
-        T v[U];
-        int e[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            e[u] = base + kBlock * u + (int)threadIdx.x;
-            const int ec = e[u] < P ? e[u] : P - 1;
-            // column j of packed entry ec: j(j+1)/2 <= ec < (j+1)(j+2)/2
-            int j = (int)((sqrtf(8.0f * (float)ec + 1.0f) - 1.0f) * 0.5f);
-            while (j * (j + 1) / 2 > ec) --j;
-            while ((j + 1) * (j + 2) / 2 <= ec) ++j;
-            v[u] = H[(int64_t)j * ldh + (ec - j * (j + 1) / 2)];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (e[u] < P) Hp[e[u]] = v[u];
-    }
-    __syncthreads();
-    if (threadIdx.x >= kWave) return;
-    T yr[KW];
-#pragma unroll
-    for (int q = 0; q < KW; ++q) yr[q] = lane + kWave * q < k ? y[lane + kWave * q] : T(0);
-    for (int j = k - 1; j >= 0; --j) {
-        const int jq = j / kWave, jl = j % kWave;
-        T mine = yr[0];
-#pragma unroll
-        for (int q = 1; q < KW; ++q)
-            if (q == jq) mine = yr[q];
-        T yj = __shfl(mine, jl, kWave);
-        if (yj != T(0)) yj = yj / Hp[j * (j + 1) / 2 + j];
-#pragma unroll
-        for (int q = 0; q < KW; ++q) {
-            const int i = lane + kWave * q;
-            if (q == jq && lane == jl) yr[q] = yj;
-            if (yj != T(0) && i < j) yr[q] = yr[q] - yj * Hp[j * (j + 1) / 2 + i];
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < KW; ++q)
-        if (lane + kWave * q < k) y[lane + kWave * q] = yr[q];
-}
-
-// The same upper solve by one wave64 (k <= 64): lane i holds y_i, the
-// column sweep's scalar is broadcast with a shuffle, H(0:k,0:k) is in LDS
-// (column j at Hs[j * 64]). No barrier inside the sweep.
-template <class T>
-__device__ __forceinline__ T trsv_upper_wave(int k, const T* Hs, T y, int lane) {
-    for (int j = k - 1; j >= 0; --j) {
-        T yj = __shfl(y, j, kWave);
-        if (yj != T(0)) yj = yj / Hs[j * kWave + j];
-        if (lane == j) y = yj;
-        if (yj != T(0) && lane < j) y = y - yj * Hs[j * kWave + lane];
-    }
-    return y;
-}
-#pragma clang fp contract(on)
-
-// x += X(T(V y)): mixed form gemv(1, V, y, 0, tmp); copy; axpy(1, tmp, x)
-// (same-precision form gemv(1, V, y, 1, x) gives the same fl(t + x))
-// SOLVE (k <= 64): y = H(0:k,0:k)^-1 s(0:k) is formed first by every
-// workgroup (trsv_upper_wave) — one launch per restart instead of two. s is
-// not overwritten (the next prologue resets it).
-template <class T, class X, bool SOLVE>
-__global__ __launch_bounds__(kBlock) void k_update_x(int n, const T* __restrict__ V, int64_t ld, int k,
-                                                     const T* __restrict__ y, const T* __restrict__ H, int ldh,
-                                                     X* __restrict__ x) {
-    __shared__ T ys[SOLVE ? kWave : 1024];
-    if constexpr (SOLVE) {
-        __shared__ T Hs[kWave * kWave];
-        for (int e = threadIdx.x; e < k * kWave; e += kBlock) {
-            const int j = e / kWave, i = e % kWave;
-            Hs[e] = i <= j ? H[(int64_t)j * ldh + i] : T(0);
-        }
-        __syncthreads();
-        if (threadIdx.x < kWave) {
-            const int lane = threadIdx.x;
-            T yv = lane < k ? y[lane] : T(0);
-            yv = trsv_upper_wave(k, Hs, yv, lane);
-            ys[lane] = yv;  // (s itself is left as is: every workgroup reads it)
-        }
-    } else {
-        for (int j = threadIdx.x; j < k; j += kBlock) ys[j] = y[j];
-    }
-    __syncthreads();
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        double t = 0.0;
-        for (int j = 0; j < k; ++j) t += (double)V[(int64_t)j * ld + i] * (double)ys[j];
-        x[i] = x[i] + (X)(T)t;
-    }
-}
-
-// k_update_x<T, X, true> with the column count NC = k <= kNC a compile-time
-// constant: each lane owns 4 rows and loads the basis in batches (the
-// runtime-k form waited for every few columns in turn). Same arithmetic:
-// t = sum_j V_ij y_j in fp64 in j order, x_i = x_i + X(T(t)).
-template <class T, class X, int NC>
-__global__ __launch_bounds__(kCombineBlock) void k_update_x_nc(int n, const T* __restrict__ V, int64_t ld,
-                                                                const T* __restrict__ y, const T* __restrict__ H,
-                                                                int ldh, X* __restrict__ x) {
-    static_assert(NC >= 1 && NC <= kNC, "one panel");
-    constexpr int BS = kCombineBlock, B = kColBatch<T>;
-    __shared__ T Hs[NC * kWave];
-    __shared__ double ys[NC];
-    for (int e = threadIdx.x; e < NC * kWave; e += BS) {
-        const int j = e / kWave, i = e % kWave;
-        Hs[e] = i <= j && i < NC ? H[(int64_t)j * ldh + i] : T(0);
-    }
-    __syncthreads();
-    if (threadIdx.x < kWave) {
-        const int lane = threadIdx.x;
-        T yv = lane < NC ? y[lane] : T(0);
-        yv = trsv_upper_wave(NC, Hs, yv, lane);
-        if (lane < NC) ys[lane] = (double)yv;
-    }
-    __syncthreads();
-    const int n4 = n & ~3;
-    for (int i = 4 * (blockIdx.x * BS + threadIdx.x); i < n4; i += 4 * gridDim.x * BS) {
-        Raw4<X> xr;
-        xr.load(x + i);
-        double t[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int c0 = 0; c0 < NC; c0 += B) {
-            Raw4<T> v[B];
-#pragma unroll
-            for (int u = 0; u < B; ++u)
-                if (c0 + u < NC) v[u].load(V + (int64_t)(c0 + u) * ld + i);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < B; ++u)
-                if (c0 + u < NC) {
-                    const double yu = ys[c0 + u];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) t[r] += v[u][r] * yu;
-                }
-        }
-        X xo[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) xo[r] = (X)xr[r] + (X)(T)t[r];
-        Row4<X>::store(x + i, xo);
-    }
-    for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
-        double t = 0.0;
-#pragma unroll
-        for (int j = 0; j < NC; ++j) t += (double)V[(int64_t)j * ld + i] * ys[j];
-        x[i] = x[i] + (X)(T)t;
-    }
-}
-
-}  // namespace
-
-// ---------------------------------------------------------------- plan object
-struct mpg_arnoldi {
-    mpg_ctx* ctx = nullptr;
-    mpg_arnoldi_desc d{};
-    int combo = 0;    // type combination (see dispatch below)
-    int G = 1;        // workgroups of the row-parallel panel kernels
-    int Grb = 1;      // workgroups of the row-block (SpMV) kernels: one per row block
-    int last_G = 1;   // partial count per column written by the last producer
-    double* last_part = nullptr;  // ... and the buffer it wrote (partial or dpart)
-    int64_t ld = 0;   // leading dimension of V (elements)
-    size_t tsize = 8;
-    void* V = nullptr;
-    void* H = nullptr;      // (m+1) x m
-    void* small = nullptr;  // cs, sn, s (m+1 each), inv, corr (m+1), coef scratch
-    void* w[2] = {nullptr, nullptr};      // row 0 of each w buffer
-    void* wbase[2] = {nullptr, nullptr};  // the allocations: `front` entries before row 0
-    int front = 0;                        // MPG_FRONT_PAD(d.n_front)
-    double* partial = nullptr;  // (kNC + 4) x G
-    double* dpart = nullptr;    // kNC x Gd: one-panel dots partials (read by the CGS update that writes `partial`)
-    double* sums = nullptr;     // m + 4
-    double* report = nullptr;   // 4 + m
-    unsigned* counters = nullptr;  // last-arriver tickets: [0] dots, [32] CGS + Givens (zeroed at create)
-    int Gd = 1;                    // workgroups (kCombineBlock threads) of the combining panel dots
-    SellCopy sell;  // sliced-ELL copy of the Arnoldi matrix (nslices == 0: CSR row blocks)
-    SellCopy sell_outer;        // ... of the outer-precision values, for the residual prologue
-    NodeCopy node;              // node-block copy of the Arnoldi matrix (nblk > 0: the Arnoldi SpMV uses it)
-    bool outer_is_inner = false;  // the prologue runs on `sell` (baseline / single modes)
-    // SELL SpMV with the panel dots fused (SellDots): per-workgroup partials,
-    // group tickets, group size and count
-    double* fd_part = nullptr;
-    unsigned* fd_cnt = nullptr;
-    int fd_gs = 0, fd_ng = 0;
-
-    char* small_at(int slot) const { return static_cast<char*>(small) + (size_t)slot * (d.m + 1) * tsize; }
-    void* cs() const { return small_at(0); }
-    void* sn() const { return small_at(1); }
-    void* s() const { return small_at(2); }
-    void* corr() const { return small_at(3); }
-    void* inv() const { return small_at(4); }
-};
-
-namespace {
-
-// combos: 0 baseline <d,d,d,d>; 1 single-prec <d,d,f,d>; 2 single <f,f,f,f>;
-//         3 mixed <f,d,f,f>; 4 mixed-half <f,d,f,h>
-int combo_of(const mpg_arnoldi_desc& d) {
-    if (d.vec_type == MPG_F64 && d.outer_type == MPG_F64 && d.inner_val == MPG_F64)
-        return d.prec_type == MPG_F64 ? 0 : (d.prec_type == MPG_F32 ? 1 : -1);
-    if (d.vec_type == MPG_F32 && d.prec_type == MPG_F32) {
-        if (d.outer_type == MPG_F32 && d.inner_val == MPG_F32) return 2;
-        if (d.outer_type == MPG_F64 && d.inner_val == MPG_F32) return 3;
-        if (d.outer_type == MPG_F64 && d.inner_val == MPG_F16) return 4;
-    }
-    return -1;
-}
-
-template <class F>
-int dispatch(int combo, F&& f) {
-    switch (combo) {
-        case 0: return f(double(), double(), double(), double());
-        case 1: return f(double(), double(), float(), double());
-        case 2: return f(float(), float(), float(), float());
-        case 3: return f(float(), double(), float(), float());
-        case 4: return f(float(), double(), float(), half_v());
-        default: return MPG_ERR_UNSUPPORTED;
-    }
-}
-
-// MPG_CSR_MODE (the Arnoldi CSR SpMV, k_step_spmv<..., MODE>): bit 0
-// non-temporal matrix streams, bit 1 XCD-ordered row blocks
-int csr_mode() {
-    const char* e = std::getenv("MPG_CSR_MODE");
-    return e && *e >= '0' && *e <= '4' ? *e - '0' : 0;
-}
-
-// Tiles per workgroup of the node-block SpMV (MPG_NODE_TPW: 1 one tile
-// each, N > 1 a pipelined walk of N tiles; default 2; 0: as many as keep
-// the grid at kNodeGroups workgroups, so the Givens step folds in).
-// Measured (profiles/r05_node_ab.jsonl): fem27 248 / 218 / 215-228 / 223-238
-// / 255 us at 1 / 2 / 4 / 8 / 16 (auto, folded: 247), C4's stencil 341 /
-// 295-312 / 300 / 306-334 / 345 (auto 355): longer walks leave the grid's
-// tail to fewer workgroups, two tiles in flight is the gain.
-constexpr int kNodeGroups = 2048;
-int node_tpw(const NodeCopy& S) {
-    const int v = node_tpw_default();
-    if (v >= 1) return v;
-    return std::max(2, (S.ntiles + kNodeGroups - 1) / kNodeGroups);
-}
-
-int row_grid(const mpg_arnoldi* a) { return a->G; }
-int rb_grid(const mpg_arnoldi* a) { return a->Grb; }
-
-template <class T>
-GivensArgs<T> givens_args(const mpg_arnoldi* a, int k) {
-    return GivensArgs<T>{k,
-                         a->d.m,
-                         a->d.orth == kOrthCGSR ? static_cast<const T*>(a->corr()) : nullptr,
-                         static_cast<T*>(a->H),
-                         static_cast<T*>(a->cs()),
-                         static_cast<T*>(a->sn()),
-                         static_cast<T*>(a->s()),
-                         static_cast<T*>(a->inv()),
-                         a->report};
-}
 
 int64_t sell_copy_bytes(const mpg_arnoldi* a);
 
@@ -1868,6 +59,26 @@ int arnoldi_sell_build(mpg_arnoldi* a, int format) {
         return MPG_ERR_ALLOC;
     if (a->outer_is_inner) return MPG_OK;
     return sell_build(a->ctx, a->d.A, a->d.outer_type, a->d.val_outer, 2, a->sell_outer);
+}
+
+
+// fp64 accumulation here; fp32 accumulation (mpg_arnoldi_set_accum, fp32
+// Arnoldi only) in arnoldi_acc32.hip
+int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
+    return a && a->acc32 ? mpg_acc32::spmv(a, k, fold, dots) : spmv_run<double>(a, k, fold, dots);
+}
+int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
+    return a && a->acc32 ? mpg_acc32::dots(a, k, combine) : dots_run<double>(a, k, combine);
+}
+int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_partials = false, bool no_next = false) {
+    return a && a->acc32 ? mpg_acc32::cgs(a, k, pass, givens, from_partials, no_next)
+                         : cgs_run<double>(a, k, pass, givens, from_partials, no_next);
+}
+int mgs_impl(mpg_arnoldi_t a, int k, int j, bool from_partials) {
+    return a && a->acc32 ? mpg_acc32::mgs(a, k, j, from_partials) : mgs_run<double>(a, k, j, from_partials);
+}
+int givens_impl(mpg_arnoldi_t a, int k, bool from_partials) {
+    return a && a->acc32 ? mpg_acc32::givens(a, k, from_partials) : givens_run<double>(a, k, from_partials);
 }
 
 }  // namespace
@@ -2084,164 +295,7 @@ int mpg_arnoldi_prologue_finish_partials(mpg_arnoldi_t a) {
 }
 
 int mpg_arnoldi_reduce(mpg_arnoldi_t a, int ncols) {
-    if (!a || ncols < 1 || ncols > a->d.m + 4) return MPG_ERR_ARG;
-    // one column per workgroup: 256 threads when the producer left <= 512
-    // partials per column (one or two loads per thread), else 1024
-    if (a->last_G <= 2 * kBlock) k_reduce_partials<kBlock><<<ncols, kBlock, 0, a->ctx->stream>>>(a->last_G, a->last_part, a->sums);
-    else k_reduce_partials<1024><<<ncols, 1024, 0, a->ctx->stream>>>(a->last_G, a->last_part, a->sums);
-    MPG_LAUNCH_CHECK(a->ctx);
-    return MPG_OK;
-}
-
-// fold: 0 plain; 1 Givens(k-1) folded, ||w||^2 from sums[0]; 2 from the partials.
-// dots: the panel dots fused (SellDots; MPG_ERR_UNSUPPORTED where the SELL
-// copy, an fp32 basis with fp32 values, int16 columns and the window are
-// not all present -- the caller then launches the dots itself).
-// workgroup of the SELL step kernel without fused dots (4 slices per 256)
-#ifndef MPG_STEP_SELL_BLOCK
-#define MPG_STEP_SELL_BLOCK 256
-#endif
-constexpr int kStepSellBlock = MPG_STEP_SELL_BLOCK;
-using kBlockC = std::integral_constant<int, kBlock>;
-
-static int spmv_impl(mpg_arnoldi_t a, int k, int fold, bool dots = false) {
-    if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
-    if (dots && (a->d.n <= 0 || a->sell.nslices == 0 || !a->sell.c16 || !a->sell.win || (a->combo != 2 && a->combo != 3) ||
-                 k + 1 > kNC || a->d.orth == kOrthMGS))
-        return MPG_ERR_UNSUPPORTED;
-    if (fold && (k < 1 || a->d.m > kFoldMaxM)) return MPG_ERR_ARG;
-    const mpg_csr* A = a->d.A;
-    int st = dispatch(a->combo, [&](auto t, auto, auto p, auto vi) {
-        using T = decltype(t);
-        using P = decltype(p);
-        using VI = decltype(vi);
-        const P* diag = a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr;
-        GivensFold<T> gf{nullptr, 0, {}};
-        if (fold)
-            gf = GivensFold<T>{fold == 2 ? a->last_part : a->sums, fold == 2 ? a->last_G : 0, givens_args<T>(a, k - 1)};
-        if (a->sell.nslices > 0) {
-            const auto& S = a->sell;
-            if (fold == 2 && a->last_G > kBlock) return (int)MPG_ERR_ARG;  // k_step_sell folds <= kBlock partials
-            return sell_dispatch(S, [&](auto ci, auto wc) {
-                using CI = decltype(ci);
-                constexpr int Wc = decltype(wc)::value;
-                auto launch = [&](auto kern, SellDots dd, auto bs) {
-                    constexpr int BS = decltype(bs)::value;
-                    const int grid = (S.nslices + BS / kWave - 1) / (BS / kWave);
-                    launch_timed(a->ctx, kern, dim3(grid), dim3(BS),
-                            a->d.n, -a->front, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
-                            static_cast<const typename SellStore<VI>::type*>(S.val),
-                            static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
-                            static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, dd,
-                            S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
-                            static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
-                            S.ustride, sell_xcd_order(S) ? 1 : 0, S.rows);
-                    return (int)MPG_OK;
-                };
-                if constexpr (std::is_same_v<T, float> && std::is_same_v<VI, float> &&
-                              std::is_same_v<CI, int16_t>) {
-                    if (dots) {
-                        const SellDots dd{k + 1, a->fd_gs, a->fd_ng, a->fd_part, a->fd_cnt, a->dpart};
-                        auto pick = [&](auto dn) {
-                            constexpr int DN = decltype(dn)::value;
-                            return fold ? launch(k_step_sell<T, P, VI, CI, Wc, true, true, DN>, dd, kBlockC())
-                                        : launch(k_step_sell<T, P, VI, CI, Wc, true, false, DN>, dd, kBlockC());
-                        };
-                        if (k + 1 <= 8) return pick(std::integral_constant<int, 8>());
-                        if (k + 1 <= 16) return pick(std::integral_constant<int, 16>());
-                        return pick(std::integral_constant<int, 32>());
-                    }
-                }
-                return sell_dispatch_win(S.win, [&](auto wn) {
-                    constexpr bool WN = decltype(wn)::value;
-                    using BSC = std::integral_constant<int, kStepSellBlock>;
-                    const int be = sell_uniform(S) ? sell_pair(S) : 0;
-                    if constexpr (std::is_same_v<CI, int16_t> && (Wc == 2 || Wc == 4)) if (be) {
-                        auto launch2 = [&](auto kern) {
-                            const int grid = (S.nslices + 2 * (kStepSellBlock / kWave) - 1) / (2 * (kStepSellBlock / kWave));
-                            launch_timed(a->ctx, kern, dim3(grid), dim3(kStepSellBlock),
-                                    a->d.n, -a->front, a->d.n_ext, S.nslices, S.off, static_cast<const CI*>(S.col),
-                                    static_cast<const typename SellStore<VI>::type*>(S.val),
-                                    static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()),
-                                    static_cast<T*>(a->V), a->ld, k, diag, static_cast<T*>(a->w[(k + 1) & 1]), gf,
-                                    SellDots{}, S.sbase, S.spat, S.coff, static_cast<const CI*>(S.pat), S.xrp, S.xcol,
-                                    static_cast<const typename SellStore<VI>::type*>(S.xval), a->d.inner_row_exp,
-                                    S.ustride, sell_xcd_order(S) ? 1 : 0);
-                            return (int)MPG_OK;
-                        };
-                        const char* pge = std::getenv("MPG_SELL_PREGATHER");
-                        if (!WN && pge && *pge == '0') {
-                            if (be == 8)
-                                return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 8, kStepSellBlock, false>)
-                                            : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 8, kStepSellBlock, false>);
-                            return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 12, kStepSellBlock, false>)
-                                        : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 12, kStepSellBlock, false>);
-                        }
-                        if (be == 8)
-                            return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 8, kStepSellBlock>)
-                                        : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 8, kStepSellBlock>);
-                        if constexpr (Wc == 2) if (be == 10)
-                            return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 10, kStepSellBlock>)
-                                        : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 10, kStepSellBlock>);
-                        if (be != 12) return (int)MPG_ERR_UNSUPPORTED;
-                        return fold ? launch2(k_step_sell2<T, P, VI, Wc, WN, true, 12, kStepSellBlock>)
-                                    : launch2(k_step_sell2<T, P, VI, Wc, WN, false, 12, kStepSellBlock>);
-                    }
-                    if constexpr (!WN && !std::is_same_v<CI, int16_t>) if (sell_pipe(S)) {
-                        if (sell_uniform(S))
-                            return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock, true, true>,
-                                                 SellDots{}, BSC())
-                                        : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock, true, true>,
-                                                 SellDots{}, BSC());
-                        return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock, false, true>,
-                                             SellDots{}, BSC())
-                                    : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock, false, true>,
-                                             SellDots{}, BSC());
-                    }
-                    if (sell_uniform(S))
-                        return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock, true>,
-                                             SellDots{}, BSC())
-                                    : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock, true>,
-                                             SellDots{}, BSC());
-                    return fold ? launch(k_step_sell<T, P, VI, CI, Wc, WN, true, 0, kStepSellBlock>, SellDots{}, BSC())
-                                : launch(k_step_sell<T, P, VI, CI, Wc, WN, false, 0, kStepSellBlock>, SellDots{}, BSC());
-                });
-            });
-        }
-        if (a->node.nblk > 0) {
-            const NodeCopy& S = a->node;
-            const int tpw = node_tpw(S);
-            auto go = [&](auto kern) {
-                launch_timed(a->ctx, kern, dim3((S.ntiles + tpw - 1) / tpw), dim3(kBlock),
-                             static_cast<const int32_t*>(S.tiles), static_cast<const int32_t*>(S.bptr),
-                             static_cast<const char*>(S.recs), static_cast<const T*>(a->w[k & 1]),
-                             static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k, diag,
-                             static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp, S.ntiles, S.nblk, tpw,
-                             node_xcd(S));
-                return (int)MPG_OK;
-            };
-            if (tpw > 1) return fold ? go(k_step_node<T, P, VI, true>) : go(k_step_node<T, P, VI, false>);
-            return fold ? go(k_step_node<T, P, VI, true, false>) : go(k_step_node<T, P, VI, false, false>);
-        }
-        const int mode = csr_mode();
-        auto kern = mode == 1   ? (fold ? k_step_spmv<T, P, VI, true, 1> : k_step_spmv<T, P, VI, false, 1>)
-                    : mode == 2 ? (fold ? k_step_spmv<T, P, VI, true, 2> : k_step_spmv<T, P, VI, false, 2>)
-                    : mode == 3 ? (fold ? k_step_spmv<T, P, VI, true, 3> : k_step_spmv<T, P, VI, false, 3>)
-                    : mode == 4 ? (fold ? k_step_spmv<T, P, VI, true, 4> : k_step_spmv<T, P, VI, false, 4>)
-                                : (fold ? k_step_spmv<T, P, VI, true> : k_step_spmv<T, P, VI, false>);
-        launch_timed(a->ctx, kern, dim3(rb_grid(a)), dim3(kBlock),
-            A->blocks, A->nblocks, A->rowptr, A->col, static_cast<const VI*>(a->d.val_inner), A->nnz,
-            static_cast<const T*>(a->w[k & 1]), static_cast<const T*>(a->inv()), static_cast<T*>(a->V), a->ld, k,
-            diag, static_cast<T*>(a->w[(k + 1) & 1]), gf, a->d.inner_row_exp);
-        return (int)MPG_OK;
-    });
-    if (st) return st;
-    if (dots) {
-        a->last_G = a->fd_ng;
-        a->last_part = a->dpart;
-    }
-    MPG_LAUNCH_CHECK(a->ctx);
-    return MPG_OK;
+    return a && a->acc32 ? mpg_acc32::reduce(a, ncols) : reduce_run<double>(a, ncols);
 }
 
 int mpg_arnoldi_spmv(mpg_arnoldi_t a, int k) { return spmv_impl(a, k, 0); }
@@ -2277,261 +331,32 @@ int mpg_arnoldi_fold_pays(mpg_arnoldi_t a) {
     return (S.nslices + per_group - 1) / per_group <= limit ? 1 : 0;
 }
 
-// row groups per panel of k_dots_panels: about one workgroup per CU in all
-// (the same on every rank: uniform groups set Gd = kCombineGroups), so each
-// column has <= kCombineGroups / 2 partials for k_cgs_update_wide
-static int wide_groups(const mpg_arnoldi* a, int ncols) {
-    const int np = (ncols + kNC - 1) / kNC;
-    return std::max(1, std::min(a->Gd, kCombineGroups / np));
-}
-
-// measurement: the armed stamp slots (mpg_arnoldi_stamp_next) for this launch when they hold all of its waves;
-// disarmed either way
-static unsigned long long* take_stamp(mpg_arnoldi* a, int64_t waves) {
-    unsigned long long* p = a->ctx->stamp_next;
-    a->ctx->stamp_next = nullptr;
-    return p && waves <= a->ctx->stamp_cap ? p : nullptr;
-}
-
-static int dots_impl(mpg_arnoldi_t a, int k, bool combine) {
-    if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
-    const int ndots_all = a->d.orth == kOrthMGS ? 1 : k + 1;
-    if (combine && ndots_all > kNC) return MPG_ERR_ARG;
-    // an armed stamp belongs to this launch whatever its form (disarmed
-    // here); only the one-panel k_dots_nc stores stamps
-    unsigned long long* sp = take_stamp(a, (int64_t)a->Gd * (kCombineBlock / kWave));
-    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
-        using T = decltype(t);
-        if (combine) {
-            k_panel_dots<T, kCombineBlock, true><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, 0, ndots_all, static_cast<const T*>(a->w[(k + 1) & 1]),
-                a->partial, a->counters, a->sums);
-            return (int)MPG_OK;
-        }
-        if (ndots_all <= kNC) {  // one panel: 1024-thread workgroups, one per CU -> Gd partials per column
-            return with_nc<kNC>(ndots_all, [&](auto nc) {
-                constexpr int NC = decltype(nc)::value;
-                const T* Vp = static_cast<const T*>(a->V);
-                const T* wp = static_cast<const T*>(a->w[(k + 1) & 1]);
-                if (sp)
-                    k_dots_nc<T, kCombineBlock, NC, true>
-                        <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, Vp, a->ld, wp, a->dpart, sp);
-                else
-                    k_dots_nc<T, kCombineBlock, NC>
-                        <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, Vp, a->ld, wp, a->dpart, nullptr);
-                return (int)MPG_OK;
-            });
-        }
-        if (ndots_all <= kWideMax) {  // every panel in one launch -> wide_groups(a, k) partials per column
-            const int np = (ndots_all + kNC - 1) / kNC;
-            return with_nc<kNC>(ndots_all - (np - 1) * kNC, [&](auto ncl) {
-                k_dots_panels<T, kCombineBlock, decltype(ncl)::value>
-                    <<<dim3(wide_groups(a, ndots_all), np), kCombineBlock, 0, a->ctx->stream>>>(
-                        a->d.n, static_cast<const T*>(a->V), a->ld, static_cast<const T*>(a->w[(k + 1) & 1]),
-                        a->dpart);
-                return (int)MPG_OK;
-            });
-        }
-        for (int c0 = 0; c0 < ndots_all; c0 += kNC) {
-            const int nc = ndots_all - c0 < kNC ? ndots_all - c0 : kNC;
-            k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, c0, nc, static_cast<const T*>(a->w[(k + 1) & 1]),
-                a->partial, nullptr, nullptr);
-        }
-        return (int)MPG_OK;
-    });
-    const bool wide = !combine && ndots_all > kNC && ndots_all <= kWideMax;
-    a->last_G = combine || ndots_all <= kNC ? a->Gd : wide ? wide_groups(a, ndots_all) : row_grid(a);
-    a->last_part = !combine && ndots_all <= kWideMax ? a->dpart : a->partial;
-    if (st) return st;
-    MPG_LAUNCH_CHECK(a->ctx);
-    return MPG_OK;
-}
-
 int mpg_arnoldi_dots(mpg_arnoldi_t a, int k) { return dots_impl(a, k, false); }
 int mpg_arnoldi_dots_sums(mpg_arnoldi_t a, int k) { return dots_impl(a, k, true); }
-
-// MPG_CGS_PREFETCH=1: the in-launch-sum CGS update issues its first row
-// group under the coefficient sums (k_cgs_update_nc<..., PF>)
-static bool cgs_prefetch() {
-    const char* e = std::getenv("MPG_CGS_PREFETCH");
-    return e && *e == '1';
-}
-
-// no_next (CGSR at 32 < k + 1 <= kWideMax, one GPU): a pass that takes its
-// coefficients from the preceding one-launch panel dots and emits no next
-// dots (the caller launches k_dots_panels on the updated w instead)
-static int cgs_impl(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_partials = false, bool no_next = false) {
-    if (!a || k < 0 || k >= a->d.m || pass < 0 || pass > 1 || k + 1 > 256) return MPG_ERR_ARG;
-    const bool cgsr = a->d.orth == kOrthCGSR;
-    const bool next_dots = cgsr && pass == 0 && !no_next;
-    if (givens && (next_dots || a->d.m > kFoldMaxM || from_partials)) return MPG_ERR_ARG;
-    if (no_next && (!cgsr || !from_partials || k + 1 <= kNC)) return MPG_ERR_ARG;
-    // from_partials: the coefficients are summed from the preceding one-panel
-    // dots' partials inside this launch (no reduce launch)
-    if (from_partials && ((pass != 0 && !no_next) || k + 1 > kWideMax || a->last_part != a->dpart)) return MPG_ERR_ARG;
-    if (from_partials && k + 1 > kNC && (next_dots || a->last_G > kWideMax)) return MPG_ERR_ARG;
-    const double* src = from_partials ? a->dpart : a->sums;
-    const int part_G = from_partials ? a->last_G : 0;  // Gd (k_dots_nc) or fd_ng (k_step_sell's dots)
-    if (part_G > kCombineGroups) return MPG_ERR_ARG;
-    // an armed stamp belongs to this launch whatever its form (disarmed here);
-    // only the one-panel product form below stores stamps
-    unsigned long long* sp = take_stamp(a, (int64_t)a->Gd * (kCombineBlock / kWave));
-    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
-        using T = decltype(t);
-        T* coef_out = pass == 0 ? static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) : static_cast<T*>(a->corr());
-        T* w = static_cast<T*>(a->w[(k + 1) & 1]);
-        const GivensArgs<T> g = givens_args<T>(a, k);
-        if (next_dots && k + 1 <= kNC && !from_partials) {
-            // 256-thread workgroups (the NC fp64 dot accumulators need more
-            // than the 128 VGPRs of a 1024-thread one) -> row_grid partials
-            return with_nc<kNC>(k + 1, [&](auto nc) {
-                k_cgs_update_nc<T, kBlock, decltype(nc)::value, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                    a->d.n, static_cast<const T*>(a->V), a->ld, src, 0, coef_out, w, a->partial, nullptr);
-                return (int)MPG_OK;
-            });
-        } else if (next_dots) {
-            if (from_partials)
-                k_cgs_update<T, true, false, kBlock, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                    a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, part_G);
-            else
-                k_cgs_update<T, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                    a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, 0);
-            for (int c0 = kNC; c0 < k + 1; c0 += kNC) {
-                const int nc = k + 1 - c0 < kNC ? k + 1 - c0 : kNC;
-                k_panel_dots<T><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                    a->d.n, static_cast<const T*>(a->V), a->ld, c0, nc, w, a->partial, nullptr, nullptr);
-            }
-        } else if (givens) {
-            k_cgs_update<T, false, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, a->counters + 32, g, 0);
-        } else if (from_partials && k + 1 > kNC) {  // GMRES(100): sums from k_dots_panels' partials
-            k_cgs_update_wide<T, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k + 1, src, part_G, coef_out, w, a->partial);
-        } else if (k + 1 <= kNC) {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
-            // the wave stamps of the product form only (in-launch sums, no
-            // prefetch): the one bench.py's phases time
-            if (!from_partials || cgs_prefetch()) sp = nullptr;
-            return with_nc<kNC>(k + 1, [&](auto nc) {
-                constexpr int NC = decltype(nc)::value;
-                const T* Vp = static_cast<const T*>(a->V);
-                // (the prefetch variant for one batch of columns only: wider
-                // panels spill with the prefetched batch held across the sums)
-                if constexpr (NC <= kColBatch<T>) {
-                    if (from_partials && cgs_prefetch()) {
-                        k_cgs_update_nc<T, kCombineBlock, NC, true, false, true>
-                            <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, Vp, a->ld, src, part_G, coef_out,
-                                                                           w, a->partial, nullptr);
-                        return (int)MPG_OK;
-                    }
-                }
-                if (from_partials && sp)
-                    k_cgs_update_nc<T, kCombineBlock, NC, true, false, false, true>
-                        <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, Vp, a->ld, src, part_G, coef_out, w,
-                                                                       a->partial, sp);
-                else if (from_partials)
-                    k_cgs_update_nc<T, kCombineBlock, NC, true><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                        a->d.n, Vp, a->ld, src, part_G, coef_out, w, a->partial, nullptr);
-                else
-                    k_cgs_update_nc<T, kCombineBlock, NC, false><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                        a->d.n, Vp, a->ld, src, 0, coef_out, w, a->partial, nullptr);
-                return (int)MPG_OK;
-            });
-        } else {
-            k_cgs_update<T, false, false, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, src, coef_out, w, a->partial, nullptr, g, 0);
-        }
-        return (int)MPG_OK;
-    });
-    a->last_G = next_dots || givens ? row_grid(a) : a->Gd;
-    a->last_part = a->partial;
-    if (st) return st;
-    MPG_LAUNCH_CHECK(a->ctx);
-    return MPG_OK;
-}
 
 int mpg_arnoldi_cgs(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, false); }
 int mpg_arnoldi_cgs_partials(mpg_arnoldi_t a, int k) { return cgs_impl(a, k, 0, false, true); }
 int mpg_arnoldi_cgs_givens(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, true); }
 int mpg_arnoldi_cgsr_wide_pass(mpg_arnoldi_t a, int k, int pass) { return cgs_impl(a, k, pass, false, true, true); }
 
-static int mgs_impl(mpg_arnoldi_t a, int k, int j, bool from_partials) {
-    if (!a || k < 0 || k >= a->d.m || j < 0 || j > k) return MPG_ERR_ARG;
-    // from_partials: h_jk from the previous launch's partials; the update
-    // writes into the other partial buffer (the previous one is still read)
-    const double* src = from_partials ? a->last_part : a->sums;
-    const int src_G = from_partials ? a->last_G : 0;
-    double* dst = from_partials && a->last_part == a->partial ? a->dpart : a->partial;
-    if (from_partials && src_G > kCombineGroups * 4) return MPG_ERR_ARG;
-    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
-        using T = decltype(t);
-        T* hjk = static_cast<T*>(a->H) + (int64_t)k * (a->d.m + 1) + j;
-        k_mgs_update<T, kCombineBlock><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-            a->d.n, static_cast<const T*>(a->V), a->ld, j, k, src, src_G, hjk, static_cast<T*>(a->w[(k + 1) & 1]),
-            dst);
-        return (int)MPG_OK;
-    });
-    a->last_G = a->Gd;
-    a->last_part = dst;
-    if (st) return st;
-    MPG_LAUNCH_CHECK(a->ctx);
-    return MPG_OK;
-}
-
 int mpg_arnoldi_mgs(mpg_arnoldi_t a, int k, int j) { return mgs_impl(a, k, j, false); }
 int mpg_arnoldi_mgs_partials(mpg_arnoldi_t a, int k, int j) { return mgs_impl(a, k, j, true); }
-
-static int givens_impl(mpg_arnoldi_t a, int k, bool from_partials) {
-    if (!a || k < 0 || k >= a->d.m) return MPG_ERR_ARG;
-    int st = dispatch(a->combo, [&](auto t, auto, auto, auto) {
-        using T = decltype(t);
-        k_givens<T><<<1, kBlock, 0, a->ctx->stream>>>(givens_args<T>(a, k), from_partials ? a->last_part : a->sums,
-                                                      from_partials ? a->last_G : 0);
-        return MPG_OK;
-    });
-    if (st) return st;
-    MPG_LAUNCH_CHECK(a->ctx);
-    return MPG_OK;
-}
 
 int mpg_arnoldi_givens(mpg_arnoldi_t a, int k) { return givens_impl(a, k, false); }
 int mpg_arnoldi_givens_partials(mpg_arnoldi_t a, int k) { return givens_impl(a, k, true); }
 
 int mpg_arnoldi_update(mpg_arnoldi_t a, int k) {
-    if (!a || k < 0 || k > a->d.m || k > 1024) return MPG_ERR_ARG;
-    if (k == 0) return MPG_OK;
-    int st = dispatch(a->combo, [&](auto t, auto x, auto, auto) {
-        using T = decltype(t);
-        using X = decltype(x);
-        if (k <= kNC) {  // x is an aligned allocation: row groups of 4 are 16/32-B aligned
-            return with_nc<kNC>(k, [&](auto nc) {
-                k_update_x_nc<T, X, decltype(nc)::value><<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(
-                    a->d.n, static_cast<const T*>(a->V), a->ld, static_cast<const T*>(a->s()),
-                    static_cast<const T*>(a->H), a->d.m + 1, static_cast<X*>(a->d.x));
-                return (int)MPG_OK;
-            });
-        } else if (k <= kWave) {
-            k_update_x<T, X, true><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, static_cast<const T*>(a->s()),
-                static_cast<const T*>(a->H), a->d.m + 1, static_cast<X*>(a->d.x));
-        } else {
-            const size_t packed = (size_t)k * (k + 1) / 2 * sizeof(T);
-            if (k <= 2 * kWave && packed <= 65536)
-                k_trsv_upper_lds<T, 2><<<1, kBlock, packed, a->ctx->stream>>>(
-                    k, a->d.m + 1, static_cast<const T*>(a->H), static_cast<T*>(a->s()));
-            else
-                k_trsv_upper<T><<<1, kBlock, 0, a->ctx->stream>>>(k, a->d.m + 1, static_cast<const T*>(a->H),
-                                                                  static_cast<T*>(a->s()));
-            k_update_x<T, X, false><<<row_grid(a), kBlock, 0, a->ctx->stream>>>(
-                a->d.n, static_cast<const T*>(a->V), a->ld, k, static_cast<const T*>(a->s()), nullptr, 0,
-                static_cast<X*>(a->d.x));
-        }
-        return (int)MPG_OK;
-    });
-    if (st) return st;
-    MPG_LAUNCH_CHECK(a->ctx);
+    return a && a->acc32 ? mpg_acc32::update(a, k) : update_run<double>(a, k);
+}
+
+int mpg_arnoldi_set_accum(mpg_arnoldi_t a, int accum) {
+    if (!a || (accum != MPG_ACCUM_F64 && accum != MPG_ACCUM_F32)) return MPG_ERR_ARG;
+    // an fp64 Arnoldi accumulates in fp64 either way (cblas_d*: the reference's class)
+    a->acc32 = accum == MPG_ACCUM_F32 && a->tsize == 4;
     return MPG_OK;
 }
+
+int mpg_arnoldi_accum(mpg_arnoldi_t a) { return !a ? MPG_ERR_ARG : a->acc32 ? MPG_ACCUM_F32 : MPG_ACCUM_F64; }
 
 double* mpg_arnoldi_sums_dev(mpg_arnoldi_t a) { return a ? a->sums : nullptr; }
 void* mpg_arnoldi_wprev_dev(mpg_arnoldi_t a, int k) { return a ? a->w[k & 1] : nullptr; }

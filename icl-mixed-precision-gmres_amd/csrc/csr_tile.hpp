@@ -209,19 +209,26 @@ __device__ __forceinline__ void stage_products_interior(int s, int e, const int3
     }
 }
 
-// Row sums of one row block: epi(row, fp64 sum, pre(row)) is called once per
-// row. pre(row) loads the row's epilogue operands; for this lane's first row
-// it is issued ahead of the tile, so its latency hides under the tile's.
-template <bool NT = false, class V, class XF, class PF, class EPI>
+// Row sums of one row block: epi(row, sum, pre(row)) is called once per
+// row (the sum in the accumulation class A: fp64, or fp32 -- mac / add_prod,
+// internal.hpp). pre(row) loads the row's epilogue operands; for this lane's
+// first row it is issued ahead of the tile, so its latency hides under the
+// tile's.
+template <bool NT = false, class A = double, class V, class XF, class PF, class EPI>
 __device__ __forceinline__ void csr_row_block(int r0, int r1, int s, int e, const int32_t* __restrict__ rowptr,
                                               const int32_t* __restrict__ col, const V* __restrict__ val,
                                               int64_t nnz_total, XF xval, PF pre, EPI epi, double* prod,
                                               double* scratch) {
-    // s, e = rowptr[r0], rowptr[r1] (the analysis' nnz starts of the block)
-    if (r1 - r0 == 1) {
-        double acc = 0.0;
-        for (int i = s + threadIdx.x; i < e; i += kBlock) acc += scalar_val(val, i) * xval(col[i]);
-        const double sum = block_sum<kBlock>(acc, scratch);
+    // s, e = rowptr[r0], rowptr[r1] (the analysis' nnz starts of the block).
+    // Row mode (strided lanes, a tree sum) only for a row the stream mode
+    // cannot stage: a short row that mpg_csr_create left alone in its block
+    // (the next row is long, or it is the matrix's last) is summed in CSR
+    // order like every other short row, so the SELL and node-block copies,
+    // which sum every row in that order, keep giving its bits.
+    if (r1 - r0 == 1 && e - s > kNnzCap) {
+        A acc = A(0);
+        for (int i = s + threadIdx.x; i < e; i += kBlock) mac(acc, scalar_val(val, i), xval(col[i]));
+        const A sum = block_sum<kBlock>(acc, reinterpret_cast<A*>(scratch));
         if (threadIdx.x == 0) epi(r0, sum, pre(r0));
         __syncthreads();  // the row's outputs are visible to the whole workgroup
         return;
@@ -238,8 +245,8 @@ __device__ __forceinline__ void csr_row_block(int r0, int r1, int s, int e, cons
         const bool first = r == threadIdx.x;
         const int a = (first ? ra : rowptr[r0 + r]) - s;
         const int z = (first ? rz : rowptr[r0 + r + 1]) - s;
-        double acc = 0.0;
-        for (int j = a; j < z; ++j) acc += prod[j];
+        A acc = A(0);
+        for (int j = a; j < z; ++j) add_prod(acc, prod[j]);
         epi(r0 + r, acc, first ? pf : pre(r0 + r));
     }
     __syncthreads();

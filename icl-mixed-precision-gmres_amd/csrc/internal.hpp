@@ -183,6 +183,28 @@ __device__ __forceinline__ T block_max(T v, T* scratch) {
 
 template <class T> struct acc_type { using type = double; };
 
+// acc + a * b in the accumulation class of a kernel (arnoldi_kernels.hpp):
+// fp64 (one fused multiply-add), or fp32 -- the fp64 product (exact for
+// fp32 / fp16 operands) rounded to fp32, then an fp32 add: the same two
+// roundings in every storage format (SELL, node blocks, CSR tiles), so the
+// formats keep giving one another's bits under either class
+// (fp32: contraction off -- for fp32 operands the compiler would otherwise
+// narrow the exact fp64 product to an fp32 multiply and fuse it with the add
+// into an fp32 FMA on the SELL copy, while the tiles add products staged in
+// LDS: measured 87 of 90 steps differing between SELL and CSR)
+__device__ __forceinline__ void mac(double& acc, double a, double b) { acc += a * b; }
+__device__ __forceinline__ void mac(float& acc, double a, double b) {
+#pragma clang fp contract(off)
+    const float p = (float)(a * b);
+    acc = acc + p;
+}
+// acc + p, p an exact fp64 product (the tiles' LDS products), in the class
+__device__ __forceinline__ void add_prod(double& acc, double p) { acc += p; }
+__device__ __forceinline__ void add_prod(float& acc, double p) {
+#pragma clang fp contract(off)
+    acc = acc + (float)p;
+}
+
 __device__ __forceinline__ float to_float(uint16_t h) {
     return __half2float(__ushort_as_half(h));
 }

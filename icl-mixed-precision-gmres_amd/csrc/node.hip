@@ -1,5 +1,7 @@
 // Build of the node-block copy of the Arnoldi matrix (node_tile.hpp).
 #include "node_tile.hpp"
+#include "ride.hpp"
+#include "scalar_program.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -165,22 +167,49 @@ __global__ __launch_bounds__(kBlock) void k_node_fill_padded(int nn, const int32
 }
 
 // y = alpha * A x + beta * y over the node copy: the CSR tile's epilogue
-// (spmv.hip k_csr_adaptive) on node_tiles' row sums
-template <class VI, class X>
+// (spmv.hip k_csr_adaptive) on node_tiles' row sums.
+// Rides (round 6; the SELL copy's since round 5, sell.hip):
+// prog.count > 0: workgroup 0 runs that scalar program (the surface's Givens
+// step of the previous Arnoldi step, which this SpMV neither reads nor
+// writes: kernels_hip.cpp checks the operands) and the tiles take the other
+// workgroups. NORM: x is w; every workgroup forms a = T(1) / h from the
+// ||w||^2 partials (norm_scale, ride.hpp), multiplies T(a x_c) -- scal_recip's
+// product, the vector the separate launches would store and read -- and
+// stores v_i = T(a x_i) for its own rows: the bits of mpg_scal_recip_nrm2_*
+// followed by the plain node SpMV.
+template <class VI, class X, bool NORM = false>
 __global__ __launch_bounds__(kBlock) void k_node_spmv(const int32_t* __restrict__ tiles,
                                                       const int32_t* __restrict__ bptr, const char* __restrict__ recs,
                                                       int ntiles, int64_t nblk, int tpw, int xcd,
-                                                      const X* __restrict__ x, X alpha, X beta, X* __restrict__ y) {
+                                                      const X* __restrict__ x, X alpha, X beta, X* __restrict__ y,
+                                                      ScalarProgram prog, NormArgs<X> nm) {
     __shared__ double prod[kNodeProd];
-    const int g = xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    double pv = 0.0;  // NORM: this lane's ||w||^2 partial, issued first
+    if constexpr (NORM) pv = (int)threadIdx.x < nm.nparts ? nm.part[threadIdx.x] : 0.0;
+    int b = (int)blockIdx.x, G = (int)gridDim.x;
+    if (prog.count > 0) {
+        if (b == 0) {
+            __shared__ double plds[3 * kProgStage + 1];
+            if constexpr (NORM) (void)norm_scale(nm, pv);  // h(k+1,k) stored before the program reads it
+            if (threadIdx.x < kWave) run_scalar_program<kProgStage>(prog, plds);
+            return;
+        }
+        --b;
+        --G;
+    }
+    X a = X(1);
+    if constexpr (NORM) a = norm_scale(nm, pv);
+    const int g = xcd ? xcd_block(b, G) : b;
     const int t0 = g * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
+    auto sc = [&](X v) { return NORM ? (X)(a * v) : v; };
     node_tiles<VI>(
         t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, [&](int c) { return x[c]; },
-        [&](X v) { return (double)v; },
+        [&](X v) { return (double)sc(v); },
         [&](int i) { return beta == X(0) ? X(0) : y[i]; },
         [&](int i, double sum, X yi) {
             const X t = (X)sum;
             y[i] = beta == X(0) ? alpha * t : alpha * t + beta * yi;
+            if constexpr (NORM) nm.v[i] = sc(x[i]);
         },
         prod);
 }
@@ -189,6 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_node_spmv(const int32_t* __restrict_
 
 struct mpg_node {
     mpg_ctx* ctx = nullptr;
+    int cols = 0;
     mpg::NodeCopy S;
 };
 
@@ -324,19 +354,39 @@ int64_t node_bytes(const NodeCopy& S) {
 
 }  // namespace mpg
 
-template <class X>
-static int node_spmv_impl(mpg_ctx_t ctx, mpg_node_t A, X alpha, const X* x, X beta, X* y) {
+template <class X, bool NORM = false>
+static int node_spmv_impl(mpg_ctx_t ctx, mpg_node_t A, X alpha, const X* x, X beta, X* y,
+                          const ScalarProgram& prog = ScalarProgram{}, const NormArgs<X>& nm = NormArgs<X>{}) {
     if (!ctx || !A) return MPG_ERR_ARG;
     if (A->S.vtype != (sizeof(X) == 8 ? MPG_F64 : MPG_F32)) return MPG_ERR_ARG;
-    if (A->S.ntiles == 0) return MPG_OK;
+    if (A->S.ntiles == 0) {
+        if (NORM) return MPG_ERR_ARG;
+        return prog.count > 0 ? mpg_scalar_program(ctx, prog.ops, prog.count) : MPG_OK;
+    }
     int tpw = node_tpw_default();
     if (tpw < 1) tpw = 2;
     using VI = std::conditional_t<sizeof(X) == 8, double, float>;
-    k_node_spmv<VI, X><<<(A->S.ntiles + tpw - 1) / tpw, kBlock, 0, ctx->stream>>>(
+    const int grid = (A->S.ntiles + tpw - 1) / tpw + (prog.count > 0 ? 1 : 0);
+    k_node_spmv<VI, X, NORM><<<grid, kBlock, 0, ctx->stream>>>(
         A->S.tiles, A->S.bptr, static_cast<const char*>(A->S.recs), A->S.ntiles, A->S.nblk, tpw, node_xcd(A->S), x,
-        alpha, beta, y);
+        alpha, beta, y, prog, nm);
     MPG_LAUNCH_CHECK(ctx);
     return MPG_OK;
+}
+
+template <class X>
+static int node_spmv_norm(mpg_ctx_t c, mpg_node_t A, int32_t nparts, X* h, const X* w, X* v, X alpha, X* y,
+                          const mpg_scalar_op* ops, int32_t nops) {
+    ScalarProgram prog;
+    if (!c || !A || !h || !w || !v || !y || nparts < 1 || nparts > kBlock || A->cols != kNodeDof * A->S.nn ||
+        make_scalar_program(ops, nops, prog) != MPG_OK)
+        return MPG_ERR_ARG;
+    NormArgs<X> nm;
+    nm.part = c->red_ws;
+    nm.nparts = nparts;
+    nm.h = h;
+    nm.v = v;
+    return node_spmv_impl<X, true>(c, A, alpha, w, X(0), y, prog, nm);
 }
 
 
@@ -350,6 +400,7 @@ int mpg_node_create(mpg_ctx_t ctx, mpg_csr_t A, int32_t vtype, const void* vals,
     mpg_node* h = new (std::nothrow) mpg_node();
     if (!h) return MPG_ERR_ALLOC;
     h->ctx = ctx;
+    h->cols = A->cols;
     if (int st = node_build(ctx, A, vtype, vals, false, h->S, alt_bytes)) {
         delete h;
         return st;
@@ -385,6 +436,26 @@ int mpg_node_spmv_f64(mpg_ctx_t ctx, mpg_node_t A, double alpha, const double* x
 }
 int mpg_node_spmv_f32(mpg_ctx_t ctx, mpg_node_t A, float alpha, const float* x, float beta, float* y) {
     return node_spmv_impl(ctx, A, alpha, x, beta, y);
+}
+int mpg_node_spmv_prog_f64(mpg_ctx_t ctx, mpg_node_t A, double alpha, const double* x, double beta, double* y,
+                           const mpg_scalar_op* ops, int32_t nops) {
+    ScalarProgram prog;
+    if (make_scalar_program(ops, nops, prog) != MPG_OK) return MPG_ERR_ARG;
+    return node_spmv_impl(ctx, A, alpha, x, beta, y, prog);
+}
+int mpg_node_spmv_prog_f32(mpg_ctx_t ctx, mpg_node_t A, float alpha, const float* x, float beta, float* y,
+                           const mpg_scalar_op* ops, int32_t nops) {
+    ScalarProgram prog;
+    if (make_scalar_program(ops, nops, prog) != MPG_OK) return MPG_ERR_ARG;
+    return node_spmv_impl(ctx, A, alpha, x, beta, y, prog);
+}
+int mpg_node_spmv_norm_f64(mpg_ctx_t c, mpg_node_t A, int32_t nparts, double* h, const double* w, double* v,
+                           double alpha, double* y, const mpg_scalar_op* ops, int32_t nops) {
+    return node_spmv_norm<double>(c, A, nparts, h, w, v, alpha, y, ops, nops);
+}
+int mpg_node_spmv_norm_f32(mpg_ctx_t c, mpg_node_t A, int32_t nparts, float* h, const float* w, float* v,
+                           float alpha, float* y, const mpg_scalar_op* ops, int32_t nops) {
+    return node_spmv_norm<float>(c, A, nparts, h, w, v, alpha, y, ops, nops);
 }
 
 }  // extern "C"

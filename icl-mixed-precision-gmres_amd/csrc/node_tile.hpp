@@ -115,10 +115,10 @@ struct NodeWords {
     }
 };
 
-// Row sums of tile t: epi(row, fp64 sum, pre(row)) once per matrix row of
+// Row sums of tile t: epi(row, sum, pre(row)) once per matrix row of
 // the tile's node rows. pre(row) for this lane's first row is issued ahead
 // of the tile's loads.
-template <class VI, class XF, class PF, class EPI>
+template <class VI, class A = double, class XF, class PF, class EPI>
 __device__ __forceinline__ void node_tile(int t, const int32_t* __restrict__ tiles, const int32_t* __restrict__ bptr,
                                           const char* __restrict__ recs, XF xval, PF pre, EPI epi,
                                           double* __restrict__ prod) {
@@ -154,12 +154,12 @@ __device__ __forceinline__ void node_tile(int t, const int32_t* __restrict__ til
         const bool first = r == (int)threadIdx.x;
         const int nr = nr0 + r / kNodeDof, k = r % kNodeDof;
         const int a = first ? fa : bptr[nr] - b0, z = first ? fz : bptr[nr + 1] - b0;
-        double acc = 0.0;
+        A acc = A(0);
         for (int b = a; b < z; ++b) {
             const double* p = prod + b * (kNodeDof * kNodeDof) + kNodeDof * k;
-            acc += p[0];
-            acc += p[1];
-            acc += p[2];
+            add_prod(acc, p[0]);
+            add_prod(acc, p[1]);
+            add_prod(acc, p[2]);
         }
         epi(kNodeDof * nr0 + r, acc, first ? pf : pre(kNodeDof * nr0 + r));
     }
@@ -176,7 +176,7 @@ __device__ __forceinline__ void node_tile(int t, const int32_t* __restrict__ til
 // (Issuing the next tile's gathers before this tile's row sums and
 // converting them after was slower: fem27 211 -> 231 us, C4 301 -> 327,
 // stencil27p 347 -> 357; profiles/r05_node_ab.jsonl.)
-template <class VI, class XR, class XF, class PF, class EPI>
+template <class VI, class A = double, class XR, class XF, class PF, class EPI>
 __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __restrict__ tiles,
                                            const int32_t* __restrict__ tb0, const int32_t* __restrict__ bptr,
                                            const char* __restrict__ recs, int64_t nblk, XR xraw, XF xfin, PF pre,
@@ -216,7 +216,7 @@ __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __rest
             const bool first = r == l;
             const int nr = nr0 + r / kNodeDof, k = r % kNodeDof;
             const int a = first ? fa : bptr[nr] - b0, z = first ? fz : bptr[nr + 1] - b0;
-            double acc = 0.0;
+            A acc = A(0);
             int b = a;
             // kNodeSumAhead blocks' products read before any is added (the
             // same order): one LDS round trip per four blocks, not per block
@@ -230,13 +230,13 @@ __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __rest
                     v[3 * u + 2] = p[2];
                 }
 #pragma unroll
-                for (int u = 0; u < 3 * kNodeSumAhead; ++u) acc += v[u];
+                for (int u = 0; u < 3 * kNodeSumAhead; ++u) add_prod(acc, v[u]);
             }
             for (; b < z; ++b) {
                 const double* p = prod + b * (kNodeDof * kNodeDof) + kNodeDof * k;
-                acc += p[0];
-                acc += p[1];
-                acc += p[2];
+                add_prod(acc, p[0]);
+                add_prod(acc, p[1]);
+                add_prod(acc, p[2]);
             }
             epi(kNodeDof * nr0 + r, acc, first ? pf : pre(kNodeDof * nr0 + r));
         }

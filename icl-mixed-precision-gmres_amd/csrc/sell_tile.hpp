@@ -251,18 +251,19 @@ struct SellRow {
     }
     // acc += the batch at step q with its gathered x, in CSR order; xs(x)
     // is the fp64 operand (a kernel that gathers x raw, before the scale it
-    // is multiplied by is known, applies the scale here)
-    template <class X, class XS>
-    __device__ __forceinline__ void sum_gathered(int q, const X (&x)[U][W], XS xs, double& acc) const {
+    // is multiplied by is known, applies the scale here); acc in the
+    // accumulation class (mac, internal.hpp)
+    template <class X, class XS, class A>
+    __device__ __forceinline__ void sum_gathered(int q, const X (&x)[U][W], XS xs, A& acc) const {
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int e = 0; e < W; ++e)
-                if (q + u < steps && SellCol<CI>::live(c[u][e])) acc += widen(v[u][e]) * xs(x[u][e]);
+                if (q + u < steps && SellCol<CI>::live(c[u][e])) mac(acc, widen(v[u][e]), xs(x[u][e]));
     }
     // acc += the batch loaded at step q, in CSR order
-    template <class XF>
-    __device__ __forceinline__ void sum(int q, XF xval, double& acc) const {
+    template <class XF, class A>
+    __device__ __forceinline__ void sum(int q, XF xval, A& acc) const {
         double x[U][W];
         gather(xval, x);
         sum_gathered(q, x, [](double a) { return a; }, acc);
@@ -271,10 +272,10 @@ struct SellRow {
 
 // The row sum from a CSR in CSR order with SellRow::sum's arithmetic (a
 // stepped copy's flagged slices, from the copy's sub-CSR); i < 0: no row, 0.
-template <class S, class XF>
-__device__ __forceinline__ double csr_row_sum(int i, const int32_t* __restrict__ rowptr,
-                                              const int32_t* __restrict__ col, const S* __restrict__ val, XF xval) {
-    double acc = 0.0;
+template <class A = double, class S, class XF>
+__device__ __forceinline__ A csr_row_sum(int i, const int32_t* __restrict__ rowptr,
+                                         const int32_t* __restrict__ col, const S* __restrict__ val, XF xval) {
+    A acc = A(0);
     if (i < 0) return acc;
     const int j0 = rowptr[i], e = rowptr[i + 1];
     if (j0 >= e) return acc;
@@ -297,7 +298,7 @@ __device__ __forceinline__ double csr_row_sum(int i, const int32_t* __restrict__
         for (int b = 0; b < B; ++b) x[b] = xval(c[b]);
 #pragma unroll
         for (int b = 0; b < B; ++b)
-            if (j + b < e) acc += widen(v[b]) * x[b];
+            if (j + b < e) mac(acc, widen(v[b]), x[b]);
     }
     return acc;
 }

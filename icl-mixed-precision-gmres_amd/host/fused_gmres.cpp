@@ -359,6 +359,8 @@ FusedEngine::FusedEngine(mpg_ctx_t ctx, const mpg_solve_args& a, Comm* comm, int
     // rows all in range: the unscaled kernels (no exponent loads, same bits)
     d.inner_row_exp = I.half_stats[0] > 0 ? I.row_exp.as<int8_t>() : nullptr;
     check(mpg_arnoldi_create(ctx, &d, &I.arn), "mpg_arnoldi_create", ctx);
+    // fp32 Arnoldi: the reference's fp32 accumulation class on request (arnoldi.h)
+    if (a.accum) check(mpg_arnoldi_set_accum(I.arn, MPG_ACCUM_F32), "mpg_arnoldi_set_accum", ctx);
     // ranks all-reduce per-workgroup partials in place: same count on every rank
     // (MPG_UNIFORM_GROUPS=1 gives one GPU the ranks' partial counts: a P = 1
     // RCCL solve then has the single-GPU solve's bits, tests/test_dist_gpu.py)
@@ -1513,6 +1515,11 @@ int mpg_engine_spmv_layout(mpg_engine_t e, int32_t* format, int32_t* vec_width, 
 int mpg_engine_sell_columns(mpg_engine_t e, int32_t* form, int64_t* csr_slices, int64_t* implicit_slices) {
     if (!e || !e->eng) return MPG_ERR_ARG;
     return mpg_arnoldi_sell_columns(e->eng->arnoldi(), form, csr_slices, implicit_slices);
+}
+
+int mpg_engine_accum(mpg_engine_t e) {
+    if (!e || !e->eng) return MPG_ERR_ARG;
+    return mpg_arnoldi_accum(e->eng->arnoldi());
 }
 
 int mpg_engine_givens_folded(mpg_engine_t e) {

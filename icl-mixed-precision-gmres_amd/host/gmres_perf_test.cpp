@@ -80,6 +80,12 @@ int main(int argc, char* argv[]) {
         else if (f == "--ngpus") ngpus = std::stoi(next());
         else if (f == "--half-unscaled") a.half_unscaled = 1;
         else if (f == "--stop-on-breakdown") a.stop_on_breakdown = 1;
+        else if (f == "--accum") {  // fp32 Arnoldi's accumulation class (solve.h)
+            const std::string v = next();
+            if (v == "f64") a.accum = 0;
+            else if (v == "f32") a.accum = 1;
+            else { std::cout << "Unknown accumulation (f64 | f32)" << std::endl; return 1; }
+        }
         else if (f == "--mode") {
             const std::string v = next();
             if (v == "mixed") a.mode = MPG_MODE_MIXED;

@@ -893,11 +893,12 @@ template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Ve
                                    Vect<double, Hip> y) {
     assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
                              : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
-    if (mpg_node_t nd = A.node()) {
-        check(mpg_node_spmv_f64(C, nd, alpha, x.data(), beta, y.data()), "spmv (node blocks)");
-        ++mpg::tl_spmv_counts[0];
-    } else if (mpg_sell_t s = A.sell()) {
-        ++mpg::tl_spmv_counts[1];
+    mpg_node_t nd = A.node();
+    mpg_sell_t s = nd ? nullptr : A.sell();
+    if (nd || s) {
+        // node blocks (round 6) or SELL-64: the same rides -- add_vector's
+        // normalisation and the previous step's Givens program in this launch
+        ++mpg::tl_spmv_counts[nd ? 0 : 1];
         mpg_scalar_op ops[MPG_SCALAR_PROGRAM_MAX];
         int nops = 0;
         mpg_ctx_t c = nullptr;
@@ -906,16 +907,25 @@ template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Ve
         const void* w = nullptr;
         if (beta == double(0) && x.n() == y.n() &&
             mpg::take_ride(x.data(), y.data(), (int64_t)x.n(), true, ops, nops, c, np, h, w)) {
-            // add_vector's normalisation and the Givens program ride this SpMV
-            check(mpg_sell_spmv_norm_f64(c, s, np, static_cast<double*>(h), static_cast<const double*>(w), x.data(), alpha,
-                                         y.data(), ops, nops),
+            check(nd ? mpg_node_spmv_norm_f64(c, nd, np, static_cast<double*>(h), static_cast<const double*>(w), x.data(),
+                                               alpha, y.data(), ops, nops)
+                     : mpg_sell_spmv_norm_f64(c, s, np, static_cast<double*>(h), static_cast<const double*>(w), x.data(),
+                                               alpha, y.data(), ops, nops),
                   "spmv (normalising)", c);
             return;
         }
+        // (a deferred normalisation this SpMV does not take is issued first: it
+        // writes w's value back and V(:,k+1), which the SpMV may read)
+        mpg::flush_ride();
         c = mpg::take_scalar_ops_for(x.data(), x.n() * 8, y.data(), y.n() * 8, ops, nops);
-        check(nops ? mpg_sell_spmv_prog_f64(c, s, alpha, x.data(), beta, y.data(), ops, nops)
-                   : mpg_sell_spmv_f64(c, s, alpha, x.data(), beta, y.data()),
-              "spmv");
+        if (nd)
+            check(nops ? mpg_node_spmv_prog_f64(c, nd, alpha, x.data(), beta, y.data(), ops, nops)
+                       : mpg_node_spmv_f64(c, nd, alpha, x.data(), beta, y.data()),
+                  "spmv (node blocks)");
+        else
+            check(nops ? mpg_sell_spmv_prog_f64(c, s, alpha, x.data(), beta, y.data(), ops, nops)
+                       : mpg_sell_spmv_f64(c, s, alpha, x.data(), beta, y.data()),
+                  "spmv");
     } else {
         check(mpg_csr_spmv_f64(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
         ++mpg::tl_spmv_counts[2];
@@ -925,11 +935,12 @@ template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<
                                   Vect<float, Hip> y) {
     assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
                              : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
-    if (mpg_node_t nd = A.node()) {
-        check(mpg_node_spmv_f32(C, nd, alpha, x.data(), beta, y.data()), "spmv (node blocks)");
-        ++mpg::tl_spmv_counts[0];
-    } else if (mpg_sell_t s = A.sell()) {
-        ++mpg::tl_spmv_counts[1];
+    mpg_node_t nd = A.node();
+    mpg_sell_t s = nd ? nullptr : A.sell();
+    if (nd || s) {
+        // node blocks (round 6) or SELL-64: the same rides -- add_vector's
+        // normalisation and the previous step's Givens program in this launch
+        ++mpg::tl_spmv_counts[nd ? 0 : 1];
         mpg_scalar_op ops[MPG_SCALAR_PROGRAM_MAX];
         int nops = 0;
         mpg_ctx_t c = nullptr;
@@ -938,16 +949,25 @@ template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<
         const void* w = nullptr;
         if (beta == float(0) && x.n() == y.n() &&
             mpg::take_ride(x.data(), y.data(), (int64_t)x.n(), false, ops, nops, c, np, h, w)) {
-            // add_vector's normalisation and the Givens program ride this SpMV
-            check(mpg_sell_spmv_norm_f32(c, s, np, static_cast<float*>(h), static_cast<const float*>(w), x.data(), alpha,
-                                         y.data(), ops, nops),
+            check(nd ? mpg_node_spmv_norm_f32(c, nd, np, static_cast<float*>(h), static_cast<const float*>(w), x.data(),
+                                               alpha, y.data(), ops, nops)
+                     : mpg_sell_spmv_norm_f32(c, s, np, static_cast<float*>(h), static_cast<const float*>(w), x.data(),
+                                               alpha, y.data(), ops, nops),
                   "spmv (normalising)", c);
             return;
         }
+        // (a deferred normalisation this SpMV does not take is issued first: it
+        // writes w's value back and V(:,k+1), which the SpMV may read)
+        mpg::flush_ride();
         c = mpg::take_scalar_ops_for(x.data(), x.n() * 4, y.data(), y.n() * 4, ops, nops);
-        check(nops ? mpg_sell_spmv_prog_f32(c, s, alpha, x.data(), beta, y.data(), ops, nops)
-                   : mpg_sell_spmv_f32(c, s, alpha, x.data(), beta, y.data()),
-              "spmv");
+        if (nd)
+            check(nops ? mpg_node_spmv_prog_f32(c, nd, alpha, x.data(), beta, y.data(), ops, nops)
+                       : mpg_node_spmv_f32(c, nd, alpha, x.data(), beta, y.data()),
+                  "spmv (node blocks)");
+        else
+            check(nops ? mpg_sell_spmv_prog_f32(c, s, alpha, x.data(), beta, y.data(), ops, nops)
+                       : mpg_sell_spmv_f32(c, s, alpha, x.data(), beta, y.data()),
+                  "spmv");
     } else {
         check(mpg_csr_spmv_f32(C, A.applied_csr(), alpha, A.applied_vals(), x.data(), beta, y.data()), "spmv");
         ++mpg::tl_spmv_counts[2];

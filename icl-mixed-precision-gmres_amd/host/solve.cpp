@@ -207,6 +207,12 @@ extern "C" int mpg_solve(const mpg_solve_args* args, mpg_solve_result* result) {
     try {
         if (args->n <= 0 || args->rlen <= 0 || !args->rowptr || !args->col || !args->val || !args->b)
             throw std::invalid_argument("invalid solve arguments (n, rlen, CSR arrays and b are required)");
+        if (args->accum != 0 && args->accum != 1) throw std::invalid_argument("accum: 0 (f64) or 1 (f32)");
+        if (args->accum && args->engine != MPG_ENGINE_FUSED && args->mode != MPG_MODE_BASELINE &&
+            args->mode != MPG_MODE_SINGLE_PREC)
+            throw mpg::StatusError(MPG_ERR_UNSUPPORTED,
+                                   "mpgmres: accum f32 runs on the fused engine only (the operator surface's "
+                                   "kernels accumulate in fp64)");
         mpg::set_quiet(!args->verbose);
         mpg_ctx_t ctx = nullptr;
         mpg::check(mpg_ctx_create(args->device, &ctx), "mpg_ctx_create");

@@ -23,7 +23,8 @@
  *   update(k)  y = H(0:k,0:k)^-1 s(0:k); x += V(:,0:k) y  (gmres.cpp:276-290)
  *
  * Every global reduction is two-stage: phase kernels write per-workgroup
- * fp64 partials, mpg_arnoldi_reduce sums them in a fixed order into
+ * partials (fp64 storage; fp32 values under MPG_ACCUM_F32, below),
+ * mpg_arnoldi_reduce sums them in a fixed order into
  * `sums` (fp64). A row-partitioned multi-GPU caller all-reduces `sums`
  * across ranks between the two (mpg_arnoldi_sums_dev), and exchanges the
  * halo entries of w_prev / x (mpg_arnoldi_halo_*), before the consumers
@@ -215,6 +216,34 @@ int mpg_arnoldi_num_groups(mpg_arnoldi_t a);
 double* mpg_arnoldi_partials_dev(mpg_arnoldi_t a);
 int mpg_arnoldi_partials_count(mpg_arnoldi_t a);
 int mpg_arnoldi_uniform_groups(mpg_arnoldi_t a);
+
+/* Accumulation class of an fp32 Arnoldi (vec_type MPG_F32), set once after
+ * create, before the first cycle:
+ *   MPG_ACCUM_F64 (default)  every dot, norm, gemv and SpMV row sum adds the
+ *                            fp32 products in fp64 and rounds once;
+ *   MPG_ACCUM_F32            every partial sum is an fp32 value: SpMV row
+ *                            sums (products rounded to fp32, added in CSR
+ *                            order), panel dots and the ||w||^2 partials
+ *                            (fp32 fused multiply-adds per lane, fp32 wave /
+ *                            workgroup trees), the partials' combines, the
+ *                            CGS update's V c and the solution update's V y
+ *                            -- the class of the reference's cblas_sdot /
+ *                            snrm2 / sgemv and mkl_sparse_s_mv
+ *                            (kernels_mkl.cpp:82,94,104,114,284,348) and of
+ *                            its GPU backend's cublasSdot / Sgemv /
+ *                            cusparseScsrmv (kernels_cuda.cpp:132,160,530,609).
+ *                            The once-per-cycle prologue (the fp64 residual
+ *                            and the norms of T(r), w and x) keeps fp64
+ *                            sums; so does a multi-rank all-reduce of the
+ *                            partials (ncclFloat64 sums of fp32 values).
+ * An fp64 Arnoldi accumulates in fp64 whatever is asked (cblas_d*: the
+ * reference's class); mpg_arnoldi_accum reports what runs. The panel dots
+ * fused into the SpMV (mpg_arnoldi_spmv_dots) exist in fp64 only
+ * (MPG_ERR_UNSUPPORTED under MPG_ACCUM_F32: the caller launches the dots). */
+#define MPG_ACCUM_F64 0
+#define MPG_ACCUM_F32 1
+int mpg_arnoldi_set_accum(mpg_arnoldi_t a, int accum);
+int mpg_arnoldi_accum(mpg_arnoldi_t a);
 
 #ifdef __cplusplus
 }

@@ -362,6 +362,22 @@ int mpg_node_destroy(mpg_node_t A);
 int mpg_node_layout(mpg_node_t A, int64_t* blocks, int32_t* tiles, int64_t* bytes, int64_t* padded);
 int mpg_node_spmv_f64(mpg_ctx_t ctx, mpg_node_t A, double alpha, const double* x, double beta, double* y);
 int mpg_node_spmv_f32(mpg_ctx_t ctx, mpg_node_t A, float alpha, const float* x, float beta, float* y);
+/* The node SpMV with the operator surface's rides (round 6), the forms of
+ * mpg_sell_spmv_prog_* / mpg_sell_spmv_norm_* below on the node-block copy:
+ * _prog runs a scalar program in one extra workgroup of the launch; _norm
+ * forms h = T(sqrt(sum of the nparts ||w||^2 partials in the context
+ * workspace)), v = T(T(1)/h * w) and y = alpha * T(A v) in one launch (A
+ * square; w and y must not overlap) -- the bits of mpg_scal_recip_nrm2_*
+ * followed by mpg_node_spmv_prog_* (Orthogonalization.hpp:51-60, then the
+ * next step's spmv, gmres.cpp:213). */
+int mpg_node_spmv_prog_f64(mpg_ctx_t ctx, mpg_node_t A, double alpha, const double* x, double beta, double* y,
+                           const mpg_scalar_op* ops, int32_t nops);
+int mpg_node_spmv_prog_f32(mpg_ctx_t ctx, mpg_node_t A, float alpha, const float* x, float beta, float* y,
+                           const mpg_scalar_op* ops, int32_t nops);
+int mpg_node_spmv_norm_f64(mpg_ctx_t ctx, mpg_node_t A, int32_t nparts, double* h, const double* w, double* v,
+                           double alpha, double* y, const mpg_scalar_op* ops, int32_t nops);
+int mpg_node_spmv_norm_f32(mpg_ctx_t ctx, mpg_node_t A, int32_t nparts, float* h, const float* w, float* v,
+                           float alpha, float* y, const mpg_scalar_op* ops, int32_t nops);
 /* The same SpMV with a scalar program (mpg_scalar_program) run by one extra
  * workgroup of the launch, concurrently with the rows: for a program whose
  * operands the SpMV neither reads nor writes (the caller checks). Replaces

@@ -70,6 +70,11 @@ typedef struct {
                                   return MPG_ERR_BREAKDOWN (--stop-on-breakdown); 0: the reference's
                                   behaviour (Orthogonalization.hpp:56-59 divides unguarded and the
                                   restart loop runs on), the count is only reported */
+    int32_t accum;         /* fp32 Arnoldi's accumulation class (MPG_ACCUM_F64 0 / MPG_ACCUM_F32 1,
+                              arnoldi.h): 1 keeps every dot, norm, gemv and SpMV partial sum in fp32 --
+                              the class of the reference's cblas_s* / mkl_sparse_s_mv (--accum f32);
+                              fused engine only (the operator surface refuses it: MPG_ERR_UNSUPPORTED);
+                              ignored by an fp64 Arnoldi and by the oracle */
 } mpg_solve_args;
 
 typedef struct {
@@ -173,6 +178,8 @@ int64_t mpg_engine_sell_shared_slices(mpg_engine_t e);
 int mpg_engine_sell_sigma(mpg_engine_t e);
 /* 1: the Givens step of step k-1 rides SpMV(k) (mpg_arnoldi_fold_pays); 0: its own launch */
 int mpg_engine_givens_folded(mpg_engine_t e);
+/* the accumulation class the engine's Arnoldi runs: MPG_ACCUM_F64 0 / MPG_ACCUM_F32 1 (arnoldi.h) */
+int mpg_engine_accum(mpg_engine_t e);
 /* ranks of the engine's communicator as its transport reports them: 1 for a
  * single-GPU engine, ncclCommCount for an RCCL rank, the world size for the
  * host transport; < 0 on error */

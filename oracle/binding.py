@@ -40,6 +40,7 @@ def lib() -> C.CDLL:
         _lib.oracle_max_threads.restype = C.c_int
         _lib.oracle_solve.restype = C.c_int
         _lib.oracle_force_loops.argtypes = [C.c_int]
+        _lib.oracle_force_loops_mode.argtypes = [C.c_int]
         _lib.oracle_cbwr_branch.restype = C.c_int
         d, f, i, p = C.c_double, C.c_float, C.c_int, C.c_void_p
         _lib.oracle_spmv_f64.argtypes = [i, p, p, p, d, p, d, p]
@@ -96,6 +97,15 @@ def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
+# the loop kernels' summation of fp32 operands (oracle/cpu_blas.cpp): "loops"
+# fp32 products summed in fp64 (rounded once); "seq32" every partial sum in
+# fp32, one sequential chain (a scalar CPU BLAS's class and order);
+# "pair32" fp32 partial sums in pairwise (tree) order over the long
+# reductions (dots, norms, gemv^T) -- the order of a GPU reduction -- and in
+# index order over a row of A and over a gemv row's basis columns
+LOOP_MODES = {"loops": 0, "seq32": 1, "pair32": 2}
+
+
 def solve(mpg, A, b, x_true=None, backend=None, **opts):
     """Run the oracle on the same mpg_solve_args the HIP path takes.
     backend="loops" runs this solve on the loop kernels even where MKL loaded
@@ -111,13 +121,13 @@ def solve(mpg, A, b, x_true=None, backend=None, **opts):
     args, keep = mpg.make_args(A, b, x_true, **opts)
     fn = lib().oracle_solve
     fn.argtypes = [C.POINTER(type(args)), C.POINTER(mpg.SolveResult)]
-    if backend not in (None, "mkl", "loops"):
+    if backend not in (None, "mkl") + tuple(LOOP_MODES):
         raise ValueError(f"oracle backend {backend!r}")
-    lib().oracle_force_loops(int(backend == "loops"))
+    lib().oracle_force_loops_mode(LOOP_MODES.get(backend, -1))
     try:
         return mpg.run_solve(fn, args, A.nrows)
     finally:
-        lib().oracle_force_loops(0)
+        lib().oracle_force_loops_mode(-1)
 
 
 def spmv(A, x: np.ndarray, alpha=1.0, beta=0.0, y=None, dtype=np.float64) -> np.ndarray:

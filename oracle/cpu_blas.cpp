@@ -18,6 +18,15 @@ namespace {
 MklApi g_api;
 MklApi g_off;  // loaded = false: the loop kernels
 std::atomic<bool> g_force_loops{false};
+// the loop kernels' summation of fp32 operands (force_loops(mode)):
+// kSumF64 fp32 products summed in fp64 in index order, rounded once (the HIP
+// kernels' default class); kSumSeq32 every partial sum an fp32 value, one
+// sequential chain in index order (a scalar CPU BLAS); kSumPair32 fp32
+// partial sums in pairwise (tree) order over the long reductions -- the
+// shape of a GPU reduction (cublasSdot / Sgemv, the HIP kernels under
+// accum f32) -- and sequentially over the short ones (a row of A, the k+1
+// basis columns of one gemv row)
+std::atomic<int> g_sum{kSumF64};
 std::once_flag g_once;
 
 template <class F>
@@ -105,8 +114,43 @@ void rotg_loops(T* a, T* b, T* c, T* s) {
     *b = z;
 }
 
+// fp32 sums of a[i] * b[i] (products rounded to fp32; the oracle is built
+// with -ffp-contract=off, so no fused multiply-add)
+float sum_seq32(int n, const float* a, const float* b) {
+    float s = 0.f;
+    for (int i = 0; i < n; ++i) s += a[i] * b[i];
+    return s;
+}
+float sum_pair32(int n, const float* a, const float* b) {
+    if (n <= 8) return sum_seq32(n, a, b);
+    const int h = n / 2;
+    return sum_pair32(h, a, b) + sum_pair32(n - h, a + h, b + h);
+}
+float sum32(int n, const float* a, const float* b) {
+    return g_sum.load(std::memory_order_relaxed) == kSumPair32 ? sum_pair32(n, a, b) : sum_seq32(n, a, b);
+}
+
 template <class T>
 void gemv_loops(bool trans, int rows, int cols, T alpha, const T* A, int lda, const T* x, T beta, T* y) {
+    if constexpr (sizeof(T) == 4) {
+        if (g_sum.load(std::memory_order_relaxed) != kSumF64) {
+            if (trans) {  // one fp32 reduction over the rows per column
+#pragma omp parallel for schedule(static)
+                for (int j = 0; j < cols; ++j) {
+                    const T t = sum32(rows, A + (size_t)j * lda, x);
+                    y[j] = beta == T(0) ? alpha * t : alpha * t + beta * y[j];
+                }
+            } else {  // each row: the k+1 column terms in order in fp32
+#pragma omp parallel for schedule(static)
+                for (int i = 0; i < rows; ++i) {
+                    T t = 0;
+                    for (int j = 0; j < cols; ++j) t += A[(size_t)j * lda + i] * x[j];
+                    y[i] = beta == T(0) ? alpha * t : alpha * t + beta * y[i];
+                }
+            }
+            return;
+        }
+    }
     if (trans) {
 #pragma omp parallel for schedule(static)
         for (int j = 0; j < cols; ++j) {
@@ -143,7 +187,12 @@ const MklApi& mkl() {
     return g_force_loops.load(std::memory_order_relaxed) ? g_off : g_api;
 }
 
-void force_loops(bool on) { g_force_loops.store(on, std::memory_order_relaxed); }
+void force_loops(bool on) { force_loops_mode(on ? kSumF64 : -1); }
+void force_loops_mode(int mode) {
+    g_force_loops.store(mode >= 0, std::memory_order_relaxed);
+    g_sum.store(mode >= 0 ? mode : kSumF64, std::memory_order_relaxed);
+}
+int loop_sum_mode() { return g_sum.load(std::memory_order_relaxed); }
 
 const char* backend_name() { return mkl().loaded ? "mkl" : "loops"; }
 
@@ -163,6 +212,7 @@ double dot(int n, const double* x, const double* y) {
 }
 float dot(int n, const float* x, const float* y) {
     if (mkl().loaded) return mkl().sdot(n, x, 1, y, 1);
+    if (g_sum.load(std::memory_order_relaxed) != kSumF64) return sum32(n, x, y);
     double s = 0;
     for (int i = 0; i < n; ++i) s += (double)x[i] * y[i];
     return (float)s;
@@ -175,6 +225,7 @@ double nrm2(int n, const double* x) {
 }
 float nrm2(int n, const float* x) {
     if (mkl().loaded) return mkl().snrm2(n, x, 1);
+    if (g_sum.load(std::memory_order_relaxed) != kSumF64) return std::sqrt(sum32(n, x, x));
     double s = 0;
     for (int i = 0; i < n; ++i) s += (double)x[i] * x[i];
     return (float)std::sqrt(s);

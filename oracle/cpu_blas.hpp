@@ -60,6 +60,11 @@ const MklApi& mkl();
 // Use the loop kernels (fp32 products summed in fp64, in index order) while
 // on, whether or not MKL loaded: a machine-independent summation order.
 void force_loops(bool on);
+// the loop kernels with a summation mode for fp32 operands (cpu_blas.cpp:
+// kSumF64, kSumSeq32, kSumPair32); -1: MKL again
+enum { kSumF64 = 0, kSumSeq32 = 1, kSumPair32 = 2 };
+void force_loops_mode(int mode);
+int loop_sum_mode();
 const char* backend_name();
 void set_threads(int threads);
 int max_threads();

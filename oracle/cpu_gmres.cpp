@@ -101,6 +101,15 @@ void spmv(float alpha, const Csr<float>& A, const float* x, float beta, float* y
             throw std::runtime_error("mkl_sparse_s_mv failed");
         return;
     }
+    if (loop_sum_mode() != kSumF64) {  // fp32 row sums in CSR order, products rounded to fp32
+#pragma omp parallel for schedule(static)
+        for (int i = 0; i < A.n; ++i) {
+            float t = 0.f;
+            for (int k = A.rp[i]; k < A.rp[i + 1]; ++k) t += A.v[k] * x[A.ci[k]];
+            y[i] = beta == 0 ? alpha * t : alpha * t + beta * y[i];
+        }
+        return;
+    }
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < A.n; ++i) {
         double s = 0;
@@ -702,6 +711,9 @@ const char* oracle_backend() { return oracle::backend_name(); }
 int oracle_max_threads() { return oracle::max_threads(); }
 int oracle_cbwr_branch() { return oracle::cbwr_branch(); }
 void oracle_force_loops(int on) { oracle::force_loops(on != 0); }
+// -1 MKL, 0 loops with fp64 sums, 1 loops with sequential fp32 sums, 2 loops
+// with pairwise fp32 sums (cpu_blas.hpp)
+void oracle_force_loops_mode(int mode) { oracle::force_loops_mode(mode); }
 
 int oracle_solve(const mpg_solve_args* a, mpg_solve_result* r) {
     if (!a || !r) return -2;

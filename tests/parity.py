@@ -39,7 +39,18 @@ preconditioner every step (modes mixed, single, mixed-half, single-prec):
     parity failure: forward error at convergence depends on conditioning);
   * when converged, the final backward error is <= tol.
 Live-oracle comparisons of fp32 Arnoldi on large inputs (compare_mkl, round
-5) compare with the MKL oracle two-sidedly. The oracle's MKL is pinned to one
+5) compare with the MKL oracle two-sidedly. Round 6 adds the GPU's fp32
+accumulation class (accum="f32": every partial sum of the fp32 Arnoldi in
+fp32, the reference's cblas_s* / mkl_sparse_s_mv class) and, for it, an
+envelope without the fp64-summing loop kernels: MKL at MKL_THREADS and the
+oracle's "pair32" loop mode (the same fp32-accumulating operations, long
+reductions in pairwise order). Within the fp32 class the accumulation ORDER
+sets how fast plain CGS loses orthogonality (BAND-300k m = 100, cycle-1
+backward error: one sequential fp32 chain 1.5e-7, MKL 6.0e-9, pairwise fp32
+4.5e-10, GPU f32 3.9e-10, fp64 sums 2.4e-10; stencil27p: 1.4e-7, 2.7e-8,
+8.07e-9, GPU f32 8.07e-9, 8.06e-9 -- profiles/r06_accum/), and a GPU
+reduction is a tree, as is the reference's own GPU backend's (cublasSdot /
+Sgemv, kernels_cuda.cpp:132,160). The oracle's MKL is pinned to one
 code branch (MKL_CBWR=COMPATIBLE, set by oracle/binding.py: conditional
 numerical reproducibility) and run at fixed thread counts (MKL_THREADS), so
 its bits no longer depend on the host: the same digests on the build
@@ -172,18 +183,27 @@ def mkl_envelope_ok(refs, got, mode: str, factor: float = 3.0):
     return True, ""
 
 
-def compare_mkl(oracle, mpg, A, b, xt, got, opts: dict, label: str = "", runs: dict = None):
+def compare_mkl(oracle, mpg, A, b, xt, got, opts: dict, label: str = "", runs: dict = None,
+                extra: tuple = ("loops",)):
     """Two-sided parity with the MKL oracle (module docstring): the oracle at
-    each of MKL_THREADS (pinned MKL branch) and on its loop kernels; got
-    compared with the 1-thread MKL run, its per-cycle backward errors inside
-    the runs' envelope. runs: a cache {threads or "loops": Result}."""
+    each of MKL_THREADS (pinned MKL branch) and on the loop-kernel modes in
+    `extra`; got compared with the 1-thread MKL run, its per-cycle backward
+    errors inside the runs' envelope. The fp64-accumulating GPU class takes
+    extra=("loops",) (fp32 products summed in fp64: its own class); a GPU run
+    in the reference's fp32 class (accum="f32") takes
+    extra=("pair32",): the same fp32-accumulating arithmetic in a tree order,
+    the order of a GPU reduction (oracle/binding.py LOOP_MODES). runs: a
+    cache {threads or loop mode: Result}."""
     runs = {} if runs is None else runs
+    opts = {k: v for k, v in opts.items() if k != "accum"}  # (the oracle's class is its backend's)
     for t in MKL_THREADS:
         if t not in runs:
             runs[t] = oracle.solve(mpg, A, b, xt, backend="mkl", threads=t, **opts)
-    if "loops" not in runs:
-        runs["loops"] = oracle.solve(mpg, A, b, xt, backend="loops", threads=1, **opts)
-    refs = [runs[t] for t in MKL_THREADS] + [runs["loops"]]
+    refs = [runs[t] for t in MKL_THREADS]
+    for mode in extra:
+        if mode not in runs:
+            runs[mode] = oracle.solve(mpg, A, b, xt, backend=mode, threads=1, **opts)
+        refs.append(runs[mode])
     compare(as_ref(refs[0]), got, opts["mode"], opts["tol"], opts["rlen"], label, envelope=refs)
     return runs
 

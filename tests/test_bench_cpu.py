@@ -61,6 +61,60 @@ def test_launcher_starts_n_ranks():
     assert other[0]["master"] == lines[0]["master"]
 
 
+def test_launcher_world8_rehearses_the_setup_over_gloo():
+    """The N = 8 run's CPU-side set-up, pre-flighted: eight
+    rank processes, one gloo process group (the only torch group a rank
+    makes; the data path's RCCL communicator is the engine's own), each
+    rank's BAND block analysed and the halo lists swapped: rank q receives
+    5 rows from q-1 and 4 from q+1 (offsets -5..+4) and sends the mirror;
+    rank 0's 128-byte unique-id stand-in reaches every rank."""
+    p = _bench(["--gpus", "8", "--dry-run", "--n-local", "2000"], timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    others = [json.loads(ln.split("] ", 1)[1]) for ln in p.stderr.splitlines()
+              if ln.startswith("[rank ") and ln.split("] ", 1)[1].startswith("{")]
+    ranks = sorted(lines + others, key=lambda d: d["rank"])
+    assert [d["rank"] for d in ranks] == list(range(8)), p.stderr[-2000:]
+    for d in ranks:
+        q = d["rank"]
+        assert d["world"] == 8 and d["process_group"] == "gloo" and d["uid_bytes"] == 128
+        want_recv = {**({str(q - 1): 5} if q > 0 else {}), **({str(q + 1): 4} if q < 7 else {})}
+        want_send = {**({str(q - 1): 4} if q > 0 else {}), **({str(q + 1): 5} if q < 7 else {})}
+        assert d["halo_recv"] == want_recv and d["halo_send"] == want_send, d
+        assert d["n_ext"] == 2000 + (4 if q < 7 else 0)
+        assert any("ncclAllReduce" in c for c in d["step_collectives"])
+
+
+class _Res:
+    def __init__(self, iters, secs):
+        self.total_iters, self.gmres_seconds = iters, secs
+
+
+def test_cpu_baseline_respects_its_budget_and_reports_best():
+    """A CPU leg stops its timed solves when the next would overrun the leg's
+    budget (the N = 8 legs on 80M / 100M-nnz matrices stay bounded), keeps at
+    least one per orthogonalisation, and reports the faster one as `best`."""
+    import argparse
+    import time
+
+    def slow_solve(mpg, A, b, xt, orth, max_restarts, threads, **o):
+        t = 0.3 if orth == "cgs" else 0.1  # MGS the faster, as MKL's is
+        time.sleep(t)
+        return _Res(30 * max_restarts, t)
+
+    args = argparse.Namespace(orth="cgs", cpu_cycles=2, cpu_runs=50, cpu_budget_s=2.0, rlen=30, mode="mixed")
+    opts = dict(mode="mixed", orth="cgs", prec="identity", rlen=30, tol=0.0, max_restarts=10, device=0)
+    t0 = time.perf_counter()
+    cpu = bench.cpu_baseline(None, None, None, None, opts, args, solve=slow_solve)
+    wall = time.perf_counter() - t0
+    assert wall < 2.0 + 0.3 + 0.3 + 0.5, wall  # the budget, one overrunning solve and the warm-ups
+    assert 1 <= len(cpu["by_orth"]["cgs"]["runs"]) < 50 and 1 <= len(cpu["by_orth"]["mgs"]["runs"]) < 50
+    assert cpu["value"] == cpu["by_orth"]["cgs"]["median"] and cpu["best_orth"] == "mgs"
+    assert cpu["best"] == cpu["by_orth"]["mgs"]["median"] > cpu["value"]
+    bench.vs_gpu(cpu, 26000.0)
+    assert cpu["vs_gpu_best"] == round(26000.0 / cpu["best"], 2) < cpu["vs_gpu"]
+
+
 def test_launcher_fails_when_a_rank_fails():
     p = _bench(["--gpus", "3", "--dry-run"], {"MPG_BENCH_DRY_FAIL_RANK": "1"})
     assert p.returncode != 0

@@ -642,3 +642,115 @@ def test_node_spmv_matches_csr(hip, mpg, t, which):
     finally:
         hip.lib.mpg_node_destroy(node)
         hip.lib.mpg_csr_destroy(csr)
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
+def test_isolated_short_rows_sum_in_csr_order(hip, t):
+    """A short row that mpg_csr_create leaves alone in its row block (the next
+    row is longer than a stream-mode tile, or it is the matrix's last row) is
+    summed in CSR order like every other short row -- the order of the SELL
+    and node-block copies -- not by the long-row tree. Rows of 50
+    entries alternate with rows of 2100: every short row is isolated. The
+    short rows' y equals a host restatement of the CSR tile bit for bit: each
+    product rounded to fp64 (exact for fp32 operands), added in CSR order in
+    fp64, then rounded to the vector type."""
+    dt = np.float64 if t == "f64" else np.float32
+    CT = C.c_double if t == "f64" else C.c_float
+    g = rng(11)
+    nrows, ncols = 41, 2100
+    lens = [50 if r % 2 == 0 else 2100 for r in range(nrows)]
+    rowptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    col = np.concatenate([np.sort(g.choice(ncols, L, replace=False)) for L in lens]).astype(np.int32)
+    val = g.uniform(-1, 1, rowptr[-1]).astype(dt)
+    x = g.uniform(-1, 1, ncols).astype(dt)
+    drp, dci, dv, dx, dy = hip.buf(rowptr), hip.buf(col), hip.buf(val), hip.buf(x), hip.buf(np.zeros(nrows, dt))
+    csr = C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, nrows, ncols, int(rowptr[-1]), rowptr.ctypes.data, drp.p, dci.p,
+                                     C.byref(csr)))
+    try:
+        assert hip.lib.mpg_csr_num_blocks(csr) == nrows  # every row alone in its block
+        hip.call(f"mpg_csr_spmv_{t}", csr, CT(1.0), dv.p, dx.p, CT(0.0), dy.p)
+        y = dy.get()
+    finally:
+        hip.lib.mpg_csr_destroy(csr)
+    for r in range(0, nrows, 2):
+        acc = 0.0
+        for j in range(rowptr[r], rowptr[r + 1]):
+            acc += float(val[j]) * float(x[col[j]])
+        assert y[r] == dt(acc), (r, y[r], dt(acc))
+
+
+@pytest.mark.parametrize("t", ["f64", "f32"])
+@pytest.mark.parametrize("which", ["stencil27", "fem27", "fem27p"])
+def test_node_spmv_rides_match_separate_launches(hip, mpg, t, which):
+    """Round 6: the operator surface's rides on the node-block
+    copy. mpg_node_spmv_norm_* (h = T(sqrt(sum of the ||w||^2 partials)),
+    v = T(T(1)/h w), y = T(A v), workgroup 0 storing h before the riding
+    Givens program reads it) gives the bits of mpg_scal_recip_nrm2_* then
+    mpg_node_spmv_prog_*, and mpg_node_spmv_prog_* the bits of
+    mpg_scalar_program then mpg_node_spmv_* -- whose y is mpg_csr_spmv_*'s."""
+    dt = np.float64 if t == "f64" else np.float32
+    CT = C.c_double if t == "f64" else C.c_float
+    vt = 0 if t == "f64" else 1
+    f64 = 1 if t == "f64" else 0
+    A = {"stencil27": lambda: mpg.gen_stencil27(30, 3), "fem27": lambda: mpg.gen_spec("fem27:24:3:70:13"),
+         "fem27p": lambda: mpg.gen_spec("fem27:24:3:70:13:32:5")}[which]()
+    g = rng(29)
+    n = A.nrows
+    w = g.uniform(-1, 1, n).astype(dt)
+    k = 7
+    col0 = g.normal(size=k + 2).astype(dt)
+    th = g.uniform(0, 2 * np.pi, k)
+    c0, s0 = np.cos(th).astype(dt), np.sin(th).astype(dt)
+    sv0 = np.zeros(k + 2, dt)
+    sv0[k] = dt(g.normal())
+    drp, dci, dv = hip.buf(A.rowptr), hip.buf(A.col), hip.buf(A.val.astype(dt))
+    csr, node = C.c_void_p(), C.c_void_p()
+    hip.check(hip.lib.mpg_csr_create(hip.ctx, A.nrows, A.ncols, A.nnz, A.rowptr.ctypes.data, drp.p, dci.p, C.byref(csr)))
+    hip.check(hip.lib.mpg_node_create(hip.ctx, csr, vt, dv.p, C.c_int64(-1), C.byref(node)))
+    out = {}
+    try:
+        assert node.value
+        for how in ("norm", "norm-apart", "norm-noprog", "norm-noprog-apart", "prog", "prog-apart", "csr"):
+            col = hip.buf(np.concatenate([col0, np.zeros(1, dt)]))
+            c, s = hip.buf(np.concatenate([c0, np.zeros(2, dt)])), hip.buf(np.concatenate([s0, np.zeros(2, dt)]))
+            sv = hip.buf(sv0)
+            rec = hip.buf(np.zeros(1, dt))
+            dw, dvk, dy = hip.buf(w), hip.buf(n, dt), hip.buf(np.full(n, 7.0, dt))
+            ops = (ScalarOp * 4)()
+            specs = [(2, k, [col.p, None, c.p, s.p]), (0, 0, [col.at(k), col.at(k + 1), c.at(k), s.at(k)]),
+                     (1, 0, [sv.at(k), sv.at(k + 1), c.at(k), s.at(k)]), (3, 0, [sv.at(k + 1), rec.at(0), None, None])]
+            for i, (op, kk, ps) in enumerate(specs):
+                ops[i].op, ops[i].f64, ops[i].k, ops[i].alpha = op, f64, kk, 0.0
+                for j, q in enumerate(ps):
+                    ops[i].p[j] = q.value if q is not None else None
+            nops = 0 if "noprog" in how else 4
+            if how.startswith("norm"):
+                np_ = C.c_int32()
+                hip.call(f"mpg_nrm2_partials_{t}", C.c_int64(n), dw.p, C.byref(np_))
+                if how.endswith("apart"):
+                    hip.call(f"mpg_scal_recip_nrm2_{t}", np_, col.at(k + 1), C.c_int64(n), dw.p, dvk.p)
+                    hip.call(f"mpg_node_spmv_prog_{t}", node, CT(1.0), dvk.p, CT(0.0), dy.p, C.cast(ops, C.c_void_p),
+                             nops)
+                else:
+                    hip.call(f"mpg_node_spmv_norm_{t}", node, np_, col.at(k + 1), dw.p, dvk.p, CT(1.0), dy.p,
+                             C.cast(ops, C.c_void_p), nops)
+            elif how == "prog":
+                hip.call(f"mpg_node_spmv_prog_{t}", node, CT(1.0), dw.p, CT(0.5), dy.p, C.cast(ops, C.c_void_p), 4)
+            elif how == "prog-apart":
+                hip.check(hip.lib.mpg_scalar_program(hip.ctx, ops, 4), "mpg_scalar_program")
+                hip.call(f"mpg_node_spmv_{t}", node, CT(1.0), dw.p, CT(0.5), dy.p)
+            else:  # the CSR SpMV of the normalised vector of the "norm" run
+                dvn = hip.buf(out["norm"][5])
+                hip.call(f"mpg_csr_spmv_{t}", csr, CT(1.0), dv.p, dvn.p, CT(0.0), dy.p)
+            out[how] = [b.get() for b in (col, c, s, sv, rec, dvk, dy)]
+    finally:
+        hip.lib.mpg_node_destroy(node)
+        hip.lib.mpg_csr_destroy(csr)
+    for ride, apart in (("norm", "norm-apart"), ("norm-noprog", "norm-noprog-apart"), ("prog", "prog-apart")):
+        for a, b in zip(out[ride], out[apart]):
+            assert np.array_equal(a, b), (ride, apart)
+    assert np.array_equal(out["csr"][6], out["norm"][6])
+    h = np.sqrt(np.sum(w.astype(np.float64) ** 2))
+    assert abs(out["norm-noprog"][0][k + 1] - h) <= 1e-6 * h
+    assert out["norm"][4][0] != 0 and out["prog"][4][0] != 0

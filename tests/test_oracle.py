@@ -216,3 +216,57 @@ def test_parity_rejects_a_wrong_x(mpg, oracle, mode):
         bad.err_norm = float(np.linalg.norm(bad.x - xt))
         with pytest.raises(AssertionError, match="x head|x sum"):
             compare(ref, bad, mode, 1e-10, 12, f"moved at {where}")
+
+
+def test_oracle_fp32_summation_modes(mpg, oracle):
+    """The oracle's fp32 summation modes (oracle/binding.py LOOP_MODES): on a
+    small problem "pair32" and "seq32" reproduce numpy's fp32 arithmetic for
+    a dot product (pairwise blocks of 8 / one chain), and the SpMV rounds each
+    product to fp32 and adds in CSR order -- the GPU's f32 class
+    (internal.hpp mac) -- in both modes."""
+    g = np.random.default_rng(3)
+    x = g.uniform(-1, 1, 1000).astype(np.float32)
+    y = g.uniform(-1, 1, 1000).astype(np.float32)
+
+    def seq(a, b):
+        s = np.float32(0)
+        for u, v in zip(a, b):
+            s = np.float32(s + np.float32(u * v))
+        return s
+
+    def pair(a, b):
+        if len(a) <= 8:
+            return seq(a, b)
+        h = len(a) // 2
+        return np.float32(pair(a[:h], b[:h]) + pair(a[h:], b[h:]))
+
+    A = mpg.gen_band(400, 5, 4, seed=7)
+    xv = g.uniform(-1, 1, A.nrows).astype(np.float32)
+    want = np.array([seq(A.val[A.rowptr[i]:A.rowptr[i + 1]].astype(np.float32),
+                         xv[A.col[A.rowptr[i]:A.rowptr[i + 1]]]) for i in range(A.nrows)], dtype=np.float32)
+    for mode, ref in (("seq32", seq), ("pair32", pair)):
+        oracle.lib().oracle_force_loops_mode(oracle.LOOP_MODES[mode])
+        try:
+            got = oracle.dot(x, y)
+            ys = oracle.spmv(A, xv, dtype=np.float32)
+        finally:
+            oracle.lib().oracle_force_loops_mode(-1)
+        assert got == ref(x, y), (mode, got, ref(x, y))
+        np.testing.assert_array_equal(ys, want)
+
+
+def test_fp32_summation_order_sets_cgs_accuracy(mpg, oracle):
+    """Why the GPU's fp32 class (accum="f32") is held to MKL plus the pairwise
+    fp32 mode (tests/parity.py compare_mkl): within fp32 accumulation the
+    ORDER sets how fast plain CGS loses orthogonality. BAND-300k, GMRES(100),
+    2 cycles: cycle-1 backward error one sequential fp32 chain > MKL (SIMD
+    chains) > pairwise fp32 >= fp64 sums (profiles/r06_accum/order.jsonl:
+    1.5e-7, 6.0e-9, 4.5e-10, 2.4e-10)."""
+    A = mpg.gen_band(300_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(mode="mixed", orth="cgs", prec="jacobi", rlen=100, tol=0.0, max_restarts=2)
+    be = {m: oracle.solve(mpg, A, b, xt, backend=m, threads=1 if m == "mkl" else 0, **opts).backward_error[1]
+          for m in ("seq32", "mkl", "pair32", "loops")}
+    assert be["seq32"] > 5 * be["mkl"] > 25 * be["pair32"], be
+    assert be["loops"] <= be["pair32"] <= 3 * be["loops"], be

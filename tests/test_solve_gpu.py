@@ -313,7 +313,7 @@ def test_surface_normalisation_ride_same_bits(mpg, matrix, orth, mode, prec, mon
     kernel (7-point Laplacian) and the stepped kernel with CSR-summed slices
     (27-point, 3 dof, planes past 32767 rows); CGS must actually ride, and
     the cycles still record and replay."""
-    monkeypatch.setenv("MPG_SURFACE_NODE", "0")  # (the rides are the SELL kernels'; node blocks: no ride)
+    monkeypatch.setenv("MPG_SURFACE_NODE", "0")  # (the SELL kernels' rides; node blocks: the next test)
     A = {"band": lambda: mpg.gen_band(100_000, 5, 4, seed=7), "lap": lambda: mpg.gen_laplace3d(40),
          "stencil27": lambda: mpg.gen_stencil27(105, 3, ny=105, nz=3)}[matrix]()
     xt = mpg.rand_vect(A.nrows, 42)
@@ -338,6 +338,45 @@ def test_surface_normalisation_ride_same_bits(mpg, matrix, orth, mode, prec, mon
             assert delta["rides"] >= 2 * 27 and delta["flushed"] <= 2, delta
         elif orth == "mgs":
             assert delta == {"redirects": 0, "rides": 0, "flushed": 0}, delta
+    ref = got["0"]
+    for fuse in ("", "13"):
+        g = got[fuse]
+        assert g.total_iters == ref.total_iters == 90, (fuse, g.total_iters)
+        assert np.array_equal(g.step_res, ref.step_res), fuse
+        assert np.array_equal(g.x, ref.x) and g.res_norm == ref.res_norm, fuse
+
+
+@pytest.mark.parametrize("prec", ["identity", "jacobi"])
+@pytest.mark.parametrize("mode", ["mixed", "baseline", "single"])
+@pytest.mark.parametrize("orth", ["cgs", "mgs", "cgsr"])
+@pytest.mark.parametrize("matrix", ["fem27", "stencil27p"])
+def test_surface_node_ride_same_bits(mpg, matrix, orth, mode, prec, monkeypatch):
+    """Round 6: the same rides on the node-block copy
+    (mpg_node_spmv_norm_* / _prog_*): the surface's SpMV runs on node blocks,
+    CGS rides every step but a cycle's last, and the solve has the bits of the
+    surface without the ride (MPG_SURFACE_FUSE=13) and of every call on its own
+    (0)."""
+    monkeypatch.delenv("MPG_SURFACE_NODE", raising=False)
+    A = {"fem27": lambda: mpg.gen_fem27(24, 3, keep_pct=70, seed=13),
+         "stencil27p": lambda: mpg.gen_stencil27p(40, 3, ny=40, nz=8, block=64, perm_seed=5)}[matrix]()
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(engine="surface", mode=mode, orth=orth, prec=prec, rlen=30, tol=0.0, max_restarts=3)
+    got = {}
+    for fuse in ("", "13", "0"):
+        if fuse:
+            monkeypatch.setenv("MPG_SURFACE_FUSE", fuse)
+        else:
+            monkeypatch.delenv("MPG_SURFACE_FUSE", raising=False)
+        before, sp0 = mpg.surface_ride_counts(), mpg.surface_spmv_counts()
+        got[fuse] = mpg.solve(A, b, xt, **opts)
+        after, sp1 = mpg.surface_ride_counts(), mpg.surface_spmv_counts()
+        delta = {k: after[k] - before[k] for k in after}
+        assert sp1["node"] > sp0["node"] and sp1["sell"] == sp0["sell"], (sp0, sp1)
+        if fuse:
+            assert delta["redirects"] == 0 and delta["rides"] == 0, delta
+        elif orth == "cgs":
+            assert delta["rides"] >= 2 * 27 and delta["flushed"] <= 2, delta
     ref = got["0"]
     for fuse in ("", "13"):
         g = got[fuse]
