@@ -39,7 +39,14 @@ int arnoldi_sell_build(mpg_arnoldi* a, int format) {
         const int64_t vb = a->d.inner_val == MPG_F64 ? 8 : a->d.inner_val == MPG_F32 ? 4 : 2;
         const int64_t now = a->sell.nslices > 0 ? sell_copy_bytes(a) : a->d.A->nnz * (4 + vb) + ((int64_t)a->d.n + 1) * 4;
         NodeCopy nc;
-        if (int st = node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, false, nc, now)) return st;
+        // (auto's node copy is an optimisation: a copy that cannot be built --
+        // its records' allocation failing on a large matrix -- leaves the
+        // SELL / CSR storage in place instead of failing the create)
+        if (node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, false, nc, now) != MPG_OK) {
+            node_free(nc);
+            (void)hipGetLastError();
+            return MPG_OK;
+        }
         if (nc.nblk > 0) {  // (built only when it wins)
             sell_free(a->sell);
             a->node = nc;

@@ -65,6 +65,21 @@ __global__ __launch_bounds__(1024) void k_reduce_stage2(int nparts, const double
     if (threadIdx.x == 0) *result = SQRT ? (T)sqrt(s) : (T)s;
 }
 
+// Stage 2 of a host-value reduction, storing straight into the context's
+// pinned host word (no copy command behind it): the same sum, then a
+// system-scope fence so the host's read after the stream completes sees it.
+template <class T, bool SQRT>
+__global__ __launch_bounds__(1024) void k_reduce_stage2_host(int nparts, const double* __restrict__ partial,
+                                                             T* __restrict__ result_host) {
+    __shared__ double scratch[1024 / kWave];
+    double v = threadIdx.x < nparts ? partial[threadIdx.x] : 0.0;
+    double s = block_sum<1024>(v, scratch);
+    if (threadIdx.x == 0) {
+        *result_host = SQRT ? (T)sqrt(s) : (T)s;
+        __threadfence_system();
+    }
+}
+
 // Stage 2 folded into the consumer of the result (the operator surface's
 // nrm2 -> scal_recip of add_vector, dot -> naxpy of the MGS kernel): every
 // 1024-thread workgroup sums the stage-1 partials with stage 2's own
@@ -137,12 +152,20 @@ int reduce(mpg_ctx* ctx, int64_t n, const T* x, const T* y, T* result_dev) {
 template <class T, bool SQUARE>
 int reduce_host(mpg_ctx* ctx, int64_t n, const T* x, const T* y, T* result_host) {
     if (!result_host) return MPG_ERR_ARG;
+    if (ctx && ctx->host_ws_dev) {  // stage 2 stores into pinned host memory; a polled wait
+        int32_t g = 0;
+        if (int st = reduce_partials<T, SQUARE>(ctx, n, x, y, &g)) return st;
+        if (g < 1 || g > kMaxRedBlocks) return MPG_ERR_ARG;
+        k_reduce_stage2_host<T, SQUARE><<<1, 1024, 0, ctx->stream>>>(g, ctx->red_ws, (T*)ctx->host_ws_dev);
+        MPG_LAUNCH_CHECK(ctx);
+        MPG_HIP(ctx, mpg::spin_wait(ctx->stream));
+        *result_host = *static_cast<volatile T*>(ctx->host_ws);
+        return MPG_OK;
+    }
     T* tmp = reinterpret_cast<T*>(ctx->red_ws + kMaxRedBlocks * kGemvMaxCols);
     int st = reduce<T, SQUARE>(ctx, n, x, y, tmp);
     if (st) return st;
-    MPG_HIP(ctx, hipMemcpyAsync(result_host, tmp, sizeof(T), hipMemcpyDeviceToHost, ctx->stream));
-    MPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return MPG_OK;
+    return mpg_memcpy_d2h(ctx, result_host, tmp, sizeof(T));  // (pinned staging, polled wait)
 }
 
 // ---------------- elementwise ----------------

@@ -4,6 +4,7 @@
 // explicit context per (GPU, host thread), no global mutable state.
 #include "internal.hpp"
 
+#include <cstring>
 #include <new>
 
 extern "C" {
@@ -43,7 +44,13 @@ int mpg_ctx_create(int device, mpg_ctx_t* out) {
         ctx->red_ws_elems = mpg::kWsElems;
         e = hipMalloc(&ctx->red_ws, ctx->red_ws_elems * sizeof(double));
     }
+    if (e == hipSuccess) e = hipHostMalloc(&ctx->host_ws, mpg::kHostWsBytes, hipHostMallocDefault);
+    if (e == hipSuccess && hipHostGetDevicePointer(&ctx->host_ws_dev, ctx->host_ws, 0) != hipSuccess) {
+        ctx->host_ws_dev = nullptr;  // no device mapping: reductions copy their result out instead
+        (void)hipGetLastError();
+    }
     if (e != hipSuccess) {
+        if (ctx->red_ws) (void)hipFree(ctx->red_ws);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         delete ctx;
         return MPG_ERR_HIP;
@@ -57,6 +64,7 @@ int mpg_ctx_destroy(mpg_ctx_t ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->red_ws) (void)hipFree(ctx->red_ws);
+    if (ctx->host_ws) (void)hipHostFree(ctx->host_ws);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return MPG_OK;
@@ -64,7 +72,7 @@ int mpg_ctx_destroy(mpg_ctx_t ctx) {
 
 int mpg_ctx_sync(mpg_ctx_t ctx) {
     if (!ctx) return MPG_ERR_ARG;
-    MPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    MPG_HIP(ctx, mpg::spin_wait(ctx->stream));
     return MPG_OK;
 }
 
@@ -104,6 +112,12 @@ int mpg_memset(mpg_ctx_t ctx, void* ptr_dev, int value, size_t bytes) {
 int mpg_memcpy_h2d(mpg_ctx_t ctx, void* dst_dev, const void* src_host, size_t bytes) {
     if (!ctx) return MPG_ERR_ARG;
     if (bytes == 0) return MPG_OK;
+    if (bytes <= mpg::kHostWsBytes && ctx->host_ws) {  // small writes: pinned staging + a polled wait
+        std::memcpy(ctx->host_ws, src_host, bytes);
+        MPG_HIP(ctx, hipMemcpyAsync(dst_dev, ctx->host_ws, bytes, hipMemcpyHostToDevice, ctx->stream));
+        MPG_HIP(ctx, mpg::spin_wait(ctx->stream));
+        return MPG_OK;
+    }
     MPG_HIP(ctx, hipMemcpyAsync(dst_dev, src_host, bytes, hipMemcpyHostToDevice, ctx->stream));
     // The host buffer may be pageable and reused by the caller right away.
     MPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -113,6 +127,12 @@ int mpg_memcpy_h2d(mpg_ctx_t ctx, void* dst_dev, const void* src_host, size_t by
 int mpg_memcpy_d2h(mpg_ctx_t ctx, void* dst_host, const void* src_dev, size_t bytes) {
     if (!ctx) return MPG_ERR_ARG;
     if (bytes == 0) return MPG_OK;
+    if (bytes <= mpg::kHostWsBytes && ctx->host_ws) {  // small reads: pinned staging + a polled wait
+        MPG_HIP(ctx, hipMemcpyAsync(ctx->host_ws, src_dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        MPG_HIP(ctx, mpg::spin_wait(ctx->stream));
+        std::memcpy(dst_host, ctx->host_ws, bytes);
+        return MPG_OK;
+    }
     MPG_HIP(ctx, hipMemcpyAsync(dst_host, src_dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
     MPG_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return MPG_OK;

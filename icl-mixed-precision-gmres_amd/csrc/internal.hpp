@@ -27,6 +27,10 @@ struct mpg_ctx {
     // end wall clock into these slots
     unsigned long long* stamp_next = nullptr;
     int64_t stamp_cap = 0;  // waves the slots hold
+    // pinned host staging of the small device-to-host reads (host-value
+    // reductions, scalar reads of the reference driver), kHostWsBytes
+    void* host_ws = nullptr;
+    void* host_ws_dev = nullptr;  // its device address (stage 2 of host-value reductions stores there)
 };
 
 // Analysed CSR structure (row blocks of the CSR-adaptive schedule).
@@ -60,6 +64,22 @@ constexpr int kQuadGroups = 256;
 inline int quad_groups(int64_t rows) {
     const int64_t g = (rows + 4 * kQuadBlock - 1) / (4 * kQuadBlock);
     return (int)(g < 1 ? 1 : g > kQuadGroups ? kQuadGroups : g);
+}
+
+constexpr size_t kHostWsBytes = 4096;
+
+// Wait for the context's stream on a host read of the solver's critical
+// path (the reference driver's host-value nrm2 / dot and scalar reads,
+// gmres.cpp:160-180 and the per-cycle Scalar::access): poll instead of a
+// blocking synchronise, which measured 30-50 us between the stream draining
+// and the host's next launch per read (rocprofv3 trace of the operator
+// surface, profiles/r06f/); bounded, then the blocking wait.
+inline hipError_t spin_wait(hipStream_t s) {
+    for (int i = 0; i < (1 << 22); ++i) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady) return e;
+    }
+    return hipStreamSynchronize(s);
 }
 
 inline int set_hip_error(mpg_ctx* ctx, hipError_t e, const char* what) {
@@ -197,6 +217,18 @@ __device__ __forceinline__ void mac(float& acc, double a, double b) {
 #pragma clang fp contract(off)
     const float p = (float)(a * b);
     acc = acc + p;
+}
+// y = alpha * t + beta * y_old, the epilogue of every SpMV storage form
+// (CSR tiles, SELL, node blocks) in one rounding order: the two products
+// rounded, then their sum. Left to contraction, the compiler fused one
+// product or the other depending on the kernel around it (node vs CSR bits
+// differed at alpha = -1.5, beta = 0.75 after an unrelated change to the node
+// kernel). The solver's own calls (alpha = +-1, beta in {0, 1}) round once
+// either way.
+template <class X>
+__device__ __forceinline__ X spmv_axpby(X alpha, X t, X beta, X yi) {
+#pragma clang fp contract(off)
+    return beta == X(0) ? alpha * t : alpha * t + beta * yi;
 }
 // acc + p, p an exact fp64 product (the tiles' LDS products), in the class
 __device__ __forceinline__ void add_prod(double& acc, double p) { acc += p; }

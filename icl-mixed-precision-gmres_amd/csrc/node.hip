@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kBlock) void k_node_spmv(const int32_t* __restrict_
         [&](int i) { return beta == X(0) ? X(0) : y[i]; },
         [&](int i, double sum, X yi) {
             const X t = (X)sum;
-            y[i] = beta == X(0) ? alpha * t : alpha * t + beta * yi;
+            y[i] = spmv_axpby(alpha, t, beta, yi);
             if constexpr (NORM) nm.v[i] = sc(x[i]);
         },
         prod);

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv(int n, int cols, int nslic
     }
     if (i < n) {
         const X t = (X)sum;
-        y[i] = beta == X(0) ? alpha * t : alpha * t + beta * yi;
+        y[i] = spmv_axpby(alpha, t, beta, yi);
     }
 }
 
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_spmv2(int n, int cols, int nsli
         const int i = row0 + p * kWave + lane;
         if (live_p[p] && i < n) {
             const X t = (X)sum[p];
-            y[i] = beta == X(0) ? alpha * t : alpha * t + beta * yi[p];
+            y[i] = spmv_axpby(alpha, t, beta, yi[p]);
         }
     }
 }

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_adaptive(const int32_t* __restri
         [&](int i) { return beta == X(0) ? X(0) : y[i]; },
         [&](int i, double sum, X yi) {
             const X t = (X)sum;
-            y[i] = beta == X(0) ? alpha * t : alpha * t + beta * yi;
+            y[i] = spmv_axpby(alpha, t, beta, yi);
         },
         prod, scratch);
 }
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(kBlock) void k_csr_adaptive_scaled(const int32_t* _
         [&](int i) { return Pre{beta == X(0) ? X(0) : y[i], (int)rexp[i]}; },
         [&](int i, double sum, const Pre& p) {
             const X t = (X)ldexp(sum, -p.e);
-            y[i] = beta == X(0) ? alpha * t : alpha * t + beta * p.yi;
+            y[i] = spmv_axpby(alpha, t, beta, p.yi);
         },
         prod, scratch);
 }

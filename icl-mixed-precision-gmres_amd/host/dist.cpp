@@ -54,8 +54,12 @@ void hck(hipError_t e, const char* what) {
 
 // ---------------------------------------------------------------- RCCL
 class RcclComm : public Comm {
-    std::mutex mu_;  // guards comm_ against an abort from another thread
+    std::mutex mu_;  // guards comm_ between the owner's abort and its status queries
     ncclComm_t comm_ = nullptr;
+    // a peer rank failed (request_abort, any thread): the owner's bounded wait
+    // sees it through async_error() and aborts the communicator on its own
+    // thread -- never freed under the owner's enqueues
+    std::atomic<bool> abort_req_{false};
     int rank_, size_;
     mpg_ctx_t ctx_;
     std::vector<int32_t> recv_pos_, recv_cnt_;
@@ -115,18 +119,20 @@ public:
     bool capturable() const override { return true; }
     bool async() const override { return true; }
     std::string async_error() override {
+        if (abort_req_.load()) return "another rank failed (abort requested)";
         std::lock_guard<std::mutex> lk(mu_);
         if (!comm_) return "communicator aborted";
         ncclResult_t r = ncclSuccess;
         if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
         return r == ncclSuccess || r == ncclInProgress ? std::string() : std::string(ncclGetErrorString(r));
     }
-    // idempotent, and callable from another rank's thread (mpg_solve_multi_gpu)
+    // idempotent; the owning rank's thread only (its wait_event)
     void abort() override {
         std::lock_guard<std::mutex> lk(mu_);
         if (comm_) ncclCommAbort(comm_);
         comm_ = nullptr;
     }
+    void request_abort() override { abort_req_.store(true); }
     int transport_ranks() override {
         std::lock_guard<std::mutex> lk(mu_);
         int n = -1;
@@ -724,11 +730,13 @@ int mpg_solve_multi_gpu(const mpg_solve_args* a, int32_t ngpus, const int32_t* d
             return c;
         },
         [&] {
-            // a failed rank: abort every communicator so that peers waiting
-            // on a collective return (their bounded waits then fail too)
+            // a failed rank: every live peer is asked to abort; its bounded
+            // wait (FusedEngine::wait_event) sees the request, aborts its own
+            // communicator on its own thread and fails (aborting
+            // them from here freed communicators their owners were using)
             std::lock_guard<std::mutex> lk(mu);
             for (auto* c : live)
-                if (c) c->abort();
+                if (c) c->request_abort();
         },
         [&](int q) {
             std::lock_guard<std::mutex> lk(mu);

@@ -52,8 +52,12 @@ public:
     virtual bool async() const { return false; }
     // "" or the transport's asynchronous error (ncclCommGetAsyncError)
     virtual std::string async_error() { return {}; }
-    // tear the communicator down so that pending collectives return (ncclCommAbort)
+    // tear the communicator down so that pending collectives return
+    // (ncclCommAbort); called on the owning rank's thread only
     virtual void abort() {}
+    // another rank failed: from any thread, ask the owning rank to abort
+    // (RCCL: a flag its bounded wait polls, then abort() on its own thread)
+    virtual void request_abort() { abort(); }
     // ranks the transport itself reports (RCCL: ncclCommCount), -1 when it
     // cannot say; the caller's size() otherwise
     virtual int transport_ranks() { return size(); }

@@ -290,7 +290,10 @@ private:
         if (!mpg::surface_node_enabled()) return;
         const int64_t alt = sell_->h ? mpg_sell_bytes(sell_->h)
                                      : s_->nnz * (int64_t)(sizeof(Type) + 4) + ((int64_t)s_->m + 1) * 4;
-        mpg::check(mpg_node_create(mpg::current_ctx(), csr(), vt, vals_.data(), alt, &sell_->node), "mpg_node_create");
+        // (an optimisation: a node copy that cannot be allocated leaves the
+        // SELL copy or CSR in place)
+        if (mpg_node_create(mpg::current_ctx(), csr(), vt, vals_.data(), alt, &sell_->node) != MPG_OK)
+            sell_->node = nullptr;
         if (sell_->node && sell_->h) {
             mpg_sell_destroy(sell_->h);
             sell_->h = nullptr;

@@ -76,7 +76,13 @@ def test_accum32_changes_the_arithmetic(mpg):
 def test_accum32_storage_forms_same_bits(mpg, which):
     """The f32 class is one arithmetic in every storage form: products rounded
     to fp32 and added in CSR order on SELL, node blocks and CSR row blocks
-    (mac / add_prod, internal.hpp), so the three give one another's bits."""
+    (mac / add_prod, internal.hpp), so the Arnoldi SpMVs give one another's
+    bits. Node blocks and CSR agree over the whole solve; SELL over cycle 0
+    (x0 = 0, so its residual is b in any order): from the first restart on,
+    the fp64 residual prologue differs -- SELL's fp64 row sums contract to
+    fused multiply-adds of fp64 products, the CSR tile adds the products it
+    staged in LDS (the same in accum f64, tools/accum_forms_diag.py,
+    profiles/r06_accum/forms.jsonl)."""
     if which == "stencil27p":
         A = mpg.gen_stencil27p(40, 3, ny=40, nz=8, block=64, perm_seed=5)
     else:
@@ -85,9 +91,9 @@ def test_accum32_storage_forms_same_bits(mpg, which):
     b = mpg.host_spmv(A, xt)
     opts = dict(mode="mixed", orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3)
     got = {f: _solve32(mpg, A, b, xt, spmv_format=f, **opts) for f in ("csr", "sell", "node")}
-    for f in ("sell", "node"):
-        np.testing.assert_array_equal(got[f].step_res, got["csr"].step_res, err_msg=f)
-        np.testing.assert_array_equal(got[f].x, got["csr"].x, err_msg=f)
+    np.testing.assert_array_equal(got["node"].step_res, got["csr"].step_res)
+    np.testing.assert_array_equal(got["node"].x, got["csr"].x)
+    np.testing.assert_array_equal(got["sell"].step_res[:30], got["csr"].step_res[:30])
 
 
 _MKL = {}
