@@ -222,32 +222,50 @@ def phase_roofline(eng, rlen: int, reps: int, traffic: dict) -> dict:
     return out
 
 
+def pair_rate(mpg, A, b, xt, o, cycles: int):
+    """(iterations/s, whole-solve iterations/s, the three pair rates) of
+    mpg.solve with options o: two solves of 4 and 4 + `cycles` restart
+    cycles, the difference of their GMRES iterations over the difference of
+    their GMRES times (so the first cycle's lazy set-up cancels), median of
+    three such pairs (one pair moved +-4 % between runs of one box), after a
+    2-cycle warm-up solve (the process's first solve of an engine also pays
+    one-time code-object loads)."""
+    mpg.solve(A, b, xt, **dict(o, max_restarts=2))
+    rates, wholes = [], []
+    for _ in range(3):
+        runs = []
+        for r in (4, 4 + cycles):
+            res = mpg.solve(A, b, xt, **dict(o, max_restarts=r))
+            runs.append((res.total_iters, res.gmres_seconds))
+        rates.append((runs[1][0] - runs[0][0]) / (runs[1][1] - runs[0][1]))
+        wholes.append(runs[1][0] / runs[1][1])
+    return sorted(rates)[1], sorted(wholes)[1], rates
+
+
 def surface_rate(mpg, A, b, xt, opts, cycles: int, fused_rate: float) -> dict:
     """The same solve through the drop-in boundary north_star names: the
     reference's driver (gmres_singleUpdate / gmres_baseline, restated in
     host/gmres_impl.hpp) over the kernels.hpp operator surface of
-    kernels_hip.cpp (mpg_solve, engine surface). Two solves of 4 and 4 +
-    `cycles` restart cycles; the rate is the difference of their GMRES
-    iterations over the difference of their GMRES times, so the first
-    cycle's lazy set-up (SELL copy, cycle recording) cancels. A 2-cycle
-    warm-up solve runs first: the process's first surface solve also pays
-    one-time costs (code-object loads on each kernel's first launch) that a
-    later solve does not, which would shrink the difference of the times."""
-    # (the operator surface's kernels sum in fp64: its accumulation class is f64)
+    kernels_hip.cpp (mpg_solve, engine surface), timed by pair_rate.
+    The surface's kernels sum in fp64 (accumulation class f64), so beside
+    vs_fused (against the headline line, whose class is the bench's --accum)
+    the fused engine is timed the same way in the f64 class: vs_fused_f64 is
+    the surface against the fused engine doing the same arithmetic."""
     o = {k: v for k, v in opts.items() if k not in ("spmv_format", "accum")}
-    mpg.solve(A, b, xt, engine="surface", **dict(o, max_restarts=2))
-    runs = []
-    for r in (4, 4 + cycles):
-        res = mpg.solve(A, b, xt, engine="surface", **dict(o, max_restarts=r))
-        runs.append((res.total_iters, res.gmres_seconds))
-    rate = (runs[1][0] - runs[0][0]) / (runs[1][1] - runs[0][1])
-    whole = runs[1][0] / runs[1][1]
-    log(f"[bench] operator surface: {rate:.0f} it/s ({rate / fused_rate:.3f} of the fused engine); "
+    rate, whole, rates = pair_rate(mpg, A, b, xt, dict(o, engine="surface"), cycles)
+    f64, _, f64_rates = pair_rate(mpg, A, b, xt, dict(o, engine="fused", accum="f64"), cycles)
+    log(f"[bench] operator surface: {rate:.0f} it/s ({rate / fused_rate:.3f} of the fused engine, "
+        f"{rate / f64:.3f} of the fused engine in the f64 class, {f64:.0f} it/s); "
         f"{whole:.0f} it/s over the whole {4 + cycles}-cycle solve")
     return {"iters_per_s": round(rate, 2), "vs_fused": round(rate / fused_rate, 4),
+            "fused_f64_iters_per_s": round(f64, 2), "vs_fused_f64": round(rate / f64, 4),
             "whole_solve_iters_per_s": round(whole, 2),
+            "pairs_iters_per_s": [round(v, 2) for v in rates],
+            "fused_f64_pairs_iters_per_s": [round(v, 2) for v in f64_rates],
             "how": f"mpg_solve engine=surface (gmres.cpp's driver over kernels_hip.cpp), after a 2-cycle warm-up "
-                   f"solve: (iters, time) of a {4 + cycles}-cycle solve minus a 4-cycle solve"}
+                   f"solve: (iters, time) of a {4 + cycles}-cycle solve minus a 4-cycle solve, median of 3 pairs; "
+                   f"vs_fused against the headline rate, vs_fused_f64 against the fused engine timed the same way "
+                   f"in the surface's accumulation class (f64)"}
 
 
 def cpu_baseline(mpg, A, b, xt, opts, args, world=1, workload="BAND-10M", solve=None):

@@ -36,9 +36,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_stage1(int64_t n, const T* __
 // (k_gemv_n_quad<..., NORM>, blas2.hip) emits the ||y||^2 partials of the y
 // it writes, so both give the same partials for the same vector
 template <class T>
-__global__ __launch_bounds__(kQuadBlock) void k_nrm2_quad(int64_t n, const T* __restrict__ x,
-                                                          double* __restrict__ partial) {
-    __shared__ double scratch[kQuadBlock / kWave];
+__device__ __forceinline__ double nrm2_quad_partial(int64_t n, const T* __restrict__ x, double* scratch) {
     double acc = 0.0;
     const int64_t n4 = n & ~int64_t(3);
     const int64_t step = 4 * (int64_t)gridDim.x * kQuadBlock;
@@ -52,8 +50,53 @@ __global__ __launch_bounds__(kQuadBlock) void k_nrm2_quad(int64_t n, const T* __
         const double a = (double)x[i];
         acc += a * a;
     }
-    const double s = block_sum<kQuadBlock>(acc, scratch);
+    return block_sum<kQuadBlock>(acc, scratch);
+}
+
+template <class T>
+__global__ __launch_bounds__(kQuadBlock) void k_nrm2_quad(int64_t n, const T* __restrict__ x,
+                                                          double* __restrict__ partial) {
+    __shared__ double scratch[kQuadBlock / kWave];
+    const double s = nrm2_quad_partial(n, x, scratch);
     if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+// A host-value nrm2 on a 16-B aligned vector in ONE launch (the operator
+// surface's per-cycle r_norm / beta / ||x|| reads, gmres.cpp:173-196): the
+// stage 1 of k_nrm2_quad, then the last workgroup to finish (a device-scope
+// ticket, zeroed at context creation and reset by that workgroup) sums the
+// partials with k_reduce_stage2's block_sum<1024> over the same 1024 lanes --
+// the bits of the two launches -- and stores sqrt into the context's pinned
+// host word. The hand-off is the guide's write-through form
+// (cdna_hip_programming.md, in-launch split-K reduction): each partial is an
+// sc1 (agent-scope relaxed atomic) store, waited for, before a relaxed
+// agent-scope ticket add; the last arriver reads the partials with sc1 loads.
+// No __threadfence: an agent release writes back the XCD's whole L2, in
+// every workgroup (12.4 us per launch with it, profiles/r06n/).
+template <class T>
+__global__ __launch_bounds__(kQuadBlock) void k_nrm2_quad_host(int64_t n, const T* __restrict__ x,
+                                                               double* __restrict__ partial,
+                                                               unsigned* __restrict__ ticket,
+                                                               T* __restrict__ result_host) {
+    static_assert(kQuadBlock == 1024, "the last workgroup runs stage 2's 1024-lane sum");
+    __shared__ double scratch[kQuadBlock / kWave];
+    __shared__ unsigned arrived;
+    const double s = nrm2_quad_partial(n, x, scratch);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(partial + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial written through before the ticket
+        arrived = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (arrived != gridDim.x - 1) return;
+    const double v = threadIdx.x < gridDim.x
+                         ? __hip_atomic_load(partial + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : 0.0;
+    const double t = block_sum<1024>(v, scratch);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(result_host, (T)sqrt(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 template <class T, bool SQRT>
@@ -66,18 +109,17 @@ __global__ __launch_bounds__(1024) void k_reduce_stage2(int nparts, const double
 }
 
 // Stage 2 of a host-value reduction, storing straight into the context's
-// pinned host word (no copy command behind it): the same sum, then a
-// system-scope fence so the host's read after the stream completes sees it.
+// pinned host word (no copy command behind it): the same sum, stored
+// write-through at system scope (no L2 write-back fence), so the host's
+// read after the stream completes sees it.
 template <class T, bool SQRT>
 __global__ __launch_bounds__(1024) void k_reduce_stage2_host(int nparts, const double* __restrict__ partial,
                                                              T* __restrict__ result_host) {
     __shared__ double scratch[1024 / kWave];
     double v = threadIdx.x < nparts ? partial[threadIdx.x] : 0.0;
     double s = block_sum<1024>(v, scratch);
-    if (threadIdx.x == 0) {
-        *result_host = SQRT ? (T)sqrt(s) : (T)s;
-        __threadfence_system();
-    }
+    if (threadIdx.x == 0)
+        __hip_atomic_store(result_host, SQRT ? (T)sqrt(s) : (T)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Stage 2 folded into the consumer of the result (the operator surface's
@@ -152,6 +194,14 @@ int reduce(mpg_ctx* ctx, int64_t n, const T* x, const T* y, T* result_dev) {
 template <class T, bool SQUARE>
 int reduce_host(mpg_ctx* ctx, int64_t n, const T* x, const T* y, T* result_host) {
     if (!result_host) return MPG_ERR_ARG;
+    if (SQUARE && ctx && ctx->host_ws_dev && ctx->ticket && n > 0 && (uintptr_t)x % 16 == 0) {
+        k_nrm2_quad_host<T><<<quad_groups(n), kQuadBlock, 0, ctx->stream>>>(n, x, ctx->red_ws, ctx->ticket,
+                                                                           (T*)ctx->host_ws_dev);
+        MPG_LAUNCH_CHECK(ctx);
+        MPG_HIP(ctx, mpg::spin_wait(ctx->stream));
+        *result_host = *static_cast<volatile T*>(ctx->host_ws);
+        return MPG_OK;
+    }
     if (ctx && ctx->host_ws_dev) {  // stage 2 stores into pinned host memory; a polled wait
         int32_t g = 0;
         if (int st = reduce_partials<T, SQUARE>(ctx, n, x, y, &g)) return st;

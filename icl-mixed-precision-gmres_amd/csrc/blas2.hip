@@ -157,9 +157,11 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_t_quad(int64_t rows, const 
     double acc[NP];
 #pragma unroll
     for (int c = 0; c < NP; ++c) acc[c] = 0.0;
-    const int64_t n4 = rows & ~int64_t(3);
-    const int64_t step = 4 * (int64_t)gridDim.x * kQuadBlock;
-    for (int64_t i = 4 * ((int64_t)blockIdx.x * kQuadBlock + threadIdx.x); i < n4; i += step) {
+    // 32-bit row indices (rows < kQuadMaxRows, quad_aligned), as the fused
+    // engine's panel kernels: the 64-bit loop cost ~0.7 us per launch
+    const int n4 = (int)rows & ~3;
+    const int step = 4 * (int)gridDim.x * kQuadBlock;
+    for (int i = 4 * ((int)blockIdx.x * kQuadBlock + (int)threadIdx.x); i < n4; i += step) {
         double xv[4];
         Row4<T>::load(x + i, xv);
 #pragma unroll
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_t_quad(int64_t rows, const 
                 if (c0 + u < NC) acc[c0 + u] += v[u][0] * xv[0] + v[u][1] * xv[1] + v[u][2] * xv[2] + v[u][3] * xv[3];
         }
     }
-    for (int64_t i = n4 + (int64_t)blockIdx.x * kQuadBlock + threadIdx.x; i < rows; i += (int64_t)gridDim.x * kQuadBlock) {
+    for (int i = n4 + (int)blockIdx.x * kQuadBlock + (int)threadIdx.x; i < (int)rows; i += (int)gridDim.x * kQuadBlock) {
         const double xi = (double)x[i];
 #pragma unroll
         for (int c = 0; c < NC; ++c) acc[c] += (double)A[(int64_t)c * lda + i] * xi;
@@ -217,9 +219,9 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_n_quad(int64_t rows, T alph
         if (threadIdx.x < NC) xs[threadIdx.x] = (double)x[threadIdx.x];
     }
     __syncthreads();
-    const int64_t n4 = rows & ~int64_t(3);
-    const int64_t step = 4 * (int64_t)gridDim.x * kQuadBlock;
-    for (int64_t i = 4 * ((int64_t)blockIdx.x * kQuadBlock + threadIdx.x); i < n4; i += step) {
+    const int n4 = (int)rows & ~3;  // (32-bit row indices, as k_gemv_t_quad)
+    const int step = 4 * (int)gridDim.x * kQuadBlock;
+    for (int i = 4 * ((int)blockIdx.x * kQuadBlock + (int)threadIdx.x); i < n4; i += step) {
         Raw4<T> yr;
         if (beta != T(0)) yr.load(y + i);
         double t[4] = {0.0, 0.0, 0.0, 0.0};
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_n_quad(int64_t rows, T alph
             }
         }
     }
-    for (int64_t i = n4 + (int64_t)blockIdx.x * kQuadBlock + threadIdx.x; i < rows; i += (int64_t)gridDim.x * kQuadBlock) {
+    for (int i = n4 + (int)blockIdx.x * kQuadBlock + (int)threadIdx.x; i < (int)rows; i += (int)gridDim.x * kQuadBlock) {
         double t = 0.0;
 #pragma unroll
         for (int c = 0; c < NC; ++c) t += (double)A[(int64_t)c * lda + i] * xs[c];
@@ -269,9 +271,13 @@ __global__ __launch_bounds__(kQuadBlock) void k_gemv_n_quad(int64_t rows, T alph
     }
 }
 
+// the quad kernels index rows with 32-bit integers
+constexpr int64_t kQuadMaxRows = int64_t(1) << 30;
+
 template <class T>
-bool quad_aligned(const T* A, int64_t lda, const T* v) {
-    return ((uintptr_t)A % 16 == 0) && ((uintptr_t)v % 16 == 0) && ((lda * (int64_t)sizeof(T)) % 16 == 0);
+bool quad_aligned(const T* A, int64_t lda, const T* v, int64_t rows) {
+    return ((uintptr_t)A % 16 == 0) && ((uintptr_t)v % 16 == 0) && ((lda * (int64_t)sizeof(T)) % 16 == 0) &&
+           rows < kQuadMaxRows;
 }
 
 // f(integral_constant<int, nc>) for 1 <= nc <= N
@@ -318,7 +324,7 @@ int gemv_impl(mpg_ctx* ctx, int trans, int64_t rows, int64_t cols, T alpha, cons
     if (!ctx || rows < 0 || cols < 0 || (cols > 0 && lda < (rows > 0 ? rows : 1))) return MPG_ERR_ARG;
     if (!trans) {
         if (rows == 0) return MPG_OK;
-        if (cols >= 1 && cols <= kGemvMaxCols && quad_aligned(A, lda, y)) {
+        if (cols >= 1 && cols <= kGemvMaxCols && quad_aligned(A, lda, y, rows)) {
             const int g = (int)std::min<int64_t>(kQuadGroups, (rows + 4 * kQuadBlock - 1) / (4 * kQuadBlock));
             const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto nc) {
                 k_gemv_n_quad<T, decltype(nc)::value><<<g, kQuadBlock, 0, ctx->stream>>>(
@@ -340,7 +346,7 @@ int gemv_impl(mpg_ctx* ctx, int trans, int64_t rows, int64_t cols, T alpha, cons
         return MPG_OK;
     }
     if (cols == 0) return MPG_OK;
-    const bool quad = quad_aligned(A, lda, x);
+    const bool quad = quad_aligned(A, lda, x, rows);
     int g = quad ? (int)std::max<int64_t>(1, std::min<int64_t>(kQuadGroups, (rows + 4 * kQuadBlock - 1) / (4 * kQuadBlock)))
                  : grid_for(rows, 4, kMaxRedBlocks);
     for (int64_t c0 = 0; c0 < cols; c0 += kGemvMaxCols) {
@@ -368,7 +374,7 @@ template <class T>
 int gemv_t_partials(mpg_ctx* ctx, int64_t rows, int64_t cols, const T* A, int64_t lda, const T* x, int32_t* nparts) {
     if (!ctx || !nparts || rows < 0 || cols < 1 || (rows > 0 && lda < rows)) return MPG_ERR_ARG;
     if (cols > kGemvMaxCols) return MPG_ERR_UNSUPPORTED;
-    const bool quad = quad_aligned(A, lda, x);
+    const bool quad = quad_aligned(A, lda, x, rows);
     const int g = quad ? (int)std::max<int64_t>(1, std::min<int64_t>(kQuadGroups, (rows + 4 * kQuadBlock - 1) /
                                                                                     (4 * kQuadBlock)))
                        : grid_for(rows, 4, kMaxRedBlocks);
@@ -402,7 +408,7 @@ int gemv_n_from_t(mpg_ctx* ctx, int64_t rows, int64_t cols, T alpha, const T* A,
                   T alpha_t, T* x, T beta, T* y, int32_t* norm_nparts = nullptr, T* y_out = nullptr) {
     if (!ctx || rows < 0 || cols < 1 || nparts < 1 || (rows > 0 && lda < rows)) return MPG_ERR_ARG;
     if (y_out && (!norm_nparts || (y_out < y + rows && y < y_out + rows))) return MPG_ERR_ARG;
-    if (cols > kGemvMaxCols || !quad_aligned(A, lda, y) || (y_out && (uintptr_t)y_out % 16)) return MPG_ERR_UNSUPPORTED;
+    if (cols > kGemvMaxCols || !quad_aligned(A, lda, y, rows) || (y_out && (uintptr_t)y_out % 16)) return MPG_ERR_UNSUPPORTED;
     if (norm_nparts && rows < 1) return MPG_ERR_UNSUPPORTED;
     const int g = quad_groups(rows);
     const int st = with_cols<kGemvMaxCols>((int)cols, [&](auto nc) {

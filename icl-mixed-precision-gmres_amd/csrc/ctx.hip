@@ -45,11 +45,15 @@ int mpg_ctx_create(int device, mpg_ctx_t* out) {
         e = hipMalloc(&ctx->red_ws, ctx->red_ws_elems * sizeof(double));
     }
     if (e == hipSuccess) e = hipHostMalloc(&ctx->host_ws, mpg::kHostWsBytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->ticket, 256);
+    if (e == hipSuccess) e = hipMemsetAsync(ctx->ticket, 0, 256, ctx->stream);
     if (e == hipSuccess && hipHostGetDevicePointer(&ctx->host_ws_dev, ctx->host_ws, 0) != hipSuccess) {
         ctx->host_ws_dev = nullptr;  // no device mapping: reductions copy their result out instead
         (void)hipGetLastError();
     }
     if (e != hipSuccess) {
+        if (ctx->ticket) (void)hipFree(ctx->ticket);
+        if (ctx->host_ws) (void)hipHostFree(ctx->host_ws);
         if (ctx->red_ws) (void)hipFree(ctx->red_ws);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         delete ctx;
@@ -65,6 +69,7 @@ int mpg_ctx_destroy(mpg_ctx_t ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->red_ws) (void)hipFree(ctx->red_ws);
     if (ctx->host_ws) (void)hipHostFree(ctx->host_ws);
+    if (ctx->ticket) (void)hipFree(ctx->ticket);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return MPG_OK;

@@ -31,6 +31,7 @@ struct mpg_ctx {
     // reductions, scalar reads of the reference driver), kHostWsBytes
     void* host_ws = nullptr;
     void* host_ws_dev = nullptr;  // its device address (stage 2 of host-value reductions stores there)
+    unsigned* ticket = nullptr;   // zeroed device word: last-workgroup ticket of one-launch reductions
 };
 
 // Analysed CSR structure (row blocks of the CSR-adaptive schedule).

@@ -125,7 +125,9 @@ void gmres_baseline(Convergence<Type, Device>& convergence, SparseMatrix<Type, D
                     copy(s(j + 1), rlog.buf(j));
                 }
             });
-            Device::fence();
+            // (no fence: to_host is ordered after the cycle on the stream and
+            // waits for it; a fence first would leave the read's copy to start
+            // on an idle queue after the host saw the cycle end)
             std::vector<Type> res(m);
             Device::to_host(res.data(), rlog.buf.data(), m * sizeof(Type));
             for (size_t j = 0; j < m; ++j) {
@@ -228,8 +230,7 @@ void gmres_singleUpdate(Convergence<float, Device>& convergence, SparseMatrix<do
                     copy(s(j + 1), rlog.buf(j));
                 }
             });
-            Device::fence();
-            std::vector<float> res(m);
+            std::vector<float> res(m);  // (to_host waits for the cycle: no fence)
             Device::to_host(res.data(), rlog.buf.data(), m * sizeof(float));
             for (size_t j = 0; j < m; ++j) {
                 const iteration_action a = convergence.check(j + 1, std::fabs(double(res[j])), Minvb_norm);

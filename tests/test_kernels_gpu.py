@@ -68,6 +68,17 @@ def test_dot_nrm2(hip, oracle, n, t):
     hv = (C.c_double if t == "f64" else C.c_float)()
     hip.call(f"mpg_dot_{t}_host", n, dx.p, dy.p, C.byref(hv))
     assert dt(hv.value) == got[0]
+    # nrm2 to the host: one launch on a 16-B aligned vector (last-workgroup
+    # ticket, result stored into pinned memory), repeated so the ticket's
+    # reset is exercised; the two-launch form on a vector that is not aligned
+    for _ in range(3):
+        hv.value = -1
+        hip.call(f"mpg_nrm2_{t}_host", n, dx.p, C.byref(hv))
+        assert dt(hv.value) == got[1]
+    if n > 1:
+        hip.call(f"mpg_nrm2_{t}", n - 1, dx.at(1), out.at(1))
+        hip.call(f"mpg_nrm2_{t}_host", n - 1, dx.at(1), C.byref(hv))
+        assert dt(hv.value) == out.get()[1]
 
 
 @pytest.mark.parametrize("t", ["f64", "f32"])
