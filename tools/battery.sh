@@ -12,9 +12,11 @@
 #   irr      irregular SpMV A/B (c4p, fem27, fem27p; auto / csr / sell)
 #   irrpmc   FETCH_SIZE, WRITE_SIZE and TCC hit/miss passes of the irregular SpMVs
 #   c4pmc    FETCH_SIZE and TCC hit/miss passes of C4's stepped SpMV
+#   lappmc   FETCH_SIZE, WRITE_SIZE and TCC hit/miss passes of LAP-1M's SpMV
 #   n2       bench --gpus 2 rehearsal with both ranks on GPU 0 (gloo host transport)
 #   node     node-block SpMV A/B (tiles per workgroup, XCD order) on the 3-dof stand-ins
 #   ranks    C4 / C5 rank blocks at P = 8 (tools/rank_blocks.py), and C4's under PMC
+#   surfirr  the operator surface against the fused engine on fem27 and C4's stencil (node blocks)
 set -u
 tag=${1:?usage: tools/battery.sh TAG step...}
 shift
@@ -41,8 +43,14 @@ for s in "$@"; do
               cmds+=("${tag}_${c}_w|200|timeout -s KILL 190 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${tag}_irrpmc/${c}_write -o write -- python3 tools/spmv_ab.py --case $c --var spmv_format=auto --reps 1 --cycles 1")
               cmds+=("${tag}_${c}_h|200|timeout -s KILL 190 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/${tag}_irrpmc/${c}_hit -o hit -- python3 tools/spmv_ab.py --case $c --var spmv_format=auto --reps 1 --cycles 1")
             done ;;
+    lappmc) for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "TCC_HIT_sum TCC_MISS_sum:hit"; do
+              cmds+=("${tag}_lap_${pass##*:}|200|timeout -s KILL 190 rocprofv3 --pmc ${pass%%:*} --output-format csv -d gpurun_out/${tag}_lappmc/${pass##*:} -o ${pass##*:} -- python3 tools/spmv_ab.py --case lap1m --var spmv_format=auto --reps 1 --cycles 1")
+            done ;;
     c4pmc) cmds+=("${tag}_c4f|200|timeout -s KILL 190 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${tag}_c4pmc/fetch -o fetch -- python3 tools/spmv_ab.py --case c4 --var spmv_format=auto --reps 1 --cycles 1")
            cmds+=("${tag}_c4h|200|timeout -s KILL 190 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/${tag}_c4pmc/hit -o hit -- python3 tools/spmv_ab.py --case c4 --var spmv_format=auto --reps 1 --cycles 1") ;;
+    surfirr) for sp in fem27:111 stencil27:111; do
+               cmds+=("${tag}_surf_${sp%%:*}|400|python -u tools/surface_vs_fused.py cgs --spec=$sp --cycles=10")
+             done ;;
     n2) cmds+=("${tag}_n2|400|MPG_BENCH_SHARED_GPU=1 python -u bench.py --gpus 2 --steps 5 --warmup 1 > gpurun_out/${tag}_bench_n2.json") ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac

@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--cpu-cycles", type=int, default=2)
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="comma-separated case prefixes, e.g. C4,C5")
+    ap.add_argument("--accum", default="f32", choices=["f64", "f32"],
+                    help="accumulation class of the fp32 Arnoldi (bench.py's default: f32, the reference's)")
     args = ap.parse_args()
     from __graft_entry__ import _load
 
@@ -80,7 +82,8 @@ def main():
         b = mpg.host_spmv(A, xt)
         opts = dict(mode=case["mode"], orth=case["orth"], prec="identity", rlen=rlen, tol=0.0,
                     max_restarts=cycles + 10)
-        eng = mpg.Engine(A, b, xt, **opts)
+        eng = mpg.Engine(A, b, xt, accum=args.accum, **opts)
+        accum = eng.spmv_layout()["accum"]
         eng.run(2)
         eng.sync()
         it0 = eng.total_iters
@@ -120,7 +123,7 @@ def main():
             cpu = {"it_s": round(r.total_iters / r.gmres_seconds, 2), "iterations": int(r.total_iters),
                    "mode": cmode, "threads": binding.lib().oracle_max_threads(), "backend": binding.backend()}
         line = {"case": case["name"], "spec": case["spec"], "rlen": rlen, "n": A.nrows, "nnz": A.nnz,
-                "mode": case["mode"], "orth": case["orth"], "phases_graph": phases,
+                "mode": case["mode"], "orth": case["orth"], "accum": accum, "phases_graph": phases,
                 "gmres_it_s": round(its, 1), "spmv_us": round(spmv_ms * 1e3, 2), "spmv_gbs": round(gbs, 1),
                 "spmv_frac_8tbs": round(gbs / 8000, 3), "spmv_storage_gbs": round(gbs_storage, 1),
                 "spmv_storage_frac_8tbs": round(gbs_storage / 8000, 3), "spmv_timing": "in-cycle kernel events",

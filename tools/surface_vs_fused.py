@@ -2,7 +2,9 @@
 flow over kernels_hip.cpp) against the fused engine on BAND-1M (or --spec, a
 generator spec as the CLI's, e.g. fem27:111), mixed GMRES(30), --cycles
 restart cycles per solve (default 20) after a 1-cycle warm-up solve;
-gmres_seconds times the whole solve (set-up of the cycle program included).
+gmres_seconds times the whole solve (set-up of the cycle program included);
+"steady" is bench.py's form: the difference of a (2 + cycles)- and a
+2-cycle solve, median of three pairs, so one-time set-up cancels.
 
 usage: python tools/surface_vs_fused.py [orth ...] [--engines=surface,fused] [--cycles=N] [--spec=SPEC]"""
 import sys
@@ -38,8 +40,16 @@ def main():
             opts = dict(engine=eng, mode="mixed", orth=orth, prec="identity", rlen=30, tol=0.0)
             mpg.solve(A, b, xt, max_restarts=1, **opts)
             r = mpg.solve(A, b, xt, max_restarts=cycles, **opts)
+            # steady state as bench.py's surface figure: (iters, time) of a
+            # (2 + cycles)-cycle solve minus a 2-cycle solve, median of 3
+            pairs = []
+            for _ in range(3):
+                r2 = mpg.solve(A, b, xt, max_restarts=2, **opts)
+                rn = mpg.solve(A, b, xt, max_restarts=2 + cycles, **opts)
+                pairs.append((rn.total_iters - r2.total_iters) / (rn.gmres_seconds - r2.gmres_seconds))
             print(spec or "band1m", orth, eng, r.total_iters, "iters", round(r.gmres_seconds, 4), "s",
-                  round(r.total_iters / r.gmres_seconds, 1), "it/s", flush=True)
+                  round(r.total_iters / r.gmres_seconds, 1), "it/s whole solve;", round(sorted(pairs)[1], 1),
+                  "it/s steady (pairs", [round(v, 1) for v in pairs], ")", flush=True)
 
 
 if __name__ == "__main__":
