@@ -198,7 +198,8 @@ __global__ __launch_bounds__(kBlock) void k_node_spmv(const int32_t* __restrict_
         --G;
     }
     X a = X(1);
-    if constexpr (NORM) a = norm_scale(nm, pv);
+    __shared__ double nscratch[NORM ? kBlock / kWave : 1];
+    __shared__ X a_s;
     const int g = xcd ? xcd_block(b, G) : b;
     const int t0 = g * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
     auto sc = [&](X v) { return NORM ? (X)(a * v) : v; };
@@ -211,7 +212,10 @@ __global__ __launch_bounds__(kBlock) void k_node_spmv(const int32_t* __restrict_
             y[i] = spmv_axpby(alpha, t, beta, yi);
             if constexpr (NORM) nm.v[i] = sc(x[i]);
         },
-        prod);
+        prod, [&] {
+            // the scale, formed while the first tile's gathers are in flight
+            if constexpr (NORM) a = norm_scale_lds(nm, pv, nscratch, &a_s);
+        });
 }
 
 }  // namespace

@@ -176,11 +176,17 @@ __device__ __forceinline__ void node_tile(int t, const int32_t* __restrict__ til
 // (Issuing the next tile's gathers before this tile's row sums and
 // converting them after was slower: fem27 211 -> 231 us, C4 301 -> 327,
 // stencil27p 347 -> 357; profiles/r05_node_ab.jsonl.)
-template <class VI, class A = double, class XR, class XF, class PF, class EPI>
+// first(): called by every thread once, after the first tile's raw gathers
+// are issued and before xfin is applied to them (k_node_spmv's riding
+// normalisation forms its scale there, under the gathers' latency).
+struct NoFirst {
+    __device__ __forceinline__ void operator()() const {}
+};
+template <class VI, class A = double, class XR, class XF, class PF, class EPI, class FIRST = NoFirst>
 __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __restrict__ tiles,
                                            const int32_t* __restrict__ tb0, const int32_t* __restrict__ bptr,
                                            const char* __restrict__ recs, int64_t nblk, XR xraw, XF xfin, PF pre,
-                                           EPI epi, double* __restrict__ prod) {
+                                           EPI epi, double* __restrict__ prod, FIRST first = FIRST{}) {
     constexpr int R = NodeRec<VI>::R;
     const int l = threadIdx.x;
     auto rec = [&](int t) {
@@ -200,7 +206,9 @@ __device__ __forceinline__ void node_tiles(int t0, int t1, const int32_t* __rest
         const int fa = bptr[nf] - b0, fz = bptr[nf + 1] - b0;
         const auto pf = pre(kNodeDof * nr0 + rf);
         const int c = cur.col();
-        const double x0 = xfin(xraw(c)), x1 = xfin(xraw(c + 1)), x2 = xfin(xraw(c + 2));
+        const auto r0 = xraw(c), r1 = xraw(c + 1), r2 = xraw(c + 2);
+        if (t == t0) first();
+        const double x0 = xfin(r0), x1 = xfin(r1), x2 = xfin(r2);
         if (t + 1 < t1) nxt.load(rec(t + 1));
         if (l < nb) {
             double* p = prod + l * (kNodeDof * kNodeDof);

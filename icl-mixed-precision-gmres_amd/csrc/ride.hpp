@@ -46,4 +46,32 @@ __device__ __forceinline__ X norm_scale(const NormArgs<X>& nm, double pv) {
     return a_s;
 }
 
+// norm_scale with LDS-only barriers (lds_barrier), for a kernel that has
+// issued global loads it does not want drained yet (k_node_spmv: the first
+// tile's records and raw x gathers are in flight while the workgroup sums the
+// partials; a __syncthreads would wait for them first -- C4's node SpMV ran
+// 360 us with the plain form against 290 us without the ride). The same
+// block_sum<kBlock> order (wave sums, then thread 0 adds them in wave
+// order), the same bits. scratch: kBlock / kWave doubles; a_s: one X.
+template <class X>
+__device__ __forceinline__ X norm_scale_lds(const NormArgs<X>& nm, double pv, double* scratch, X* a_s) {
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const double v = wave_sum(pv);
+    if (lane == 0) scratch[wid] = v;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+        double s = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / kWave; ++w) s += scratch[w];
+        const X r = (X)sqrt(s);
+        if (blockIdx.x == 0) {
+            *nm.h = r;
+            __threadfence();  // the riding program reads h(k+1,k)
+        }
+        *a_s = X(1) / r;
+    }
+    lds_barrier();
+    return *a_s;
+}
+
 }  // namespace mpg
