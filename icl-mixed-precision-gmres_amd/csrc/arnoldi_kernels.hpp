@@ -1058,6 +1058,10 @@ __device__ __forceinline__ void dots_panel(int n, const T* __restrict__ V, int64
                 if (c0 + u < NC)
                     acc[c0 + u] += v[u].template at<A>(0) * wv[0] + v[u].template at<A>(1) * wv[1] +
                                    v[u].template at<A>(2) * wv[2] + v[u].template at<A>(3) * wv[3];
+            // the next batch's loads after this batch's adds: without it the
+            // fp32 class's NC = 32 form issued all 32 columns' loads first
+            // (128 VGPRs, 180 B of scratch per lane)
+            asm volatile("" : "+v"(acc[c0]) : : "memory");
         }
     }
     for (int i = n4 + blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {

@@ -389,6 +389,22 @@ bool take_ride(const void* x, const void* y, int64_t n, bool f64, mpg_scalar_op*
     return true;
 }
 
+// A node SpMV with more than kNodeNormRideGroups workgroups does not take
+// add_vector's normalisation: every workgroup of the riding form re-sums the
+// ||w||^2 partials and stores its rows of V(:,k+1), which at C4's size (71k
+// workgroups) cost 342 us per launch against 296 us plain
+// (profiles/r06_irr_pmc/), more than the separate scal_recip launch. The
+// first such SpMV of a solve turns the redirect off for the rest of the
+// scope, so the CGS gemv writes w itself again (no copy back).
+constexpr int32_t kNodeNormRideGroups = 4096;
+bool node_takes_norm_ride(mpg_node_t nd) {
+    int32_t tiles = 0;
+    if (mpg_node_layout(nd, nullptr, &tiles, nullptr, nullptr) != MPG_OK) return false;
+    if ((tiles + 1) / 2 <= kNodeNormRideGroups) return true;
+    tl_ride_score = 0;
+    return false;
+}
+
 mpg_ctx_t current_ctx() {
     tl_norm.y = nullptr;
     flush_ride();
@@ -905,7 +921,7 @@ template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Ve
         int32_t np = 0;
         void* h = nullptr;
         const void* w = nullptr;
-        if (beta == double(0) && x.n() == y.n() &&
+        if (beta == double(0) && x.n() == y.n() && (!nd || mpg::node_takes_norm_ride(nd)) &&
             mpg::take_ride(x.data(), y.data(), (int64_t)x.n(), true, ops, nops, c, np, h, w)) {
             check(nd ? mpg_node_spmv_norm_f64(c, nd, np, static_cast<double*>(h), static_cast<const double*>(w), x.data(),
                                                alpha, y.data(), ops, nops)
@@ -947,7 +963,7 @@ template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<
         int32_t np = 0;
         void* h = nullptr;
         const void* w = nullptr;
-        if (beta == float(0) && x.n() == y.n() &&
+        if (beta == float(0) && x.n() == y.n() && (!nd || mpg::node_takes_norm_ride(nd)) &&
             mpg::take_ride(x.data(), y.data(), (int64_t)x.n(), false, ops, nops, c, np, h, w)) {
             check(nd ? mpg_node_spmv_norm_f32(c, nd, np, static_cast<float*>(h), static_cast<const float*>(w), x.data(),
                                                alpha, y.data(), ops, nops)

@@ -42,6 +42,9 @@ void discard_pending_reduction();
 // add_vector's normalisation deferred to ride the next SpMV (kernels_hip.cpp,
 // MPG_SURFACE_FUSE bit 16): issue it now as the separate calls would have
 void flush_ride();
+// false (and the redirect off for the rest of the solve) when a node SpMV's
+// grid is too large for the normalisation to ride it (kernels_hip.cpp)
+bool node_takes_norm_ride(mpg_node_t nd);
 bool defer_norm(mpg_ctx_t c, int32_t nparts, void* h, const void* x, void* y, int64_t n, bool f64);
 void* redirect_target(mpg_ctx_t c, void* y, int64_t n, bool f64);
 void set_redirect(mpg_ctx_t c, void* w, void* sp, int64_t n, bool f64);
