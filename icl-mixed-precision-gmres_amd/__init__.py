@@ -203,6 +203,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_engine_slices_per_wave.argtypes = [C.c_void_p]
     lib.mpg_engine_givens_folded.argtypes = [C.c_void_p]
     lib.mpg_engine_accum.argtypes = [C.c_void_p]
+    lib.mpg_engine_prologue_format.argtypes = [C.c_void_p]
     lib.mpg_engine_sell_shared_slices.argtypes = [C.c_void_p]
     lib.mpg_engine_sell_shared_slices.restype = C.c_int64
     lib.mpg_engine_sell_sigma.argtypes = [C.c_void_p]
@@ -882,7 +883,8 @@ class Engine:
                 "stored": st.value, "window": bool(win.value),
                 "slices_per_wave": int(self._lib.mpg_engine_slices_per_wave(self._h)),
                 "givens_folded": bool(self._lib.mpg_engine_givens_folded(self._h) == 1),
-                "accum": {0: "f64", 1: "f32"}[int(self._lib.mpg_engine_accum(self._h))]}
+                "accum": {0: "f64", 1: "f32"}[int(self._lib.mpg_engine_accum(self._h))],
+                "prologue": {1: "csr", 2: "sell", 3: "node"}[int(self._lib.mpg_engine_prologue_format(self._h))]}
 
     def sell_columns(self) -> dict:
         """Column form of the Arnoldi SpMV's SELL copy (mpg_engine_sell_columns):

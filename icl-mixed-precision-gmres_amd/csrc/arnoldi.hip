@@ -31,8 +31,41 @@ int64_t sell_copy_bytes(const mpg_arnoldi* a);
 // when the matrix has one and node_wins over what auto would run otherwise
 // (the SpMV is HBM-bound; 3-dof FEM: 4.44 B per fp32 nonzero against CSR's
 // 8). MPG_NODE=0: never.
+// The residual prologue on node blocks when the Arnoldi SpMV runs on them
+// (k_node_rowsums + k_prologue_rows: the CSR prologue's bits): the node copy
+// itself when it holds the outer values (baseline mode), else an fp64 node
+// copy of them when it streams fewer bytes than the fp64 CSR arrays. One GPU
+// (no lower halo); optional: a copy that cannot be built leaves the CSR
+// prologue. MPG_NODE_PROLOGUE=0: never.
+void node_prologue_build(mpg_arnoldi* a) {
+    const char* e = std::getenv("MPG_NODE_PROLOGUE");
+    if ((e && *e == '0') || a->node.nblk == 0 || a->d.n_front != 0 || a->d.outer_type != MPG_F64) return;
+    if (hipMalloc((void**)&a->rsum, (size_t)std::max(a->d.n, 1) * sizeof(double)) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    if (a->d.val_outer == a->d.val_inner && a->d.inner_val == MPG_F64) {
+        a->node_res = &a->node;
+        return;
+    }
+    const int64_t csr = a->d.A->nnz * 12 + ((int64_t)a->d.n + 1) * 4;
+    if (node_build(a->ctx, a->d.A, MPG_F64, a->d.val_outer, false, a->node_outer, csr) != MPG_OK ||
+        a->node_outer.nblk == 0) {
+        node_free(a->node_outer);
+        (void)hipGetLastError();
+        (void)hipFree(a->rsum);
+        a->rsum = nullptr;
+        return;
+    }
+    a->node_res = &a->node_outer;
+}
+
 int arnoldi_sell_build(mpg_arnoldi* a, int format) {
-    if (format == 3) return node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, true, a->node);
+    if (format == 3) {
+        if (int st = node_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, true, a->node)) return st;
+        node_prologue_build(a);
+        return MPG_OK;
+    }
     if (int st = sell_build(a->ctx, a->d.A, a->d.inner_val, a->d.val_inner, format, a->sell)) return st;
     const char* ne = std::getenv("MPG_NODE");
     if (format == 0 && !(ne && *ne == '0')) {
@@ -50,6 +83,7 @@ int arnoldi_sell_build(mpg_arnoldi* a, int format) {
         if (nc.nblk > 0) {  // (built only when it wins)
             sell_free(a->sell);
             a->node = nc;
+            node_prologue_build(a);
             return MPG_OK;
         }
     }
@@ -207,6 +241,8 @@ int mpg_arnoldi_destroy(mpg_arnoldi_t a) {
     sell_free(a->sell);
     sell_free(a->sell_outer);
     node_free(a->node);
+    node_free(a->node_outer);
+    if (a->rsum) (void)hipFree(a->rsum);
     delete a;
     return MPG_OK;
 }
@@ -219,6 +255,19 @@ int mpg_arnoldi_prologue(mpg_arnoldi_t a) {
         using X = decltype(x);
         using P = decltype(p);
         const P* diag = a->d.jacobi ? static_cast<const P*>(a->d.diag) : nullptr;
+        if (a->node_res && a->rsum) {
+            const NodeCopy& N = *a->node_res;
+            int tpw = node_tpw_default();
+            if (tpw < 1) tpw = 2;
+            k_node_rowsums<X><<<(N.ntiles + tpw - 1) / tpw, kBlock, 0, a->ctx->stream>>>(
+                N.tiles, N.bptr, static_cast<const char*>(N.recs), N.ntiles, N.nblk, tpw, node_xcd(N),
+                static_cast<const X*>(a->d.x), a->rsum);
+            a->last_G = rb_grid(a);
+            k_prologue_rows<T, X, P><<<rb_grid(a), kBlock, 0, a->ctx->stream>>>(
+                A->blocks, A->nblocks, a->rsum, static_cast<const X*>(a->d.x), static_cast<const X*>(a->d.b), diag,
+                static_cast<T*>(a->w[0]), a->partial);
+            return (int)MPG_OK;
+        }
         const SellCopy* S = a->outer_is_inner ? &a->sell : &a->sell_outer;
         if (S->nslices > 0 && S->vtype == a->d.outer_type) {
             const int grid = (S->nslices + kBlock / kWave - 1) / (kBlock / kWave);
@@ -364,6 +413,13 @@ int mpg_arnoldi_set_accum(mpg_arnoldi_t a, int accum) {
 }
 
 int mpg_arnoldi_accum(mpg_arnoldi_t a) { return !a ? MPG_ERR_ARG : a->acc32 ? MPG_ACCUM_F32 : MPG_ACCUM_F64; }
+
+int mpg_arnoldi_prologue_format(mpg_arnoldi_t a) {
+    if (!a) return MPG_ERR_ARG;
+    if (a->node_res && a->rsum) return 3;
+    const SellCopy* S = a->outer_is_inner ? &a->sell : &a->sell_outer;
+    return S->nslices > 0 && S->vtype == a->d.outer_type ? 2 : 1;
+}
 
 double* mpg_arnoldi_sums_dev(mpg_arnoldi_t a) { return a ? a->sums : nullptr; }
 void* mpg_arnoldi_wprev_dev(mpg_arnoldi_t a, int k) { return a ? a->w[k & 1] : nullptr; }

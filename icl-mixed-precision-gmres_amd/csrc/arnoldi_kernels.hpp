@@ -136,6 +136,60 @@ __global__ __launch_bounds__(kBlock) void k_prologue(const int32_t* __restrict__
     store_partials<4>(acc, 3, partial);
 }
 
+// The residual prologue on node blocks (round 6), in two launches whose
+// arithmetic is k_prologue's: k_node_rowsums forms every row's fp64 sum of
+// A x on the node copy of the outer values (the CSR tile's products in CSR
+// storage order, node_tile.hpp), then k_prologue_rows runs k_prologue's
+// epilogue on those sums with k_prologue's grid, row blocks and lane-to-row
+// map (for_rows / csr_row_block: lane t takes rows r0 + t, r0 + t + 256, ...
+// of each of its workgroup's blocks), so every lane's three norm partials
+// add the same terms in the same order and the cycle keeps the CSR bits.
+// (A single row past kNnzCap, csr_row_block's tree-summed row mode, cannot
+// occur: a node row holds at most kNodeCap blocks.) fem27 / C4: 8.9 B per
+// nonzero of fp64 records against CSR's 12.
+template <class X>
+__global__ __launch_bounds__(kBlock) void k_node_rowsums(const int32_t* __restrict__ tiles,
+                                                         const int32_t* __restrict__ bptr,
+                                                         const char* __restrict__ recs, int ntiles, int64_t nblk,
+                                                         int tpw, int xcd, const X* __restrict__ x,
+                                                         double* __restrict__ rsum) {
+    __shared__ double prod[kNodeProd];
+    const int g = xcd ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int t0 = g * tpw, t1 = t0 + tpw < ntiles ? t0 + tpw : ntiles;
+    node_tiles<X>(
+        t0, t1, tiles, tiles + ntiles + 1, bptr, recs, nblk, [&](int c) { return x[c]; },
+        [&](X v) { return (double)v; }, [&](int) { return 0; }, [&](int i, double sum, int) { rsum[i] = sum; },
+        prod);
+}
+
+template <class T, class X, class P>
+__global__ __launch_bounds__(kBlock) void k_prologue_rows(const int32_t* __restrict__ blocks, int nblocks,
+                                                          const double* __restrict__ rsum,
+                                                          const X* __restrict__ x, const X* __restrict__ b,
+                                                          const P* __restrict__ diag, T* __restrict__ w,
+                                                          double* __restrict__ partial) {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    auto epi = [&](int i) {  // k_prologue's epilogue, on the same sum
+        const X t = (X)rsum[i];
+        const X r = b[i] - t;
+        T wi = (T)r;
+        acc[0] += (double)wi * (double)wi;
+        P pw = (P)wi;
+        if (diag) pw = P(0) * pw + P(1) * diag[i] * pw;
+        wi = (T)pw;
+        acc[1] += (double)wi * (double)wi;
+        acc[2] += (double)x[i] * (double)x[i];
+        w[i] = wi;
+    };
+    int rb0, rb1;
+    my_blocks(nblocks, rb0, rb1);
+    for (int bk = rb0; bk < rb1; ++bk) {
+        const int r0 = blocks[bk], r1 = blocks[bk + 1];
+        for (int r = threadIdx.x; r < r1 - r0; r += kBlock) epi(r0 + r);
+    }
+    store_partials<4>(acc, 3, partial);
+}
+
 // The same prologue on a SELL-64 copy of the outer-precision values (one
 // wave per slice, one lane per row; loads issued in need order as in
 // k_step_sell): r = b - A x (X), w = M(T(r)), partials ||T(r)||^2,
@@ -1774,6 +1828,12 @@ struct mpg_arnoldi {
     SellCopy sell;  // sliced-ELL copy of the Arnoldi matrix (nslices == 0: CSR row blocks)
     SellCopy sell_outer;        // ... of the outer-precision values, for the residual prologue
     NodeCopy node;              // node-block copy of the Arnoldi matrix (nblk > 0: the Arnoldi SpMV uses it)
+    // the residual prologue on node blocks (round 6): an fp64 node copy of the
+    // outer values (or `node` itself when it holds them) and the fp64 row sums
+    // A x it writes for k_prologue_rows; nullptr / empty: the CSR prologue
+    NodeCopy node_outer;
+    const NodeCopy* node_res = nullptr;
+    double* rsum = nullptr;
     bool outer_is_inner = false;  // the prologue runs on `sell` (baseline / single modes)
     // SELL SpMV with the panel dots fused (SellDots): per-workgroup partials,
     // group tickets, group size and count

@@ -1522,6 +1522,11 @@ int mpg_engine_accum(mpg_engine_t e) {
     return mpg_arnoldi_accum(e->eng->arnoldi());
 }
 
+int mpg_engine_prologue_format(mpg_engine_t e) {
+    if (!e || !e->eng) return MPG_ERR_ARG;
+    return mpg_arnoldi_prologue_format(e->eng->arnoldi());
+}
+
 int mpg_engine_givens_folded(mpg_engine_t e) {
     if (!e || !e->eng) return MPG_ERR_ARG;
     return e->eng->givens_folded() ? 1 : 0;

@@ -245,6 +245,11 @@ int mpg_arnoldi_uniform_groups(mpg_arnoldi_t a);
 int mpg_arnoldi_set_accum(mpg_arnoldi_t a, int accum);
 int mpg_arnoldi_accum(mpg_arnoldi_t a);
 
+/* Storage the residual prologue runs on: 1 CSR row blocks, 2 the SELL copy
+ * of the outer values, 3 node blocks (row sums on the node copy, then the
+ * CSR prologue's epilogue and norm partials: its bits). */
+int mpg_arnoldi_prologue_format(mpg_arnoldi_t a);
+
 #ifdef __cplusplus
 }
 #endif

@@ -180,6 +180,8 @@ int mpg_engine_sell_sigma(mpg_engine_t e);
 int mpg_engine_givens_folded(mpg_engine_t e);
 /* the accumulation class the engine's Arnoldi runs: MPG_ACCUM_F64 0 / MPG_ACCUM_F32 1 (arnoldi.h) */
 int mpg_engine_accum(mpg_engine_t e);
+/* the residual prologue's storage (mpg_arnoldi_prologue_format: 1 CSR, 2 SELL, 3 node blocks) */
+int mpg_engine_prologue_format(mpg_engine_t e);
 /* ranks of the engine's communicator as its transport reports them: 1 for a
  * single-GPU engine, ncclCommCount for an RCCL rank, the world size for the
  * host transport; < 0 on error */

@@ -167,6 +167,29 @@ def test_node_blocks_same_bits_as_csr(mpg, which, mode, orth, prec):
     assert got.res_norm == ref.res_norm
 
 
+@pytest.mark.parametrize("mode", ["mixed", "baseline", "mixed-half"])
+@pytest.mark.parametrize("which", ["stencil27", "fem27p"])
+def test_node_prologue_same_bits(mpg, monkeypatch, which, mode):
+    """The residual prologue on node blocks (round 6; k_node_rowsums +
+    k_prologue_rows: the node copy's fp64 row sums, then the CSR prologue's
+    epilogue and norm partials with its own grid and lane-to-row map) gives
+    the CSR prologue's bits: whole solves with it and with MPG_NODE_PROLOGUE=0
+    agree to the last bit, and the layout reports which one ran."""
+    A, xt, b = _node_problem(mpg, which)
+    opts = dict(mode=mode, orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3, spmv_format="node")
+    got = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("MPG_NODE_PROLOGUE", env)
+        eng = mpg.Engine(A, b, xt, **opts)
+        lay = eng.spmv_layout()
+        eng.close()
+        assert lay["format"] == "node" and lay["prologue"] == ("node" if env == "1" else "csr"), lay
+        got[env] = mpg.solve(A, b, xt, engine="fused", **opts)
+    assert got["1"].total_iters == got["0"].total_iters == 90
+    assert np.array_equal(got["1"].step_res, got["0"].step_res) and np.array_equal(got["1"].x, got["0"].x)
+    assert got["1"].res_norm == got["0"].res_norm
+
+
 def test_node_blocks_refused(mpg, monkeypatch):
     """spmv_format="node" fails loudly where no node copy can be built (rows
     not a multiple of 3; exact blocks only, MPG_NODE_PAD=0, on a band and on

@@ -87,7 +87,7 @@ def test_spmv_layout_choice(mpg):
         assert e.spmv_layout() == {"format": "sell", "vec_width": 2, "col_bytes": 2,
                                    "stored": -(-A.nrows // 64) * 64 * 10, "window": True,
                                    "slices_per_wave": 2,  # uniform int16 slices: k_step_sell2
-                                   "givens_folded": True, "accum": "f64"}
+                                   "givens_folded": True, "accum": "f64", "prologue": "sell"}
     finally:
         e.close()
     B = _arrow(mpg, 3000)
