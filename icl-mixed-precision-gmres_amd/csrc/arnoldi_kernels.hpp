@@ -1175,6 +1175,7 @@ __global__ __launch_bounds__(BS) void k_cgs_update_nc(int n, const T* __restrict
     stamp_at<STAMP>(stamp, 0);
     static_assert(!FROM_PARTS || BS >= 32 * NC, "32 lanes per column");
     static_assert(!PF || (FROM_PARTS && !NEXT_DOTS), "prefetch under the partial sums");
+    static_assert(!PF || NC <= kColBatch<T>, "the prefetch form holds one batch of columns (the only form run)");
     constexpr int B = kColBatch<T>;
     constexpr int B0 = NC < B ? NC : B;
     __shared__ A coef[NC];

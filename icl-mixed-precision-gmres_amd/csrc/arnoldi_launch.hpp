@@ -267,11 +267,18 @@ int dots_run(mpg_arnoldi_t a, int k, bool combine) {
 }
 
 
-// MPG_CGS_PREFETCH=1: the in-launch-sum CGS update issues its first row
-// group under the coefficient sums (k_cgs_update_nc<..., PF>)
+// The in-launch-sum CGS update issuing its first row group under the
+// coefficient sums (k_cgs_update_nc<..., PF>, steps with k + 1 <= one batch
+// of columns): on by default in the fp32 accumulation class, where the held
+// batch fits its registers (BAND-10M, 8 interleaved bench runs each:
+// 26.92k against 26.75k it/s, the update 11.98 against 12.27 us;
+// profiles/r06_pf/), off in the fp64 class (round 4: no gain).
+// MPG_CGS_PREFETCH=0 / 1 forces it.
+template <class A>
 inline bool cgs_prefetch() {
     const char* e = std::getenv("MPG_CGS_PREFETCH");
-    return e && *e == '1';
+    if (e && (*e == '0' || *e == '1')) return *e == '1';
+    return std::is_same_v<A, float>;
 }
 
 // no_next (CGSR at 32 < k + 1 <= kWideMax, one GPU): a pass that takes its
@@ -328,14 +335,20 @@ int cgs_run(mpg_arnoldi_t a, int k, int pass, bool givens, bool from_partials, b
         } else if (k + 1 <= kNC) {  // last pass: 1024-thread workgroups, one per CU -> Gd ||w||^2 partials
             // the wave stamps of the product form only (in-launch sums, no
             // prefetch): the one bench.py's phases time
-            if (!from_partials || cgs_prefetch()) sp = nullptr;
+            // (an armed stamp times the stamped product form, so a measured
+            // launch never takes the prefetch variant)
+            if (!from_partials) sp = nullptr;
+            const bool pf = from_partials && !sp && cgs_prefetch<A>();
             return with_nc<kNC>(k + 1, [&](auto nc) {
                 constexpr int NC = decltype(nc)::value;
                 const T* Vp = static_cast<const T*>(a->V);
                 // (the prefetch variant for one batch of columns only: wider
-                // panels spill with the prefetched batch held across the sums)
+                // panels spilled with the prefetched batch held across the sums
+                // in the fp64 class, and in the fp32 class the wider forms
+                // (NC 9..28, no spills) aborted the process on the box
+                // (round 6, profiles/r06_pf/); they are not built)
                 if constexpr (NC <= kColBatch<T>) {
-                    if (from_partials && cgs_prefetch()) {
+                    if (pf) {
                         k_cgs_update_nc<T, kCombineBlock, NC, true, false, true, false, A>
                             <<<a->Gd, kCombineBlock, 0, a->ctx->stream>>>(a->d.n, Vp, a->ld, src, part_G, coef_out,
                                                                            w, a->partial, nullptr);

@@ -429,19 +429,23 @@ def test_surface_gemv_emits_nrm2_partials_same_bits(mpg, orth, mode, monkeypatch
         assert np.array_equal(p.step_res, q.step_res) and np.array_equal(p.x, q.x), A.nrows
 
 
-@pytest.mark.parametrize("flag,engine", [("MPG_CGS_PREFETCH", "fused"), ("MPG_SURFACE_PAIR", "surface")])
+@pytest.mark.parametrize("flag,engine,accum", [("MPG_CGS_PREFETCH", "fused", "f64"), ("MPG_CGS_PREFETCH", "fused", "f32"),
+                                               ("MPG_SURFACE_PAIR", "surface", "f64")])
 @pytest.mark.parametrize("mode", ["mixed", "baseline"])
-def test_round4_kernel_variants_same_bits(mpg, flag, engine, mode, monkeypatch):
+def test_round4_kernel_variants_same_bits(mpg, flag, engine, accum, mode, monkeypatch):
     """Round-4 kernel forms that must not change a bit: the CGS update that
-    issues its first row group under the coefficient sums (MPG_CGS_PREFETCH)
-    and the operator surface's two-slice-per-wave SELL SpMV (MPG_SURFACE_PAIR,
-    on by default) -- the same operands summed in the same order."""
+    issues its first row group under the coefficient sums (MPG_CGS_PREFETCH;
+    on by default in the fp32 accumulation class since round 6) and the
+    operator surface's two-slice-per-wave SELL SpMV (MPG_SURFACE_PAIR, on by
+    default) -- the same operands summed in the same order."""
     res = {}
     for mpg_case in ("band", "lap"):
         A = mpg.gen_band(120_000, 5, 4, seed=7) if mpg_case == "band" else mpg.gen_laplace3d(40)
         xt = mpg.rand_vect(A.nrows, 42)
         b = mpg.host_spmv(A, xt)
         opts = dict(mode=mode, orth="cgs", prec="jacobi", rlen=30, tol=0.0, max_restarts=3)
+        if accum == "f32":
+            opts["accum"] = "f32"
         for v in ("0", "1"):
             monkeypatch.setenv(flag, v)
             res[(mpg_case, v)] = mpg.solve(A, b, xt, engine=engine, **opts)
