@@ -151,6 +151,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_cycle_program_counts.argtypes = [C.POINTER(_I64)] * 3
     lib.mpg_surface_ride_counts.argtypes = [C.POINTER(_I64)] * 3
     lib.mpg_surface_spmv_counts.argtypes = [C.POINTER(_I64)] * 3
+    lib.mpg_surface_host_norm_hits.argtypes = [C.POINTER(_I64)]
     lib.mpg_engine_report.argtypes = [C.c_void_p, C.POINTER(SolveResult)]
     lib.mpg_engine_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     lib.mpg_engine_sync.argtypes = [C.c_void_p]
@@ -564,6 +565,15 @@ def surface_ride_counts() -> dict:
     v = [_I64() for _ in range(3)]
     host_lib().mpg_surface_ride_counts(*[C.byref(x) for x in v])
     return {"redirects": v[0].value, "rides": v[1].value, "flushed": v[2].value}
+
+
+def surface_host_norm_hits() -> int:
+    """Host-value nrm2 calls of the operator surface on this thread answered
+    from the previous read of the same, unwritten vector
+    (mpg_surface_host_norm_hits)."""
+    v = _I64()
+    host_lib().mpg_surface_host_norm_hits(C.byref(v))
+    return v.value
 
 
 def surface_spmv_counts() -> dict:

@@ -23,6 +23,12 @@ namespace mpg {
 namespace {
 thread_local mpg_ctx_t tl_ctx = nullptr;
 thread_local bool tl_owned = false;
+// Device work this thread has issued through the surface: every operator
+// takes its context from ctx_no_flush() (directly or through current_ctx()),
+// which counts it, and a cycle program's graph replay counts itself
+// (note_device_writes). The host-value nrm2 memo below is valid while the
+// count has not moved.
+thread_local uint64_t tl_writes = 0;
 
 struct OwnedCtxReaper {
     ~OwnedCtxReaper() {
@@ -100,6 +106,7 @@ bool batch_enabled() {
 }
 
 mpg_ctx_t ctx_no_flush() {
+    ++tl_writes;
     if (!tl_ctx) {
         const char* env = std::getenv("MPG_DEVICE");
         int dev = env ? std::atoi(env) : 0;
@@ -136,8 +143,9 @@ thread_local PendingReduction tl_red;
 // 2 dot -> naxpy, 4 gemv^T -> gemv, 8 gemv -> nrm2: the CGS update emits
 // the ||w||^2 partials that the nrm2 of add_vector would compute, below;
 // 16 scal_recip -> spmv: add_vector's normalisation rides the next SELL
-// SpMV, below); unset: kFuseDefault; 0: none
-constexpr int kFuseDefault = 1 | 4 | 8 | 16;
+// SpMV, below; 32 the host-value nrm2 memo, below); unset: kFuseDefault;
+// 0: none
+constexpr int kFuseDefault = 1 | 4 | 8 | 16 | 32;
 
 // The ||y||^2 stage-1 partials a fused CGS gemv (mpg_gemv_n_from_t_nrm2_*)
 // left in the context workspace: an nrm2 of exactly that y as the very
@@ -405,6 +413,58 @@ bool node_takes_norm_ride(mpg_node_t nd) {
     return false;
 }
 
+void note_device_writes() { ++tl_writes; }
+
+// ---- host-value nrm2 memo (round 6, MPG_SURFACE_FUSE bit 32) ----
+// The reference's restart section reads nrm2(w) to the host three times
+// with nothing written in between when the preconditioner is the identity
+// (r_norm, beta, first_vector's norm: gmres.cpp:176-196, Orthogonalization.hpp:
+// 36-45), each a host round trip. A host-value nrm2 of the same vector on the
+// same context, with no device work issued through the surface since the
+// read and nothing deferred or queued, returns that read's value: the same
+// deterministic sum of the same bits. Host-value reductions only read, so
+// the context they take does not count as device work (read_ctx), unless
+// taking it issued deferred work.
+namespace {
+struct HostNormMemo {
+    const void* p = nullptr;
+    int64_t n = 0;
+    bool f64 = false;
+    double v = 0;
+    mpg_ctx_t ctx = nullptr;
+    uint64_t token = 0;
+};
+thread_local HostNormMemo tl_hn[2];
+thread_local int tl_hn_next = 0;
+thread_local int64_t tl_hn_hits = 0;
+bool nothing_deferred() { return !tl_dnorm.on && !tl_redir.w && tl_nops == 0 && tl_red.kind == 0; }
+}  // namespace
+
+bool host_norm_hit(const void* p, int64_t n, bool f64, double& v) {
+    if (!fuse_enabled(32) || !tl_ctx || !nothing_deferred()) return false;
+    for (const HostNormMemo& m : tl_hn)
+        if (m.p == p && m.n == n && m.f64 == f64 && m.ctx == tl_ctx && m.token == tl_writes) {
+            v = m.v;
+            ++tl_hn_hits;
+            return true;
+        }
+    return false;
+}
+
+void host_norm_store(const void* p, int64_t n, bool f64, double v) {
+    tl_hn[tl_hn_next] = HostNormMemo{p, n, f64, v, tl_ctx, tl_writes};
+    tl_hn_next ^= 1;
+}
+
+mpg_ctx_t current_ctx();
+mpg_ctx_t read_ctx() {
+    const bool deferred = !nothing_deferred();
+    const uint64_t before = tl_writes;
+    mpg_ctx_t c = current_ctx();
+    if (!deferred) tl_writes = before;
+    return c;
+}
+
 mpg_ctx_t current_ctx() {
     tl_norm.y = nullptr;
     flush_ride();
@@ -420,6 +480,7 @@ ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) {
     if (tl_red.kind) flush_pending_reduction();
     tl_ctx = ctx;
     tl_ride_score = 2;  // (what the ride learned belongs to the previous scope's solve)
+    tl_hn[0] = tl_hn[1] = HostNormMemo{};  // (so does the host-value nrm2 memo)
 }
 ScopedContext::~ScopedContext() {
     // the queue and a pending stage 2 belong to this scope's context; a
@@ -536,13 +597,13 @@ template <> void copy<float, double, Hip>(Scalar<float, Hip> x, Scalar<double, H
 template <> double dot<double, Hip>(Vect<double, Hip> x, Vect<double, Hip> y) {
     assert(x.n() == y.n());
     double r;
-    check(mpg_dot_f64_host(C, x.n(), x.data(), y.data(), &r), "dot");
+    check(mpg_dot_f64_host(mpg::read_ctx(), x.n(), x.data(), y.data(), &r), "dot");
     return r;
 }
 template <> float dot<float, Hip>(Vect<float, Hip> x, Vect<float, Hip> y) {
     assert(x.n() == y.n());
     float r;
-    check(mpg_dot_f32_host(C, x.n(), x.data(), y.data(), &r), "dot");
+    check(mpg_dot_f32_host(mpg::read_ctx(), x.n(), x.data(), y.data(), &r), "dot");
     return r;
 }
 template <> void dot<double, Hip>(Vect<double, Hip> x, Vect<double, Hip> y, Scalar<double, Hip> r) {
@@ -569,12 +630,17 @@ template <> void dot<float, Hip>(Vect<float, Hip> x, Vect<float, Hip> y, Scalar<
 }
 template <> double nrm2<double, Hip>(Vect<double, Hip> x) {
     double r;
-    check(mpg_nrm2_f64_host(C, x.n(), x.data(), &r), "nrm2");
+    if (mpg::host_norm_hit(x.data(), (int64_t)x.n(), true, r)) return r;
+    check(mpg_nrm2_f64_host(mpg::read_ctx(), x.n(), x.data(), &r), "nrm2");
+    mpg::host_norm_store(x.data(), (int64_t)x.n(), true, r);
     return r;
 }
 template <> float nrm2<float, Hip>(Vect<float, Hip> x) {
+    double m;
+    if (mpg::host_norm_hit(x.data(), (int64_t)x.n(), false, m)) return (float)m;
     float r;
-    check(mpg_nrm2_f32_host(C, x.n(), x.data(), &r), "nrm2");
+    check(mpg_nrm2_f32_host(mpg::read_ctx(), x.n(), x.data(), &r), "nrm2");
+    mpg::host_norm_store(x.data(), (int64_t)x.n(), false, r);
     return r;
 }
 template <> void nrm2<double, Hip>(Vect<double, Hip> x, Scalar<double, Hip> r) {
@@ -731,6 +797,11 @@ void set_redirect(mpg_ctx_t c, void* w, void* sp, int64_t n, bool f64) {
     ++tl_ride_counts[0];
 }
 }  // namespace mpg
+
+extern "C" int mpg_surface_host_norm_hits(int64_t* hits) {
+    if (hits) *hits = mpg::tl_hn_hits;
+    return MPG_OK;
+}
 
 extern "C" int mpg_surface_spmv_counts(int64_t* node, int64_t* sell, int64_t* csr) {
     if (node) *node = mpg::tl_spmv_counts[0];

@@ -42,6 +42,9 @@ void discard_pending_reduction();
 // add_vector's normalisation deferred to ride the next SpMV (kernels_hip.cpp,
 // MPG_SURFACE_FUSE bit 16): issue it now as the separate calls would have
 void flush_ride();
+// device work issued outside an operator call (a cycle program's graph replay):
+// ends the host-value nrm2 memo (kernels_hip.cpp)
+void note_device_writes();
 // false (and the redirect off for the rest of the solve) when a node SpMV's
 // grid is too large for the normalisation to ride it (kernels_hip.cpp)
 bool node_takes_norm_ride(mpg_node_t nd);
@@ -149,6 +152,7 @@ public:
     template <class F>
     void run(F&& steps) {
         if (g_) {
+            note_device_writes();
             check(mpg_graph_launch(ctx_, g_), "cycle program launch", ctx_);
             count(1);
             return;
@@ -191,6 +195,7 @@ public:
             return;
         }
         g_ = g;
+        note_device_writes();
         check(mpg_graph_launch(ctx_, g_), "cycle program launch", ctx_);
         count(0);
     }

@@ -207,6 +207,10 @@ int mpg_surface_ride_counts(int64_t* redirects, int64_t* rides, int64_t* flushed
  * they ran on: node blocks (mpg_node_spmv_*), SELL-64, CSR. Pointers may be
  * NULL. */
 int mpg_surface_spmv_counts(int64_t* node, int64_t* sell, int64_t* csr);
+/* Host-value nrm2 calls of the operator surface on this thread answered from
+ * the memo of the same vector's previous read (MPG_SURFACE_FUSE bit 32: no
+ * device work issued through the surface in between, nothing deferred). */
+int mpg_surface_host_norm_hits(int64_t* hits);
 
 #ifdef __cplusplus
 }

@@ -299,6 +299,34 @@ def test_surface_cycle_program_matches_eager(mpg, orth, mode, prec, monkeypatch)
     assert p.res_norm == e.res_norm and p.err_norm == e.err_norm
 
 
+@pytest.mark.parametrize("mode", ["mixed", "baseline"])
+@pytest.mark.parametrize("prec", ["identity", "jacobi"])
+def test_surface_host_norm_memo(mpg, mode, prec, monkeypatch):
+    """Round 6 (MPG_SURFACE_FUSE bit 32): a host-value nrm2 of a vector that
+    nothing has written since its last host read returns that read (the
+    reference's restart section reads ||w|| as r_norm, beta and in
+    first_vector). With the identity preconditioner beta and first_vector's
+    read are answered from it, with Jacobi only first_vector's (gdmv writes
+    w between r_norm and beta); the solve keeps the bits of the surface
+    without the memo."""
+    A = mpg.gen_band(100_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(engine="surface", mode=mode, orth="cgs", prec=prec, rlen=30, tol=0.0, max_restarts=3)
+    monkeypatch.delenv("MPG_SURFACE_FUSE", raising=False)
+    h0 = mpg.surface_host_norm_hits()
+    on = mpg.solve(A, b, xt, **opts)
+    hits = mpg.surface_host_norm_hits() - h0
+    monkeypatch.setenv("MPG_SURFACE_FUSE", str(1 | 4 | 8 | 16))
+    h1 = mpg.surface_host_norm_hits()
+    off = mpg.solve(A, b, xt, **opts)
+    assert mpg.surface_host_norm_hits() == h1
+    assert hits >= (2 * 3 if prec == "identity" else 3), hits
+    assert on.total_iters == off.total_iters == 90
+    assert np.array_equal(on.step_res, off.step_res) and np.array_equal(on.x, off.x)
+    assert on.res_norm == off.res_norm
+
+
 @pytest.mark.parametrize("matrix", ["band", "lap", "stencil27"])
 @pytest.mark.parametrize("orth", ["cgs", "mgs", "cgsr"])
 @pytest.mark.parametrize("mode", ["mixed", "baseline", "single"])
