@@ -17,6 +17,7 @@
 #include "panel.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 using namespace mpg;
 
@@ -478,13 +479,107 @@ __global__ __launch_bounds__(kBlock) void k_trsv(int upper, int trans, int n, co
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += kBlock) x[i] = xs[i];
 }
+
+// lane j's value in every lane (j wave-uniform): scalar reads, no LDS
+__device__ __forceinline__ float wave_bcast(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+__device__ __forceinline__ double wave_bcast(double v, int j) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), j);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// n <= 64 (the surface's y = H(0:k,0:k)^-1 s of a restart cycle): one wave,
+// the matrix staged into LDS with all its loads in flight at once and lane i
+// holding x(i), so a step waits on neither global memory nor a barrier (x(j)
+// is broadcast by a shuffle). k_trsv waited for two dependent global loads
+// per step: 21.7 us at n = 30 in the surface's restart section
+// (profiles/r06_surface/r06o_cycle_timeline.txt). The same operations in the
+// same order per element as k_trsv: the same bits (MPG_TRSV_WAVE=0: k_trsv).
+template <class T, bool UPPER>
+__global__ __launch_bounds__(kWave) void k_trsv_wave(int trans, int n, const T* __restrict__ A,
+                                                     int64_t lda, T* __restrict__ x) {
+    extern __shared__ unsigned char smem_raw[];
+    T* As = reinterpret_cast<T*>(smem_raw);  // A(i, j) at As[j n + i]
+    const int lane = threadIdx.x;
+    // lane i loads row i of 32 columns at a time, every load of a batch
+    // issued before any LDS store (clamped indices, masked stores): one
+    // memory round trip per 32 columns
+    constexpr int B = 32;
+    const int ic = lane < n ? lane : n - 1;
+    T xi = x[ic];
+    for (int j0 = 0; j0 < n; j0 += B) {
+        T r[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) r[u] = A[(int64_t)(j0 + u < n ? j0 + u : n - 1) * lda + ic];
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+            if (j0 + u < n && lane < n) As[(j0 + u) * n + lane] = r[u];
+    }
+    if (lane >= n) xi = T(0);
+    __syncthreads();
+    if (!trans) {
+        // per step the chain is lane j's division, a scalar broadcast and
+        // one product-difference; the column's LDS read is issued a step
+        // ahead. Every lane divides its own entry by its own diagonal (only
+        // lane j's quotient is used), so no step reads LDS for the diagonal.
+        const T di = As[ic * n + ic];
+        int j = UPPER ? n - 1 : 0;
+        T aj = As[j * n + ic];
+        for (int step = 0; step < n; ++step, j += UPPER ? -1 : 1) {
+            const int jn = step + 1 < n ? (UPPER ? j - 1 : j + 1) : j;
+            const T a = aj;
+            aj = As[jn * n + ic];
+            T q = xi;
+            if (q != T(0)) q = q / di;
+            const T xj = wave_bcast(q, j);
+            if (lane == j) xi = xj;
+            const bool mine = UPPER ? lane < j : (lane > j && lane < n);
+            if (xj != T(0) && mine) xi = xi - xj * a;
+        }
+        if (lane < n) x[lane] = xi;
+        return;
+    }
+    // the transposed forms are serial dot products (k_trsv's order), from LDS
+    T* xs = As + n * n;
+    if (lane < n) xs[lane] = xi;
+    __syncthreads();
+    if (lane == 0) {
+        if (UPPER) {
+            for (int j = 0; j < n; ++j) {
+                T temp = xs[j];
+                for (int i = 0; i < j; ++i) temp = temp - As[j * n + i] * xs[i];
+                xs[j] = temp / As[j * n + j];
+            }
+        } else {
+            for (int j = n - 1; j >= 0; --j) {
+                T temp = xs[j];
+                for (int i = n - 1; i > j; --i) temp = temp - As[j * n + i] * xs[i];
+                xs[j] = temp / As[j * n + j];
+            }
+        }
+    }
+    __syncthreads();
+    if (lane < n) x[lane] = xs[lane];
+}
 #pragma clang fp contract(on)
+
+inline bool trsv_wave() {
+    const char* e = std::getenv("MPG_TRSV_WAVE");
+    return !(e && *e == '0');
+}
 
 template <class T>
 int trsv_impl(mpg_ctx* ctx, int upper, int trans, int64_t n, const T* A, int64_t lda, T* x) {
     if (!ctx || n < 0 || n > 4096 || (n > 0 && lda < n)) return MPG_ERR_ARG;
     if (n == 0) return MPG_OK;
-    k_trsv<T><<<1, kBlock, n * sizeof(T), ctx->stream>>>(upper, trans, (int)n, A, lda, x);
+    if (n <= kWave && trsv_wave())
+        (upper ? k_trsv_wave<T, true> : k_trsv_wave<T, false>)<<<1, kWave, (n * n + n) * sizeof(T), ctx->stream>>>(
+            trans, (int)n, A, lda, x);
+    else
+        k_trsv<T><<<1, kBlock, n * sizeof(T), ctx->stream>>>(upper, trans, (int)n, A, lda, x);
     MPG_LAUNCH_CHECK(ctx);
     return MPG_OK;
 }

@@ -215,6 +215,35 @@ def test_trsv_upper(hip, oracle, t, n):
         assert np.allclose(dv.get(), exp, rtol=1e3 * tol, atol=1e3 * tol)
 
 
+@pytest.mark.parametrize("t", ["f64", "f32"])
+def test_trsv_wave_same_bits(hip, t, monkeypatch):
+    """The one-wave LDS-staged trsv (n <= 64) against the workgroup form
+    (MPG_TRSV_WAVE=0): the same bits in all four (upper, trans) forms, at
+    n = 1 ... 64 and ld > n; n = 65 takes the workgroup form either way."""
+    dt = np.float64 if t == "f64" else np.float32
+    for n in (1, 2, 7, 30, 31, 63, 64, 65):
+        g = rng(100 + n)
+        ld = n + 3
+        M = np.zeros((ld, n), dt, order="F")
+        M[:n] = g.uniform(-1, 1, (n, n)) + np.diag(g.uniform(2, 3, n))
+        y = g.uniform(-1, 1, n).astype(dt)
+        y[n // 2] = 0  # a zero right-hand entry: the skipped update
+        for upper in (1, 0):
+            for trans in (0, 1):
+                got = {}
+                for wave in ("1", "0"):
+                    monkeypatch.setenv("MPG_TRSV_WAVE", wave)
+                    dM, dv = hip.buf(M.ravel(order="F")), hip.buf(y)
+                    hip.call(f"mpg_trsv_{t}", upper, trans, n, dM.p, ld, dv.p)
+                    got[wave] = dv.get()
+                assert np.array_equal(got["1"].view(np.uint8), got["0"].view(np.uint8)), (n, upper, trans)
+                tri = np.triu(M[:n]) if upper else np.tril(M[:n])
+                op = (tri.T if trans else tri).astype(np.float64)
+                exp = np.linalg.solve(op, y.astype(np.float64))
+                tol = 1e3 * 64 * (F64_EPS if t == "f64" else F32_EPS)
+                assert np.allclose(got["1"], exp, rtol=tol, atol=tol)
+
+
 def _spmv_case(mpg, kind):
     if kind == "band":
         return mpg.gen_band(200_000, 5, 4, seed=11)

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--var", action="append", required=True, help="NAME=VALUE[,NAME=VALUE] per variant")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cycles", type=int, default=2)
+    ap.add_argument("--accum", default="f32", help="accumulation class of the fp32 Arnoldi (f32 | f64)")
     args = ap.parse_args()
     from __graft_entry__ import _load
 
@@ -66,7 +67,8 @@ def main():
             # (a variant's spmv_format=auto|csr|sell picks the storage; the rest are environment flags)
             fmt = v.pop("spmv_format", "auto")
             e = with_env(v, lambda: mpg.Engine(A, b, xt, mode=mode, orth="cgs", prec="identity", rlen=30, tol=0.0,
-                                              max_restarts=1000, spmv_format=fmt))
+                                              max_restarts=1000, spmv_format=fmt,
+                                              accum=args.accum))
             v["spmv_format"] = fmt
             with_env(v, lambda: e.run(1))
             engs.append(e)
