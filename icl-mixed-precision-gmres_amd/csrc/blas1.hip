@@ -77,7 +77,8 @@ template <class T>
 __global__ __launch_bounds__(kQuadBlock) void k_nrm2_quad_host(int64_t n, const T* __restrict__ x,
                                                                double* __restrict__ partial,
                                                                unsigned* __restrict__ ticket,
-                                                               T* __restrict__ result_host) {
+                                                               T* __restrict__ result_host,
+                                                               unsigned* __restrict__ flag_host, unsigned seq) {
     static_assert(kQuadBlock == 1024, "the last workgroup runs stage 2's 1024-lane sum");
     __shared__ double scratch[kQuadBlock / kWave];
     __shared__ unsigned arrived;
@@ -96,6 +97,10 @@ __global__ __launch_bounds__(kQuadBlock) void k_nrm2_quad_host(int64_t n, const 
     if (threadIdx.x == 0) {
         __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(result_host, (T)sqrt(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (flag_host) {  // the result written through before the host's flag (mpg::host_poll)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(flag_host, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -195,10 +200,12 @@ template <class T, bool SQUARE>
 int reduce_host(mpg_ctx* ctx, int64_t n, const T* x, const T* y, T* result_host) {
     if (!result_host) return MPG_ERR_ARG;
     if (SQUARE && ctx && ctx->host_ws_dev && ctx->ticket && n > 0 && (uintptr_t)x % 16 == 0) {
-        k_nrm2_quad_host<T><<<quad_groups(n), kQuadBlock, 0, ctx->stream>>>(n, x, ctx->red_ws, ctx->ticket,
-                                                                           (T*)ctx->host_ws_dev);
+        const bool poll = mpg::host_poll_on();
+        const unsigned seq = poll ? mpg::host_seq_next(ctx) : 0u;
+        k_nrm2_quad_host<T><<<quad_groups(n), kQuadBlock, 0, ctx->stream>>>(
+            n, x, ctx->red_ws, ctx->ticket, (T*)ctx->host_ws_dev, poll ? mpg::host_flag_dev(ctx) : nullptr, seq);
         MPG_LAUNCH_CHECK(ctx);
-        MPG_HIP(ctx, mpg::spin_wait(ctx->stream));
+        MPG_HIP(ctx, poll ? mpg::host_poll(ctx, seq) : mpg::spin_wait(ctx->stream));
         *result_host = *static_cast<volatile T*>(ctx->host_ws);
         return MPG_OK;
     }

@@ -4,8 +4,33 @@
 // explicit context per (GPU, host thread), no global mutable state.
 #include "internal.hpp"
 
+#include <cstdlib>
 #include <cstring>
 #include <new>
+
+namespace {
+// Small device -> host reads (the operator surface's per-cycle residual log):
+// one workgroup stores the words straight into the context's pinned staging
+// block with system-scope stores, as the host-value reductions do, so a read
+// is one kernel on the stream and a polled wait instead of a runtime copy
+// (a blit dispatch with a gap of its own before it). MPG_D2H_KERNEL=0: the
+// runtime copy.
+// With a flag (mpg::host_poll): every lane's stores waited for, then one
+// lane stores the sequence number.
+__global__ __launch_bounds__(256) void k_d2h_words(const uint32_t* __restrict__ src, uint32_t* dst, int words,
+                                                   unsigned* flag, unsigned seq) {
+    for (int t = threadIdx.x; t < words; t += blockDim.x)
+        __hip_atomic_store(dst + t, src[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!flag) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+bool d2h_kernel() {
+    const char* e = std::getenv("MPG_D2H_KERNEL");
+    return !(e && *e == '0');
+}
+}  // namespace
 
 extern "C" {
 
@@ -44,7 +69,14 @@ int mpg_ctx_create(int device, mpg_ctx_t* out) {
         ctx->red_ws_elems = mpg::kWsElems;
         e = hipMalloc(&ctx->red_ws, ctx->red_ws_elems * sizeof(double));
     }
-    if (e == hipSuccess) e = hipHostMalloc(&ctx->host_ws, mpg::kHostWsBytes, hipHostMallocDefault);
+    // coherent (fine-grained): the host polls words that kernels store while
+    // they run (mpg::host_poll); the default kind if that is refused
+    if (e == hipSuccess && hipHostMalloc(&ctx->host_ws, mpg::kHostWsBytes + 64, hipHostMallocCoherent) != hipSuccess) {
+        (void)hipGetLastError();
+        ctx->host_ws = nullptr;
+        e = hipHostMalloc(&ctx->host_ws, mpg::kHostWsBytes + 64, hipHostMallocDefault);
+    }
+    if (e == hipSuccess) std::memset(ctx->host_ws, 0, mpg::kHostWsBytes + 64);
     if (e == hipSuccess) e = hipMalloc((void**)&ctx->ticket, 256);
     if (e == hipSuccess) e = hipMemsetAsync(ctx->ticket, 0, 256, ctx->stream);
     if (e == hipSuccess && hipHostGetDevicePointer(&ctx->host_ws_dev, ctx->host_ws, 0) != hipSuccess) {
@@ -133,7 +165,21 @@ int mpg_memcpy_d2h(mpg_ctx_t ctx, void* dst_host, const void* src_dev, size_t by
     if (!ctx) return MPG_ERR_ARG;
     if (bytes == 0) return MPG_OK;
     if (bytes <= mpg::kHostWsBytes && ctx->host_ws) {  // small reads: pinned staging + a polled wait
-        MPG_HIP(ctx, hipMemcpyAsync(ctx->host_ws, src_dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        if (ctx->host_ws_dev && bytes % 4 == 0 && (uintptr_t)src_dev % 4 == 0 && d2h_kernel()) {
+            const bool poll = mpg::host_poll_on();
+            const unsigned seq = poll ? mpg::host_seq_next(ctx) : 0u;
+            k_d2h_words<<<1, 256, 0, ctx->stream>>>(static_cast<const uint32_t*>(src_dev),
+                                                   static_cast<uint32_t*>(ctx->host_ws_dev), (int)(bytes / 4),
+                                                   poll ? mpg::host_flag_dev(ctx) : nullptr, seq);
+            MPG_HIP(ctx, hipGetLastError());
+            if (poll) {
+                MPG_HIP(ctx, mpg::host_poll(ctx, seq));
+                std::memcpy(dst_host, ctx->host_ws, bytes);
+                return MPG_OK;
+            }
+        } else {
+            MPG_HIP(ctx, hipMemcpyAsync(ctx->host_ws, src_dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        }
         MPG_HIP(ctx, mpg::spin_wait(ctx->stream));
         std::memcpy(dst_host, ctx->host_ws, bytes);
         return MPG_OK;

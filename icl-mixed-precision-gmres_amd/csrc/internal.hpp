@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "mpgmres/capi.h"
@@ -32,6 +33,7 @@ struct mpg_ctx {
     void* host_ws = nullptr;
     void* host_ws_dev = nullptr;  // its device address (stage 2 of host-value reductions stores there)
     unsigned* ticket = nullptr;   // zeroed device word: last-workgroup ticket of one-launch reductions
+    unsigned host_seq = 0;        // the last sequence number a host read's kernel was given (host_flag)
 };
 
 // Analysed CSR structure (row blocks of the CSR-adaptive schedule).
@@ -75,6 +77,50 @@ constexpr size_t kHostWsBytes = 4096;
 // blocking synchronise, which measured 30-50 us between the stream draining
 // and the host's next launch per read (rocprofv3 trace of the operator
 // surface, profiles/r06f/); bounded, then the blocking wait.
+// The word after the staging block (hipHostMalloc'd kHostWsBytes + 64):
+// a host read's kernel stores its sequence number there after its payload
+// (host_flag_dev), and the host polls that word instead of the stream
+// (host_poll), so the read does not wait for the kernel's end-of-pipe
+// release and the runtime's completion signal. MPG_HOST_POLL=0: stream polls.
+inline volatile unsigned* host_flag(mpg_ctx* ctx) {
+    return reinterpret_cast<volatile unsigned*>(static_cast<char*>(ctx->host_ws) + kHostWsBytes);
+}
+inline unsigned* host_flag_dev(mpg_ctx* ctx) {
+    return reinterpret_cast<unsigned*>(static_cast<char*>(ctx->host_ws_dev) + kHostWsBytes);
+}
+inline bool host_poll_on() {
+    const char* e = std::getenv("MPG_HOST_POLL");
+    return !(e && *e == '0');
+}
+// next sequence number (never 0: the word starts at 0)
+inline unsigned host_seq_next(mpg_ctx* ctx) {
+    if (++ctx->host_seq == 0) ++ctx->host_seq;
+    return ctx->host_seq;
+}
+// Wait until the flag holds seq. Every 256 polls the stream is queried too:
+// a failed launch returns its error, and a stream that completed without
+// the flag set is an error (the payload cannot be trusted).
+inline hipError_t host_poll(mpg_ctx* ctx, unsigned seq) {
+    volatile unsigned* f = host_flag(ctx);
+    for (unsigned i = 1;; ++i) {
+        if (*f == seq) {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            return hipSuccess;
+        }
+        if ((i & 255) == 0) {
+            const hipError_t e = hipStreamQuery(ctx->stream);
+            if (e == hipSuccess) {
+                if (*f == seq) {
+                    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+                    return hipSuccess;
+                }
+                return hipErrorUnknown;
+            }
+            if (e != hipErrorNotReady) return e;
+        }
+    }
+}
+
 inline hipError_t spin_wait(hipStream_t s) {
     for (int i = 0; i < (1 << 22); ++i) {
         const hipError_t e = hipStreamQuery(s);

@@ -215,6 +215,29 @@ def test_trsv_upper(hip, oracle, t, n):
         assert np.allclose(dv.get(), exp, rtol=1e3 * tol, atol=1e3 * tol)
 
 
+def test_small_d2h_reads(hip, monkeypatch):
+    """Small device -> host reads (<= 4 KiB: the kernel that stores into the
+    pinned staging block for whole aligned words, the runtime copy otherwise)
+    return the bytes written by the kernel just before them on the stream."""
+    import ctypes as C
+
+    n = 2048
+    g = rng(7)
+    for form in ("1", "0"):
+        monkeypatch.setenv("MPG_D2H_KERNEL", form)
+        for it in range(3):
+            x = g.uniform(-1, 1, n).astype(np.float32)
+            dx, dy = hip.buf(x), hip.buf(n, np.float32)
+            hip.call("mpg_scal_copy_f32", n, 2.0, dx.p, dy.p)
+            full = dy.get()
+            assert np.array_equal(full, x * np.float32(2))
+            for off, nbytes in ((0, 4), (0, 120), (4, 4096 - 4), (0, 4096), (1, 7), (2, 6), (0, 3), (12, 4097)):
+                out = np.zeros(nbytes, np.uint8)
+                hip.check(hip.lib.mpg_memcpy_d2h(hip.ctx, out.ctypes.data, C.c_void_p(dy.ptr.value + off), C.c_size_t(nbytes)),
+                          "d2h")
+                assert np.array_equal(out, full.view(np.uint8)[off:off + nbytes]), (form, off, nbytes)
+
+
 @pytest.mark.parametrize("t", ["f64", "f32"])
 def test_trsv_wave_same_bits(hip, t, monkeypatch):
     """The one-wave LDS-staged trsv (n <= 64) against the workgroup form
