@@ -152,6 +152,7 @@ def _declare_host(lib: C.CDLL) -> None:
     lib.mpg_surface_ride_counts.argtypes = [C.POINTER(_I64)] * 3
     lib.mpg_surface_spmv_counts.argtypes = [C.POINTER(_I64)] * 3
     lib.mpg_surface_host_norm_hits.argtypes = [C.POINTER(_I64)]
+    lib.mpg_surface_host_norm_pairs.argtypes = [C.POINTER(_I64)]
     lib.mpg_engine_report.argtypes = [C.c_void_p, C.POINTER(SolveResult)]
     lib.mpg_engine_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     lib.mpg_engine_sync.argtypes = [C.c_void_p]
@@ -277,6 +278,8 @@ _HIP_DECLS.update({
     "mpg_copy_f32f64": ([_P, _I64, _P, _P], C.c_int),
     "mpg_copy_f64f16": ([_P, _I64, _P, _P], C.c_int),
     "mpg_copy_f32f16": ([_P, _I64, _P, _P], C.c_int),
+    "mpg_nrm2_pair_host": ([_P, _I64, C.c_int, _P, C.c_int, _P, C.POINTER(C.c_double), C.POINTER(C.c_double)],
+                           C.c_int),
 })
 
 
@@ -573,6 +576,15 @@ def surface_host_norm_hits() -> int:
     (mpg_surface_host_norm_hits)."""
     v = _I64()
     host_lib().mpg_surface_host_norm_hits(C.byref(v))
+    return v.value
+
+
+def surface_host_norm_pairs() -> int:
+    """Host-value nrm2 calls of the operator surface on this thread that also
+    read the residual SpMV's input vector's norm in the same launch
+    (mpg_surface_host_norm_pairs)."""
+    v = _I64()
+    host_lib().mpg_surface_host_norm_pairs(C.byref(v))
     return v.value
 
 

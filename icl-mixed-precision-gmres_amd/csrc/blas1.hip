@@ -5,6 +5,7 @@
 // partial per workgroup into the context workspace, stage 2: one workgroup
 // sums the partials in a fixed order and writes the result on device).
 #include "internal.hpp"
+#include "mpgmres/arnoldi.h"  // mpg_dtype_t
 #include "panel.hpp"
 #include "scalar_program.hpp"
 
@@ -186,6 +187,68 @@ int consume_partials(mpg_ctx* ctx, int32_t nparts, T* result_dev, int64_t n, con
     const int g = (int)std::max<int64_t>(1, std::min<int64_t>(256, (n + 4 * 1024 - 1) / (4 * 1024)));
     k_consume_partials<T, OP><<<g, 1024, 0, ctx->stream>>>(nparts, ctx->red_ws, result_dev, n, x, y);
     MPG_LAUNCH_CHECK(ctx);
+    return MPG_OK;
+}
+
+// Two host-value norms in one launch (the operator surface's restart
+// section reads ||w|| and then ||x||, gmres.cpp:173-196; kernels_hip.cpp
+// pairs them): each vector's stage 1 and stage 2 exactly as
+// k_nrm2_quad_host runs them alone (the same workgroups, lanes and
+// block_sum orders), so each result has the bits of its own one-launch
+// read; one ticket, one hand-off, one host poll.
+template <class T1, class T2>
+__global__ __launch_bounds__(kQuadBlock) void k_nrm2_pair_quad_host(int64_t n, const T1* __restrict__ a,
+                                                                    const T2* __restrict__ b,
+                                                                    double* __restrict__ partial,
+                                                                    unsigned* __restrict__ ticket,
+                                                                    T1* __restrict__ ra_host, T2* __restrict__ rb_host,
+                                                                    unsigned* __restrict__ flag_host, unsigned seq) {
+    static_assert(kQuadBlock == 1024, "the last workgroup runs stage 2's 1024-lane sum");
+    __shared__ double scratch[kQuadBlock / kWave];
+    __shared__ unsigned arrived;
+    const double sa = nrm2_quad_partial(n, a, scratch);
+    const double sb = nrm2_quad_partial(n, b, scratch);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(partial + blockIdx.x, sa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(partial + kQuadGroups + blockIdx.x, sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // both partials written through before the ticket
+        arrived = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (arrived != gridDim.x - 1) return;
+    const bool mine = threadIdx.x < gridDim.x;
+    const double va =
+        mine ? __hip_atomic_load(partial + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    const double vb = mine ? __hip_atomic_load(partial + kQuadGroups + threadIdx.x, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : 0.0;
+    const double ta = block_sum<1024>(va, scratch);
+    const double tb = block_sum<1024>(vb, scratch);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ra_host, (T1)sqrt(ta), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(rb_host, (T2)sqrt(tb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (flag_host) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(flag_host, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+template <class T1, class T2>
+int nrm2_pair_host(mpg_ctx* ctx, int64_t n, const T1* a, const T2* b, double* ra, double* rb) {
+    if ((uintptr_t)a % 16 != 0 || (uintptr_t)b % 16 != 0) return MPG_ERR_UNSUPPORTED;
+    const bool poll = mpg::host_poll_on();
+    const unsigned seq = poll ? mpg::host_seq_next(ctx) : 0u;
+    char* hd = static_cast<char*>(ctx->host_ws_dev);
+    k_nrm2_pair_quad_host<T1, T2><<<quad_groups(n), kQuadBlock, 0, ctx->stream>>>(
+        n, a, b, ctx->red_ws, ctx->ticket, reinterpret_cast<T1*>(hd), reinterpret_cast<T2*>(hd + 8),
+        poll ? mpg::host_flag_dev(ctx) : nullptr, seq);
+    MPG_LAUNCH_CHECK(ctx);
+    MPG_HIP(ctx, poll ? mpg::host_poll(ctx, seq) : mpg::spin_wait(ctx->stream));
+    const char* hw = static_cast<const char*>(ctx->host_ws);
+    *ra = (double)*reinterpret_cast<const volatile T1*>(hw);
+    *rb = (double)*reinterpret_cast<const volatile T2*>(hw + 8);
     return MPG_OK;
 }
 
@@ -387,6 +450,17 @@ int mpg_nrm2_f64(mpg_ctx_t c, int64_t n, const double* x, double* r) { return re
 int mpg_nrm2_f32(mpg_ctx_t c, int64_t n, const float* x, float* r) { return reduce<float, true>(c, n, x, x, r); }
 int mpg_nrm2_f64_host(mpg_ctx_t c, int64_t n, const double* x, double* r) { return reduce_host<double, true>(c, n, x, x, r); }
 int mpg_nrm2_f32_host(mpg_ctx_t c, int64_t n, const float* x, float* r) { return reduce_host<float, true>(c, n, x, x, r); }
+int mpg_nrm2_pair_host(mpg_ctx_t c, int64_t n, int type_a, const void* a, int type_b, const void* b, double* norm_a,
+                       double* norm_b) {
+    if (!c || !a || !b || !norm_a || !norm_b || n < 1) return MPG_ERR_ARG;
+    if (!c->host_ws_dev || !c->ticket) return MPG_ERR_UNSUPPORTED;
+    const bool a64 = type_a == MPG_F64, b64 = type_b == MPG_F64;
+    if ((!a64 && type_a != MPG_F32) || (!b64 && type_b != MPG_F32)) return MPG_ERR_ARG;
+    if (a64 && b64) return nrm2_pair_host(c, n, (const double*)a, (const double*)b, norm_a, norm_b);
+    if (a64) return nrm2_pair_host(c, n, (const double*)a, (const float*)b, norm_a, norm_b);
+    if (b64) return nrm2_pair_host(c, n, (const float*)a, (const double*)b, norm_a, norm_b);
+    return nrm2_pair_host(c, n, (const float*)a, (const float*)b, norm_a, norm_b);
+}
 int mpg_dot_acc_f64(mpg_ctx_t c, int64_t n, const double* x, const double* y, double* acc) {
     if (!c || n < 0) return MPG_ERR_ARG;
     int g = grid_for(n, 4, kMaxRedBlocks);

@@ -16,6 +16,7 @@
 #include <sstream>
 
 #include "kernels.hpp"
+#include "mpgmres/arnoldi.h"  // mpg_dtype_t
 #include "mpgmres/solve.h"
 
 namespace mpg {
@@ -143,9 +144,10 @@ thread_local PendingReduction tl_red;
 // 2 dot -> naxpy, 4 gemv^T -> gemv, 8 gemv -> nrm2: the CGS update emits
 // the ||w||^2 partials that the nrm2 of add_vector would compute, below;
 // 16 scal_recip -> spmv: add_vector's normalisation rides the next SELL
-// SpMV, below; 32 the host-value nrm2 memo, below); unset: kFuseDefault;
+// SpMV, below; 32 the host-value nrm2 memo, below; 64 the residual
+// SpMV's input read with the next host nrm2, below); unset: kFuseDefault;
 // 0: none
-constexpr int kFuseDefault = 1 | 4 | 8 | 16 | 32;
+constexpr int kFuseDefault = 1 | 4 | 8 | 16 | 32 | 64;
 
 // The ||y||^2 stage-1 partials a fused CGS gemv (mpg_gemv_n_from_t_nrm2_*)
 // left in the context workspace: an nrm2 of exactly that y as the very
@@ -456,6 +458,48 @@ void host_norm_store(const void* p, int64_t n, bool f64, double v) {
     tl_hn_next ^= 1;
 }
 
+// ---- ||x|| read with ||w|| (round 6, MPG_SURFACE_FUSE bit 64) ----
+// The restart section reads r_norm = ||w|| and, with nothing written in
+// between when the preconditioner is the identity, x_norm = ||x|| of the x
+// the residual SpMV (alpha -1, beta 1) has just read (gmres.cpp:173-196).
+// That SpMV's input is remembered; the next host-value nrm2 that misses the
+// memo reads both norms in one launch and one host round trip
+// (mpg_nrm2_pair_host: each with the bits of its own read) and memoises
+// both, so ||x|| is a memo hit when nothing was written since. Any surface
+// deallocation forgets the remembered vector (it is never read after free).
+namespace {
+struct NormPrefetch {
+    const void* p = nullptr;
+    int64_t n = 0;
+    bool f64 = false;
+    mpg_ctx_t ctx = nullptr;
+};
+thread_local NormPrefetch tl_npf;
+thread_local int64_t tl_npf_pairs = 0;
+}  // namespace
+
+void note_residual_spmv(const void* x, int64_t n, bool f64) {
+    if (fuse_enabled(64) && fuse_enabled(32) && n > 0) tl_npf = NormPrefetch{x, n, f64, tl_ctx};
+}
+void forget_norm_prefetch() { tl_npf = NormPrefetch{}; }
+
+mpg_ctx_t read_ctx();
+bool host_norm_pair(const void* p, int64_t n, bool f64, double& v) {
+    const NormPrefetch q = tl_npf;
+    if (!q.p || q.p == p || q.n != n || !tl_ctx || q.ctx != tl_ctx || !fuse_enabled(64) || !fuse_enabled(32))
+        return false;
+    tl_npf = NormPrefetch{};
+    double vq = 0;
+    mpg_ctx_t c = read_ctx();
+    const int st = mpg_nrm2_pair_host(c, n, f64 ? MPG_F64 : MPG_F32, p, q.f64 ? MPG_F64 : MPG_F32, q.p, &v, &vq);
+    if (st == MPG_ERR_UNSUPPORTED) return false;
+    check(st, "nrm2 (paired read)", c);
+    host_norm_store(q.p, n, q.f64, vq);
+    host_norm_store(p, n, f64, v);
+    ++tl_npf_pairs;
+    return true;
+}
+
 mpg_ctx_t current_ctx();
 mpg_ctx_t read_ctx() {
     const bool deferred = !nothing_deferred();
@@ -481,6 +525,7 @@ ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) {
     tl_ctx = ctx;
     tl_ride_score = 2;  // (what the ride learned belongs to the previous scope's solve)
     tl_hn[0] = tl_hn[1] = HostNormMemo{};  // (so does the host-value nrm2 memo)
+    tl_npf = NormPrefetch{};
 }
 ScopedContext::~ScopedContext() {
     // the queue and a pending stage 2 belong to this scope's context; a
@@ -549,6 +594,7 @@ void* Hip::allocate(size_t bytes) {
     return p;
 }
 void Hip::deallocate(void* p) {
+    mpg::forget_norm_prefetch();
     if (p) mpg_free(current_ctx(), p);
 }
 void Hip::to_host(void* dst, const void* src, size_t bytes) {
@@ -631,6 +677,7 @@ template <> void dot<float, Hip>(Vect<float, Hip> x, Vect<float, Hip> y, Scalar<
 template <> double nrm2<double, Hip>(Vect<double, Hip> x) {
     double r;
     if (mpg::host_norm_hit(x.data(), (int64_t)x.n(), true, r)) return r;
+    if (mpg::host_norm_pair(x.data(), (int64_t)x.n(), true, r)) return r;
     check(mpg_nrm2_f64_host(mpg::read_ctx(), x.n(), x.data(), &r), "nrm2");
     mpg::host_norm_store(x.data(), (int64_t)x.n(), true, r);
     return r;
@@ -638,6 +685,7 @@ template <> double nrm2<double, Hip>(Vect<double, Hip> x) {
 template <> float nrm2<float, Hip>(Vect<float, Hip> x) {
     double m;
     if (mpg::host_norm_hit(x.data(), (int64_t)x.n(), false, m)) return (float)m;
+    if (mpg::host_norm_pair(x.data(), (int64_t)x.n(), false, m)) return (float)m;
     float r;
     check(mpg_nrm2_f32_host(mpg::read_ctx(), x.n(), x.data(), &r), "nrm2");
     mpg::host_norm_store(x.data(), (int64_t)x.n(), false, r);
@@ -800,6 +848,11 @@ void set_redirect(mpg_ctx_t c, void* w, void* sp, int64_t n, bool f64) {
 
 extern "C" int mpg_surface_host_norm_hits(int64_t* hits) {
     if (hits) *hits = mpg::tl_hn_hits;
+    return MPG_OK;
+}
+
+extern "C" int mpg_surface_host_norm_pairs(int64_t* pairs) {
+    if (pairs) *pairs = mpg::tl_npf_pairs;
     return MPG_OK;
 }
 
@@ -980,6 +1033,7 @@ template <> void spmv<double, Hip>(double alpha, SparseMatrix<double, Hip> A, Ve
                                    Vect<double, Hip> y) {
     assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
                              : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
+    if (alpha == double(-1) && beta == double(1)) mpg::note_residual_spmv(x.data(), (int64_t)x.n(), true);
     mpg_node_t nd = A.node();
     mpg_sell_t s = nd ? nullptr : A.sell();
     if (nd || s) {
@@ -1022,6 +1076,7 @@ template <> void spmv<float, Hip>(float alpha, SparseMatrix<float, Hip> A, Vect<
                                   Vect<float, Hip> y) {
     assert(A.is_transposed() ? ((size_t)A.nrows() == x.n() && (size_t)A.ncols() == y.n())
                              : ((size_t)A.ncols() == x.n() && (size_t)A.nrows() == y.n()));
+    if (alpha == float(-1) && beta == float(1)) mpg::note_residual_spmv(x.data(), (int64_t)x.n(), false);
     mpg_node_t nd = A.node();
     mpg_sell_t s = nd ? nullptr : A.sell();
     if (nd || s) {

@@ -109,6 +109,13 @@ int mpg_nrm2_f64(mpg_ctx_t ctx, int64_t n, const double* x, double* result_dev);
 int mpg_nrm2_f32(mpg_ctx_t ctx, int64_t n, const float* x, float* result_dev);
 int mpg_nrm2_f64_host(mpg_ctx_t ctx, int64_t n, const double* x, double* result_host);
 int mpg_nrm2_f32_host(mpg_ctx_t ctx, int64_t n, const float* x, float* result_host);
+// ||a|| and ||b|| (each MPG_F32 or MPG_F64 of mpg_dtype_t, arnoldi.h; n rows, 16-B aligned) in one
+// launch and one host read, each with the bits of its own mpg_nrm2_*_host
+// (the operator surface's restart section: ||w|| with the ||x|| the
+// reference's driver reads next, gmres.cpp:173-196); results widened to
+// double. MPG_ERR_UNSUPPORTED: unaligned, or no pinned staging.
+int mpg_nrm2_pair_host(mpg_ctx_t ctx, int64_t n, int type_a, const void* a, int type_b, const void* b,
+                       double* norm_a_host, double* norm_b_host);
 /* Split reductions (the operator surface defers stage 2 into the consumer
  * of the result; kernels_hip.cpp). *_partials runs stage 1 only: *nparts
  * fp64 partials in the context workspace, valid until the next reduction on

@@ -211,6 +211,11 @@ int mpg_surface_spmv_counts(int64_t* node, int64_t* sell, int64_t* csr);
  * the memo of the same vector's previous read (MPG_SURFACE_FUSE bit 32: no
  * device work issued through the surface in between, nothing deferred). */
 int mpg_surface_host_norm_hits(int64_t* hits);
+/* Host-value nrm2 calls of the operator surface on this thread that also
+ * read the norm of the vector the preceding residual SpMV (alpha -1, beta 1)
+ * took as input, in one launch (mpg_nrm2_pair_host; MPG_SURFACE_FUSE bit
+ * 64): that vector's next host nrm2 is then a memo hit. */
+int mpg_surface_host_norm_pairs(int64_t* pairs);
 
 #ifdef __cplusplus
 }

@@ -327,6 +327,71 @@ def test_surface_host_norm_memo(mpg, mode, prec, monkeypatch):
     assert on.res_norm == off.res_norm
 
 
+@pytest.mark.parametrize("mode", ["mixed", "baseline", "single"])
+@pytest.mark.parametrize("prec", ["identity", "jacobi"])
+def test_surface_host_norm_pair(mpg, mode, prec, monkeypatch):
+    """Round 6 (MPG_SURFACE_FUSE bit 64): the restart section's r_norm read
+    also reads ||x|| of the residual SpMV's input in the same launch
+    (mpg_nrm2_pair_host), and x_norm is then a memo hit when nothing wrote
+    in between (identity; with Jacobi gdmv writes w first, so x_norm reads
+    again). The solve keeps the bits of the surface without the pairing and
+    of the surface without any memo."""
+    A = mpg.gen_band(100_000, 5, 4, seed=7)
+    xt = mpg.rand_vect(A.nrows, 42)
+    b = mpg.host_spmv(A, xt)
+    opts = dict(engine="surface", mode=mode, orth="cgs", prec=prec, rlen=30, tol=0.0, max_restarts=3)
+    monkeypatch.delenv("MPG_SURFACE_FUSE", raising=False)
+    p0, h0 = mpg.surface_host_norm_pairs(), mpg.surface_host_norm_hits()
+    on = mpg.solve(A, b, xt, **opts)
+    pairs, hits = mpg.surface_host_norm_pairs() - p0, mpg.surface_host_norm_hits() - h0
+    monkeypatch.setenv("MPG_SURFACE_FUSE", str(1 | 4 | 8 | 16 | 32))
+    p1, h1 = mpg.surface_host_norm_pairs(), mpg.surface_host_norm_hits()
+    mid = mpg.solve(A, b, xt, **opts)
+    assert mpg.surface_host_norm_pairs() == p1
+    hits_memo_only = mpg.surface_host_norm_hits() - h1
+    monkeypatch.setenv("MPG_SURFACE_FUSE", str(1 | 4 | 8 | 16))
+    off = mpg.solve(A, b, xt, **opts)
+    assert pairs >= 3, pairs  # one per restart section (3 cycles + the final residual)
+    if prec == "identity":
+        assert hits >= hits_memo_only + 3, (hits, hits_memo_only)  # x_norm answered by the pair
+    for r in (mid, off):
+        assert on.total_iters == r.total_iters == 90
+        assert np.array_equal(on.step_res, r.step_res) and np.array_equal(on.x, r.x)
+        assert on.res_norm == r.res_norm
+
+
+def test_nrm2_pair_host_same_bits(hip):
+    """mpg_nrm2_pair_host: each norm with the bits of its own
+    mpg_nrm2_*_host, for every type pair, tails (n not a multiple of 4) and
+    one workgroup up to the full stage-1 grid."""
+    import ctypes as C
+
+    F64, F32 = 0, 1
+    g = np.random.default_rng(5)
+    for n in (1, 7, 4099, 1_000_003, 4_000_000):
+        for ta, tb in ((F32, F64), (F64, F64), (F32, F32), (F64, F32)):
+            dta = np.float64 if ta == F64 else np.float32
+            dtb = np.float64 if tb == F64 else np.float32
+            a = (g.standard_normal(n) * 3).astype(dta)
+            bvec = g.standard_normal(n).astype(dtb)
+            da, db = hip.buf(a), hip.buf(bvec)
+            ra, rb = C.c_double(), C.c_double()
+            hip.check(hip.lib.mpg_nrm2_pair_host(hip.ctx, n, ta, da.p, tb, db.p, C.byref(ra), C.byref(rb)), "pair")
+            ref = []
+            for t, d in ((ta, da), (tb, db)):
+                if t == F64:
+                    r = C.c_double()
+                    hip.check(hip.lib.mpg_nrm2_f64_host(hip.ctx, n, d.p, C.byref(r)), "nrm2")
+                else:
+                    r = C.c_float()
+                    hip.check(hip.lib.mpg_nrm2_f32_host(hip.ctx, n, d.p, C.byref(r)), "nrm2")
+                ref.append(float(r.value))
+            assert ra.value == ref[0] and rb.value == ref[1], (n, ta, tb, ra.value, rb.value, ref)
+            assert np.isclose(ra.value, np.linalg.norm(a.astype(np.float64)), rtol=1e-6)
+            da.free()
+            db.free()
+
+
 @pytest.mark.parametrize("matrix", ["band", "lap", "stencil27"])
 @pytest.mark.parametrize("orth", ["cgs", "mgs", "cgsr"])
 @pytest.mark.parametrize("mode", ["mixed", "baseline", "single"])
