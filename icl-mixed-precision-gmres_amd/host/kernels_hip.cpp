@@ -162,9 +162,15 @@ struct NormMemo {
     int32_t nparts = 0;
 };
 thread_local NormMemo tl_norm;
-bool fuse_enabled(int bit) {
+int read_fuse_mask() {
     const char* env = std::getenv("MPG_SURFACE_FUSE");
-    const int mask = env && *env ? std::atoi(env) : kFuseDefault;
+    return env && *env ? std::atoi(env) & 0x7fffffff : kFuseDefault;
+}
+// read once when a ScopedContext opens (a solve), not on every call of the
+// restart section, whose launches the host paces; -1: no scope open
+thread_local int tl_fuse_mask = -1;
+bool fuse_enabled(int bit) {
+    const int mask = tl_fuse_mask >= 0 ? tl_fuse_mask : read_fuse_mask();
     return (mask & bit) != 0;
 }
 }  // namespace
@@ -517,7 +523,7 @@ mpg_ctx_t current_ctx() {
     return ctx_no_flush();
 }
 
-ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) {
+ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx), prev_fuse_(tl_fuse_mask) {
     tl_norm.y = nullptr;
     flush_ride();
     if (tl_nops) flush_scalar_ops();
@@ -526,6 +532,7 @@ ScopedContext::ScopedContext(mpg_ctx_t ctx) : prev_(tl_ctx) {
     tl_ride_score = 2;  // (what the ride learned belongs to the previous scope's solve)
     tl_hn[0] = tl_hn[1] = HostNormMemo{};  // (so does the host-value nrm2 memo)
     tl_npf = NormPrefetch{};
+    tl_fuse_mask = read_fuse_mask();
 }
 ScopedContext::~ScopedContext() {
     // the queue and a pending stage 2 belong to this scope's context; a
@@ -547,6 +554,7 @@ ScopedContext::~ScopedContext() {
         }
     }
     tl_ctx = prev_;
+    tl_fuse_mask = prev_fuse_;
 }
 
 void build_transpose(CsrStructure& s) {

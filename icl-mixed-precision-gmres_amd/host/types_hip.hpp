@@ -61,6 +61,7 @@ mpg_ctx_t current_ctx();
 
 class ScopedContext {
     mpg_ctx_t prev_;
+    int prev_fuse_;  // the enclosing scope's MPG_SURFACE_FUSE mask (-1: none)
 public:
     explicit ScopedContext(mpg_ctx_t ctx);
     ~ScopedContext();
