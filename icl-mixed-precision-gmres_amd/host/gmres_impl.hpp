@@ -79,6 +79,10 @@ void gmres_baseline(Convergence<Type, Device>& convergence, SparseMatrix<Type, D
     const bool defer = !convergence.needs_arnoldi_residual();
     mpg::ArnoldiResidualLog<Type, Device> rlog(m, defer);
     mpg::CycleProgram<Device> cycle;
+    // the solution update after a full deferred cycle (k = m): device-only
+    // too, so recorded and replayed like the cycle (its launches would
+    // otherwise be paced by the host's)
+    mpg::CycleProgram<Device> update(false);
 
     convergence.setup(orth);
 
@@ -164,7 +168,10 @@ void gmres_baseline(Convergence<Type, Device>& convergence, SparseMatrix<Type, D
                     break;
             }
         }
-        solution_update(orth, x, k, h, s);
+        if (defer)
+            update.run([&] { solution_update(orth, x, k, h, s); });
+        else
+            solution_update(orth, x, k, h, s);
     }
 }
 
@@ -183,6 +190,10 @@ void gmres_singleUpdate(Convergence<float, Device>& convergence, SparseMatrix<do
     const bool defer = !convergence.needs_arnoldi_residual();
     mpg::ArnoldiResidualLog<float, Device> rlog(m, defer);
     mpg::CycleProgram<Device> cycle;
+    // the solution update after a full deferred cycle (k = m): device-only
+    // too, so recorded and replayed like the cycle (its launches would
+    // otherwise be paced by the host's)
+    mpg::CycleProgram<Device> update(false);
 
     convergence.setup(orth);
 
@@ -267,7 +278,10 @@ void gmres_singleUpdate(Convergence<float, Device>& convergence, SparseMatrix<do
                     break;
             }
         }
-        solution_update(orth, x, k, h, s, w, r_accum);
+        if (defer)
+            update.run([&] { solution_update(orth, x, k, h, s, w, r_accum); });
+        else
+            solution_update(orth, x, k, h, s, w, r_accum);
     }
 }
 

@@ -50,6 +50,7 @@ std::shared_ptr<void> device_alloc(size_t bytes) {
 template <class Device>
 class CycleProgram {
 public:
+    explicit CycleProgram(bool /*counted*/ = true) {}
     template <class F>
     void run(F&& steps) {
         steps();

@@ -6,6 +6,7 @@
 #ifndef MPGMRES_TYPES_HIP_HPP
 #define MPGMRES_TYPES_HIP_HPP
 
+#include <cstdlib>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -136,12 +137,17 @@ class CycleProgram<Hip> {
     mpg_ctx_t ctx_ = nullptr;
     int cycles_ = 0;
     bool eager_;
+    bool counted_;  // in mpg_cycle_program_counts (the Arnoldi cycle; not the solution update)
 
     static bool enabled();
     static void count(int which);  // 0 recorded, 1 replayed, 2 voided
 
 public:
-    CycleProgram() : eager_(!enabled()) {}
+    // (MPG_SURFACE_UPDATE_PROG=0: the solution update runs eagerly)
+    explicit CycleProgram(bool counted = true)
+        : eager_(!enabled() || (!counted && std::getenv("MPG_SURFACE_UPDATE_PROG") &&
+                                *std::getenv("MPG_SURFACE_UPDATE_PROG") == '0')),
+          counted_(counted) {}
     ~CycleProgram() {
         if (g_) mpg_graph_destroy(g_);
     }
@@ -155,7 +161,7 @@ public:
         if (g_) {
             note_device_writes();
             check(mpg_graph_launch(ctx_, g_), "cycle program launch", ctx_);
-            count(1);
+            if (counted_) count(1);
             return;
         }
         if (eager_ || cycles_++ == 0) {
@@ -191,14 +197,14 @@ public:
         if (!ok || st != MPG_OK || !g) {
             if (g) mpg_graph_destroy(g);
             eager_ = true;
-            count(2);
+            if (counted_) count(2);
             steps();
             return;
         }
         g_ = g;
         note_device_writes();
         check(mpg_graph_launch(ctx_, g_), "cycle program launch", ctx_);
-        count(0);
+        if (counted_) count(0);
     }
 };
 
